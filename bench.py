@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Headline benchmark: verified signatures / second for the whole node (BASELINE.json).
+
+Workload (BASELINE.json configs[1]): per GPU, a batch of
+2^20 Ed25519 (EDDSA_ED25519_SHA512) signatures over 4096 keys and 270-byte
+SignableData-sized messages, 12% corrupted across Appendix A classes A1-A7, seeded
+synthetic data (no network, no JVM). One step = one full pass of the hot path over the
+batch with every input already resident in HBM: key prep (decode + tables for every key)
+-> verify every item -> status bytes in HBM, plus (N > 1) the RCCL all-gather of the
+per-GPU verdict vectors, the engine's only collective.
+
+Launch: ``python bench.py`` (N = 1) or ``torchrun --nproc-per-node N bench.py --gpus N``;
+one process per GPU, each verifying its own shard (weak scaling). Rank 0 prints ONE JSON
+line. ``roofline`` prices the dominant kernel (k_ed_verify) in 32x32->64 multiply-
+accumulates against the measured v_mad_u64_u32 peak (profiles/r01/ubench_int.json);
+``cpu_baseline`` is the C restatement of the reference's algorithms (oracle/c, "port")
+timed on a bounded sample on the host cores (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "verified sigs/sec (whole node), Ed25519 + ECDSA-P256, at 1/2/4/8 MI355X"
+# Algorithmic work per Ed25519 verify, frozen from the C restatement of i2p 0.2.0
+# (oracle/c/ed25519_i2p.c counters): 1673 field multiplies + 1326 squarings
+# per engineVerify, each priced at 64 MAC32 (a 256x256-bit product in 32-bit words).
+N_FE_ED25519 = 2999
+MAC32_PER_ED25519 = N_FE_ED25519 * 64
+# v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
+PEAK_MAC32_PER_S = 2.7944e13
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--items", type=int, default=1 << 20, help="items per GPU")
+    ap.add_argument("--keys", type=int, default=4096)
+    ap.add_argument("--msg-len", type=int, default=270)
+    ap.add_argument("--corrupt-permille", type=int, default=120)
+    ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
+    ap.add_argument("--threads", type=int, default=0, help="host threads for data generation / CPU baseline")
+    return ap.parse_args()
+
+
+def host_threads(req):
+    if req > 0:
+        return req
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = int(env) if env and env.isdigit() else 16
+    return max(1, min(n, os.cpu_count() or 1, 16))
+
+
+def cpu_baseline(batch, seconds, threads):
+    """oracle/c (C restatement of i2p 0.2.0 / BC 1.57 semantics) on a bounded sample."""
+    from corda_amd.batch import Batch
+    from oracle import c_oracle
+    probe = min(batch.n, 256 * threads)
+    sub = Batch(batch.keys, batch.items[:probe], batch.arena)
+    t = time.perf_counter()
+    c_oracle.verify_batch(sub, 0, threads)
+    dt = time.perf_counter() - t
+    n = int(min(batch.n, max(probe, probe * seconds / max(dt, 1e-6))))
+    sub = Batch(batch.keys, batch.items[:n], batch.arena)
+    t = time.perf_counter()
+    st = c_oracle.verify_batch(sub, 0, threads)
+    dt = time.perf_counter() - t
+    return {"value": round(n / dt, 1), "unit": "sigs/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} items of the rank-0 batch (incl. key decode for all {len(batch.keys)} keys), "
+                      f"oracle/c or_verify_batch over {threads} threads, {dt:.1f} s; JVM reference "
+                      f"unavailable (no JDK / i2p / BouncyCastle jars on the box)"}, st
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    threads = host_threads(a.threads)
+
+    from corda_amd.engine import Engine
+    from tools.workload import wl
+
+    # ---- synthetic shard for this rank (outside the timed region) ----
+    t0 = time.time()
+    batch, labels = wl.ed25519_batch(a.items, n_keys=a.keys, msg_len=a.msg_len,
+                                     corrupt_permille=a.corrupt_permille, seed=a.seed + 7919 * rank,
+                                     nthreads=threads)
+    gen_s = time.time() - t0
+    eng = Engine(local)
+    eng.reserve(len(batch.keys), batch.n)
+    keys_d = torch.from_numpy(batch.keys.view(np.uint8)).to(dev)
+    items_d = torch.from_numpy(batch.items.view(np.uint8)).to(dev)
+    arena_d = torch.from_numpy(batch.arena).to(dev)
+    status_d = torch.full((batch.n,), 255, dtype=torch.uint8, device=dev)
+    gathered = torch.empty((world * batch.n,), dtype=torch.uint8, device=dev) if world > 1 else None
+    n_keys, n_items, arena_len = len(batch.keys), batch.n, int(batch.arena.size)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    ev = []
+
+    def step(timed):
+        eng.prepare_keys_device(keys_d.data_ptr(), n_keys, arena_d.data_ptr(), arena_len, sptr)
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        eng.verify_items_device(keys_d.data_ptr(), n_keys, items_d.data_ptr(), n_items, arena_d.data_ptr(),
+                                arena_len, status_d.data_ptr(), 0, sptr)
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, status_d)
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev])) if ev else float("nan")
+    st = status_d.cpu().numpy()
+    counts = {k: int(v) for k, v in zip(*np.unique(st, return_counts=True))}
+    # label sanity (full parity lives in tests/test_gpu_parity.py)
+    valid_ok = bool(np.all(st[labels == 0] == 0))
+
+    total_items = n_items * world * a.steps
+    value = total_items / elapsed
+    achieved = n_items * MAC32_PER_ED25519 / (kern_ms * 1e-3)
+    roof = {"bound": "valu-int", "achieved": round(achieved / 1e12, 3), "peak": round(PEAK_MAC32_PER_S / 1e12, 3),
+            "unit": "TMAC32/s", "frac": round(achieved / PEAK_MAC32_PER_S, 4), "traffic": None,
+            "kernel": "k_ed_verify (+k_misc_status)", "kernel_ms": round(kern_ms, 3),
+            "work_per_item": f"{N_FE_ED25519} i2p field mul/sq x 64 MAC32 = {MAC32_PER_ED25519} MAC32"}
+    traffic_file = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    if os.path.exists(traffic_file):
+        with open(traffic_file) as f:
+            tr = json.load(f)
+        if tr.get("items") == n_items:
+            roof["traffic"] = tr.get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu, cst = cpu_baseline(batch, a.cpu_seconds, threads)
+        cpu["parity_on_sample"] = bool(np.array_equal(cst, st[:cst.size]))
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "sigs/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: seeded RFC 8032 Ed25519 signatures (tools/workload), no JVM capture",
+            "config": {"workload": "BASELINE configs[1]: 2^20 Ed25519 sigs per GPU, bit-exact verdicts incl. "
+                                   "corrupted sigs", "items_per_gpu": n_items, "keys": n_keys,
+                       "msg_len": a.msg_len, "corrupt_permille": a.corrupt_permille,
+                       "parallelism": f"shard{world}" + ("+rccl_allgather(verdicts)" if world > 1 else "")},
+            "roofline": roof, "cpu_baseline": cpu,
+            "verdicts": {"counts": counts, "valid_labels_all_valid": valid_ok},
+            "gen_s": round(gen_s, 1),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

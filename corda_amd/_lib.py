@@ -1,0 +1,85 @@
+"""ctypes binding of libcordagpu.so (include/cordagpu.h).
+
+The library is built in-tree (``make -C corda_amd/csrc`` or ``__graft_entry__.build()``)
+and loaded from ``corda_amd/libcordagpu.so``. There is no fallback: if the library is
+missing, or the device cannot run it, every entry point raises ``EngineUnavailable``.
+"""
+import ctypes
+import os
+import re
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcordagpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cordagpu.h")
+
+_lib = None
+_lock = threading.Lock()
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+class cg_stats(ctypes.Structure):
+    _fields_ = [("n_items", ctypes.c_uint64), ("n_keys", ctypes.c_uint64), ("ms_h2d", ctypes.c_double),
+                ("ms_key_prep", ctypes.c_double), ("ms_verify", ctypes.c_double), ("ms_d2h", ctypes.c_double),
+                ("ms_total", ctypes.c_double)]
+
+
+class cg_config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32), ("max_items", ctypes.c_uint64),
+                ("max_arena", ctypes.c_uint64)]
+
+
+def declared_symbols():
+    """Function names declared in include/cordagpu.h."""
+    with open(HEADER_PATH) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(cg_\w+)\s*\(", src, re.M)))
+
+
+def lib():
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise EngineUnavailable(f"{LIB_PATH} not built (run __graft_entry__.build() or make -C corda_amd/csrc)")
+            L = ctypes.CDLL(LIB_PATH)
+            vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+            L.cg_abi_version.restype = i32
+            L.cg_build_info.restype = ctypes.c_char_p
+            L.cg_device_count.restype = i32
+            L.cg_last_error.restype = ctypes.c_char_p
+            L.cg_open.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(cg_config)]
+            L.cg_open.restype = i32
+            L.cg_close.argtypes = [vp]
+            L.cg_close.restype = None
+            L.cg_reserve.argtypes = [vp, u32, u64]
+            L.cg_verify_batch.argtypes = [vp, vp, u32, vp, u64, vp, u64, u32, vp, ctypes.POINTER(cg_stats)]
+            L.cg_verify_batch_device.argtypes = [vp, vp, u32, vp, u64, vp, u64, u32, vp, vp]
+            L.cg_prepare_keys_device.argtypes = [vp, vp, u32, vp, u64, vp]
+            L.cg_prepare_keys_device.restype = i32
+            L.cg_verify_items_device.argtypes = [vp, vp, u32, vp, u64, vp, u64, u32, vp, vp]
+            L.cg_verify_items_device.restype = i32
+            L.cg_sha256_batch.argtypes = [vp, vp, u64, vp, u64, vp]
+            L.cg_sha512_batch.argtypes = [vp, vp, u64, vp, u64, vp]
+            L.cg_sha256_batch_device.argtypes = [vp, vp, u64, vp, u64, vp, vp]
+            L.cg_merkle_roots.argtypes = [vp, vp, vp, vp, u64, vp, vp]
+            L.cg_tx_ids.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, vp]
+            L.cg_tx_ids_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, vp, vp]
+            for name in ("cg_reserve", "cg_verify_batch", "cg_verify_batch_device", "cg_sha256_batch",
+                         "cg_sha512_batch", "cg_sha256_batch_device", "cg_merkle_roots", "cg_tx_ids",
+                         "cg_tx_ids_device"):
+                getattr(L, name).restype = i32
+            _lib = L
+        return _lib
+
+
+def last_error():
+    return lib().cg_last_error().decode(errors="replace")
+
+
+def check(rc, what):
+    if rc != 0:
+        raise EngineUnavailable(f"{what} failed ({rc}): {last_error()}")

@@ -1,0 +1,96 @@
+"""Batch layout shared by the host mirror, tests and bench: numpy views of the C ABI structs.
+
+``KEY_DTYPE`` / ``ITEM_DTYPE`` / ``SPAN_DTYPE`` / ``COMPONENT_DTYPE`` / ``TX_DTYPE`` are
+byte-for-byte ``cg_key`` / ``cg_item`` / ``cg_span`` / ``cg_component`` / ``cg_tx`` of
+include/cordagpu.h. ``BatchBuilder`` packs (key, sig, clear) triples the way a JVM
+caller of ``Crypto.verifyBatch`` would: each distinct PublicKey object once in the key
+table (as TransactionSignature.by references it), signatures and clear data appended to
+one arena.
+"""
+import numpy as np
+
+KEY_DTYPE = np.dtype([("off", "<u8"), ("len", "<u2"), ("scheme", "u1"), ("fmt", "u1"), ("reserved", "<u4")])
+ITEM_DTYPE = np.dtype([("sig_off", "<u8"), ("msg_off", "<u8"), ("msg_len", "<u4"), ("key_idx", "<u4"),
+                       ("sig_len", "<u2"), ("reserved0", "<u2"), ("reserved1", "<u4")])
+SPAN_DTYPE = np.dtype([("off", "<u8"), ("len", "<u8")])
+COMPONENT_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("flags", "<u4")])
+TX_DTYPE = np.dtype([("first", "<u8"), ("n", "<u4"), ("reserved", "<u4"), ("salt_off", "<u8")])
+assert KEY_DTYPE.itemsize == 16 and ITEM_DTYPE.itemsize == 32 and SPAN_DTYPE.itemsize == 16
+assert COMPONENT_DTYPE.itemsize == 16 and TX_DTYPE.itemsize == 24
+
+# status codes (include/cordagpu.h)
+VALID, INVALID, SIG_MALFORMED, KEY_INVALID, UNSUPPORTED, EMPTY, NOT_RUN = 0, 1, 2, 3, 4, 5, 255
+STATUS_NAMES = {VALID: "VALID", INVALID: "INVALID", SIG_MALFORMED: "SIG_MALFORMED", KEY_INVALID: "KEY_INVALID",
+                UNSUPPORTED: "UNSUPPORTED", EMPTY: "EMPTY", NOT_RUN: "NOT_RUN"}
+STATUS_BY_NAME = {v: k for k, v in STATUS_NAMES.items()}
+ECDSA_SECP256K1_SHA256, ECDSA_SECP256R1_SHA256, EDDSA_ED25519_SHA512 = 2, 3, 4
+KEY_RAW, KEY_SPKI, KEY_SEC1 = 0, 1, 2
+MODE_DOVERIFY, MODE_ISVALID = 0, 1
+
+
+class Batch:
+    """Packed batch: ``keys`` (KEY_DTYPE), ``items`` (ITEM_DTYPE), ``arena`` (uint8)."""
+
+    def __init__(self, keys, items, arena):
+        self.keys = keys
+        self.items = items
+        self.arena = arena
+
+    @property
+    def n(self):
+        return len(self.items)
+
+
+class BatchBuilder:
+    def __init__(self):
+        self._chunks = []
+        self._size = 0
+        self._keys = []
+        self._key_index = {}
+        self._items = []
+
+    def _append(self, b, align=1):
+        pad = (-self._size) % align
+        if pad:
+            self._chunks.append(bytes(pad))
+            self._size += pad
+        off = self._size
+        if b:
+            self._chunks.append(bytes(b))
+            self._size += len(b)
+        return off
+
+    def key(self, scheme, fmt, key_bytes):
+        """Registers a public key once (identity = (scheme, fmt, bytes)); returns its index."""
+        k = (int(scheme), int(fmt), bytes(key_bytes))
+        idx = self._key_index.get(k)
+        if idx is None:
+            off = self._append(key_bytes, 4)
+            idx = len(self._keys)
+            self._keys.append((off, len(key_bytes), scheme, fmt))
+            self._key_index[k] = idx
+        return idx
+
+    def add(self, key_idx, sig, msg):
+        sig_off = self._append(sig, 4)
+        msg_off = self._append(msg, 4)
+        self._items.append((sig_off, msg_off, len(msg), key_idx, len(sig)))
+        return len(self._items) - 1
+
+    def add_with_key(self, scheme, fmt, key_bytes, sig, msg):
+        return self.add(self.key(scheme, fmt, key_bytes), sig, msg)
+
+    def build(self):
+        keys = np.zeros(len(self._keys), dtype=KEY_DTYPE)
+        for i, (off, ln, scheme, fmt) in enumerate(self._keys):
+            keys[i] = (off, ln, scheme, fmt, 0)
+        items = np.zeros(len(self._items), dtype=ITEM_DTYPE)
+        if self._items:
+            arr = np.array(self._items, dtype=np.uint64)
+            items["sig_off"] = arr[:, 0]
+            items["msg_off"] = arr[:, 1]
+            items["msg_len"] = arr[:, 2]
+            items["key_idx"] = arr[:, 3]
+            items["sig_len"] = arr[:, 4]
+        arena = np.frombuffer(b"".join(self._chunks) + bytes(16), dtype=np.uint8).copy()
+        return Batch(keys, items, arena)

@@ -1,0 +1,367 @@
+// C ABI of the MI355X batch signature-verification engine (include/cordagpu.h).
+//
+// Thin host layer: argument checks, per-context device workspace, H2D/D2H for the
+// host-buffer entry points, and kernel launches through engine.h. No CPU fallback: every
+// verdict is computed by the HIP kernels; if the device is unusable the call fails with
+// CG_ERR_DEVICE and the status bytes stay CG_NOT_RUN.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cordagpu.h"
+#include "engine.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, const char* detail = "") {
+  char buf[512];
+  snprintf(buf, sizeof buf, fmt, detail);
+  g_err = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  char buf[512];
+  snprintf(buf, sizeof buf, "%s: %s", where, hipGetErrorString(e));
+  g_err = buf;
+  return CG_ERR_DEVICE;
+}
+
+#define HIP_TRY(expr, where)               \
+  do {                                     \
+    hipError_t _e = (expr);                \
+    if (_e != hipSuccess) return hip_fail(_e, where); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes + bytes / 4 + 256;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct cg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DevBuf keyprep, keys, items, arena, status, aux0, aux1, aux2;
+};
+
+extern "C" {
+
+int cg_abi_version(void) { return CG_ABI_VERSION; }
+
+const char* cg_build_info(void) {
+  return "corda_amd libcordagpu: HIP kernels for gfx950 (Ed25519 i2p-0.2.0 semantics, ECDSA BC-1.57 semantics, "
+         "SHA-256/512, Merkle tx ids)";
+}
+
+int cg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char* cg_last_error(void) { return g_err.c_str(); }
+
+int cg_open(cg_ctx** out, const cg_config* cfg) {
+  if (!out) return fail(CG_ERR_ARG, "cg_open: out is NULL");
+  *out = nullptr;
+  int dev = cfg ? cfg->device : 0;
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n), "hipGetDeviceCount");
+  if (dev < 0 || dev >= n) return fail(CG_ERR_ARG, "cg_open: device ordinal out of range");
+  HIP_TRY(hipSetDevice(dev), "hipSetDevice");
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties");
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(CG_ERR_DEVICE, "cg_open: kernels are built for gfx950, device is %s", prop.gcnArchName);
+  cg_ctx* c = new cg_ctx();
+  c->device = dev;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return hip_fail(e, "hipStreamCreate");
+  }
+  e = cg::upload_constants();
+  if (e != hipSuccess) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return hip_fail(e, "upload_constants");
+  }
+  *out = c;
+  return CG_OK;
+}
+
+void cg_close(cg_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  c->keyprep.release();
+  c->keys.release();
+  c->items.release();
+  c->arena.release();
+  c->status.release();
+  c->aux0.release();
+  c->aux1.release();
+  c->aux2.release();
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int cg_reserve(cg_ctx* c, uint32_t max_keys, uint64_t max_items) {
+  if (!c) return fail(CG_ERR_ARG, "cg_reserve: ctx is NULL");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(max_keys)), "hipMalloc(keyprep)");
+  (void)max_items;
+  return CG_OK;
+}
+
+int cg_verify_batch_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items,
+                           uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
+                           uint8_t* d_status, void* hip_stream) {
+  if (!c) return fail(CG_ERR_ARG, "cg_verify_batch_device: ctx is NULL");
+  if (n_items && (!d_items || !d_status)) return fail(CG_ERR_ARG, "cg_verify_batch_device: NULL buffer");
+  if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_verify_batch_device: bad mode");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  if (c->keyprep.cap < cg::keyprep_bytes(n_keys)) {
+    // growing the workspace synchronises the device; cg_reserve ahead of time avoids it
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
+  }
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  HIP_TRY(cg::launch_verify(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p, s),
+          "launch_verify");
+  return CG_OK;
+}
+
+int cg_prepare_keys_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena,
+                           uint64_t arena_len, void* hip_stream) {
+  if (!c) return fail(CG_ERR_ARG, "cg_prepare_keys_device: ctx is NULL");
+  if (n_keys && !d_keys) return fail(CG_ERR_ARG, "cg_prepare_keys_device: keys is NULL");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  if (c->keyprep.cap < cg::keyprep_bytes(n_keys)) {
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
+  }
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  HIP_TRY(cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s), "launch_keyprep");
+  return CG_OK;
+}
+
+int cg_verify_items_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items,
+                           uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
+                           uint8_t* d_status, void* hip_stream) {
+  if (!c) return fail(CG_ERR_ARG, "cg_verify_items_device: ctx is NULL");
+  if (n_items && (!d_items || !d_status)) return fail(CG_ERR_ARG, "cg_verify_items_device: NULL buffer");
+  if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_verify_items_device: bad mode");
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->keyprep.cap < cg::keyprep_bytes(n_keys))
+    return fail(CG_ERR_ARG, "cg_verify_items_device: keys were not prepared (call cg_prepare_keys_device)");
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  HIP_TRY(cg::launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p, s),
+          "launch_items");
+  return CG_OK;
+}
+
+int cg_verify_batch(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
+                    const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
+                    cg_stats* stats) {
+  if (!c) return fail(CG_ERR_ARG, "cg_verify_batch: ctx is NULL");
+  if (n_items && (!items || !status_out)) return fail(CG_ERR_ARG, "cg_verify_batch: NULL buffer");
+  if (n_keys && !keys) return fail(CG_ERR_ARG, "cg_verify_batch: keys is NULL");
+  if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_verify_batch: arena is NULL");
+  if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_verify_batch: bad mode");
+  for (uint64_t i = 0; i < n_items; ++i) status_out[i] = CG_NOT_RUN;
+  if (n_items == 0) return CG_OK;
+  auto t0 = std::chrono::steady_clock::now();
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  const size_t arena_alloc = ((arena_len + 3) & ~(uint64_t)3) + 16;
+  HIP_TRY(c->keys.ensure(sizeof(cg_key) * (n_keys ? n_keys : 1)), "hipMalloc(keys)");
+  HIP_TRY(c->items.ensure(sizeof(cg_item) * n_items), "hipMalloc(items)");
+  HIP_TRY(c->arena.ensure(arena_alloc), "hipMalloc(arena)");
+  HIP_TRY(c->status.ensure(n_items), "hipMalloc(status)");
+  HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
+  hipStream_t s = c->stream;
+  hipEvent_t ev[4];
+  for (auto& e : ev) HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+  HIP_TRY(hipEventRecord(ev[0], s), "hipEventRecord");
+  if (n_keys) HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, s), "H2D keys");
+  HIP_TRY(hipMemcpyAsync(c->items.p, items, sizeof(cg_item) * n_items, hipMemcpyHostToDevice, s), "H2D items");
+  if (arena_len) HIP_TRY(hipMemcpyAsync(c->arena.p, arena, arena_len, hipMemcpyHostToDevice, s), "H2D arena");
+  HIP_TRY(hipEventRecord(ev[1], s), "hipEventRecord");
+  HIP_TRY(cg::launch_verify((const cg_key*)c->keys.p, n_keys, (const cg_item*)c->items.p, n_items,
+                            (const uint8_t*)c->arena.p, arena_len, mode, (uint8_t*)c->status.p, c->keyprep.p, s),
+          "launch_verify");
+  HIP_TRY(hipEventRecord(ev[2], s), "hipEventRecord");
+  HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n_items, hipMemcpyDeviceToHost, s), "D2H status");
+  HIP_TRY(hipEventRecord(ev[3], s), "hipEventRecord");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (stats) {
+    float a = 0, b = 0, d = 0;
+    hipEventElapsedTime(&a, ev[0], ev[1]);
+    hipEventElapsedTime(&b, ev[1], ev[2]);
+    hipEventElapsedTime(&d, ev[2], ev[3]);
+    stats->n_items = n_items;
+    stats->n_keys = n_keys;
+    stats->ms_h2d = a;
+    stats->ms_key_prep = 0;
+    stats->ms_verify = b;
+    stats->ms_d2h = d;
+    stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  for (auto& e : ev) hipEventDestroy(e);
+  return CG_OK;
+}
+
+int cg_sha256_batch_device(cg_ctx* c, const cg_span* d_spans, uint64_t n, const uint8_t* d_arena,
+                           uint64_t arena_len, uint8_t* d_digests, void* hip_stream) {
+  if (!c) return fail(CG_ERR_ARG, "cg_sha256_batch_device: ctx is NULL");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  HIP_TRY(cg::launch_sha256(d_spans, n, d_arena, arena_len, d_digests, s), "launch_sha256");
+  return CG_OK;
+}
+
+static int hash_batch(cg_ctx* c, const cg_span* spans, uint64_t n, const uint8_t* arena, uint64_t arena_len,
+                      uint8_t* out, int which) {
+  if (!c) return fail(CG_ERR_ARG, "hash batch: ctx is NULL");
+  if (n && (!spans || !out)) return fail(CG_ERR_ARG, "hash batch: NULL buffer");
+  if (n == 0) return CG_OK;
+  const size_t dlen = which == 256 ? 32 : 64;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  HIP_TRY(c->items.ensure(sizeof(cg_span) * n), "hipMalloc(spans)");
+  HIP_TRY(c->arena.ensure(((arena_len + 3) & ~(uint64_t)3) + 16), "hipMalloc(arena)");
+  HIP_TRY(c->aux0.ensure(dlen * n), "hipMalloc(digests)");
+  HIP_TRY(hipMemcpyAsync(c->items.p, spans, sizeof(cg_span) * n, hipMemcpyHostToDevice, s), "H2D spans");
+  if (arena_len) HIP_TRY(hipMemcpyAsync(c->arena.p, arena, arena_len, hipMemcpyHostToDevice, s), "H2D arena");
+  if (which == 256)
+    HIP_TRY(cg::launch_sha256((const cg_span*)c->items.p, n, (const uint8_t*)c->arena.p, arena_len,
+                              (uint8_t*)c->aux0.p, s), "launch_sha256");
+  else
+    HIP_TRY(cg::launch_sha512((const cg_span*)c->items.p, n, (const uint8_t*)c->arena.p, arena_len,
+                              (uint8_t*)c->aux0.p, s), "launch_sha512");
+  HIP_TRY(hipMemcpyAsync(out, c->aux0.p, dlen * n, hipMemcpyDeviceToHost, s), "D2H digests");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  return CG_OK;
+}
+
+int cg_sha256_batch(cg_ctx* c, const cg_span* spans, uint64_t n, const uint8_t* arena, uint64_t arena_len,
+                    uint8_t* out) {
+  return hash_batch(c, spans, n, arena, arena_len, out, 256);
+}
+int cg_sha512_batch(cg_ctx* c, const cg_span* spans, uint64_t n, const uint8_t* arena, uint64_t arena_len,
+                    uint8_t* out) {
+  return hash_batch(c, spans, n, arena, arena_len, out, 512);
+}
+
+int cg_tx_ids_device(cg_ctx* c, const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps, uint64_t n_comps,
+                     const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids, uint8_t* d_status,
+                     void* hip_stream) {
+  if (!c) return fail(CG_ERR_ARG, "cg_tx_ids_device: ctx is NULL");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  if (c->aux2.cap < 32 * (n_comps ? n_comps : 1)) {
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    HIP_TRY(c->aux2.ensure(32 * (n_comps ? n_comps : 1)), "hipMalloc(leaf ws)");
+  }
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  HIP_TRY(cg::launch_tx_ids(d_txs, n_tx, d_comps, n_comps, d_arena, arena_len, d_ids, d_status,
+                            (uint8_t*)c->aux2.p, s), "launch_tx_ids");
+  return CG_OK;
+}
+
+int cg_tx_ids(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_component* comps, uint64_t n_comps,
+              const uint8_t* arena, uint64_t arena_len, uint8_t* ids_out, uint8_t* status_out) {
+  if (!c) return fail(CG_ERR_ARG, "cg_tx_ids: ctx is NULL");
+  if (n_tx && (!txs || !ids_out || !status_out)) return fail(CG_ERR_ARG, "cg_tx_ids: NULL buffer");
+  if (n_tx == 0) return CG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  HIP_TRY(c->keys.ensure(sizeof(cg_tx) * n_tx), "hipMalloc(txs)");
+  HIP_TRY(c->items.ensure(sizeof(cg_component) * (n_comps ? n_comps : 1)), "hipMalloc(comps)");
+  HIP_TRY(c->arena.ensure(((arena_len + 3) & ~(uint64_t)3) + 16), "hipMalloc(arena)");
+  HIP_TRY(c->aux0.ensure(32 * n_tx), "hipMalloc(ids)");
+  HIP_TRY(c->status.ensure(n_tx), "hipMalloc(status)");
+  HIP_TRY(c->aux2.ensure(32 * (n_comps ? n_comps : 1)), "hipMalloc(leaf ws)");
+  HIP_TRY(hipMemcpyAsync(c->keys.p, txs, sizeof(cg_tx) * n_tx, hipMemcpyHostToDevice, s), "H2D txs");
+  if (n_comps)
+    HIP_TRY(hipMemcpyAsync(c->items.p, comps, sizeof(cg_component) * n_comps, hipMemcpyHostToDevice, s), "H2D comps");
+  if (arena_len) HIP_TRY(hipMemcpyAsync(c->arena.p, arena, arena_len, hipMemcpyHostToDevice, s), "H2D arena");
+  HIP_TRY(cg::launch_tx_ids((const cg_tx*)c->keys.p, n_tx, (const cg_component*)c->items.p, n_comps,
+                            (const uint8_t*)c->arena.p, arena_len, (uint8_t*)c->aux0.p, (uint8_t*)c->status.p,
+                            (uint8_t*)c->aux2.p, s), "launch_tx_ids");
+  HIP_TRY(hipMemcpyAsync(ids_out, c->aux0.p, 32 * n_tx, hipMemcpyDeviceToHost, s), "D2H ids");
+  HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n_tx, hipMemcpyDeviceToHost, s), "D2H status");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  return CG_OK;
+}
+
+int cg_merkle_roots(cg_ctx* c, const uint8_t* leaves, const uint64_t* first, const uint32_t* count, uint64_t n,
+                    uint8_t* roots_out, uint8_t* status_out) {
+  if (!c) return fail(CG_ERR_ARG, "cg_merkle_roots: ctx is NULL");
+  if (n && (!first || !count || !roots_out || !status_out)) return fail(CG_ERR_ARG, "cg_merkle_roots: NULL buffer");
+  if (n == 0) return CG_OK;
+  uint64_t total = 0, ws = 0;
+  std::vector<uint64_t> wsoff(n);
+  for (uint64_t j = 0; j < n; ++j) {
+    if (first[j] + count[j] > total) total = first[j] + count[j];
+    wsoff[j] = ws;
+    ws += count[j];
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  HIP_TRY(c->arena.ensure(32 * (total ? total : 1)), "hipMalloc(leaves)");
+  HIP_TRY(c->keys.ensure(8 * n), "hipMalloc(first)");
+  HIP_TRY(c->items.ensure(4 * n), "hipMalloc(count)");
+  HIP_TRY(c->aux0.ensure(32 * n), "hipMalloc(roots)");
+  HIP_TRY(c->status.ensure(n), "hipMalloc(status)");
+  HIP_TRY(c->aux1.ensure(32 * (ws ? ws : 1)), "hipMalloc(ws)");
+  HIP_TRY(c->aux2.ensure(8 * n), "hipMalloc(wsoff)");
+  if (total) HIP_TRY(hipMemcpyAsync(c->arena.p, leaves, 32 * total, hipMemcpyHostToDevice, s), "H2D leaves");
+  HIP_TRY(hipMemcpyAsync(c->keys.p, first, 8 * n, hipMemcpyHostToDevice, s), "H2D first");
+  HIP_TRY(hipMemcpyAsync(c->items.p, count, 4 * n, hipMemcpyHostToDevice, s), "H2D count");
+  HIP_TRY(hipMemcpyAsync(c->aux2.p, wsoff.data(), 8 * n, hipMemcpyHostToDevice, s), "H2D wsoff");
+  HIP_TRY(cg::launch_merkle_roots((const uint8_t*)c->arena.p, (const uint64_t*)c->keys.p, (const uint32_t*)c->items.p,
+                                  n, (uint8_t*)c->aux0.p, (uint8_t*)c->status.p, (uint8_t*)c->aux1.p,
+                                  (const uint64_t*)c->aux2.p, s),
+          "launch_merkle_roots");
+  HIP_TRY(hipMemcpyAsync(roots_out, c->aux0.p, 32 * n, hipMemcpyDeviceToHost, s), "D2H roots");
+  HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n, hipMemcpyDeviceToHost, s), "D2H status");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  return CG_OK;
+}
+
+}  // extern "C"

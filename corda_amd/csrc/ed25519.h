@@ -1,0 +1,252 @@
+// Ed25519 verification with i2p-eddsa-0.2.0 verdict semantics, one signature per lane.
+//
+// Reference path: Crypto.isValid -> JCA -> i2p EdDSAEngine.engineVerify
+// (core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559, scheme Crypto.kt:120-133).
+// The verdict rule reproduced here (oracle/ed25519_i2p.py restates it):
+//   sig.length != 64                        -> SIG_MALFORMED
+//   h = SHA-512(R || Abyte || M) mod L       (Abyte = canonical re-encoding of decoded A)
+//   S' = slide(S) value = S - 2^256 * escape (no S < L check; the carry i2p's slide()
+//        drops past bit 255 is reproduced by sc_slide_escapes)
+//   accept iff encode(h*(-A) + S'*B) == sig[0..32] byte for byte
+// The arithmetic is our own: signed radix-16 fixed windows (uniform control flow across the
+// 64 lanes of a wave) over a per-key table of 8 multiples of -A and a constant table of 8
+// multiples of B, instead of i2p's vartime sliding window. Same group element, same bytes.
+#pragma once
+#include "ge25519.h"
+#include "sc25519.h"
+#include "sha2.h"
+
+struct Ed25519Consts {
+  fe d, d2, sqrtm1;
+  ge_niels Btab[9];  // index k: k*B (k = 0 is the identity)
+};
+
+// Per-key precomputation (device workspace), produced once per distinct key (the JVM
+// decodes a PublicKey object once: EdDSAPublicKeySpec -> GroupElement + Aneg precompute).
+struct EdKeyPrep {
+  uint32_t status;      // 0 ok, else CG_KEY_INVALID / CG_UNSUPPORTED
+  uint32_t abyte[8];    // canonical encoding of A (hashed into h)
+  uint32_t pad[7];
+  ge_cached tab[9];     // index k: k*(-A) (k = 0 is the identity)
+};
+
+#define ED_ST_VALID 0
+#define ED_ST_INVALID 1
+#define ED_ST_SIG_MALFORMED 2
+#define ED_ST_KEY_INVALID 3
+
+CG_HD void ge_cached_identity(ge_cached& c) {
+  fe_1(c.YpX);
+  fe_1(c.YmX);
+  fe_1(c.Z);
+  fe_0(c.T2d);
+}
+
+CG_HD void ge_niels_identity(ge_niels& c) {
+  fe_1(c.ypx);
+  fe_1(c.ymx);
+  fe_0(c.xy2d);
+}
+
+// i2p GroupElement(curve, byte[] s): y = s with bit 255 masked (y >= p accepted), x from
+// u/v; no square root -> KEY_INVALID; sign fix-up (x = 0 with sign bit 1 is accepted).
+CG_HD int ed_decode_point(ge_p3& A, const uint32_t aw[8], const Ed25519Consts& C) {
+  fe y, yy, u, v, v3, x, vxx, chk;
+  fe_frombytes_words(y, aw);
+  fe_sq(yy, y);
+  fe one;
+  fe_1(one);
+  fe_sub(u, yy, one);
+  fe_carry(u);
+  fe_mul(v, yy, C.d);
+  fe_add(v, v, one);
+  fe_sq(v3, v);
+  fe_mul(v3, v3, v);        // v^3
+  fe_sq(x, v3);
+  fe_mul(x, x, v);          // v^7
+  fe_mul(x, x, u);          // u v^7
+  fe_pow22523(x, x);        // (u v^7)^((p-5)/8)
+  fe_mul(x, x, v3);
+  fe_mul(x, x, u);          // u v^3 (u v^7)^((p-5)/8)
+  fe_sq(vxx, x);
+  fe_mul(vxx, vxx, v);
+  fe_sub(chk, vxx, u);
+  if (!fe_iszero(chk)) {
+    fe_add(chk, vxx, u);
+    if (!fe_iszero(chk)) return ED_ST_KEY_INVALID;
+    fe_mul(x, x, C.sqrtm1);
+  }
+  if ((uint32_t)fe_isnegative(x) != (aw[7] >> 31)) {
+    fe_neg(x, x);
+    fe_carry(x);
+  }
+  fe_copy(A.X, x);
+  fe_copy(A.Y, y);
+  fe_1(A.Z);
+  fe_mul(A.T, x, y);
+  return ED_ST_VALID;
+}
+
+CG_HD void ed_encode_affine(uint32_t out[8], const fe& X, const fe& Y, const fe& Z) {
+  fe zi, x, y;
+  fe_invert(zi, Z);
+  fe_mul(x, X, zi);
+  fe_mul(y, Y, zi);
+  fe_tobytes_words(out, y);
+  out[7] |= (uint32_t)fe_isnegative(x) << 31;
+}
+
+// key bytes (raw A, 32 bytes) -> EdKeyPrep
+CG_HD void ed_key_prep(EdKeyPrep& kp, const uint32_t aw[8], const Ed25519Consts& C) {
+  ge_p3 A;
+  kp.status = (uint32_t)ed_decode_point(A, aw, C);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) kp.pad[i] = 0;
+  if (kp.status != ED_ST_VALID) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kp.abyte[i] = 0;
+    return;
+  }
+  ed_encode_affine(kp.abyte, A.X, A.Y, A.Z);
+  // -A
+  ge_p3 N;
+  fe_neg(N.X, A.X);
+  fe_carry(N.X);
+  fe_copy(N.Y, A.Y);
+  fe_copy(N.Z, A.Z);
+  fe_neg(N.T, A.T);
+  fe_carry(N.T);
+  ge_cached_identity(kp.tab[0]);
+  ge_cached c1;
+  ge_p3_to_cached(c1, N, C.d2);
+  kp.tab[1] = c1;
+  ge_p3 P = N;
+  ge_p1p1 t;
+  for (int k = 2; k <= 8; ++k) {
+    ge_add_cached(t, P, c1);
+    ge_p1p1_to_p3(P, t);
+    ge_p3_to_cached(kp.tab[k], P, C.d2);
+  }
+}
+
+// One signature. sig words: R = sw[0..7], S = sw[8..15] (little-endian).
+CG_HD int ed_verify_core(const EdKeyPrep& kp, const ge_cached* ktab, const uint32_t sw[16], const uint8_t* arena,
+                         uint64_t len_rounded, uint64_t msg_off, uint64_t msg_len, const Ed25519Consts& C,
+                         const ge_niels* btab) {
+  // h = SHA-512(R || Abyte || M) mod L
+  uint32_t pre[16], hw[16], h[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    pre[i] = sw[i];
+    pre[8 + i] = kp.abyte[i];
+  }
+  sha512_prefix64_msg(hw, pre, arena, len_rounded, msg_off, msg_len);
+  sc_reduce512(h, hw);
+  // S' = slide value of S, reduced mod L
+  uint32_t s[8], sr[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = sw[8 + i];
+  sc_reduce256(sr, s);
+  if (s[7] >> 31) {
+    if (sc_slide_escapes(s)) {
+      uint32_t r1[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r1[i] = sc_R1w(i);
+      sc_sub(sr, sr, r1);
+    }
+  }
+  uint32_t eh[16], es[16];
+  sc_recode16(eh, h);
+  sc_recode16(es, sr);
+  // R' = h*(-A) + S'*B, fixed signed radix-16 windows, most significant first
+  ge_p3 R;
+  ge_p3_0(R);
+  ge_p1p1 t;
+  ge_p2 q;
+  for (int i = 63; i >= 0; --i) {
+    if (i != 63) {
+      ge_p3_to_p2(q, R);
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p2(q, t);
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p2(q, t);
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p2(q, t);
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(R, t);
+    }
+    const int da = sc_digit(eh, i);
+    const int db = sc_digit(es, i);
+    const uint32_t ia = (uint32_t)(da < 0 ? -da : da);
+    const uint32_t ib = (uint32_t)(db < 0 ? -db : db);
+    ge_cached ca = ktab[ia];
+    ge_cached_cneg(ca, da < 0);
+    ge_add_cached(t, R, ca);
+    ge_p1p1_to_p3(R, t);
+    ge_niels nb = btab[ib];
+    ge_niels_cneg(nb, db < 0);
+    ge_madd(t, R, nb);
+    ge_p1p1_to_p3(R, t);
+  }
+  uint32_t enc[8];
+  ed_encode_affine(enc, R.X, R.Y, R.Z);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) diff |= enc[i] ^ sw[i];
+  return diff == 0 ? ED_ST_VALID : ED_ST_INVALID;
+}
+
+// Host-side constant construction (also used by the host test build).
+CG_HD void ed_consts_init(Ed25519Consts& C) {
+  fe a, b, t;
+  fe_0(a);
+  a.v[0] = 121665;
+  fe_0(b);
+  b.v[0] = 121666;
+  fe_invert(t, b);
+  fe_mul(C.d, a, t);
+  fe_neg(C.d, C.d);
+  fe_carry(C.d);
+  fe_add(C.d2, C.d, C.d);
+  fe_carry(C.d2);
+  // sqrt(-1) = 2^((p-1)/4): compute as 2^((p-5)/8 * 2 + 1) ... use pow22523: x^((p-5)/8)
+  // with x = 4: sqrt(-1) = 2^((p-1)/4) = (2^2)^((p-5)/8) * 2
+  fe four, two;
+  fe_0(four);
+  four.v[0] = 4;
+  fe_0(two);
+  two.v[0] = 2;
+  fe_pow22523(t, four);
+  fe_mul(C.sqrtm1, t, two);
+  // base point: y = 4/5, x even
+  fe five, y;
+  fe_0(five);
+  five.v[0] = 5;
+  fe_invert(t, five);
+  fe_mul(y, four, t);
+  uint32_t yw[8];
+  fe_tobytes_words(yw, y);
+  ge_p3 B;
+  ed_decode_point(B, yw, C);
+  ge_niels_identity(C.Btab[0]);
+  ge_p3 P = B;
+  ge_cached cb;
+  ge_p3_to_cached(cb, B, C.d2);
+  ge_p1p1 tt;
+  for (int k = 1; k <= 8; ++k) {
+    if (k > 1) {
+      ge_add_cached(tt, P, cb);
+      ge_p1p1_to_p3(P, tt);
+    }
+    fe zi, x, yy, xy;
+    fe_invert(zi, P.Z);
+    fe_mul(x, P.X, zi);
+    fe_mul(yy, P.Y, zi);
+    fe_add(C.Btab[k].ypx, yy, x);
+    fe_carry(C.Btab[k].ypx);
+    fe_sub(C.Btab[k].ymx, yy, x);
+    fe_carry(C.Btab[k].ymx);
+    fe_mul(xy, x, yy);
+    fe_mul(C.Btab[k].xy2d, xy, C.d2);
+  }
+}

@@ -1,0 +1,46 @@
+// Internal interface between the C ABI host code (cordagpu.cpp) and the HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/cordagpu.h"
+
+namespace cg {
+
+struct DeviceConsts;  // opaque
+
+// Upload the constant tables (curve constants, base-point tables) for the current device.
+hipError_t upload_constants();
+
+// Bytes of per-key workspace for n_keys keys.
+size_t keyprep_bytes(uint32_t n_keys);
+
+// Enqueue the whole verify pipeline for one batch on `stream`:
+//   key prep (one lane per key) -> per-scheme verify (one lane per item) -> status bytes.
+hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
+                         void* d_keyprep, hipStream_t stream);
+hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                          void* d_keyprep, hipStream_t stream);
+hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                        const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
+                        const void* d_keyprep, hipStream_t stream);
+
+// Hashing kernels
+hipError_t launch_sha256(const cg_span* d_spans, uint64_t n, const uint8_t* d_arena, uint64_t arena_len,
+                         uint8_t* d_out, hipStream_t stream);
+hipError_t launch_sha512(const cg_span* d_spans, uint64_t n, const uint8_t* d_arena, uint64_t arena_len,
+                         uint8_t* d_out, hipStream_t stream);
+
+// WireTransaction ids: leaf hashing + per-tx Merkle levels. `d_leaf_ws` must hold
+// 32 * n_comps bytes.
+hipError_t launch_tx_ids(const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps, uint64_t n_comps,
+                         const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids, uint8_t* d_status,
+                         uint8_t* d_leaf_ws, hipStream_t stream);
+
+// Merkle roots over independent leaf lists.
+hipError_t launch_merkle_roots(const uint8_t* d_leaves, const uint64_t* d_first, const uint32_t* d_count,
+                               uint64_t n, uint8_t* d_roots, uint8_t* d_status, uint8_t* d_ws,
+                               const uint64_t* d_wsoff, hipStream_t stream);
+
+}  // namespace cg

@@ -1,0 +1,231 @@
+// SHA-256 / SHA-512 batch hashing and Merkle transaction ids for gfx950.
+//
+//   k_sha256 / k_sha512   one lane per message (SecureHash.sha256, SecureHash.kt:37)
+//   k_tx_ids              one lane per WireTransaction: nonce_i = SHA256(salt || BE32(i)),
+//                         leaf_i = SHA256(blob_i || nonce_i) (salt leaf: SHA256(blob)),
+//                         zero-hash padding to 2^k, pairwise SHA256(L || R) levels
+//                         (MerkleTransaction.kt:16-33,93; MerkleTree.kt:27-66)
+//   k_merkle_roots        one lane per leaf list (MerkleTree.getMerkleTree)
+#include <hip/hip_runtime.h>
+
+#include "engine.h"
+#include "sha2.h"
+
+namespace cg {
+
+__device__ __forceinline__ uint64_t r4(uint64_t x) { return (x + 3) & ~(uint64_t)3; }
+
+__global__ void __launch_bounds__(256) k_sha256(const cg_span* __restrict__ spans, uint64_t n,
+                                                const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const cg_span sp = spans[i];
+  uint32_t h[8];
+  if (sp.off > arena_len || sp.len > arena_len - sp.off) {
+    for (int k = 0; k < 8; ++k) h[k] = 0;
+  } else {
+    sha256_arena_suffix(h, arena, r4(arena_len), sp.off, sp.len, nullptr);
+  }
+  uint32_t* o = (uint32_t*)(out + 32 * i);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = __builtin_bswap32(h[k]);
+}
+
+__global__ void __launch_bounds__(256) k_sha512(const cg_span* __restrict__ spans, uint64_t n,
+                                                const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const cg_span sp = spans[i];
+  uint64_t h[8];
+  if (sp.off > arena_len || sp.len > arena_len - sp.off) {
+    for (int k = 0; k < 8; ++k) h[k] = 0;
+  } else {
+    sha512_arena(h, arena, r4(arena_len), sp.off, sp.len);
+  }
+  uint32_t* o = (uint32_t*)(out + 64 * i);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    o[2 * k] = __builtin_bswap32((uint32_t)(h[k] >> 32));
+    o[2 * k + 1] = __builtin_bswap32((uint32_t)h[k]);
+  }
+}
+
+// SHA-256 of a 64-byte message given as 16 big-endian words (one Merkle node)
+__device__ __forceinline__ void sha256_node(uint32_t out[8], const uint32_t l[8], const uint32_t r[8]) {
+  uint32_t s[8], w[16];
+  sha256_init(s);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    w[k] = l[k];
+    w[8 + k] = r[k];
+  }
+  sha256_compress(s, w);
+  w[0] = 0x80000000u;
+#pragma unroll
+  for (int k = 1; k < 15; ++k) w[k] = 0;
+  w[15] = 512;
+  sha256_compress(s, w);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = s[k];
+}
+
+__device__ __forceinline__ void ld_node(uint32_t v[8], const uint8_t* ws, uint64_t idx) {
+  const uint4* p = (const uint4*)(ws + 32 * idx);
+  const uint4 a = p[0], b = p[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st_node(uint8_t* ws, uint64_t idx, const uint32_t v[8]) {
+  uint4* p = (uint4*)(ws + 32 * idx);
+  p[0] = make_uint4(v[0], v[1], v[2], v[3]);
+  p[1] = make_uint4(v[4], v[5], v[6], v[7]);
+}
+
+// In-place Merkle reduction of n big-endian-word leaves at ws[base .. base+n); root -> root.
+__device__ void merkle_inplace(uint32_t root[8], uint8_t* ws, uint64_t base, uint32_t n) {
+  if (n == 1) {
+    ld_node(root, ws, base);
+    return;
+  }
+  uint32_t m = 1;
+  while (m < n) m <<= 1;
+  uint32_t real = n;  // entries of the current level that are stored (the rest are zeroHash)
+  while (m > 1) {
+    const uint32_t half = m >> 1;
+    for (uint32_t j = 0; j < half; ++j) {
+      uint32_t l[8], r[8], o[8];
+      if (2 * j < real) ld_node(l, ws, base + 2 * j);
+      else for (int k = 0; k < 8; ++k) l[k] = 0;
+      if (2 * j + 1 < real) ld_node(r, ws, base + 2 * j + 1);
+      else for (int k = 0; k < 8; ++k) r[k] = 0;
+      sha256_node(o, l, r);
+      if (half == 1) {
+        for (int k = 0; k < 8; ++k) root[k] = o[k];
+      } else {
+        st_node(ws, base + j, o);
+      }
+    }
+    real = half;
+    m = half;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_tx_ids(const cg_tx* __restrict__ txs, uint64_t n_tx,
+                                                const cg_component* __restrict__ comps, uint64_t n_comps,
+                                                const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                uint8_t* __restrict__ ids, uint8_t* __restrict__ status,
+                                                uint8_t* __restrict__ ws) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tx) return;
+  const cg_tx tx = txs[t];
+  uint32_t root[8];
+  uint8_t st = 0;
+  const uint64_t lr = r4(arena_len);
+  if (tx.n == 0 || tx.first > n_comps || tx.n > n_comps - tx.first || tx.salt_off > arena_len ||
+      arena_len - tx.salt_off < 32) {
+    st = 1;
+    for (int k = 0; k < 8; ++k) root[k] = 0;
+  } else {
+    uint32_t salt_be[9];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) salt_be[k] = __builtin_bswap32(cg_ld_bytes4(arena, lr, tx.salt_off + 4 * k));
+    for (uint32_t i = 0; i < tx.n; ++i) {
+      const cg_component c = comps[tx.first + i];
+      uint32_t leaf[8];
+      if (c.off > arena_len || c.len > arena_len - c.off) {
+        st = 2;
+        for (int k = 0; k < 8; ++k) leaf[k] = 0;
+      } else if (c.flags & 1u) {
+        sha256_arena_suffix(leaf, arena, lr, c.off, c.len, nullptr);
+      } else {
+        // nonce = SHA256(salt || BE32(i)) : 36 bytes, one block
+        uint32_t s[8], w[16], nonce[8];
+        sha256_init(s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = salt_be[k];
+        w[8] = i;
+        w[9] = 0x80000000u;
+#pragma unroll
+        for (int k = 10; k < 15; ++k) w[k] = 0;
+        w[15] = 36 * 8;
+        sha256_compress(s, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nonce[k] = s[k];
+        sha256_arena_suffix(leaf, arena, lr, c.off, c.len, nonce);
+      }
+      st_node(ws, tx.first + i, leaf);
+    }
+    merkle_inplace(root, ws, tx.first, tx.n);
+  }
+  uint32_t* o = (uint32_t*)(ids + 32 * t);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = __builtin_bswap32(root[k]);
+  status[t] = st;
+}
+
+// leaves: raw digest bytes; ws holds a copy of each list (big-endian words) at first[j]
+__global__ void __launch_bounds__(256) k_merkle_roots(const uint8_t* __restrict__ leaves,
+                                                      const uint64_t* __restrict__ first,
+                                                      const uint32_t* __restrict__ count, uint64_t n,
+                                                      uint8_t* __restrict__ roots, uint8_t* __restrict__ status,
+                                                      uint8_t* __restrict__ ws, const uint64_t* __restrict__ wsoff) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t cnt = count[j];
+  uint32_t root[8];
+  if (cnt == 0) {
+    for (int k = 0; k < 8; ++k) root[k] = 0;
+    status[j] = 1;
+  } else {
+    const uint64_t f = first[j], b = wsoff[j];
+    for (uint32_t i = 0; i < cnt; ++i) {
+      uint32_t v[8];
+      ld_node(v, leaves, f + i);
+      for (int k = 0; k < 8; ++k) v[k] = __builtin_bswap32(v[k]);
+      st_node(ws, b + i, v);
+    }
+    merkle_inplace(root, ws, b, cnt);
+    status[j] = 0;
+  }
+  uint32_t* o = (uint32_t*)(roots + 32 * j);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) o[k] = __builtin_bswap32(root[k]);
+}
+
+static unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+hipError_t launch_sha256(const cg_span* d_spans, uint64_t n, const uint8_t* d_arena, uint64_t arena_len,
+                         uint8_t* d_out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_sha256, dim3(blocks(n)), dim3(256), 0, s, d_spans, n, d_arena, arena_len, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sha512(const cg_span* d_spans, uint64_t n, const uint8_t* d_arena, uint64_t arena_len,
+                         uint8_t* d_out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_sha512, dim3(blocks(n)), dim3(256), 0, s, d_spans, n, d_arena, arena_len, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_tx_ids(const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps, uint64_t n_comps,
+                         const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids, uint8_t* d_status,
+                         uint8_t* d_leaf_ws, hipStream_t s) {
+  if (!n_tx) return hipSuccess;
+  hipLaunchKernelGGL(k_tx_ids, dim3(blocks(n_tx)), dim3(256), 0, s, d_txs, n_tx, d_comps, n_comps, d_arena,
+                     arena_len, d_ids, d_status, d_leaf_ws);
+  return hipGetLastError();
+}
+
+hipError_t launch_merkle_roots(const uint8_t* d_leaves, const uint64_t* d_first, const uint32_t* d_count, uint64_t n,
+                               uint8_t* d_roots, uint8_t* d_status, uint8_t* d_ws, const uint64_t* d_wsoff,
+                               hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_merkle_roots, dim3(blocks(n)), dim3(256), 0, s, d_leaves, d_first, d_count, n, d_roots,
+                     d_status, d_ws, d_wsoff);
+  return hipGetLastError();
+}
+
+}  // namespace cg

@@ -1,0 +1,302 @@
+// FIPS 180-4 SHA-256 / SHA-512 for one message per lane (host + device).
+//
+// Messages are read straight out of the caller's arena with 4-byte loads
+// (unaligned offsets handled by a funnel shift), so nothing is staged per item.
+// SHA-512 runs on 64-bit words (two VGPRs each); on gfx950 a 64-bit rotate is two
+// v_alignbit_b32, a 64-bit add one v_add_co + one v_addc.
+#pragma once
+#include "fe25519.h"
+
+#if defined(__HIPCC__)
+#define CG_BSWAP32(x) __builtin_bswap32(x)
+#else
+#define CG_BSWAP32(x) __builtin_bswap32(x)
+#endif
+
+CG_HD uint32_t cg_ld32(const uint8_t* p) { return *(const uint32_t*)p; }
+
+// 4 little-endian bytes at arena[off..off+4); bytes at or past `len_rounded` (the arena
+// length rounded up to 4) read as 0. The arena base must be 4-byte aligned.
+CG_HD uint32_t cg_ld_bytes4(const uint8_t* arena, uint64_t len_rounded, uint64_t off) {
+  const uint64_t a0 = off & ~(uint64_t)3;
+  const uint32_t sh = (uint32_t)(off & 3) * 8u;
+  const uint32_t w0 = a0 < len_rounded ? cg_ld32(arena + a0) : 0u;
+  if (sh == 0) return w0;
+  const uint32_t w1 = (a0 + 4) < len_rounded ? cg_ld32(arena + a0 + 4) : 0u;
+  return (w0 >> sh) | (w1 << (32u - sh));
+}
+
+// Big-endian 32-bit word at message byte position `pos` (multiple of 4) of msg||0x80||0..
+// with only the message part loaded; `len` = message length.
+CG_HD uint32_t cg_msg_word_be(const uint8_t* arena, uint64_t len_rounded, uint64_t msg_off, uint64_t len,
+                              uint64_t pos) {
+  uint32_t raw = 0;
+  if (pos < len) raw = cg_ld_bytes4(arena, len_rounded, msg_off + pos);
+  const uint64_t rem = len > pos ? len - pos : 0;  // valid bytes in this word (capped below)
+  uint32_t w;
+  if (rem >= 4) {
+    w = raw;
+  } else {
+    const uint32_t keep = rem ? (0xffffffffu >> (32u - 8u * (uint32_t)rem)) : 0u;
+    w = raw & keep;
+    if (pos <= len) w |= 0x80u << (8u * (uint32_t)rem);  // pad byte lives in this word
+  }
+  return CG_BSWAP32(w);
+}
+
+// ----------------------------------------------------------------- SHA-512
+CG_HD uint64_t cg_rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+CG_HD uint64_t cg_k512(int i) {
+  const uint64_t K[80] = {
+      0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+      0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+      0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+      0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+      0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+      0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+      0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+      0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+      0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+      0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+      0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+      0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+      0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+      0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+      0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+      0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+      0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+      0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+      0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+      0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+  return K[i];
+}
+
+CG_HD void sha512_init(uint64_t s[8]) {
+  s[0] = 0x6a09e667f3bcc908ULL;
+  s[1] = 0xbb67ae8584caa73bULL;
+  s[2] = 0x3c6ef372fe94f82bULL;
+  s[3] = 0xa54ff53a5f1d36f1ULL;
+  s[4] = 0x510e527fade682d1ULL;
+  s[5] = 0x9b05688c2b3e6c1fULL;
+  s[6] = 0x1f83d9abfb41bd6bULL;
+  s[7] = 0x5be0cd19137e2179ULL;
+}
+
+CG_HD void sha512_compress(uint64_t s[8], uint64_t w[16]) {
+  uint64_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+  for (int i = 0; i < 80; ++i) {
+    uint64_t wi;
+    if (i < 16) {
+      wi = w[i];
+    } else {
+      const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+      const uint64_t s0 = cg_rotr64(w15, 1) ^ cg_rotr64(w15, 8) ^ (w15 >> 7);
+      const uint64_t s1 = cg_rotr64(w2, 19) ^ cg_rotr64(w2, 61) ^ (w2 >> 6);
+      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    const uint64_t t1 = h + (cg_rotr64(e, 14) ^ cg_rotr64(e, 18) ^ cg_rotr64(e, 41)) + ((e & f) ^ (~e & g)) +
+                        cg_k512(i) + wi;
+    const uint64_t t2 = (cg_rotr64(a, 28) ^ cg_rotr64(a, 34) ^ cg_rotr64(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  s[0] += a;
+  s[1] += b;
+  s[2] += c;
+  s[3] += d;
+  s[4] += e;
+  s[5] += f;
+  s[6] += g;
+  s[7] += h;
+}
+
+// SHA-512(prefix64 || msg) where prefix64 is 16 little-endian words (e.g. R || Abyte).
+// Output: the 64 digest bytes as 16 little-endian words (ready for sc_reduce512).
+CG_HD void sha512_prefix64_msg(uint32_t out[16], const uint32_t prefix[16], const uint8_t* arena,
+                               uint64_t len_rounded, uint64_t msg_off, uint64_t msg_len) {
+  uint64_t s[8];
+  sha512_init(s);
+  const uint64_t n = 64 + msg_len;
+  const uint64_t nblocks = (n + 17 + 127) >> 7;
+  for (uint64_t blk = 0; blk < nblocks; ++blk) {
+    uint64_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t pos = blk * 128 + (uint64_t)j * 8;  // stream byte position
+      uint32_t hi, lo;
+      if (pos < 64) {
+        hi = CG_BSWAP32(prefix[pos >> 2]);
+        lo = CG_BSWAP32(prefix[(pos >> 2) + 1]);
+      } else {
+        hi = cg_msg_word_be(arena, len_rounded, msg_off, msg_len, pos - 64);
+        lo = cg_msg_word_be(arena, len_rounded, msg_off, msg_len, pos - 60);
+      }
+      // a block's padding words beyond the message read as 0 (or 0x80..); the final 16 bytes
+      // of the last block carry the bit length
+      if (blk == nblocks - 1 && j == 15) {
+        hi = (uint32_t)((n * 8) >> 32);
+        lo = (uint32_t)(n * 8);
+      } else if (blk == nblocks - 1 && j == 14) {
+        hi = 0;
+        lo = 0;
+      }
+      w[j] = ((uint64_t)hi << 32) | lo;
+    }
+    sha512_compress(s, w);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    out[2 * k] = CG_BSWAP32((uint32_t)(s[k] >> 32));
+    out[2 * k + 1] = CG_BSWAP32((uint32_t)s[k]);
+  }
+}
+
+// Plain SHA-512 of arena[off, off+len)
+CG_HD void sha512_arena(uint64_t s_out[8], const uint8_t* arena, uint64_t len_rounded, uint64_t off, uint64_t len) {
+  uint64_t s[8];
+  sha512_init(s);
+  const uint64_t nblocks = (len + 17 + 127) >> 7;
+  for (uint64_t blk = 0; blk < nblocks; ++blk) {
+    uint64_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t pos = blk * 128 + (uint64_t)j * 8;
+      uint32_t hi = cg_msg_word_be(arena, len_rounded, off, len, pos);
+      uint32_t lo = cg_msg_word_be(arena, len_rounded, off, len, pos + 4);
+      if (blk == nblocks - 1 && j == 15) {
+        hi = (uint32_t)((len * 8) >> 32);
+        lo = (uint32_t)(len * 8);
+      } else if (blk == nblocks - 1 && j == 14) {
+        hi = 0;
+        lo = 0;
+      }
+      w[j] = ((uint64_t)hi << 32) | lo;
+    }
+    sha512_compress(s, w);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s_out[k] = s[k];
+}
+
+// ----------------------------------------------------------------- SHA-256
+CG_HD uint32_t cg_rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+CG_HD uint32_t cg_k256(int i) {
+  const uint32_t K[64] = {
+      0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+      0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+      0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+      0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+      0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+      0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+      0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+      0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+  return K[i];
+}
+
+CG_HD void sha256_init(uint32_t s[8]) {
+  s[0] = 0x6a09e667;
+  s[1] = 0xbb67ae85;
+  s[2] = 0x3c6ef372;
+  s[3] = 0xa54ff53a;
+  s[4] = 0x510e527f;
+  s[5] = 0x9b05688c;
+  s[6] = 0x1f83d9ab;
+  s[7] = 0x5be0cd19;
+}
+
+CG_HD void sha256_compress(uint32_t s[8], uint32_t w[16]) {
+  uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    uint32_t wi;
+    if (i < 16) {
+      wi = w[i];
+    } else {
+      const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+      const uint32_t s0 = cg_rotr32(w15, 7) ^ cg_rotr32(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = cg_rotr32(w2, 17) ^ cg_rotr32(w2, 19) ^ (w2 >> 10);
+      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    const uint32_t t1 =
+        h + (cg_rotr32(e, 6) ^ cg_rotr32(e, 11) ^ cg_rotr32(e, 25)) + ((e & f) ^ (~e & g)) + cg_k256(i) + wi;
+    const uint32_t t2 = (cg_rotr32(a, 2) ^ cg_rotr32(a, 13) ^ cg_rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  s[0] += a;
+  s[1] += b;
+  s[2] += c;
+  s[3] += d;
+  s[4] += e;
+  s[5] += f;
+  s[6] += g;
+  s[7] += h;
+}
+
+// SHA-256 of arena[off, off+len) || suffix (0 or 32 bytes given as 8 big-endian words;
+// used for serialised-component || nonce, MerkleTransaction.kt:23). Output: the state as
+// 8 big-endian words (the digest).
+CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t len_rounded, uint64_t off,
+                               uint64_t len, const uint32_t* suffix_be /* 8 words or null */) {
+  uint32_t s[8];
+  sha256_init(s);
+  const uint64_t sfx = suffix_be ? 32 : 0;
+  const uint64_t n = len + sfx;
+  const uint64_t nblocks = (n + 9 + 63) >> 6;
+  for (uint64_t blk = 0; blk < nblocks; ++blk) {
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t pos = blk * 64 + (uint64_t)j * 4;
+      uint32_t v;
+      if (pos + 4 <= len) {
+        v = CG_BSWAP32(cg_ld_bytes4(arena, len_rounded, off + pos));
+      } else if (sfx && (len & 3) == 0 && pos >= len && pos + 4 <= n) {
+        v = suffix_be[(pos - len) >> 2];
+      } else if (pos > n) {
+        v = 0;
+      } else {
+        uint32_t acc = 0;
+        for (int bb = 0; bb < 4; ++bb) {
+          const uint64_t p = pos + (uint64_t)bb;
+          uint32_t byte;
+          if (p < len) {
+            byte = cg_ld_bytes4(arena, len_rounded, off + p) & 0xffu;
+          } else if (p < n) {
+            const uint64_t q = p - len;
+            byte = (suffix_be[q >> 2] >> (24 - 8 * (q & 3))) & 0xffu;
+          } else {
+            byte = (p == n) ? 0x80u : 0u;
+          }
+          acc = (acc << 8) | byte;
+        }
+        v = acc;
+      }
+      w[j] = v;
+    }
+    if (blk == nblocks - 1) {
+      w[14] = (uint32_t)((n * 8) >> 32);
+      w[15] = (uint32_t)(n * 8);
+    }
+    sha256_compress(s, w);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = s[k];
+}

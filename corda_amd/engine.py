@@ -1,0 +1,131 @@
+"""One MI355X verification context (``cg_ctx``) per device, over the C ABI.
+
+``Engine.verify(batch)`` is the batch form of Crypto.isValid / Crypto.doVerify
+(core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:474-484,553-559): one status byte
+per item, codes as in include/cordagpu.h. ``Engine.verify_device`` is the same on
+buffers already resident in HBM (raw device pointers, e.g. ``torch.Tensor.data_ptr()``).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .batch import COMPONENT_DTYPE, MODE_DOVERIFY, SPAN_DTYPE, TX_DTYPE
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None and a.size else None
+
+
+class Engine:
+    def __init__(self, device=0):
+        L = _lib.lib()
+        cfg = _lib.cg_config(device, 0, 0, 0)
+        h = ctypes.c_void_p()
+        _lib.check(L.cg_open(ctypes.byref(h), ctypes.byref(cfg)), f"cg_open(device={device})")
+        self._h = h
+        self.device = device
+        self.last_stats = None
+
+    def close(self):
+        if self._h:
+            _lib.lib().cg_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ signatures
+    def verify(self, batch, mode=MODE_DOVERIFY):
+        st = np.full(batch.n, 255, dtype=np.uint8)
+        stats = _lib.cg_stats()
+        rc = _lib.lib().cg_verify_batch(self._h, _p(batch.keys), len(batch.keys), _p(batch.items), batch.n,
+                                        _p(batch.arena), batch.arena.size, mode, _p(st), ctypes.byref(stats))
+        _lib.check(rc, "cg_verify_batch")
+        self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_stats._fields_}
+        return st
+
+    def reserve(self, max_keys, max_items):
+        _lib.check(_lib.lib().cg_reserve(self._h, max_keys, max_items), "cg_reserve")
+
+    def verify_device(self, d_keys, n_keys, d_items, n_items, d_arena, arena_len, d_status, mode=MODE_DOVERIFY,
+                      stream=0):
+        """Asynchronous: enqueues on `stream` (a hipStream_t as int; 0 = the context's stream)."""
+        rc = _lib.lib().cg_verify_batch_device(self._h, d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode,
+                                               d_status, stream or None)
+        _lib.check(rc, "cg_verify_batch_device")
+
+    def prepare_keys_device(self, d_keys, n_keys, d_arena, arena_len, stream=0):
+        _lib.check(_lib.lib().cg_prepare_keys_device(self._h, d_keys, n_keys, d_arena, arena_len, stream or None),
+                   "cg_prepare_keys_device")
+
+    def verify_items_device(self, d_keys, n_keys, d_items, n_items, d_arena, arena_len, d_status,
+                            mode=MODE_DOVERIFY, stream=0):
+        rc = _lib.lib().cg_verify_items_device(self._h, d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode,
+                                               d_status, stream or None)
+        _lib.check(rc, "cg_verify_items_device")
+
+    # ------------------------------------------------------------------ hashing
+    @staticmethod
+    def _spans(msgs):
+        chunks, spans, off = [], np.zeros(len(msgs), dtype=SPAN_DTYPE), 0
+        for i, m in enumerate(msgs):
+            pad = (-off) % 4
+            if pad:
+                chunks.append(bytes(pad))
+                off += pad
+            spans[i] = (off, len(m))
+            chunks.append(bytes(m))
+            off += len(m)
+        arena = np.frombuffer(b"".join(chunks) + bytes(8), dtype=np.uint8).copy()
+        return spans, arena
+
+    def sha256(self, msgs):
+        spans, arena = self._spans(msgs)
+        out = np.zeros(32 * len(msgs), dtype=np.uint8)
+        _lib.check(_lib.lib().cg_sha256_batch(self._h, _p(spans), len(msgs), _p(arena), arena.size - 8, _p(out)),
+                   "cg_sha256_batch")
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(len(msgs))]
+
+    def sha512(self, msgs):
+        spans, arena = self._spans(msgs)
+        out = np.zeros(64 * len(msgs), dtype=np.uint8)
+        _lib.check(_lib.lib().cg_sha512_batch(self._h, _p(spans), len(msgs), _p(arena), arena.size - 8, _p(out)),
+                   "cg_sha512_batch")
+        return [out[64 * i:64 * i + 64].tobytes() for i in range(len(msgs))]
+
+    def merkle_roots(self, leaf_lists):
+        """MerkleTree.getMerkleTree(leaves).hash for each list; returns (roots, status)."""
+        n = len(leaf_lists)
+        first = np.zeros(n, dtype=np.uint64)
+        count = np.zeros(n, dtype=np.uint32)
+        flat, pos = [], 0
+        for j, lv in enumerate(leaf_lists):
+            first[j] = pos
+            count[j] = len(lv)
+            flat.extend(bytes(x) for x in lv)
+            pos += len(lv)
+        leaves = np.frombuffer(b"".join(flat) + bytes(32), dtype=np.uint8).copy()
+        roots = np.zeros(32 * n, dtype=np.uint8)
+        st = np.zeros(n, dtype=np.uint8)
+        _lib.check(_lib.lib().cg_merkle_roots(self._h, _p(leaves), _p(first), _p(count), n, _p(roots), _p(st)),
+                   "cg_merkle_roots")
+        return [roots[32 * j:32 * j + 32].tobytes() for j in range(n)], st
+
+    def tx_ids(self, txs, comps, arena):
+        """WireTransaction.id for packed transactions (TX_DTYPE / COMPONENT_DTYPE / arena)."""
+        assert txs.dtype == TX_DTYPE and comps.dtype == COMPONENT_DTYPE
+        ids = np.zeros(32 * len(txs), dtype=np.uint8)
+        st = np.zeros(len(txs), dtype=np.uint8)
+        _lib.check(_lib.lib().cg_tx_ids(self._h, _p(txs), len(txs), _p(comps), len(comps), _p(arena), arena.size,
+                                        _p(ids), _p(st)), "cg_tx_ids")
+        return ids.reshape(-1, 32), st

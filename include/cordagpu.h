@@ -1,0 +1,198 @@
+/* cordagpu.h — C ABI of the MI355X batch signature-verification engine for Corda.
+ *
+ * This is the drop-in boundary. Every entry point is plain C: pointers,
+ * sizes and status bytes; no torch, HIP or C++ types. A JVM binds it with JNI / Panama
+ * (INTEGRATION.md), Python with ctypes (corda_amd/_lib.py).
+ *
+ * What each entry point replaces in the reference (paths relative to the Corda tree):
+ *
+ *   cg_verify_batch      N x Crypto.isValid / Crypto.doVerify(scheme, publicKey, sig, clear)
+ *                        core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:474-484 (doVerify)
+ *                        and :553-559 (isValid -> JCA Signature.initVerify/update/verify into
+ *                        i2p EdDSAEngine / BouncyCastle SHA256withECDSA). Serial callers:
+ *                        TransactionWithSignatures.checkSignaturesAreValid
+ *                        (core/.../transactions/TransactionWithSignatures.kt:58-62).
+ *   cg_verify_batch_device  the same, with every buffer already resident in HBM (verifier
+ *                        process / bench: no PCIe in the timed region).
+ *   cg_sha256_batch      N x SecureHash.sha256(bytes)   core/.../crypto/SecureHash.kt:37
+ *   cg_sha512_batch      N x SHA-512 (the EdDSA challenge digest, i2p engine)
+ *   cg_tx_ids            N x WireTransaction.id = MerkleTree.getMerkleTree(
+ *                        availableComponentHashes).hash  core/.../transactions/WireTransaction.kt:39,104,
+ *                        MerkleTransaction.kt:16-33,74-93, core/.../crypto/MerkleTree.kt:27-66
+ *   cg_merkle_roots      N x MerkleTree.getMerkleTree(leaves).hash  MerkleTree.kt:27-66
+ *
+ * Status bytes never collapse to "valid": an item the engine did not run is CG_NOT_RUN.
+ * Ownership: the caller owns every buffer; the library copies what it needs and keeps no
+ * pointer after a call returns. Threading: a cg_ctx serialises its own calls internally;
+ * distinct contexts (one per GPU) run concurrently.
+ */
+#ifndef CORDAGPU_H
+#define CORDAGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CG_ABI_VERSION 1
+
+/* Corda SignatureScheme.schemeNumberID (Crypto.kt:78-184). Others => CG_UNSUPPORTED. */
+enum {
+  CG_RSA_SHA256 = 1,
+  CG_ECDSA_SECP256K1_SHA256 = 2,
+  CG_ECDSA_SECP256R1_SHA256 = 3,
+  CG_EDDSA_ED25519_SHA512 = 4,
+  CG_SPHINCS256_SHA256 = 5,
+  CG_COMPOSITE_KEY = 6
+};
+
+/* Public-key byte formats. */
+enum {
+  CG_KEY_RAW = 0,  /* Ed25519: 32-byte A (what Kryo writes, Kryo.kt:333); ECDSA: 64-byte X||Y big-endian */
+  CG_KEY_SPKI = 1, /* X.509 SubjectPublicKeyInfo DER == PublicKey.getEncoded() (44 / 91 / 88 bytes) */
+  CG_KEY_SEC1 = 2  /* ECDSA only: 04||X||Y or 02/03||X */
+};
+
+/* Per-item verdicts. */
+enum {
+  CG_VALID = 0,         /* isValid == true */
+  CG_INVALID = 1,       /* isValid == false; doVerify => SignatureException("Signature Verification failed!") */
+  CG_SIG_MALFORMED = 2, /* engine SignatureException: Ed25519 length != 64, ECDSA DER decode failure */
+  CG_KEY_INVALID = 3,   /* key decode IllegalArgumentException / InvalidKeyException */
+  CG_UNSUPPORTED = 4,   /* IllegalArgumentException("Unsupported key/algorithm ...") */
+  CG_EMPTY = 5,         /* doVerify: IllegalArgumentException("Signature data is empty!" / "Clear data is empty...") */
+  CG_NOT_RUN = 255
+};
+
+/* Verification semantics. */
+enum {
+  CG_MODE_DOVERIFY = 0, /* Crypto.doVerify: empty sig / clear => CG_EMPTY */
+  CG_MODE_ISVALID = 1   /* Crypto.isValid: no empty checks (empty sig => CG_SIG_MALFORMED) */
+};
+
+/* Infrastructure return codes (per-item outcomes are always in status_out). */
+enum {
+  CG_OK = 0,
+  CG_ERR_ARG = -1,
+  CG_ERR_DEVICE = -2,
+  CG_ERR_NOMEM = -3,
+  CG_ERR_RANGE = -4 /* an offset/length points outside the arena */
+};
+
+/* One public key, referenced by index from items (the JVM's PublicKey object). */
+typedef struct cg_key {
+  uint64_t off;      /* key bytes at arena[off .. off+len) */
+  uint16_t len;
+  uint8_t scheme;    /* CG_* scheme id */
+  uint8_t fmt;       /* CG_KEY_* */
+  uint32_t reserved; /* must be 0 */
+} cg_key;            /* 16 bytes */
+
+/* One signature to verify: (keys[key_idx], sig, clear). */
+typedef struct cg_item {
+  uint64_t sig_off;  /* signature bytes at arena[sig_off .. sig_off+sig_len) */
+  uint64_t msg_off;  /* clear data at arena[msg_off .. msg_off+msg_len) */
+  uint32_t msg_len;
+  uint32_t key_idx;  /* index into the cg_key table */
+  uint16_t sig_len;
+  uint16_t reserved0;
+  uint32_t reserved1;
+} cg_item;           /* 32 bytes */
+
+/* One variable-length message for the hashing entry points. */
+typedef struct cg_span {
+  uint64_t off;
+  uint64_t len;
+} cg_span;
+
+/* Transaction component (Kryo-serialised bytes produced on the host). */
+typedef struct cg_component {
+  uint64_t off;
+  uint32_t len;
+  uint32_t flags;    /* bit 0: privacy-salt leaf (hashed without nonce, MerkleTransaction.kt:23-30) */
+} cg_component;      /* 16 bytes */
+
+/* One WireTransaction: components comps[first .. first+n) in availableComponents order
+ * (inputs, attachments, outputs, commands, notary?, timeWindow?, privacySalt). */
+typedef struct cg_tx {
+  uint64_t first;
+  uint32_t n;
+  uint32_t reserved;
+  uint64_t salt_off; /* 32-byte PrivacySalt value at arena[salt_off] (nonce = SHA256(salt||BE32(i))) */
+} cg_tx;             /* 24 bytes */
+
+typedef struct cg_config {
+  int32_t device;        /* HIP device ordinal */
+  uint32_t flags;        /* reserved, 0 */
+  uint64_t max_items;    /* workspace sizing hint (0 = grow on demand) */
+  uint64_t max_arena;    /* workspace sizing hint (0 = grow on demand) */
+} cg_config;
+
+typedef struct cg_stats {
+  uint64_t n_items;
+  uint64_t n_keys;
+  double ms_h2d;         /* host->device copy (host-buffer entry points only) */
+  double ms_key_prep;    /* key decode + table build kernels */
+  double ms_verify;      /* verify kernels */
+  double ms_d2h;
+  double ms_total;
+} cg_stats;
+
+typedef struct cg_ctx cg_ctx;
+
+/* Library / device info. */
+int cg_abi_version(void);
+const char* cg_build_info(void);
+int cg_device_count(void);
+const char* cg_last_error(void); /* thread-local message for the last non-OK return */
+
+int cg_open(cg_ctx** out, const cg_config* cfg);
+void cg_close(cg_ctx* ctx);
+
+/* Host buffers in, host status bytes out (copies through pinned staging). */
+int cg_verify_batch(cg_ctx* ctx, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
+                    const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
+                    cg_stats* stats_opt);
+
+/* Device-resident buffers (HBM pointers) on the caller's HIP stream (hipStream_t as void*,
+ * NULL = default stream). Asynchronous: returns after enqueueing; status is valid once the
+ * stream has reached that point. Workspace comes from the ctx (reserve with cg_reserve). */
+int cg_reserve(cg_ctx* ctx, uint32_t max_keys, uint64_t max_items);
+int cg_verify_batch_device(cg_ctx* ctx, const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items,
+                           uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
+                           uint8_t* d_status, void* hip_stream);
+/* The two halves of cg_verify_batch_device: decode + precompute every key of the table into
+ * the ctx workspace (the JVM's PublicKey construction), then verify items against it. A
+ * verify call must follow a prepare call for the same key table on the same stream. */
+int cg_prepare_keys_device(cg_ctx* ctx, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena,
+                           uint64_t arena_len, void* hip_stream);
+int cg_verify_items_device(cg_ctx* ctx, const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items,
+                           uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
+                           uint8_t* d_status, void* hip_stream);
+
+/* Hashing. digests_out: 32*n (sha256) / 64*n (sha512) bytes. */
+int cg_sha256_batch(cg_ctx* ctx, const cg_span* spans, uint64_t n, const uint8_t* arena, uint64_t arena_len,
+                    uint8_t* digests_out);
+int cg_sha512_batch(cg_ctx* ctx, const cg_span* spans, uint64_t n, const uint8_t* arena, uint64_t arena_len,
+                    uint8_t* digests_out);
+int cg_sha256_batch_device(cg_ctx* ctx, const cg_span* d_spans, uint64_t n, const uint8_t* d_arena,
+                           uint64_t arena_len, uint8_t* d_digests, void* hip_stream);
+
+/* Merkle roots of n independent leaf lists: leaf list j = leaves[32*first[j] .. 32*(first[j]+count[j])).
+ * A list with count 0 gets status 1 (MerkleTreeException) and a zero root. */
+int cg_merkle_roots(cg_ctx* ctx, const uint8_t* leaves, const uint64_t* first, const uint32_t* count,
+                    uint64_t n, uint8_t* roots_out, uint8_t* status_out);
+
+/* WireTransaction ids: ids_out 32*n_tx bytes; status_out 0 ok / 1 empty tx. */
+int cg_tx_ids(cg_ctx* ctx, const cg_tx* txs, uint64_t n_tx, const cg_component* comps, uint64_t n_comps,
+              const uint8_t* arena, uint64_t arena_len, uint8_t* ids_out, uint8_t* status_out);
+int cg_tx_ids_device(cg_ctx* ctx, const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps,
+                     uint64_t n_comps, const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids,
+                     uint8_t* d_status, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CORDAGPU_H */

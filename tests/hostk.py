@@ -1,0 +1,53 @@
+"""ctypes access to tests/native/libhostkernels.so (host build of the HIP lane code)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "native", "libhostkernels.so")
+P = 2 ** 255 - 19
+L = 2 ** 252 + 27742317777372353535851937790883648493
+OFFS = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+
+
+def build():
+    src = os.path.join(HERE, "native", "host_kernels.cpp")
+    if not os.path.exists(SO) or os.path.getmtime(SO) < max(
+            os.path.getmtime(os.path.join(HERE, "..", "corda_amd", "csrc", f))
+            for f in os.listdir(os.path.join(HERE, "..", "corda_amd", "csrc")) if f.endswith(".h")) or \
+            os.path.getmtime(SO) < os.path.getmtime(src):
+        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-DFE_BOUNDS_CHECK", "-fPIC", "-shared",
+                               "-o", SO, src])
+    return ctypes.CDLL(SO)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = build()
+    return _lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def limbs_to_int(v):
+    return sum(int(x) << o for x, o in zip(v, OFFS))
+
+
+def int_to_limbs(x):
+    out = []
+    for i, o in enumerate(OFFS):
+        w = 26 if i % 2 == 0 else 25
+        out.append((x >> o) & ((1 << w) - 1))
+    return np.array(out, dtype=np.uint32)
+
+
+def words(b):
+    return np.frombuffer(bytes(b), dtype="<u4").copy()

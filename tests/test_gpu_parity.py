@@ -1,0 +1,164 @@
+"""GPU parity tests: the HIP path through the C ABI against the oracle.
+
+Every verdict / digest is compared bit-for-bit with the CPU restatement of the reference
+(oracle/, C and Python) on the same inputs:
+  * the committed golden fixtures (tests/golden/*.json; RFC 8032, OpenSSL-cross-checked
+    valid signatures, every Appendix A corruption class), in doVerify and isValid modes;
+  * seeded synthetic batches at the BASELINE configs' shape, checked item by item against
+    the C oracle (liboracle.so) and against the corruption labels;
+  * SHA-256 / SHA-512 / Merkle / tx-id fixtures.
+"""
+import numpy as np
+import pytest
+
+import golden_io
+from corda_amd import batch as B
+from oracle import c_oracle, corda as ocorda
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(engine, items_json, mode):
+    b, exp, exp_iv = golden_io.sig_batch(items_json)
+    st = engine.verify(b, mode)
+    want = exp if mode == B.MODE_DOVERIFY else exp_iv
+    bad = np.nonzero(st != want)[0]
+    msgs = [f"{items_json[i]['class']} {items_json[i]['note']}: want {B.STATUS_NAMES[int(want[i])]} "
+            f"got {B.STATUS_NAMES.get(int(st[i]), st[i])}" for i in bad[:20]]
+    assert len(bad) == 0, "\n".join(msgs)
+
+
+@pytest.mark.parametrize("mode", [B.MODE_DOVERIFY, B.MODE_ISVALID])
+def test_ed25519_golden(engine, mode):
+    _check(engine, golden_io.load("ed25519.json"), mode)
+
+
+@pytest.mark.parametrize("mode", [B.MODE_DOVERIFY, B.MODE_ISVALID])
+def test_ecdsa_golden(engine, mode):
+    items = golden_io.load("ecdsa.json")
+    b, exp, exp_iv = golden_io.sig_batch(items)
+    st = engine.verify(b, mode)
+    want = exp if mode == B.MODE_DOVERIFY else exp_iv
+    if np.all(st[[i for i, it in enumerate(items)]] == B.NOT_RUN):
+        pytest.xfail("ECDSA kernels not built into this library yet")
+    bad = np.nonzero(st != want)[0]
+    msgs = [f"{items[i]['class']} {items[i]['note']}: want {B.STATUS_NAMES[int(want[i])]} "
+            f"got {B.STATUS_NAMES.get(int(st[i]), st[i])}" for i in bad[:20]]
+    assert len(bad) == 0, "\n".join(msgs)
+
+
+def test_mixed_golden_shuffled(engine):
+    """Ed25519 and ECDSA items interleaved in one batch, shuffled, keys shared."""
+    items = golden_io.load("ed25519.json") + golden_io.load("ecdsa.json")
+    rng = np.random.default_rng(3)
+    perm = rng.permutation(len(items))
+    items = [items[i] for i in perm]
+    b, exp, _ = golden_io.sig_batch(items)
+    st = engine.verify(b, B.MODE_DOVERIFY)
+    ed = np.array([it["scheme"] == 4 for it in items])
+    assert np.array_equal(st[ed], exp[ed])
+    ec_ok = np.all(st[~ed] == exp[~ed]) or np.all(st[~ed] == B.NOT_RUN)
+    assert ec_ok
+
+
+def test_synthetic_ed25519_vs_c_oracle(engine):
+    from tools.workload import wl
+    b, labels = wl.ed25519_batch(60000, n_keys=512, msg_len=270, corrupt_permille=150, seed=11, bad_key_every=64,
+                                 nthreads=16)
+    st = engine.verify(b, B.MODE_DOVERIFY)
+    ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
+    assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
+    # labels: A1/A2/A3/A6 invalid, A4 valid, A7 malformed (where the key decodes)
+    kok = ref != B.KEY_INVALID
+    assert np.all(st[(labels == 0) & kok] == B.VALID)
+    assert np.all(st[np.isin(labels, [1, 2, 3, 6]) & kok] == B.INVALID)
+    assert np.all(st[(labels == 4) & kok] == B.VALID)
+    assert np.all(st[(labels == 7) & kok] == B.SIG_MALFORMED)
+
+
+def test_edge_batches(engine):
+    from corda_amd.batch import BatchBuilder
+    items = golden_io.load("ed25519.json")
+    # empty batch
+    eb = BatchBuilder().build()
+    assert engine.verify(eb).size == 0
+    # unsupported scheme, bad key index, item outside the arena
+    bb = BatchBuilder()
+    it = items[5]
+    k = bb.key(4, 0, bytes.fromhex(it["key"]))
+    bb.add(k, bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"]))
+    k1 = bb.key(1, 1, b"\x30" * 300)  # RSA key: unsupported
+    bb.add(k1, b"\x01" * 256, b"m")
+    b = bb.build()
+    items_arr = b.items.copy()
+    extra = np.zeros(2, dtype=B.ITEM_DTYPE)
+    extra[0] = items_arr[0]
+    extra[0]["key_idx"] = 99  # out of range
+    extra[1] = items_arr[0]
+    extra[1]["msg_off"] = b.arena.size + 100  # outside arena
+    b.items = np.concatenate([items_arr, extra])
+    st = engine.verify(b)
+    assert st.tolist() == [B.STATUS_BY_NAME[it["expect"]], B.UNSUPPORTED, B.NOT_RUN, B.NOT_RUN]
+
+
+def test_sha_fixtures(engine):
+    fx = golden_io.load("sha.json")
+    msgs = [bytes.fromhex(x["msg"]) for x in fx]
+    assert [d.hex() for d in engine.sha256(msgs)] == [x["sha256"] for x in fx]
+    assert [d.hex() for d in engine.sha512(msgs)] == [x["sha512"] for x in fx]
+
+
+def test_merkle_fixtures(engine):
+    from corda_amd import merkle
+    fx = golden_io.load("merkle.json")
+    roots = [x for x in fx if x["kind"] == "root"]
+    got, st = engine.merkle_roots([[bytes.fromhex(l) for l in x["leaves"]] for x in roots] + [[]])
+    assert [g.hex() for g in got[:-1]] == [x["root"] for x in roots]
+    assert st.tolist() == [0] * len(roots) + [1]
+    txs = [x for x in fx if x["kind"] == "txid"]
+    ids, st = merkle.tx_ids([([bytes.fromhex(c) for c in x["components"]], bytes.fromhex(x["salt"]),
+                              bytes.fromhex(x["salt_blob"])) for x in txs], engine)
+    assert [i.hex() for i in ids] == [x["id"] for x in txs]
+
+
+def test_tx_ids_random_vs_oracle(engine):
+    from corda_amd import merkle
+    rng = np.random.default_rng(5)
+    txs = []
+    for t in range(3000):
+        n = int(rng.integers(0, 20))
+        blobs = [rng.integers(0, 256, int(rng.integers(0, 700)), dtype=np.uint8).tobytes() for _ in range(n)]
+        salt = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        txs.append((blobs, salt, b"\x01" + salt))
+    ids, st = merkle.tx_ids(txs, engine)
+    for (blobs, salt, sb), got in zip(txs, ids):
+        assert got == ocorda.tx_id(blobs, salt, sb)
+    assert np.all(st == 0)
+
+
+def test_crypto_api_behaviour():
+    """The reference's own behavioural tests (CryptoUtilsTest.kt:233-286,
+    TransactionSignatureTest.kt:33-40) through the host mirror."""
+    from corda_amd.crypto import (Crypto, IllegalArgumentException, PublicKey, SignatureException)
+    from oracle import ed25519_i2p as ed
+    seed = ed.entropy_seed(70)
+    pub = PublicKey(4, ed.public_from_seed(seed))
+    data = b"Hello World"
+    sig = ed.sign(seed, data)
+    assert Crypto.do_verify(pub, sig, data) is True
+    assert Crypto.is_valid(pub, sig, data) is True
+    with pytest.raises(IllegalArgumentException):
+        Crypto.do_verify(pub, sig, b"")
+    with pytest.raises(IllegalArgumentException):
+        Crypto.do_verify(pub, b"", data)
+    zeros = bytes(100)
+    assert Crypto.do_verify(pub, ed.sign(seed, zeros), zeros)
+    big = np.random.default_rng(1).integers(0, 256, 1000000, dtype=np.uint8).tobytes()
+    assert Crypto.do_verify(pub, ed.sign(seed, big), big)
+    bad = bytearray(sig)
+    bad[0] = (bad[0] + 1) & 0xFF
+    with pytest.raises(SignatureException):
+        Crypto.do_verify(pub, bytes(bad), data)
+    assert Crypto.is_valid(pub, bytes(bad), data) is False
+    with pytest.raises(SignatureException):
+        Crypto.is_valid(pub, sig[:63], data)

@@ -1,0 +1,123 @@
+"""The exact lane arithmetic of the HIP kernels (corda_amd/csrc/*.h), compiled for the
+host with FE_BOUNDS_CHECK (every limb bound assumed by fe25519.h is asserted; a violated
+bound aborts the process), checked against Python big integers and the oracle.
+CPU only: this is where kernel arithmetic is debugged before it reaches a GPU."""
+import random
+
+import numpy as np
+
+import golden_io
+import hostk
+from hostk import L, P, limbs_to_int, ptr, words
+from oracle import c_oracle, ed25519_i2p as ed
+
+TIGHT = [(1 << 26) - 1 if i % 2 == 0 else (1 << 25) + (1 << 18) for i in range(10)]
+
+
+def test_fe_mul_sq_bounds_and_values():
+    lib = hostk.lib()
+    rng = random.Random(1)
+    out = np.zeros(10, dtype=np.uint32)
+    for trial in range(4000):
+        fm, gm = rng.choice([1, 2, 3, 5]), rng.choice([1, 2, 3])
+        if trial < 64:
+            f = np.array([t * fm for t in TIGHT], dtype=np.uint32)
+            g = np.array([t * gm for t in TIGHT], dtype=np.uint32)
+        else:
+            f = np.array([rng.randrange(0, t * fm + 1) for t in TIGHT], dtype=np.uint32)
+            g = np.array([rng.randrange(0, t * gm + 1) for t in TIGHT], dtype=np.uint32)
+        lib.t_fe_mul(ptr(f), ptr(g), ptr(out))
+        assert limbs_to_int(out) % P == limbs_to_int(f) * limbs_to_int(g) % P
+        if fm <= 2:
+            lib.t_fe_sq(ptr(f), ptr(out))
+            assert limbs_to_int(out) % P == limbs_to_int(f) ** 2 % P
+
+
+def test_fe_tobytes_canonical():
+    lib = hostk.lib()
+    rng = random.Random(2)
+    w = np.zeros(8, dtype=np.uint32)
+    for trial in range(3000):
+        m = rng.choice([1, 2, 3, 5])
+        f = np.array([rng.randrange(0, t * m + 1) for t in TIGHT], dtype=np.uint32)
+        if trial < 40:  # values near p and 2p
+            v = (P + rng.randrange(-40, 40)) % (1 << 255)
+            f = hostk.int_to_limbs(v)
+        lib.t_fe_tobytes(ptr(f), ptr(w))
+        assert int.from_bytes(w.tobytes(), "little") == limbs_to_int(f) % P
+
+
+def test_fe_invert():
+    lib = hostk.lib()
+    rng = random.Random(3)
+    out = np.zeros(10, dtype=np.uint32)
+    for _ in range(50):
+        x = rng.randrange(1, P)
+        lib.t_fe_invert(ptr(hostk.int_to_limbs(x)), ptr(out))
+        assert limbs_to_int(out) * x % P == 1
+
+
+def test_sc_reduce512():
+    lib = hostk.lib()
+    rng = random.Random(4)
+    o = np.zeros(8, dtype=np.uint32)
+    for trial in range(3000):
+        x = rng.getrandbits(512) if trial > 6 else [0, 2 ** 512 - 1, L, 2 * L, L - 1, 2 ** 256, L * L][trial]
+        lib.t_sc_reduce512(ptr(words(x.to_bytes(64, "little"))), ptr(o))
+        assert int.from_bytes(o.tobytes(), "little") == x % L
+
+
+def test_slide_escape_matches_literal_slide():
+    lib = hostk.lib()
+    rng = random.Random(5)
+    for trial in range(3000):
+        s = rng.getrandbits(256) | (1 << 255) if trial % 3 else rng.getrandbits(256)
+        if trial < 4:
+            s = [2 ** 256 - 1, 2 ** 255, 2 ** 256 - L, 2 ** 255 + 2 ** 251][trial]
+        sb = s.to_bytes(32, "little")
+        assert bool(lib.t_slide_escapes(ptr(words(sb)))) == (ed.slide_value(sb) < 0)
+
+
+def test_recode16():
+    lib = hostk.lib()
+    rng = random.Random(6)
+    d = np.zeros(64, dtype=np.int32)
+    for _ in range(500):
+        a = rng.randrange(0, L)
+        lib.t_recode16(ptr(words(a.to_bytes(32, "little"))), ptr(d))
+        assert sum(int(x) << (4 * i) for i, x in enumerate(d)) == a
+        assert d.min() >= -8 and d.max() <= 8
+
+
+def test_ed25519_lane_verify_on_fixtures():
+    lib = hostk.lib()
+    n = 0
+    for it in golden_io.load("ed25519.json"):
+        key, sig, msg = bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"])
+        if it["key_fmt"] != 0 or len(key) != 32 or len(sig) != 64:
+            continue
+        m = np.frombuffer(msg + bytes(8), dtype=np.uint8).copy()
+        st = lib.t_ed_verify(ptr(words(key)), ptr(words(sig)), ptr(m), len(msg))
+        got = {0: "VALID", 1: "INVALID", 3: "KEY_INVALID"}[st]
+        assert got == it["expect_isvalid"], it["note"]
+        n += 1
+    assert n > 200
+
+
+def test_sha_lane_code():
+    import ctypes
+    lib = hostk.lib()
+    rng = np.random.default_rng(7)
+    out = np.zeros(16, dtype=np.uint32)
+    for ln in list(range(0, 300, 7)) + [111, 112, 239, 240]:
+        msg = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+        pre = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+        for off in (0, 1, 2, 3):
+            buf = np.frombuffer(bytes(off) + msg + bytes(16), dtype=np.uint8).copy()
+            lib.t_sha512_prefix(ptr(words(pre)), ptr(buf), ctypes.c_uint64(off), ctypes.c_uint64(ln), ptr(out))
+            assert out.tobytes() == c_oracle.sha512(pre + msg)
+            sfx = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+            o8 = np.zeros(8, dtype=np.uint32)
+            sw = np.frombuffer(sfx, dtype=">u4").astype(np.uint32)
+            lib.t_sha256_suffix(ptr(buf), ctypes.c_uint64(off), ctypes.c_uint64(ln), ptr(sw), ptr(o8))
+            assert o8.astype(">u4").tobytes() == c_oracle.sha256(msg + sfx)

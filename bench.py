@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
     ap.add_argument("--threads", type=int, default=0, help="host threads for data generation / CPU baseline")
+    ap.add_argument("--ecdsa-items", type=int, default=1 << 18,
+                    help="items of the secondary ECDSA measurement (N = 1 only; 0 disables)")
     return ap.parse_args()
 
 
@@ -113,47 +115,72 @@ def main():
     status_d = torch.full((batch.n,), 255, dtype=torch.uint8, device=dev)
     gathered = torch.empty((world * batch.n,), dtype=torch.uint8, device=dev) if world > 1 else None
     n_keys, n_items, arena_len = len(batch.keys), batch.n, int(batch.arena.size)
-    stream = torch.cuda.current_stream(dev)
+    # one explicit stream for the engine, the timing events and the RCCL all-gather
+    stream = torch.cuda.Stream(device=dev)
     sptr = stream.cuda_stream
+    torch.cuda.set_stream(stream)
 
-    ev = []
+    def run(keys_t, n_keys_, items_t, n_items_, arena_t, arena_len_, status_t, steps, warmup, gather):
+        ev = []
 
-    def step(timed):
-        eng.prepare_keys_device(keys_d.data_ptr(), n_keys, arena_d.data_ptr(), arena_len, sptr)
-        if timed:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        eng.verify_items_device(keys_d.data_ptr(), n_keys, items_d.data_ptr(), n_items, arena_d.data_ptr(),
-                                arena_len, status_d.data_ptr(), 0, sptr)
-        if timed:
-            e1.record(stream)
-            ev.append((e0, e1))
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, status_d)
+        def step(timed):
+            eng.prepare_keys_device(keys_t.data_ptr(), n_keys_, arena_t.data_ptr(), arena_len_, sptr)
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            eng.verify_items_device(keys_t.data_ptr(), n_keys_, items_t.data_ptr(), n_items_, arena_t.data_ptr(),
+                                    arena_len_, status_t.data_ptr(), 0, sptr)
+            if timed:
+                e1.record(stream)
+                ev.append((e0, e1))
+            if gather:
+                dist.all_gather_into_tensor(gathered, status_t)
 
-    for _ in range(a.warmup):
-        step(False)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t = time.perf_counter()
-    for _ in range(a.steps):
-        step(True)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        for _ in range(warmup):
+            step(False)
+        torch.cuda.synchronize(dev)
+        if gather:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(steps):
+            step(True)
+        torch.cuda.synchronize(dev)
+        if gather:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t
+        if gather:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el, float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
 
-    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev])) if ev else float("nan")
+    elapsed, kern_ms = run(keys_d, n_keys, items_d, n_items, arena_d, arena_len, status_d, a.steps, a.warmup,
+                           world > 1)
+
+    extra = {}
+    if world == 1 and a.ecdsa_items > 0:
+        # BASELINE configs[2] shape (secp256r1 / secp256k1 batches), outside the headline value
+        for curve, name in ((1, "ecdsa_secp256r1"), (0, "ecdsa_secp256k1")):
+            pool = min(a.ecdsa_items, 65536)
+            eb, _ = wl.ecdsa_batch(curve, pool, n_keys=2048, msg_len=a.msg_len, corrupt_permille=100,
+                                   seed=a.seed + 17 + curve, nthreads=threads)
+            reps = max(1, a.ecdsa_items // pool)
+            items_rep = np.tile(eb.items, reps)
+            ek = torch.from_numpy(eb.keys.view(np.uint8)).to(dev)
+            ei = torch.from_numpy(items_rep.view(np.uint8)).to(dev)
+            ea = torch.from_numpy(eb.arena).to(dev)
+            es = torch.full((len(items_rep),), 255, dtype=torch.uint8, device=dev)
+            el, km = run(ek, len(eb.keys), ei, len(items_rep), ea, int(eb.arena.size), es, max(2, a.steps // 2), 1,
+                         False)
+            n_e = len(items_rep)
+            extra[name] = {"value": round(n_e * max(2, a.steps // 2) / el, 1), "unit": "sigs/s",
+                           "items": n_e, "unique_items": pool, "kernel_ms": round(km, 3)}
+
     st = status_d.cpu().numpy()
-    counts = {k: int(v) for k, v in zip(*np.unique(st, return_counts=True))}
+    counts = {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}
     # label sanity (full parity lives in tests/test_gpu_parity.py)
     valid_ok = bool(np.all(st[labels == 0] == 0))
 
@@ -186,7 +213,7 @@ def main():
                                    "corrupted sigs", "items_per_gpu": n_items, "keys": n_keys,
                        "msg_len": a.msg_len, "corrupt_permille": a.corrupt_permille,
                        "parallelism": f"shard{world}" + ("+rccl_allgather(verdicts)" if world > 1 else "")},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "secondary": extra,
             "verdicts": {"counts": counts, "valid_labels_all_valid": valid_ok},
             "gen_s": round(gen_s, 1),
         }

@@ -23,8 +23,10 @@
 
 #if defined(__HIPCC__)
 #define CG_HD __host__ __device__ __forceinline__
+#define CG_HDS __host__ __device__ static __forceinline__  // static member functions
 #else
 #define CG_HD static inline
+#define CG_HDS static inline
 #endif
 
 #ifdef FE_BOUNDS_CHECK

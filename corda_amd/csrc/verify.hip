@@ -9,6 +9,7 @@
 // behind Crypto.doVerify (Crypto.kt:474-484).
 #include <hip/hip_runtime.h>
 
+#include "ecdsa.h"
 #include "ed25519.h"
 #include "engine.h"
 
@@ -88,6 +89,53 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
   status[i] = st;
 }
 
+// ------------------------------------------------------------------ ECDSA (BC 1.57 semantics)
+__constant__ EcConsts c_ec[2];  // [CG_CURVE_K1], [CG_CURVE_R1]
+
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_keyprep(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   EcKeyPrep* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_keys) return;
+  const cg_key k = keys[i];
+  const uint8_t want = C == CG_CURVE_R1 ? CG_ECDSA_SECP256R1_SHA256 : CG_ECDSA_SECP256K1_SHA256;
+  if (k.scheme != want) return;
+  if (!in_arena(k.off, k.len, arena_len)) {
+    out[i].status = CG_KEY_INVALID;
+    return;
+  }
+  const uint32_t st = ec_key_prep_bytes<C>(out[i], arena, round4(arena_len), k.off, k.len, k.fmt, c_ec[C]);
+  out[i].status = st ? CG_KEY_INVALID : 0u;
+}
+
+template <int C>
+__global__ void __launch_bounds__(256) k_ec_verify(const cg_item* __restrict__ items, uint64_t n_items,
+                                                   const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                   const EcKeyPrep* __restrict__ kps,
+                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   uint32_t mode, uint8_t* __restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items) return;
+  const cg_item it = items[i];
+  if (it.key_idx >= n_keys) return;
+  const uint8_t want = C == CG_CURVE_R1 ? CG_ECDSA_SECP256R1_SHA256 : CG_ECDSA_SECP256K1_SHA256;
+  if (keys[it.key_idx].scheme != want) return;
+  const EcKeyPrep* kp = kps + it.key_idx;
+  uint8_t st;
+  if (kp->status != 0) {
+    st = CG_KEY_INVALID;
+  } else if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
+    st = CG_EMPTY;
+  } else if (!in_arena(it.sig_off, it.sig_len, arena_len) || !in_arena(it.msg_off, it.msg_len, arena_len)) {
+    st = CG_NOT_RUN;
+  } else {
+    st = (uint8_t)ecdsa_verify_core<C>(*kp, arena, round4(arena_len), it.sig_off, it.sig_len, it.msg_off, it.msg_len,
+                                       c_ec[C]);
+  }
+  status[i] = st;
+}
+
 __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_items, const cg_key* __restrict__ keys,
                               uint32_t n_keys, uint8_t* __restrict__ status) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -100,24 +148,32 @@ __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_item
   const uint8_t s = keys[ki].scheme;
   if (s != CG_EDDSA_ED25519_SHA512 && s != CG_ECDSA_SECP256R1_SHA256 && s != CG_ECDSA_SECP256K1_SHA256)
     status[i] = CG_UNSUPPORTED;
-  else if (s != CG_EDDSA_ED25519_SHA512)
-    status[i] = CG_NOT_RUN;  // ECDSA kernels overwrite
 }
 
 hipError_t upload_constants() {
   Ed25519Consts h;
   ed_consts_init(h);
-  return hipMemcpyToSymbol(HIP_SYMBOL(c_ed), &h, sizeof h, 0, hipMemcpyHostToDevice);
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_ed), &h, sizeof h, 0, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return e;
+  EcConsts k[2];
+  ec_consts_init<CG_CURVE_K1>(k[CG_CURVE_K1]);
+  ec_consts_init<CG_CURVE_R1>(k[CG_CURVE_R1]);
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_ec), k, sizeof k, 0, hipMemcpyHostToDevice);
 }
 
-size_t keyprep_bytes(uint32_t n_keys) { return (size_t)(n_keys ? n_keys : 1) * sizeof(EdKeyPrep); }
+// workspace: [EdKeyPrep x n_keys][EcKeyPrep x n_keys]
+static size_t ed_region(uint32_t n_keys) { return ((size_t)(n_keys ? n_keys : 1) * sizeof(EdKeyPrep) + 255) & ~(size_t)255; }
+size_t keyprep_bytes(uint32_t n_keys) { return ed_region(n_keys) + (size_t)(n_keys ? n_keys : 1) * sizeof(EcKeyPrep); }
 
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream) {
   if (n_keys == 0) return hipSuccess;
   const uint32_t B = 64;  // one wave per block: keys are few, spread them over CUs
-  hipLaunchKernelGGL(k_ed_keyprep, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, d_arena,
-                     arena_len, (EdKeyPrep*)d_keyprep);
+  const dim3 g((n_keys + B - 1) / B);
+  EcKeyPrep* ec = (EcKeyPrep*)((uint8_t*)d_keyprep + ed_region(n_keys));
+  hipLaunchKernelGGL(k_ed_keyprep, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, (EdKeyPrep*)d_keyprep);
+  hipLaunchKernelGGL(k_ec_keyprep<CG_CURVE_R1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, ec);
+  hipLaunchKernelGGL(k_ec_keyprep<CG_CURVE_K1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, ec);
   return hipGetLastError();
 }
 
@@ -131,6 +187,11 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
                      d_status);
   hipLaunchKernelGGL(k_ed_verify, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
                      (const EdKeyPrep*)d_keyprep, d_arena, arena_len, mode, d_status);
+  const EcKeyPrep* ec = (const EcKeyPrep*)((const uint8_t*)d_keyprep + ed_region(n_keys));
+  hipLaunchKernelGGL(k_ec_verify<CG_CURVE_R1>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys,
+                     n_keys, ec, d_arena, arena_len, mode, d_status);
+  hipLaunchKernelGGL(k_ec_verify<CG_CURVE_K1>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys,
+                     n_keys, ec, d_arena, arena_len, mode, d_status);
   return hipGetLastError();
 }
 

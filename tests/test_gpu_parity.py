@@ -162,3 +162,28 @@ def test_crypto_api_behaviour():
     assert Crypto.is_valid(pub, bytes(bad), data) is False
     with pytest.raises(SignatureException):
         Crypto.is_valid(pub, sig[:63], data)
+
+
+@pytest.mark.parametrize("curve", [0, 1])
+def test_synthetic_ecdsa_vs_c_oracle(engine, curve):
+    from tools.workload import wl
+    b, labels = wl.ecdsa_batch(curve, 20000, n_keys=256, msg_len=270, corrupt_permille=150, seed=21 + curve,
+                               nthreads=16)
+    st = engine.verify(b, B.MODE_DOVERIFY)
+    ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
+    assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
+    assert np.all(st[labels == 0] == B.VALID) and np.all(st[labels == 2] == B.VALID)
+    assert np.all(st[np.isin(labels, [1, 3])] == B.INVALID)
+    assert np.all(st[np.isin(labels, [6, 7])] == B.SIG_MALFORMED)
+
+
+def test_mixed_notary_batch_vs_c_oracle(engine):
+    """Config 5 shape in miniature: 70% Ed25519 / 20% P-256 / 10% k1, shuffled."""
+    from tools.workload import wl
+    e, _ = wl.ed25519_batch(14000, n_keys=256, corrupt_permille=120, seed=31, nthreads=16)
+    r1, _ = wl.ecdsa_batch(1, 4000, n_keys=128, corrupt_permille=100, seed=32, nthreads=16)
+    k1, _ = wl.ecdsa_batch(0, 2000, n_keys=128, corrupt_permille=100, seed=33, nthreads=16)
+    b, _ = wl.concat([e, r1, k1], shuffle_seed=34)
+    st = engine.verify(b, B.MODE_DOVERIFY)
+    ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
+    assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"

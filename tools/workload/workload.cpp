@@ -321,3 +321,258 @@ uint64_t wl_ed25519_arena_bytes(uint64_t n_items, uint32_t n_keys, uint32_t msg_
   return 32ull * n_keys + ((64 + msg_len + 3 + 4) & ~3ull) * n_items + 64;
 }
 }
+
+// ---------------------------------------------------------------- ECDSA (secp256r1 / k1)
+#include "../../corda_amd/csrc/ecdsa.h"
+
+namespace {
+EcConsts g_K[2];
+u256w g_gcx[2][64][9], g_gcy[2][64][9];  // comb: d * 16^i * G, affine Montgomery
+bool g_ec_init = false;
+
+template <int C>
+void ec_comb_init() {
+  ec_consts_init<C>(g_K[C]);
+  Jac P = {g_K[C].gx[1], g_K[C].gy[1], g_K[C].one_p};
+  for (int i = 0; i < 64; ++i) {
+    u256w px, py;
+    jac_to_affine<C>(px, py, P, g_K[C]);
+    ec_table8<C>(g_gcx[C][i], g_gcy[C][i], px, py, g_K[C]);
+    for (int k = 0; k < 4; ++k) jac_dbl<C>(P, P);
+  }
+}
+
+void ec_init() {
+  if (!g_ec_init) {
+    ec_comb_init<CG_CURVE_K1>();
+    ec_comb_init<CG_CURVE_R1>();
+    g_ec_init = true;
+  }
+}
+
+// affine plain (x, y) of k*G (k < n), via the comb (digits of k in [-8, 8], 65 windows)
+template <int C>
+void ec_mul_base(u256w& x, u256w& y, const u256w& k) {
+  uint32_t d[17];
+  ec_recode16(d, k);
+  Jac R;
+  u256_zero(R.X);
+  R.Y = g_K[C].one_p;
+  u256_zero(R.Z);
+  for (int i = 0; i <= 64; ++i) {
+    const int a = i == 64 ? (int)d[16] : ec_digit(d, i);
+    if (!a) continue;
+    const int ia = a < 0 ? -a : a;
+    // window 64 has weight 16^64 = 16 * 16^63
+    u256w yy = i == 64 ? g_gcy[C][63][1] : g_gcy[C][i][ia];
+    u256w xx = i == 64 ? g_gcx[C][63][1] : g_gcx[C][i][ia];
+    if (i == 64) {  // carry digit (0 or 1): add 16 * (16^63 G) via 4 doublings of a copy
+      Jac T = {xx, yy, g_K[C].one_p};
+      for (int k2 = 0; k2 < 4; ++k2) jac_dbl<C>(T, T);
+      u256w tx, ty;
+      jac_to_affine<C>(tx, ty, T, g_K[C]);
+      xx = tx;
+      yy = ty;
+    }
+    if (a < 0) mm_neg<C, 0>(yy, yy);
+    jac_madd<C>(R, R, xx, yy, g_K[C]);
+  }
+  u256w xm, ym, one;
+  jac_to_affine<C>(xm, ym, R, g_K[C]);
+  u256_zero(one);
+  one.w[0] = 1;
+  mm_mul<C, 0>(x, xm, one);
+  mm_mul<C, 0>(y, ym, one);
+}
+
+void put_be32(uint8_t* out, const u256w& v) {
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t w = v.w[7 - i];
+    out[4 * i] = (uint8_t)(w >> 24);
+    out[4 * i + 1] = (uint8_t)(w >> 16);
+    out[4 * i + 2] = (uint8_t)(w >> 8);
+    out[4 * i + 3] = (uint8_t)w;
+  }
+}
+
+// DER INTEGER of a non-negative 256-bit value (minimal), returns bytes written
+int der_int_enc(uint8_t* out, const u256w& v, bool extra_pad) {
+  uint8_t be[32];
+  put_be32(be, v);
+  int s = 0;
+  while (s < 31 && be[s] == 0) ++s;
+  const bool pad = (be[s] & 0x80) != 0 || extra_pad;
+  const int len = 32 - s + (pad ? 1 : 0);
+  out[0] = 0x02;
+  out[1] = (uint8_t)len;
+  int o = 2;
+  if (pad) out[o++] = 0;
+  memcpy(out + o, be + s, 32 - s);
+  return 2 + len;
+}
+
+template <int C>
+void rand_scalar(u256w& k, uint64_t& s) {
+  for (;;) {
+    for (int i = 0; i < 8; ++i) k.w[i] = (uint32_t)splitmix(s);
+    if (!u256_iszero(k) && u256_lt_mod<C, 1>(k)) return;
+  }
+}
+
+// sign: returns DER length; r_out/s_out plain
+template <int C>
+int ec_sign(uint8_t* der, const u256w& d, const uint8_t* msg, size_t len, uint64_t& rng, int cls, u256w& r,
+            u256w& s) {
+  const EcConsts& K = g_K[C];
+  uint32_t h[8];
+  sha256_arena_suffix(h, msg, (len + 3) & ~3ull, 0, len, nullptr);
+  u256w e;
+  for (int i = 0; i < 8; ++i) e.w[i] = h[7 - i];
+  if (!u256_lt_mod<C, 1>(e)) {
+    uint32_t br = 0;
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t x = (uint64_t)e.w[i] - Mod<C, 1>::w(i) - br;
+      e.w[i] = (uint32_t)x;
+      br = (uint32_t)(x >> 63);
+    }
+  }
+  for (;;) {
+    u256w k, x, y;
+    rand_scalar<C>(k, rng);
+    ec_mul_base<C>(x, y, k);
+    r = x;
+    if (!u256_lt_mod<C, 1>(r)) {
+      uint32_t br = 0;
+      for (int i = 0; i < 8; ++i) {
+        const uint64_t t = (uint64_t)r.w[i] - Mod<C, 1>::w(i) - br;
+        r.w[i] = (uint32_t)t;
+        br = (uint32_t)(t >> 63);
+      }
+    }
+    if (u256_iszero(r)) continue;
+    // s = k^-1 (e + r d) mod n  (Montgomery mod n)
+    u256w km, kinv, rd, t, sm, one;
+    mm_mul<C, 1>(km, k, K.r2_n);
+    mm_inv<C, 1>(kinv, km, K.one_n);  // k^-1 R
+    mm_mul<C, 1>(rd, r, d);           // r d R^-1
+    mm_mul<C, 1>(rd, rd, K.r2_n);     // r d
+    mm_add<C, 1>(t, e, rd);           // e + r d (plain, < n)
+    mm_mul<C, 1>(sm, t, kinv);        // (e + r d) k^-1 (plain)
+    s = sm;
+    (void)one;
+    if (u256_iszero(s)) continue;
+    break;
+  }
+  if (cls == 2) {  // E2 high-S: s' = n - s (still valid)
+    u256w z;
+    u256_zero(z);
+    mm_sub<C, 1>(s, z, s);
+  }
+  uint8_t body[96];
+  int o = 0;
+  u256w rr = r, ss = s;
+  if (cls == 3) u256_zero(rr);  // E3 r = 0
+  o += der_int_enc(body + o, rr, cls == 5);  // E5 non-minimal INTEGER (extra 00)
+  o += der_int_enc(body + o, ss, false);
+  if (cls == 7) {  // E7 three elements: append INTEGER 1
+    body[o++] = 0x02;
+    body[o++] = 0x01;
+    body[o++] = 0x01;
+  }
+  der[0] = 0x30;
+  der[1] = (uint8_t)o;
+  memcpy(der + 2, body, o);
+  int n = 2 + o;
+  if (cls == 6) der[n++] = 0;  // E6 trailing byte
+  return n;
+}
+}  // namespace
+
+extern "C" {
+// curve: 0 = secp256k1 (scheme 2), 1 = secp256r1 (scheme 3). d_out 32 B (LE words), pub_out 64 B X||Y BE.
+void wl_ecdsa_keys(int curve, uint32_t n_keys, uint64_t seed, uint8_t* d_out, uint8_t* pub_out, int nthreads) {
+  init();
+  ec_init();
+  if (nthreads <= 0) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) {
+    th.emplace_back([=]() {
+      for (uint32_t i = (uint32_t)t; i < n_keys; i += (uint32_t)nthreads) {
+        uint64_t s = seed * 0x9e3779b97f4a7c15ULL + i + 1;
+        u256w d, x, y;
+        if (curve == 1) {
+          rand_scalar<CG_CURVE_R1>(d, s);
+          ec_mul_base<CG_CURVE_R1>(x, y, d);
+        } else {
+          rand_scalar<CG_CURVE_K1>(d, s);
+          ec_mul_base<CG_CURVE_K1>(x, y, d);
+        }
+        memcpy(d_out + 32 * (size_t)i, d.w, 32);
+        put_be32(pub_out + 64 * (size_t)i, x);
+        put_be32(pub_out + 64 * (size_t)i + 32, y);
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
+uint64_t wl_ecdsa_arena_bytes(uint64_t n_items, uint32_t n_keys, uint32_t msg_len) {
+  return 64ull * n_keys + ((80 + msg_len + 3) & ~3ull) * n_items + 64;
+}
+
+// labels: 0 valid, 1 E1 msg flip, 2 E2 high-S (valid), 3 E3 r = 0, 5 E5 non-minimal,
+// 6 E6 trailing byte, 7 E7 three elements
+void wl_ecdsa_items(int curve, uint64_t n_items, uint32_t n_keys, const uint8_t* ds, const uint8_t* pubs,
+                    uint32_t msg_len, uint32_t corrupt_permille, uint64_t seed, uint8_t* arena, cg_key* keys_out,
+                    cg_item* items_out, uint8_t* labels_out, int nthreads) {
+  init();
+  ec_init();
+  const uint8_t scheme = curve == 1 ? CG_ECDSA_SECP256R1_SHA256 : CG_ECDSA_SECP256K1_SHA256;
+  for (uint32_t i = 0; i < n_keys; ++i) {
+    memcpy(arena + 64 * (size_t)i, pubs + 64 * (size_t)i, 64);
+    keys_out[i].off = 64ull * i;
+    keys_out[i].len = 64;
+    keys_out[i].scheme = scheme;
+    keys_out[i].fmt = CG_KEY_RAW;
+    keys_out[i].reserved = 0;
+  }
+  const uint64_t base = 64ull * n_keys;
+  const uint64_t stride = (80 + msg_len + 3) & ~3ull;
+  if (nthreads <= 0) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) {
+    th.emplace_back([=]() {
+      for (uint64_t i = (uint64_t)t; i < n_items; i += (uint64_t)nthreads) {
+        uint64_t s = seed ^ (i * 0xd6e8feb86659fd93ULL);
+        const uint32_t k = (uint32_t)(splitmix(s) % n_keys);
+        uint8_t* p = arena + base + stride * i;
+        uint8_t* msg = p + 80;
+        for (uint32_t b = 0; b < msg_len; b += 8) {
+          uint64_t v = splitmix(s);
+          memcpy(msg + b, &v, (msg_len - b) < 8 ? (msg_len - b) : 8);
+        }
+        int cls = 0;
+        if (splitmix(s) % 1000 < corrupt_permille) {
+          const int choices[6] = {1, 2, 3, 5, 6, 7};
+          cls = choices[splitmix(s) % 6];
+        }
+        u256w d, r, sv;
+        memcpy(d.w, ds + 32 * (size_t)k, 32);
+        int n;
+        if (curve == 1) n = ec_sign<CG_CURVE_R1>(p, d, msg, msg_len, s, cls, r, sv);
+        else n = ec_sign<CG_CURVE_K1>(p, d, msg, msg_len, s, cls, r, sv);
+        if (cls == 1) msg[splitmix(s) % msg_len] ^= (uint8_t)(1u << (splitmix(s) & 7));
+        items_out[i].sig_off = base + stride * i;
+        items_out[i].msg_off = base + stride * i + 80;
+        items_out[i].msg_len = msg_len;
+        items_out[i].key_idx = k;
+        items_out[i].sig_len = (uint16_t)n;
+        items_out[i].reserved0 = 0;
+        items_out[i].reserved1 = 0;
+        labels_out[i] = (uint8_t)cls;
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+}
+}

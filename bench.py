@@ -35,6 +35,8 @@ N_FE_ED25519 = 2999
 MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
+# kernel generation whose PMC traffic profile is committed (profiles/r01/pmc_traffic.json)
+KERNEL_VERSION = "ed25519_v1"
 
 
 def parse():
@@ -98,6 +100,7 @@ def main():
     torch.cuda.set_device(dev)
     threads = host_threads(a.threads)
 
+    from corda_amd import shard
     from corda_amd.engine import Engine
     from tools.workload import wl
 
@@ -113,7 +116,7 @@ def main():
     items_d = torch.from_numpy(batch.items.view(np.uint8)).to(dev)
     arena_d = torch.from_numpy(batch.arena).to(dev)
     status_d = torch.full((batch.n,), 255, dtype=torch.uint8, device=dev)
-    gathered = torch.empty((world * batch.n,), dtype=torch.uint8, device=dev) if world > 1 else None
+    gathered_out = []
     n_keys, n_items, arena_len = len(batch.keys), batch.n, int(batch.arena.size)
     # one explicit stream for the engine, the timing events and the RCCL all-gather
     stream = torch.cuda.Stream(device=dev)
@@ -135,7 +138,8 @@ def main():
                 e1.record(stream)
                 ev.append((e0, e1))
             if gather:
-                dist.all_gather_into_tensor(gathered, status_t)
+                # the engine's only collective: RCCL all-gather of the per-GPU verdict bytes
+                gathered_out.append(shard.gather_verdicts(status_t, world * n_items_, world))
 
         for _ in range(warmup):
             step(False)
@@ -195,7 +199,7 @@ def main():
     if os.path.exists(traffic_file):
         with open(traffic_file) as f:
             tr = json.load(f)
-        if tr.get("items") == n_items:
+        if tr.get("items") == n_items and tr.get("kernel_version") == KERNEL_VERSION:
             roof["traffic"] = tr.get("hbm_bytes_per_launch")
 
     cpu = None

@@ -29,9 +29,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "verified sigs/sec (whole node), Ed25519 + ECDSA-P256, at 1/2/4/8 MI355X"
 # Algorithmic work per Ed25519 verify, frozen from the C restatement of i2p 0.2.0
-# (oracle/c/ed25519_i2p.c counters): 1673 field multiplies + 1326 squarings
-# per engineVerify, each priced at 64 MAC32 (a 256x256-bit product in 32-bit words).
-N_FE_ED25519 = 2999
+# (oracle/c/ed25519_i2p.c counters): 1601 field multiplies + 1258
+# squarings per engineVerify (key decode excluded), each priced at 64 MAC32.
+N_FE_ED25519 = 2859
 MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13

@@ -66,7 +66,7 @@ struct cg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  DevBuf keyprep, keys, items, arena, status, aux0, aux1, aux2;
+  DevBuf keyprep, itemws, keys, items, arena, status, aux0, aux1, aux2;
 };
 
 extern "C" {
@@ -120,6 +120,7 @@ void cg_close(cg_ctx* c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   c->keyprep.release();
+  c->itemws.release();
   c->keys.release();
   c->items.release();
   c->arena.release();
@@ -136,7 +137,7 @@ int cg_reserve(cg_ctx* c, uint32_t max_keys, uint64_t max_items) {
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
   HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(max_keys)), "hipMalloc(keyprep)");
-  (void)max_items;
+  HIP_TRY(c->itemws.ensure(cg::item_ws_bytes(max_items)), "hipMalloc(item workspace)");
   return CG_OK;
 }
 
@@ -148,13 +149,15 @@ int cg_verify_batch_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_verify_batch_device: bad mode");
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  if (c->keyprep.cap < cg::keyprep_bytes(n_keys)) {
+  if (c->keyprep.cap < cg::keyprep_bytes(n_keys) || c->itemws.cap < cg::item_ws_bytes(n_items)) {
     // growing the workspace synchronises the device; cg_reserve ahead of time avoids it
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
     HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
+    HIP_TRY(c->itemws.ensure(cg::item_ws_bytes(n_items)), "hipMalloc(item workspace)");
   }
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  HIP_TRY(cg::launch_verify(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p, s),
+  HIP_TRY(cg::launch_verify(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p,
+                            c->itemws.p, s),
           "launch_verify");
   return CG_OK;
 }
@@ -184,8 +187,13 @@ int cg_verify_items_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   if (c->keyprep.cap < cg::keyprep_bytes(n_keys))
     return fail(CG_ERR_ARG, "cg_verify_items_device: keys were not prepared (call cg_prepare_keys_device)");
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  if (c->itemws.cap < cg::item_ws_bytes(n_items)) {
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    HIP_TRY(c->itemws.ensure(cg::item_ws_bytes(n_items)), "hipMalloc(item workspace)");
+  }
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  HIP_TRY(cg::launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p, s),
+  HIP_TRY(cg::launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p,
+                           c->itemws.p, s),
           "launch_items");
   return CG_OK;
 }
@@ -209,6 +217,7 @@ int cg_verify_batch(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_ite
   HIP_TRY(c->arena.ensure(arena_alloc), "hipMalloc(arena)");
   HIP_TRY(c->status.ensure(n_items), "hipMalloc(status)");
   HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
+  HIP_TRY(c->itemws.ensure(cg::item_ws_bytes(n_items)), "hipMalloc(item workspace)");
   hipStream_t s = c->stream;
   hipEvent_t ev[4];
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e), "hipEventCreate");
@@ -218,7 +227,8 @@ int cg_verify_batch(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_ite
   if (arena_len) HIP_TRY(hipMemcpyAsync(c->arena.p, arena, arena_len, hipMemcpyHostToDevice, s), "H2D arena");
   HIP_TRY(hipEventRecord(ev[1], s), "hipEventRecord");
   HIP_TRY(cg::launch_verify((const cg_key*)c->keys.p, n_keys, (const cg_item*)c->items.p, n_items,
-                            (const uint8_t*)c->arena.p, arena_len, mode, (uint8_t*)c->status.p, c->keyprep.p, s),
+                            (const uint8_t*)c->arena.p, arena_len, mode, (uint8_t*)c->status.p, c->keyprep.p,
+                            c->itemws.p, s),
           "launch_verify");
   HIP_TRY(hipEventRecord(ev[2], s), "hipEventRecord");
   HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n_items, hipMemcpyDeviceToHost, s), "D2H status");

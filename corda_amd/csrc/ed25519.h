@@ -250,3 +250,169 @@ CG_HD void ed_consts_init(Ed25519Consts& C) {
     fe_mul(C.Btab[k].xy2d, xy, C.d2);
   }
 }
+
+// ====================================================================== v2: row tables
+// [k]P for a 253-bit k is computed as sum_i 16^i sum_j e_{8j+i} (2^{32j} P) where e are the
+// 64 signed radix-16 digits of k: 8 "rows" P_j = 2^{32j} P, each with the affine multiples
+// 1..8 * P_j. 7 x 4 doublings replace 63 x 4; the same table shape serves -A (per key) and
+// B (constant, staged in LDS).
+struct EdRowTab {
+  ge_niels t[8][8];  // t[j][k-1] = k * 2^{32j} * P, affine niels, tight
+};
+
+struct Ed25519Rows {
+  EdRowTab B;
+};
+
+// Normalise 8 extended points to affine niels with one inversion (Montgomery's trick).
+CG_HD void ed_niels_batch8(ge_niels out[8], const ge_p3 P[8], const fe& d2) {
+  fe acc[8], inv, t;
+  fe_copy(acc[0], P[0].Z);
+  for (int k = 1; k < 8; ++k) fe_mul(acc[k], acc[k - 1], P[k].Z);
+  fe_invert(inv, acc[7]);
+  for (int k = 7; k >= 0; --k) {
+    fe zi;
+    if (k > 0) {
+      fe_mul(zi, inv, acc[k - 1]);
+      fe_mul(t, inv, P[k].Z);
+      fe_copy(inv, t);
+    } else {
+      fe_copy(zi, inv);
+    }
+    fe x, y, xy;
+    fe_mul(x, P[k].X, zi);
+    fe_mul(y, P[k].Y, zi);
+    fe_add(out[k].ypx, y, x);
+    fe_carry(out[k].ypx);
+    fe_sub(out[k].ymx, y, x);
+    fe_carry(out[k].ymx);
+    fe_mul(xy, x, y);
+    fe_mul(out[k].xy2d, xy, d2);
+  }
+}
+
+// 2^32 * P (32 doublings)
+CG_HD void ed_dbl32(ge_p3& R, const ge_p3& P) {
+  ge_p2 q;
+  ge_p1p1 t;
+  ge_p3_to_p2(q, P);
+  for (int i = 0; i < 31; ++i) {
+    ge_p2_dbl(t, q);
+    ge_p1p1_to_p2(q, t);
+  }
+  ge_p2_dbl(t, q);
+  ge_p1p1_to_p3(R, t);
+}
+
+// multiples 1..8 of P -> niels row
+CG_HD void ed_row_from_point(ge_niels row[8], const ge_p3& P, const fe& d2) {
+  ge_p3 M[8];
+  M[0] = P;
+  ge_cached c;
+  ge_p3_to_cached(c, P, d2);
+  ge_p1p1 t;
+  for (int k = 1; k < 8; ++k) {
+    ge_add_cached(t, M[k - 1], c);
+    ge_p1p1_to_p3(M[k], t);
+  }
+  ed_niels_batch8(row, M, d2);
+}
+
+CG_HD void ed_rows_init(EdRowTab& T, const ge_p3& P, const fe& d2) {
+  ge_p3 Pj = P;
+  for (int j = 0; j < 8; ++j) {
+    ed_row_from_point(T.t[j], Pj, d2);
+    if (j < 7) ed_dbl32(Pj, Pj);
+  }
+}
+
+// -A as an extended point from a decoded key prep status (host/tests)
+CG_HD void ed_neg_point(ge_p3& N, const ge_p3& A) {
+  fe_neg(N.X, A.X);
+  fe_carry(N.X);
+  fe_copy(N.Y, A.Y);
+  fe_copy(N.Z, A.Z);
+  fe_neg(N.T, A.T);
+  fe_carry(N.T);
+}
+
+// Select row entry |d| (d in [-8, 8]) with sign; d == 0 gives the identity.
+CG_HD void ed_row_pick(ge_niels& out, const ge_niels* row, int d) {
+  const int a = d < 0 ? -d : d;
+  const ge_niels& src = row[a > 0 ? a - 1 : 0];
+  out = src;
+  if (a == 0) ge_niels_identity(out);
+  ge_niels_cneg(out, d < 0);
+}
+
+// Prologue shared by v2: challenge, S' and digits. Returns false if nothing to compute.
+CG_HD void ed_scalars(uint32_t eh[16], uint32_t es[16], const uint32_t abyte[8], const uint32_t sw[16],
+                      const uint8_t* arena, uint64_t len_rounded, uint64_t msg_off, uint64_t msg_len) {
+  uint32_t pre[16], hw[16], h[8];
+  for (int i = 0; i < 8; ++i) {
+    pre[i] = sw[i];
+    pre[8 + i] = abyte[i];
+  }
+  sha512_prefix64_msg(hw, pre, arena, len_rounded, msg_off, msg_len);
+  sc_reduce512(h, hw);
+  uint32_t s[8], sr[8];
+  for (int i = 0; i < 8; ++i) s[i] = sw[8 + i];
+  sc_reduce256(sr, s);
+  if (s[7] >> 31) {
+    if (sc_slide_escapes(s)) {
+      uint32_t r1[8];
+      for (int i = 0; i < 8; ++i) r1[i] = sc_R1w(i);
+      sc_sub(sr, sr, r1);
+    }
+  }
+  sc_recode16(eh, h);
+  sc_recode16(es, sr);
+}
+
+// R' = h*(-A) + S'*B with row tables; result left projective (X:Y:Z).
+CG_HD void ed_double_scalar_rows(ge_p2& out, const uint32_t eh[16], const uint32_t es[16], const EdRowTab& TA,
+                                 const EdRowTab& TB) {
+  ge_p3 R;
+  ge_p3_0(R);
+  ge_p1p1 t;
+  ge_p2 q;
+  for (int i = 7; i >= 0; --i) {
+    if (i != 7) {
+      ge_p3_to_p2(q, R);
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p2(q, t);
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p2(q, t);
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p2(q, t);
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(R, t);
+    }
+    for (int j = 0; j < 8; ++j) {
+      ge_niels n;
+      ed_row_pick(n, TA.t[j], sc_digit(eh, 8 * j + i));
+      ge_madd(t, R, n);
+      ge_p1p1_to_p3(R, t);
+      ed_row_pick(n, TB.t[j], sc_digit(es, 8 * j + i));
+      ge_madd(t, R, n);
+      if (i == 0 && j == 7) {
+        ge_p1p1_to_p2(out, t);
+        return;
+      }
+      ge_p1p1_to_p3(R, t);
+    }
+  }
+}
+
+// encode (X:Y:Z) given zi = 1/Z, compare with R bytes
+CG_HD int ed_encode_cmp(const ge_p2& P, const fe& zi, const uint32_t rw[8]) {
+  fe x, y;
+  fe_mul(x, P.X, zi);
+  fe_mul(y, P.Y, zi);
+  uint32_t enc[8];
+  fe_tobytes_words(enc, y);
+  enc[7] |= (uint32_t)fe_isnegative(x) << 31;
+  uint32_t diff = 0;
+  for (int i = 0; i < 8; ++i) diff |= enc[i] ^ rw[i];
+  return diff == 0 ? ED_ST_VALID : ED_ST_INVALID;
+}

@@ -1,9 +1,13 @@
 // Batch signature verification kernels for gfx950.
 //
 // Pipeline per batch (all on the caller's stream, no host round trip):
-//   k_ed_keyprep   one lane per distinct key: decode A, canonical Abyte, 8 multiples of -A
-//   k_ed_verify    one lane per Ed25519 item: SHA-512 challenge, scalar prep, 64-window
-//                  double-scalar multiplication, encode + byte compare
+//   k_ed_keyprep_rows  one lane per distinct key: decode A, canonical Abyte, row bases
+//                      2^{32j} (-A), j = 0..7
+//   k_ed_keyprep_tab   one lane per (key, row): affine multiples 1..8 of the row base
+//   k_ed_verify        one lane per Ed25519 item: SHA-512 challenge, scalar prep, 8 windows
+//                      x (8 rows of -A + 8 rows of B) mixed additions, 28 doublings
+//   k_ed_finish        16 items per lane: batch inversion, encode, byte compare
+//   k_ec_keyprep / k_ec_verify  ECDSA secp256r1 / secp256k1
 //   k_misc_status  one lane per item of an unsupported scheme / bad key index
 // Replaces, per item, the JCA call at core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559
 // behind Crypto.doVerify (Crypto.kt:474-484).
@@ -25,14 +29,26 @@ __device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t ar
   return off <= arena_len && len <= arena_len - off;
 }
 
-__global__ void __launch_bounds__(256) k_ed_keyprep(const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                    EdKeyPrep* __restrict__ out) {
+// ------------------------------------------------------------------ Ed25519 (i2p 0.2.0 semantics)
+// Key workspace (per distinct key):
+//   EdKeyHdr  status + canonical Abyte                                   64 B
+//   EdRowTab  t[j][k-1] = k * 2^{32j} * (-A), affine niels                7680 B
+//   row bases 2^{32j} * (-A), j = 0..7 (extended; scratch for the table)  1280 B
+struct EdKeyHdr {
+  uint32_t status;
+  uint32_t abyte[8];
+  uint32_t pad[7];
+};
+
+__constant__ EdRowTab c_ed_rows;  // B rows (constant), staged into LDS by k_ed_verify
+
+__global__ void __launch_bounds__(64) k_ed_keyprep_rows(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                        const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                        EdKeyHdr* __restrict__ hdr, ge_p3* __restrict__ bases) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_keys) return;
   const cg_key k = keys[i];
   if (k.scheme != CG_EDDSA_ED25519_SHA512) return;
-  EdKeyPrep& kp = out[i];
   const uint64_t lr = round4(arena_len);
   uint64_t a_off = k.off;
   bool ok = in_arena(k.off, k.len, arena_len);
@@ -45,33 +61,89 @@ __global__ void __launch_bounds__(256) k_ed_keyprep(const cg_key* __restrict__ k
   } else {
     ok = false;
   }
-  if (!ok) {
-    kp.status = CG_KEY_INVALID;
-    return;
-  }
-  uint32_t aw[8];
+  EdKeyHdr h;
+  for (int w = 0; w < 7; ++w) h.pad[w] = 0;
+  for (int w = 0; w < 8; ++w) h.abyte[w] = 0;
+  h.status = CG_KEY_INVALID;
+  if (ok) {
+    uint32_t aw[8];
 #pragma unroll
-  for (int w = 0; w < 8; ++w) aw[w] = cg_ld_bytes4(arena, lr, a_off + 4 * w);
-  EdKeyPrep local;
-  ed_key_prep(local, aw, c_ed);
-  kp = local;
-  if (local.status != ED_ST_VALID) kp.status = CG_KEY_INVALID;
+    for (int w = 0; w < 8; ++w) aw[w] = cg_ld_bytes4(arena, lr, a_off + 4 * w);
+    ge_p3 A;
+    if (ed_decode_point(A, aw, c_ed) == ED_ST_VALID) {
+      h.status = 0;
+      ed_encode_affine(h.abyte, A.X, A.Y, A.Z);
+      ge_p3 P;
+      ed_neg_point(P, A);
+      for (int j = 0; j < 8; ++j) {
+        bases[(size_t)i * 8 + j] = P;
+        if (j < 7) ed_dbl32(P, P);
+      }
+    }
+  }
+  hdr[i] = h;
+}
+
+__global__ void __launch_bounds__(64) k_ed_keyprep_tab(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                       const EdKeyHdr* __restrict__ hdr,
+                                                       const ge_p3* __restrict__ bases,
+                                                       EdRowTab* __restrict__ tabs) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = g >> 3, j = g & 7;
+  if (i >= n_keys) return;
+  if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || hdr[i].status != 0) return;
+  ge_niels row[8];
+  ed_row_from_point(row, bases[(size_t)i * 8 + j], c_ed.d2);
+  for (int k = 0; k < 8; ++k) tabs[i].t[j][k] = row[k];
+}
+
+#define ED_PENDING 254u
+
+__device__ __forceinline__ void ld_niels(ge_niels& n, const ge_niels* src) {
+  const uint4* p = (const uint4*)src;
+  uint32_t* d = (uint32_t*)&n;
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    const uint4 v = p[q];
+    d[4 * q] = v.x;
+    d[4 * q + 1] = v.y;
+    d[4 * q + 2] = v.z;
+    d[4 * q + 3] = v.w;
+  }
+  const uint2 v = ((const uint2*)src)[14];
+  d[28] = v.x;
+  d[29] = v.y;
+}
+
+__device__ __forceinline__ void pick(ge_niels& out, const ge_niels* row, int d) {
+  const int a = d < 0 ? -d : d;
+  ld_niels(out, row + (a > 0 ? a - 1 : 0));
+  if (a == 0) ge_niels_identity(out);
+  ge_niels_cneg(out, d < 0);
 }
 
 __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ items, uint64_t n_items,
                                                    const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                   const EdKeyPrep* __restrict__ kps,
+                                                   const EdKeyHdr* __restrict__ hdr,
+                                                   const EdRowTab* __restrict__ tabs,
                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                   uint32_t mode, uint8_t* __restrict__ status) {
+                                                   uint32_t mode, uint8_t* __restrict__ status,
+                                                   ge_p2* __restrict__ rout) {
+  __shared__ EdRowTab sB;
+  {
+    const uint32_t* src = (const uint32_t*)&c_ed_rows;
+    uint32_t* dst = (uint32_t*)&sB;
+    for (uint32_t w = threadIdx.x; w < sizeof(EdRowTab) / 4; w += blockDim.x) dst[w] = src[w];
+  }
+  __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_items) return;
   const cg_item it = items[i];
   if (it.key_idx >= n_keys) return;
-  const cg_key k = keys[it.key_idx];
-  if (k.scheme != CG_EDDSA_ED25519_SHA512) return;
-  const EdKeyPrep* kp = kps + it.key_idx;
+  if (keys[it.key_idx].scheme != CG_EDDSA_ED25519_SHA512) return;
+  const EdKeyHdr* kh = hdr + it.key_idx;
   uint8_t st;
-  if (kp->status != 0) {
+  if (kh->status != 0) {
     st = CG_KEY_INVALID;
   } else if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
     st = CG_EMPTY;
@@ -81,12 +153,92 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
     st = CG_SIG_MALFORMED;
   } else {
     const uint64_t lr = round4(arena_len);
-    uint32_t sw[16];
+    uint32_t sw[16], ab[8];
 #pragma unroll
     for (int w = 0; w < 16; ++w) sw[w] = cg_ld_bytes4(arena, lr, it.sig_off + 4 * w);
-    st = (uint8_t)ed_verify_core(*kp, kp->tab, sw, arena, lr, it.msg_off, it.msg_len, c_ed, c_ed.Btab);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) ab[w] = kh->abyte[w];
+    uint32_t eh[16], es[16];
+    ed_scalars(eh, es, ab, sw, arena, lr, it.msg_off, it.msg_len);
+    const EdRowTab* TA = tabs + it.key_idx;
+    ge_p3 R;
+    ge_p3_0(R);
+    ge_p1p1 t;
+    ge_p2 q;
+    for (int w = 7; w >= 0; --w) {
+      if (w != 7) {
+        ge_p3_to_p2(q, R);
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p3(R, t);
+      }
+      for (int j = 0; j < 8; ++j) {
+        ge_niels n;
+        pick(n, TA->t[j], sc_digit(eh, 8 * j + w));
+        ge_madd(t, R, n);
+        ge_p1p1_to_p3(R, t);
+        pick(n, sB.t[j], sc_digit(es, 8 * j + w));
+        ge_madd(t, R, n);
+        if (w == 0 && j == 7) {
+          ge_p1p1_to_p2(q, t);
+        } else {
+          ge_p1p1_to_p3(R, t);
+        }
+      }
+    }
+    rout[i] = q;
+    st = (uint8_t)ED_PENDING;
   }
   status[i] = st;
+}
+
+// Encode + compare for 16 consecutive items per lane: one inversion per lane (Montgomery's
+// trick) instead of one per item.
+#define ED_FINISH_K 16
+__global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ items, uint64_t n_items,
+                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   uint8_t* __restrict__ status, const ge_p2* __restrict__ rin) {
+  const uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * ED_FINISH_K;
+  if (base >= n_items) return;
+  const uint32_t cnt = (uint32_t)((n_items - base) < ED_FINISH_K ? (n_items - base) : ED_FINISH_K);
+  fe acc[ED_FINISH_K];
+  fe run;
+  fe_1(run);
+  uint32_t pend = 0;
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const bool p = status[base + k] == ED_PENDING;
+    pend |= (uint32_t)p << k;
+    if (p) {
+      fe_mul(run, run, rin[base + k].Z);
+    }
+    fe_copy(acc[k], run);
+  }
+  if (!pend) return;
+  fe inv;
+  fe_invert(inv, run);
+  const uint64_t lr = round4(arena_len);
+  for (int k = (int)cnt - 1; k >= 0; --k) {
+    if (!((pend >> k) & 1u)) continue;
+    fe zi, t;
+    // acc[k] = prod of pending Z up to k; inv = 1 / acc[k]
+    int prev = k - 1;
+    while (prev >= 0 && !((pend >> prev) & 1u)) --prev;
+    if (prev >= 0) fe_mul(zi, inv, acc[prev]);
+    else fe_copy(zi, inv);
+    fe_mul(t, inv, rin[base + k].Z);
+    fe_copy(inv, t);
+    const ge_p2 P = rin[base + k];
+    uint32_t rw[8];
+    const uint64_t so = items[base + k].sig_off;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) rw[w] = cg_ld_bytes4(arena, lr, so + 4 * w);
+    status[base + k] = (uint8_t)ed_encode_cmp(P, zi, rw);
+  }
 }
 
 // ------------------------------------------------------------------ ECDSA (BC 1.57 semantics)
@@ -155,53 +307,100 @@ hipError_t upload_constants() {
   ed_consts_init(h);
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_ed), &h, sizeof h, 0, hipMemcpyHostToDevice);
   if (e != hipSuccess) return e;
+  {
+    ge_p3 B;
+    fe x, y, two_inv, t;
+    fe_sub(x, h.Btab[1].ypx, h.Btab[1].ymx);
+    fe_add(y, h.Btab[1].ypx, h.Btab[1].ymx);
+    fe_0(t);
+    t.v[0] = 2;
+    fe_invert(two_inv, t);
+    fe_mul(B.X, x, two_inv);
+    fe_mul(B.Y, y, two_inv);
+    fe_1(B.Z);
+    fe_mul(B.T, B.X, B.Y);
+    static EdRowTab rows;
+    ed_rows_init(rows, B, h.d2);
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_ed_rows), &rows, sizeof rows, 0, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return e;
+  }
   EcConsts k[2];
   ec_consts_init<CG_CURVE_K1>(k[CG_CURVE_K1]);
   ec_consts_init<CG_CURVE_R1>(k[CG_CURVE_R1]);
   return hipMemcpyToSymbol(HIP_SYMBOL(c_ec), k, sizeof k, 0, hipMemcpyHostToDevice);
 }
 
-// workspace: [EdKeyPrep x n_keys][EcKeyPrep x n_keys]
-static size_t ed_region(uint32_t n_keys) { return ((size_t)(n_keys ? n_keys : 1) * sizeof(EdKeyPrep) + 255) & ~(size_t)255; }
-size_t keyprep_bytes(uint32_t n_keys) { return ed_region(n_keys) + (size_t)(n_keys ? n_keys : 1) * sizeof(EcKeyPrep); }
+// key workspace: [EdKeyHdr][EdRowTab][row bases][EcKeyPrep], each region n_keys long
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+struct KeyWs {
+  EdKeyHdr* hdr;
+  EdRowTab* tab;
+  ge_p3* bases;
+  EcKeyPrep* ec;
+};
+static KeyWs key_ws(void* base, uint32_t n_keys) {
+  const size_t n = n_keys ? n_keys : 1;
+  uint8_t* p = (uint8_t*)base;
+  KeyWs w;
+  w.hdr = (EdKeyHdr*)p;
+  p += al256(n * sizeof(EdKeyHdr));
+  w.tab = (EdRowTab*)p;
+  p += al256(n * sizeof(EdRowTab));
+  w.bases = (ge_p3*)p;
+  p += al256(n * 8 * sizeof(ge_p3));
+  w.ec = (EcKeyPrep*)p;
+  return w;
+}
+size_t keyprep_bytes(uint32_t n_keys) {
+  const size_t n = n_keys ? n_keys : 1;
+  return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(EdRowTab)) + al256(n * 8 * sizeof(ge_p3)) +
+         n * sizeof(EcKeyPrep);
+}
+size_t item_ws_bytes(uint64_t n_items) { return (size_t)(n_items ? n_items : 1) * sizeof(ge_p2); }
 
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream) {
   if (n_keys == 0) return hipSuccess;
   const uint32_t B = 64;  // one wave per block: keys are few, spread them over CUs
   const dim3 g((n_keys + B - 1) / B);
-  EcKeyPrep* ec = (EcKeyPrep*)((uint8_t*)d_keyprep + ed_region(n_keys));
-  hipLaunchKernelGGL(k_ed_keyprep, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, (EdKeyPrep*)d_keyprep);
-  hipLaunchKernelGGL(k_ec_keyprep<CG_CURVE_R1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, ec);
-  hipLaunchKernelGGL(k_ec_keyprep<CG_CURVE_K1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, ec);
+  KeyWs w = key_ws(d_keyprep, n_keys);
+  hipLaunchKernelGGL(k_ed_keyprep_rows, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.hdr, w.bases);
+  hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((8 * n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
+                     w.bases, w.tab);
+  hipLaunchKernelGGL(k_ec_keyprep<CG_CURVE_R1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.ec);
+  hipLaunchKernelGGL(k_ec_keyprep<CG_CURVE_K1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.ec);
   return hipGetLastError();
 }
 
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                        const void* d_keyprep, hipStream_t stream) {
+                        const void* d_keyprep, void* d_item_ws, hipStream_t stream) {
   if (n_items == 0) return hipSuccess;
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
+  KeyWs w = key_ws((void*)d_keyprep, n_keys);
   hipLaunchKernelGGL(k_misc_status, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
                      d_status);
-  hipLaunchKernelGGL(k_ed_verify, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
-                     (const EdKeyPrep*)d_keyprep, d_arena, arena_len, mode, d_status);
-  const EcKeyPrep* ec = (const EcKeyPrep*)((const uint8_t*)d_keyprep + ed_region(n_keys));
+  hipLaunchKernelGGL(k_ed_verify, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys, w.hdr,
+                     w.tab, d_arena, arena_len, mode, d_status, (ge_p2*)d_item_ws);
+  const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
+  hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, n_items, d_arena, arena_len,
+                     d_status, (const ge_p2*)d_item_ws);
   hipLaunchKernelGGL(k_ec_verify<CG_CURVE_R1>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys,
-                     n_keys, ec, d_arena, arena_len, mode, d_status);
+                     n_keys, w.ec, d_arena, arena_len, mode, d_status);
   hipLaunchKernelGGL(k_ec_verify<CG_CURVE_K1>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys,
-                     n_keys, ec, d_arena, arena_len, mode, d_status);
+                     n_keys, w.ec, d_arena, arena_len, mode, d_status);
   return hipGetLastError();
 }
 
 hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                          const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                         void* d_keyprep, hipStream_t stream) {
+                         void* d_keyprep, void* d_item_ws, hipStream_t stream) {
   if (n_items == 0) return hipSuccess;
   hipError_t e = launch_keyprep(d_keys, n_keys, d_arena, arena_len, d_keyprep, stream);
   if (e != hipSuccess) return e;
-  return launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, d_keyprep, stream);
+  return launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, d_keyprep, d_item_ws,
+                      stream);
 }
 
 }  // namespace cg

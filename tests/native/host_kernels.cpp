@@ -116,3 +116,42 @@ void t_mm_mul(int curve, int n, const uint32_t* a, const uint32_t* b, uint32_t* 
   memcpy(out, r.w, 32);
 }
 }
+
+// ---------------------------------------------------------------- Ed25519 v2 (row tables)
+static EdRowTab g_TB;
+static int g_rinit = 0;
+extern "C" int t_ed_verify_v2(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len) {
+  init();
+  if (!g_rinit) {
+    ge_p3 B;
+    fe x, y, two_inv, t;
+    fe_sub(x, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+    fe_add(y, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+    fe_0(t);
+    t.v[0] = 2;
+    fe_invert(two_inv, t);
+    fe_mul(B.X, x, two_inv);
+    fe_mul(B.Y, y, two_inv);
+    fe_1(B.Z);
+    fe_mul(B.T, B.X, B.Y);
+    ed_rows_init(g_TB, B, g_C.d2);
+    g_rinit = 1;
+  }
+  static EdKeyPrep kp;
+  ed_key_prep(kp, aw, g_C);
+  if (kp.status) return (int)kp.status;
+  ge_p3 A, N;
+  ed_decode_point(A, aw, g_C);
+  ed_neg_point(N, A);
+  static EdRowTab TA;
+  ed_rows_init(TA, N, g_C.d2);
+  static uint8_t buf[1 << 20];
+  memcpy(buf, msg, msg_len);
+  uint32_t eh[16], es[16];
+  ed_scalars(eh, es, kp.abyte, sw, buf, (msg_len + 3) & ~3ull, 0, msg_len);
+  ge_p2 R;
+  ed_double_scalar_rows(R, eh, es, TA, g_TB);
+  fe zi;
+  fe_invert(zi, R.Z);
+  return ed_encode_cmp(R, zi, sw);
+}

@@ -66,7 +66,7 @@ struct cg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  DevBuf keyprep, itemws, keys, items, arena, status, aux0, aux1, aux2;
+  DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
 };
 
 extern "C" {
@@ -106,10 +106,14 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     return hip_fail(e, "hipStreamCreate");
   }
   e = cg::upload_constants();
+  if (e == hipSuccess) e = c->btab.ensure(cg::btab_bytes());
+  if (e == hipSuccess) e = cg::init_btab(c->btab.p, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
+    c->btab.release();
     hipStreamDestroy(c->stream);
     delete c;
-    return hip_fail(e, "upload_constants");
+    return hip_fail(e, "upload_constants / base-point table");
   }
   *out = c;
   return CG_OK;
@@ -121,6 +125,7 @@ void cg_close(cg_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   c->keyprep.release();
   c->itemws.release();
+  c->btab.release();
   c->keys.release();
   c->items.release();
   c->arena.release();
@@ -157,7 +162,7 @@ int cg_verify_batch_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   }
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIP_TRY(cg::launch_verify(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p,
-                            c->itemws.p, s),
+                            c->itemws.p, c->btab.p, s),
           "launch_verify");
   return CG_OK;
 }
@@ -193,7 +198,7 @@ int cg_verify_items_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   }
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIP_TRY(cg::launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p,
-                           c->itemws.p, s),
+                           c->itemws.p, c->btab.p, s),
           "launch_items");
   return CG_OK;
 }
@@ -228,7 +233,7 @@ int cg_verify_batch(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_ite
   HIP_TRY(hipEventRecord(ev[1], s), "hipEventRecord");
   HIP_TRY(cg::launch_verify((const cg_key*)c->keys.p, n_keys, (const cg_item*)c->items.p, n_items,
                             (const uint8_t*)c->arena.p, arena_len, mode, (uint8_t*)c->status.p, c->keyprep.p,
-                            c->itemws.p, s),
+                            c->itemws.p, c->btab.p, s),
           "launch_verify");
   HIP_TRY(hipEventRecord(ev[2], s), "hipEventRecord");
   HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n_items, hipMemcpyDeviceToHost, s), "D2H status");

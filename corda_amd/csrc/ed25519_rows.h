@@ -1,0 +1,148 @@
+// Ed25519 double-scalar multiplication over per-key "row" tables, generic in the signed
+// window width W and the number of windows K per row.
+//
+// A 253-bit scalar k is recoded into D = ceil(253 / W) + 1 signed radix-2^W digits
+// e_t in [-2^(W-1), 2^(W-1)]. Digit t = K j + i belongs to row j and window i, so
+//     [k] P = sum_{i<K} 2^{W i} sum_{j<R} e_{K j + i} P_j,   P_j = 2^{W K j} P.
+// Each row stores the affine multiples 1..2^(W-1) of P_j (niels form, 120 B each). The loop
+// runs K windows, (K-1) W doublings in total, and one mixed addition per digit. With W = 6,
+// K = 4: 43 digits in 11 rows, 18 doublings, 86 mixed additions for h(-A) + S'B (the 4-bit
+// 8-row layout needed 28 doublings and 128 additions). Every lane runs the same sequence:
+// no data-dependent control flow, so the 64 lanes of a wave never diverge.
+#pragma once
+#include "ed25519.h"
+
+template <int W, int K>
+struct EdRowsCfg {
+  // the top digit keeps >= 1 bit of headroom for the recoding carry unless W divides 253
+  static constexpr int kDigits = (253 + W - 1) / W + (253 % W == 0 ? 1 : 0);
+  static constexpr int kRows = (kDigits + K - 1) / K;
+  static constexpr int kMult = 1 << (W - 1);  // entries per row: 1 .. 2^(W-1)
+  static constexpr int kPackedWords = (kDigits + 3) / 4;
+};
+
+template <int W, int K>
+struct EdRowTabW {
+  ge_niels t[EdRowsCfg<W, K>::kRows][EdRowsCfg<W, K>::kMult];
+};
+
+// signed radix-2^W digits of a < 2^253, packed 4 per word as signed bytes
+template <int W>
+CG_HD void sc_recode_w(uint32_t* packed, int nwords, const uint32_t a[8]) {
+  constexpr int D = (253 + W - 1) / W + (253 % W == 0 ? 1 : 0);
+  for (int w = 0; w < nwords; ++w) packed[w] = 0;
+  int carry = 0;
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+    const int bit = t * W;
+    uint32_t v = 0;
+    if (bit < 256) {
+      const int wi = bit >> 5, sh = bit & 31;
+      uint64_t x = (uint64_t)a[wi] >> sh;
+      if (sh + W > 32 && wi + 1 < 8) x |= (uint64_t)a[wi + 1] << (32 - sh);
+      v = (uint32_t)x & ((1u << W) - 1);
+    }
+    int e = (int)v + carry;
+    carry = (e + (1 << (W - 1))) >> W;
+    e -= carry << W;
+    packed[t >> 2] |= ((uint32_t)(e & 0xff)) << ((t & 3) * 8);
+  }
+}
+
+CG_HD int sc_digit_b(const uint32_t* packed, int t) {
+  return (int)(int8_t)(uint8_t)(packed[t >> 2] >> ((t & 3) * 8));
+}
+
+// 2^n * P
+CG_HD void ed_dbl_n(ge_p3& R, const ge_p3& P, int n) {
+  ge_p2 q;
+  ge_p1p1 t;
+  ge_p3_to_p2(q, P);
+  for (int i = 0; i < n - 1; ++i) {
+    ge_p2_dbl(t, q);
+    ge_p1p1_to_p2(q, t);
+  }
+  ge_p2_dbl(t, q);
+  ge_p1p1_to_p3(R, t);
+}
+
+// Affine niels multiples 1..M of P (M a multiple of 8), normalised in groups of 8.
+template <int M>
+CG_HD void ed_row_multiples(ge_niels* row, const ge_p3& P, const fe& d2) {
+  ge_cached c;
+  ge_p3_to_cached(c, P, d2);
+  ge_p3 cur = P;
+  ge_p1p1 t;
+  for (int g = 0; g < M / 8; ++g) {
+    ge_p3 pts[8];
+    for (int k = 0; k < 8; ++k) {
+      if (g == 0 && k == 0) {
+        pts[0] = P;
+      } else {
+        ge_add_cached(t, cur, c);
+        ge_p1p1_to_p3(pts[k], t);
+      }
+      cur = pts[k];
+    }
+    ed_niels_batch8(row + 8 * g, pts, d2);
+  }
+}
+
+template <int W, int K>
+CG_HD void ed_rows_w_init(EdRowTabW<W, K>& T, const ge_p3& P, const fe& d2) {
+  typedef EdRowsCfg<W, K> C;
+  ge_p3 Pj = P;
+  for (int j = 0; j < C::kRows; ++j) {
+    ed_row_multiples<C::kMult>(T.t[j], Pj, d2);
+    if (j + 1 < C::kRows) ed_dbl_n(Pj, Pj, W * K);
+  }
+}
+
+// entry |d| of a row (d in [-M, M]) with sign; 0 gives the identity
+CG_HD void ed_pick_w(ge_niels& out, const ge_niels* row, int d) {
+  const int a = d < 0 ? -d : d;
+  out = row[a > 0 ? a - 1 : 0];
+  if (a == 0) ge_niels_identity(out);
+  ge_niels_cneg(out, d < 0);
+}
+
+// R' = h*(-A) + S'*B (digits already recoded), left projective.
+template <int W, int K, class RowA, class RowB>
+CG_HD void ed_double_scalar_w(ge_p2& out, const uint32_t* eh, const uint32_t* es, const RowA& TA, const RowB& TB) {
+  typedef EdRowsCfg<W, K> C;
+  ge_p3 R;
+  ge_p3_0(R);
+  ge_p1p1 t;
+  ge_p2 q;
+  bool have_q = false;
+  for (int i = K - 1; i >= 0; --i) {
+    if (i != K - 1) {
+      ge_p3_to_p2(q, R);
+      for (int d = 0; d < W - 1; ++d) {
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+      }
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(R, t);
+    }
+    for (int j = 0; j < C::kRows; ++j) {
+      const int tdig = K * j + i;
+      if (tdig >= C::kDigits) continue;
+      ge_niels n;
+      ed_pick_w(n, TA.t[j], sc_digit_b(eh, tdig));
+      ge_madd(t, R, n);
+      ge_p1p1_to_p3(R, t);
+      ed_pick_w(n, TB.t[j], sc_digit_b(es, tdig));
+      ge_madd(t, R, n);
+      const bool last = (i == 0) && (j + 1 == C::kRows);
+      if (last) {
+        ge_p1p1_to_p2(q, t);
+        have_q = true;
+      } else {
+        ge_p1p1_to_p3(R, t);
+      }
+    }
+  }
+  if (!have_q) ge_p3_to_p2(q, R);
+  out = q;
+}

@@ -19,14 +19,17 @@ size_t keyprep_bytes(uint32_t n_keys);
 //   key prep (one lane per key) -> per-scheme verify (one lane per item) -> status bytes.
 hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                          const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                         void* d_keyprep, void* d_item_ws, hipStream_t stream);
+                         void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream);
+// Constant base-point row table: size and one-time initialisation (per context).
+size_t btab_bytes();
+hipError_t init_btab(void* d_btab, hipStream_t stream);
 // Bytes of per-item workspace (projective Ed25519 results awaiting the batched inversion).
 size_t item_ws_bytes(uint64_t n_items);
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream);
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                        const void* d_keyprep, void* d_item_ws, hipStream_t stream);
+                        const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream);
 
 // Hashing kernels
 hipError_t launch_sha256(const cg_span* d_spans, uint64_t n, const uint8_t* d_arena, uint64_t arena_len,

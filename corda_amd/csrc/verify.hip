@@ -2,10 +2,10 @@
 //
 // Pipeline per batch (all on the caller's stream, no host round trip):
 //   k_ed_keyprep_rows  one lane per distinct key: decode A, canonical Abyte, row bases
-//                      2^{32j} (-A), j = 0..7
-//   k_ed_keyprep_tab   one lane per (key, row): affine multiples 1..8 of the row base
-//   k_ed_verify        one lane per Ed25519 item: SHA-512 challenge, scalar prep, 8 windows
-//                      x (8 rows of -A + 8 rows of B) mixed additions, 28 doublings
+//                      2^{24j} (-A), j = 0..10
+//   k_ed_keyprep_tab   one lane per (key, row, 8 multiples): affine multiples of the row base
+//   k_ed_verify        one lane per Ed25519 item: SHA-512 challenge, scalar prep, 4 windows
+//                      x (11 rows of -A + 11 rows of B) mixed additions, 18 doublings
 //   k_ed_finish        16 items per lane: batch inversion, encode, byte compare
 //   k_ec_keyprep / k_ec_verify  ECDSA secp256r1 / secp256k1
 //   k_misc_status  one lane per item of an unsupported scheme / bad key index
@@ -15,6 +15,7 @@
 
 #include "ecdsa.h"
 #include "ed25519.h"
+#include "ed25519_rows.h"
 #include "engine.h"
 
 namespace cg {
@@ -30,17 +31,21 @@ __device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t ar
 }
 
 // ------------------------------------------------------------------ Ed25519 (i2p 0.2.0 semantics)
+// Row tables (ed25519_rows.h) with signed radix-64 digits: 43 digits in 11 rows of 4 windows.
+#define ED_W 6
+#define ED_K 4
+typedef EdRowsCfg<ED_W, ED_K> EdCfg;
+typedef EdRowTabW<ED_W, ED_K> EdTab;  // 11 x 32 affine niels = 42240 B
+
 // Key workspace (per distinct key):
-//   EdKeyHdr  status + canonical Abyte                                   64 B
-//   EdRowTab  t[j][k-1] = k * 2^{32j} * (-A), affine niels                7680 B
-//   row bases 2^{32j} * (-A), j = 0..7 (extended; scratch for the table)  1280 B
+//   EdKeyHdr  status + canonical Abyte                               64 B
+//   EdTab     t[j][k-1] = k * 2^{24j} * (-A), affine niels           42240 B
+//   bases     2^{24j} * (-A), j = 0..10 (extended; table scratch)    1760 B
 struct EdKeyHdr {
   uint32_t status;
   uint32_t abyte[8];
   uint32_t pad[7];
 };
-
-__constant__ EdRowTab c_ed_rows;  // B rows (constant), staged into LDS by k_ed_verify
 
 __global__ void __launch_bounds__(64) k_ed_keyprep_rows(const cg_key* __restrict__ keys, uint32_t n_keys,
                                                         const uint8_t* __restrict__ arena, uint64_t arena_len,
@@ -75,26 +80,73 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_rows(const cg_key* __restrict
       ed_encode_affine(h.abyte, A.X, A.Y, A.Z);
       ge_p3 P;
       ed_neg_point(P, A);
-      for (int j = 0; j < 8; ++j) {
-        bases[(size_t)i * 8 + j] = P;
-        if (j < 7) ed_dbl32(P, P);
+      for (int j = 0; j < EdCfg::kRows; ++j) {
+        bases[(size_t)i * EdCfg::kRows + j] = P;
+        if (j + 1 < EdCfg::kRows) ed_dbl_n(P, P, ED_W * ED_K);
       }
     }
   }
   hdr[i] = h;
 }
 
+// m * P for a small m >= 1 (double-and-add, MSB first)
+__device__ void ed_small_mul(ge_p3& R, const ge_p3& P, uint32_t m) {
+  ge_cached c;
+  ge_p3_to_cached(c, P, c_ed.d2);
+  R = P;
+  ge_p1p1 t;
+  int top = 31 - __builtin_clz(m);
+  for (int b = top - 1; b >= 0; --b) {
+    ge_p3_dbl(t, R);
+    ge_p1p1_to_p3(R, t);
+    if ((m >> b) & 1u) {
+      ge_add_cached(t, R, c);
+      ge_p1p1_to_p3(R, t);
+    }
+  }
+}
+
+// one lane per (key, row, group of 8 multiples)
 __global__ void __launch_bounds__(64) k_ed_keyprep_tab(const cg_key* __restrict__ keys, uint32_t n_keys,
                                                        const EdKeyHdr* __restrict__ hdr,
-                                                       const ge_p3* __restrict__ bases,
-                                                       EdRowTab* __restrict__ tabs) {
+                                                       const ge_p3* __restrict__ bases, EdTab* __restrict__ tabs) {
+  constexpr uint32_t G = EdCfg::kMult / 8;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = g >> 3, j = g & 7;
+  const uint32_t i = g / (EdCfg::kRows * G);
+  const uint32_t rem = g % (EdCfg::kRows * G);
+  const uint32_t j = rem / G, grp = rem % G;
   if (i >= n_keys) return;
   if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || hdr[i].status != 0) return;
+  const ge_p3 P = bases[(size_t)i * EdCfg::kRows + j];
+  ge_p3 pts[8];
+  ed_small_mul(pts[0], P, 8 * grp + 1);
+  ge_cached c;
+  ge_p3_to_cached(c, P, c_ed.d2);
+  ge_p1p1 t;
+  for (int k = 1; k < 8; ++k) {
+    ge_add_cached(t, pts[k - 1], c);
+    ge_p1p1_to_p3(pts[k], t);
+  }
   ge_niels row[8];
-  ed_row_from_point(row, bases[(size_t)i * 8 + j], c_ed.d2);
-  for (int k = 0; k < 8; ++k) tabs[i].t[j][k] = row[k];
+  ed_niels_batch8(row, pts, c_ed.d2);
+  for (int k = 0; k < 8; ++k) tabs[i].t[j][8 * grp + k] = row[k];
+}
+
+// B rows, built once per context by the same code
+__global__ void k_ed_btab_init(EdTab* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  ge_p3 B;
+  fe x, y, two_inv, t;
+  fe_sub(x, c_ed.Btab[1].ypx, c_ed.Btab[1].ymx);
+  fe_add(y, c_ed.Btab[1].ypx, c_ed.Btab[1].ymx);
+  fe_0(t);
+  t.v[0] = 2;
+  fe_invert(two_inv, t);
+  fe_mul(B.X, x, two_inv);
+  fe_mul(B.Y, y, two_inv);
+  fe_1(B.Z);
+  fe_mul(B.T, B.X, B.Y);
+  ed_rows_w_init<ED_W, ED_K>(*out, B, c_ed.d2);
 }
 
 #define ED_PENDING 254u
@@ -124,16 +176,16 @@ __device__ __forceinline__ void pick(ge_niels& out, const ge_niels* row, int d) 
 
 __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ items, uint64_t n_items,
                                                    const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                   const EdKeyHdr* __restrict__ hdr,
-                                                   const EdRowTab* __restrict__ tabs,
+                                                   const EdKeyHdr* __restrict__ hdr, const EdTab* __restrict__ tabs,
+                                                   const EdTab* __restrict__ btab,
                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                    uint32_t mode, uint8_t* __restrict__ status,
                                                    ge_p2* __restrict__ rout) {
-  __shared__ EdRowTab sB;
+  __shared__ EdTab sB;
   {
-    const uint32_t* src = (const uint32_t*)&c_ed_rows;
-    uint32_t* dst = (uint32_t*)&sB;
-    for (uint32_t w = threadIdx.x; w < sizeof(EdRowTab) / 4; w += blockDim.x) dst[w] = src[w];
+    const uint4* src = (const uint4*)btab;
+    uint4* dst = (uint4*)&sB;
+    for (uint32_t w = threadIdx.x; w < sizeof(EdTab) / 16; w += blockDim.x) dst[w] = src[w];
   }
   __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -158,39 +210,32 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
     for (int w = 0; w < 16; ++w) sw[w] = cg_ld_bytes4(arena, lr, it.sig_off + 4 * w);
 #pragma unroll
     for (int w = 0; w < 8; ++w) ab[w] = kh->abyte[w];
-    uint32_t eh[16], es[16];
-    ed_scalars(eh, es, ab, sw, arena, lr, it.msg_off, it.msg_len);
-    const EdRowTab* TA = tabs + it.key_idx;
-    ge_p3 R;
-    ge_p3_0(R);
-    ge_p1p1 t;
-    ge_p2 q;
-    for (int w = 7; w >= 0; --w) {
-      if (w != 7) {
-        ge_p3_to_p2(q, R);
-        ge_p2_dbl(t, q);
-        ge_p1p1_to_p2(q, t);
-        ge_p2_dbl(t, q);
-        ge_p1p1_to_p2(q, t);
-        ge_p2_dbl(t, q);
-        ge_p1p1_to_p2(q, t);
-        ge_p2_dbl(t, q);
-        ge_p1p1_to_p3(R, t);
-      }
-      for (int j = 0; j < 8; ++j) {
-        ge_niels n;
-        pick(n, TA->t[j], sc_digit(eh, 8 * j + w));
-        ge_madd(t, R, n);
-        ge_p1p1_to_p3(R, t);
-        pick(n, sB.t[j], sc_digit(es, 8 * j + w));
-        ge_madd(t, R, n);
-        if (w == 0 && j == 7) {
-          ge_p1p1_to_p2(q, t);
-        } else {
-          ge_p1p1_to_p3(R, t);
-        }
+    // h = SHA-512(R || Abyte || M) mod L ; S' = slide value of S mod L
+    uint32_t pre[16], hw[16], h[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      pre[w] = sw[w];
+      pre[8 + w] = ab[w];
+    }
+    sha512_prefix64_msg(hw, pre, arena, lr, it.msg_off, it.msg_len);
+    sc_reduce512(h, hw);
+    uint32_t s[8], sr[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) s[w] = sw[8 + w];
+    sc_reduce256(sr, s);
+    if (s[7] >> 31) {
+      if (sc_slide_escapes(s)) {
+        uint32_t r1[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) r1[w] = sc_R1w(w);
+        sc_sub(sr, sr, r1);
       }
     }
+    uint32_t eh[EdCfg::kPackedWords], es[EdCfg::kPackedWords];
+    sc_recode_w<ED_W>(eh, EdCfg::kPackedWords, h);
+    sc_recode_w<ED_W>(es, EdCfg::kPackedWords, sr);
+    ge_p2 q;
+    ed_double_scalar_w<ED_W, ED_K>(q, eh, es, tabs[it.key_idx], sB);
     rout[i] = q;
     st = (uint8_t)ED_PENDING;
   }
@@ -307,23 +352,7 @@ hipError_t upload_constants() {
   ed_consts_init(h);
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_ed), &h, sizeof h, 0, hipMemcpyHostToDevice);
   if (e != hipSuccess) return e;
-  {
-    ge_p3 B;
-    fe x, y, two_inv, t;
-    fe_sub(x, h.Btab[1].ypx, h.Btab[1].ymx);
-    fe_add(y, h.Btab[1].ypx, h.Btab[1].ymx);
-    fe_0(t);
-    t.v[0] = 2;
-    fe_invert(two_inv, t);
-    fe_mul(B.X, x, two_inv);
-    fe_mul(B.Y, y, two_inv);
-    fe_1(B.Z);
-    fe_mul(B.T, B.X, B.Y);
-    static EdRowTab rows;
-    ed_rows_init(rows, B, h.d2);
-    e = hipMemcpyToSymbol(HIP_SYMBOL(c_ed_rows), &rows, sizeof rows, 0, hipMemcpyHostToDevice);
-    if (e != hipSuccess) return e;
-  }
+
   EcConsts k[2];
   ec_consts_init<CG_CURVE_K1>(k[CG_CURVE_K1]);
   ec_consts_init<CG_CURVE_R1>(k[CG_CURVE_R1]);
@@ -334,7 +363,7 @@ hipError_t upload_constants() {
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct KeyWs {
   EdKeyHdr* hdr;
-  EdRowTab* tab;
+  EdTab* tab;
   ge_p3* bases;
   EcKeyPrep* ec;
 };
@@ -344,16 +373,16 @@ static KeyWs key_ws(void* base, uint32_t n_keys) {
   KeyWs w;
   w.hdr = (EdKeyHdr*)p;
   p += al256(n * sizeof(EdKeyHdr));
-  w.tab = (EdRowTab*)p;
-  p += al256(n * sizeof(EdRowTab));
+  w.tab = (EdTab*)p;
+  p += al256(n * sizeof(EdTab));
   w.bases = (ge_p3*)p;
-  p += al256(n * 8 * sizeof(ge_p3));
+  p += al256(n * EdCfg::kRows * sizeof(ge_p3));
   w.ec = (EcKeyPrep*)p;
   return w;
 }
 size_t keyprep_bytes(uint32_t n_keys) {
   const size_t n = n_keys ? n_keys : 1;
-  return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(EdRowTab)) + al256(n * 8 * sizeof(ge_p3)) +
+  return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(EdTab)) + al256(n * EdCfg::kRows * sizeof(ge_p3)) +
          n * sizeof(EcKeyPrep);
 }
 size_t item_ws_bytes(uint64_t n_items) { return (size_t)(n_items ? n_items : 1) * sizeof(ge_p2); }
@@ -365,16 +394,23 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   const dim3 g((n_keys + B - 1) / B);
   KeyWs w = key_ws(d_keyprep, n_keys);
   hipLaunchKernelGGL(k_ed_keyprep_rows, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.hdr, w.bases);
-  hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((8 * n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
+  const uint32_t lanes = n_keys * EdCfg::kRows * (EdCfg::kMult / 8);
+  hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((lanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
                      w.bases, w.tab);
   hipLaunchKernelGGL(k_ec_keyprep<CG_CURVE_R1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.ec);
   hipLaunchKernelGGL(k_ec_keyprep<CG_CURVE_K1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.ec);
   return hipGetLastError();
 }
 
+size_t btab_bytes() { return sizeof(EdTab); }
+hipError_t init_btab(void* d_btab, hipStream_t stream) {
+  hipLaunchKernelGGL(k_ed_btab_init, dim3(1), dim3(64), 0, stream, (EdTab*)d_btab);
+  return hipGetLastError();
+}
+
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                        const void* d_keyprep, void* d_item_ws, hipStream_t stream) {
+                        const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream) {
   if (n_items == 0) return hipSuccess;
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
@@ -382,7 +418,7 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
   hipLaunchKernelGGL(k_misc_status, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
                      d_status);
   hipLaunchKernelGGL(k_ed_verify, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys, w.hdr,
-                     w.tab, d_arena, arena_len, mode, d_status, (ge_p2*)d_item_ws);
+                     w.tab, (const EdTab*)d_btab, d_arena, arena_len, mode, d_status, (ge_p2*)d_item_ws);
   const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
   hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, n_items, d_arena, arena_len,
                      d_status, (const ge_p2*)d_item_ws);
@@ -395,12 +431,12 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
 
 hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                          const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                         void* d_keyprep, void* d_item_ws, hipStream_t stream) {
+                         void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream) {
   if (n_items == 0) return hipSuccess;
   hipError_t e = launch_keyprep(d_keys, n_keys, d_arena, arena_len, d_keyprep, stream);
   if (e != hipSuccess) return e;
   return launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, d_keyprep, d_item_ws,
-                      stream);
+                      d_btab, stream);
 }
 
 }  // namespace cg

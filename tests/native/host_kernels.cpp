@@ -155,3 +155,68 @@ extern "C" int t_ed_verify_v2(const uint32_t* aw, const uint32_t* sw, const uint
   fe_invert(zi, R.Z);
   return ed_encode_cmp(R, zi, sw);
 }
+
+// ---------------------------------------------------------------- Ed25519 rows, generic W/K
+#include "../../corda_amd/csrc/ed25519_rows.h"
+template <int W, int K>
+static int verify_w(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len) {
+  init();
+  typedef EdRowTabW<W, K> Tab;
+  static Tab* TB = nullptr;
+  static Tab* TA = nullptr;
+  if (!TB) {
+    TB = new Tab;
+    TA = new Tab;
+    ge_p3 B;
+    fe x, y, two_inv, t;
+    fe_sub(x, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+    fe_add(y, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+    fe_0(t);
+    t.v[0] = 2;
+    fe_invert(two_inv, t);
+    fe_mul(B.X, x, two_inv);
+    fe_mul(B.Y, y, two_inv);
+    fe_1(B.Z);
+    fe_mul(B.T, B.X, B.Y);
+    ed_rows_w_init<W, K>(*TB, B, g_C.d2);
+  }
+  static EdKeyPrep kp;
+  ed_key_prep(kp, aw, g_C);
+  if (kp.status) return (int)kp.status;
+  ge_p3 A, N;
+  ed_decode_point(A, aw, g_C);
+  ed_neg_point(N, A);
+  ed_rows_w_init<W, K>(*TA, N, g_C.d2);
+  static uint8_t buf[1 << 20];
+  memcpy(buf, msg, msg_len);
+  // scalars
+  uint32_t pre[16], hw[16], h[8];
+  for (int i = 0; i < 8; ++i) {
+    pre[i] = sw[i];
+    pre[8 + i] = kp.abyte[i];
+  }
+  sha512_prefix64_msg(hw, pre, buf, (msg_len + 3) & ~3ull, 0, msg_len);
+  sc_reduce512(h, hw);
+  uint32_t s[8], sr[8];
+  for (int i = 0; i < 8; ++i) s[i] = sw[8 + i];
+  sc_reduce256(sr, s);
+  if ((s[7] >> 31) && sc_slide_escapes(s)) {
+    uint32_t r1[8];
+    for (int i = 0; i < 8; ++i) r1[i] = sc_R1w(i);
+    sc_sub(sr, sr, r1);
+  }
+  const int NW = EdRowsCfg<W, K>::kPackedWords;
+  uint32_t eh[NW], es[NW];
+  sc_recode_w<W>(eh, NW, h);
+  sc_recode_w<W>(es, NW, sr);
+  ge_p2 R;
+  ed_double_scalar_w<W, K>(R, eh, es, *TA, *TB);
+  fe zi;
+  fe_invert(zi, R.Z);
+  return ed_encode_cmp(R, zi, sw);
+}
+extern "C" int t_ed_verify_w(int w, const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len) {
+  if (w == 4) return verify_w<4, 8>(aw, sw, msg, msg_len);
+  if (w == 5) return verify_w<5, 4>(aw, sw, msg, msg_len);
+  return verify_w<6, 4>(aw, sw, msg, msg_len);
+}

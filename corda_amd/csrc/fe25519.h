@@ -42,6 +42,15 @@ struct fe {
   uint32_t v[10];
 };
 
+// Host-build op counters (tests/native/host_kernels.cpp): define the executed-work figure
+// bench.py prices the kernels with. Compiled out of the device build.
+#ifdef FE_OP_COUNT
+extern uint64_t g_fe_nmul, g_fe_nsq;
+#define FE_COUNT(c) (++(c))
+#else
+#define FE_COUNT(c) ((void)0)
+#endif
+
 #define FE_M26 0x3ffffffu
 #define FE_M25 0x1ffffffu
 
@@ -142,6 +151,7 @@ CG_HD void fe_reduce_cols(fe& out, fe_acc_t* h) {
 
 // h = f * g
 CG_HD void fe_mul(fe& out, const fe& f, const fe& g) {
+  FE_COUNT(g_fe_nmul);
   uint32_t g19[10], f2[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
@@ -172,6 +182,7 @@ CG_HD void fe_mul(fe& out, const fe& f, const fe& g) {
 CG_HD void fe_sq(fe& out, const fe& f) {
   // term (i<j): 2 f_i f_j, times 2 if both odd, times 19 if i+j >= 10
   // term (i=i): f_i^2, times 2 if i odd, times 19 if 2i >= 10
+  FE_COUNT(g_fe_nsq);
   uint32_t f2[10], f19[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) {

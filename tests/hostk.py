@@ -18,7 +18,7 @@ def build():
             os.path.getmtime(os.path.join(HERE, "..", "corda_amd", "csrc", f))
             for f in os.listdir(os.path.join(HERE, "..", "corda_amd", "csrc")) if f.endswith(".h")) or \
             os.path.getmtime(SO) < os.path.getmtime(src):
-        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-DFE_BOUNDS_CHECK", "-fPIC", "-shared",
+        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-DFE_BOUNDS_CHECK", "-DFE_OP_COUNT", "-fPIC", "-shared",
                                "-o", SO, src])
     return ctypes.CDLL(SO)
 
@@ -36,6 +36,7 @@ def lib():
         L.t_sha512_prefix.argtypes = [vp, vp, u64, u64, vp]
         L.t_sha256_suffix.argtypes = [vp, u64, u64, vp, vp]
         L.t_mm_mul.argtypes = [i32, i32, vp, vp, vp]
+        L.t_ed_count_w6.argtypes = [vp, vp, vp, u64, vp]
         _lib = L
     return _lib
 

@@ -5,6 +5,9 @@
 #include <string.h>
 
 #include "../../corda_amd/csrc/ed25519.h"
+#ifdef FE_OP_COUNT
+uint64_t g_fe_nmul = 0, g_fe_nsq = 0;
+#endif
 
 static Ed25519Consts g_C;
 static int g_init = 0;
@@ -219,4 +222,71 @@ extern "C" int t_ed_verify_w(int w, const uint32_t* aw, const uint32_t* sw, cons
   if (w == 4) return verify_w<4, 8>(aw, sw, msg, msg_len);
   if (w == 5) return verify_w<5, 4>(aw, sw, msg, msg_len);
   return verify_w<6, 4>(aw, sw, msg, msg_len);
+}
+
+// ---------------------------------------------------------------- executed-work counters
+// Field multiplies / squarings the GPU path executes (same code, host build):
+//   out[0..1] per item in k_ed_verify (double-scalar over the W=6, K=4 rows)
+//   out[2..3] per item in k_ed_finish excluding the shared inversion (prefix product,
+//             unwinding, encode)
+//   out[4..5] one fe_invert (shared by ED_FINISH_K items)
+//   out[6..7] per key: k_ed_keyprep_rows + k_ed_keyprep_tab (decode, Abyte, 11 bases, 352
+//             affine multiples)
+extern "C" int t_ed_count_w6(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len,
+                             uint64_t* out) {
+#ifdef FE_OP_COUNT
+  init();
+  (void)verify_w<6, 4>(aw, sw, msg, msg_len);  // builds static tables once
+  typedef EdRowsCfg<6, 4> C;
+  static EdRowTabW<6, 4> TA;
+  ge_p3 A, N;
+  // per key
+  g_fe_nmul = g_fe_nsq = 0;
+  {
+    static EdKeyPrep kp;
+    fe x, y, z;
+    (void)x; (void)y; (void)z;
+    ed_decode_point(A, aw, g_C);
+    uint32_t ab[8];
+    ed_encode_affine(ab, A.X, A.Y, A.Z);
+    ed_neg_point(N, A);
+    ed_rows_w_init<6, 4>(TA, N, g_C.d2);
+  }
+  out[6] = g_fe_nmul;
+  out[7] = g_fe_nsq;
+  // per item: double-scalar with fixed digits (the schedule is data-independent)
+  uint32_t h[8], sr[8];
+  for (int i = 0; i < 8; ++i) {
+    h[i] = 0x9e3779b9u * (i + 1);
+    sr[i] = 0x7f4a7c15u * (i + 3);
+  }
+  h[7] &= 0x0fffffffu;
+  sr[7] &= 0x0fffffffu;
+  uint32_t eh[C::kPackedWords], es[C::kPackedWords];
+  sc_recode_w<6>(eh, C::kPackedWords, h);
+  sc_recode_w<6>(es, C::kPackedWords, sr);
+  ge_p2 R;
+  g_fe_nmul = g_fe_nsq = 0;
+  ed_double_scalar_w<6, 4>(R, eh, es, TA, TA);
+  out[0] = g_fe_nmul;
+  out[1] = g_fe_nsq;
+  // finish per item: prefix product (1 mul), unwinding (2 mul), encode (2 mul)
+  g_fe_nmul = g_fe_nsq = 0;
+  fe run, zi, t;
+  fe_1(run);
+  fe_mul(run, run, R.Z);
+  fe_mul(zi, run, R.Z);
+  fe_mul(t, zi, R.Z);
+  (void)ed_encode_cmp(R, zi, sw);
+  out[2] = g_fe_nmul;
+  out[3] = g_fe_nsq;
+  g_fe_nmul = g_fe_nsq = 0;
+  fe_invert(t, R.Z);
+  out[4] = g_fe_nmul;
+  out[5] = g_fe_nsq;
+  return 0;
+#else
+  (void)aw; (void)sw; (void)msg; (void)msg_len; (void)out;
+  return -1;
+#endif
 }

@@ -5,6 +5,7 @@ CPU only: this is where kernel arithmetic is debugged before it reaches a GPU.""
 import random
 
 import numpy as np
+import pytest
 
 import golden_io
 import hostk
@@ -121,3 +122,39 @@ def test_sha_lane_code():
             sw = np.frombuffer(sfx, dtype=">u4").astype(np.uint32)
             lib.t_sha256_suffix(ptr(buf), ctypes.c_uint64(off), ctypes.c_uint64(ln), ptr(sw), ptr(o8))
             assert o8.astype(">u4").tobytes() == c_oracle.sha256(msg + sfx)
+
+
+@pytest.mark.parametrize("w", [4, 6])
+def test_ed25519_row_table_lane_verify_on_fixtures(w):
+    """The radix-2^W row-table double-scalar path (k_ed_verify's arithmetic) on the fixtures."""
+    import ctypes
+    lib = hostk.lib()
+    lib.t_ed_verify_w.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_uint64]
+    n = 0
+    for it in golden_io.load("ed25519.json"):
+        key, sig, msg = bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"])
+        if it["key_fmt"] != 0 or len(key) != 32 or len(sig) != 64:
+            continue
+        m = np.frombuffer(msg + bytes(8), dtype=np.uint8).copy()
+        st = lib.t_ed_verify_w(w, ptr(words(key)), ptr(words(sig)), ptr(m), len(msg))
+        got = {0: "VALID", 1: "INVALID", 3: "KEY_INVALID"}[st]
+        assert got == it["expect_isvalid"], it["note"]
+        n += 1
+    assert n > 200
+
+
+def test_executed_work_constants_match_lane_code():
+    """bench.py prices k_ed_verify + k_ed_finish with the field products the lane code
+    executes; the constants there must equal what the host build of that code counts."""
+    import bench
+    lib = hostk.lib()
+    it = next(i for i in golden_io.load("ed25519.json") if i["expect"] == "VALID" and i["key_fmt"] == 0)
+    key, sig, msg = bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"])
+    m = np.frombuffer(msg + bytes(8), dtype=np.uint8).copy()
+    out = np.zeros(8, dtype=np.uint64)
+    assert lib.t_ed_count_w6(ptr(words(key)), ptr(words(sig)), ptr(m), len(msg), ptr(out)) == 0
+    mul_v, sq_v, mul_f, sq_f, mul_i, sq_i = (int(x) for x in out[:6])
+    assert (mul_v, sq_v) == bench.ED_VERIFY_FE, (mul_v, sq_v)
+    assert (mul_f, sq_f) == bench.ED_FINISH_FE, (mul_f, sq_f)
+    assert (mul_i, sq_i) == bench.ED_INVERT_FE, (mul_i, sq_i)

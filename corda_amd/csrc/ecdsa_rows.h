@@ -1,0 +1,361 @@
+// ECDSA double-scalar multiplication u1 G + u2 Q over "row" tables (signed radix-64 digits,
+// the same row/window layout as the Ed25519 path in ed25519_rows.h), plus the split
+// per-item pipeline pieces: parse+hash (prep), batched s^-1 (inv), ladder + x-check.
+//
+// A scalar k < 2^256 is recoded into 43 signed digits e_t in [-32, 32]; digit t = 4j + i
+// belongs to row j (11 rows) and window i (4 windows):
+//     [k] P = sum_{i<4} 2^{6i} sum_{j<11} e_{4j+i} P_j,   P_j = 2^{24j} P.
+// Each row stores the affine multiples 1..32 of P_j (x, y in Montgomery form, 64 B each):
+// 22 528 B per point. The G rows are built once per context; the Q rows once per key.
+// The loop does 18 Jacobian doublings and one mixed addition per non-zero digit (<= 86),
+// against BouncyCastle's ~256 doublings + wNAF additions (ECAlgorithms.sumOfTwoMultiplies).
+// Exception cases (R = +-T, R = infinity) are handled inside jac_madd, so adversarial
+// inputs stay exact; honest lanes never take those branches.
+#pragma once
+#include "ecdsa.h"
+
+#define EC_W 6
+#define EC_WINDOWS 4
+#define EC_DIGITS 43
+#define EC_ROWS 11
+#define EC_MULT 32
+#define EC_PACKED 11
+
+struct EcAff {
+  u256w x, y;  // affine, Montgomery form
+};
+
+struct EcRowTab {
+  EcAff t[EC_ROWS][EC_MULT];  // t[j][k-1] = k * 2^{24j} * P
+};
+
+// Signed radix-64 digits of a < 2^256, 4 per word as signed bytes. The top digit covers
+// bits 252..255 (+ carry <= 16), so no digit overflows.
+CG_HD void ec_recode_w6(uint32_t packed[EC_PACKED], const u256w& a) {
+#pragma unroll
+  for (int w = 0; w < EC_PACKED; ++w) packed[w] = 0;
+  int carry = 0;
+#pragma unroll
+  for (int t = 0; t < EC_DIGITS; ++t) {
+    const int bit = t * EC_W;
+    const int wi = bit >> 5, sh = bit & 31;
+    uint64_t x = (uint64_t)a.w[wi] >> sh;
+    if (sh + EC_W > 32 && wi + 1 < 8) x |= (uint64_t)a.w[wi + 1] << (32 - sh);
+    int e = (int)((uint32_t)x & 63u) + carry;
+    carry = (e + 32) >> 6;
+    e -= carry << 6;
+    packed[t >> 2] |= ((uint32_t)(e & 0xff)) << ((t & 3) * 8);
+  }
+}
+
+CG_HD int ec_digit6(const uint32_t* packed, int t) {
+  return (int)(int8_t)(uint8_t)(packed[t >> 2] >> ((t & 3) * 8));
+}
+
+// General Jacobian addition r = p + q (add-2007-bl), exception-complete.
+template <int C>
+CG_HD void jac_add(Jac& r, const Jac& p, const Jac& q, const EcConsts& K) {
+  if (u256_iszero(p.Z)) {
+    r = q;
+    return;
+  }
+  if (u256_iszero(q.Z)) {
+    r = p;
+    return;
+  }
+  u256w Z1Z1, Z2Z2, U1, U2, S1, S2, H, rr, I, J, V, t;
+  mm_sq<C, 0>(Z1Z1, p.Z);
+  mm_sq<C, 0>(Z2Z2, q.Z);
+  mm_mul<C, 0>(U1, p.X, Z2Z2);
+  mm_mul<C, 0>(U2, q.X, Z1Z1);
+  mm_mul<C, 0>(S1, p.Y, q.Z);
+  mm_mul<C, 0>(S1, S1, Z2Z2);
+  mm_mul<C, 0>(S2, q.Y, p.Z);
+  mm_mul<C, 0>(S2, S2, Z1Z1);
+  mm_sub<C, 0>(H, U2, U1);
+  mm_sub<C, 0>(rr, S2, S1);
+  if (u256_iszero(H)) {
+    if (u256_iszero(rr)) {
+      jac_dbl<C>(r, p);
+    } else {
+      u256_zero(r.X);
+      r.Y = K.one_p;
+      u256_zero(r.Z);
+    }
+    return;
+  }
+  mm_add<C, 0>(I, H, H);
+  mm_sq<C, 0>(I, I);
+  mm_mul<C, 0>(J, H, I);
+  mm_add<C, 0>(rr, rr, rr);
+  mm_mul<C, 0>(V, U1, I);
+  Jac o;
+  mm_sq<C, 0>(o.X, rr);
+  mm_sub<C, 0>(o.X, o.X, J);
+  mm_add<C, 0>(t, V, V);
+  mm_sub<C, 0>(o.X, o.X, t);
+  mm_sub<C, 0>(t, V, o.X);
+  mm_mul<C, 0>(o.Y, rr, t);
+  mm_mul<C, 0>(t, S1, J);
+  mm_add<C, 0>(t, t, t);
+  mm_sub<C, 0>(o.Y, o.Y, t);
+  mm_add<C, 0>(t, p.Z, q.Z);
+  mm_sq<C, 0>(t, t);
+  mm_sub<C, 0>(t, t, Z1Z1);
+  mm_sub<C, 0>(t, t, Z2Z2);
+  mm_mul<C, 0>(o.Z, t, H);
+  r = o;
+}
+
+// 2^n * P
+template <int C>
+CG_HD void jac_dbl_n(Jac& r, const Jac& p, int n) {
+  Jac t = p;
+  for (int i = 0; i < n; ++i) jac_dbl<C>(t, t);
+  r = t;
+}
+
+// One row: the affine multiples 1..32 of the (finite, prime-order) Jacobian point `base`.
+// `scratch` holds 32 Jacobian points and 32 prefix products (the batch inversion runs
+// through memory, not registers). One field inversion per row.
+struct EcRowScratch {
+  Jac p[EC_MULT];
+  u256w pre[EC_MULT];
+};
+
+template <int C>
+CG_HD void ec_row_build(EcAff* row, const Jac& base, EcRowScratch& s, const EcConsts& K) {
+  Jac acc = base;
+  s.p[0] = acc;
+  s.pre[0] = acc.Z;
+  for (int k = 1; k < EC_MULT; ++k) {
+    jac_add<C>(acc, acc, base, K);  // k = 1: P + P goes through the doubling branch
+    s.p[k] = acc;
+    mm_mul<C, 0>(s.pre[k], s.pre[k - 1], acc.Z);
+  }
+  u256w inv;
+  mm_inv<C, 0>(inv, s.pre[EC_MULT - 1], K.one_p);
+  for (int k = EC_MULT - 1; k >= 0; --k) {
+    u256w zi, zi2, zi3;
+    if (k > 0) {
+      mm_mul<C, 0>(zi, inv, s.pre[k - 1]);
+      mm_mul<C, 0>(inv, inv, s.p[k].Z);
+    } else {
+      zi = inv;
+    }
+    mm_sq<C, 0>(zi2, zi);
+    mm_mul<C, 0>(zi3, zi2, zi);
+    mm_mul<C, 0>(row[k].x, s.p[k].X, zi2);
+    mm_mul<C, 0>(row[k].y, s.p[k].Y, zi3);
+  }
+}
+
+// The 11 row bases 2^{24j} P of an affine (Montgomery) point.
+template <int C>
+CG_HD void ec_row_bases(Jac bases[EC_ROWS], const u256w& xm, const u256w& ym, const EcConsts& K) {
+  Jac P = {xm, ym, K.one_p};
+  for (int j = 0; j < EC_ROWS; ++j) {
+    bases[j] = P;
+    if (j + 1 < EC_ROWS) jac_dbl_n<C>(P, P, EC_W * EC_WINDOWS);
+  }
+}
+
+// Key decode (BC 1.57 semantics: SPKI / raw / SEC1, point validated on the curve) to the
+// affine point in Montgomery form. Returns 0 ok / 3 KEY_INVALID.
+template <int C>
+CG_HD uint32_t ec_key_decode_xy(u256w& xm, u256w& ym, const u256w& x, const u256w& y, const EcConsts& K) {
+  if (!u256_lt_mod<C, 0>(x) || !u256_lt_mod<C, 0>(y)) return 3;
+  u256w l, rr;
+  mm_mul<C, 0>(xm, x, K.r2_p);
+  mm_mul<C, 0>(ym, y, K.r2_p);
+  mm_sq<C, 0>(l, ym);
+  mm_sq<C, 0>(rr, xm);
+  mm_mul<C, 0>(rr, rr, xm);
+  if (C == CG_CURVE_R1) {  // x^3 - 3x + b
+    u256w t;
+    mm_add<C, 0>(t, xm, xm);
+    mm_add<C, 0>(t, t, xm);
+    mm_sub<C, 0>(rr, rr, t);
+  }
+  mm_add<C, 0>(rr, rr, K.b_m);
+  return u256_eq(l, rr) ? 0u : 3u;
+}
+
+template <int C>
+CG_HD uint32_t ec_key_decode_bytes(u256w& xm, u256w& ym, const uint8_t* arena, uint64_t lr, uint64_t off,
+                                   uint32_t len, uint32_t fmt, const EcConsts& K) {
+  u256w x, y;
+  uint64_t pt = off;
+  uint32_t ptlen = len;
+  if (fmt == 1) {  // SPKI
+    const uint32_t pl = C == CG_CURVE_R1 ? 26 : 23;
+    if (len != pl + 65) return 3;
+    for (uint32_t i = 0; i < pl; ++i)
+      if (der_byte(arena, lr, off + i) != ec_spki_prefix_byte(C, (int)i)) return 3;
+    pt = off + pl;
+    ptlen = 65;
+  } else if (fmt == 0) {  // RAW
+    if (len != 64) return 3;
+    ec_load_be32(x, arena, lr, off);
+    ec_load_be32(y, arena, lr, off + 32);
+    return ec_key_decode_xy<C>(xm, ym, x, y, K);
+  } else if (fmt != 2) {
+    return 3;
+  }
+  const uint32_t tag = ptlen ? der_byte(arena, lr, pt) : 0u;
+  if (ptlen == 65 && tag == 4) {
+    ec_load_be32(x, arena, lr, pt + 1);
+    ec_load_be32(y, arena, lr, pt + 33);
+    return ec_key_decode_xy<C>(xm, ym, x, y, K);
+  }
+  if (ptlen == 33 && (tag == 2 || tag == 3)) {
+    ec_load_be32(x, arena, lr, pt + 1);
+    if (!ec_decompress<C>(y, x, tag & 1u, K)) return 3;
+    return ec_key_decode_xy<C>(xm, ym, x, y, K);
+  }
+  return 3;
+}
+
+// ---------------------------------------------------------------- per-item pipeline
+// Item workspace between the three stages (96 B): after prep {r, s, e}; after inv {r, u1, u2}.
+struct EcItemWs {
+  u256w r, a, b;
+};
+
+// Stage 1: DER, range checks, e = SHA-256(M) mod n. Returns 0 (pending: ws filled),
+// 1 INVALID or 2 SIG_MALFORMED.
+template <int C>
+CG_HD uint32_t ecdsa_prep(EcItemWs& ws, const uint8_t* arena, uint64_t lr, uint64_t sig_off, uint32_t sig_len,
+                          uint64_t msg_off, uint64_t msg_len) {
+  u256w r, s;
+  bool range_ok = false;
+  if (der_sig(arena, lr, sig_off, sig_len, r, s, &range_ok)) return 2;
+  if (!range_ok) return 1;
+  if (!u256_lt_mod<C, 1>(r) || !u256_lt_mod<C, 1>(s)) return 1;
+  uint32_t h[8];
+  sha256_arena_suffix(h, arena, lr, msg_off, msg_len, nullptr);
+  u256w e;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) e.w[i] = h[7 - i];
+  if (!u256_lt_mod<C, 1>(e)) {  // e < 2^256 < 2n
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t x = (uint64_t)e.w[i] - Mod<C, 1>::w(i) - br;
+      e.w[i] = (uint32_t)x;
+      br = (uint32_t)(x >> 63);
+    }
+  }
+  ws.r = r;
+  ws.a = s;
+  ws.b = e;
+  return 0;
+}
+
+// Stage 2 (per group): w = s^-1 by one shared inversion (Montgomery's trick); u1 = e w,
+// u2 = r w (plain). `sel` marks the pending items of this curve among ws[0..cnt).
+template <int C, int G>
+CG_HD void ecdsa_batch_inv(EcItemWs* ws, uint32_t cnt, uint32_t sel, const EcConsts& K) {
+  u256w pre[G];
+  u256w run = K.one_n;
+  for (uint32_t k = 0; k < cnt; ++k) {
+    if ((sel >> k) & 1u) {
+      u256w sm;
+      mm_mul<C, 1>(sm, ws[k].a, K.r2_n);  // s * R (Montgomery)
+      mm_mul<C, 1>(run, run, sm);
+    }
+    pre[k] = run;
+  }
+  if (!sel) return;
+  u256w inv;
+  mm_inv<C, 1>(inv, run, K.one_n);  // (prod s R)^-1 R
+  for (int k = (int)cnt - 1; k >= 0; --k) {
+    if (!((sel >> k) & 1u)) continue;
+    int prev = k - 1;
+    while (prev >= 0 && !((sel >> prev) & 1u)) --prev;
+    u256w wm, sm;
+    if (prev >= 0) mm_mul<C, 1>(wm, inv, pre[prev]);
+    else wm = inv;
+    mm_mul<C, 1>(sm, ws[k].a, K.r2_n);
+    mm_mul<C, 1>(inv, inv, sm);
+    u256w u1, u2;
+    mm_mul<C, 1>(u1, ws[k].b, wm);
+    mm_mul<C, 1>(u2, ws[k].r, wm);
+    ws[k].a = u1;
+    ws[k].b = u2;
+  }
+}
+
+template <class RowT>
+CG_HD void ec_pick(u256w& x, u256w& y, const RowT* row, int a) {
+  const EcAff& e = row[a - 1];
+  x = e.x;
+  y = e.y;
+}
+
+// Stage 3: R = u1 G + u2 Q over the row tables; x(R) == r (mod n) by BC's inversion-free test.
+// TG / TQ point at [EC_ROWS][EC_MULT] arrays (LDS or global). Returns 0 VALID / 1 INVALID.
+template <int C, class TabG, class TabQ>
+CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG, const TabQ& TQ,
+                                  const EcConsts& K) {
+  uint32_t d1[EC_PACKED], d2[EC_PACKED];
+  ec_recode_w6(d1, u1);
+  ec_recode_w6(d2, u2);
+  Jac R;
+  u256_zero(R.X);
+  R.Y = K.one_p;
+  u256_zero(R.Z);
+  for (int i = EC_WINDOWS - 1; i >= 0; --i) {
+    if (i != EC_WINDOWS - 1) {
+#pragma unroll 1
+      for (int d = 0; d < EC_W; ++d) jac_dbl<C>(R, R);
+    }
+#pragma unroll 1
+    for (int j = 0; j < EC_ROWS; ++j) {
+      const int t = EC_WINDOWS * j + i;
+      if (t >= EC_DIGITS) continue;
+      const int a = ec_digit6(d1, t);
+      if (a != 0) {
+        u256w x, y;
+        ec_pick(x, y, TG.t[j], a < 0 ? -a : a);
+        if (a < 0) mm_neg<C, 0>(y, y);
+        jac_madd<C>(R, R, x, y, K);
+      }
+      const int b = ec_digit6(d2, t);
+      if (b != 0) {
+        u256w x, y;
+        ec_pick(x, y, TQ.t[j], b < 0 ? -b : b);
+        if (b < 0) mm_neg<C, 0>(y, y);
+        jac_madd<C>(R, R, x, y, K);
+      }
+    }
+  }
+  if (u256_iszero(R.Z)) return 1;
+  u256w z2, t, rm;
+  mm_sq<C, 0>(z2, R.Z);
+  mm_mul<C, 0>(rm, r, K.r2_p);
+  mm_mul<C, 0>(t, rm, z2);
+  if (u256_eq(t, R.X)) return 0;
+  u256w rn;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (uint64_t)r.w[i] + Mod<C, 1>::w(i);
+    rn.w[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  if (c == 0 && u256_lt_mod<C, 0>(rn)) {
+    mm_mul<C, 0>(rm, rn, K.r2_p);
+    mm_mul<C, 0>(t, rm, z2);
+    if (u256_eq(t, R.X)) return 0;
+  }
+  return 1;
+}
+
+// G rows (per context) from the curve constants.
+template <int C>
+CG_HD void ec_g_rows_init(EcRowTab& T, EcRowScratch& s, const EcConsts& K) {
+  Jac bases[EC_ROWS];
+  ec_row_bases<C>(bases, K.gx[1], K.gy[1], K);
+  for (int j = 0; j < EC_ROWS; ++j) ec_row_build<C>(T.t[j], bases[j], s, K);
+}

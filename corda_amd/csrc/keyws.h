@@ -1,0 +1,109 @@
+// Shared layout of the per-key and per-item device workspaces and the constant tables, used
+// by the Ed25519 (verify_ed.hip), ECDSA (verify_ec.hip) and dispatch (verify.hip) units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ecdsa.h"
+#include "ecdsa_rows.h"
+#include "ed25519.h"
+#include "ed25519_rows.h"
+#include "engine.h"
+
+namespace cg {
+
+__device__ __forceinline__ uint64_t round4(uint64_t x) { return (x + 3) & ~(uint64_t)3; }
+
+__device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t arena_len) {
+  return off <= arena_len && len <= arena_len - off;
+}
+
+// Row tables (ed25519_rows.h) with signed radix-64 digits: 43 digits in 11 rows of 4 windows.
+#define ED_W 6
+#define ED_K 4
+typedef EdRowsCfg<ED_W, ED_K> EdCfg;
+typedef EdRowTabW<ED_W, ED_K> EdTab;  // 11 x 32 affine niels = 42240 B
+
+// Per-key header: status (0 = decoded) and, for Ed25519, the canonical Abyte i2p hashes.
+struct EdKeyHdr {
+  uint32_t status;
+  uint32_t abyte[8];
+  uint32_t pad[7];
+};
+
+// A key is either Ed25519 or ECDSA: its table and row-base slots are shared.
+union TabSlot {
+  EdTab ed;
+  EcRowTab ec;
+};
+union BaseSlot {
+  ge_p3 ed;
+  Jac ec;
+};
+
+// Key workspace, each region n_keys long (a key is either Ed25519 or ECDSA, so the table and
+// base slots are shared: TabSlot / BaseSlot unions give one stride for both schemes):
+//   hdr      EdKeyHdr (status [+ Abyte])                       64 B
+//   tab      EdTab | EcRowTab                                  42 240 B
+//   bases    11 x (ge_p3 | Jac)                                1 760 B
+//   ecs      11 x EcRowScratch (ECDSA batch-inversion scratch) 45 056 B
+static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+struct KeyWs {
+  EdKeyHdr* hdr;
+  TabSlot* tab;
+  BaseSlot* bases;
+  EcRowScratch* ecs;
+};
+static inline KeyWs key_ws(void* base, uint32_t n_keys) {
+  const size_t n = n_keys ? n_keys : 1;
+  uint8_t* p = (uint8_t*)base;
+  KeyWs w;
+  w.hdr = (EdKeyHdr*)p;
+  p += al256(n * sizeof(EdKeyHdr));
+  w.tab = (TabSlot*)p;
+  p += al256(n * sizeof(TabSlot));
+  w.bases = (BaseSlot*)p;
+  p += al256(n * EdCfg::kRows * sizeof(BaseSlot));
+  w.ecs = (EcRowScratch*)p;
+  return w;
+}
+static inline size_t key_ws_bytes(uint32_t n_keys) {
+  const size_t n = n_keys ? n_keys : 1;
+  return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(TabSlot)) + al256(n * EdCfg::kRows * sizeof(BaseSlot)) +
+         n * EC_ROWS * sizeof(EcRowScratch);
+}
+
+// Per-item workspace slot: projective Ed25519 R' awaiting the batched inversion, or the
+// ECDSA stage hand-off. Reused across schemes: k_ed_finish has consumed the Ed25519 slots
+// before the ECDSA stages write theirs, and each curve runs its three stages in turn.
+constexpr size_t ITEM_SLOT = sizeof(ge_p2) > sizeof(EcItemWs) ? sizeof(ge_p2) : sizeof(EcItemWs);
+
+// Constant tables per context: [Ed25519 B rows][G rows k1][G rows r1][row scratch]
+static inline size_t const_tab_bytes() { return sizeof(EdTab) + 2 * sizeof(EcRowTab) + sizeof(EcRowScratch); }
+static inline const EcRowTab* gtab(const void* d_btab, int curve) {
+  return (const EcRowTab*)((const uint8_t*)d_btab + sizeof(EdTab)) + curve;
+}
+static inline EcRowScratch* const_scratch(void* d_btab) {
+  return (EcRowScratch*)((uint8_t*)d_btab + sizeof(EdTab) + 2 * sizeof(EcRowTab));
+}
+
+// Intermediate per-item status codes (never returned to the caller)
+#define ED_PENDING 254u
+#define EC_PENDING_BASE 250u  // + curve: parsed + hashed, awaiting the ladder
+
+// Per-scheme halves (verify_ed.hip / verify_ec.hip)
+hipError_t ed_upload_constants();
+hipError_t ed_init_const(void* d_btab, hipStream_t stream);
+void ed_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                       const KeyWs& w, hipStream_t stream);
+void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                     const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
+                     void* d_item_ws, const void* d_btab, hipStream_t stream);
+hipError_t ec_upload_constants();
+hipError_t ec_init_const(void* d_btab, hipStream_t stream);
+void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                       const KeyWs& w, hipStream_t stream);
+void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                     const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
+                     void* d_item_ws, const void* d_btab, hipStream_t stream);
+
+}  // namespace cg

@@ -1,337 +1,15 @@
-// Batch signature verification kernels for gfx950.
+// Batch signature verification for gfx950: dispatch over the per-scheme kernels.
 //
 // Pipeline per batch (all on the caller's stream, no host round trip):
-//   k_ed_keyprep_rows  one lane per distinct key: decode A, canonical Abyte, row bases
-//                      2^{24j} (-A), j = 0..10
-//   k_ed_keyprep_tab   one lane per (key, row, 8 multiples): affine multiples of the row base
-//   k_ed_verify        one lane per Ed25519 item: SHA-512 challenge, scalar prep, 4 windows
-//                      x (11 rows of -A + 11 rows of B) mixed additions, 18 doublings
-//   k_ed_finish        16 items per lane: batch inversion, encode, byte compare
-//   k_ec_keyprep / k_ec_verify  ECDSA secp256r1 / secp256k1
-//   k_misc_status  one lane per item of an unsupported scheme / bad key index
+//   key prep      verify_ed.hip k_ed_keyprep_rows/_tab, verify_ec.hip k_ec_keyprep_rows/_tab
+//   items         k_misc_status (unsupported scheme / bad key index), then the Ed25519 stages
+//                 (k_ed_verify, k_ed_finish), then per curve the ECDSA stages (k_ec_prep,
+//                 k_ec_inv, k_ec_ladder). Each stage writes the final status byte of its items.
 // Replaces, per item, the JCA call at core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559
 // behind Crypto.doVerify (Crypto.kt:474-484).
-#include <hip/hip_runtime.h>
-
-#include "ecdsa.h"
-#include "ed25519.h"
-#include "ed25519_rows.h"
-#include "engine.h"
+#include "keyws.h"
 
 namespace cg {
-
-__constant__ Ed25519Consts c_ed;
-
-static const uint8_t ED_SPKI_PREFIX[12] = {0x30, 0x2a, 0x30, 0x05, 0x06, 0x03, 0x2b, 0x65, 0x70, 0x03, 0x21, 0x00};
-
-__device__ __forceinline__ uint64_t round4(uint64_t x) { return (x + 3) & ~(uint64_t)3; }
-
-__device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t arena_len) {
-  return off <= arena_len && len <= arena_len - off;
-}
-
-// ------------------------------------------------------------------ Ed25519 (i2p 0.2.0 semantics)
-// Row tables (ed25519_rows.h) with signed radix-64 digits: 43 digits in 11 rows of 4 windows.
-#define ED_W 6
-#define ED_K 4
-typedef EdRowsCfg<ED_W, ED_K> EdCfg;
-typedef EdRowTabW<ED_W, ED_K> EdTab;  // 11 x 32 affine niels = 42240 B
-
-// Key workspace (per distinct key):
-//   EdKeyHdr  status + canonical Abyte                               64 B
-//   EdTab     t[j][k-1] = k * 2^{24j} * (-A), affine niels           42240 B
-//   bases     2^{24j} * (-A), j = 0..10 (extended; table scratch)    1760 B
-struct EdKeyHdr {
-  uint32_t status;
-  uint32_t abyte[8];
-  uint32_t pad[7];
-};
-
-__global__ void __launch_bounds__(64) k_ed_keyprep_rows(const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                        const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                        EdKeyHdr* __restrict__ hdr, ge_p3* __restrict__ bases) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_keys) return;
-  const cg_key k = keys[i];
-  if (k.scheme != CG_EDDSA_ED25519_SHA512) return;
-  const uint64_t lr = round4(arena_len);
-  uint64_t a_off = k.off;
-  bool ok = in_arena(k.off, k.len, arena_len);
-  if (ok && k.fmt == CG_KEY_RAW) {
-    ok = k.len == 32;
-  } else if (ok && k.fmt == CG_KEY_SPKI) {
-    ok = k.len == 44;
-    for (int b = 0; ok && b < 12; ++b) ok = (cg_ld_bytes4(arena, lr, k.off + b) & 0xffu) == ED_SPKI_PREFIX[b];
-    a_off = k.off + 12;
-  } else {
-    ok = false;
-  }
-  EdKeyHdr h;
-  for (int w = 0; w < 7; ++w) h.pad[w] = 0;
-  for (int w = 0; w < 8; ++w) h.abyte[w] = 0;
-  h.status = CG_KEY_INVALID;
-  if (ok) {
-    uint32_t aw[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) aw[w] = cg_ld_bytes4(arena, lr, a_off + 4 * w);
-    ge_p3 A;
-    if (ed_decode_point(A, aw, c_ed) == ED_ST_VALID) {
-      h.status = 0;
-      ed_encode_affine(h.abyte, A.X, A.Y, A.Z);
-      ge_p3 P;
-      ed_neg_point(P, A);
-      for (int j = 0; j < EdCfg::kRows; ++j) {
-        bases[(size_t)i * EdCfg::kRows + j] = P;
-        if (j + 1 < EdCfg::kRows) ed_dbl_n(P, P, ED_W * ED_K);
-      }
-    }
-  }
-  hdr[i] = h;
-}
-
-// m * P for a small m >= 1 (double-and-add, MSB first)
-__device__ void ed_small_mul(ge_p3& R, const ge_p3& P, uint32_t m) {
-  ge_cached c;
-  ge_p3_to_cached(c, P, c_ed.d2);
-  R = P;
-  ge_p1p1 t;
-  int top = 31 - __builtin_clz(m);
-  for (int b = top - 1; b >= 0; --b) {
-    ge_p3_dbl(t, R);
-    ge_p1p1_to_p3(R, t);
-    if ((m >> b) & 1u) {
-      ge_add_cached(t, R, c);
-      ge_p1p1_to_p3(R, t);
-    }
-  }
-}
-
-// one lane per (key, row, group of 8 multiples)
-__global__ void __launch_bounds__(64) k_ed_keyprep_tab(const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                       const EdKeyHdr* __restrict__ hdr,
-                                                       const ge_p3* __restrict__ bases, EdTab* __restrict__ tabs) {
-  constexpr uint32_t G = EdCfg::kMult / 8;
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = g / (EdCfg::kRows * G);
-  const uint32_t rem = g % (EdCfg::kRows * G);
-  const uint32_t j = rem / G, grp = rem % G;
-  if (i >= n_keys) return;
-  if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || hdr[i].status != 0) return;
-  const ge_p3 P = bases[(size_t)i * EdCfg::kRows + j];
-  ge_p3 pts[8];
-  ed_small_mul(pts[0], P, 8 * grp + 1);
-  ge_cached c;
-  ge_p3_to_cached(c, P, c_ed.d2);
-  ge_p1p1 t;
-  for (int k = 1; k < 8; ++k) {
-    ge_add_cached(t, pts[k - 1], c);
-    ge_p1p1_to_p3(pts[k], t);
-  }
-  ge_niels row[8];
-  ed_niels_batch8(row, pts, c_ed.d2);
-  for (int k = 0; k < 8; ++k) tabs[i].t[j][8 * grp + k] = row[k];
-}
-
-// B rows, built once per context by the same code
-__global__ void k_ed_btab_init(EdTab* __restrict__ out) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  ge_p3 B;
-  fe x, y, two_inv, t;
-  fe_sub(x, c_ed.Btab[1].ypx, c_ed.Btab[1].ymx);
-  fe_add(y, c_ed.Btab[1].ypx, c_ed.Btab[1].ymx);
-  fe_0(t);
-  t.v[0] = 2;
-  fe_invert(two_inv, t);
-  fe_mul(B.X, x, two_inv);
-  fe_mul(B.Y, y, two_inv);
-  fe_1(B.Z);
-  fe_mul(B.T, B.X, B.Y);
-  ed_rows_w_init<ED_W, ED_K>(*out, B, c_ed.d2);
-}
-
-#define ED_PENDING 254u
-
-__device__ __forceinline__ void ld_niels(ge_niels& n, const ge_niels* src) {
-  const uint4* p = (const uint4*)src;
-  uint32_t* d = (uint32_t*)&n;
-#pragma unroll
-  for (int q = 0; q < 7; ++q) {
-    const uint4 v = p[q];
-    d[4 * q] = v.x;
-    d[4 * q + 1] = v.y;
-    d[4 * q + 2] = v.z;
-    d[4 * q + 3] = v.w;
-  }
-  const uint2 v = ((const uint2*)src)[14];
-  d[28] = v.x;
-  d[29] = v.y;
-}
-
-__device__ __forceinline__ void pick(ge_niels& out, const ge_niels* row, int d) {
-  const int a = d < 0 ? -d : d;
-  ld_niels(out, row + (a > 0 ? a - 1 : 0));
-  if (a == 0) ge_niels_identity(out);
-  ge_niels_cneg(out, d < 0);
-}
-
-__global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ items, uint64_t n_items,
-                                                   const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                   const EdKeyHdr* __restrict__ hdr, const EdTab* __restrict__ tabs,
-                                                   const EdTab* __restrict__ btab,
-                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                   uint32_t mode, uint8_t* __restrict__ status,
-                                                   ge_p2* __restrict__ rout) {
-  __shared__ EdTab sB;
-  {
-    const uint4* src = (const uint4*)btab;
-    uint4* dst = (uint4*)&sB;
-    for (uint32_t w = threadIdx.x; w < sizeof(EdTab) / 16; w += blockDim.x) dst[w] = src[w];
-  }
-  __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_items) return;
-  const cg_item it = items[i];
-  if (it.key_idx >= n_keys) return;
-  if (keys[it.key_idx].scheme != CG_EDDSA_ED25519_SHA512) return;
-  const EdKeyHdr* kh = hdr + it.key_idx;
-  uint8_t st;
-  if (kh->status != 0) {
-    st = CG_KEY_INVALID;
-  } else if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
-    st = CG_EMPTY;
-  } else if (!in_arena(it.sig_off, it.sig_len, arena_len) || !in_arena(it.msg_off, it.msg_len, arena_len)) {
-    st = CG_NOT_RUN;
-  } else if (it.sig_len != 64) {
-    st = CG_SIG_MALFORMED;
-  } else {
-    const uint64_t lr = round4(arena_len);
-    uint32_t sw[16], ab[8];
-#pragma unroll
-    for (int w = 0; w < 16; ++w) sw[w] = cg_ld_bytes4(arena, lr, it.sig_off + 4 * w);
-#pragma unroll
-    for (int w = 0; w < 8; ++w) ab[w] = kh->abyte[w];
-    // h = SHA-512(R || Abyte || M) mod L ; S' = slide value of S mod L
-    uint32_t pre[16], hw[16], h[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      pre[w] = sw[w];
-      pre[8 + w] = ab[w];
-    }
-    sha512_prefix64_msg(hw, pre, arena, lr, it.msg_off, it.msg_len);
-    sc_reduce512(h, hw);
-    uint32_t s[8], sr[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) s[w] = sw[8 + w];
-    sc_reduce256(sr, s);
-    if (s[7] >> 31) {
-      if (sc_slide_escapes(s)) {
-        uint32_t r1[8];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) r1[w] = sc_R1w(w);
-        sc_sub(sr, sr, r1);
-      }
-    }
-    uint32_t eh[EdCfg::kPackedWords], es[EdCfg::kPackedWords];
-    sc_recode_w<ED_W>(eh, EdCfg::kPackedWords, h);
-    sc_recode_w<ED_W>(es, EdCfg::kPackedWords, sr);
-    ge_p2 q;
-    ed_double_scalar_w<ED_W, ED_K>(q, eh, es, tabs[it.key_idx], sB);
-    rout[i] = q;
-    st = (uint8_t)ED_PENDING;
-  }
-  status[i] = st;
-}
-
-// Encode + compare for 16 consecutive items per lane: one inversion per lane (Montgomery's
-// trick) instead of one per item.
-#define ED_FINISH_K 16
-__global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ items, uint64_t n_items,
-                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                   uint8_t* __restrict__ status, const ge_p2* __restrict__ rin) {
-  const uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * ED_FINISH_K;
-  if (base >= n_items) return;
-  const uint32_t cnt = (uint32_t)((n_items - base) < ED_FINISH_K ? (n_items - base) : ED_FINISH_K);
-  fe acc[ED_FINISH_K];
-  fe run;
-  fe_1(run);
-  uint32_t pend = 0;
-  for (uint32_t k = 0; k < cnt; ++k) {
-    const bool p = status[base + k] == ED_PENDING;
-    pend |= (uint32_t)p << k;
-    if (p) {
-      fe_mul(run, run, rin[base + k].Z);
-    }
-    fe_copy(acc[k], run);
-  }
-  if (!pend) return;
-  fe inv;
-  fe_invert(inv, run);
-  const uint64_t lr = round4(arena_len);
-  for (int k = (int)cnt - 1; k >= 0; --k) {
-    if (!((pend >> k) & 1u)) continue;
-    fe zi, t;
-    // acc[k] = prod of pending Z up to k; inv = 1 / acc[k]
-    int prev = k - 1;
-    while (prev >= 0 && !((pend >> prev) & 1u)) --prev;
-    if (prev >= 0) fe_mul(zi, inv, acc[prev]);
-    else fe_copy(zi, inv);
-    fe_mul(t, inv, rin[base + k].Z);
-    fe_copy(inv, t);
-    const ge_p2 P = rin[base + k];
-    uint32_t rw[8];
-    const uint64_t so = items[base + k].sig_off;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) rw[w] = cg_ld_bytes4(arena, lr, so + 4 * w);
-    status[base + k] = (uint8_t)ed_encode_cmp(P, zi, rw);
-  }
-}
-
-// ------------------------------------------------------------------ ECDSA (BC 1.57 semantics)
-__constant__ EcConsts c_ec[2];  // [CG_CURVE_K1], [CG_CURVE_R1]
-
-template <int C>
-__global__ void __launch_bounds__(64) k_ec_keyprep(const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                   EcKeyPrep* __restrict__ out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_keys) return;
-  const cg_key k = keys[i];
-  const uint8_t want = C == CG_CURVE_R1 ? CG_ECDSA_SECP256R1_SHA256 : CG_ECDSA_SECP256K1_SHA256;
-  if (k.scheme != want) return;
-  if (!in_arena(k.off, k.len, arena_len)) {
-    out[i].status = CG_KEY_INVALID;
-    return;
-  }
-  const uint32_t st = ec_key_prep_bytes<C>(out[i], arena, round4(arena_len), k.off, k.len, k.fmt, c_ec[C]);
-  out[i].status = st ? CG_KEY_INVALID : 0u;
-}
-
-template <int C>
-__global__ void __launch_bounds__(256) k_ec_verify(const cg_item* __restrict__ items, uint64_t n_items,
-                                                   const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                   const EcKeyPrep* __restrict__ kps,
-                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                   uint32_t mode, uint8_t* __restrict__ status) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_items) return;
-  const cg_item it = items[i];
-  if (it.key_idx >= n_keys) return;
-  const uint8_t want = C == CG_CURVE_R1 ? CG_ECDSA_SECP256R1_SHA256 : CG_ECDSA_SECP256K1_SHA256;
-  if (keys[it.key_idx].scheme != want) return;
-  const EcKeyPrep* kp = kps + it.key_idx;
-  uint8_t st;
-  if (kp->status != 0) {
-    st = CG_KEY_INVALID;
-  } else if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
-    st = CG_EMPTY;
-  } else if (!in_arena(it.sig_off, it.sig_len, arena_len) || !in_arena(it.msg_off, it.msg_len, arena_len)) {
-    st = CG_NOT_RUN;
-  } else {
-    st = (uint8_t)ecdsa_verify_core<C>(*kp, arena, round4(arena_len), it.sig_off, it.sig_len, it.msg_off, it.msg_len,
-                                       c_ec[C]);
-  }
-  status[i] = st;
-}
 
 __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_items, const cg_key* __restrict__ keys,
                               uint32_t n_keys, uint8_t* __restrict__ status) {
@@ -348,63 +26,27 @@ __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_item
 }
 
 hipError_t upload_constants() {
-  Ed25519Consts h;
-  ed_consts_init(h);
-  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_ed), &h, sizeof h, 0, hipMemcpyHostToDevice);
+  hipError_t e = ed_upload_constants();
   if (e != hipSuccess) return e;
-
-  EcConsts k[2];
-  ec_consts_init<CG_CURVE_K1>(k[CG_CURVE_K1]);
-  ec_consts_init<CG_CURVE_R1>(k[CG_CURVE_R1]);
-  return hipMemcpyToSymbol(HIP_SYMBOL(c_ec), k, sizeof k, 0, hipMemcpyHostToDevice);
+  return ec_upload_constants();
 }
 
-// key workspace: [EdKeyHdr][EdRowTab][row bases][EcKeyPrep], each region n_keys long
-static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
-struct KeyWs {
-  EdKeyHdr* hdr;
-  EdTab* tab;
-  ge_p3* bases;
-  EcKeyPrep* ec;
-};
-static KeyWs key_ws(void* base, uint32_t n_keys) {
-  const size_t n = n_keys ? n_keys : 1;
-  uint8_t* p = (uint8_t*)base;
-  KeyWs w;
-  w.hdr = (EdKeyHdr*)p;
-  p += al256(n * sizeof(EdKeyHdr));
-  w.tab = (EdTab*)p;
-  p += al256(n * sizeof(EdTab));
-  w.bases = (ge_p3*)p;
-  p += al256(n * EdCfg::kRows * sizeof(ge_p3));
-  w.ec = (EcKeyPrep*)p;
-  return w;
+size_t keyprep_bytes(uint32_t n_keys) { return key_ws_bytes(n_keys); }
+size_t item_ws_bytes(uint64_t n_items) { return (size_t)(n_items ? n_items : 1) * ITEM_SLOT; }
+size_t btab_bytes() { return const_tab_bytes(); }
+
+hipError_t init_btab(void* d_btab, hipStream_t stream) {
+  hipError_t e = ed_init_const(d_btab, stream);
+  if (e != hipSuccess) return e;
+  return ec_init_const(d_btab, stream);
 }
-size_t keyprep_bytes(uint32_t n_keys) {
-  const size_t n = n_keys ? n_keys : 1;
-  return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(EdTab)) + al256(n * EdCfg::kRows * sizeof(ge_p3)) +
-         n * sizeof(EcKeyPrep);
-}
-size_t item_ws_bytes(uint64_t n_items) { return (size_t)(n_items ? n_items : 1) * sizeof(ge_p2); }
 
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream) {
   if (n_keys == 0) return hipSuccess;
-  const uint32_t B = 64;  // one wave per block: keys are few, spread them over CUs
-  const dim3 g((n_keys + B - 1) / B);
-  KeyWs w = key_ws(d_keyprep, n_keys);
-  hipLaunchKernelGGL(k_ed_keyprep_rows, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.hdr, w.bases);
-  const uint32_t lanes = n_keys * EdCfg::kRows * (EdCfg::kMult / 8);
-  hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((lanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
-                     w.bases, w.tab);
-  hipLaunchKernelGGL(k_ec_keyprep<CG_CURVE_R1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.ec);
-  hipLaunchKernelGGL(k_ec_keyprep<CG_CURVE_K1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.ec);
-  return hipGetLastError();
-}
-
-size_t btab_bytes() { return sizeof(EdTab); }
-hipError_t init_btab(void* d_btab, hipStream_t stream) {
-  hipLaunchKernelGGL(k_ed_btab_init, dim3(1), dim3(64), 0, stream, (EdTab*)d_btab);
+  const KeyWs w = key_ws(d_keyprep, n_keys);
+  ed_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, stream);
+  ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, stream);
   return hipGetLastError();
 }
 
@@ -414,18 +56,13 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
   if (n_items == 0) return hipSuccess;
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
-  KeyWs w = key_ws((void*)d_keyprep, n_keys);
+  const KeyWs w = key_ws((void*)d_keyprep, n_keys);
   hipLaunchKernelGGL(k_misc_status, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
                      d_status);
-  hipLaunchKernelGGL(k_ed_verify, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys, w.hdr,
-                     w.tab, (const EdTab*)d_btab, d_arena, arena_len, mode, d_status, (ge_p2*)d_item_ws);
-  const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
-  hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, n_items, d_arena, arena_len,
-                     d_status, (const ge_p2*)d_item_ws);
-  hipLaunchKernelGGL(k_ec_verify<CG_CURVE_R1>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys,
-                     n_keys, w.ec, d_arena, arena_len, mode, d_status);
-  hipLaunchKernelGGL(k_ec_verify<CG_CURVE_K1>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys,
-                     n_keys, w.ec, d_arena, arena_len, mode, d_status);
+  ed_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_item_ws, d_btab,
+                  stream);
+  ec_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_item_ws, d_btab,
+                  stream);
   return hipGetLastError();
 }
 

@@ -1,0 +1,184 @@
+// ECDSA (SHA256withECDSA) verification kernels on secp256r1 / secp256k1, BouncyCastle 1.57
+// semantics (ecdsa.h header comment).
+//   k_ec_keyprep_rows  one lane per ECDSA key: decode + validate Q, row bases 2^{24j} Q
+//   k_ec_keyprep_tab   one lane per (key, row): 32 affine multiples, one batched inversion
+//   k_ec_prep          one lane per item: DER, range checks, SHA-256, e mod n
+//   k_ec_inv           16 items per lane: one shared inversion of s mod n -> u1, u2
+//   k_ec_ladder        one lane per item: u1 G + u2 Q over the row tables (G rows in LDS),
+//                      BC's inversion-free x(R) == r check
+// Replaces, per item, BC DSABase.engineVerify behind Crypto.isValid
+// (core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559, schemes :92-117).
+#include "keyws.h"
+
+namespace cg {
+
+__constant__ EcConsts c_ec[2];  // [CG_CURVE_K1], [CG_CURVE_R1]
+
+#define EC_INV_K 16
+
+template <int C>
+__device__ __forceinline__ uint8_t ec_scheme() {
+  return C == CG_CURVE_R1 ? CG_ECDSA_SECP256R1_SHA256 : CG_ECDSA_SECP256K1_SHA256;
+}
+
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_keyprep_rows(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                        const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                        EdKeyHdr* __restrict__ hdr, BaseSlot* __restrict__ bases) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_keys) return;
+  const cg_key k = keys[i];
+  if (k.scheme != ec_scheme<C>()) return;
+  EdKeyHdr h;
+  for (int w = 0; w < 7; ++w) h.pad[w] = 0;
+  for (int w = 0; w < 8; ++w) h.abyte[w] = 0;
+  h.status = CG_KEY_INVALID;
+  if (in_arena(k.off, k.len, arena_len)) {
+    u256w xm, ym;
+    if (ec_key_decode_bytes<C>(xm, ym, arena, round4(arena_len), k.off, k.len, k.fmt, c_ec[C]) == 0) {
+      h.status = 0;
+      Jac b[EC_ROWS];
+      ec_row_bases<C>(b, xm, ym, c_ec[C]);
+      for (int j = 0; j < EC_ROWS; ++j) bases[(size_t)i * EC_ROWS + j].ec = b[j];
+    }
+  }
+  hdr[i] = h;
+}
+
+// one lane per (key, row)
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_keyprep_tab(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                       const EdKeyHdr* __restrict__ hdr,
+                                                       const BaseSlot* __restrict__ bases, TabSlot* __restrict__ tabs,
+                                                       EcRowScratch* __restrict__ scratch) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = g / EC_ROWS, j = g % EC_ROWS;
+  if (i >= n_keys) return;
+  if (keys[i].scheme != ec_scheme<C>() || hdr[i].status != 0) return;
+  ec_row_build<C>(tabs[i].ec.t[j], bases[g].ec, scratch[g], c_ec[C]);
+}
+
+template <int C>
+__global__ void k_ec_grows_init(EcRowTab* __restrict__ out, EcRowScratch* __restrict__ scratch) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  ec_g_rows_init<C>(*out, *scratch, c_ec[C]);
+}
+
+template <int C>
+__global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ items, uint64_t n_items,
+                                                 const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                 const EdKeyHdr* __restrict__ hdr,
+                                                 const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                 uint32_t mode, uint8_t* __restrict__ status,
+                                                 EcItemWs* __restrict__ ws) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items) return;
+  const cg_item it = items[i];
+  if (it.key_idx >= n_keys) return;
+  if (keys[it.key_idx].scheme != ec_scheme<C>()) return;
+  uint8_t st;
+  if (hdr[it.key_idx].status != 0) {
+    st = CG_KEY_INVALID;
+  } else if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
+    st = CG_EMPTY;
+  } else if (!in_arena(it.sig_off, it.sig_len, arena_len) || !in_arena(it.msg_off, it.msg_len, arena_len)) {
+    st = CG_NOT_RUN;
+  } else {
+    EcItemWs w;
+    const uint32_t r = ecdsa_prep<C>(w, arena, round4(arena_len), it.sig_off, it.sig_len, it.msg_off, it.msg_len);
+    if (r == 0) {
+      ws[i] = w;
+      st = (uint8_t)(EC_PENDING_BASE + C);
+    } else {
+      st = (uint8_t)r;
+    }
+  }
+  status[i] = st;
+}
+
+template <int C>
+__global__ void __launch_bounds__(256) k_ec_inv(uint64_t n_items, const uint8_t* __restrict__ status,
+                                                EcItemWs* __restrict__ ws) {
+  const uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * EC_INV_K;
+  if (base >= n_items) return;
+  const uint32_t cnt = (uint32_t)((n_items - base) < EC_INV_K ? (n_items - base) : EC_INV_K);
+  uint32_t sel = 0;
+  for (uint32_t k = 0; k < cnt; ++k) sel |= (uint32_t)(status[base + k] == EC_PENDING_BASE + C) << k;
+  if (!sel) return;
+  ecdsa_batch_inv<C, EC_INV_K>(ws + base, cnt, sel, c_ec[C]);
+}
+
+template <int C>
+__global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ items, uint64_t n_items,
+                                                   const TabSlot* __restrict__ tabs,
+                                                   const EcRowTab* __restrict__ gtab, uint8_t* __restrict__ status,
+                                                   const EcItemWs* __restrict__ ws) {
+  __shared__ EcRowTab sG;
+  {
+    const uint4* src = (const uint4*)gtab;
+    uint4* dst = (uint4*)&sG;
+    for (uint32_t w = threadIdx.x; w < sizeof(EcRowTab) / 16; w += blockDim.x) dst[w] = src[w];
+  }
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items) return;
+  if (status[i] != EC_PENDING_BASE + C) return;
+  const EcItemWs w = ws[i];
+  status[i] = (uint8_t)ecdsa_ladder_check<C>(w.a, w.b, w.r, sG, tabs[items[i].key_idx].ec, c_ec[C]);
+}
+
+hipError_t ec_upload_constants() {
+  EcConsts k[2];
+  ec_consts_init<CG_CURVE_K1>(k[CG_CURVE_K1]);
+  ec_consts_init<CG_CURVE_R1>(k[CG_CURVE_R1]);
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_ec), k, sizeof k, 0, hipMemcpyHostToDevice);
+}
+
+hipError_t ec_init_const(void* d_btab, hipStream_t stream) {
+  hipLaunchKernelGGL(k_ec_grows_init<CG_CURVE_K1>, dim3(1), dim3(64), 0, stream,
+                     (EcRowTab*)gtab(d_btab, CG_CURVE_K1), const_scratch(d_btab));
+  hipLaunchKernelGGL(k_ec_grows_init<CG_CURVE_R1>, dim3(1), dim3(64), 0, stream,
+                     (EcRowTab*)gtab(d_btab, CG_CURVE_R1), const_scratch(d_btab));
+  return hipGetLastError();
+}
+
+void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                       const KeyWs& w, hipStream_t stream) {
+  const uint32_t B = 64;
+  const dim3 g((n_keys + B - 1) / B);
+  hipLaunchKernelGGL(k_ec_keyprep_rows<CG_CURVE_R1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len,
+                     w.hdr, w.bases);
+  hipLaunchKernelGGL(k_ec_keyprep_rows<CG_CURVE_K1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len,
+                     w.hdr, w.bases);
+  const uint32_t elanes = n_keys * EC_ROWS;
+  hipLaunchKernelGGL(k_ec_keyprep_tab<CG_CURVE_R1>, dim3((elanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys,
+                     w.hdr, w.bases, w.tab, w.ecs);
+  hipLaunchKernelGGL(k_ec_keyprep_tab<CG_CURVE_K1>, dim3((elanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys,
+                     w.hdr, w.bases, w.tab, w.ecs);
+}
+
+template <int C>
+static void launch_curve(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
+                         const KeyWs& w, void* d_item_ws, const void* d_btab, hipStream_t stream) {
+  const uint32_t B = 256;
+  const uint64_t grid = (n_items + B - 1) / B;
+  EcItemWs* ws = (EcItemWs*)d_item_ws;
+  hipLaunchKernelGGL(k_ec_prep<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys, w.hdr,
+                     d_arena, arena_len, mode, d_status, ws);
+  const uint64_t igrid = (n_items + (uint64_t)B * EC_INV_K - 1) / ((uint64_t)B * EC_INV_K);
+  hipLaunchKernelGGL(k_ec_inv<C>, dim3((unsigned)igrid), dim3(B), 0, stream, n_items, (const uint8_t*)d_status, ws);
+  hipLaunchKernelGGL(k_ec_ladder<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, w.tab,
+                     gtab(d_btab, C), d_status, (const EcItemWs*)ws);
+}
+
+void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                     const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
+                     void* d_item_ws, const void* d_btab, hipStream_t stream) {
+  launch_curve<CG_CURVE_R1>(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_item_ws,
+                            d_btab, stream);
+  launch_curve<CG_CURVE_K1>(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_item_ws,
+                            d_btab, stream);
+}
+
+}  // namespace cg

@@ -1,0 +1,290 @@
+// Ed25519 (EDDSA_ED25519_SHA512) verification kernels, i2p 0.2.0 semantics.
+//   k_ed_keyprep_rows  one lane per distinct key: decode A, canonical Abyte, row bases
+//                      2^{24j} (-A), j = 0..10
+//   k_ed_keyprep_tab   one lane per (key, row, 8 multiples): affine multiples of the row base
+//   k_ed_verify        one lane per item: SHA-512 challenge, scalar prep, 4 windows
+//                      x (11 rows of -A + 11 rows of B) mixed additions, 18 doublings
+//   k_ed_finish        16 items per lane: batch inversion, encode, byte compare
+// Replaces, per item, i2p EdDSAEngine.engineVerify behind Crypto.isValid
+// (core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559, scheme :120-133).
+#include "keyws.h"
+
+namespace cg {
+
+__constant__ Ed25519Consts c_ed;
+
+static const uint8_t ED_SPKI_PREFIX[12] = {0x30, 0x2a, 0x30, 0x05, 0x06, 0x03, 0x2b, 0x65, 0x70, 0x03, 0x21, 0x00};
+
+__global__ void __launch_bounds__(64) k_ed_keyprep_rows(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                        const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                        EdKeyHdr* __restrict__ hdr, BaseSlot* __restrict__ bases) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_keys) return;
+  const cg_key k = keys[i];
+  if (k.scheme != CG_EDDSA_ED25519_SHA512) return;
+  const uint64_t lr = round4(arena_len);
+  uint64_t a_off = k.off;
+  bool ok = in_arena(k.off, k.len, arena_len);
+  if (ok && k.fmt == CG_KEY_RAW) {
+    ok = k.len == 32;
+  } else if (ok && k.fmt == CG_KEY_SPKI) {
+    ok = k.len == 44;
+    for (int b = 0; ok && b < 12; ++b) ok = (cg_ld_bytes4(arena, lr, k.off + b) & 0xffu) == ED_SPKI_PREFIX[b];
+    a_off = k.off + 12;
+  } else {
+    ok = false;
+  }
+  EdKeyHdr h;
+  for (int w = 0; w < 7; ++w) h.pad[w] = 0;
+  for (int w = 0; w < 8; ++w) h.abyte[w] = 0;
+  h.status = CG_KEY_INVALID;
+  if (ok) {
+    uint32_t aw[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) aw[w] = cg_ld_bytes4(arena, lr, a_off + 4 * w);
+    ge_p3 A;
+    if (ed_decode_point(A, aw, c_ed) == ED_ST_VALID) {
+      h.status = 0;
+      ed_encode_affine(h.abyte, A.X, A.Y, A.Z);
+      ge_p3 P;
+      ed_neg_point(P, A);
+      for (int j = 0; j < EdCfg::kRows; ++j) {
+        bases[(size_t)i * EdCfg::kRows + j].ed = P;
+        if (j + 1 < EdCfg::kRows) ed_dbl_n(P, P, ED_W * ED_K);
+      }
+    }
+  }
+  hdr[i] = h;
+}
+
+// m * P for a small m >= 1 (double-and-add, MSB first)
+__device__ void ed_small_mul(ge_p3& R, const ge_p3& P, uint32_t m) {
+  ge_cached c;
+  ge_p3_to_cached(c, P, c_ed.d2);
+  R = P;
+  ge_p1p1 t;
+  int top = 31 - __builtin_clz(m);
+  for (int b = top - 1; b >= 0; --b) {
+    ge_p3_dbl(t, R);
+    ge_p1p1_to_p3(R, t);
+    if ((m >> b) & 1u) {
+      ge_add_cached(t, R, c);
+      ge_p1p1_to_p3(R, t);
+    }
+  }
+}
+
+// one lane per (key, row, group of 8 multiples)
+__global__ void __launch_bounds__(64) k_ed_keyprep_tab(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                       const EdKeyHdr* __restrict__ hdr,
+                                                       const BaseSlot* __restrict__ bases,
+                                                       TabSlot* __restrict__ tabs) {
+  constexpr uint32_t G = EdCfg::kMult / 8;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = g / (EdCfg::kRows * G);
+  const uint32_t rem = g % (EdCfg::kRows * G);
+  const uint32_t j = rem / G, grp = rem % G;
+  if (i >= n_keys) return;
+  if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || hdr[i].status != 0) return;
+  const ge_p3 P = bases[(size_t)i * EdCfg::kRows + j].ed;
+  ge_p3 pts[8];
+  ed_small_mul(pts[0], P, 8 * grp + 1);
+  ge_cached c;
+  ge_p3_to_cached(c, P, c_ed.d2);
+  ge_p1p1 t;
+  for (int k = 1; k < 8; ++k) {
+    ge_add_cached(t, pts[k - 1], c);
+    ge_p1p1_to_p3(pts[k], t);
+  }
+  ge_niels row[8];
+  ed_niels_batch8(row, pts, c_ed.d2);
+  for (int k = 0; k < 8; ++k) tabs[i].ed.t[j][8 * grp + k] = row[k];
+}
+
+// B rows, built once per context by the same code
+__global__ void k_ed_btab_init(EdTab* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  ge_p3 B;
+  fe x, y, two_inv, t;
+  fe_sub(x, c_ed.Btab[1].ypx, c_ed.Btab[1].ymx);
+  fe_add(y, c_ed.Btab[1].ypx, c_ed.Btab[1].ymx);
+  fe_0(t);
+  t.v[0] = 2;
+  fe_invert(two_inv, t);
+  fe_mul(B.X, x, two_inv);
+  fe_mul(B.Y, y, two_inv);
+  fe_1(B.Z);
+  fe_mul(B.T, B.X, B.Y);
+  ed_rows_w_init<ED_W, ED_K>(*out, B, c_ed.d2);
+}
+
+
+__device__ __forceinline__ void ld_niels(ge_niels& n, const ge_niels* src) {
+  const uint4* p = (const uint4*)src;
+  uint32_t* d = (uint32_t*)&n;
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    const uint4 v = p[q];
+    d[4 * q] = v.x;
+    d[4 * q + 1] = v.y;
+    d[4 * q + 2] = v.z;
+    d[4 * q + 3] = v.w;
+  }
+  const uint2 v = ((const uint2*)src)[14];
+  d[28] = v.x;
+  d[29] = v.y;
+}
+
+__device__ __forceinline__ void pick(ge_niels& out, const ge_niels* row, int d) {
+  const int a = d < 0 ? -d : d;
+  ld_niels(out, row + (a > 0 ? a - 1 : 0));
+  if (a == 0) ge_niels_identity(out);
+  ge_niels_cneg(out, d < 0);
+}
+
+__global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ items, uint64_t n_items,
+                                                   const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                   const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs,
+                                                   const EdTab* __restrict__ btab,
+                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   uint32_t mode, uint8_t* __restrict__ status,
+                                                   ge_p2* __restrict__ rout) {
+  __shared__ EdTab sB;
+  {
+    const uint4* src = (const uint4*)btab;
+    uint4* dst = (uint4*)&sB;
+    for (uint32_t w = threadIdx.x; w < sizeof(EdTab) / 16; w += blockDim.x) dst[w] = src[w];
+  }
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items) return;
+  const cg_item it = items[i];
+  if (it.key_idx >= n_keys) return;
+  if (keys[it.key_idx].scheme != CG_EDDSA_ED25519_SHA512) return;
+  const EdKeyHdr* kh = hdr + it.key_idx;
+  uint8_t st;
+  if (kh->status != 0) {
+    st = CG_KEY_INVALID;
+  } else if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
+    st = CG_EMPTY;
+  } else if (!in_arena(it.sig_off, it.sig_len, arena_len) || !in_arena(it.msg_off, it.msg_len, arena_len)) {
+    st = CG_NOT_RUN;
+  } else if (it.sig_len != 64) {
+    st = CG_SIG_MALFORMED;
+  } else {
+    const uint64_t lr = round4(arena_len);
+    uint32_t sw[16], ab[8];
+#pragma unroll
+    for (int w = 0; w < 16; ++w) sw[w] = cg_ld_bytes4(arena, lr, it.sig_off + 4 * w);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) ab[w] = kh->abyte[w];
+    // h = SHA-512(R || Abyte || M) mod L ; S' = slide value of S mod L
+    uint32_t pre[16], hw[16], h[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      pre[w] = sw[w];
+      pre[8 + w] = ab[w];
+    }
+    sha512_prefix64_msg(hw, pre, arena, lr, it.msg_off, it.msg_len);
+    sc_reduce512(h, hw);
+    uint32_t s[8], sr[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) s[w] = sw[8 + w];
+    sc_reduce256(sr, s);
+    if (s[7] >> 31) {
+      if (sc_slide_escapes(s)) {
+        uint32_t r1[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) r1[w] = sc_R1w(w);
+        sc_sub(sr, sr, r1);
+      }
+    }
+    uint32_t eh[EdCfg::kPackedWords], es[EdCfg::kPackedWords];
+    sc_recode_w<ED_W>(eh, EdCfg::kPackedWords, h);
+    sc_recode_w<ED_W>(es, EdCfg::kPackedWords, sr);
+    ge_p2 q;
+    ed_double_scalar_w<ED_W, ED_K>(q, eh, es, tabs[it.key_idx].ed, sB);
+    rout[i] = q;
+    st = (uint8_t)ED_PENDING;
+  }
+  status[i] = st;
+}
+
+// Encode + compare for 16 consecutive items per lane: one inversion per lane (Montgomery's
+// trick) instead of one per item.
+#define ED_FINISH_K 16
+__global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ items, uint64_t n_items,
+                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   uint8_t* __restrict__ status, const ge_p2* __restrict__ rin) {
+  const uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * ED_FINISH_K;
+  if (base >= n_items) return;
+  const uint32_t cnt = (uint32_t)((n_items - base) < ED_FINISH_K ? (n_items - base) : ED_FINISH_K);
+  fe acc[ED_FINISH_K];
+  fe run;
+  fe_1(run);
+  uint32_t pend = 0;
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const bool p = status[base + k] == ED_PENDING;
+    pend |= (uint32_t)p << k;
+    if (p) {
+      fe_mul(run, run, rin[base + k].Z);
+    }
+    fe_copy(acc[k], run);
+  }
+  if (!pend) return;
+  fe inv;
+  fe_invert(inv, run);
+  const uint64_t lr = round4(arena_len);
+  for (int k = (int)cnt - 1; k >= 0; --k) {
+    if (!((pend >> k) & 1u)) continue;
+    fe zi, t;
+    // acc[k] = prod of pending Z up to k; inv = 1 / acc[k]
+    int prev = k - 1;
+    while (prev >= 0 && !((pend >> prev) & 1u)) --prev;
+    if (prev >= 0) fe_mul(zi, inv, acc[prev]);
+    else fe_copy(zi, inv);
+    fe_mul(t, inv, rin[base + k].Z);
+    fe_copy(inv, t);
+    const ge_p2 P = rin[base + k];
+    uint32_t rw[8];
+    const uint64_t so = items[base + k].sig_off;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) rw[w] = cg_ld_bytes4(arena, lr, so + 4 * w);
+    status[base + k] = (uint8_t)ed_encode_cmp(P, zi, rw);
+  }
+}
+
+hipError_t ed_upload_constants() {
+  Ed25519Consts h;
+  ed_consts_init(h);
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_ed), &h, sizeof h, 0, hipMemcpyHostToDevice);
+}
+
+hipError_t ed_init_const(void* d_btab, hipStream_t stream) {
+  hipLaunchKernelGGL(k_ed_btab_init, dim3(1), dim3(64), 0, stream, (EdTab*)d_btab);
+  return hipGetLastError();
+}
+
+void ed_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                       const KeyWs& w, hipStream_t stream) {
+  const uint32_t B = 64;  // one wave per block: keys are few, spread them over CUs
+  hipLaunchKernelGGL(k_ed_keyprep_rows, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, d_arena,
+                     arena_len, w.hdr, w.bases);
+  const uint32_t lanes = n_keys * EdCfg::kRows * (EdCfg::kMult / 8);
+  hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((lanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
+                     w.bases, w.tab);
+}
+
+void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                     const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
+                     void* d_item_ws, const void* d_btab, hipStream_t stream) {
+  const uint32_t B = 256;
+  const uint64_t grid = (n_items + B - 1) / B;
+  hipLaunchKernelGGL(k_ed_verify, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys, w.hdr,
+                     w.tab, (const EdTab*)d_btab, d_arena, arena_len, mode, d_status, (ge_p2*)d_item_ws);
+  const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
+  hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, n_items, d_arena, arena_len,
+                     d_status, (const ge_p2*)d_item_ws);
+}
+
+}  // namespace cg

@@ -290,3 +290,38 @@ extern "C" int t_ed_count_w6(const uint32_t* aw, const uint32_t* sw, const uint8
   return -1;
 #endif
 }
+
+// ---------------------------------------------------------------- ECDSA rows (v2 pipeline)
+#include "../../corda_amd/csrc/ecdsa_rows.h"
+template <int C>
+static int ecdsa_rows_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off, uint32_t key_len, uint32_t fmt,
+                             uint64_t sig_off, uint32_t sig_len, uint64_t msg_off, uint64_t msg_len) {
+  kinit();
+  const EcConsts& K = g_K[C];
+  static EcRowTab* TG[2] = {nullptr, nullptr};
+  static EcRowTab* TQ = new EcRowTab;
+  static EcRowScratch* S = new EcRowScratch;
+  if (!TG[C]) {
+    TG[C] = new EcRowTab;
+    ec_g_rows_init<C>(*TG[C], *S, K);
+  }
+  u256w xm, ym;
+  uint32_t st = ec_key_decode_bytes<C>(xm, ym, arena, lr, key_off, key_len, fmt, K);
+  if (st) return (int)st;
+  Jac bases[EC_ROWS];
+  ec_row_bases<C>(bases, xm, ym, K);
+  for (int j = 0; j < EC_ROWS; ++j) ec_row_build<C>(TQ->t[j], bases[j], *S, K);
+  EcItemWs ws;
+  st = ecdsa_prep<C>(ws, arena, lr, sig_off, sig_len, msg_off, msg_len);
+  if (st) return (int)st;
+  ecdsa_batch_inv<C, 1>(&ws, 1, 1u, K);
+  return (int)ecdsa_ladder_check<C>(ws.a, ws.b, ws.r, *TG[C], *TQ, K);
+}
+extern "C" int t_ecdsa_verify_rows(int scheme, const uint8_t* arena, uint64_t arena_len, uint64_t key_off,
+                                   uint32_t key_len, uint32_t fmt, uint64_t sig_off, uint32_t sig_len,
+                                   uint64_t msg_off, uint64_t msg_len) {
+  const uint64_t lr = (arena_len + 3) & ~3ull;
+  if (scheme == 3)
+    return ecdsa_rows_verify<CG_CURVE_R1>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len);
+  return ecdsa_rows_verify<CG_CURVE_K1>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len);
+}

@@ -158,3 +158,23 @@ def test_executed_work_constants_match_lane_code():
     assert (mul_v, sq_v) == bench.ED_VERIFY_FE, (mul_v, sq_v)
     assert (mul_f, sq_f) == bench.ED_FINISH_FE, (mul_f, sq_f)
     assert (mul_i, sq_i) == bench.ED_INVERT_FE, (mul_i, sq_i)
+
+
+@pytest.mark.parametrize("fn", ["t_ecdsa_verify", "t_ecdsa_verify_rows"])
+def test_ecdsa_lane_verify_on_fixtures(fn):
+    """ECDSA lane code (the fixed-window core and the row-table pipeline: prep -> batched
+    inverse -> ladder + x-check) on every ECDSA fixture, isValid semantics."""
+    lib = hostk.lib()
+    f = getattr(lib, fn)
+    names = {0: "VALID", 1: "INVALID", 2: "SIG_MALFORMED", 3: "KEY_INVALID"}
+    n = 0
+    for it in golden_io.load("ecdsa.json"):
+        key, sig, msg = bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"])
+        if it["scheme"] not in (2, 3):
+            continue
+        arena = np.frombuffer(key + sig + msg + bytes(8), dtype=np.uint8).copy()
+        st = f(it["scheme"], ptr(arena), len(key) + len(sig) + len(msg), 0, len(key), it["key_fmt"], len(key),
+               len(sig), len(key) + len(sig), len(msg))
+        assert names[st] == it["expect_isvalid"], (it["class"], it["note"])
+        n += 1
+    assert n > 300

@@ -1,8 +1,8 @@
 """Batch layout shared by the host mirror, tests and bench: numpy views of the C ABI structs.
 
-``KEY_DTYPE`` / ``ITEM_DTYPE`` / ``SPAN_DTYPE`` / ``COMPONENT_DTYPE`` / ``TX_DTYPE`` are
-byte-for-byte ``cg_key`` / ``cg_item`` / ``cg_span`` / ``cg_component`` / ``cg_tx`` of
-include/cordagpu.h. ``BatchBuilder`` packs (key, sig, clear) triples the way a JVM
+``KEY_DTYPE`` / ``ITEM_DTYPE`` / ``SPAN_DTYPE`` / ``COMPONENT_DTYPE`` / ``TX_DTYPE`` /
+``TXSIG_DTYPE`` / ``TMPL_DTYPE`` are byte-for-byte ``cg_key`` / ``cg_item`` / ``cg_span`` /
+``cg_component`` / ``cg_tx`` / ``cg_txsig`` / ``cg_signable_tmpl`` of include/cordagpu.h. ``BatchBuilder`` packs (key, sig, clear) triples the way a JVM
 caller of ``Crypto.verifyBatch`` would: each distinct PublicKey object once in the key
 table (as TransactionSignature.by references it), signatures and clear data appended to
 one arena.
@@ -15,6 +15,10 @@ ITEM_DTYPE = np.dtype([("sig_off", "<u8"), ("msg_off", "<u8"), ("msg_len", "<u4"
 SPAN_DTYPE = np.dtype([("off", "<u8"), ("len", "<u8")])
 COMPONENT_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("flags", "<u4")])
 TX_DTYPE = np.dtype([("first", "<u8"), ("n", "<u4"), ("reserved", "<u4"), ("salt_off", "<u8")])
+TXSIG_DTYPE = np.dtype([("sig_off", "<u8"), ("tx_idx", "<u4"), ("key_idx", "<u4"), ("sig_len", "<u2"),
+                        ("tmpl", "<u2"), ("reserved", "<u4")])
+TMPL_DTYPE = np.dtype([("prefix_off", "<u8"), ("suffix_off", "<u8"), ("prefix_len", "<u4"), ("suffix_len", "<u4")])
+assert TXSIG_DTYPE.itemsize == 24 and TMPL_DTYPE.itemsize == 24
 assert KEY_DTYPE.itemsize == 16 and ITEM_DTYPE.itemsize == 32 and SPAN_DTYPE.itemsize == 16
 assert COMPONENT_DTYPE.itemsize == 16 and TX_DTYPE.itemsize == 24
 

@@ -67,6 +67,8 @@ struct cg_ctx {
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
+  // transaction pipeline: verify items, spliced messages, templates; host-entry staging
+  DevBuf txitems, msgs, tmpls, h_txs, h_comps, h_sigs, h_ids, h_txst;
 };
 
 extern "C" {
@@ -133,6 +135,8 @@ void cg_close(cg_ctx* c) {
   c->aux0.release();
   c->aux1.release();
   c->aux2.release();
+  for (DevBuf* b : {&c->txitems, &c->msgs, &c->tmpls, &c->h_txs, &c->h_comps, &c->h_sigs, &c->h_ids, &c->h_txst})
+    b->release();
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -375,6 +379,113 @@ int cg_merkle_roots(cg_ctx* c, const uint8_t* leaves, const uint64_t* first, con
           "launch_merkle_roots");
   HIP_TRY(hipMemcpyAsync(roots_out, c->aux0.p, 32 * n, hipMemcpyDeviceToHost, s), "D2H roots");
   HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n, hipMemcpyDeviceToHost, s), "D2H status");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  return CG_OK;
+}
+
+// cg_verify_transactions_device with the ctx lock held
+static int verify_transactions_locked(cg_ctx* c, const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps,
+                                      uint64_t n_comps, const cg_key* d_keys, uint32_t n_keys, const cg_txsig* d_sigs,
+                                      uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,
+                                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_ids,
+                                      uint8_t* d_tx_status, uint8_t* d_sig_status, hipStream_t s) {
+  uint64_t maxlen = 0;
+  for (uint32_t k = 0; k < n_tmpls; ++k) {
+    const uint64_t l = (uint64_t)tmpls[k].prefix_len + 32u + tmpls[k].suffix_len;
+    if (l > maxlen) maxlen = l;
+  }
+  uint64_t slot = (maxlen + 15) & ~(uint64_t)15;
+  if (slot == 0) slot = 16;
+  const size_t need_leaf = 32 * (n_comps ? n_comps : 1), need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1),
+               need_msgs = slot * (n_sigs ? n_sigs : 1), need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
+  if (c->aux2.cap < need_leaf || c->txitems.cap < need_items || c->msgs.cap < need_msgs ||
+      c->tmpls.cap < need_tmpl || c->keyprep.cap < cg::keyprep_bytes(n_keys) ||
+      c->itemws.cap < cg::item_ws_bytes(n_sigs)) {
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    HIP_TRY(c->aux2.ensure(need_leaf), "hipMalloc(leaf ws)");
+    HIP_TRY(c->txitems.ensure(need_items), "hipMalloc(tx items)");
+    HIP_TRY(c->msgs.ensure(need_msgs), "hipMalloc(spliced messages)");
+    HIP_TRY(c->tmpls.ensure(need_tmpl), "hipMalloc(templates)");
+    HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
+    HIP_TRY(c->itemws.ensure(cg::item_ws_bytes(n_sigs)), "hipMalloc(item workspace)");
+  }
+  if (n_tmpls)
+    HIP_TRY(hipMemcpyAsync(c->tmpls.p, tmpls, sizeof(cg_signable_tmpl) * n_tmpls, hipMemcpyHostToDevice, s),
+            "H2D templates");
+  HIP_TRY(cg::launch_tx_ids(d_txs, n_tx, d_comps, n_comps, d_arena, arena_len, d_ids, d_tx_status,
+                            (uint8_t*)c->aux2.p, s), "launch_tx_ids");
+  if (n_sigs == 0) return CG_OK;
+  HIP_TRY(cg::launch_tx_sig_items(d_sigs, n_sigs, (const cg_signable_tmpl*)c->tmpls.p, n_tmpls, d_tx_status, n_tx,
+                                  d_ids, d_arena, arena_len, slot, (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s),
+          "launch_tx_sig_items");
+  HIP_TRY(cg::launch_verify(d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode,
+                            d_sig_status, c->keyprep.p, c->itemws.p, c->btab.p, s, (const uint8_t*)c->msgs.p,
+                            slot * n_sigs),
+          "launch_verify");
+  return CG_OK;
+}
+
+int cg_verify_transactions_device(cg_ctx* c, const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps,
+                                  uint64_t n_comps, const cg_key* d_keys, uint32_t n_keys, const cg_txsig* d_sigs,
+                                  uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,
+                                  const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_ids,
+                                  uint8_t* d_tx_status, uint8_t* d_sig_status, void* hip_stream) {
+  if (!c) return fail(CG_ERR_ARG, "cg_verify_transactions_device: ctx is NULL");
+  if (n_tx && (!d_txs || !d_ids || !d_tx_status)) return fail(CG_ERR_ARG, "cg_verify_transactions_device: NULL tx buffer");
+  if (n_sigs && (!d_sigs || !d_sig_status)) return fail(CG_ERR_ARG, "cg_verify_transactions_device: NULL sig buffer");
+  if (n_tmpls && !tmpls) return fail(CG_ERR_ARG, "cg_verify_transactions_device: templates is NULL");
+  if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_verify_transactions_device: bad mode");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  return verify_transactions_locked(c, d_txs, n_tx, d_comps, n_comps, d_keys, n_keys, d_sigs, n_sigs, tmpls, n_tmpls,
+                                    d_arena, arena_len, mode, d_ids, d_tx_status, d_sig_status, s);
+}
+
+int cg_verify_transactions(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_component* comps, uint64_t n_comps,
+                           const cg_key* keys, uint32_t n_keys, const cg_txsig* sigs, uint64_t n_sigs,
+                           const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
+                           uint64_t arena_len, uint32_t mode, uint8_t* ids_out, uint8_t* tx_status_out,
+                           uint8_t* sig_status_out) {
+  if (!c) return fail(CG_ERR_ARG, "cg_verify_transactions: ctx is NULL");
+  if (n_tx && (!txs || !ids_out || !tx_status_out)) return fail(CG_ERR_ARG, "cg_verify_transactions: NULL tx buffer");
+  if (n_sigs && (!sigs || !sig_status_out)) return fail(CG_ERR_ARG, "cg_verify_transactions: NULL sig buffer");
+  if (n_comps && !comps) return fail(CG_ERR_ARG, "cg_verify_transactions: comps is NULL");
+  if (n_keys && !keys) return fail(CG_ERR_ARG, "cg_verify_transactions: keys is NULL");
+  if (n_tmpls && !tmpls) return fail(CG_ERR_ARG, "cg_verify_transactions: templates is NULL");
+  if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_verify_transactions: arena is NULL");
+  if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_verify_transactions: bad mode");
+  for (uint64_t i = 0; i < n_sigs; ++i) sig_status_out[i] = CG_NOT_RUN;
+  if (n_tx == 0 && n_sigs == 0) return CG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  HIP_TRY(c->h_txs.ensure(sizeof(cg_tx) * (n_tx ? n_tx : 1)), "hipMalloc(txs)");
+  HIP_TRY(c->h_comps.ensure(sizeof(cg_component) * (n_comps ? n_comps : 1)), "hipMalloc(comps)");
+  HIP_TRY(c->keys.ensure(sizeof(cg_key) * (n_keys ? n_keys : 1)), "hipMalloc(keys)");
+  HIP_TRY(c->h_sigs.ensure(sizeof(cg_txsig) * (n_sigs ? n_sigs : 1)), "hipMalloc(sigs)");
+  HIP_TRY(c->arena.ensure(((arena_len + 3) & ~(uint64_t)3) + 16), "hipMalloc(arena)");
+  HIP_TRY(c->h_ids.ensure(32 * (n_tx ? n_tx : 1)), "hipMalloc(ids)");
+  HIP_TRY(c->h_txst.ensure(n_tx ? n_tx : 1), "hipMalloc(tx status)");
+  HIP_TRY(c->status.ensure(n_sigs ? n_sigs : 1), "hipMalloc(sig status)");
+  if (n_tx) HIP_TRY(hipMemcpyAsync(c->h_txs.p, txs, sizeof(cg_tx) * n_tx, hipMemcpyHostToDevice, s), "H2D txs");
+  if (n_comps)
+    HIP_TRY(hipMemcpyAsync(c->h_comps.p, comps, sizeof(cg_component) * n_comps, hipMemcpyHostToDevice, s),
+            "H2D comps");
+  if (n_keys) HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, s), "H2D keys");
+  if (n_sigs)
+    HIP_TRY(hipMemcpyAsync(c->h_sigs.p, sigs, sizeof(cg_txsig) * n_sigs, hipMemcpyHostToDevice, s), "H2D sigs");
+  if (arena_len) HIP_TRY(hipMemcpyAsync(c->arena.p, arena, arena_len, hipMemcpyHostToDevice, s), "H2D arena");
+  int rc = verify_transactions_locked(c, (const cg_tx*)c->h_txs.p, n_tx, (const cg_component*)c->h_comps.p, n_comps,
+                                      (const cg_key*)c->keys.p, n_keys, (const cg_txsig*)c->h_sigs.p, n_sigs, tmpls,
+                                      n_tmpls, (const uint8_t*)c->arena.p, arena_len, mode, (uint8_t*)c->h_ids.p,
+                                      (uint8_t*)c->h_txst.p, (uint8_t*)c->status.p, s);
+  if (rc != CG_OK) return rc;
+  if (n_tx) {
+    HIP_TRY(hipMemcpyAsync(ids_out, c->h_ids.p, 32 * n_tx, hipMemcpyDeviceToHost, s), "D2H ids");
+    HIP_TRY(hipMemcpyAsync(tx_status_out, c->h_txst.p, n_tx, hipMemcpyDeviceToHost, s), "D2H tx status");
+  }
+  if (n_sigs) HIP_TRY(hipMemcpyAsync(sig_status_out, c->status.p, n_sigs, hipMemcpyDeviceToHost, s), "D2H sig status");
   HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
   return CG_OK;
 }

@@ -19,7 +19,8 @@ size_t keyprep_bytes(uint32_t n_keys);
 //   key prep (one lane per key) -> per-scheme verify (one lane per item) -> status bytes.
 hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                          const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                         void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream);
+                         void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
+                         const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0);
 // Constant base-point row table: size and one-time initialisation (per context).
 size_t btab_bytes();
 hipError_t init_btab(void* d_btab, hipStream_t stream);
@@ -27,9 +28,12 @@ hipError_t init_btab(void* d_btab, hipStream_t stream);
 size_t item_ws_bytes(uint64_t n_items);
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream);
+// `d_msgs` (optional): the engine's spliced-message workspace, read by items flagged
+// CG_ITEM_MSG_WS (keyws.h); caller items never carry that flag.
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                        const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream);
+                        const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
+                        const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0);
 
 // Hashing kernels
 hipError_t launch_sha256(const cg_span* d_spans, uint64_t n, const uint8_t* d_arena, uint64_t arena_len,
@@ -42,6 +46,13 @@ hipError_t launch_sha512(const cg_span* d_spans, uint64_t n, const uint8_t* d_ar
 hipError_t launch_tx_ids(const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps, uint64_t n_comps,
                          const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids, uint8_t* d_status,
                          uint8_t* d_leaf_ws, hipStream_t stream);
+
+// Transaction pipeline: per-signature verify items + spliced SignableData messages (one
+// `slot`-byte message slot per signature in d_msgs; slot a multiple of 16).
+hipError_t launch_tx_sig_items(const cg_txsig* d_sigs, uint64_t n_sigs, const cg_signable_tmpl* d_tmpls,
+                               uint32_t n_tmpls, const uint8_t* d_tx_status, uint64_t n_tx, const uint8_t* d_ids,
+                               const uint8_t* d_arena, uint64_t arena_len, uint64_t slot, cg_item* d_items,
+                               uint8_t* d_msgs, hipStream_t stream);
 
 // Merkle roots over independent leaf lists.
 hipError_t launch_merkle_roots(const uint8_t* d_leaves, const uint64_t* d_first, const uint32_t* d_count,

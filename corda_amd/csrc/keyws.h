@@ -17,6 +17,22 @@ __device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t ar
   return off <= arena_len && len <= arena_len - off;
 }
 
+// Item flag (cg_item.reserved0, set only by the engine's own pipelines): the clear data lives
+// in the engine's spliced-message workspace, not in the caller's arena. Launches without that
+// workspace (every caller-facing entry point) pass msgs = nullptr, and the flag is ignored.
+#define CG_ITEM_MSG_WS 1u
+__device__ __forceinline__ bool item_in_ws(const cg_item& it, const uint8_t* msgs) {
+  return (it.reserved0 & CG_ITEM_MSG_WS) && msgs != nullptr;
+}
+__device__ __forceinline__ const uint8_t* item_msg_arena(const cg_item& it, const uint8_t* arena,
+                                                         const uint8_t* msgs) {
+  return item_in_ws(it, msgs) ? msgs : arena;
+}
+__device__ __forceinline__ uint64_t item_msg_len(const cg_item& it, uint64_t arena_len, uint64_t msgs_len,
+                                                 const uint8_t* msgs) {
+  return item_in_ws(it, msgs) ? msgs_len : arena_len;
+}
+
 // Row tables (ed25519_rows.h) with signed radix-64 digits: 43 digits in 11 rows of 4 windows.
 #define ED_W 6
 #define ED_K 4
@@ -97,13 +113,15 @@ void ed_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_a
                        const KeyWs& w, hipStream_t stream);
 void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     void* d_item_ws, const void* d_btab, hipStream_t stream);
+                     const uint8_t* d_msgs, uint64_t msgs_len, void* d_item_ws, const void* d_btab,
+                     hipStream_t stream);
 hipError_t ec_upload_constants();
 hipError_t ec_init_const(void* d_btab, hipStream_t stream);
 void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                        const KeyWs& w, hipStream_t stream);
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     void* d_item_ws, const void* d_btab, hipStream_t stream);
+                     const uint8_t* d_msgs, uint64_t msgs_len, void* d_item_ws, const void* d_btab,
+                     hipStream_t stream);
 
 }  // namespace cg

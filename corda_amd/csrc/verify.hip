@@ -52,28 +52,30 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
 
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                        const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream) {
+                        const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
+                        const uint8_t* d_msgs, uint64_t msgs_len) {
   if (n_items == 0) return hipSuccess;
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
   const KeyWs w = key_ws((void*)d_keyprep, n_keys);
   hipLaunchKernelGGL(k_misc_status, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
                      d_status);
-  ed_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_item_ws, d_btab,
-                  stream);
-  ec_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_item_ws, d_btab,
-                  stream);
+  ed_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len,
+                  d_item_ws, d_btab, stream);
+  ec_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len,
+                  d_item_ws, d_btab, stream);
   return hipGetLastError();
 }
 
 hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                          const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                         void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream) {
+                         void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
+                         const uint8_t* d_msgs, uint64_t msgs_len) {
   if (n_items == 0) return hipSuccess;
   hipError_t e = launch_keyprep(d_keys, n_keys, d_arena, arena_len, d_keyprep, stream);
   if (e != hipSuccess) return e;
   return launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, d_keyprep, d_item_ws,
-                      d_btab, stream);
+                      d_btab, stream, d_msgs, msgs_len);
 }
 
 }  // namespace cg

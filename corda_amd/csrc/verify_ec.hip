@@ -69,6 +69,7 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
                                                  const cg_key* __restrict__ keys, uint32_t n_keys,
                                                  const EdKeyHdr* __restrict__ hdr,
                                                  const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                 const uint8_t* __restrict__ msgs, uint64_t msgs_len,
                                                  uint32_t mode, uint8_t* __restrict__ status,
                                                  EcItemWs* __restrict__ ws) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -81,11 +82,14 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
     st = CG_KEY_INVALID;
   } else if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
     st = CG_EMPTY;
-  } else if (!in_arena(it.sig_off, it.sig_len, arena_len) || !in_arena(it.msg_off, it.msg_len, arena_len)) {
+  } else if (!in_arena(it.sig_off, it.sig_len, arena_len) ||
+             !in_arena(it.msg_off, it.msg_len, item_msg_len(it, arena_len, msgs_len, msgs))) {
     st = CG_NOT_RUN;
   } else {
     EcItemWs w;
-    const uint32_t r = ecdsa_prep<C>(w, arena, round4(arena_len), it.sig_off, it.sig_len, it.msg_off, it.msg_len);
+    const uint32_t r = ecdsa_prep<C>(w, arena, round4(arena_len), it.sig_off, it.sig_len,
+                                     item_msg_arena(it, arena, msgs), round4(item_msg_len(it, arena_len, msgs_len, msgs)),
+                                     it.msg_off, it.msg_len);
     if (r == 0) {
       ws[i] = w;
       st = (uint8_t)(EC_PENDING_BASE + C);
@@ -160,12 +164,13 @@ void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_a
 template <int C>
 static void launch_curve(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                          const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                         const KeyWs& w, void* d_item_ws, const void* d_btab, hipStream_t stream) {
+                         const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len, void* d_item_ws,
+                         const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
   EcItemWs* ws = (EcItemWs*)d_item_ws;
   hipLaunchKernelGGL(k_ec_prep<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys, w.hdr,
-                     d_arena, arena_len, mode, d_status, ws);
+                     d_arena, arena_len, d_msgs, msgs_len, mode, d_status, ws);
   const uint64_t igrid = (n_items + (uint64_t)B * EC_INV_K - 1) / ((uint64_t)B * EC_INV_K);
   hipLaunchKernelGGL(k_ec_inv<C>, dim3((unsigned)igrid), dim3(B), 0, stream, n_items, (const uint8_t*)d_status, ws);
   hipLaunchKernelGGL(k_ec_ladder<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, w.tab,
@@ -174,11 +179,12 @@ static void launch_curve(const cg_key* d_keys, uint32_t n_keys, const cg_item* d
 
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     void* d_item_ws, const void* d_btab, hipStream_t stream) {
-  launch_curve<CG_CURVE_R1>(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_item_ws,
-                            d_btab, stream);
-  launch_curve<CG_CURVE_K1>(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_item_ws,
-                            d_btab, stream);
+                     const uint8_t* d_msgs, uint64_t msgs_len, void* d_item_ws, const void* d_btab,
+                     hipStream_t stream) {
+  launch_curve<CG_CURVE_R1>(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs,
+                            msgs_len, d_item_ws, d_btab, stream);
+  launch_curve<CG_CURVE_K1>(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs,
+                            msgs_len, d_item_ws, d_btab, stream);
 }
 
 }  // namespace cg

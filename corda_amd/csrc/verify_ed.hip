@@ -147,6 +147,7 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
                                                    const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs,
                                                    const EdTab* __restrict__ btab,
                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   const uint8_t* __restrict__ msgs, uint64_t msgs_len,
                                                    uint32_t mode, uint8_t* __restrict__ status,
                                                    ge_p2* __restrict__ rout) {
   __shared__ EdTab sB;
@@ -167,7 +168,8 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
     st = CG_KEY_INVALID;
   } else if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
     st = CG_EMPTY;
-  } else if (!in_arena(it.sig_off, it.sig_len, arena_len) || !in_arena(it.msg_off, it.msg_len, arena_len)) {
+  } else if (!in_arena(it.sig_off, it.sig_len, arena_len) ||
+             !in_arena(it.msg_off, it.msg_len, item_msg_len(it, arena_len, msgs_len, msgs))) {
     st = CG_NOT_RUN;
   } else if (it.sig_len != 64) {
     st = CG_SIG_MALFORMED;
@@ -185,7 +187,8 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
       pre[w] = sw[w];
       pre[8 + w] = ab[w];
     }
-    sha512_prefix64_msg(hw, pre, arena, lr, it.msg_off, it.msg_len);
+    sha512_prefix64_msg(hw, pre, item_msg_arena(it, arena, msgs), round4(item_msg_len(it, arena_len, msgs_len, msgs)),
+                        it.msg_off, it.msg_len);
     sc_reduce512(h, hw);
     uint32_t s[8], sr[8];
 #pragma unroll
@@ -277,11 +280,13 @@ void ed_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_a
 
 void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     void* d_item_ws, const void* d_btab, hipStream_t stream) {
+                     const uint8_t* d_msgs, uint64_t msgs_len, void* d_item_ws, const void* d_btab,
+                     hipStream_t stream) {
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
   hipLaunchKernelGGL(k_ed_verify, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys, w.hdr,
-                     w.tab, (const EdTab*)d_btab, d_arena, arena_len, mode, d_status, (ge_p2*)d_item_ws);
+                     w.tab, (const EdTab*)d_btab, d_arena, arena_len, d_msgs, msgs_len, mode, d_status,
+                     (ge_p2*)d_item_ws);
   const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
   hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, n_items, d_arena, arena_len,
                      d_status, (const ge_p2*)d_item_ws);

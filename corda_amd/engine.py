@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from .batch import COMPONENT_DTYPE, MODE_DOVERIFY, SPAN_DTYPE, TX_DTYPE
+from .batch import COMPONENT_DTYPE, KEY_DTYPE, MODE_DOVERIFY, SPAN_DTYPE, TMPL_DTYPE, TX_DTYPE, TXSIG_DTYPE
 
 
 def _p(a):
@@ -129,3 +129,28 @@ class Engine:
         _lib.check(_lib.lib().cg_tx_ids(self._h, _p(txs), len(txs), _p(comps), len(comps), _p(arena), arena.size,
                                         _p(ids), _p(st)), "cg_tx_ids")
         return ids.reshape(-1, 32), st
+
+    # ------------------------------------------------------------------ transactions
+    def verify_transactions(self, txs, comps, keys, sigs, tmpls, arena, mode=MODE_DOVERIFY):
+        """Tx ids + every signature over SignableData(id, metadata) in one call
+        (cg_verify_transactions). Returns (ids [n_tx, 32], tx_status, sig_status)."""
+        assert txs.dtype == TX_DTYPE and comps.dtype == COMPONENT_DTYPE and keys.dtype == KEY_DTYPE
+        assert sigs.dtype == TXSIG_DTYPE and tmpls.dtype == TMPL_DTYPE
+        ids = np.zeros(32 * len(txs), dtype=np.uint8)
+        txst = np.zeros(len(txs), dtype=np.uint8)
+        sst = np.full(len(sigs), 255, dtype=np.uint8)
+        rc = _lib.lib().cg_verify_transactions(self._h, _p(txs), len(txs), _p(comps), len(comps), _p(keys), len(keys),
+                                               _p(sigs), len(sigs), _p(tmpls), len(tmpls), _p(arena), arena.size,
+                                               mode, _p(ids), _p(txst), _p(sst))
+        _lib.check(rc, "cg_verify_transactions")
+        return ids.reshape(-1, 32), txst, sst
+
+    def verify_transactions_device(self, d_txs, n_tx, d_comps, n_comps, d_keys, n_keys, d_sigs, n_sigs, tmpls,
+                                   d_arena, arena_len, d_ids, d_tx_status, d_sig_status, mode=MODE_DOVERIFY,
+                                   stream=0):
+        """Asynchronous device form; `tmpls` is a host TMPL_DTYPE array (template bytes in the arena)."""
+        assert tmpls.dtype == TMPL_DTYPE
+        rc = _lib.lib().cg_verify_transactions_device(self._h, d_txs, n_tx, d_comps, n_comps, d_keys, n_keys, d_sigs,
+                                                      n_sigs, _p(tmpls), len(tmpls), d_arena, arena_len, mode, d_ids,
+                                                      d_tx_status, d_sig_status, stream or None)
+        _lib.check(rc, "cg_verify_transactions_device")

@@ -11,14 +11,18 @@ is then rebuilt in list order so the exception type, message and the index it re
 exactly those of the serial loop.
 
 The signed clear data of a TransactionSignature is ``SignableData(txId, metadata)``
-serialised with Kryo (Crypto.kt:499-502). That serialiser is not part of this engine
-(SURVEY §8(f1)); callers pass ``signable_data(tx_id, metadata) -> bytes``.
+serialised with Kryo (Crypto.kt:499-502). ``check_signatures_are_valid_batch`` takes it from
+the caller (``signable_data(tx_id, sig) -> bytes``). ``verify_wire_transactions`` is the
+whole-pipeline form: it takes WireTransaction components, computes every id on the GPU and
+splices the ids into per-metadata SignableData templates (corda_amd/signable.py) on the GPU
+too, so the host never serialises per signature.
 """
 from dataclasses import dataclass, field
 
 import numpy as np
 
 from . import batch as B
+from . import signable
 from .crypto import BatchItem, Crypto, PublicKey, SCHEME_CODE_NAMES
 
 
@@ -90,3 +94,87 @@ def verify_signatures_except(stx, signable_data, allowed_to_be_missing=(), crypt
     needed = {k for k in stx.required_signing_keys if k not in sig_keys} - set(allowed_to_be_missing)
     if needed:
         raise SignaturesMissingException(needed, stx.id)
+
+
+# ---------------------------------------------------------------------------------------------
+# WireTransaction-level pipeline: ids on the GPU, then every signature over SignableData(id).
+
+@dataclass
+class WireTransactionData:
+    """The bytes WireTransaction.id is computed from (MerkleTransaction.kt:74-93): the
+    serialised components in availableComponents order (inputs, attachments, outputs,
+    commands, notary?, timeWindow?), the 32-byte PrivacySalt and its serialisation (the last
+    leaf, hashed without a nonce)."""
+    components: list
+    salt: bytes
+    salt_blob: bytes
+
+
+@dataclass
+class SignedWireTransaction:
+    wtx: WireTransactionData
+    sigs: list                       # TransactionSignature
+    required_signing_keys: set = field(default_factory=set)
+
+
+def pack_signed_transactions(stxs):
+    """One arena for components, salts, keys, signatures and SignableData templates; returns
+    (txs, comps, keys, sigs, tmpls, arena) in the include/cordagpu.h layouts."""
+    bb = B.BatchBuilder()
+    comps, tx_rows, sig_rows, tmpl_rows, tmpl_index = [], [], [], [], {}
+
+    def tmpl_for(pv, sid):
+        k = (pv, sid)
+        if k not in tmpl_index:
+            pre, suf = signable.template(pv, sid)
+            tmpl_index[k] = len(tmpl_rows)
+            tmpl_rows.append((bb._append(pre, 4), bb._append(suf, 4), len(pre), len(suf)))
+        return tmpl_index[k]
+
+    for t, stx in enumerate(stxs):
+        w = stx.wtx
+        first = len(comps)
+        for blob in w.components:
+            comps.append((bb._append(blob, 4), len(blob), 0))
+        comps.append((bb._append(w.salt_blob, 4), len(w.salt_blob), 1))
+        tx_rows.append((first, len(w.components) + 1, 0, bb._append(w.salt, 4)))
+        for s in stx.sigs:
+            k = bb.key(s.by.scheme, s.by.fmt, s.by.encoded)
+            sig_rows.append((bb._append(s.bytes, 4), t, k, len(s.bytes), tmpl_for(s.platform_version,
+                                                                                  s.scheme_number_id), 0))
+    built = bb.build()
+    txs = np.array(tx_rows, dtype=B.TX_DTYPE) if tx_rows else np.zeros(0, B.TX_DTYPE)
+    c = np.array(comps, dtype=B.COMPONENT_DTYPE) if comps else np.zeros(0, B.COMPONENT_DTYPE)
+    sg = np.array(sig_rows, dtype=B.TXSIG_DTYPE) if sig_rows else np.zeros(0, B.TXSIG_DTYPE)
+    tm = np.array(tmpl_rows, dtype=B.TMPL_DTYPE) if tmpl_rows else np.zeros(0, B.TMPL_DTYPE)
+    return txs, c, built.keys, sg, tm, built.arena
+
+
+def verify_wire_transactions(stxs, crypto=Crypto):
+    """For each SignedWireTransaction: its id (WireTransaction.id) and None if every
+    signature verifies, else (index, exception) of the FIRST failing signature in list order
+    -- what ``SignedTransaction.verifySignaturesExcept`` would throw first
+    (TransactionWithSignatures.kt:58-61). Ids, SignableData messages and verdicts are all
+    computed on the GPU in one cg_verify_transactions call."""
+    from .merkle import MerkleTreeException
+    txs, comps, keys, sigs, tmpls, arena = pack_signed_transactions(stxs)
+    ids, txst, sst = crypto.engine().verify_transactions(txs, comps, keys, sigs, tmpls, arena, B.MODE_DOVERIFY)
+    out_ids, results, pos = [], [], 0
+    for t, stx in enumerate(stxs):
+        if txst[t] != 0:
+            out_ids.append(None)
+            results.append((0, MerkleTreeException("Cannot calculate Merkle root on empty hash list.")))
+            pos += len(stx.sigs)
+            continue
+        out_ids.append(bytes(ids[t]))
+        res = None
+        for i, s in enumerate(stx.sigs):
+            st = int(sst[pos + i])
+            if st != B.VALID and res is None:
+                try:
+                    crypto.raise_for_status(st, SCHEME_CODE_NAMES.get(s.by.scheme, ""), do_verify=True)
+                except Exception as e:  # noqa: BLE001 - mirrored JVM exception
+                    res = (i, e)
+        results.append(res)
+        pos += len(stx.sigs)
+    return out_ids, results

@@ -192,6 +192,46 @@ int cg_tx_ids_device(cg_ctx* ctx, const cg_tx* d_txs, uint64_t n_tx, const cg_co
                      uint64_t n_comps, const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids,
                      uint8_t* d_status, void* hip_stream);
 
+/* ---- Transaction pipeline: WireTransaction ids -> SignableData -> every signature.
+ * Replaces, for a batch of SignedTransactions, the serial
+ *   id = WireTransaction.id (MerkleTransaction.kt:74-93, WireTransaction.kt:39)
+ *   for (sig in sigs) Crypto.doVerify(id, sig)        (TransactionWithSignatures.kt:58-61,
+ *                                                      Crypto.kt:499-502)
+ * The clear data of signature s is SignableData(id, s.metadata).serialize(): for a fixed
+ * metadata value that is prefix || id || suffix, so the caller passes one template per metadata
+ * value (template bytes inside the arena) and the engine splices the device-computed ids in.
+ * Signatures of a transaction whose id cannot be computed (status != 0), or that reference a
+ * transaction / template out of range, get CG_NOT_RUN. */
+typedef struct cg_signable_tmpl {
+  uint64_t prefix_off; /* prefix bytes at arena[prefix_off .. +prefix_len) */
+  uint64_t suffix_off; /* suffix bytes at arena[suffix_off .. +suffix_len) */
+  uint32_t prefix_len;
+  uint32_t suffix_len;
+} cg_signable_tmpl;    /* 24 bytes */
+
+typedef struct cg_txsig {
+  uint64_t sig_off;    /* signature bytes at arena[sig_off .. +sig_len) */
+  uint32_t tx_idx;     /* transaction whose id is signed */
+  uint32_t key_idx;    /* TransactionSignature.by, index into the cg_key table */
+  uint16_t sig_len;
+  uint16_t tmpl;       /* SignatureMetadata template index */
+  uint32_t reserved;   /* must be 0 */
+} cg_txsig;            /* 24 bytes */
+
+/* Device buffers in HBM except `tmpls` (a small host array). ids: 32*n_tx, tx_status: n_tx
+ * (0 ok / 1 MerkleTreeException / 2 component outside the arena), sig_status: n_sigs. */
+int cg_verify_transactions_device(cg_ctx* ctx, const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps,
+                                  uint64_t n_comps, const cg_key* d_keys, uint32_t n_keys, const cg_txsig* d_sigs,
+                                  uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,
+                                  const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_ids,
+                                  uint8_t* d_tx_status, uint8_t* d_sig_status, void* hip_stream);
+/* Host buffers in and out (copies through the ctx). */
+int cg_verify_transactions(cg_ctx* ctx, const cg_tx* txs, uint64_t n_tx, const cg_component* comps, uint64_t n_comps,
+                           const cg_key* keys, uint32_t n_keys, const cg_txsig* sigs, uint64_t n_sigs,
+                           const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
+                           uint64_t arena_len, uint32_t mode, uint8_t* ids_out, uint8_t* tx_status_out,
+                           uint8_t* sig_status_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -312,7 +312,7 @@ static int ecdsa_rows_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
   ec_row_bases<C>(bases, xm, ym, K);
   for (int j = 0; j < EC_ROWS; ++j) ec_row_build<C>(TQ->t[j], bases[j], *S, K);
   EcItemWs ws;
-  st = ecdsa_prep<C>(ws, arena, lr, sig_off, sig_len, msg_off, msg_len);
+  st = ecdsa_prep<C>(ws, arena, lr, sig_off, sig_len, arena, lr, msg_off, msg_len);
   if (st) return (int)st;
   ecdsa_batch_inv<C, 1>(&ws, 1, 1u, K);
   return (int)ecdsa_ladder_check<C>(ws.a, ws.b, ws.r, *TG[C], *TQ, K);

@@ -187,3 +187,89 @@ def test_mixed_notary_batch_vs_c_oracle(engine):
     st = engine.verify(b, B.MODE_DOVERIFY)
     ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
     assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
+
+
+def test_tx_pipeline_vs_generator_and_oracle(engine):
+    """Config 4 in miniature through cg_verify_transactions: ids computed on the GPU equal
+    the generator's and the oracle's WireTransaction.id; every signature over the spliced
+    SignableData(id) gets the verdict of its label, and a sample matches the oracle."""
+    from corda_amd import signable
+    from tools.workload import wl
+    w = wl.tx_pipeline(3000, n_keys=97, seed=41, corrupt_permille=60, nthreads=16)
+    ids, txst, sst = engine.verify_transactions(w.txs, w.comps, w.keys, w.sigs, w.tmpls, w.arena)
+    assert np.all(txst == 0)
+    assert np.array_equal(ids, w.ids)
+    a = w.arena.tobytes()
+    for t in range(0, len(w.txs), 97):
+        r = w.txs[t]
+        cs = w.comps[r["first"]:r["first"] + r["n"]]
+        blobs = [a[c["off"]:c["off"] + c["len"]] for c in cs]
+        assert ocorda.tx_id(blobs[:-1], a[r["salt_off"]:r["salt_off"] + 32], blobs[-1]) == ids[t].tobytes()
+    assert np.all(sst[w.labels == 0] == B.VALID)
+    assert np.all(sst[w.labels == 1] == B.INVALID)
+    assert np.count_nonzero(w.labels) > 0
+    for j in range(0, len(w.sigs), 53):
+        s = w.sigs[j]
+        k = w.keys[s["key_idx"]]
+        msg = signable.serialize(ids[s["tx_idx"]].tobytes(), 1, 4)
+        want = ocorda.verify_item(4, 0, a[k["off"]:k["off"] + 32], a[s["sig_off"]:s["sig_off"] + 64], msg)
+        assert sst[j] == want
+
+
+def test_tx_pipeline_edges(engine):
+    """Empty transaction (MerkleTreeException), signature rows pointing at a missing tx or
+    template: CG_NOT_RUN; mixed-scheme signers (Ed25519 + secp256r1) through the host mirror
+    with the serial loop's first-failure semantics (TransactionWithSignatures.kt:58-61)."""
+    from corda_amd import signable
+    from corda_amd import transactions as T
+    from corda_amd.crypto import PublicKey, SignatureException
+    from oracle import ecdsa_bc as ec, ed25519_i2p as ed
+    rng = np.random.default_rng(9)
+    seeds = [ed.entropy_seed(20 + i) for i in range(3)]
+    ed_keys = [PublicKey(4, ed.public_from_seed(s)) for s in seeds]
+    d = 0x1234567890abcdef1234567890abcdef1234567890abcdef1234567890abcdef
+    r1_key = PublicKey(3, ec.raw_key(ec.public_point(3, d)))
+    stxs, expect = [], []
+    for t in range(12):
+        comps = [rng.integers(0, 256, int(rng.integers(1, 300)), dtype=np.uint8).tobytes()
+                 for _ in range(0 if t == 5 else int(rng.integers(1, 9)))]
+        salt = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        wtx = T.WireTransactionData(comps, salt, b"\x01" + salt)
+        tid = ocorda.tx_id(comps, salt, b"\x01" + salt)
+        sigs = []
+        for i, s in enumerate(seeds):
+            sigs.append(T.TransactionSignature(ed.sign(s, signable.serialize(tid, 1, 4)), ed_keys[i], 1, 4))
+        rr, ss = ec.sign(3, d, signable.serialize(tid, 1, 3), 1000 + t)
+        sigs.append(T.TransactionSignature(ec.der_encode_sig(rr, ss), r1_key, 1, 3))
+        bad = None
+        if t % 3 == 1:  # corrupt signature 2 and 3: the first failure (index 2) must be reported
+            for i in (2, 3):
+                b = bytearray(sigs[i].bytes)
+                b[4] ^= 1
+                sigs[i] = T.TransactionSignature(bytes(b), sigs[i].by, 1, sigs[i].scheme_number_id)
+            bad = 2
+        if t % 4 == 2:  # metadata mismatch: signed for schemeNumberID 4, claims 3 -> invalid
+            sigs[0] = T.TransactionSignature(sigs[0].bytes, sigs[0].by, 1, 3)
+            bad = 0
+        stxs.append(T.SignedWireTransaction(wtx, sigs))
+        expect.append((bad, tid))
+    ids, results = T.verify_wire_transactions(stxs)
+    for (bad, tid), got_id, res in zip(expect, ids, results):
+        assert got_id == tid  # t = 5: no components, the salt leaf alone
+        if bad is None:
+            assert res is None
+        else:
+            assert res[0] == bad and isinstance(res[1], SignatureException)
+    # raw ABI: rows pointing at a missing tx / template, and a transaction with no leaves at
+    # all (MerkleTree.getMerkleTree on an empty list -> MerkleTreeException): CG_NOT_RUN
+    txs, comps, keys, sigs, tmpls, arena = T.pack_signed_transactions(stxs[:3])
+    sigs = sigs.copy()
+    sigs[0]["tx_idx"] = 99
+    sigs[1]["tmpl"] = 7
+    txs = txs.copy()
+    txs[2]["n"] = 0
+    _, txst, sst = engine.verify_transactions(txs, comps, keys, sigs, tmpls, arena)
+    assert sst[0] == B.NOT_RUN and sst[1] == B.NOT_RUN
+    assert txst.tolist() == [0, 0, 1]
+    assert np.all(sst[sigs["tx_idx"] == 2] == B.NOT_RUN)
+    assert sst[2:8].tolist() == [B.VALID, B.VALID, B.VALID, B.VALID, B.INVALID, B.INVALID]  # tx 1: sigs 2, 3 bad

@@ -96,3 +96,87 @@ def concat(batches, shuffle_seed=None):
         perm = np.random.default_rng(shuffle_seed).permutation(len(items))
         items = items[perm]
     return Batch(keys, items, np.concatenate(arenas + [np.zeros(64, dtype=np.uint8)])), perm
+
+
+class TxPipeline:
+    """A packed config-4 workload: WireTransactions + their signatures (include/cordagpu.h
+    layouts) and the generator's own tx ids and corruption labels."""
+
+    def __init__(self, txs, comps, keys, sigs, tmpls, arena, ids, labels):
+        self.txs, self.comps, self.keys, self.sigs, self.tmpls, self.arena = txs, comps, keys, sigs, tmpls, arena
+        self.ids, self.labels = ids, labels
+
+
+def tx_pipeline(n_tx, n_keys=1024, seed=4, corrupt_permille=20, nthreads=8, comp_len=(80, 600)):
+    """Config 4 shape: n_tx WireTransactions with 1+Poisson(1) inputs,
+    Poisson(3) outputs, 1+Poisson(3) commands, a notary and the privacy-salt leaf (~11
+    components), component blobs uniform in comp_len bytes; one Ed25519 signature per command
+    (random signer among keys 1..n_keys-1) plus the notary's (key 0), each over
+    SignableData(id, SignatureMetadata(1, 4)) (corda_amd/signable.py template)."""
+    from corda_amd import signable
+    from corda_amd.batch import COMPONENT_DTYPE, KEY_DTYPE, TMPL_DTYPE, TX_DTYPE, TXSIG_DTYPE
+    L = lib()
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    L.wl_tx_sign.argtypes = [u64, vp, vp, vp, u64, u64, vp, vp, vp, vp, u32, vp, u32, u32, u64, vp, vp, i32]
+    rng = np.random.default_rng(seed)
+    n_in = 1 + rng.poisson(1, n_tx)
+    n_out = rng.poisson(3, n_tx)
+    n_cmd = 1 + rng.poisson(3, n_tx)
+    ncomp = (n_in + n_out + n_cmd + 2).astype(np.int64)  # + notary + salt leaf
+    first = np.concatenate([[0], np.cumsum(ncomp)[:-1]])
+    total = int(ncomp.sum())
+    lens = rng.integers(comp_len[0], comp_len[1] + 1, total).astype(np.int64)
+    is_salt = np.zeros(total, dtype=bool)
+    is_salt[first + ncomp - 1] = True
+    lens[is_salt] = 40
+    pre, suf = signable.template(1, 4)
+    # arena: [keys][template][components][salts][signatures]
+    key_base = 0
+    tmpl_base = 32 * n_keys
+    comp_base = (tmpl_base + len(pre) + len(suf) + 3 + 15) & ~15
+    aligned = (lens + 3) & ~3
+    comp_off = comp_base + np.concatenate([[0], np.cumsum(aligned)[:-1]])
+    salt_base = int(comp_base + aligned.sum())
+    n_sig_tx = n_cmd + 1
+    n_sigs = int(n_sig_tx.sum())
+    sig_base = salt_base + 32 * n_tx
+    arena_len = sig_base + 64 * n_sigs
+    arena = np.zeros(arena_len + 64, dtype=np.uint8)
+    body = salt_base - comp_base
+    arena[comp_base:salt_base] = np.random.default_rng(seed + 1).integers(
+        0, 2 ** 63, (body + 7) // 8, dtype=np.int64).view(np.uint8)[:body]
+    arena[salt_base:sig_base] = rng.integers(0, 256, 32 * n_tx, dtype=np.uint8)
+    arena[tmpl_base:tmpl_base + len(pre)] = np.frombuffer(pre, np.uint8)
+    arena[tmpl_base + len(pre):tmpl_base + len(pre) + len(suf)] = np.frombuffer(suf, np.uint8)
+    comps = np.zeros(total, dtype=COMPONENT_DTYPE)
+    comps["off"] = comp_off
+    comps["len"] = lens
+    comps["flags"] = is_salt.astype(np.uint32)
+    txs = np.zeros(n_tx, dtype=TX_DTYPE)
+    txs["first"] = first
+    txs["n"] = ncomp
+    txs["salt_off"] = salt_base + 32 * np.arange(n_tx)
+    seeds = np.zeros(32 * n_keys, dtype=np.uint8)
+    pubs = np.zeros(32 * n_keys, dtype=np.uint8)
+    L.wl_ed25519_keys(n_keys, seed, 0, _p(seeds), _p(pubs), nthreads)
+    arena[key_base:key_base + 32 * n_keys] = pubs
+    keys = np.zeros(n_keys, dtype=KEY_DTYPE)
+    keys["off"] = 32 * np.arange(n_keys)
+    keys["len"] = 32
+    keys["scheme"] = 4
+    sigs = np.zeros(n_sigs, dtype=TXSIG_DTYPE)
+    sigs["tx_idx"] = np.repeat(np.arange(n_tx), n_sig_tx)
+    signer = rng.integers(1, max(2, n_keys), n_sigs)
+    last = np.cumsum(n_sig_tx) - 1
+    signer[last] = 0  # the notary signs last
+    sigs["key_idx"] = signer
+    sigs["sig_off"] = sig_base + 64 * np.arange(n_sigs)
+    sigs["sig_len"] = 64
+    tmpls = np.zeros(1, dtype=TMPL_DTYPE)
+    tmpls[0] = (tmpl_base, tmpl_base + len(pre), len(pre), len(suf))
+    ids = np.zeros(32 * n_tx, dtype=np.uint8)
+    labels = np.zeros(n_sigs, dtype=np.uint8)
+    L.wl_tx_sign(n_tx, _p(txs), _p(comps), _p(arena), arena_len, n_sigs, _p(sigs), _p(seeds), _p(pubs),
+                 _p(arena[tmpl_base:]), len(pre), _p(arena[tmpl_base + len(pre):]), len(suf), corrupt_permille,
+                 seed, _p(ids), _p(labels), nthreads)
+    return TxPipeline(txs, comps, keys, sigs, tmpls, arena[:arena_len + 64], ids.reshape(-1, 32), labels)

@@ -576,3 +576,100 @@ void wl_ecdsa_items(int curve, uint64_t n_items, uint32_t n_keys, const uint8_t*
   for (auto& x : th) x.join();
 }
 }
+
+// ---------------------------------------------------------------- transaction pipeline (config 4)
+namespace {
+void sha256_bytes_suffix(uint8_t out[32], const uint8_t* arena, uint64_t arena_len, uint64_t off, uint64_t len,
+                         const uint32_t* suffix_be) {
+  uint32_t h[8];
+  sha256_arena_suffix(h, arena, (arena_len + 3) & ~3ull, off, len, suffix_be);
+  for (int k = 0; k < 8; ++k)
+    for (int j = 0; j < 4; ++j) out[4 * k + j] = (uint8_t)(h[k] >> (24 - 8 * j));
+}
+
+void sha256_64(uint8_t out[32], const uint8_t l[32], const uint8_t r[32]) {
+  uint8_t buf[64 + 8];
+  memcpy(buf, l, 32);
+  memcpy(buf + 32, r, 32);
+  sha256_bytes_suffix(out, buf, 64, 0, 64, nullptr);
+}
+
+// WireTransaction.id (MerkleTransaction.kt:16-33,74-93; MerkleTree.kt:27-66), host side
+void tx_id(uint8_t id[32], const cg_tx& tx, const cg_component* comps, const uint8_t* arena, uint64_t arena_len) {
+  std::vector<uint8_t> lv(32 * (size_t)tx.n);
+  for (uint32_t i = 0; i < tx.n; ++i) {
+    const cg_component& c = comps[tx.first + i];
+    if (c.flags & 1u) {
+      sha256_bytes_suffix(&lv[32 * i], arena, arena_len, c.off, c.len, nullptr);
+    } else {
+      uint8_t nb[40];
+      memcpy(nb, arena + tx.salt_off, 32);
+      nb[32] = (uint8_t)(i >> 24);
+      nb[33] = (uint8_t)(i >> 16);
+      nb[34] = (uint8_t)(i >> 8);
+      nb[35] = (uint8_t)i;
+      uint8_t nonce[32];
+      sha256_bytes_suffix(nonce, nb, 36, 0, 36, nullptr);
+      uint32_t nbe[8];
+      for (int k = 0; k < 8; ++k)
+        nbe[k] = ((uint32_t)nonce[4 * k] << 24) | ((uint32_t)nonce[4 * k + 1] << 16) |
+                 ((uint32_t)nonce[4 * k + 2] << 8) | nonce[4 * k + 3];
+      sha256_bytes_suffix(&lv[32 * i], arena, arena_len, c.off, c.len, nbe);
+    }
+  }
+  uint32_t m = 1;
+  while (m < tx.n) m <<= 1;
+  lv.resize(32 * (size_t)m, 0);
+  while (m > 1) {
+    for (uint32_t j = 0; j < m / 2; ++j) sha256_64(&lv[32 * j], &lv[64 * j], &lv[64 * j + 32]);
+    m /= 2;
+  }
+  memcpy(id, lv.data(), 32);
+}
+}  // namespace
+
+extern "C" {
+// Config 4 generator: given packed transactions (cg_tx / cg_component / arena,
+// laid out by tools/workload/wl.py), computes every id on the host and writes, for every
+// signature row, an Ed25519 signature over prefix || id || suffix (the SignableData template,
+// corda_amd/signable.py) into arena[sig_off..+64). corrupt_permille of the signatures get one
+// flipped bit of R (labels_out[j] = 1).
+void wl_tx_sign(uint64_t n_tx, const cg_tx* txs, const cg_component* comps, uint8_t* arena, uint64_t arena_len,
+                uint64_t n_sigs, const cg_txsig* sigs, const uint8_t* seeds, const uint8_t* pubs,
+                const uint8_t* prefix, uint32_t pre_len, const uint8_t* suffix, uint32_t suf_len,
+                uint32_t corrupt_permille, uint64_t seed, uint8_t* ids_out, uint8_t* labels_out, int nthreads) {
+  init();
+  if (nthreads <= 0) nthreads = 1;
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+      th.emplace_back([=]() {
+        for (uint64_t i = (uint64_t)t; i < n_tx; i += (uint64_t)nthreads)
+          tx_id(ids_out + 32 * i, txs[i], comps, arena, arena_len);
+      });
+    for (auto& x : th) x.join();
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t)
+    th.emplace_back([=]() {
+      std::vector<uint8_t> msg(pre_len + 32 + suf_len);
+      memcpy(msg.data(), prefix, pre_len);
+      memcpy(msg.data() + pre_len + 32, suffix, suf_len);
+      for (uint64_t j = (uint64_t)t; j < n_sigs; j += (uint64_t)nthreads) {
+        const cg_txsig& sg = sigs[j];
+        memcpy(msg.data() + pre_len, ids_out + 32 * (uint64_t)sg.tx_idx, 32);
+        uint8_t* sig = arena + sg.sig_off;
+        sign(sig, seeds + 32 * (size_t)sg.key_idx, pubs + 32 * (size_t)sg.key_idx, msg.data(), msg.size());
+        uint64_t s = seed ^ (j * 0x9e3779b97f4a7c15ULL);
+        uint8_t label = 0;
+        if ((uint32_t)(splitmix(s) % 1000) < corrupt_permille) {
+          const uint64_t rb = splitmix(s);
+          sig[(rb >> 8) % 31] ^= (uint8_t)(1u << (rb & 7));
+          label = 1;
+        }
+        labels_out[j] = label;
+      }
+    });
+  for (auto& x : th) x.join();
+}
+}

@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--threads", type=int, default=0, help="host threads for data generation / CPU baseline")
     ap.add_argument("--ecdsa-items", type=int, default=1 << 18,
                     help="items of the secondary ECDSA measurement (N = 1 only; 0 disables)")
+    ap.add_argument("--pipeline-txs", type=int, default=1 << 18,
+                    help="WireTransactions of the secondary config-4 pipeline measurement (N = 1 only; 0 disables)")
+    ap.add_argument("--mixed-items", type=int, default=1 << 20,
+                    help="items of the secondary config-5-shaped mixed batch (N = 1 only; 0 disables)")
     return ap.parse_args()
 
 
@@ -97,6 +101,91 @@ def cpu_baseline(batch, seconds, threads):
             "sample": f"first {n} items of the rank-0 batch (incl. key decode for all {len(batch.keys)} keys), "
                       f"oracle/c or_verify_batch over {threads} threads, {dt:.1f} s; JVM reference "
                       f"unavailable (no JDK / i2p / BouncyCastle jars on the box)"}, st
+
+
+def bench_mixed(a, wl, eng, dev, stream, run, threads):
+    """BASELINE configs[4] shape on one GPU: 70% Ed25519 / 20% secp256r1 / 10% secp256k1,
+    shuffled, no deduplication (ECDSA items are tiled from 65 536-item pools)."""
+    import torch
+    n = a.mixed_items
+    ne, nr = int(n * 0.7), int(n * 0.2)
+    nk = n - ne - nr
+    e, _ = wl.ed25519_batch(ne, n_keys=a.keys, msg_len=a.msg_len, corrupt_permille=a.corrupt_permille,
+                            seed=a.seed + 101, nthreads=threads)
+    parts = [e]
+    for curve, cnt in ((1, nr), (0, nk)):
+        pool, _ = wl.ecdsa_batch(curve, min(cnt, 65536), n_keys=1024, msg_len=a.msg_len, corrupt_permille=100,
+                                 seed=a.seed + 103 + curve, nthreads=threads)
+        pool.items = np.resize(pool.items, cnt)
+        parts.append(pool)
+    b, _ = wl.concat(parts, shuffle_seed=a.seed + 107)
+    kd = torch.from_numpy(b.keys.view(np.uint8)).to(dev)
+    idd = torch.from_numpy(b.items.view(np.uint8)).to(dev)
+    ad = torch.from_numpy(b.arena).to(dev)
+    sd = torch.full((b.n,), 255, dtype=torch.uint8, device=dev)
+    steps = max(2, a.steps // 2)
+    el, km = run(kd, len(b.keys), idd, b.n, ad, int(b.arena.size), sd, steps, 1, False)
+    st = sd.cpu().numpy()
+    return {"value": round(b.n * steps / el, 1), "unit": "sigs/s", "items": b.n, "keys": len(b.keys),
+            "mix": {"ed25519": ne, "secp256r1": nr, "secp256k1": nk}, "kernel_ms": round(km, 3),
+            "ms_per_step": round(el / steps * 1e3, 3),
+            "verdicts": {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
+
+
+def bench_pipeline(a, wl, eng, dev, stream, threads):
+    """BASELINE configs[3] shape: WireTransaction ids (SHA-256 Merkle) for every transaction,
+    SignableData(id) spliced from the template, every signature verified -- one
+    cg_verify_transactions_device call per step. Also times the id pass alone (cg_tx_ids_device)
+    and reports its input bytes / time."""
+    import torch
+    from corda_amd import _lib
+    t0 = time.time()
+    w = wl.tx_pipeline(a.pipeline_txs, n_keys=1024, seed=a.seed + 211, corrupt_permille=20, nthreads=threads)
+    gen = time.time() - t0
+    up = lambda x: torch.from_numpy(x.view(np.uint8)).to(dev)  # noqa: E731
+    txd, cd, kd, sgd, ad = up(w.txs), up(w.comps), up(w.keys), up(w.sigs), up(w.arena)
+    n_tx, n_sig = len(w.txs), len(w.sigs)
+    idd = torch.zeros(32 * n_tx, dtype=torch.uint8, device=dev)
+    tsd = torch.zeros(n_tx, dtype=torch.uint8, device=dev)
+    ssd = torch.full((n_sig,), 255, dtype=torch.uint8, device=dev)
+    sptr = stream.cuda_stream
+    L = _lib.lib()
+    steps = max(2, a.steps // 2)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t = time.perf_counter()
+        e0.record(stream)
+        for _ in range(steps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t) / steps, e0.elapsed_time(e1) / steps
+
+    def ids_only():
+        _lib.check(L.cg_tx_ids_device(eng._h, txd.data_ptr(), n_tx, cd.data_ptr(), len(w.comps), ad.data_ptr(),
+                                      len(w.arena), idd.data_ptr(), tsd.data_ptr(), sptr), "cg_tx_ids_device")
+
+    def full():
+        eng.verify_transactions_device(txd.data_ptr(), n_tx, cd.data_ptr(), len(w.comps), kd.data_ptr(), len(w.keys),
+                                       sgd.data_ptr(), n_sig, w.tmpls, ad.data_ptr(), len(w.arena), idd.data_ptr(),
+                                       tsd.data_ptr(), ssd.data_ptr(), stream=sptr)
+
+    _, ids_ms = timed(ids_only)
+    el, full_ms = timed(full)
+    ids = idd.cpu().numpy().reshape(-1, 32)
+    sst = ssd.cpu().numpy()
+    comp_bytes = int(w.comps["len"].astype(np.int64).sum())
+    parity = bool(np.array_equal(ids, w.ids) and np.all(sst[w.labels == 0] == 0) and np.all(sst[w.labels == 1] == 1))
+    return {"value": round(n_sig / el, 1), "unit": "sigs/s", "txs": n_tx, "sigs": n_sig,
+            "components": len(w.comps), "component_bytes": comp_bytes,
+            "tx_per_s": round(n_tx / el, 1), "ms_per_step": round(el * 1e3, 3), "kernel_ms": round(full_ms, 3),
+            "tx_ids": {"ms": round(ids_ms, 3), "tx_per_s": round(n_tx / (ids_ms * 1e-3), 1),
+                       "input_GBps": round(comp_bytes / (ids_ms * 1e-3) / 1e9, 1)},
+            "parity_vs_generator": parity, "gen_s": round(gen, 1),
+            "note": "BASELINE configs[3] is 1M txs; default 2^18 keeps host-side signing within the bench budget"}
 
 
 def main():
@@ -196,6 +285,11 @@ def main():
             n_e = len(items_rep)
             extra[name] = {"value": round(n_e * max(2, a.steps // 2) / el, 1), "unit": "sigs/s",
                            "items": n_e, "unique_items": pool, "kernel_ms": round(km, 3)}
+
+    if world == 1 and a.mixed_items > 0:
+        extra["notary_mixed"] = bench_mixed(a, wl, eng, dev, stream, run, threads)
+    if world == 1 and a.pipeline_txs > 0:
+        extra["tx_pipeline"] = bench_pipeline(a, wl, eng, dev, stream, threads)
 
     st = status_d.cpu().numpy()
     counts = {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}

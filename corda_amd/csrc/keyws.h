@@ -56,6 +56,21 @@ union BaseSlot {
   Jac ec;
 };
 
+// Per-batch plan: item indices partitioned by scheme class (stable: input order within a
+// class). Each scheme's kernels walk one dense range of `perm`, so no lane idles on another
+// scheme's item, and the per-item workspace is indexed by plan position. (Grouping by key as
+// well was measured: no gain on k_ed_verify, which is VALU-bound, and per-key atomics
+// serialise on a hot key such as a notary's.)
+#define PLAN_ED 0
+#define PLAN_R1 1
+#define PLAN_K1 2
+#define PLAN_CLASSES 3
+struct Plan {
+  const uint32_t* perm;    // plan position -> item index
+  const uint32_t* ranges;  // class c occupies positions [ranges[c], ranges[c + 1])
+};
+__device__ __forceinline__ int plan_class_of_curve(int curve) { return curve == 1 ? PLAN_R1 : PLAN_K1; }
+
 // Key workspace, each region n_keys long (a key is either Ed25519 or ECDSA, so the table and
 // base slots are shared: TabSlot / BaseSlot unions give one stride for both schemes):
 //   hdr      EdKeyHdr (status [+ Abyte])                       64 B
@@ -88,10 +103,34 @@ static inline size_t key_ws_bytes(uint32_t n_keys) {
          n * EC_ROWS * sizeof(EcRowScratch);
 }
 
-// Per-item workspace slot: projective Ed25519 R' awaiting the batched inversion, or the
-// ECDSA stage hand-off. Reused across schemes: k_ed_finish has consumed the Ed25519 slots
-// before the ECDSA stages write theirs, and each curve runs its three stages in turn.
+// Per-item workspace slot (indexed by plan position, so the schemes never share one):
+// projective Ed25519 R' awaiting the batched inversion, or the ECDSA stage hand-off.
 constexpr size_t ITEM_SLOT = sizeof(ge_p2) > sizeof(EcItemWs) ? sizeof(ge_p2) : sizeof(EcItemWs);
+// Item workspace: [slots: n x ITEM_SLOT, by plan position][perm: n x u32]
+//                 [per-block class counts: PLAN_CLASSES x ceil(n / 256) x u32][ranges: 4 x u32]
+struct ItemWs {
+  void* slots;
+  uint32_t* perm;
+  uint32_t* bcnt;
+  uint32_t* ranges;
+};
+static inline ItemWs item_ws(void* base, uint64_t n_items) {
+  const size_t n = n_items ? n_items : 1;
+  uint8_t* p = (uint8_t*)base;
+  ItemWs w;
+  w.slots = p;
+  p += al256(n * ITEM_SLOT);
+  w.perm = (uint32_t*)p;
+  p += al256(n * sizeof(uint32_t));
+  w.bcnt = (uint32_t*)p;
+  p += al256(PLAN_CLASSES * ((n + 255) / 256) * sizeof(uint32_t));
+  w.ranges = (uint32_t*)p;
+  return w;
+}
+static inline size_t item_ws_total(uint64_t n_items) {
+  const size_t n = n_items ? n_items : 1;
+  return al256(n * ITEM_SLOT) + al256(n * sizeof(uint32_t)) + al256(PLAN_CLASSES * ((n + 255) / 256) * 4) + 64;
+}
 
 // Constant tables per context: [Ed25519 B rows][G rows k1][G rows r1][row scratch]
 static inline size_t const_tab_bytes() { return sizeof(EdTab) + 2 * sizeof(EcRowTab) + sizeof(EcRowScratch); }
@@ -113,7 +152,7 @@ void ed_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_a
                        const KeyWs& w, hipStream_t stream);
 void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     const uint8_t* d_msgs, uint64_t msgs_len, void* d_item_ws, const void* d_btab,
+                     const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
                      hipStream_t stream);
 hipError_t ec_upload_constants();
 hipError_t ec_init_const(void* d_btab, hipStream_t stream);
@@ -121,7 +160,7 @@ void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_a
                        const KeyWs& w, hipStream_t stream);
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     const uint8_t* d_msgs, uint64_t msgs_len, void* d_item_ws, const void* d_btab,
+                     const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
                      hipStream_t stream);
 
 }  // namespace cg

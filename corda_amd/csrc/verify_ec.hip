@@ -64,19 +64,24 @@ __global__ void k_ec_grows_init(EcRowTab* __restrict__ out, EcRowScratch* __rest
   ec_g_rows_init<C>(*out, *scratch, c_ec[C]);
 }
 
+// Plan positions of curve C: [ranges[c], ranges[c + 1]), c = plan_class_of_curve(C)
+#define EC_RANGE(C)                                   \
+  const int cls = plan_class_of_curve(C);             \
+  const uint32_t beg = ranges[cls], end = ranges[cls + 1]
+
 template <int C>
-__global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ items, uint64_t n_items,
-                                                 const cg_key* __restrict__ keys, uint32_t n_keys,
+__global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
+                                                 const uint32_t* __restrict__ ranges,
                                                  const EdKeyHdr* __restrict__ hdr,
                                                  const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                  const uint8_t* __restrict__ msgs, uint64_t msgs_len,
                                                  uint32_t mode, uint8_t* __restrict__ status,
                                                  EcItemWs* __restrict__ ws) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_items) return;
+  EC_RANGE(C);
+  const uint64_t p = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= end) return;
+  const uint32_t i = perm[p];
   const cg_item it = items[i];
-  if (it.key_idx >= n_keys) return;
-  if (keys[it.key_idx].scheme != ec_scheme<C>()) return;
   uint8_t st;
   if (hdr[it.key_idx].status != 0) {
     st = CG_KEY_INVALID;
@@ -91,7 +96,7 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
                                      item_msg_arena(it, arena, msgs), round4(item_msg_len(it, arena_len, msgs_len, msgs)),
                                      it.msg_off, it.msg_len);
     if (r == 0) {
-      ws[i] = w;
+      ws[p] = w;
       st = (uint8_t)(EC_PENDING_BASE + C);
     } else {
       st = (uint8_t)r;
@@ -101,22 +106,27 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
 }
 
 template <int C>
-__global__ void __launch_bounds__(256) k_ec_inv(uint64_t n_items, const uint8_t* __restrict__ status,
-                                                EcItemWs* __restrict__ ws) {
-  const uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * EC_INV_K;
-  if (base >= n_items) return;
-  const uint32_t cnt = (uint32_t)((n_items - base) < EC_INV_K ? (n_items - base) : EC_INV_K);
+__global__ void __launch_bounds__(256) k_ec_inv(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
+                                                const uint8_t* __restrict__ status, EcItemWs* __restrict__ ws) {
+  EC_RANGE(C);
+  const uint64_t base = (uint64_t)beg + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * EC_INV_K;
+  if (base >= end) return;
+  const uint32_t cnt = (uint32_t)((end - base) < EC_INV_K ? (end - base) : EC_INV_K);
   uint32_t sel = 0;
-  for (uint32_t k = 0; k < cnt; ++k) sel |= (uint32_t)(status[base + k] == EC_PENDING_BASE + C) << k;
+  for (uint32_t k = 0; k < cnt; ++k) sel |= (uint32_t)(status[perm[base + k]] == EC_PENDING_BASE + C) << k;
   if (!sel) return;
   ecdsa_batch_inv<C, EC_INV_K>(ws + base, cnt, sel, c_ec[C]);
 }
 
 template <int C>
-__global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ items, uint64_t n_items,
+__global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
+                                                   const uint32_t* __restrict__ ranges,
                                                    const TabSlot* __restrict__ tabs,
                                                    const EcRowTab* __restrict__ gtab, uint8_t* __restrict__ status,
                                                    const EcItemWs* __restrict__ ws) {
+  EC_RANGE(C);
+  const uint64_t p0 = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x;
+  if (p0 >= end) return;  // whole block past this curve's range
   __shared__ EcRowTab sG;
   {
     const uint4* src = (const uint4*)gtab;
@@ -124,10 +134,11 @@ __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ i
     for (uint32_t w = threadIdx.x; w < sizeof(EcRowTab) / 16; w += blockDim.x) dst[w] = src[w];
   }
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_items) return;
+  const uint64_t p = p0 + threadIdx.x;
+  if (p >= end) return;
+  const uint32_t i = perm[p];
   if (status[i] != EC_PENDING_BASE + C) return;
-  const EcItemWs w = ws[i];
+  const EcItemWs w = ws[p];
   status[i] = (uint8_t)ecdsa_ladder_check<C>(w.a, w.b, w.r, sG, tabs[items[i].key_idx].ec, c_ec[C]);
 }
 
@@ -162,29 +173,31 @@ void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_a
 }
 
 template <int C>
-static void launch_curve(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
-                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                         const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len, void* d_item_ws,
-                         const void* d_btab, hipStream_t stream) {
+static void launch_curve(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
+                         uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len,
+                         const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
-  const uint64_t grid = (n_items + B - 1) / B;
-  EcItemWs* ws = (EcItemWs*)d_item_ws;
-  hipLaunchKernelGGL(k_ec_prep<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys, w.hdr,
+  const uint64_t grid = (n_items + B - 1) / B;  // a curve's range is at most n_items long
+  EcItemWs* ws = (EcItemWs*)iw.slots;
+  hipLaunchKernelGGL(k_ec_prep<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
                      d_arena, arena_len, d_msgs, msgs_len, mode, d_status, ws);
   const uint64_t igrid = (n_items + (uint64_t)B * EC_INV_K - 1) / ((uint64_t)B * EC_INV_K);
-  hipLaunchKernelGGL(k_ec_inv<C>, dim3((unsigned)igrid), dim3(B), 0, stream, n_items, (const uint8_t*)d_status, ws);
-  hipLaunchKernelGGL(k_ec_ladder<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, w.tab,
+  hipLaunchKernelGGL(k_ec_inv<C>, dim3((unsigned)igrid), dim3(B), 0, stream, iw.perm, iw.ranges,
+                     (const uint8_t*)d_status, ws);
+  hipLaunchKernelGGL(k_ec_ladder<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.tab,
                      gtab(d_btab, C), d_status, (const EcItemWs*)ws);
 }
 
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     const uint8_t* d_msgs, uint64_t msgs_len, void* d_item_ws, const void* d_btab,
+                     const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
                      hipStream_t stream) {
-  launch_curve<CG_CURVE_R1>(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs,
-                            msgs_len, d_item_ws, d_btab, stream);
-  launch_curve<CG_CURVE_K1>(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs,
-                            msgs_len, d_item_ws, d_btab, stream);
+  (void)d_keys;
+  (void)n_keys;
+  launch_curve<CG_CURVE_R1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, d_btab,
+                            stream);
+  launch_curve<CG_CURVE_K1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, d_btab,
+                            stream);
 }
 
 }  // namespace cg

@@ -142,14 +142,17 @@ __device__ __forceinline__ void pick(ge_niels& out, const ge_niels* row, int d) 
   ge_niels_cneg(out, d < 0);
 }
 
-__global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ items, uint64_t n_items,
-                                                   const cg_key* __restrict__ keys, uint32_t n_keys,
+__global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
+                                                   const uint32_t* __restrict__ ranges,
                                                    const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs,
                                                    const EdTab* __restrict__ btab,
                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                    const uint8_t* __restrict__ msgs, uint64_t msgs_len,
                                                    uint32_t mode, uint8_t* __restrict__ status,
                                                    ge_p2* __restrict__ rout) {
+  const uint32_t end = ranges[PLAN_ED + 1];
+  const uint64_t p0 = (uint64_t)ranges[PLAN_ED] + (uint64_t)blockIdx.x * blockDim.x;
+  if (p0 >= end) return;  // whole block past this scheme's range (grids are sized for all items)
   __shared__ EdTab sB;
   {
     const uint4* src = (const uint4*)btab;
@@ -157,11 +160,10 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
     for (uint32_t w = threadIdx.x; w < sizeof(EdTab) / 16; w += blockDim.x) dst[w] = src[w];
   }
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_items) return;
+  const uint64_t p = p0 + threadIdx.x;
+  if (p >= end) return;
+  const uint32_t i = perm[p];
   const cg_item it = items[i];
-  if (it.key_idx >= n_keys) return;
-  if (keys[it.key_idx].scheme != CG_EDDSA_ED25519_SHA512) return;
   const EdKeyHdr* kh = hdr + it.key_idx;
   uint8_t st;
   if (kh->status != 0) {
@@ -207,7 +209,7 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
     sc_recode_w<ED_W>(es, EdCfg::kPackedWords, sr);
     ge_p2 q;
     ed_double_scalar_w<ED_W, ED_K>(q, eh, es, tabs[it.key_idx].ed, sB);
-    rout[i] = q;
+    rout[p] = q;
     st = (uint8_t)ED_PENDING;
   }
   status[i] = st;
@@ -216,18 +218,20 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
 // Encode + compare for 16 consecutive items per lane: one inversion per lane (Montgomery's
 // trick) instead of one per item.
 #define ED_FINISH_K 16
-__global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ items, uint64_t n_items,
+__global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
+                                                   const uint32_t* __restrict__ ranges,
                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                    uint8_t* __restrict__ status, const ge_p2* __restrict__ rin) {
-  const uint64_t base = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * ED_FINISH_K;
-  if (base >= n_items) return;
-  const uint32_t cnt = (uint32_t)((n_items - base) < ED_FINISH_K ? (n_items - base) : ED_FINISH_K);
+  const uint32_t end = ranges[PLAN_ED + 1];
+  const uint64_t base = (uint64_t)ranges[PLAN_ED] + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * ED_FINISH_K;
+  if (base >= end) return;
+  const uint32_t cnt = (uint32_t)((end - base) < ED_FINISH_K ? (end - base) : ED_FINISH_K);
   fe acc[ED_FINISH_K];
   fe run;
   fe_1(run);
   uint32_t pend = 0;
   for (uint32_t k = 0; k < cnt; ++k) {
-    const bool p = status[base + k] == ED_PENDING;
+    const bool p = status[perm[base + k]] == ED_PENDING;
     pend |= (uint32_t)p << k;
     if (p) {
       fe_mul(run, run, rin[base + k].Z);
@@ -249,11 +253,12 @@ __global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ i
     fe_mul(t, inv, rin[base + k].Z);
     fe_copy(inv, t);
     const ge_p2 P = rin[base + k];
+    const uint32_t i = perm[base + k];
     uint32_t rw[8];
-    const uint64_t so = items[base + k].sig_off;
+    const uint64_t so = items[i].sig_off;
 #pragma unroll
     for (int w = 0; w < 8; ++w) rw[w] = cg_ld_bytes4(arena, lr, so + 4 * w);
-    status[base + k] = (uint8_t)ed_encode_cmp(P, zi, rw);
+    status[i] = (uint8_t)ed_encode_cmp(P, zi, rw);
   }
 }
 
@@ -280,16 +285,17 @@ void ed_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_a
 
 void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     const uint8_t* d_msgs, uint64_t msgs_len, void* d_item_ws, const void* d_btab,
+                     const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
                      hipStream_t stream) {
+  (void)d_keys;
+  (void)n_keys;
   const uint32_t B = 256;
-  const uint64_t grid = (n_items + B - 1) / B;
-  hipLaunchKernelGGL(k_ed_verify, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys, w.hdr,
-                     w.tab, (const EdTab*)d_btab, d_arena, arena_len, d_msgs, msgs_len, mode, d_status,
-                     (ge_p2*)d_item_ws);
+  const uint64_t grid = (n_items + B - 1) / B;  // the Ed25519 range is at most n_items long
+  hipLaunchKernelGGL(k_ed_verify, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, w.tab,
+                     (const EdTab*)d_btab, d_arena, arena_len, d_msgs, msgs_len, mode, d_status, (ge_p2*)iw.slots);
   const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
-  hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, n_items, d_arena, arena_len,
-                     d_status, (const ge_p2*)d_item_ws);
+  hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
+                     arena_len, d_status, (const ge_p2*)iw.slots);
 }
 
 }  // namespace cg

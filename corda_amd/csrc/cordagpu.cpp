@@ -65,6 +65,7 @@ struct DevBuf {
 struct cg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  cg::Fork fork = {{nullptr, nullptr}, nullptr, {nullptr, nullptr}};
   std::mutex mu;
   DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
   // transaction pipeline: verify items, spliced messages, templates; host-entry staging
@@ -107,15 +108,17 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     delete c;
     return hip_fail(e, "hipStreamCreate");
   }
-  e = cg::upload_constants();
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamCreateWithFlags(&c->fork.side[k], hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.start, hipEventDisableTiming);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.done[k], hipEventDisableTiming);
+  if (e == hipSuccess) e = cg::upload_constants();
   if (e == hipSuccess) e = c->btab.ensure(cg::btab_bytes());
   if (e == hipSuccess) e = cg::init_btab(c->btab.p, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
-    c->btab.release();
-    hipStreamDestroy(c->stream);
-    delete c;
-    return hip_fail(e, "upload_constants / base-point table");
+    const int rc = hip_fail(e, "side streams / upload_constants / base-point tables");
+    cg_close(c);
+    return rc;
   }
   *out = c;
   return CG_OK;
@@ -137,6 +140,14 @@ void cg_close(cg_ctx* c) {
   c->aux2.release();
   for (DevBuf* b : {&c->txitems, &c->msgs, &c->tmpls, &c->h_txs, &c->h_comps, &c->h_sigs, &c->h_ids, &c->h_txst})
     b->release();
+  for (int k = 0; k < 2; ++k) {
+    if (c->fork.side[k]) {
+      hipStreamSynchronize(c->fork.side[k]);
+      hipStreamDestroy(c->fork.side[k]);
+    }
+    if (c->fork.done[k]) hipEventDestroy(c->fork.done[k]);
+  }
+  if (c->fork.start) hipEventDestroy(c->fork.start);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -166,7 +177,7 @@ int cg_verify_batch_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   }
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIP_TRY(cg::launch_verify(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p,
-                            c->itemws.p, c->btab.p, s),
+                            c->itemws.p, c->btab.p, s, nullptr, 0, &c->fork),
           "launch_verify");
   return CG_OK;
 }
@@ -182,7 +193,7 @@ int cg_prepare_keys_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
     HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
   }
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  HIP_TRY(cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s), "launch_keyprep");
+  HIP_TRY(cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork), "launch_keyprep");
   return CG_OK;
 }
 
@@ -237,7 +248,7 @@ int cg_verify_batch(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_ite
   HIP_TRY(hipEventRecord(ev[1], s), "hipEventRecord");
   HIP_TRY(cg::launch_verify((const cg_key*)c->keys.p, n_keys, (const cg_item*)c->items.p, n_items,
                             (const uint8_t*)c->arena.p, arena_len, mode, (uint8_t*)c->status.p, c->keyprep.p,
-                            c->itemws.p, c->btab.p, s),
+                            c->itemws.p, c->btab.p, s, nullptr, 0, &c->fork),
           "launch_verify");
   HIP_TRY(hipEventRecord(ev[2], s), "hipEventRecord");
   HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n_items, hipMemcpyDeviceToHost, s), "D2H status");
@@ -420,7 +431,7 @@ static int verify_transactions_locked(cg_ctx* c, const cg_tx* d_txs, uint64_t n_
           "launch_tx_sig_items");
   HIP_TRY(cg::launch_verify(d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode,
                             d_sig_status, c->keyprep.p, c->itemws.p, c->btab.p, s, (const uint8_t*)c->msgs.p,
-                            slot * n_sigs),
+                            slot * n_sigs, &c->fork),
           "launch_verify");
   return CG_OK;
 }

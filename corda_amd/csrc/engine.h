@@ -9,6 +9,14 @@ namespace cg {
 
 struct DeviceConsts;  // opaque
 
+// Two side streams + events owned by a context: key preparation of the two ECDSA curves runs
+// on them concurrently with the Ed25519 key preparation (each is a latency-bound chain of
+// doublings on few waves), joined back into the caller's stream before anything reads keys.
+struct Fork {
+  hipStream_t side[2];
+  hipEvent_t start, done[2];
+};
+
 // Upload the constant tables (curve constants, base-point tables) for the current device.
 hipError_t upload_constants();
 
@@ -20,14 +28,14 @@ size_t keyprep_bytes(uint32_t n_keys);
 hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                          const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
                          void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
-                         const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0);
+                         const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0, const Fork* fork = nullptr);
 // Constant base-point row table: size and one-time initialisation (per context).
 size_t btab_bytes();
 hipError_t init_btab(void* d_btab, hipStream_t stream);
 // Bytes of per-item workspace (projective Ed25519 results awaiting the batched inversion).
 size_t item_ws_bytes(uint64_t n_items);
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                          void* d_keyprep, hipStream_t stream);
+                          void* d_keyprep, hipStream_t stream, const Fork* fork = nullptr);
 // `d_msgs` (optional): the engine's spliced-message workspace, read by items flagged
 // CG_ITEM_MSG_WS (keyws.h); caller items never carry that flag.
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,

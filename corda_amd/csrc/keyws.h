@@ -157,7 +157,7 @@ void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_ite
 hipError_t ec_upload_constants();
 hipError_t ec_init_const(void* d_btab, hipStream_t stream);
 void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                       const KeyWs& w, hipStream_t stream);
+                       const KeyWs& w, hipStream_t stream_r1, hipStream_t stream_k1);
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
                      const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,

@@ -158,18 +158,18 @@ hipError_t ec_init_const(void* d_btab, hipStream_t stream) {
 }
 
 void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                       const KeyWs& w, hipStream_t stream) {
+                       const KeyWs& w, hipStream_t stream_r1, hipStream_t stream_k1) {
   const uint32_t B = 64;
   const dim3 g((n_keys + B - 1) / B);
-  hipLaunchKernelGGL(k_ec_keyprep_rows<CG_CURVE_R1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len,
-                     w.hdr, w.bases);
-  hipLaunchKernelGGL(k_ec_keyprep_rows<CG_CURVE_K1>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len,
-                     w.hdr, w.bases);
   const uint32_t elanes = n_keys * EC_ROWS;
-  hipLaunchKernelGGL(k_ec_keyprep_tab<CG_CURVE_R1>, dim3((elanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys,
-                     w.hdr, w.bases, w.tab, w.ecs);
-  hipLaunchKernelGGL(k_ec_keyprep_tab<CG_CURVE_K1>, dim3((elanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys,
-                     w.hdr, w.bases, w.tab, w.ecs);
+  hipLaunchKernelGGL(k_ec_keyprep_rows<CG_CURVE_R1>, g, dim3(B), 0, stream_r1, d_keys, n_keys, d_arena, arena_len,
+                     w.hdr, w.bases);
+  hipLaunchKernelGGL(k_ec_keyprep_tab<CG_CURVE_R1>, dim3((elanes + B - 1) / B), dim3(B), 0, stream_r1, d_keys,
+                     n_keys, w.hdr, w.bases, w.tab, w.ecs);
+  hipLaunchKernelGGL(k_ec_keyprep_rows<CG_CURVE_K1>, g, dim3(B), 0, stream_k1, d_keys, n_keys, d_arena, arena_len,
+                     w.hdr, w.bases);
+  hipLaunchKernelGGL(k_ec_keyprep_tab<CG_CURVE_K1>, dim3((elanes + B - 1) / B), dim3(B), 0, stream_k1, d_keys,
+                     n_keys, w.hdr, w.bases, w.tab, w.ecs);
 }
 
 template <int C>

@@ -325,3 +325,40 @@ extern "C" int t_ecdsa_verify_rows(int scheme, const uint8_t* arena, uint64_t ar
     return ecdsa_rows_verify<CG_CURVE_R1>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len);
   return ecdsa_rows_verify<CG_CURVE_K1>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len);
 }
+
+// ---------------------------------------------------------------- 29-bit Montgomery
+#include "../../corda_amd/csrc/mont29.h"
+template <int C, int N>
+static void m29_mul_words(const uint32_t* a, const uint32_t* b, uint32_t* out, int lazy) {
+  f29 x, y, r;
+  f29_from_words(x, a);
+  f29_from_words(y, b);
+  if (lazy) {  // feed x + x and y + y (limbs < 2^30, value < 4m) as the operands
+    m29_add_lazy(x, x, x);
+    m29_add_lazy(y, y, y);
+  }
+  m29_mul<C, N>(r, x, y);
+  m29_to_words_canon<C, N>(out, r);
+}
+extern "C" void t_m29_op(int curve, int n, int op, const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  // op 0: a b R^-1; 1: (2a)(2b) R^-1 via lazy sums; 2: a + b; 3: a - b (inputs reduced < 2m)
+  if (op <= 1) {
+    if (curve == 1 && n == 0) m29_mul_words<1, 0>(a, b, out, op);
+    else if (curve == 1) m29_mul_words<1, 1>(a, b, out, op);
+    else if (n == 0) m29_mul_words<0, 0>(a, b, out, op);
+    else m29_mul_words<0, 1>(a, b, out, op);
+    return;
+  }
+  f29 x, y, r;
+  f29_from_words(x, a);
+  f29_from_words(y, b);
+#define M29_BIN(CC, NN)                                    \
+  if (op == 2) m29_add<CC, NN>(r, x, y);                   \
+  else m29_sub<CC, NN>(r, x, y);                           \
+  m29_to_words_canon<CC, NN>(out, r);
+  if (curve == 1 && n == 0) { M29_BIN(1, 0) }
+  else if (curve == 1) { M29_BIN(1, 1) }
+  else if (n == 0) { M29_BIN(0, 0) }
+  else { M29_BIN(0, 1) }
+#undef M29_BIN
+}

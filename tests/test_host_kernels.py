@@ -178,3 +178,41 @@ def test_ecdsa_lane_verify_on_fixtures(fn):
         assert names[st] == it["expect_isvalid"], (it["class"], it["note"])
         n += 1
     assert n > 300
+
+
+M29_MODS = {(1, 0): 2 ** 256 - 2 ** 224 + 2 ** 192 + 2 ** 96 - 1,
+            (1, 1): 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551,
+            (0, 0): 2 ** 256 - 2 ** 32 - 977,
+            (0, 1): 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141}
+
+
+@pytest.mark.parametrize("curve,n", sorted(M29_MODS))
+def test_mont29_ops(curve, n):
+    """mont29.h (ECDSA field / scalar arithmetic) against Python integers, including values
+    in [m, 2m) (the reduced range) and the lazy-sum operands, with every column bound asserted."""
+    import ctypes
+    lib = hostk.lib()
+    lib.t_m29_op.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p]
+    m = M29_MODS[(curve, n)]
+    rinv = pow(2 ** 261, -1, m)
+    rng = random.Random(curve * 2 + n)
+    edge = [0, 1, m - 1, m, m + 1, 2 * m - 1, 2 ** 256 - 1 if 2 ** 256 - 1 < 2 * m else 2 * m - 2]
+    vals = edge + [rng.randrange(0, 2 * m) for _ in range(300)]
+    out = np.zeros(8, dtype=np.uint32)
+
+    def w(x):
+        return np.frombuffer(x.to_bytes(32, "little"), dtype=np.uint32).copy()
+
+    for t in range(len(vals)):
+        a, b = vals[t], vals[(t * 7 + 3) % len(vals)]
+        if a >= 2 ** 256 or b >= 2 ** 256:
+            continue
+        lib.t_m29_op(curve, n, 0, ptr(w(a)), ptr(w(b)), ptr(out))
+        assert int.from_bytes(out.tobytes(), "little") == a * b * rinv % m
+        lib.t_m29_op(curve, n, 1, ptr(w(a)), ptr(w(b)), ptr(out))
+        assert int.from_bytes(out.tobytes(), "little") == 4 * a * b * rinv % m
+        lib.t_m29_op(curve, n, 2, ptr(w(a)), ptr(w(b)), ptr(out))
+        assert int.from_bytes(out.tobytes(), "little") == (a + b) % m
+        lib.t_m29_op(curve, n, 3, ptr(w(a)), ptr(w(b)), ptr(out))
+        assert int.from_bytes(out.tobytes(), "little") == (a - b) % m

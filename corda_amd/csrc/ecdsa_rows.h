@@ -5,8 +5,8 @@
 // A scalar k < 2^256 is recoded into 43 signed digits e_t in [-32, 32]; digit t = 4j + i
 // belongs to row j (11 rows) and window i (4 windows):
 //     [k] P = sum_{i<4} 2^{6i} sum_{j<11} e_{4j+i} P_j,   P_j = 2^{24j} P.
-// Each row stores the affine multiples 1..32 of P_j (x, y in Montgomery form, 64 B each):
-// 22 528 B per point. The G rows are built once per context; the Q rows once per key.
+// Each row stores the affine multiples 1..32 of P_j (x, y in Montgomery form, 72 B each):
+// 25 344 B per point. The G rows are built once per context; the Q rows once per key.
 // The loop does 18 Jacobian doublings and one mixed addition per non-zero digit (<= 86),
 // against BouncyCastle's ~256 doublings + wNAF additions (ECAlgorithms.sumOfTwoMultiplies).
 // Exception cases (R = +-T, R = infinity) are handled inside jac_madd, so adversarial
@@ -22,7 +22,7 @@
 #define EC_PACKED 11
 
 struct EcAff {
-  u256w x, y;  // affine, Montgomery form
+  f29 x, y;  // affine, Montgomery form
 };
 
 struct EcRowTab {
@@ -55,55 +55,53 @@ CG_HD int ec_digit6(const uint32_t* packed, int t) {
 // General Jacobian addition r = p + q (add-2007-bl), exception-complete.
 template <int C>
 CG_HD void jac_add(Jac& r, const Jac& p, const Jac& q, const EcConsts& K) {
-  if (u256_iszero(p.Z)) {
+  if (m29_iszero<C, 0>(p.Z)) {
     r = q;
     return;
   }
-  if (u256_iszero(q.Z)) {
+  if (m29_iszero<C, 0>(q.Z)) {
     r = p;
     return;
   }
-  u256w Z1Z1, Z2Z2, U1, U2, S1, S2, H, rr, I, J, V, t;
-  mm_sq<C, 0>(Z1Z1, p.Z);
-  mm_sq<C, 0>(Z2Z2, q.Z);
-  mm_mul<C, 0>(U1, p.X, Z2Z2);
-  mm_mul<C, 0>(U2, q.X, Z1Z1);
-  mm_mul<C, 0>(S1, p.Y, q.Z);
-  mm_mul<C, 0>(S1, S1, Z2Z2);
-  mm_mul<C, 0>(S2, q.Y, p.Z);
-  mm_mul<C, 0>(S2, S2, Z1Z1);
-  mm_sub<C, 0>(H, U2, U1);
-  mm_sub<C, 0>(rr, S2, S1);
-  if (u256_iszero(H)) {
-    if (u256_iszero(rr)) {
+  f29 Z1Z1, Z2Z2, U1, U2, S1, S2, H, rr, I, J, V, t;
+  m29_sq<C, 0>(Z1Z1, p.Z);
+  m29_sq<C, 0>(Z2Z2, q.Z);
+  m29_mul<C, 0>(U1, p.X, Z2Z2);
+  m29_mul<C, 0>(U2, q.X, Z1Z1);
+  m29_mul<C, 0>(S1, p.Y, q.Z);
+  m29_mul<C, 0>(S1, S1, Z2Z2);
+  m29_mul<C, 0>(S2, q.Y, p.Z);
+  m29_mul<C, 0>(S2, S2, Z1Z1);
+  m29_sub<C, 0>(H, U2, U1);
+  m29_sub<C, 0>(rr, S2, S1);
+  if (m29_iszero<C, 0>(H)) {
+    if (m29_iszero<C, 0>(rr)) {
       jac_dbl<C>(r, p);
     } else {
-      u256_zero(r.X);
-      r.Y = K.one_p;
-      u256_zero(r.Z);
+      jac_set_inf<C>(r, K);
     }
     return;
   }
-  mm_add<C, 0>(I, H, H);
-  mm_sq<C, 0>(I, I);
-  mm_mul<C, 0>(J, H, I);
-  mm_add<C, 0>(rr, rr, rr);
-  mm_mul<C, 0>(V, U1, I);
+  m29_add_lazy(I, H, H);
+  m29_sq<C, 0>(I, I);
+  m29_mul<C, 0>(J, H, I);
+  m29_mul<C, 0>(V, U1, I);
+  m29_add_lazy(rr, rr, rr);
   Jac o;
-  mm_sq<C, 0>(o.X, rr);
-  mm_sub<C, 0>(o.X, o.X, J);
-  mm_add<C, 0>(t, V, V);
-  mm_sub<C, 0>(o.X, o.X, t);
-  mm_sub<C, 0>(t, V, o.X);
-  mm_mul<C, 0>(o.Y, rr, t);
-  mm_mul<C, 0>(t, S1, J);
-  mm_add<C, 0>(t, t, t);
-  mm_sub<C, 0>(o.Y, o.Y, t);
-  mm_add<C, 0>(t, p.Z, q.Z);
-  mm_sq<C, 0>(t, t);
-  mm_sub<C, 0>(t, t, Z1Z1);
-  mm_sub<C, 0>(t, t, Z2Z2);
-  mm_mul<C, 0>(o.Z, t, H);
+  m29_sq<C, 0>(o.X, rr);
+  m29_sub<C, 0>(o.X, o.X, J);
+  m29_add<C, 0>(t, V, V);
+  m29_sub<C, 0>(o.X, o.X, t);
+  m29_sub<C, 0>(t, V, o.X);
+  m29_mul<C, 0>(o.Y, rr, t);
+  m29_add_lazy(t, S1, S1);
+  m29_mul<C, 0>(t, t, J);
+  m29_sub<C, 0>(o.Y, o.Y, t);
+  m29_add_lazy(t, p.Z, q.Z);
+  m29_sq<C, 0>(t, t);
+  m29_sub<C, 0>(t, t, Z1Z1);
+  m29_sub<C, 0>(t, t, Z2Z2);
+  m29_mul<C, 0>(o.Z, t, H);
   r = o;
 }
 
@@ -120,7 +118,7 @@ CG_HD void jac_dbl_n(Jac& r, const Jac& p, int n) {
 // through memory, not registers). One field inversion per row.
 struct EcRowScratch {
   Jac p[EC_MULT];
-  u256w pre[EC_MULT];
+  f29 pre[EC_MULT];
 };
 
 template <int C>
@@ -131,28 +129,28 @@ CG_HD void ec_row_build(EcAff* row, const Jac& base, EcRowScratch& s, const EcCo
   for (int k = 1; k < EC_MULT; ++k) {
     jac_add<C>(acc, acc, base, K);  // k = 1: P + P goes through the doubling branch
     s.p[k] = acc;
-    mm_mul<C, 0>(s.pre[k], s.pre[k - 1], acc.Z);
+    m29_mul<C, 0>(s.pre[k], s.pre[k - 1], acc.Z);
   }
-  u256w inv;
-  mm_inv<C, 0>(inv, s.pre[EC_MULT - 1], K.one_p);
+  f29 inv;
+  m29_inv<C, 0>(inv, s.pre[EC_MULT - 1], K.one_p);
   for (int k = EC_MULT - 1; k >= 0; --k) {
-    u256w zi, zi2, zi3;
+    f29 zi, zi2, zi3;
     if (k > 0) {
-      mm_mul<C, 0>(zi, inv, s.pre[k - 1]);
-      mm_mul<C, 0>(inv, inv, s.p[k].Z);
+      m29_mul<C, 0>(zi, inv, s.pre[k - 1]);
+      m29_mul<C, 0>(inv, inv, s.p[k].Z);
     } else {
       zi = inv;
     }
-    mm_sq<C, 0>(zi2, zi);
-    mm_mul<C, 0>(zi3, zi2, zi);
-    mm_mul<C, 0>(row[k].x, s.p[k].X, zi2);
-    mm_mul<C, 0>(row[k].y, s.p[k].Y, zi3);
+    m29_sq<C, 0>(zi2, zi);
+    m29_mul<C, 0>(zi3, zi2, zi);
+    m29_mul<C, 0>(row[k].x, s.p[k].X, zi2);
+    m29_mul<C, 0>(row[k].y, s.p[k].Y, zi3);
   }
 }
 
 // The 11 row bases 2^{24j} P of an affine (Montgomery) point.
 template <int C>
-CG_HD void ec_row_bases(Jac bases[EC_ROWS], const u256w& xm, const u256w& ym, const EcConsts& K) {
+CG_HD void ec_row_bases(Jac bases[EC_ROWS], const f29& xm, const f29& ym, const EcConsts& K) {
   Jac P = {xm, ym, K.one_p};
   for (int j = 0; j < EC_ROWS; ++j) {
     bases[j] = P;
@@ -163,26 +161,18 @@ CG_HD void ec_row_bases(Jac bases[EC_ROWS], const u256w& xm, const u256w& ym, co
 // Key decode (BC 1.57 semantics: SPKI / raw / SEC1, point validated on the curve) to the
 // affine point in Montgomery form. Returns 0 ok / 3 KEY_INVALID.
 template <int C>
-CG_HD uint32_t ec_key_decode_xy(u256w& xm, u256w& ym, const u256w& x, const u256w& y, const EcConsts& K) {
+CG_HD uint32_t ec_key_decode_xy(f29& xm, f29& ym, const u256w& x, const u256w& y, const EcConsts& K) {
   if (!u256_lt_mod<C, 0>(x) || !u256_lt_mod<C, 0>(y)) return 3;
-  u256w l, rr;
-  mm_mul<C, 0>(xm, x, K.r2_p);
-  mm_mul<C, 0>(ym, y, K.r2_p);
-  mm_sq<C, 0>(l, ym);
-  mm_sq<C, 0>(rr, xm);
-  mm_mul<C, 0>(rr, rr, xm);
-  if (C == CG_CURVE_R1) {  // x^3 - 3x + b
-    u256w t;
-    mm_add<C, 0>(t, xm, xm);
-    mm_add<C, 0>(t, t, xm);
-    mm_sub<C, 0>(rr, rr, t);
-  }
-  mm_add<C, 0>(rr, rr, K.b_m);
-  return u256_eq(l, rr) ? 0u : 3u;
+  f29 l, rhs;
+  m29_from_plain<C, 0>(xm, x, K.r2_p);
+  m29_from_plain<C, 0>(ym, y, K.r2_p);
+  m29_sq<C, 0>(l, ym);
+  ec_rhs<C>(rhs, xm, K);
+  return m29_eq<C, 0>(l, rhs) ? 0u : 3u;
 }
 
 template <int C>
-CG_HD uint32_t ec_key_decode_bytes(u256w& xm, u256w& ym, const uint8_t* arena, uint64_t lr, uint64_t off,
+CG_HD uint32_t ec_key_decode_bytes(f29& xm, f29& ym, const uint8_t* arena, uint64_t lr, uint64_t off,
                                    uint32_t len, uint32_t fmt, const EcConsts& K) {
   u256w x, y;
   uint64_t pt = off;
@@ -253,41 +243,43 @@ CG_HD uint32_t ecdsa_prep(EcItemWs& ws, const uint8_t* arena, uint64_t lr, uint6
 }
 
 // Stage 2 (per group): w = s^-1 by one shared inversion (Montgomery's trick); u1 = e w,
-// u2 = r w (plain). `sel` marks the pending items of this curve among ws[0..cnt).
+// u2 = r w as canonical plain words. `sel` marks the pending items of this curve among
+// ws[0..cnt).
 template <int C, int G>
 CG_HD void ecdsa_batch_inv(EcItemWs* ws, uint32_t cnt, uint32_t sel, const EcConsts& K) {
-  u256w pre[G];
-  u256w run = K.one_n;
+  f29 pre[G];
+  f29 run = K.one_n;
   for (uint32_t k = 0; k < cnt; ++k) {
     if ((sel >> k) & 1u) {
-      u256w sm;
-      mm_mul<C, 1>(sm, ws[k].a, K.r2_n);  // s * R (Montgomery)
-      mm_mul<C, 1>(run, run, sm);
+      f29 sm;
+      m29_from_plain<C, 1>(sm, ws[k].a, K.r2_n);  // s R
+      m29_mul<C, 1>(run, run, sm);
     }
     pre[k] = run;
   }
   if (!sel) return;
-  u256w inv;
-  mm_inv<C, 1>(inv, run, K.one_n);  // (prod s R)^-1 R
+  f29 inv;
+  m29_inv<C, 1>(inv, run, K.one_n);  // (prod s)^-1 R
   for (int k = (int)cnt - 1; k >= 0; --k) {
     if (!((sel >> k) & 1u)) continue;
     int prev = k - 1;
     while (prev >= 0 && !((sel >> prev) & 1u)) --prev;
-    u256w wm, sm;
-    if (prev >= 0) mm_mul<C, 1>(wm, inv, pre[prev]);
+    f29 wm, sm, t, u;
+    if (prev >= 0) m29_mul<C, 1>(wm, inv, pre[prev]);  // s_k^-1 R
     else wm = inv;
-    mm_mul<C, 1>(sm, ws[k].a, K.r2_n);
-    mm_mul<C, 1>(inv, inv, sm);
-    u256w u1, u2;
-    mm_mul<C, 1>(u1, ws[k].b, wm);
-    mm_mul<C, 1>(u2, ws[k].r, wm);
-    ws[k].a = u1;
-    ws[k].b = u2;
+    m29_from_plain<C, 1>(sm, ws[k].a, K.r2_n);
+    m29_mul<C, 1>(inv, inv, sm);
+    f29_from_words(t, ws[k].b.w);  // e (plain)
+    m29_mul<C, 1>(u, t, wm);       // e w (plain)
+    m29_to_words_canon<C, 1>(ws[k].a.w, u);
+    f29_from_words(t, ws[k].r.w);  // r (plain)
+    m29_mul<C, 1>(u, t, wm);       // r w (plain)
+    m29_to_words_canon<C, 1>(ws[k].b.w, u);
   }
 }
 
 template <class RowT>
-CG_HD void ec_pick(u256w& x, u256w& y, const RowT* row, int a) {
+CG_HD void ec_pick(f29& x, f29& y, const RowT* row, int a) {
   const EcAff& e = row[a - 1];
   x = e.x;
   y = e.y;
@@ -302,9 +294,7 @@ CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w&
   ec_recode_w6(d1, u1);
   ec_recode_w6(d2, u2);
   Jac R;
-  u256_zero(R.X);
-  R.Y = K.one_p;
-  u256_zero(R.Z);
+  jac_set_inf<C>(R, K);
   for (int i = EC_WINDOWS - 1; i >= 0; --i) {
     if (i != EC_WINDOWS - 1) {
 #pragma unroll 1
@@ -316,26 +306,26 @@ CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w&
       if (t >= EC_DIGITS) continue;
       const int a = ec_digit6(d1, t);
       if (a != 0) {
-        u256w x, y;
+        f29 x, y;
         ec_pick(x, y, TG.t[j], a < 0 ? -a : a);
-        if (a < 0) mm_neg<C, 0>(y, y);
+        if (a < 0) m29_neg<C, 0>(y, y);
         jac_madd<C>(R, R, x, y, K);
       }
       const int b = ec_digit6(d2, t);
       if (b != 0) {
-        u256w x, y;
+        f29 x, y;
         ec_pick(x, y, TQ.t[j], b < 0 ? -b : b);
-        if (b < 0) mm_neg<C, 0>(y, y);
+        if (b < 0) m29_neg<C, 0>(y, y);
         jac_madd<C>(R, R, x, y, K);
       }
     }
   }
-  if (u256_iszero(R.Z)) return 1;
-  u256w z2, t, rm;
-  mm_sq<C, 0>(z2, R.Z);
-  mm_mul<C, 0>(rm, r, K.r2_p);
-  mm_mul<C, 0>(t, rm, z2);
-  if (u256_eq(t, R.X)) return 0;
+  if (m29_iszero<C, 0>(R.Z)) return 1;
+  f29 z2, t, rm;
+  m29_sq<C, 0>(z2, R.Z);
+  m29_from_plain<C, 0>(rm, r, K.r2_p);
+  m29_mul<C, 0>(t, rm, z2);
+  if (m29_eq<C, 0>(t, R.X)) return 0;
   u256w rn;
   uint64_t c = 0;
 #pragma unroll
@@ -345,9 +335,9 @@ CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w&
     c >>= 32;
   }
   if (c == 0 && u256_lt_mod<C, 0>(rn)) {
-    mm_mul<C, 0>(rm, rn, K.r2_p);
-    mm_mul<C, 0>(t, rm, z2);
-    if (u256_eq(t, R.X)) return 0;
+    m29_from_plain<C, 0>(rm, rn, K.r2_p);
+    m29_mul<C, 0>(t, rm, z2);
+    if (m29_eq<C, 0>(t, R.X)) return 0;
   }
   return 1;
 }
@@ -356,6 +346,6 @@ CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w&
 template <int C>
 CG_HD void ec_g_rows_init(EcRowTab& T, EcRowScratch& s, const EcConsts& K) {
   Jac bases[EC_ROWS];
-  ec_row_bases<C>(bases, K.gx[1], K.gy[1], K);
+  ec_row_bases<C>(bases, K.gx, K.gy, K);
   for (int j = 0; j < EC_ROWS; ++j) ec_row_build<C>(T.t[j], bases[j], s, K);
 }

@@ -34,7 +34,7 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_rows(const cg_key* __restrict
   for (int w = 0; w < 8; ++w) h.abyte[w] = 0;
   h.status = CG_KEY_INVALID;
   if (in_arena(k.off, k.len, arena_len)) {
-    u256w xm, ym;
+    f29 xm, ym;
     if (ec_key_decode_bytes<C>(xm, ym, arena, round4(arena_len), k.off, k.len, k.fmt, c_ec[C]) == 0) {
       h.status = 0;
       Jac b[EC_ROWS];

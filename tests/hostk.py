@@ -31,12 +31,10 @@ def lib():
     if _lib is None:
         L = build()
         vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
-        L.t_ecdsa_verify.argtypes = [i32, vp, u64, u64, u32, u32, u64, u32, u64, u64]
         L.t_ecdsa_verify_rows.argtypes = [i32, vp, u64, u64, u32, u32, u64, u32, u64, u64]
         L.t_ed_verify.argtypes = [vp, vp, vp, u64]
         L.t_sha512_prefix.argtypes = [vp, vp, u64, u64, vp]
         L.t_sha256_suffix.argtypes = [vp, u64, u64, vp, vp]
-        L.t_mm_mul.argtypes = [i32, i32, vp, vp, vp]
         L.t_ed_count_w6.argtypes = [vp, vp, vp, u64, vp]
         _lib = L
     return _lib

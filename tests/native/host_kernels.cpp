@@ -92,34 +92,6 @@ static void kinit() {
     g_kinit = 1;
   }
 }
-extern "C" {
-// scheme 2 = k1, 3 = r1. arena holds key then sig then msg (offsets given). Returns status.
-int t_ecdsa_verify(int scheme, const uint8_t* arena, uint64_t arena_len, uint64_t key_off, uint32_t key_len,
-                   uint32_t fmt, uint64_t sig_off, uint32_t sig_len, uint64_t msg_off, uint64_t msg_len) {
-  kinit();
-  static EcKeyPrep kp;
-  const uint64_t lr = (arena_len + 3) & ~3ull;
-  if (scheme == 3) {
-    uint32_t st = ec_key_prep_bytes<CG_CURVE_R1>(kp, arena, lr, key_off, key_len, fmt, g_K[1]);
-    if (st) return (int)st;
-    return (int)ecdsa_verify_core<CG_CURVE_R1>(kp, arena, lr, sig_off, sig_len, msg_off, msg_len, g_K[1]);
-  }
-  uint32_t st = ec_key_prep_bytes<CG_CURVE_K1>(kp, arena, lr, key_off, key_len, fmt, g_K[0]);
-  if (st) return (int)st;
-  return (int)ecdsa_verify_core<CG_CURVE_K1>(kp, arena, lr, sig_off, sig_len, msg_off, msg_len, g_K[0]);
-}
-void t_mm_mul(int curve, int n, const uint32_t* a, const uint32_t* b, uint32_t* out) {
-  u256w x, y, r;
-  memcpy(x.w, a, 32);
-  memcpy(y.w, b, 32);
-  if (curve == 1 && n == 0) mm_mul<1, 0>(r, x, y);
-  else if (curve == 1) mm_mul<1, 1>(r, x, y);
-  else if (n == 0) mm_mul<0, 0>(r, x, y);
-  else mm_mul<0, 1>(r, x, y);
-  memcpy(out, r.w, 32);
-}
-}
-
 // ---------------------------------------------------------------- Ed25519 v2 (row tables)
 static EdRowTab g_TB;
 static int g_rinit = 0;
@@ -305,7 +277,7 @@ static int ecdsa_rows_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
     TG[C] = new EcRowTab;
     ec_g_rows_init<C>(*TG[C], *S, K);
   }
-  u256w xm, ym;
+  f29 xm, ym;
   uint32_t st = ec_key_decode_bytes<C>(xm, ym, arena, lr, key_off, key_len, fmt, K);
   if (st) return (int)st;
   Jac bases[EC_ROWS];

@@ -160,10 +160,11 @@ def test_executed_work_constants_match_lane_code():
     assert (mul_i, sq_i) == bench.ED_INVERT_FE, (mul_i, sq_i)
 
 
-@pytest.mark.parametrize("fn", ["t_ecdsa_verify", "t_ecdsa_verify_rows"])
+@pytest.mark.parametrize("fn", ["t_ecdsa_verify_rows"])
 def test_ecdsa_lane_verify_on_fixtures(fn):
-    """ECDSA lane code (the fixed-window core and the row-table pipeline: prep -> batched
-    inverse -> ladder + x-check) on every ECDSA fixture, isValid semantics."""
+    """ECDSA lane code (the row-table pipeline: key decode -> rows -> prep -> batched
+    inverse -> ladder + x-check, 29-bit Montgomery arithmetic) on every ECDSA fixture,
+    isValid semantics."""
     lib = hostk.lib()
     f = getattr(lib, fn)
     names = {0: "VALID", 1: "INVALID", 2: "SIG_MALFORMED", 3: "KEY_INVALID"}

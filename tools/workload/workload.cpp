@@ -325,64 +325,49 @@ uint64_t wl_ed25519_arena_bytes(uint64_t n_items, uint32_t n_keys, uint32_t msg_
 // ---------------------------------------------------------------- ECDSA (secp256r1 / k1)
 #include "../../corda_amd/csrc/ecdsa.h"
 
+#include "../../corda_amd/csrc/ecdsa_rows.h"
+
 namespace {
 EcConsts g_K[2];
-u256w g_gcx[2][64][9], g_gcy[2][64][9];  // comb: d * 16^i * G, affine Montgomery
+EcRowTab g_GT[2];  // G rows (the verify path's own table construction)
 bool g_ec_init = false;
-
-template <int C>
-void ec_comb_init() {
-  ec_consts_init<C>(g_K[C]);
-  Jac P = {g_K[C].gx[1], g_K[C].gy[1], g_K[C].one_p};
-  for (int i = 0; i < 64; ++i) {
-    u256w px, py;
-    jac_to_affine<C>(px, py, P, g_K[C]);
-    ec_table8<C>(g_gcx[C][i], g_gcy[C][i], px, py, g_K[C]);
-    for (int k = 0; k < 4; ++k) jac_dbl<C>(P, P);
-  }
-}
 
 void ec_init() {
   if (!g_ec_init) {
-    ec_comb_init<CG_CURVE_K1>();
-    ec_comb_init<CG_CURVE_R1>();
+    static EcRowScratch scr;
+    ec_consts_init<CG_CURVE_K1>(g_K[0]);
+    ec_consts_init<CG_CURVE_R1>(g_K[1]);
+    ec_g_rows_init<CG_CURVE_K1>(g_GT[0], scr, g_K[0]);
+    ec_g_rows_init<CG_CURVE_R1>(g_GT[1], scr, g_K[1]);
     g_ec_init = true;
   }
 }
 
-// affine plain (x, y) of k*G (k < n), via the comb (digits of k in [-8, 8], 65 windows)
+// affine plain (x, y) of k*G (0 < k < n) over the G rows
 template <int C>
 void ec_mul_base(u256w& x, u256w& y, const u256w& k) {
-  uint32_t d[17];
-  ec_recode16(d, k);
+  const EcConsts& K = g_K[C];
+  uint32_t d[EC_PACKED];
+  ec_recode_w6(d, k);
   Jac R;
-  u256_zero(R.X);
-  R.Y = g_K[C].one_p;
-  u256_zero(R.Z);
-  for (int i = 0; i <= 64; ++i) {
-    const int a = i == 64 ? (int)d[16] : ec_digit(d, i);
-    if (!a) continue;
-    const int ia = a < 0 ? -a : a;
-    // window 64 has weight 16^64 = 16 * 16^63
-    u256w yy = i == 64 ? g_gcy[C][63][1] : g_gcy[C][i][ia];
-    u256w xx = i == 64 ? g_gcx[C][63][1] : g_gcx[C][i][ia];
-    if (i == 64) {  // carry digit (0 or 1): add 16 * (16^63 G) via 4 doublings of a copy
-      Jac T = {xx, yy, g_K[C].one_p};
-      for (int k2 = 0; k2 < 4; ++k2) jac_dbl<C>(T, T);
-      u256w tx, ty;
-      jac_to_affine<C>(tx, ty, T, g_K[C]);
-      xx = tx;
-      yy = ty;
+  jac_set_inf<C>(R, K);
+  for (int i = EC_WINDOWS - 1; i >= 0; --i) {
+    if (i != EC_WINDOWS - 1)
+      for (int t = 0; t < EC_W; ++t) jac_dbl<C>(R, R);
+    for (int j = 0; j < EC_ROWS; ++j) {
+      const int t = EC_WINDOWS * j + i;
+      if (t >= EC_DIGITS) continue;
+      const int a = ec_digit6(d, t);
+      if (!a) continue;
+      f29 xx = g_GT[C].t[j][(a < 0 ? -a : a) - 1].x, yy = g_GT[C].t[j][(a < 0 ? -a : a) - 1].y;
+      if (a < 0) m29_neg<C, 0>(yy, yy);
+      jac_madd<C>(R, R, xx, yy, K);
     }
-    if (a < 0) mm_neg<C, 0>(yy, yy);
-    jac_madd<C>(R, R, xx, yy, g_K[C]);
   }
-  u256w xm, ym, one;
-  jac_to_affine<C>(xm, ym, R, g_K[C]);
-  u256_zero(one);
-  one.w[0] = 1;
-  mm_mul<C, 0>(x, xm, one);
-  mm_mul<C, 0>(y, ym, one);
+  f29 xm, ym;
+  jac_to_affine<C>(xm, ym, R, K);
+  m29_to_plain<C, 0>(x, xm);
+  m29_to_plain<C, 0>(y, ym);
 }
 
 void put_be32(uint8_t* out, const u256w& v) {
@@ -450,23 +435,28 @@ int ec_sign(uint8_t* der, const u256w& d, const uint8_t* msg, size_t len, uint64
       }
     }
     if (u256_iszero(r)) continue;
-    // s = k^-1 (e + r d) mod n  (Montgomery mod n)
-    u256w km, kinv, rd, t, sm, one;
-    mm_mul<C, 1>(km, k, K.r2_n);
-    mm_inv<C, 1>(kinv, km, K.one_n);  // k^-1 R
-    mm_mul<C, 1>(rd, r, d);           // r d R^-1
-    mm_mul<C, 1>(rd, rd, K.r2_n);     // r d
-    mm_add<C, 1>(t, e, rd);           // e + r d (plain, < n)
-    mm_mul<C, 1>(sm, t, kinv);        // (e + r d) k^-1 (plain)
-    s = sm;
-    (void)one;
+    // s = k^-1 (e + r d) mod n  (Montgomery mod n, mont29.h)
+    f29 km, kinv, rf, df, rd, ef, t, sm;
+    m29_from_plain<C, 1>(km, k, K.r2_n);  // k R
+    m29_inv<C, 1>(kinv, km, K.one_n);     // k^-1 R
+    f29_from_words(rf, r.w);
+    f29_from_words(df, d.w);
+    m29_mul<C, 1>(rd, rf, df);            // r d R^-1
+    m29_mul<C, 1>(rd, rd, K.r2_n);        // r d
+    f29_from_words(ef, e.w);
+    m29_add<C, 1>(t, ef, rd);             // e + r d
+    m29_mul<C, 1>(sm, t, kinv);           // (e + r d) k^-1 (plain)
+    m29_to_words_canon<C, 1>(s.w, sm);
     if (u256_iszero(s)) continue;
     break;
   }
   if (cls == 2) {  // E2 high-S: s' = n - s (still valid)
-    u256w z;
-    u256_zero(z);
-    mm_sub<C, 1>(s, z, s);
+    uint32_t br = 0;
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t t = (uint64_t)Mod<C, 1>::w(i) - s.w[i] - br;
+      s.w[i] = (uint32_t)t;
+      br = (uint32_t)(t >> 63);
+    }
   }
   uint8_t body[96];
   int o = 0;

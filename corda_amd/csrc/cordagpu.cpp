@@ -321,9 +321,9 @@ int cg_tx_ids_device(cg_ctx* c, const cg_tx* d_txs, uint64_t n_tx, const cg_comp
   if (!c) return fail(CG_ERR_ARG, "cg_tx_ids_device: ctx is NULL");
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  if (c->aux2.cap < 32 * (n_comps ? n_comps : 1)) {
+  if (c->aux2.cap < cg::tx_ws_bytes(n_comps)) {
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    HIP_TRY(c->aux2.ensure(32 * (n_comps ? n_comps : 1)), "hipMalloc(leaf ws)");
+    HIP_TRY(c->aux2.ensure(cg::tx_ws_bytes(n_comps)), "hipMalloc(leaf ws)");
   }
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIP_TRY(cg::launch_tx_ids(d_txs, n_tx, d_comps, n_comps, d_arena, arena_len, d_ids, d_status,
@@ -344,7 +344,7 @@ int cg_tx_ids(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_component* co
   HIP_TRY(c->arena.ensure(((arena_len + 3) & ~(uint64_t)3) + 16), "hipMalloc(arena)");
   HIP_TRY(c->aux0.ensure(32 * n_tx), "hipMalloc(ids)");
   HIP_TRY(c->status.ensure(n_tx), "hipMalloc(status)");
-  HIP_TRY(c->aux2.ensure(32 * (n_comps ? n_comps : 1)), "hipMalloc(leaf ws)");
+  HIP_TRY(c->aux2.ensure(cg::tx_ws_bytes(n_comps)), "hipMalloc(leaf ws)");
   HIP_TRY(hipMemcpyAsync(c->keys.p, txs, sizeof(cg_tx) * n_tx, hipMemcpyHostToDevice, s), "H2D txs");
   if (n_comps)
     HIP_TRY(hipMemcpyAsync(c->items.p, comps, sizeof(cg_component) * n_comps, hipMemcpyHostToDevice, s), "H2D comps");
@@ -407,7 +407,7 @@ static int verify_transactions_locked(cg_ctx* c, const cg_tx* d_txs, uint64_t n_
   }
   uint64_t slot = (maxlen + 15) & ~(uint64_t)15;
   if (slot == 0) slot = 16;
-  const size_t need_leaf = 32 * (n_comps ? n_comps : 1), need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1),
+  const size_t need_leaf = cg::tx_ws_bytes(n_comps), need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1),
                need_msgs = slot * (n_sigs ? n_sigs : 1), need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
   if (c->aux2.cap < need_leaf || c->txitems.cap < need_items || c->msgs.cap < need_msgs ||
       c->tmpls.cap < need_tmpl || c->keyprep.cap < cg::keyprep_bytes(n_keys) ||

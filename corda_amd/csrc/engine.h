@@ -50,7 +50,8 @@ hipError_t launch_sha512(const cg_span* d_spans, uint64_t n, const uint8_t* d_ar
                          uint8_t* d_out, hipStream_t stream);
 
 // WireTransaction ids: leaf hashing + per-tx Merkle levels. `d_leaf_ws` must hold
-// 32 * n_comps bytes.
+// tx_ws_bytes(n_comps) bytes.
+size_t tx_ws_bytes(uint64_t n_comps);
 hipError_t launch_tx_ids(const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps, uint64_t n_comps,
                          const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids, uint8_t* d_status,
                          uint8_t* d_leaf_ws, hipStream_t stream);

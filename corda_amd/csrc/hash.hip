@@ -1,9 +1,10 @@
 // SHA-256 / SHA-512 batch hashing and Merkle transaction ids for gfx950.
 //
 //   k_sha256 / k_sha512   one lane per message (SecureHash.sha256, SecureHash.kt:37)
-//   k_tx_ids              one lane per WireTransaction: nonce_i = SHA256(salt || BE32(i)),
-//                         leaf_i = SHA256(blob_i || nonce_i) (salt leaf: SHA256(blob)),
-//                         zero-hash padding to 2^k, pairwise SHA256(L || R) levels
+//   k_tx_map / k_tx_leaves / k_tx_roots   WireTransaction ids: nonce_i = SHA256(salt ||
+//                         BE32(i)), leaf_i = SHA256(blob_i || nonce_i) (salt leaf: SHA256(blob)),
+//                         one lane per leaf; zero-hash padding to 2^k and pairwise
+//                         SHA256(L || R) levels, one lane per tx
 //                         (MerkleTransaction.kt:16-33,93; MerkleTree.kt:27-66)
 //   k_merkle_roots        one lane per leaf list (MerkleTree.getMerkleTree)
 #include <hip/hip_runtime.h>
@@ -112,57 +113,90 @@ __device__ void merkle_inplace(uint32_t root[8], uint8_t* ws, uint64_t base, uin
   }
 }
 
-__global__ void __launch_bounds__(256) k_tx_ids(const cg_tx* __restrict__ txs, uint64_t n_tx,
-                                                const cg_component* __restrict__ comps, uint64_t n_comps,
-                                                const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                uint8_t* __restrict__ ids, uint8_t* __restrict__ status,
-                                                uint8_t* __restrict__ ws) {
+// ---- WireTransaction ids in three stages, so the SHA-256 work is spread one lane per leaf
+// instead of one lane per transaction (a lane walking ~11 components of 80-600 bytes left
+// most of each wave waiting on its longest transaction):
+//   k_tx_map     one lane per tx: validity (status 1: no leaves / range outside the tables
+//                / salt outside the arena); tx index of each of its components; a component
+//                claimed by two transactions marks both (status 3)
+//   k_tx_leaves  one lane per component: nonce = SHA256(salt || BE32(i)), leaf =
+//                SHA256(blob || nonce) (salt leaf: SHA256(blob)); a blob outside the arena
+//                marks its transaction (status 2)
+//   k_tx_roots   one lane per tx: zero-padded pairwise levels in place -> id
+// Workspace (tx_ws_bytes): leaves 32 x n_comps, then the component -> tx map 4 x n_comps.
+#define TX_NONE 0xffffffffu
+
+__global__ void __launch_bounds__(256) k_tx_map(const cg_tx* __restrict__ txs, uint64_t n_tx, uint64_t n_comps,
+                                                uint64_t arena_len, uint32_t* __restrict__ map,
+                                                uint8_t* __restrict__ status) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tx) return;
   const cg_tx tx = txs[t];
-  uint32_t root[8];
-  uint8_t st = 0;
-  const uint64_t lr = r4(arena_len);
   if (tx.n == 0 || tx.first > n_comps || tx.n > n_comps - tx.first || tx.salt_off > arena_len ||
       arena_len - tx.salt_off < 32) {
-    st = 1;
+    status[t] = 1;
+    return;
+  }
+  for (uint32_t i = 0; i < tx.n; ++i) {
+    const uint32_t prev = atomicExch(&map[tx.first + i], (uint32_t)t);
+    if (prev != TX_NONE) {
+      status[t] = 3;
+      status[prev] = 3;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_tx_leaves(const cg_tx* __restrict__ txs, const cg_component* __restrict__ comps,
+                                                   uint64_t n_comps, const uint32_t* __restrict__ map,
+                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   uint8_t* __restrict__ status, uint8_t* __restrict__ ws) {
+  const uint64_t ci = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= n_comps) return;
+  const uint32_t t = map[ci];
+  if (t == TX_NONE) return;
+  const cg_tx tx = txs[t];
+  const cg_component c = comps[ci];
+  const uint64_t lr = r4(arena_len);
+  uint32_t leaf[8];
+  if (c.off > arena_len || c.len > arena_len - c.off) {
+    status[t] = 2;
+    for (int k = 0; k < 8; ++k) leaf[k] = 0;
+  } else if (c.flags & 1u) {
+    sha256_arena_suffix(leaf, arena, lr, c.off, c.len, nullptr);
+  } else {
+    // nonce = SHA256(salt || BE32(i)) : 36 bytes, one block
+    uint32_t s[8], w[16], nonce[8];
+    sha256_init(s);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = __builtin_bswap32(cg_ld_bytes4(arena, lr, tx.salt_off + 4 * k));
+    w[8] = (uint32_t)(ci - tx.first);
+    w[9] = 0x80000000u;
+#pragma unroll
+    for (int k = 10; k < 15; ++k) w[k] = 0;
+    w[15] = 36 * 8;
+    sha256_compress(s, w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) nonce[k] = s[k];
+    sha256_arena_suffix(leaf, arena, lr, c.off, c.len, nonce);
+  }
+  st_node(ws, ci, leaf);
+}
+
+__global__ void __launch_bounds__(256) k_tx_roots(const cg_tx* __restrict__ txs, uint64_t n_tx,
+                                                  uint8_t* __restrict__ ids, const uint8_t* __restrict__ status,
+                                                  uint8_t* __restrict__ ws) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tx) return;
+  uint32_t root[8];
+  if (status[t] != 0) {
     for (int k = 0; k < 8; ++k) root[k] = 0;
   } else {
-    uint32_t salt_be[9];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) salt_be[k] = __builtin_bswap32(cg_ld_bytes4(arena, lr, tx.salt_off + 4 * k));
-    for (uint32_t i = 0; i < tx.n; ++i) {
-      const cg_component c = comps[tx.first + i];
-      uint32_t leaf[8];
-      if (c.off > arena_len || c.len > arena_len - c.off) {
-        st = 2;
-        for (int k = 0; k < 8; ++k) leaf[k] = 0;
-      } else if (c.flags & 1u) {
-        sha256_arena_suffix(leaf, arena, lr, c.off, c.len, nullptr);
-      } else {
-        // nonce = SHA256(salt || BE32(i)) : 36 bytes, one block
-        uint32_t s[8], w[16], nonce[8];
-        sha256_init(s);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w[k] = salt_be[k];
-        w[8] = i;
-        w[9] = 0x80000000u;
-#pragma unroll
-        for (int k = 10; k < 15; ++k) w[k] = 0;
-        w[15] = 36 * 8;
-        sha256_compress(s, w);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) nonce[k] = s[k];
-        sha256_arena_suffix(leaf, arena, lr, c.off, c.len, nonce);
-      }
-      st_node(ws, tx.first + i, leaf);
-    }
+    const cg_tx tx = txs[t];
     merkle_inplace(root, ws, tx.first, tx.n);
   }
   uint32_t* o = (uint32_t*)(ids + 32 * t);
 #pragma unroll
   for (int k = 0; k < 8; ++k) o[k] = __builtin_bswap32(root[k]);
-  status[t] = st;
 }
 
 // leaves: raw digest bytes; ws holds a copy of each list (big-endian words) at first[j]
@@ -210,12 +244,22 @@ hipError_t launch_sha512(const cg_span* d_spans, uint64_t n, const uint8_t* d_ar
   return hipGetLastError();
 }
 
+size_t tx_ws_bytes(uint64_t n_comps) { return (size_t)(n_comps ? n_comps : 1) * 36 + 256; }
+
 hipError_t launch_tx_ids(const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps, uint64_t n_comps,
                          const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids, uint8_t* d_status,
-                         uint8_t* d_leaf_ws, hipStream_t s) {
+                         uint8_t* d_ws, hipStream_t s) {
   if (!n_tx) return hipSuccess;
-  hipLaunchKernelGGL(k_tx_ids, dim3(blocks(n_tx)), dim3(256), 0, s, d_txs, n_tx, d_comps, n_comps, d_arena,
-                     arena_len, d_ids, d_status, d_leaf_ws);
+  uint32_t* map = (uint32_t*)(d_ws + (((n_comps ? n_comps : 1) * 32 + 255) & ~(uint64_t)255));
+  hipError_t e = hipMemsetAsync(d_status, 0, n_tx, s);
+  if (e == hipSuccess && n_comps) e = hipMemsetAsync(map, 0xff, 4 * n_comps, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_tx_map, dim3(blocks(n_tx)), dim3(256), 0, s, d_txs, n_tx, n_comps, arena_len, map, d_status);
+  if (n_comps)
+    hipLaunchKernelGGL(k_tx_leaves, dim3(blocks(n_comps)), dim3(256), 0, s, d_txs, d_comps, n_comps,
+                       (const uint32_t*)map, d_arena, arena_len, d_status, d_ws);
+  hipLaunchKernelGGL(k_tx_roots, dim3(blocks(n_tx)), dim3(256), 0, s, d_txs, n_tx, d_ids, (const uint8_t*)d_status,
+                     d_ws);
   return hipGetLastError();
 }
 

@@ -185,7 +185,9 @@ int cg_sha256_batch_device(cg_ctx* ctx, const cg_span* d_spans, uint64_t n, cons
 int cg_merkle_roots(cg_ctx* ctx, const uint8_t* leaves, const uint64_t* first, const uint32_t* count,
                     uint64_t n, uint8_t* roots_out, uint8_t* status_out);
 
-/* WireTransaction ids: ids_out 32*n_tx bytes; status_out 0 ok / 1 empty tx. */
+/* WireTransaction ids: ids_out 32*n_tx bytes; status_out 0 ok / 1 no leaves (MerkleTreeException) or
+ * component range / salt outside the tables / 2 a component outside the arena / 3 a component
+ * claimed by more than one transaction (each component belongs to at most one tx). */
 int cg_tx_ids(cg_ctx* ctx, const cg_tx* txs, uint64_t n_tx, const cg_component* comps, uint64_t n_comps,
               const uint8_t* arena, uint64_t arena_len, uint8_t* ids_out, uint8_t* status_out);
 int cg_tx_ids_device(cg_ctx* ctx, const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps,
@@ -219,7 +221,7 @@ typedef struct cg_txsig {
 } cg_txsig;            /* 24 bytes */
 
 /* Device buffers in HBM except `tmpls` (a small host array). ids: 32*n_tx, tx_status: n_tx
- * (0 ok / 1 MerkleTreeException / 2 component outside the arena), sig_status: n_sigs. */
+ * (as cg_tx_ids), sig_status: n_sigs. */
 int cg_verify_transactions_device(cg_ctx* ctx, const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps,
                                   uint64_t n_comps, const cg_key* d_keys, uint32_t n_keys, const cg_txsig* d_sigs,
                                   uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "engine.h"
+#include "partition.h"
 #include "sha2.h"
 
 namespace cg {
@@ -123,7 +124,7 @@ __device__ void merkle_inplace(uint32_t root[8], uint8_t* ws, uint64_t base, uin
 //                SHA256(blob || nonce) (salt leaf: SHA256(blob)); a blob outside the arena
 //                marks its transaction (status 2)
 //   k_tx_roots   one lane per tx: zero-padded pairwise levels in place -> id
-// Workspace (tx_ws_bytes): leaves 32 x n_comps, then the component -> tx map 4 x n_comps.
+// Workspace (tx_ws_bytes): leaves 32 x n_comps, the component -> tx map, the leaf order.
 #define TX_NONE 0xffffffffu
 
 __global__ void __launch_bounds__(256) k_tx_map(const cg_tx* __restrict__ txs, uint64_t n_tx, uint64_t n_comps,
@@ -146,14 +147,42 @@ __global__ void __launch_bounds__(256) k_tx_map(const cg_tx* __restrict__ txs, u
   }
 }
 
+// Leaves are hashed in order of their SHA-256 block count (class = blocks - 1, capped), so the
+// 64 lanes of a wave run the same number of compressions.
+#define TX_LEAF_CLASSES 16
+__device__ __forceinline__ int tx_leaf_class(const uint32_t* map, const cg_component* comps, uint64_t ci) {
+  if (map[ci] == TX_NONE) return -1;
+  const cg_component c = comps[ci];
+  const uint64_t n = (uint64_t)c.len + ((c.flags & 1u) ? 0 : 32);
+  const uint64_t blocks = (n + 9 + 63) >> 6;
+  return (int)(blocks > TX_LEAF_CLASSES ? TX_LEAF_CLASSES - 1 : blocks - 1);
+}
+
+__global__ void __launch_bounds__(PART_B) k_tx_leaf_count(const cg_component* __restrict__ comps, uint64_t n_comps,
+                                                          const uint32_t* __restrict__ map,
+                                                          uint32_t* __restrict__ bcnt) {
+  const uint64_t ci = (uint64_t)blockIdx.x * PART_B + threadIdx.x;
+  part_count<TX_LEAF_CLASSES>(ci < n_comps ? tx_leaf_class(map, comps, ci) : -1, bcnt);
+}
+
+__global__ void __launch_bounds__(PART_B) k_tx_leaf_scatter(const cg_component* __restrict__ comps, uint64_t n_comps,
+                                                            const uint32_t* __restrict__ map,
+                                                            const uint32_t* __restrict__ boff,
+                                                            uint32_t* __restrict__ perm) {
+  const uint64_t ci = (uint64_t)blockIdx.x * PART_B + threadIdx.x;
+  part_scatter<TX_LEAF_CLASSES>(ci < n_comps ? tx_leaf_class(map, comps, ci) : -1, (uint32_t)ci, boff, perm);
+}
+
 __global__ void __launch_bounds__(256) k_tx_leaves(const cg_tx* __restrict__ txs, const cg_component* __restrict__ comps,
-                                                   uint64_t n_comps, const uint32_t* __restrict__ map,
+                                                   const uint32_t* __restrict__ perm,
+                                                   const uint32_t* __restrict__ ranges,
+                                                   const uint32_t* __restrict__ map,
                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                    uint8_t* __restrict__ status, uint8_t* __restrict__ ws) {
-  const uint64_t ci = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ci >= n_comps) return;
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ranges[TX_LEAF_CLASSES]) return;
+  const uint32_t ci = perm[p];
   const uint32_t t = map[ci];
-  if (t == TX_NONE) return;
   const cg_tx tx = txs[t];
   const cg_component c = comps[ci];
   const uint64_t lr = r4(arena_len);
@@ -244,20 +273,35 @@ hipError_t launch_sha512(const cg_span* d_spans, uint64_t n, const uint8_t* d_ar
   return hipGetLastError();
 }
 
-size_t tx_ws_bytes(uint64_t n_comps) { return (size_t)(n_comps ? n_comps : 1) * 36 + 256; }
+// workspace: [leaves 32 x n][map 4 x n][perm 4 x n][block class counts][ranges]
+static uint64_t al256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
+size_t tx_ws_bytes(uint64_t n_comps) {
+  const uint64_t n = n_comps ? n_comps : 1;
+  return al256(32 * n) + al256(4 * n) + al256(4 * n) + al256(4 * part_bcnt_words(TX_LEAF_CLASSES, n)) + 256;
+}
 
 hipError_t launch_tx_ids(const cg_tx* d_txs, uint64_t n_tx, const cg_component* d_comps, uint64_t n_comps,
                          const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids, uint8_t* d_status,
                          uint8_t* d_ws, hipStream_t s) {
   if (!n_tx) return hipSuccess;
-  uint32_t* map = (uint32_t*)(d_ws + (((n_comps ? n_comps : 1) * 32 + 255) & ~(uint64_t)255));
+  const uint64_t n = n_comps ? n_comps : 1;
+  uint32_t* map = (uint32_t*)(d_ws + al256(32 * n));
+  uint32_t* perm = map + al256(4 * n) / 4;
+  uint32_t* bcnt = perm + al256(4 * n) / 4;
+  uint32_t* ranges = bcnt + al256(4 * part_bcnt_words(TX_LEAF_CLASSES, n)) / 4;
   hipError_t e = hipMemsetAsync(d_status, 0, n_tx, s);
   if (e == hipSuccess && n_comps) e = hipMemsetAsync(map, 0xff, 4 * n_comps, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_tx_map, dim3(blocks(n_tx)), dim3(256), 0, s, d_txs, n_tx, n_comps, arena_len, map, d_status);
-  if (n_comps)
-    hipLaunchKernelGGL(k_tx_leaves, dim3(blocks(n_comps)), dim3(256), 0, s, d_txs, d_comps, n_comps,
-                       (const uint32_t*)map, d_arena, arena_len, d_status, d_ws);
+  if (n_comps) {
+    const uint32_t nblk = (uint32_t)((n_comps + PART_B - 1) / PART_B);
+    hipLaunchKernelGGL(k_tx_leaf_count, dim3(nblk), dim3(PART_B), 0, s, d_comps, n_comps, (const uint32_t*)map, bcnt);
+    hipLaunchKernelGGL(k_part_scan<TX_LEAF_CLASSES>, dim3(1), dim3(1024), 0, s, bcnt, nblk, ranges);
+    hipLaunchKernelGGL(k_tx_leaf_scatter, dim3(nblk), dim3(PART_B), 0, s, d_comps, n_comps, (const uint32_t*)map,
+                       (const uint32_t*)bcnt, perm);
+    hipLaunchKernelGGL(k_tx_leaves, dim3(blocks(n_comps)), dim3(256), 0, s, d_txs, d_comps, (const uint32_t*)perm,
+                       (const uint32_t*)ranges, (const uint32_t*)map, d_arena, arena_len, d_status, d_ws);
+  }
   hipLaunchKernelGGL(k_tx_roots, dim3(blocks(n_tx)), dim3(256), 0, s, d_txs, n_tx, d_ids, (const uint8_t*)d_status,
                      d_ws);
   return hipGetLastError();

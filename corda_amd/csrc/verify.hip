@@ -3,13 +3,14 @@
 // Pipeline per batch (all on the caller's stream, no host round trip):
 //   key prep      verify_ed.hip k_ed_keyprep_rows/_tab, verify_ec.hip k_ec_keyprep_rows/_tab
 //   items         k_misc_status (unsupported scheme / bad key index); the plan (k_plan_count,
-//                 k_plan_scan, k_plan_scatter: a stable partition of the items into one dense
-//                 range per scheme); then the Ed25519 stages (k_ed_verify, k_ed_finish) and per
+//                 k_part_scan, k_plan_scatter: a stable partition of the items into one dense
+//                 range per scheme, partition.h); then the Ed25519 stages (k_ed_verify, k_ed_finish) and per
 //                 curve the ECDSA stages (k_ec_prep, k_ec_inv, k_ec_ladder) over their ranges.
 //                 Each stage writes the final status byte of its items.
 // Replaces, per item, the JCA call at core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559
 // behind Crypto.doVerify (Crypto.kt:474-484).
 #include "keyws.h"
+#include "partition.h"
 
 namespace cg {
 
@@ -37,81 +38,20 @@ __device__ __forceinline__ int item_plan_class(const cg_item& it, const cg_key* 
                                         : -1;
 }
 
-// Stable partition by scheme class in three passes (no per-item atomics: a hot key or a
-// single-scheme batch would serialise them): per-block class counts from wave ballots, one
-// exclusive scan over (class, block), then each block writes its items' plan positions in
-// input order.
-#define PLAN_B 256
-__device__ __forceinline__ void plan_block_counts(int c, uint32_t out[PLAN_CLASSES], uint32_t below[PLAN_CLASSES]) {
-  __shared__ uint32_t wc[PLAN_B / 64][PLAN_CLASSES];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t lt = (1ull << lane) - 1ull;
-#pragma unroll
-  for (int k = 0; k < PLAN_CLASSES; ++k) {
-    const uint64_t m = __ballot(c == k);
-    if (lane == 0) wc[wave][k] = (uint32_t)__popcll(m);
-    below[k] = (uint32_t)__popcll(m & lt);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < PLAN_CLASSES; ++k) {
-    uint32_t tot = 0, before = 0;
-    for (uint32_t w = 0; w < PLAN_B / 64; ++w) {
-      if (w < wave) before += wc[w][k];
-      tot += wc[w][k];
-    }
-    out[k] = tot;
-    below[k] += before;
-  }
-}
-
-__global__ void __launch_bounds__(PLAN_B) k_plan_count(const cg_item* __restrict__ items, uint64_t n_items,
+// The plan: a stable partition of the items by scheme class (partition.h).
+__global__ void __launch_bounds__(PART_B) k_plan_count(const cg_item* __restrict__ items, uint64_t n_items,
                                                        const cg_key* __restrict__ keys, uint32_t n_keys,
                                                        uint32_t* __restrict__ bcnt) {
-  const uint64_t i = (uint64_t)blockIdx.x * PLAN_B + threadIdx.x;
-  const int c = i < n_items ? item_plan_class(items[i], keys, n_keys) : -1;
-  uint32_t tot[PLAN_CLASSES], below[PLAN_CLASSES];
-  plan_block_counts(c, tot, below);
-  if (threadIdx.x < PLAN_CLASSES) bcnt[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = tot[threadIdx.x];
+  const uint64_t i = (uint64_t)blockIdx.x * PART_B + threadIdx.x;
+  part_count<PLAN_CLASSES>(i < n_items ? item_plan_class(items[i], keys, n_keys) : -1, bcnt);
 }
 
-// One block: exclusive scan of the PLAN_CLASSES x n_blocks counts (class-major) in place, and
-// the class boundaries.
-__global__ void __launch_bounds__(1024) k_plan_scan(uint32_t* __restrict__ bcnt, uint32_t n_blocks,
-                                                    uint32_t* __restrict__ ranges) {
-  __shared__ uint32_t part[1024];
-  const uint32_t nb = PLAN_CLASSES * n_blocks;
-  const uint32_t t = threadIdx.x, per = (nb + 1023) / 1024;
-  const uint32_t lo = t * per < nb ? t * per : nb, hi = lo + per < nb ? lo + per : nb;
-  uint32_t s = 0;
-  for (uint32_t b = lo; b < hi; ++b) s += bcnt[b];
-  part[t] = s;
-  __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1) {
-    const uint32_t v = t >= off ? part[t - off] : 0u;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - s;
-  for (uint32_t b = lo; b < hi; ++b) {
-    if (b % n_blocks == 0) ranges[b / n_blocks] = run;
-    const uint32_t v = bcnt[b];
-    bcnt[b] = run;
-    run += v;
-  }
-  if (t == 1023) ranges[PLAN_CLASSES] = part[1023];
-}
-
-__global__ void __launch_bounds__(PLAN_B) k_plan_scatter(const cg_item* __restrict__ items, uint64_t n_items,
+__global__ void __launch_bounds__(PART_B) k_plan_scatter(const cg_item* __restrict__ items, uint64_t n_items,
                                                          const cg_key* __restrict__ keys, uint32_t n_keys,
                                                          const uint32_t* __restrict__ boff,
                                                          uint32_t* __restrict__ perm) {
-  const uint64_t i = (uint64_t)blockIdx.x * PLAN_B + threadIdx.x;
-  const int c = i < n_items ? item_plan_class(items[i], keys, n_keys) : -1;
-  uint32_t tot[PLAN_CLASSES], below[PLAN_CLASSES];
-  plan_block_counts(c, tot, below);
-  if (c >= 0) perm[boff[(uint64_t)c * gridDim.x + blockIdx.x] + below[c]] = (uint32_t)i;
+  const uint64_t i = (uint64_t)blockIdx.x * PART_B + threadIdx.x;
+  part_scatter<PLAN_CLASSES>(i < n_items ? item_plan_class(items[i], keys, n_keys) : -1, (uint32_t)i, boff, perm);
 }
 
 hipError_t upload_constants() {
@@ -165,10 +105,10 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
   hipLaunchKernelGGL(k_misc_status, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
                      d_status);
   // plan: a stable partition of the items by scheme class
-  const uint32_t nblk = (uint32_t)((n_items + PLAN_B - 1) / PLAN_B);
-  hipLaunchKernelGGL(k_plan_count, dim3(nblk), dim3(PLAN_B), 0, stream, d_items, n_items, d_keys, n_keys, iw.bcnt);
-  hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, stream, iw.bcnt, nblk, iw.ranges);
-  hipLaunchKernelGGL(k_plan_scatter, dim3(nblk), dim3(PLAN_B), 0, stream, d_items, n_items, d_keys, n_keys,
+  const uint32_t nblk = (uint32_t)((n_items + PART_B - 1) / PART_B);
+  hipLaunchKernelGGL(k_plan_count, dim3(nblk), dim3(PART_B), 0, stream, d_items, n_items, d_keys, n_keys, iw.bcnt);
+  hipLaunchKernelGGL(k_part_scan<PLAN_CLASSES>, dim3(1), dim3(1024), 0, stream, iw.bcnt, nblk, iw.ranges);
+  hipLaunchKernelGGL(k_plan_scatter, dim3(nblk), dim3(PART_B), 0, stream, d_items, n_items, d_keys, n_keys,
                      (const uint32_t*)iw.bcnt, iw.perm);
   ed_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
                   d_btab, stream);

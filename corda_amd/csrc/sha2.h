@@ -260,7 +260,15 @@ CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t l
   const uint64_t sfx = suffix_be ? 32 : 0;
   const uint64_t n = len + sfx;
   const uint64_t nblocks = (n + 9 + 63) >> 6;
-  for (uint64_t blk = 0; blk < nblocks; ++blk) {
+  // blocks made of message bytes only: straight loads, no per-word position logic
+  const uint64_t nfull = len >> 6;
+  for (uint64_t blk = 0; blk < nfull; ++blk) {
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = CG_BSWAP32(cg_ld_bytes4(arena, len_rounded, off + blk * 64 + 4 * j));
+    sha256_compress(s, w);
+  }
+  for (uint64_t blk = nfull; blk < nblocks; ++blk) {
     uint32_t w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {

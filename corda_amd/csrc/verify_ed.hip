@@ -45,7 +45,9 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_rows(const cg_key* __restrict
     ge_p3 A;
     if (ed_decode_point(A, aw, c_ed) == ED_ST_VALID) {
       h.status = 0;
-      ed_encode_affine(h.abyte, A.X, A.Y, A.Z);
+      // canonical Abyte: A comes out of the decode affine (Z = 1), so no inversion is needed
+      fe_tobytes_words(h.abyte, A.Y);
+      h.abyte[7] |= (uint32_t)fe_isnegative(A.X) << 31;
       ge_p3 P;
       ed_neg_point(P, A);
       for (int j = 0; j < EdCfg::kRows; ++j) {

@@ -10,7 +10,8 @@ import re
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcordagpu.so")
+# CORDA_AMD_LIB: an alternative in-tree build (A/B kernel experiments on one GPU box)
+LIB_PATH = os.environ.get("CORDA_AMD_LIB") or os.path.join(_HERE, "libcordagpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cordagpu.h")
 
 _lib = None

@@ -65,7 +65,7 @@ struct DevBuf {
 struct cg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  cg::Fork fork = {{nullptr, nullptr}, nullptr, {nullptr, nullptr}};
+  cg::Fork fork = {{nullptr, nullptr, nullptr}, nullptr, nullptr, {nullptr, nullptr, nullptr}};
   std::mutex mu;
   DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
   // transaction pipeline: verify items, spliced messages, templates; host-entry staging
@@ -108,9 +108,10 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     delete c;
     return hip_fail(e, "hipStreamCreate");
   }
-  for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamCreateWithFlags(&c->fork.side[k], hipStreamNonBlocking);
+  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamCreateWithFlags(&c->fork.side[k], hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.start, hipEventDisableTiming);
-  for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.done[k], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.decoded, hipEventDisableTiming);
+  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.ready[k], hipEventDisableTiming);
   if (e == hipSuccess) e = cg::upload_constants();
   if (e == hipSuccess) e = c->btab.ensure(cg::btab_bytes());
   if (e == hipSuccess) e = cg::init_btab(c->btab.p, c->stream);
@@ -140,14 +141,15 @@ void cg_close(cg_ctx* c) {
   c->aux2.release();
   for (DevBuf* b : {&c->txitems, &c->msgs, &c->tmpls, &c->h_txs, &c->h_comps, &c->h_sigs, &c->h_ids, &c->h_txst})
     b->release();
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 3; ++k) {
     if (c->fork.side[k]) {
       hipStreamSynchronize(c->fork.side[k]);
       hipStreamDestroy(c->fork.side[k]);
     }
-    if (c->fork.done[k]) hipEventDestroy(c->fork.done[k]);
+    if (c->fork.ready[k]) hipEventDestroy(c->fork.ready[k]);
   }
   if (c->fork.start) hipEventDestroy(c->fork.start);
+  if (c->fork.decoded) hipEventDestroy(c->fork.decoded);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -213,7 +215,7 @@ int cg_verify_items_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   }
   hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
   HIP_TRY(cg::launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p,
-                           c->itemws.p, c->btab.p, s),
+                           c->itemws.p, c->btab.p, s, nullptr, 0, &c->fork),
           "launch_items");
   return CG_OK;
 }

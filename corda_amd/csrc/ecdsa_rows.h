@@ -207,9 +207,11 @@ CG_HD uint32_t ec_key_decode_bytes(f29& xm, f29& ym, const uint8_t* arena, uint6
 }
 
 // ---------------------------------------------------------------- per-item pipeline
-// Item workspace between the three stages (96 B): after prep {r, s, e}; after inv {r, u1, u2}.
+// Item workspace between the three stages: after prep {r, s, e}; after inv {r, u1, u2}.
+// Padded to the 120-byte item slot (keyws.h), so every scheme's slot arrays share one stride.
 struct EcItemWs {
   u256w r, a, b;
+  uint32_t pad[6];
 };
 
 // Stage 1: DER, range checks, e = SHA-256(M) mod n. Returns 0 (pending: ws filled),

@@ -9,12 +9,15 @@ namespace cg {
 
 struct DeviceConsts;  // opaque
 
-// Two side streams + events owned by a context: key preparation of the two ECDSA curves runs
-// on them concurrently with the Ed25519 key preparation (each is a latency-bound chain of
-// doublings on few waves), joined back into the caller's stream before anything reads keys.
+// Side streams + events owned by a context. Key preparation forks off the caller's stream:
+// the two ECDSA curves' tables and the Ed25519 row tables are built on side streams (each is a
+// latency-bound chain of doublings on few waves), while the caller's stream goes on with the
+// work that needs only decoded keys (the plan, the SHA-512 challenges). Each consumer waits
+// for its `ready` event just before it reads tables: ready[0] secp256r1, [1] secp256k1,
+// [2] Ed25519.
 struct Fork {
-  hipStream_t side[2];
-  hipEvent_t start, done[2];
+  hipStream_t side[3];
+  hipEvent_t start, decoded, ready[3];
 };
 
 // Upload the constant tables (curve constants, base-point tables) for the current device.
@@ -41,7 +44,7 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
                         const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
-                        const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0);
+                        const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0, const Fork* fork = nullptr);
 
 // Hashing kernels
 hipError_t launch_sha256(const cg_span* d_spans, uint64_t n, const uint8_t* d_arena, uint64_t arena_len,

@@ -105,7 +105,8 @@ static inline size_t key_ws_bytes(uint32_t n_keys) {
 
 // Per-item workspace slot (indexed by plan position, so the schemes never share one):
 // projective Ed25519 R' awaiting the batched inversion, or the ECDSA stage hand-off.
-constexpr size_t ITEM_SLOT = sizeof(ge_p2) > sizeof(EcItemWs) ? sizeof(ge_p2) : sizeof(EcItemWs);
+constexpr size_t ITEM_SLOT = sizeof(ge_p2);
+static_assert(sizeof(EcItemWs) == ITEM_SLOT, "ECDSA stage hand-off must fill one item slot");
 // Item workspace: [slots: n x ITEM_SLOT, by plan position][perm: n x u32]
 //                 [per-block class counts: PLAN_CLASSES x ceil(n / 256) x u32][ranges: 4 x u32]
 struct ItemWs {
@@ -148,12 +149,13 @@ static inline EcRowScratch* const_scratch(void* d_btab) {
 // Per-scheme halves (verify_ed.hip / verify_ec.hip)
 hipError_t ed_upload_constants();
 hipError_t ed_init_const(void* d_btab, hipStream_t stream);
-void ed_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                       const KeyWs& w, hipStream_t stream);
+void ed_launch_keyprep_decode(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                              const KeyWs& w, hipStream_t stream);
+void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream);
 void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
                      const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
-                     hipStream_t stream);
+                     hipStream_t stream, hipEvent_t tables_ready);
 hipError_t ec_upload_constants();
 hipError_t ec_init_const(void* d_btab, hipStream_t stream);
 void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
@@ -161,6 +163,6 @@ void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_a
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
                      const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
-                     hipStream_t stream);
+                     hipStream_t stream, hipEvent_t ready_r1, hipEvent_t ready_k1);
 
 }  // namespace cg

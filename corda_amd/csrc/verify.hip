@@ -74,29 +74,30 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
                           void* d_keyprep, hipStream_t stream, const Fork* fork) {
   if (n_keys == 0) return hipSuccess;
   const KeyWs w = key_ws(d_keyprep, n_keys);
-  hipStream_t s_r1 = stream, s_k1 = stream;
-  if (fork) {
-    hipError_t e = hipEventRecord(fork->start, stream);
-    for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->start, 0);
-    if (e != hipSuccess) return e;
-    s_r1 = fork->side[0];
-    s_k1 = fork->side[1];
+  if (!fork) {
+    ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, stream, stream);
+    ed_launch_keyprep_decode(d_keys, n_keys, d_arena, arena_len, w, stream);
+    ed_launch_keyprep_tables(d_keys, n_keys, w, stream);
+    return hipGetLastError();
   }
-  ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, s_r1, s_k1);
-  ed_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, stream);
-  if (fork) {
-    hipError_t e = hipSuccess;
-    for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventRecord(fork->done[k], fork->side[k]);
-    for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamWaitEvent(stream, fork->done[k], 0);
-    if (e != hipSuccess) return e;
-  }
+  hipError_t e = hipEventRecord(fork->start, stream);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->start, 0);
+  if (e != hipSuccess) return e;
+  ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, fork->side[0], fork->side[1]);
+  ed_launch_keyprep_decode(d_keys, n_keys, d_arena, arena_len, w, stream);
+  e = hipEventRecord(fork->decoded, stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(fork->side[2], fork->decoded, 0);
+  if (e != hipSuccess) return e;
+  ed_launch_keyprep_tables(d_keys, n_keys, w, fork->side[2]);
+  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventRecord(fork->ready[k], fork->side[k]);
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
                         const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
-                        const uint8_t* d_msgs, uint64_t msgs_len) {
+                        const uint8_t* d_msgs, uint64_t msgs_len, const Fork* fork) {
   if (n_items == 0) return hipSuccess;
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
@@ -111,9 +112,9 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
   hipLaunchKernelGGL(k_plan_scatter, dim3(nblk), dim3(PART_B), 0, stream, d_items, n_items, d_keys, n_keys,
                      (const uint32_t*)iw.bcnt, iw.perm);
   ed_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
-                  d_btab, stream);
+                  d_btab, stream, fork ? fork->ready[2] : nullptr);
   ec_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
-                  d_btab, stream);
+                  d_btab, stream, fork ? fork->ready[0] : nullptr, fork ? fork->ready[1] : nullptr);
   return hipGetLastError();
 }
 
@@ -125,7 +126,7 @@ hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d
   hipError_t e = launch_keyprep(d_keys, n_keys, d_arena, arena_len, d_keyprep, stream, fork);
   if (e != hipSuccess) return e;
   return launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, d_keyprep, d_item_ws,
-                      d_btab, stream, d_msgs, msgs_len);
+                      d_btab, stream, d_msgs, msgs_len, fork);
 }
 
 }  // namespace cg

@@ -191,11 +191,13 @@ static void launch_curve(const cg_item* d_items, uint64_t n_items, const uint8_t
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
                      const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
-                     hipStream_t stream) {
+                     hipStream_t stream, hipEvent_t ready_r1, hipEvent_t ready_k1) {
   (void)d_keys;
   (void)n_keys;
+  if (ready_r1) hipStreamWaitEvent(stream, ready_r1, 0);
   launch_curve<CG_CURVE_R1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, d_btab,
                             stream);
+  if (ready_k1) hipStreamWaitEvent(stream, ready_k1, 0);
   launch_curve<CG_CURVE_K1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, d_btab,
                             stream);
 }

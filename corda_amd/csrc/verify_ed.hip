@@ -1,10 +1,12 @@
 // Ed25519 (EDDSA_ED25519_SHA512) verification kernels, i2p 0.2.0 semantics.
-//   k_ed_keyprep_rows  one lane per distinct key: decode A, canonical Abyte, row bases
-//                      2^{24j} (-A), j = 0..10
-//   k_ed_keyprep_tab   one lane per (key, row, 8 multiples): affine multiples of the row base
-//   k_ed_verify        one lane per item: SHA-512 challenge, scalar prep, 4 windows
-//                      x (11 rows of -A + 11 rows of B) mixed additions, 18 doublings
-//   k_ed_finish        16 items per lane: batch inversion, encode, byte compare
+//   k_ed_keyprep_decode  one lane per distinct key: decode A, canonical Abyte, -A
+//   k_ed_keyprep_chain   one lane per key: row bases 2^{24j} (-A), j = 1..10
+//   k_ed_keyprep_tab     one lane per (key, row, 8 multiples): affine multiples of the row base
+//   k_ed_hash            one lane per item: SHA-512 challenge, scalar prep, radix-64 digits
+//                        (needs only the decoded keys: overlaps the table build)
+//   k_ed_ladder          one lane per item: 4 windows x (11 rows of -A + 11 rows of B) mixed
+//                        additions, 18 doublings
+//   k_ed_finish          16 items per lane: batch inversion, encode, byte compare
 // Replaces, per item, i2p EdDSAEngine.engineVerify behind Crypto.isValid
 // (core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559, scheme :120-133).
 #include "keyws.h"
@@ -15,7 +17,8 @@ __constant__ Ed25519Consts c_ed;
 
 static const uint8_t ED_SPKI_PREFIX[12] = {0x30, 0x2a, 0x30, 0x05, 0x06, 0x03, 0x2b, 0x65, 0x70, 0x03, 0x21, 0x00};
 
-__global__ void __launch_bounds__(64) k_ed_keyprep_rows(const cg_key* __restrict__ keys, uint32_t n_keys,
+// one lane per key: decode A (i2p rules), status, canonical Abyte, row base -A
+__global__ void __launch_bounds__(64) k_ed_keyprep_decode(const cg_key* __restrict__ keys, uint32_t n_keys,
                                                         const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                         EdKeyHdr* __restrict__ hdr, BaseSlot* __restrict__ bases) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -50,13 +53,24 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_rows(const cg_key* __restrict
       h.abyte[7] |= (uint32_t)fe_isnegative(A.X) << 31;
       ge_p3 P;
       ed_neg_point(P, A);
-      for (int j = 0; j < EdCfg::kRows; ++j) {
-        bases[(size_t)i * EdCfg::kRows + j].ed = P;
-        if (j + 1 < EdCfg::kRows) ed_dbl_n(P, P, ED_W * ED_K);
-      }
+      bases[(size_t)i * EdCfg::kRows].ed = P;
     }
   }
   hdr[i] = h;
+}
+
+// one lane per key: row bases 2^{24j} (-A), j = 1..10 (a serial chain of 240 doublings)
+__global__ void __launch_bounds__(64) k_ed_keyprep_chain(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                         const EdKeyHdr* __restrict__ hdr,
+                                                         BaseSlot* __restrict__ bases) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_keys) return;
+  if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || hdr[i].status != 0) return;
+  ge_p3 P = bases[(size_t)i * EdCfg::kRows].ed;
+  for (int j = 1; j < EdCfg::kRows; ++j) {
+    ed_dbl_n(P, P, ED_W * ED_K);
+    bases[(size_t)i * EdCfg::kRows + j].ed = P;
+  }
 }
 
 // m * P for a small m >= 1 (double-and-add, MSB first)
@@ -144,26 +158,25 @@ __device__ __forceinline__ void pick(ge_niels& out, const ge_niels* row, int d) 
   ge_niels_cneg(out, d < 0);
 }
 
-__global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
-                                                   const uint32_t* __restrict__ ranges,
-                                                   const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs,
-                                                   const EdTab* __restrict__ btab,
-                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                   const uint8_t* __restrict__ msgs, uint64_t msgs_len,
-                                                   uint32_t mode, uint8_t* __restrict__ status,
-                                                   ge_p2* __restrict__ rout) {
-  const uint32_t end = ranges[PLAN_ED + 1];
-  const uint64_t p0 = (uint64_t)ranges[PLAN_ED] + (uint64_t)blockIdx.x * blockDim.x;
-  if (p0 >= end) return;  // whole block past this scheme's range (grids are sized for all items)
-  __shared__ EdTab sB;
-  {
-    const uint4* src = (const uint4*)btab;
-    uint4* dst = (uint4*)&sB;
-    for (uint32_t w = threadIdx.x; w < sizeof(EdTab) / 16; w += blockDim.x) dst[w] = src[w];
-  }
-  __syncthreads();
-  const uint64_t p = p0 + threadIdx.x;
-  if (p >= end) return;
+// Digits handed from k_ed_hash to k_ed_ladder through the item slot (the ladder reads them
+// before it writes R' into the same slot).
+struct EdDigits {
+  uint32_t eh[EdCfg::kPackedWords], es[EdCfg::kPackedWords];
+  uint32_t pad[(ITEM_SLOT - 8 * EdCfg::kPackedWords) / 4];
+};
+static_assert(sizeof(EdDigits) == ITEM_SLOT, "digits must fill one item slot");
+
+// One lane per Ed25519 plan position: status checks, h = SHA-512(R || Abyte || M) mod L,
+// S' = i2p's slide value of S mod L, both recoded to signed radix-64 digits. Needs only the
+// decoded keys (Abyte), so it runs while the key tables are still being built.
+__global__ void __launch_bounds__(256) k_ed_hash(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
+                                                 const uint32_t* __restrict__ ranges,
+                                                 const EdKeyHdr* __restrict__ hdr,
+                                                 const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                 const uint8_t* __restrict__ msgs, uint64_t msgs_len, uint32_t mode,
+                                                 uint8_t* __restrict__ status, EdDigits* __restrict__ dig) {
+  const uint64_t p = (uint64_t)ranges[PLAN_ED] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ranges[PLAN_ED + 1]) return;
   const uint32_t i = perm[p];
   const cg_item it = items[i];
   const EdKeyHdr* kh = hdr + it.key_idx;
@@ -179,17 +192,14 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
     st = CG_SIG_MALFORMED;
   } else {
     const uint64_t lr = round4(arena_len);
-    uint32_t sw[16], ab[8];
+    uint32_t sw[16];
 #pragma unroll
     for (int w = 0; w < 16; ++w) sw[w] = cg_ld_bytes4(arena, lr, it.sig_off + 4 * w);
-#pragma unroll
-    for (int w = 0; w < 8; ++w) ab[w] = kh->abyte[w];
-    // h = SHA-512(R || Abyte || M) mod L ; S' = slide value of S mod L
     uint32_t pre[16], hw[16], h[8];
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
       pre[w] = sw[w];
-      pre[8 + w] = ab[w];
+      pre[8 + w] = kh->abyte[w];
     }
     sha512_prefix64_msg(hw, pre, item_msg_arena(it, arena, msgs), round4(item_msg_len(it, arena_len, msgs_len, msgs)),
                         it.msg_off, it.msg_len);
@@ -206,15 +216,42 @@ __global__ void __launch_bounds__(256) k_ed_verify(const cg_item* __restrict__ i
         sc_sub(sr, sr, r1);
       }
     }
-    uint32_t eh[EdCfg::kPackedWords], es[EdCfg::kPackedWords];
-    sc_recode_w<ED_W>(eh, EdCfg::kPackedWords, h);
-    sc_recode_w<ED_W>(es, EdCfg::kPackedWords, sr);
-    ge_p2 q;
-    ed_double_scalar_w<ED_W, ED_K>(q, eh, es, tabs[it.key_idx].ed, sB);
-    rout[p] = q;
+    EdDigits d;
+    sc_recode_w<ED_W>(d.eh, EdCfg::kPackedWords, h);
+    sc_recode_w<ED_W>(d.es, EdCfg::kPackedWords, sr);
+    dig[p] = d;
     st = (uint8_t)ED_PENDING;
   }
   status[i] = st;
+}
+
+// One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the row tables (B rows
+// staged in LDS), left projective in the item slot.
+#ifndef ED_LADDER_WAVES_PER_SIMD
+#define ED_LADDER_WAVES_PER_SIMD 3  // 168 VGPRs: 3 waves/SIMD beat 2 (measured, r01)
+#endif
+__global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
+                                                   const uint32_t* __restrict__ ranges,
+                                                   const TabSlot* __restrict__ tabs, const EdTab* __restrict__ btab,
+                                                   const uint8_t* __restrict__ status, void* __restrict__ slots) {
+  const uint32_t end = ranges[PLAN_ED + 1];
+  const uint64_t p0 = (uint64_t)ranges[PLAN_ED] + (uint64_t)blockIdx.x * blockDim.x;
+  if (p0 >= end) return;  // whole block past this scheme's range (grids are sized for all items)
+  __shared__ EdTab sB;
+  {
+    const uint4* src = (const uint4*)btab;
+    uint4* dst = (uint4*)&sB;
+    for (uint32_t w = threadIdx.x; w < sizeof(EdTab) / 16; w += blockDim.x) dst[w] = src[w];
+  }
+  __syncthreads();
+  const uint64_t p = p0 + threadIdx.x;
+  if (p >= end) return;
+  const uint32_t i = perm[p];
+  if (status[i] != ED_PENDING) return;
+  const EdDigits d = ((const EdDigits*)slots)[p];
+  ge_p2 q;
+  ed_double_scalar_w<ED_W, ED_K>(q, d.eh, d.es, tabs[items[i].key_idx].ed, sB);
+  ((ge_p2*)slots)[p] = q;
 }
 
 // Encode + compare for 16 consecutive items per lane: one inversion per lane (Montgomery's
@@ -275,11 +312,17 @@ hipError_t ed_init_const(void* d_btab, hipStream_t stream) {
   return hipGetLastError();
 }
 
-void ed_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                       const KeyWs& w, hipStream_t stream) {
+void ed_launch_keyprep_decode(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                              const KeyWs& w, hipStream_t stream) {
   const uint32_t B = 64;  // one wave per block: keys are few, spread them over CUs
-  hipLaunchKernelGGL(k_ed_keyprep_rows, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, d_arena,
+  hipLaunchKernelGGL(k_ed_keyprep_decode, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, d_arena,
                      arena_len, w.hdr, w.bases);
+}
+
+void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream) {
+  const uint32_t B = 64;
+  hipLaunchKernelGGL(k_ed_keyprep_chain, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
+                     w.bases);
   const uint32_t lanes = n_keys * EdCfg::kRows * (EdCfg::kMult / 8);
   hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((lanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
                      w.bases, w.tab);
@@ -288,13 +331,16 @@ void ed_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_a
 void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
                      const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
-                     hipStream_t stream) {
+                     hipStream_t stream, hipEvent_t tables_ready) {
   (void)d_keys;
   (void)n_keys;
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;  // the Ed25519 range is at most n_items long
-  hipLaunchKernelGGL(k_ed_verify, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, w.tab,
-                     (const EdTab*)d_btab, d_arena, arena_len, d_msgs, msgs_len, mode, d_status, (ge_p2*)iw.slots);
+  hipLaunchKernelGGL(k_ed_hash, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
+                     arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
+  if (tables_ready) hipStreamWaitEvent(stream, tables_ready, 0);
+  hipLaunchKernelGGL(k_ed_ladder, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.tab,
+                     (const EdTab*)d_btab, (const uint8_t*)d_status, iw.slots);
   const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
   hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
                      arena_len, d_status, (const ge_p2*)iw.slots);

@@ -35,10 +35,10 @@ METRIC = "verified sigs/sec (whole node), Ed25519 + ECDSA-P256, at 1/2/4/8 MI355
 N_FE_ED25519 = 2859
 MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # Executed work of the GPU path per Ed25519 item, counted by the host build of the same lane
-# code (tests/native/host_kernels.cpp t_ed_count_w6; pinned by
+# code (tests/native/host_kernels.cpp t_ed_verify_wb / t_ed_count_w6; pinned by
 # tests/test_host_kernels.py::test_executed_work_constants_match_lane_code).
 # (field multiplies, field squarings):
-ED_VERIFY_FE = (658, 72)   # k_ed_verify: 86 mixed additions + 18 doublings over the W=6 rows
+ED_VERIFY_FE = (536, 72)   # k_ed_ladder: 43 + 26 mixed additions (W=6 rows of -A, radix-2^10 B) + 18 doublings
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
 ED_FINISH_K = 16
@@ -309,7 +309,7 @@ def main():
     i2p_equiv = n_items * MAC32_PER_ED25519 / (kern_ms * 1e-3)
     roof = {"bound": "valu-int", "achieved": round(achieved / 1e12, 3), "peak": round(PEAK_MAC32_PER_S / 1e12, 3),
             "unit": "TMAC32/s", "frac": round(achieved / PEAK_MAC32_PER_S, 4), "traffic": None,
-            "kernel": "k_ed_verify + k_ed_finish (+k_misc_status, empty ECDSA launches)",
+            "kernel": "k_ed_hash + k_ed_ladder + k_ed_finish (+ plan, k_misc_status, empty ECDSA launches)",
             "kernel_ms": round(kern_ms, 3),
             "work_per_item": f"executed: {MAC32_EXEC_PER_ED25519:.0f} MAC32 (field products the lane code "
                              f"runs: {ED_VERIFY_FE[0] + ED_FINISH_FE[0]} mul x {MAC_PER_MUL} + "

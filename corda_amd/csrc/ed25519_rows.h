@@ -146,3 +146,100 @@ CG_HD void ed_double_scalar_w(ge_p2& out, const uint32_t* eh, const uint32_t* es
   if (!have_q) ge_p3_to_p2(q, R);
   out = q;
 }
+
+// ---------------------------------------------------------------- wide-radix B table
+// S' B with signed radix-2^WB digits (WB > W): the B table is shared by every key, so it can
+// be larger than the per-key tables (it lives in global memory, L2-resident; WB = 10 is
+// 26 rows x 512 niels = 1.6 MB). B digit u is added in window i_u = floor(u K / NB), where it
+// still gets doubled 6 i_u more times, so row u holds d * 2^(WB u - W i_u) * B.
+// With W = 6, K = 4, WB = 10: 43 + 26 = 69 mixed additions instead of 86.
+template <int W, int K, int WB>
+struct EdBCfg {
+  static constexpr int kDigits = (253 + WB - 1) / WB + (253 % WB == 0 ? 1 : 0);
+  static constexpr int kMult = 1 << (WB - 1);
+  static constexpr int kPackedWords = (kDigits + 1) / 2;  // int16 digits, 2 per word
+  static constexpr int window(int u) { return (u * K) / kDigits; }
+  static constexpr int shift(int u) { return WB * u - W * window(u); }  // row scale 2^shift
+};
+
+template <int W, int K, int WB>
+struct EdBTabW {
+  ge_niels t[EdBCfg<W, K, WB>::kDigits][EdBCfg<W, K, WB>::kMult];
+};
+
+// signed radix-2^WB digits of a < 2^253, packed 2 per word as int16
+template <int WB>
+CG_HD void sc_recode_w16(uint32_t* packed, int nwords, const uint32_t a[8]) {
+  constexpr int D = (253 + WB - 1) / WB + (253 % WB == 0 ? 1 : 0);
+  for (int w = 0; w < nwords; ++w) packed[w] = 0;
+  int carry = 0;
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+    const int bit = t * WB;
+    uint32_t v = 0;
+    if (bit < 256) {
+      const int wi = bit >> 5, sh = bit & 31;
+      uint64_t x = (uint64_t)a[wi] >> sh;
+      if (sh + WB > 32 && wi + 1 < 8) x |= (uint64_t)a[wi + 1] << (32 - sh);
+      v = (uint32_t)x & ((1u << WB) - 1);
+    }
+    int e = (int)v + carry;
+    carry = (e + (1 << (WB - 1))) >> WB;
+    e -= carry << WB;
+    packed[t >> 1] |= ((uint32_t)(e & 0xffff)) << ((t & 1) * 16);
+  }
+}
+
+CG_HD int sc_digit_h(const uint32_t* packed, int t) {
+  return (int)(int16_t)(uint16_t)(packed[t >> 1] >> ((t & 1) * 16));
+}
+
+// R' = h (-A) + S' B: A over the per-key W/K rows, B over the WB table; left projective.
+// `Pick(out, row, digit)` loads a signed niels entry (identity for 0) from either table.
+template <int W, int K, int WB, class RowA, class TabB, class PickA, class PickB>
+CG_HD void ed_double_scalar_wb(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const RowA& TA, const TabB& TB,
+                               PickA pick_a, PickB pick_b) {
+  typedef EdRowsCfg<W, K> C;
+  typedef EdBCfg<W, K, WB> CB;
+  ge_p3 R;
+  ge_p3_0(R);
+  ge_p1p1 t;
+  ge_p2 q;
+  for (int i = K - 1; i >= 0; --i) {
+    if (i != K - 1) {  // R arrives as p2 (q) from the previous window's last addition
+      for (int d = 0; d < W - 1; ++d) {
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+      }
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(R, t);
+    }
+    const int u_lo = (i * CB::kDigits + K - 1) / K, u_hi = ((i + 1) * CB::kDigits + K - 1) / K;
+    const int n_a = (C::kDigits - i + K - 1) / K;  // rows with a digit in this window
+    const int n_ops = n_a + (u_hi - u_lo);
+    for (int k = 0; k < n_ops; ++k) {
+      ge_niels n;
+      if (k < n_a) {
+        pick_a(n, TA.t[k], sc_digit_b(eh, K * k + i));
+      } else {
+        pick_b(n, TB.t[u_lo + k - n_a], sc_digit_h(esb, u_lo + k - n_a));
+      }
+      ge_madd(t, R, n);
+      if (k + 1 == n_ops) {
+        ge_p1p1_to_p2(q, t);  // next: doublings (or the end), which need no T
+      } else {
+        ge_p1p1_to_p3(R, t);
+      }
+    }
+  }
+  out = q;
+}
+
+// Table rows: row u holds the affine multiples 1..kMult of 2^shift(u) B.
+template <int W, int K, int WB>
+CG_HD void ed_btab_wb_row(ge_niels* row, const ge_p3& B, int u, const fe& d2) {
+  typedef EdBCfg<W, K, WB> CB;
+  ge_p3 P = B;
+  if (CB::shift(u) > 0) ed_dbl_n(P, P, CB::shift(u));
+  ed_row_multiples<CB::kMult>(row, P, d2);
+}

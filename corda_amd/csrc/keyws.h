@@ -38,6 +38,9 @@ __device__ __forceinline__ uint64_t item_msg_len(const cg_item& it, uint64_t are
 #define ED_K 4
 typedef EdRowsCfg<ED_W, ED_K> EdCfg;
 typedef EdRowTabW<ED_W, ED_K> EdTab;  // 11 x 32 affine niels = 42240 B
+#define ED_WB 10
+typedef EdBCfg<ED_W, ED_K, ED_WB> EdBCfgT;
+typedef EdBTabW<ED_W, ED_K, ED_WB> EdBTab;  // 26 x 512 affine niels = 1.6 MB, constant
 
 // Per-key header: status (0 = decoded) and, for Ed25519, the canonical Abyte i2p hashes.
 struct EdKeyHdr {
@@ -133,13 +136,13 @@ static inline size_t item_ws_total(uint64_t n_items) {
   return al256(n * ITEM_SLOT) + al256(n * sizeof(uint32_t)) + al256(PLAN_CLASSES * ((n + 255) / 256) * 4) + 64;
 }
 
-// Constant tables per context: [Ed25519 B rows][G rows k1][G rows r1][row scratch]
-static inline size_t const_tab_bytes() { return sizeof(EdTab) + 2 * sizeof(EcRowTab) + sizeof(EcRowScratch); }
+// Constant tables per context: [Ed25519 B rows (radix 2^10)][G rows k1][G rows r1][row scratch]
+static inline size_t const_tab_bytes() { return sizeof(EdBTab) + 2 * sizeof(EcRowTab) + sizeof(EcRowScratch); }
 static inline const EcRowTab* gtab(const void* d_btab, int curve) {
-  return (const EcRowTab*)((const uint8_t*)d_btab + sizeof(EdTab)) + curve;
+  return (const EcRowTab*)((const uint8_t*)d_btab + sizeof(EdBTab)) + curve;
 }
 static inline EcRowScratch* const_scratch(void* d_btab) {
-  return (EcRowScratch*)((uint8_t*)d_btab + sizeof(EdTab) + 2 * sizeof(EcRowTab));
+  return (EcRowScratch*)((uint8_t*)d_btab + sizeof(EdBTab) + 2 * sizeof(EcRowTab));
 }
 
 // Intermediate per-item status codes (never returned to the caller)

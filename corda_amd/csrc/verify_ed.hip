@@ -4,8 +4,8 @@
 //   k_ed_keyprep_tab     one lane per (key, row, 8 multiples): affine multiples of the row base
 //   k_ed_hash            one lane per item: SHA-512 challenge, scalar prep, radix-64 digits
 //                        (needs only the decoded keys: overlaps the table build)
-//   k_ed_ladder          one lane per item: 4 windows x (11 rows of -A + 11 rows of B) mixed
-//                        additions, 18 doublings
+//   k_ed_ladder          one lane per item: 4 windows x (11 rows of -A + ~6.5 rows of the
+//                        radix-2^10 B table) mixed additions, 18 doublings
 //   k_ed_finish          16 items per lane: batch inversion, encode, byte compare
 // Replaces, per item, i2p EdDSAEngine.engineVerify behind Crypto.isValid
 // (core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559, scheme :120-133).
@@ -117,10 +117,8 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_tab(const cg_key* __restrict_
   for (int k = 0; k < 8; ++k) tabs[i].ed.t[j][8 * grp + k] = row[k];
 }
 
-// B rows, built once per context by the same code
-__global__ void k_ed_btab_init(EdTab* __restrict__ out) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  ge_p3 B;
+// The base point B as an extended point (from the constant niels table entry 1*B)
+__device__ void ed_base_point(ge_p3& B) {
   fe x, y, two_inv, t;
   fe_sub(x, c_ed.Btab[1].ypx, c_ed.Btab[1].ymx);
   fe_add(y, c_ed.Btab[1].ypx, c_ed.Btab[1].ymx);
@@ -131,9 +129,30 @@ __global__ void k_ed_btab_init(EdTab* __restrict__ out) {
   fe_mul(B.Y, y, two_inv);
   fe_1(B.Z);
   fe_mul(B.T, B.X, B.Y);
-  ed_rows_w_init<ED_W, ED_K>(*out, B, c_ed.d2);
 }
 
+// B rows (radix 2^ED_WB), built once per context: one lane per (row, group of 8 multiples)
+__global__ void __launch_bounds__(64) k_ed_btab_init(EdBTab* __restrict__ out) {
+  constexpr uint32_t G = EdBCfgT::kMult / 8;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t u = g / G, grp = g % G;
+  if (u >= (uint32_t)EdBCfgT::kDigits) return;
+  ge_p3 P;
+  ed_base_point(P);
+  if (EdBCfgT::shift(u) > 0) ed_dbl_n(P, P, EdBCfgT::shift(u));
+  ge_p3 pts[8];
+  ed_small_mul(pts[0], P, 8 * grp + 1);
+  ge_cached c;
+  ge_p3_to_cached(c, P, c_ed.d2);
+  ge_p1p1 t;
+  for (int k = 1; k < 8; ++k) {
+    ge_add_cached(t, pts[k - 1], c);
+    ge_p1p1_to_p3(pts[k], t);
+  }
+  ge_niels row[8];
+  ed_niels_batch8(row, pts, c_ed.d2);
+  for (int k = 0; k < 8; ++k) out->t[u][8 * grp + k] = row[k];
+}
 
 __device__ __forceinline__ void ld_niels(ge_niels& n, const ge_niels* src) {
   const uint4* p = (const uint4*)src;
@@ -161,8 +180,8 @@ __device__ __forceinline__ void pick(ge_niels& out, const ge_niels* row, int d) 
 // Digits handed from k_ed_hash to k_ed_ladder through the item slot (the ladder reads them
 // before it writes R' into the same slot).
 struct EdDigits {
-  uint32_t eh[EdCfg::kPackedWords], es[EdCfg::kPackedWords];
-  uint32_t pad[(ITEM_SLOT - 8 * EdCfg::kPackedWords) / 4];
+  uint32_t eh[EdCfg::kPackedWords], es[EdBCfgT::kPackedWords];
+  uint32_t pad[(ITEM_SLOT - 4 * (EdCfg::kPackedWords + EdBCfgT::kPackedWords)) / 4];
 };
 static_assert(sizeof(EdDigits) == ITEM_SLOT, "digits must fill one item slot");
 
@@ -218,7 +237,7 @@ __global__ void __launch_bounds__(256) k_ed_hash(const cg_item* __restrict__ ite
     }
     EdDigits d;
     sc_recode_w<ED_W>(d.eh, EdCfg::kPackedWords, h);
-    sc_recode_w<ED_W>(d.es, EdCfg::kPackedWords, sr);
+    sc_recode_w16<ED_WB>(d.es, EdBCfgT::kPackedWords, sr);
     dig[p] = d;
     st = (uint8_t)ED_PENDING;
   }
@@ -227,30 +246,28 @@ __global__ void __launch_bounds__(256) k_ed_hash(const cg_item* __restrict__ ite
 
 // One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the row tables (B rows
 // staged in LDS), left projective in the item slot.
+struct PickGlobal {
+  __device__ __forceinline__ void operator()(ge_niels& out, const ge_niels* row, int d) const { pick(out, row, d); }
+};
+
 #ifndef ED_LADDER_WAVES_PER_SIMD
 #define ED_LADDER_WAVES_PER_SIMD 3  // 168 VGPRs: 3 waves/SIMD beat 2 (measured, r01)
 #endif
-__global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
-                                                   const uint32_t* __restrict__ ranges,
-                                                   const TabSlot* __restrict__ tabs, const EdTab* __restrict__ btab,
-                                                   const uint8_t* __restrict__ status, void* __restrict__ slots) {
-  const uint32_t end = ranges[PLAN_ED + 1];
-  const uint64_t p0 = (uint64_t)ranges[PLAN_ED] + (uint64_t)blockIdx.x * blockDim.x;
-  if (p0 >= end) return;  // whole block past this scheme's range (grids are sized for all items)
-  __shared__ EdTab sB;
-  {
-    const uint4* src = (const uint4*)btab;
-    uint4* dst = (uint4*)&sB;
-    for (uint32_t w = threadIdx.x; w < sizeof(EdTab) / 16; w += blockDim.x) dst[w] = src[w];
-  }
-  __syncthreads();
-  const uint64_t p = p0 + threadIdx.x;
-  if (p >= end) return;
+// One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the per-key rows and the
+// constant radix-2^10 B table (both in global memory; the B table stays L2-resident), left
+// projective in the item slot.
+__global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
+    const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
+    const TabSlot* __restrict__ tabs, const EdBTab* __restrict__ btab, const uint8_t* __restrict__ status,
+    void* __restrict__ slots) {
+  const uint64_t p = (uint64_t)ranges[PLAN_ED] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ranges[PLAN_ED + 1]) return;
   const uint32_t i = perm[p];
   if (status[i] != ED_PENDING) return;
   const EdDigits d = ((const EdDigits*)slots)[p];
   ge_p2 q;
-  ed_double_scalar_w<ED_W, ED_K>(q, d.eh, d.es, tabs[items[i].key_idx].ed, sB);
+  ed_double_scalar_wb<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[items[i].key_idx].ed, *btab, PickGlobal(),
+                                         PickGlobal());
   ((ge_p2*)slots)[p] = q;
 }
 
@@ -308,7 +325,8 @@ hipError_t ed_upload_constants() {
 }
 
 hipError_t ed_init_const(void* d_btab, hipStream_t stream) {
-  hipLaunchKernelGGL(k_ed_btab_init, dim3(1), dim3(64), 0, stream, (EdTab*)d_btab);
+  const uint32_t lanes = EdBCfgT::kDigits * (EdBCfgT::kMult / 8);
+  hipLaunchKernelGGL(k_ed_btab_init, dim3((lanes + 63) / 64), dim3(64), 0, stream, (EdBTab*)d_btab);
   return hipGetLastError();
 }
 
@@ -340,7 +358,7 @@ void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_ite
                      arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
   if (tables_ready) hipStreamWaitEvent(stream, tables_ready, 0);
   hipLaunchKernelGGL(k_ed_ladder, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.tab,
-                     (const EdTab*)d_btab, (const uint8_t*)d_status, iw.slots);
+                     (const EdBTab*)d_btab, (const uint8_t*)d_status, iw.slots);
   const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
   hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
                      arena_len, d_status, (const ge_p2*)iw.slots);

@@ -334,3 +334,73 @@ extern "C" void t_m29_op(int curve, int n, int op, const uint32_t* a, const uint
   else { M29_BIN(0, 1) }
 #undef M29_BIN
 }
+
+// ---------------------------------------------------------------- Ed25519 rows + radix-2^10 B
+static EdBTabW<6, 4, 10>* g_TB10 = nullptr;
+static void tb10_init() {
+  if (g_TB10) return;
+  g_TB10 = new EdBTabW<6, 4, 10>;
+  ge_p3 B;
+  fe x, y, two_inv, t;
+  fe_sub(x, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+  fe_add(y, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+  fe_0(t);
+  t.v[0] = 2;
+  fe_invert(two_inv, t);
+  fe_mul(B.X, x, two_inv);
+  fe_mul(B.Y, y, two_inv);
+  fe_1(B.Z);
+  fe_mul(B.T, B.X, B.Y);
+  for (int u = 0; u < EdBCfg<6, 4, 10>::kDigits; ++u) ed_btab_wb_row<6, 4, 10>(g_TB10->t[u], B, u, g_C.d2);
+}
+static void host_pick(ge_niels& out, const ge_niels* row, int d) { ed_pick_w(out, row, d); }
+
+extern "C" int t_ed_verify_wb(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len,
+                              uint64_t* counts) {
+  init();
+  tb10_init();
+  typedef EdRowsCfg<6, 4> C;
+  typedef EdBCfg<6, 4, 10> CB;
+  static EdRowTabW<6, 4> TA;
+  static EdKeyPrep kp;
+  ed_key_prep(kp, aw, g_C);
+  if (kp.status) return (int)kp.status;
+  ge_p3 A, N;
+  ed_decode_point(A, aw, g_C);
+  ed_neg_point(N, A);
+  ed_rows_w_init<6, 4>(TA, N, g_C.d2);
+  static uint8_t buf[1 << 20];
+  memcpy(buf, msg, msg_len);
+  uint32_t pre[16], hw[16], h[8];
+  for (int i = 0; i < 8; ++i) {
+    pre[i] = sw[i];
+    pre[8 + i] = kp.abyte[i];
+  }
+  sha512_prefix64_msg(hw, pre, buf, (msg_len + 3) & ~3ull, 0, msg_len);
+  sc_reduce512(h, hw);
+  uint32_t s[8], sr[8];
+  for (int i = 0; i < 8; ++i) s[i] = sw[8 + i];
+  sc_reduce256(sr, s);
+  if ((s[7] >> 31) && sc_slide_escapes(s)) {
+    uint32_t r1[8];
+    for (int i = 0; i < 8; ++i) r1[i] = sc_R1w(i);
+    sc_sub(sr, sr, r1);
+  }
+  uint32_t eh[C::kPackedWords], es[CB::kPackedWords];
+  sc_recode_w<6>(eh, C::kPackedWords, h);
+  sc_recode_w16<10>(es, CB::kPackedWords, sr);
+  ge_p2 R;
+#ifdef FE_OP_COUNT
+  g_fe_nmul = g_fe_nsq = 0;
+#endif
+  ed_double_scalar_wb<6, 4, 10>(R, eh, es, TA, *g_TB10, host_pick, host_pick);
+#ifdef FE_OP_COUNT
+  if (counts) {
+    counts[0] = g_fe_nmul;
+    counts[1] = g_fe_nsq;
+  }
+#endif
+  fe zi;
+  fe_invert(zi, R.Z);
+  return ed_encode_cmp(R, zi, sw);
+}

@@ -144,6 +144,24 @@ def test_ed25519_row_table_lane_verify_on_fixtures(w):
     assert n > 200
 
 
+def test_ed25519_wide_b_lane_verify_on_fixtures():
+    """k_ed_ladder's arithmetic: -A rows (W=6, K=4) + the radix-2^10 B table (ed25519_rows.h)."""
+    import ctypes
+    lib = hostk.lib()
+    lib.t_ed_verify_wb.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]
+    n = 0
+    for it in golden_io.load("ed25519.json"):
+        key, sig, msg = bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"])
+        if it["key_fmt"] != 0 or len(key) != 32 or len(sig) != 64:
+            continue
+        m = np.frombuffer(msg + bytes(8), dtype=np.uint8).copy()
+        st = lib.t_ed_verify_wb(ptr(words(key)), ptr(words(sig)), ptr(m), len(msg), None)
+        got = {0: "VALID", 1: "INVALID", 3: "KEY_INVALID"}[st]
+        assert got == it["expect_isvalid"], it["note"]
+        n += 1
+    assert n > 200
+
+
 def test_executed_work_constants_match_lane_code():
     """bench.py prices k_ed_verify + k_ed_finish with the field products the lane code
     executes; the constants there must equal what the host build of that code counts."""
@@ -154,7 +172,12 @@ def test_executed_work_constants_match_lane_code():
     m = np.frombuffer(msg + bytes(8), dtype=np.uint8).copy()
     out = np.zeros(8, dtype=np.uint64)
     assert lib.t_ed_count_w6(ptr(words(key)), ptr(words(sig)), ptr(m), len(msg), ptr(out)) == 0
-    mul_v, sq_v, mul_f, sq_f, mul_i, sq_i = (int(x) for x in out[:6])
+    _, _, mul_f, sq_f, mul_i, sq_i = (int(x) for x in out[:6])
+    import ctypes
+    lib.t_ed_verify_wb.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]
+    lad = np.zeros(2, dtype=np.uint64)
+    assert lib.t_ed_verify_wb(ptr(words(key)), ptr(words(sig)), ptr(m), len(msg), ptr(lad)) == 0
+    mul_v, sq_v = int(lad[0]), int(lad[1])
     assert (mul_v, sq_v) == bench.ED_VERIFY_FE, (mul_v, sq_v)
     assert (mul_f, sq_f) == bench.ED_FINISH_FE, (mul_f, sq_f)
     assert (mul_i, sq_i) == bench.ED_INVERT_FE, (mul_i, sq_i)

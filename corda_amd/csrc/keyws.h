@@ -59,11 +59,9 @@ union BaseSlot {
   Jac ec;
 };
 
-// Per-batch plan: item indices partitioned by scheme class (stable: input order within a
-// class). Each scheme's kernels walk one dense range of `perm`, so no lane idles on another
-// scheme's item, and the per-item workspace is indexed by plan position. (Grouping by key as
-// well was measured: no gain on k_ed_verify, which is VALU-bound, and per-key atomics
-// serialise on a hot key such as a notary's.)
+// Per-batch plan (plan_sort.hip): item indices sorted by (scheme class, key). Each scheme's
+// kernels walk one dense range of `perm`, so no lane idles on another scheme's item; the
+// per-item workspace is indexed by plan position.
 #define PLAN_ED 0
 #define PLAN_R1 1
 #define PLAN_K1 2
@@ -110,13 +108,16 @@ static inline size_t key_ws_bytes(uint32_t n_keys) {
 // projective Ed25519 R' awaiting the batched inversion, or the ECDSA stage hand-off.
 constexpr size_t ITEM_SLOT = sizeof(ge_p2);
 static_assert(sizeof(EcItemWs) == ITEM_SLOT, "ECDSA stage hand-off must fill one item slot");
-// Item workspace: [slots: n x ITEM_SLOT, by plan position][perm: n x u32]
-//                 [per-block class counts: PLAN_CLASSES x ceil(n / 256) x u32][ranges: 4 x u32]
+// Item workspace: [slots: n x ITEM_SLOT, by plan position][perm: n x u32][ranges]
+//                 [sort keys in/out, sort values in: 3 x n x u32][radix-sort temporary storage]
+size_t plan_sort_temp_bytes(uint64_t n_items);  // plan_sort.hip
 struct ItemWs {
   void* slots;
   uint32_t* perm;
-  uint32_t* bcnt;
   uint32_t* ranges;
+  uint32_t *skey_in, *skey_out, *sval_in;
+  void* sort_temp;
+  size_t sort_temp_bytes;
 };
 static inline ItemWs item_ws(void* base, uint64_t n_items) {
   const size_t n = n_items ? n_items : 1;
@@ -126,15 +127,24 @@ static inline ItemWs item_ws(void* base, uint64_t n_items) {
   p += al256(n * ITEM_SLOT);
   w.perm = (uint32_t*)p;
   p += al256(n * sizeof(uint32_t));
-  w.bcnt = (uint32_t*)p;
-  p += al256(PLAN_CLASSES * ((n + 255) / 256) * sizeof(uint32_t));
   w.ranges = (uint32_t*)p;
+  p += 256;
+  w.skey_in = (uint32_t*)p;
+  p += al256(n * sizeof(uint32_t));
+  w.skey_out = (uint32_t*)p;
+  p += al256(n * sizeof(uint32_t));
+  w.sval_in = (uint32_t*)p;
+  p += al256(n * sizeof(uint32_t));
+  w.sort_temp = p;
+  w.sort_temp_bytes = plan_sort_temp_bytes(n);
   return w;
 }
 static inline size_t item_ws_total(uint64_t n_items) {
   const size_t n = n_items ? n_items : 1;
-  return al256(n * ITEM_SLOT) + al256(n * sizeof(uint32_t)) + al256(PLAN_CLASSES * ((n + 255) / 256) * 4) + 64;
+  return al256(n * ITEM_SLOT) + 4 * al256(n * sizeof(uint32_t)) + 256 + al256(plan_sort_temp_bytes(n));
 }
+hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d_keys, uint32_t n_keys,
+                       const ItemWs& iw, hipStream_t stream);
 
 // Constant tables per context: [Ed25519 B rows (radix 2^10)][G rows k1][G rows r1][row scratch]
 static inline size_t const_tab_bytes() { return sizeof(EdBTab) + 2 * sizeof(EcRowTab) + sizeof(EcRowScratch); }

@@ -2,15 +2,13 @@
 //
 // Pipeline per batch (all on the caller's stream, no host round trip):
 //   key prep      verify_ed.hip k_ed_keyprep_rows/_tab, verify_ec.hip k_ec_keyprep_rows/_tab
-//   items         k_misc_status (unsupported scheme / bad key index); the plan (k_plan_count,
-//                 k_part_scan, k_plan_scatter: a stable partition of the items into one dense
-//                 range per scheme, partition.h); then the Ed25519 stages (k_ed_verify, k_ed_finish) and per
+//   items         k_misc_status (unsupported scheme / bad key index); the plan (plan_sort.hip:
+//                 items sorted by (scheme, key), one dense range per scheme); then the Ed25519 stages (k_ed_verify, k_ed_finish) and per
 //                 curve the ECDSA stages (k_ec_prep, k_ec_inv, k_ec_ladder) over their ranges.
 //                 Each stage writes the final status byte of its items.
 // Replaces, per item, the JCA call at core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559
 // behind Crypto.doVerify (Crypto.kt:474-484).
 #include "keyws.h"
-#include "partition.h"
 
 namespace cg {
 
@@ -26,32 +24,6 @@ __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_item
   const uint8_t s = keys[ki].scheme;
   if (s != CG_EDDSA_ED25519_SHA512 && s != CG_ECDSA_SECP256R1_SHA256 && s != CG_ECDSA_SECP256K1_SHA256)
     status[i] = CG_UNSUPPORTED;
-}
-
-// ------------------------------------------------------------------ batch plan
-__device__ __forceinline__ int item_plan_class(const cg_item& it, const cg_key* keys, uint32_t n_keys) {
-  if (it.key_idx >= n_keys) return -1;
-  const uint8_t s = keys[it.key_idx].scheme;
-  return s == CG_EDDSA_ED25519_SHA512 ? PLAN_ED
-       : s == CG_ECDSA_SECP256R1_SHA256 ? PLAN_R1
-       : s == CG_ECDSA_SECP256K1_SHA256 ? PLAN_K1
-                                        : -1;
-}
-
-// The plan: a stable partition of the items by scheme class (partition.h).
-__global__ void __launch_bounds__(PART_B) k_plan_count(const cg_item* __restrict__ items, uint64_t n_items,
-                                                       const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                       uint32_t* __restrict__ bcnt) {
-  const uint64_t i = (uint64_t)blockIdx.x * PART_B + threadIdx.x;
-  part_count<PLAN_CLASSES>(i < n_items ? item_plan_class(items[i], keys, n_keys) : -1, bcnt);
-}
-
-__global__ void __launch_bounds__(PART_B) k_plan_scatter(const cg_item* __restrict__ items, uint64_t n_items,
-                                                         const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                         const uint32_t* __restrict__ boff,
-                                                         uint32_t* __restrict__ perm) {
-  const uint64_t i = (uint64_t)blockIdx.x * PART_B + threadIdx.x;
-  part_scatter<PLAN_CLASSES>(i < n_items ? item_plan_class(items[i], keys, n_keys) : -1, (uint32_t)i, boff, perm);
 }
 
 hipError_t upload_constants() {
@@ -105,12 +77,9 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
   const ItemWs iw = item_ws(d_item_ws, n_items);
   hipLaunchKernelGGL(k_misc_status, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
                      d_status);
-  // plan: a stable partition of the items by scheme class
-  const uint32_t nblk = (uint32_t)((n_items + PART_B - 1) / PART_B);
-  hipLaunchKernelGGL(k_plan_count, dim3(nblk), dim3(PART_B), 0, stream, d_items, n_items, d_keys, n_keys, iw.bcnt);
-  hipLaunchKernelGGL(k_part_scan<PLAN_CLASSES>, dim3(1), dim3(1024), 0, stream, iw.bcnt, nblk, iw.ranges);
-  hipLaunchKernelGGL(k_plan_scatter, dim3(nblk), dim3(PART_B), 0, stream, d_items, n_items, d_keys, n_keys,
-                     (const uint32_t*)iw.bcnt, iw.perm);
+  // plan: items sorted by (scheme class, key) (plan_sort.hip)
+  hipError_t e = launch_plan(d_items, n_items, d_keys, n_keys, iw, stream);
+  if (e != hipSuccess) return e;
   ed_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
                   d_btab, stream, fork ? fork->ready[2] : nullptr);
   ec_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,

@@ -132,6 +132,25 @@ def bench_mixed(a, wl, eng, dev, stream, run, threads):
             "verdicts": {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
 
 
+def bench_ecdsa_mixed(a, wl, dev, run, pools, n):
+    """BASELINE configs[2] shape: one shuffled batch of n ECDSA items, half secp256r1 and half
+    secp256k1, 2048 keys per curve, ~10% corrupted (items tiled from the 65 536-item pools)."""
+    import torch
+    from corda_amd.batch import Batch
+    parts = [Batch(pools[c].keys, np.resize(pools[c].items, n // 2), pools[c].arena) for c in (1, 0)]
+    b, _ = wl.concat(parts, shuffle_seed=a.seed + 29)
+    kd = torch.from_numpy(b.keys.view(np.uint8)).to(dev)
+    idd = torch.from_numpy(b.items.view(np.uint8)).to(dev)
+    ad = torch.from_numpy(b.arena).to(dev)
+    sd = torch.full((b.n,), 255, dtype=torch.uint8, device=dev)
+    steps = max(2, a.steps // 2)
+    el, km = run(kd, len(b.keys), idd, b.n, ad, int(b.arena.size), sd, steps, 1, False)
+    st = sd.cpu().numpy()
+    return {"value": round(b.n * steps / el, 1), "unit": "sigs/s", "items": b.n, "keys": len(b.keys),
+            "kernel_ms": round(km, 3), "ms_per_step": round(el / steps * 1e3, 3),
+            "verdicts": {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
+
+
 def bench_pipeline(a, wl, eng, dev, stream, threads):
     """BASELINE configs[3] shape: WireTransaction ids (SHA-256 Merkle) for every transaction,
     SignableData(id) spliced from the template, every signature verified -- one
@@ -277,10 +296,12 @@ def main():
     extra = {}
     if world == 1 and a.ecdsa_items > 0:
         # BASELINE configs[2] shape (secp256r1 / secp256k1 batches), outside the headline value
+        pools = {}
         for curve, name in ((1, "ecdsa_secp256r1"), (0, "ecdsa_secp256k1")):
             pool = min(a.ecdsa_items, 65536)
             eb, _ = wl.ecdsa_batch(curve, pool, n_keys=2048, msg_len=a.msg_len, corrupt_permille=100,
                                    seed=a.seed + 17 + curve, nthreads=threads)
+            pools[curve] = eb
             reps = max(1, a.ecdsa_items // pool)
             items_rep = np.tile(eb.items, reps)
             ek = torch.from_numpy(eb.keys.view(np.uint8)).to(dev)
@@ -292,7 +313,8 @@ def main():
             n_e = len(items_rep)
             extra[name] = {"value": round(n_e * max(2, a.steps // 2) / el, 1), "unit": "sigs/s",
                            "items": n_e, "unique_items": pool, "kernel_ms": round(km, 3)}
-
+        # configs[2] proper: one shuffled batch, half secp256r1 / half secp256k1, 4x --ecdsa-items
+        extra["ecdsa_mixed"] = bench_ecdsa_mixed(a, wl, dev, run, pools, 4 * a.ecdsa_items)
     if world == 1 and a.mixed_items > 0:
         extra["notary_mixed"] = bench_mixed(a, wl, eng, dev, stream, run, threads)
     if world == 1 and a.pipeline_txs > 0:

@@ -121,19 +121,20 @@ struct EcRowScratch {
   f29 pre[EC_MULT];
 };
 
+// cnt (<= EC_MULT) affine points first + k step, k = 0..cnt-1, with one batched inversion.
 template <int C>
-CG_HD void ec_row_build(EcAff* row, const Jac& base, EcRowScratch& s, const EcConsts& K) {
-  Jac acc = base;
+CG_HD void ec_multiples(EcAff* out, const Jac& first, const Jac& step, int cnt, EcRowScratch& s, const EcConsts& K) {
+  Jac acc = first;
   s.p[0] = acc;
   s.pre[0] = acc.Z;
-  for (int k = 1; k < EC_MULT; ++k) {
-    jac_add<C>(acc, acc, base, K);  // k = 1: P + P goes through the doubling branch
+  for (int k = 1; k < cnt; ++k) {
+    jac_add<C>(acc, acc, step, K);  // acc == step goes through the doubling branch
     s.p[k] = acc;
     m29_mul<C, 0>(s.pre[k], s.pre[k - 1], acc.Z);
   }
   f29 inv;
-  m29_inv<C, 0>(inv, s.pre[EC_MULT - 1], K.one_p);
-  for (int k = EC_MULT - 1; k >= 0; --k) {
+  m29_inv<C, 0>(inv, s.pre[cnt - 1], K.one_p);
+  for (int k = cnt - 1; k >= 0; --k) {
     f29 zi, zi2, zi3;
     if (k > 0) {
       m29_mul<C, 0>(zi, inv, s.pre[k - 1]);
@@ -143,9 +144,15 @@ CG_HD void ec_row_build(EcAff* row, const Jac& base, EcRowScratch& s, const EcCo
     }
     m29_sq<C, 0>(zi2, zi);
     m29_mul<C, 0>(zi3, zi2, zi);
-    m29_mul<C, 0>(row[k].x, s.p[k].X, zi2);
-    m29_mul<C, 0>(row[k].y, s.p[k].Y, zi3);
+    m29_mul<C, 0>(out[k].x, s.p[k].X, zi2);
+    m29_mul<C, 0>(out[k].y, s.p[k].Y, zi3);
   }
+}
+
+// One row: the affine multiples 1..32 of the (finite, prime-order) Jacobian point `base`.
+template <int C>
+CG_HD void ec_row_build(EcAff* row, const Jac& base, EcRowScratch& s, const EcConsts& K) {
+  ec_multiples<C>(row, base, base, EC_MULT, s, K);
 }
 
 // The 11 row bases 2^{24j} P of an affine (Montgomery) point.
@@ -280,48 +287,63 @@ CG_HD void ecdsa_batch_inv(EcItemWs* ws, uint32_t cnt, uint32_t sel, const EcCon
   }
 }
 
-template <class RowT>
-CG_HD void ec_pick(f29& x, f29& y, const RowT* row, int a) {
-  const EcAff& e = row[a - 1];
-  x = e.x;
-  y = e.y;
+// ---------------------------------------------------------------- wide-radix G table
+// u1 G with signed radix-2^10 digits over a constant table (G is the same for every item):
+// 26 rows x 512 affine multiples (958 464 B per curve, global memory, L2-resident). G digit u
+// is added in window i_u = floor(4u / 26) from a row pre-scaled by 2^(10u - 6 i_u), exactly
+// as the Ed25519 B table (ed25519_rows.h). 43 + 26 = 69 mixed additions instead of 86.
+#define EC_GB 10
+#define EC_G_DIGITS 26
+#define EC_G_MULT 512
+#define EC_G_PACKED 13
+
+struct EcGTab {
+  EcAff t[EC_G_DIGITS][EC_G_MULT];  // t[u][k-1] = k * 2^(10u - 6 i_u) * G
+};
+
+CG_HD int ec_g_window(int u) { return (u * EC_WINDOWS) / EC_G_DIGITS; }
+CG_HD int ec_g_shift(int u) { return EC_GB * u - EC_W * ec_g_window(u); }
+
+// signed radix-2^10 digits of a < 2^256, packed 2 per word as int16
+CG_HD void ec_recode_w10(uint32_t packed[EC_G_PACKED], const u256w& a) {
+#pragma unroll
+  for (int w = 0; w < EC_G_PACKED; ++w) packed[w] = 0;
+  int carry = 0;
+#pragma unroll
+  for (int t = 0; t < EC_G_DIGITS; ++t) {
+    const int bit = t * EC_GB;
+    const int wi = bit >> 5, sh = bit & 31;
+    uint64_t x = (uint64_t)a.w[wi] >> sh;
+    if (sh + EC_GB > 32 && wi + 1 < 8) x |= (uint64_t)a.w[wi + 1] << (32 - sh);
+    int e = (int)((uint32_t)x & 1023u) + carry;
+    carry = (e + 512) >> 10;
+    e -= carry << 10;
+    packed[t >> 1] |= ((uint32_t)(e & 0xffff)) << ((t & 1) * 16);
+  }
 }
 
-// Stage 3: R = u1 G + u2 Q over the row tables; x(R) == r (mod n) by BC's inversion-free test.
-// TG / TQ point at [EC_ROWS][EC_MULT] arrays (LDS or global). Returns 0 VALID / 1 INVALID.
-template <int C, class TabG, class TabQ>
-CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG, const TabQ& TQ,
-                                  const EcConsts& K) {
-  uint32_t d1[EC_PACKED], d2[EC_PACKED];
-  ec_recode_w6(d1, u1);
-  ec_recode_w6(d2, u2);
-  Jac R;
-  jac_set_inf<C>(R, K);
-  for (int i = EC_WINDOWS - 1; i >= 0; --i) {
-    if (i != EC_WINDOWS - 1) {
-#pragma unroll 1
-      for (int d = 0; d < EC_W; ++d) jac_dbl<C>(R, R);
-    }
-#pragma unroll 1
-    for (int j = 0; j < EC_ROWS; ++j) {
-      const int t = EC_WINDOWS * j + i;
-      if (t >= EC_DIGITS) continue;
-      const int a = ec_digit6(d1, t);
-      if (a != 0) {
-        f29 x, y;
-        ec_pick(x, y, TG.t[j], a < 0 ? -a : a);
-        if (a < 0) m29_neg<C, 0>(y, y);
-        jac_madd<C>(R, R, x, y, K);
-      }
-      const int b = ec_digit6(d2, t);
-      if (b != 0) {
-        f29 x, y;
-        ec_pick(x, y, TQ.t[j], b < 0 ? -b : b);
-        if (b < 0) m29_neg<C, 0>(y, y);
-        jac_madd<C>(R, R, x, y, K);
-      }
-    }
+CG_HD int ec_digit10(const uint32_t* packed, int t) {
+  return (int)(int16_t)(uint16_t)(packed[t >> 1] >> ((t & 1) * 16));
+}
+
+// G row u, multiples 32 g + 1 .. 32 g + 32 (one lane of the per-context table build)
+template <int C>
+CG_HD void ec_gtab_group(EcAff* out, int u, int g, EcRowScratch& s, const EcConsts& K) {
+  Jac P = {K.gx, K.gy, K.one_p};
+  if (ec_g_shift(u) > 0) jac_dbl_n<C>(P, P, ec_g_shift(u));
+  const uint32_t m = 32u * (uint32_t)g + 1u;  // first multiple, by double-and-add
+  Jac F = P;
+  for (int b = 30 - __builtin_clz(m); b >= 0; --b) {
+    jac_dbl<C>(F, F);
+    if ((m >> b) & 1u) jac_add<C>(F, F, P, K);
   }
+  ec_multiples<C>(out, F, P, EC_MULT, s, K);
+}
+
+// x(R) == r (mod n) for R = (X : Y : Z) by BC's inversion-free test (r Z^2 == X, or
+// (r + n) Z^2 == X when r + n < p). Returns 0 VALID / 1 INVALID.
+template <int C>
+CG_HD uint32_t ecdsa_x_check(const Jac& R, const u256w& r, const EcConsts& K) {
   if (m29_iszero<C, 0>(R.Z)) return 1;
   f29 z2, t, rm;
   m29_sq<C, 0>(z2, R.Z);
@@ -342,6 +364,56 @@ CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w&
     if (m29_eq<C, 0>(t, R.X)) return 0;
   }
   return 1;
+}
+
+template <class Row>
+CG_HD void ec_pick(f29& x, f29& y, const Row* row, int a) {
+  const EcAff& e = row[a - 1];
+  x = e.x;
+  y = e.y;
+}
+
+// Stage 3: R = u1 G + u2 Q (Q over the per-key radix-64 rows, G over the radix-2^10 table),
+// then the x-check. Returns 0 VALID / 1 INVALID.
+template <int C, class TabG, class TabQ>
+CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG, const TabQ& TQ,
+                                  const EcConsts& K) {
+  uint32_t dg[EC_G_PACKED], dq[EC_PACKED];
+  ec_recode_w10(dg, u1);
+  ec_recode_w6(dq, u2);
+  Jac R;
+  jac_set_inf<C>(R, K);
+  for (int i = EC_WINDOWS - 1; i >= 0; --i) {
+    if (i != EC_WINDOWS - 1) {
+#pragma unroll 1
+      for (int d = 0; d < EC_W; ++d) jac_dbl<C>(R, R);
+    }
+#pragma unroll 1
+    for (int j = 0; j < EC_ROWS; ++j) {
+      const int t = EC_WINDOWS * j + i;
+      if (t >= EC_DIGITS) continue;
+      const int b = ec_digit6(dq, t);
+      if (b != 0) {
+        f29 x, y;
+        ec_pick(x, y, TQ.t[j], b < 0 ? -b : b);
+        if (b < 0) m29_neg<C, 0>(y, y);
+        jac_madd<C>(R, R, x, y, K);
+      }
+    }
+    const int u_lo = (i * EC_G_DIGITS + EC_WINDOWS - 1) / EC_WINDOWS;
+    const int u_hi = ((i + 1) * EC_G_DIGITS + EC_WINDOWS - 1) / EC_WINDOWS;
+#pragma unroll 1
+    for (int u = u_lo; u < u_hi; ++u) {
+      const int a = ec_digit10(dg, u);
+      if (a != 0) {
+        f29 x, y;
+        ec_pick(x, y, TG.t[u], a < 0 ? -a : a);
+        if (a < 0) m29_neg<C, 0>(y, y);
+        jac_madd<C>(R, R, x, y, K);
+      }
+    }
+  }
+  return ecdsa_x_check<C>(R, r, K);
 }
 
 // G rows (per context) from the curve constants.

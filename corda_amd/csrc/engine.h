@@ -17,7 +17,7 @@ struct DeviceConsts;  // opaque
 // [2] Ed25519.
 struct Fork {
   hipStream_t side[3];
-  hipEvent_t start, decoded, ready[3];
+  hipEvent_t decoded, ready[3];
 };
 
 // Upload the constant tables (curve constants, base-point tables) for the current device.

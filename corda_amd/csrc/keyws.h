@@ -147,12 +147,15 @@ hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d
                        const ItemWs& iw, hipStream_t stream);
 
 // Constant tables per context: [Ed25519 B rows (radix 2^10)][G rows k1][G rows r1][row scratch]
-static inline size_t const_tab_bytes() { return sizeof(EdBTab) + 2 * sizeof(EcRowTab) + sizeof(EcRowScratch); }
-static inline const EcRowTab* gtab(const void* d_btab, int curve) {
-  return (const EcRowTab*)((const uint8_t*)d_btab + sizeof(EdBTab)) + curve;
+#define EC_GTAB_LANES (EC_G_DIGITS * (EC_G_MULT / EC_MULT))  // one lane per (row, group of 32)
+static inline size_t const_tab_bytes() {
+  return sizeof(EdBTab) + 2 * sizeof(EcGTab) + EC_GTAB_LANES * sizeof(EcRowScratch);
+}
+static inline const EcGTab* gtab(const void* d_btab, int curve) {
+  return (const EcGTab*)((const uint8_t*)d_btab + sizeof(EdBTab)) + curve;
 }
 static inline EcRowScratch* const_scratch(void* d_btab) {
-  return (EcRowScratch*)((uint8_t*)d_btab + sizeof(EdBTab) + 2 * sizeof(EcRowTab));
+  return (EcRowScratch*)((uint8_t*)d_btab + sizeof(EdBTab) + 2 * sizeof(EcGTab));
 }
 
 // Intermediate per-item status codes (never returned to the caller)
@@ -171,8 +174,10 @@ void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_ite
                      hipStream_t stream, hipEvent_t tables_ready);
 hipError_t ec_upload_constants();
 hipError_t ec_init_const(void* d_btab, hipStream_t stream);
-void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                       const KeyWs& w, hipStream_t stream_r1, hipStream_t stream_k1);
+void ec_launch_keyprep_decode(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                              const KeyWs& w, hipStream_t stream);
+void ec_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream_r1,
+                              hipStream_t stream_k1);
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
                      const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,

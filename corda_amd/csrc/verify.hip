@@ -47,19 +47,19 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   if (n_keys == 0) return hipSuccess;
   const KeyWs w = key_ws(d_keyprep, n_keys);
   if (!fork) {
-    ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, stream, stream);
+    ec_launch_keyprep_decode(d_keys, n_keys, d_arena, arena_len, w, stream);
     ed_launch_keyprep_decode(d_keys, n_keys, d_arena, arena_len, w, stream);
+    ec_launch_keyprep_tables(d_keys, n_keys, w, stream, stream);
     ed_launch_keyprep_tables(d_keys, n_keys, w, stream);
     return hipGetLastError();
   }
-  hipError_t e = hipEventRecord(fork->start, stream);
-  for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->start, 0);
-  if (e != hipSuccess) return e;
-  ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, fork->side[0], fork->side[1]);
+  // decode on the main stream (item prep needs the key status), tables on the side streams
+  ec_launch_keyprep_decode(d_keys, n_keys, d_arena, arena_len, w, stream);
   ed_launch_keyprep_decode(d_keys, n_keys, d_arena, arena_len, w, stream);
-  e = hipEventRecord(fork->decoded, stream);
-  if (e == hipSuccess) e = hipStreamWaitEvent(fork->side[2], fork->decoded, 0);
+  hipError_t e = hipEventRecord(fork->decoded, stream);
+  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->decoded, 0);
   if (e != hipSuccess) return e;
+  ec_launch_keyprep_tables(d_keys, n_keys, w, fork->side[0], fork->side[1]);
   ed_launch_keyprep_tables(d_keys, n_keys, w, fork->side[2]);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventRecord(fork->ready[k], fork->side[k]);
   if (e != hipSuccess) return e;

@@ -1,10 +1,12 @@
 // ECDSA (SHA256withECDSA) verification kernels on secp256r1 / secp256k1, BouncyCastle 1.57
 // semantics (ecdsa.h header comment).
-//   k_ec_keyprep_rows  one lane per ECDSA key: decode + validate Q, row bases 2^{24j} Q
+//   k_ec_keyprep_decode one lane per ECDSA key: decode + validate Q (main stream)
+//   k_ec_keyprep_chain one lane per ECDSA key: row bases 2^{24j} Q (side stream, overlaps
+//                      k_ec_prep / k_ec_inv)
 //   k_ec_keyprep_tab   one lane per (key, row): 32 affine multiples, one batched inversion
 //   k_ec_prep          one lane per item: DER, range checks, SHA-256, e mod n
 //   k_ec_inv           16 items per lane: one shared inversion of s mod n -> u1, u2
-//   k_ec_ladder        one lane per item: u1 G + u2 Q over the row tables (G rows in LDS),
+//   k_ec_ladder        one lane per item: u1 G (radix-2^10 constant table) + u2 Q (key rows),
 //                      BC's inversion-free x(R) == r check
 // Replaces, per item, BC DSABase.engineVerify behind Crypto.isValid
 // (core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559, schemes :92-117).
@@ -22,7 +24,7 @@ __device__ __forceinline__ uint8_t ec_scheme() {
 }
 
 template <int C>
-__global__ void __launch_bounds__(64) k_ec_keyprep_rows(const cg_key* __restrict__ keys, uint32_t n_keys,
+__global__ void __launch_bounds__(64) k_ec_keyprep_decode(const cg_key* __restrict__ keys, uint32_t n_keys,
                                                         const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                         EdKeyHdr* __restrict__ hdr, BaseSlot* __restrict__ bases) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -37,12 +39,24 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_rows(const cg_key* __restrict
     f29 xm, ym;
     if (ec_key_decode_bytes<C>(xm, ym, arena, round4(arena_len), k.off, k.len, k.fmt, c_ec[C]) == 0) {
       h.status = 0;
-      Jac b[EC_ROWS];
-      ec_row_bases<C>(b, xm, ym, c_ec[C]);
-      for (int j = 0; j < EC_ROWS; ++j) bases[(size_t)i * EC_ROWS + j].ec = b[j];
+      bases[(size_t)i * EC_ROWS].ec = Jac{xm, ym, c_ec[C].one_p};
     }
   }
   hdr[i] = h;
+}
+
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_keyprep_chain(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                         const EdKeyHdr* __restrict__ hdr,
+                                                         BaseSlot* __restrict__ bases) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_keys) return;
+  if (keys[i].scheme != ec_scheme<C>() || hdr[i].status != 0) return;
+  Jac P = bases[(size_t)i * EC_ROWS].ec;
+  for (int j = 1; j < EC_ROWS; ++j) {
+    jac_dbl_n<C>(P, P, EC_W * EC_WINDOWS);
+    bases[(size_t)i * EC_ROWS + j].ec = P;
+  }
 }
 
 // one lane per (key, row)
@@ -58,10 +72,13 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_tab(const cg_key* __restrict_
   ec_row_build<C>(tabs[i].ec.t[j], bases[g].ec, scratch[g], c_ec[C]);
 }
 
+// one lane per (G row u, group g of 32 multiples)
 template <int C>
-__global__ void k_ec_grows_init(EcRowTab* __restrict__ out, EcRowScratch* __restrict__ scratch) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  ec_g_rows_init<C>(*out, *scratch, c_ec[C]);
+__global__ void __launch_bounds__(64) k_ec_gtab_init(EcGTab* __restrict__ out, EcRowScratch* __restrict__ scratch) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= EC_GTAB_LANES) return;
+  const int u = (int)(l / (EC_G_MULT / EC_MULT)), g = (int)(l % (EC_G_MULT / EC_MULT));
+  ec_gtab_group<C>(&out->t[u][g * EC_MULT], u, g, scratch[l], c_ec[C]);
 }
 
 // Plan positions of curve C: [ranges[c], ranges[c + 1]), c = plan_class_of_curve(C)
@@ -122,24 +139,15 @@ template <int C>
 __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
                                                    const uint32_t* __restrict__ ranges,
                                                    const TabSlot* __restrict__ tabs,
-                                                   const EcRowTab* __restrict__ gtab, uint8_t* __restrict__ status,
+                                                   const EcGTab* __restrict__ gtab, uint8_t* __restrict__ status,
                                                    const EcItemWs* __restrict__ ws) {
   EC_RANGE(C);
-  const uint64_t p0 = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x;
-  if (p0 >= end) return;  // whole block past this curve's range
-  __shared__ EcRowTab sG;
-  {
-    const uint4* src = (const uint4*)gtab;
-    uint4* dst = (uint4*)&sG;
-    for (uint32_t w = threadIdx.x; w < sizeof(EcRowTab) / 16; w += blockDim.x) dst[w] = src[w];
-  }
-  __syncthreads();
-  const uint64_t p = p0 + threadIdx.x;
+  const uint64_t p = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= end) return;
   const uint32_t i = perm[p];
   if (status[i] != EC_PENDING_BASE + C) return;
   const EcItemWs w = ws[p];
-  status[i] = (uint8_t)ecdsa_ladder_check<C>(w.a, w.b, w.r, sG, tabs[items[i].key_idx].ec, c_ec[C]);
+  status[i] = (uint8_t)ecdsa_ladder_check<C>(w.a, w.b, w.r, *gtab, tabs[items[i].key_idx].ec, c_ec[C]);
 }
 
 hipError_t ec_upload_constants() {
@@ -150,32 +158,42 @@ hipError_t ec_upload_constants() {
 }
 
 hipError_t ec_init_const(void* d_btab, hipStream_t stream) {
-  hipLaunchKernelGGL(k_ec_grows_init<CG_CURVE_K1>, dim3(1), dim3(64), 0, stream,
-                     (EcRowTab*)gtab(d_btab, CG_CURVE_K1), const_scratch(d_btab));
-  hipLaunchKernelGGL(k_ec_grows_init<CG_CURVE_R1>, dim3(1), dim3(64), 0, stream,
-                     (EcRowTab*)gtab(d_btab, CG_CURVE_R1), const_scratch(d_btab));
+  const dim3 g((EC_GTAB_LANES + 63) / 64);
+  hipLaunchKernelGGL(k_ec_gtab_init<CG_CURVE_K1>, g, dim3(64), 0, stream, (EcGTab*)gtab(d_btab, CG_CURVE_K1),
+                     const_scratch(d_btab));
+  hipLaunchKernelGGL(k_ec_gtab_init<CG_CURVE_R1>, g, dim3(64), 0, stream, (EcGTab*)gtab(d_btab, CG_CURVE_R1),
+                     const_scratch(d_btab));
   return hipGetLastError();
 }
 
-void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                       const KeyWs& w, hipStream_t stream_r1, hipStream_t stream_k1) {
-  const uint32_t B = 64;
-  const dim3 g((n_keys + B - 1) / B);
-  const uint32_t elanes = n_keys * EC_ROWS;
-  hipLaunchKernelGGL(k_ec_keyprep_rows<CG_CURVE_R1>, g, dim3(B), 0, stream_r1, d_keys, n_keys, d_arena, arena_len,
+void ec_launch_keyprep_decode(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                              const KeyWs& w, hipStream_t stream) {
+  const dim3 g((n_keys + 63) / 64);
+  hipLaunchKernelGGL(k_ec_keyprep_decode<CG_CURVE_R1>, g, dim3(64), 0, stream, d_keys, n_keys, d_arena, arena_len,
                      w.hdr, w.bases);
-  hipLaunchKernelGGL(k_ec_keyprep_tab<CG_CURVE_R1>, dim3((elanes + B - 1) / B), dim3(B), 0, stream_r1, d_keys,
-                     n_keys, w.hdr, w.bases, w.tab, w.ecs);
-  hipLaunchKernelGGL(k_ec_keyprep_rows<CG_CURVE_K1>, g, dim3(B), 0, stream_k1, d_keys, n_keys, d_arena, arena_len,
+  hipLaunchKernelGGL(k_ec_keyprep_decode<CG_CURVE_K1>, g, dim3(64), 0, stream, d_keys, n_keys, d_arena, arena_len,
                      w.hdr, w.bases);
-  hipLaunchKernelGGL(k_ec_keyprep_tab<CG_CURVE_K1>, dim3((elanes + B - 1) / B), dim3(B), 0, stream_k1, d_keys,
-                     n_keys, w.hdr, w.bases, w.tab, w.ecs);
 }
 
 template <int C>
-static void launch_curve(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
+static void launch_tables(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream) {
+  const uint32_t B = 64, elanes = n_keys * EC_ROWS;
+  hipLaunchKernelGGL(k_ec_keyprep_chain<C>, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
+                     w.bases);
+  hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3((elanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
+                     w.bases, w.tab, w.ecs);
+}
+
+void ec_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream_r1,
+                              hipStream_t stream_k1) {
+  launch_tables<CG_CURVE_R1>(d_keys, n_keys, w, stream_r1);
+  launch_tables<CG_CURVE_K1>(d_keys, n_keys, w, stream_k1);
+}
+
+template <int C>
+static void launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
                          uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len,
-                         const ItemWs& iw, const void* d_btab, hipStream_t stream) {
+                         const ItemWs& iw, hipStream_t stream) {
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;  // a curve's range is at most n_items long
   EcItemWs* ws = (EcItemWs*)iw.slots;
@@ -184,22 +202,30 @@ static void launch_curve(const cg_item* d_items, uint64_t n_items, const uint8_t
   const uint64_t igrid = (n_items + (uint64_t)B * EC_INV_K - 1) / ((uint64_t)B * EC_INV_K);
   hipLaunchKernelGGL(k_ec_inv<C>, dim3((unsigned)igrid), dim3(B), 0, stream, iw.perm, iw.ranges,
                      (const uint8_t*)d_status, ws);
-  hipLaunchKernelGGL(k_ec_ladder<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.tab,
-                     gtab(d_btab, C), d_status, (const EcItemWs*)ws);
 }
 
+template <int C>
+static void launch_ladder(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                          const ItemWs& iw, const void* d_btab, hipStream_t stream, hipEvent_t ready) {
+  if (ready) hipStreamWaitEvent(stream, ready, 0);
+  const uint32_t B = 256;
+  const uint64_t grid = (n_items + B - 1) / B;
+  hipLaunchKernelGGL(k_ec_ladder<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.tab,
+                     gtab(d_btab, C), d_status, (const EcItemWs*)iw.slots);
+}
+
+// prep + inversion of both curves first (they need only the decoded keys), then the ladders,
+// each after its curve's key tables are ready
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
                      const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
                      hipStream_t stream, hipEvent_t ready_r1, hipEvent_t ready_k1) {
   (void)d_keys;
   (void)n_keys;
-  if (ready_r1) hipStreamWaitEvent(stream, ready_r1, 0);
-  launch_curve<CG_CURVE_R1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, d_btab,
-                            stream);
-  if (ready_k1) hipStreamWaitEvent(stream, ready_k1, 0);
-  launch_curve<CG_CURVE_K1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, d_btab,
-                            stream);
+  launch_front<CG_CURVE_R1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
+  launch_front<CG_CURVE_K1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
+  launch_ladder<CG_CURVE_R1>(d_items, n_items, d_status, w, iw, d_btab, stream, ready_r1);
+  launch_ladder<CG_CURVE_K1>(d_items, n_items, d_status, w, iw, d_btab, stream, ready_k1);
 }
 
 }  // namespace cg

@@ -270,12 +270,14 @@ static int ecdsa_rows_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
                              uint64_t sig_off, uint32_t sig_len, uint64_t msg_off, uint64_t msg_len) {
   kinit();
   const EcConsts& K = g_K[C];
-  static EcRowTab* TG[2] = {nullptr, nullptr};
+  static EcGTab* TG[2] = {nullptr, nullptr};
   static EcRowTab* TQ = new EcRowTab;
   static EcRowScratch* S = new EcRowScratch;
-  if (!TG[C]) {
-    TG[C] = new EcRowTab;
-    ec_g_rows_init<C>(*TG[C], *S, K);
+  if (!TG[C]) {  // the device table build, lane by lane
+    TG[C] = new EcGTab;
+    for (int l = 0; l < EC_G_DIGITS * (EC_G_MULT / EC_MULT); ++l)
+      ec_gtab_group<C>(&TG[C]->t[l / (EC_G_MULT / EC_MULT)][(l % (EC_G_MULT / EC_MULT)) * EC_MULT],
+                       l / (EC_G_MULT / EC_MULT), l % (EC_G_MULT / EC_MULT), *S, K);
   }
   f29 xm, ym;
   uint32_t st = ec_key_decode_bytes<C>(xm, ym, arena, lr, key_off, key_len, fmt, K);

@@ -6,7 +6,7 @@ set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/ab_$TAG
 mkdir -p $OUT
-B="python3 bench.py --steps 10 --no-cpu-baseline --ecdsa-items 0 --mixed-items 0 --pipeline-txs 0"
+B="python3 bench.py --steps 10 --no-cpu-baseline ${BENCH_ARGS:---ecdsa-items 0 --mixed-items 0 --pipeline-txs 0}"
 for round in 1 2; do
   timeout -k 10 200 $B > $OUT/base_$round.log 2>&1 || exit 1
   i=0
@@ -15,4 +15,4 @@ for round in 1 2; do
     CORDA_AMD_LIB=$v timeout -k 10 200 $B > $OUT/v${i}_$round.log 2>&1 || exit 1
   done
 done
-for f in $OUT/*.log; do echo "$f $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["kernel_ms"])')"; done
+for f in $OUT/*.log; do echo "$f $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["kernel_ms"], *[(k, v["value"], v["kernel_ms"]) for k, v in d["secondary"].items()])')"; done

@@ -38,7 +38,7 @@ MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # code (tests/native/host_kernels.cpp t_ed_verify_wb / t_ed_count_w6; pinned by
 # tests/test_host_kernels.py::test_executed_work_constants_match_lane_code).
 # (field multiplies, field squarings):
-ED_VERIFY_FE = (536, 72)   # k_ed_ladder: 43 + 26 mixed additions (W=6 rows of -A, radix-2^10 B) + 18 doublings
+ED_VERIFY_FE = (500, 24)   # k_ed_ladder: 43 + 26 mixed additions (-A rows W=6 in 2 windows, radix-2^10 B) + 6 doublings
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
 ED_FINISH_K = 16
@@ -50,7 +50,7 @@ MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
 # kernel generation whose PMC traffic profile is committed (profiles/r01/pmc_traffic.json)
-KERNEL_VERSION = "ed25519_v4"
+KERNEL_VERSION = "ed25519_v5"
 
 
 def parse():

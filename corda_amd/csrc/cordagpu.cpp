@@ -65,7 +65,7 @@ struct DevBuf {
 struct cg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  cg::Fork fork = {{nullptr, nullptr, nullptr}, nullptr, {nullptr, nullptr, nullptr}};
+  cg::Fork fork = {{nullptr, nullptr, nullptr}, nullptr, {nullptr, nullptr}, {nullptr, nullptr, nullptr}};
   std::mutex mu;
   DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
   // transaction pipeline: verify items, spliced messages, templates; host-entry staging
@@ -109,7 +109,9 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     return hip_fail(e, "hipStreamCreate");
   }
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamCreateWithFlags(&c->fork.side[k], hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.decoded, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.start, hipEventDisableTiming);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k)
+    e = hipEventCreateWithFlags(&c->fork.ec_decoded[k], hipEventDisableTiming);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.ready[k], hipEventDisableTiming);
   if (e == hipSuccess) e = cg::upload_constants();
   if (e == hipSuccess) e = c->btab.ensure(cg::btab_bytes());
@@ -147,7 +149,9 @@ void cg_close(cg_ctx* c) {
     }
     if (c->fork.ready[k]) hipEventDestroy(c->fork.ready[k]);
   }
-  if (c->fork.decoded) hipEventDestroy(c->fork.decoded);
+  if (c->fork.start) hipEventDestroy(c->fork.start);
+  for (int k = 0; k < 2; ++k)
+    if (c->fork.ec_decoded[k]) hipEventDestroy(c->fork.ec_decoded[k]);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }

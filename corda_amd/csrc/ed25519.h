@@ -87,6 +87,26 @@ CG_HD int ed_decode_point(ge_p3& A, const uint32_t aw[8], const Ed25519Consts& C
   return ED_ST_VALID;
 }
 
+// Abyte = A.toByteArray() of the point ed_decode_point would return, without the square root:
+// the canonical y (bit 255 masked, reduced mod p) and x's sign bit, which the decode's sign
+// fix-up makes equal to the encoded bit unless x = 0 (y = +-1, where the fix-up leaves 0).
+// Meaningful only for keys that decode (the caller checks the decode status separately).
+CG_HD void ed_abyte_fast(uint32_t out[8], const uint32_t aw[8]) {
+  fe y;
+  fe_frombytes_words(y, aw);
+  fe_tobytes_words(out, y);
+  uint32_t one = out[0] ^ 1u, m1 = out[0] ^ 0xffffffecu;
+#pragma unroll
+  for (int i = 1; i < 7; ++i) {
+    one |= out[i];
+    m1 |= out[i] ^ 0xffffffffu;
+  }
+  one |= out[7];
+  m1 |= out[7] ^ 0x7fffffffu;
+  const uint32_t x_zero = (one == 0u) | (m1 == 0u);
+  out[7] |= (aw[7] >> 31 & ~x_zero & 1u) << 31;
+}
+
 CG_HD void ed_encode_affine(uint32_t out[8], const fe& X, const fe& Y, const fe& Z) {
   fe zi, x, y;
   fe_invert(zi, Z);

@@ -12,6 +12,13 @@
 #pragma once
 #include "ed25519.h"
 
+// Product configuration (k_ed_keyprep_* / k_ed_ladder): -A rows of signed radix-2^6 digits in
+// 2 windows (22 rows x 32 multiples per key, 6 doublings per item), B in signed radix 2^10
+// over a constant table (26 rows x 512).
+#define ED_W 6
+#define ED_K 2
+#define ED_WB 10
+
 template <int W, int K>
 struct EdRowsCfg {
   // the top digit keeps >= 1 bit of headroom for the recoding carry unless W divides 253
@@ -88,12 +95,64 @@ CG_HD void ed_row_multiples(ge_niels* row, const ge_p3& P, const fe& d2) {
   }
 }
 
+// Affine niels multiples 1..M of P with ONE field inversion per row (Montgomery's trick over
+// the whole row): the forward pass leaves each multiple's projective X, Y, Z in its own niels
+// slot (the row is its own scratch) and the running Z prefix products in zpre[0..M-1]; the
+// backward pass turns 1 / (Z_0 ... Z_{M-1}) into every 1/Z_k. ~23 field ops per entry
+// instead of ~52 for batches of 8.
+template <int M>
+CG_HD void ed_row_build(ge_niels* row, const ge_p3& P, const fe& d2, fe* zpre) {
+  ge_cached c;
+  ge_p3_to_cached(c, P, d2);
+  ge_p3 cur = P;
+  ge_p1p1 t;
+  fe run;
+  for (int k = 0; k < M; ++k) {
+    if (k != 0) {
+      ge_add_cached(t, cur, c);
+      ge_p1p1_to_p3(cur, t);
+    }
+    ge_niels& s = row[k];
+    fe_copy(s.ypx, cur.X);
+    fe_copy(s.ymx, cur.Y);
+    fe_copy(s.xy2d, cur.Z);
+    if (k == 0) {
+      fe_copy(run, cur.Z);
+    } else {
+      fe_mul(run, run, cur.Z);
+    }
+    fe_copy(zpre[k], run);
+  }
+  fe inv;
+  fe_invert(inv, run);
+  for (int k = M - 1; k >= 0; --k) {
+    ge_niels& s = row[k];
+    fe zi;
+    if (k > 0) {
+      fe_mul(zi, inv, zpre[k - 1]);
+      fe_mul(inv, inv, s.xy2d);
+    } else {
+      fe_copy(zi, inv);
+    }
+    fe x, y, xy;
+    fe_mul(x, s.ypx, zi);
+    fe_mul(y, s.ymx, zi);
+    fe_add(s.ypx, y, x);
+    fe_carry(s.ypx);
+    fe_sub(s.ymx, y, x);
+    fe_carry(s.ymx);
+    fe_mul(xy, x, y);
+    fe_mul(s.xy2d, xy, d2);
+  }
+}
+
 template <int W, int K>
 CG_HD void ed_rows_w_init(EdRowTabW<W, K>& T, const ge_p3& P, const fe& d2) {
   typedef EdRowsCfg<W, K> C;
   ge_p3 Pj = P;
   for (int j = 0; j < C::kRows; ++j) {
-    ed_row_multiples<C::kMult>(T.t[j], Pj, d2);
+    fe zpre[C::kMult];
+    ed_row_build<C::kMult>(T.t[j], Pj, d2, zpre);
     if (j + 1 < C::kRows) ed_dbl_n(Pj, Pj, W * K);
   }
 }

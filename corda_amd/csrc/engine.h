@@ -15,9 +15,12 @@ struct DeviceConsts;  // opaque
 // work that needs only decoded keys (the plan, the SHA-512 challenges). Each consumer waits
 // for its `ready` event just before it reads tables: ready[0] secp256r1, [1] secp256k1,
 // [2] Ed25519.
+// Key prep fork: side[0] / side[1] build the secp256r1 / secp256k1 keys (decode -> chain -> tab),
+// side[2] the Ed25519 keys; `start` orders them after the main stream's earlier work,
+// ec_decoded[c] / ready[c] are what the item kernels on the main stream wait for.
 struct Fork {
   hipStream_t side[3];
-  hipEvent_t decoded, ready[3];
+  hipEvent_t start, ec_decoded[2], ready[3];
 };
 
 // Upload the constant tables (curve constants, base-point tables) for the current device.

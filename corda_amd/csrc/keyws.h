@@ -34,11 +34,13 @@ __device__ __forceinline__ uint64_t item_msg_len(const cg_item& it, uint64_t are
 }
 
 // Row tables (ed25519_rows.h) with signed radix-64 digits: 43 digits in 11 rows of 4 windows.
-#define ED_W 6
-#define ED_K 4
 typedef EdRowsCfg<ED_W, ED_K> EdCfg;
-typedef EdRowTabW<ED_W, ED_K> EdTab;  // 11 x 32 affine niels = 42240 B
-#define ED_WB 10
+typedef EdRowTabW<ED_W, ED_K> EdTab;  // 22 x 32 affine niels = 84480 B
+// base slots per key, one stride for both schemes (Ed25519 rows >= ECDSA rows)
+#define KEY_BASES EdCfg::kRows
+static_assert(KEY_BASES >= EC_ROWS, "ECDSA row bases fit a key's base slots");
+static_assert(EdCfg::kRows * EdCfg::kMult * sizeof(fe) <= EC_ROWS * sizeof(EcRowScratch),
+              "Ed25519 row-build Z prefixes live in the key's ECDSA scratch");
 typedef EdBCfg<ED_W, ED_K, ED_WB> EdBCfgT;
 typedef EdBTabW<ED_W, ED_K, ED_WB> EdBTab;  // 26 x 512 affine niels = 1.6 MB, constant
 
@@ -75,9 +77,10 @@ __device__ __forceinline__ int plan_class_of_curve(int curve) { return curve == 
 // Key workspace, each region n_keys long (a key is either Ed25519 or ECDSA, so the table and
 // base slots are shared: TabSlot / BaseSlot unions give one stride for both schemes):
 //   hdr      EdKeyHdr (status [+ Abyte])                       64 B
-//   tab      EdTab | EcRowTab                                  42 240 B
-//   bases    11 x (ge_p3 | Jac)                                1 760 B
-//   ecs      11 x EcRowScratch (ECDSA batch-inversion scratch) 45 056 B
+//   tab      EdTab | EcRowTab                                  84 480 B
+//   bases    KEY_BASES = 22 x (ge_p3 | Jac)                    3 520 B
+//   ecs      11 x EcRowScratch (ECDSA batch-inversion scratch;  50 688 B
+//            an Ed25519 key's row-build Z prefixes)
 static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct KeyWs {
   EdKeyHdr* hdr;
@@ -94,13 +97,13 @@ static inline KeyWs key_ws(void* base, uint32_t n_keys) {
   w.tab = (TabSlot*)p;
   p += al256(n * sizeof(TabSlot));
   w.bases = (BaseSlot*)p;
-  p += al256(n * EdCfg::kRows * sizeof(BaseSlot));
+  p += al256(n * KEY_BASES * sizeof(BaseSlot));
   w.ecs = (EcRowScratch*)p;
   return w;
 }
 static inline size_t key_ws_bytes(uint32_t n_keys) {
   const size_t n = n_keys ? n_keys : 1;
-  return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(TabSlot)) + al256(n * EdCfg::kRows * sizeof(BaseSlot)) +
+  return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(TabSlot)) + al256(n * KEY_BASES * sizeof(BaseSlot)) +
          n * EC_ROWS * sizeof(EcRowScratch);
 }
 
@@ -165,22 +168,24 @@ static inline EcRowScratch* const_scratch(void* d_btab) {
 // Per-scheme halves (verify_ed.hip / verify_ec.hip)
 hipError_t ed_upload_constants();
 hipError_t ed_init_const(void* d_btab, hipStream_t stream);
-void ed_launch_keyprep_decode(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+void ed_launch_key_abyte(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                         const KeyWs& w, hipStream_t stream);
+// decode -> chain -> tab
+void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                               const KeyWs& w, hipStream_t stream);
-void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream);
 void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
                      const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
                      hipStream_t stream, hipEvent_t tables_ready);
 hipError_t ec_upload_constants();
 hipError_t ec_init_const(void* d_btab, hipStream_t stream);
-void ec_launch_keyprep_decode(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                              const KeyWs& w, hipStream_t stream);
-void ec_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream_r1,
-                              hipStream_t stream_k1);
+// decode (records `decoded`: k_ec_prep needs the key status) -> chain -> tab, per curve
+void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                       const KeyWs& w, hipStream_t stream_r1, hipStream_t stream_k1, hipEvent_t decoded_r1,
+                       hipEvent_t decoded_k1);
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
                      const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
-                     hipStream_t stream, hipEvent_t ready_r1, hipEvent_t ready_k1);
+                     hipStream_t stream, const hipEvent_t decoded[2], const hipEvent_t ready[2]);
 
 }  // namespace cg

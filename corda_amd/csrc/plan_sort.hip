@@ -17,6 +17,12 @@
 
 namespace cg {
 
+// Onesweep at every size above one block: rocprim's default switches to block sort + merge
+// passes up to 2^20 items, which took ~300 us for 2^20 items over 14 key bits (ten merge
+// passes) against ~2 onesweep passes of 8 bits.
+typedef rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>
+    PlanSortConfig;
+
 static uint32_t key_bits(uint32_t n_keys) {
   uint32_t b = 1;
   while (b < 30 && (1u << b) < n_keys) ++b;
@@ -57,7 +63,7 @@ __global__ void k_plan_ranges(const uint32_t* __restrict__ skey, uint64_t n_item
 
 size_t plan_sort_temp_bytes(uint64_t n_items) {
   size_t bytes = 0;
-  rocprim::radix_sort_pairs((void*)nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+  rocprim::radix_sort_pairs<PlanSortConfig>((void*)nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                             (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)(n_items ? n_items : 1), 0u,
                             32u);
   return bytes;
@@ -70,7 +76,7 @@ hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d
   hipLaunchKernelGGL(k_plan_keys, dim3((unsigned)((n_items + B - 1) / B)), dim3(B), 0, stream, d_items, n_items,
                      d_keys, n_keys, kb, iw.skey_in, iw.sval_in);
   size_t bytes = iw.sort_temp_bytes;
-  hipError_t e = rocprim::radix_sort_pairs(iw.sort_temp, bytes, (const uint32_t*)iw.skey_in, iw.skey_out,
+  hipError_t e = rocprim::radix_sort_pairs<PlanSortConfig>(iw.sort_temp, bytes, (const uint32_t*)iw.skey_in, iw.skey_out,
                                            (const uint32_t*)iw.sval_in, iw.perm, (size_t)n_items, 0u, kb + 2,
                                            stream);
   if (e != hipSuccess) return e;

@@ -47,22 +47,21 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   if (n_keys == 0) return hipSuccess;
   const KeyWs w = key_ws(d_keyprep, n_keys);
   if (!fork) {
-    ec_launch_keyprep_decode(d_keys, n_keys, d_arena, arena_len, w, stream);
-    ed_launch_keyprep_decode(d_keys, n_keys, d_arena, arena_len, w, stream);
-    ec_launch_keyprep_tables(d_keys, n_keys, w, stream, stream);
-    ed_launch_keyprep_tables(d_keys, n_keys, w, stream);
+    ed_launch_key_abyte(d_keys, n_keys, d_arena, arena_len, w, stream);
+    ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, stream, stream, nullptr, nullptr);
+    ed_launch_keyprep_tables(d_keys, n_keys, d_arena, arena_len, w, stream);
     return hipGetLastError();
   }
-  // decode on the main stream (item prep needs the key status), tables on the side streams
-  ec_launch_keyprep_decode(d_keys, n_keys, d_arena, arena_len, w, stream);
-  ed_launch_keyprep_decode(d_keys, n_keys, d_arena, arena_len, w, stream);
-  hipError_t e = hipEventRecord(fork->decoded, stream);
-  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->decoded, 0);
+  hipError_t e = hipEventRecord(fork->start, stream);
+  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->start, 0);
   if (e != hipSuccess) return e;
-  ec_launch_keyprep_tables(d_keys, n_keys, w, fork->side[0], fork->side[1]);
-  ed_launch_keyprep_tables(d_keys, n_keys, w, fork->side[2]);
+  ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, fork->side[0], fork->side[1], fork->ec_decoded[0],
+                    fork->ec_decoded[1]);
+  ed_launch_keyprep_tables(d_keys, n_keys, d_arena, arena_len, w, fork->side[2]);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventRecord(fork->ready[k], fork->side[k]);
   if (e != hipSuccess) return e;
+  // the only key work on the main stream: Abyte for k_ed_hash (no decode)
+  ed_launch_key_abyte(d_keys, n_keys, d_arena, arena_len, w, stream);
   return hipGetLastError();
 }
 
@@ -83,7 +82,7 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
   ed_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
                   d_btab, stream, fork ? fork->ready[2] : nullptr);
   ec_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
-                  d_btab, stream, fork ? fork->ready[0] : nullptr, fork ? fork->ready[1] : nullptr);
+                  d_btab, stream, fork ? fork->ec_decoded : nullptr, fork ? fork->ready : nullptr);
   return hipGetLastError();
 }
 

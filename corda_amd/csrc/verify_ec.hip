@@ -1,9 +1,8 @@
 // ECDSA (SHA256withECDSA) verification kernels on secp256r1 / secp256k1, BouncyCastle 1.57
 // semantics (ecdsa.h header comment).
-//   k_ec_keyprep_decode one lane per ECDSA key: decode + validate Q (main stream)
-//   k_ec_keyprep_chain one lane per ECDSA key: row bases 2^{24j} Q (side stream, overlaps
-//                      k_ec_prep / k_ec_inv)
-//   k_ec_keyprep_tab   one lane per (key, row): 32 affine multiples, one batched inversion
+//   k_ec_keyprep_decode one lane per ECDSA key: decode + validate Q   (side stream of the curve;
+//   k_ec_keyprep_chain one lane per ECDSA key: row bases 2^{24j} Q      prep waits for the decode,
+//   k_ec_keyprep_tab   one lane per (key, row): 32 affine multiples     the ladder for the tab)
 //   k_ec_prep          one lane per item: DER, range checks, SHA-256, e mod n
 //   k_ec_inv           16 items per lane: one shared inversion of s mod n -> u1, u2
 //   k_ec_ladder        one lane per item: u1 G (radix-2^10 constant table) + u2 Q (key rows),
@@ -39,7 +38,7 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_decode(const cg_key* __restri
     f29 xm, ym;
     if (ec_key_decode_bytes<C>(xm, ym, arena, round4(arena_len), k.off, k.len, k.fmt, c_ec[C]) == 0) {
       h.status = 0;
-      bases[(size_t)i * EC_ROWS].ec = Jac{xm, ym, c_ec[C].one_p};
+      bases[(size_t)i * KEY_BASES].ec = Jac{xm, ym, c_ec[C].one_p};
     }
   }
   hdr[i] = h;
@@ -52,10 +51,10 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_chain(const cg_key* __restric
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_keys) return;
   if (keys[i].scheme != ec_scheme<C>() || hdr[i].status != 0) return;
-  Jac P = bases[(size_t)i * EC_ROWS].ec;
+  Jac P = bases[(size_t)i * KEY_BASES].ec;
   for (int j = 1; j < EC_ROWS; ++j) {
     jac_dbl_n<C>(P, P, EC_W * EC_WINDOWS);
-    bases[(size_t)i * EC_ROWS + j].ec = P;
+    bases[(size_t)i * KEY_BASES + j].ec = P;
   }
 }
 
@@ -69,7 +68,7 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_tab(const cg_key* __restrict_
   const uint32_t i = g / EC_ROWS, j = g % EC_ROWS;
   if (i >= n_keys) return;
   if (keys[i].scheme != ec_scheme<C>() || hdr[i].status != 0) return;
-  ec_row_build<C>(tabs[i].ec.t[j], bases[g].ec, scratch[g], c_ec[C]);
+  ec_row_build<C>(tabs[i].ec.t[j], bases[(size_t)i * KEY_BASES + j].ec, scratch[g], c_ec[C]);
 }
 
 // one lane per (G row u, group g of 32 multiples)
@@ -166,28 +165,24 @@ hipError_t ec_init_const(void* d_btab, hipStream_t stream) {
   return hipGetLastError();
 }
 
-void ec_launch_keyprep_decode(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                              const KeyWs& w, hipStream_t stream) {
-  const dim3 g((n_keys + 63) / 64);
-  hipLaunchKernelGGL(k_ec_keyprep_decode<CG_CURVE_R1>, g, dim3(64), 0, stream, d_keys, n_keys, d_arena, arena_len,
-                     w.hdr, w.bases);
-  hipLaunchKernelGGL(k_ec_keyprep_decode<CG_CURVE_K1>, g, dim3(64), 0, stream, d_keys, n_keys, d_arena, arena_len,
-                     w.hdr, w.bases);
-}
-
 template <int C>
-static void launch_tables(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream) {
+static void launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                           const KeyWs& w, hipStream_t stream, hipEvent_t decoded) {
   const uint32_t B = 64, elanes = n_keys * EC_ROWS;
-  hipLaunchKernelGGL(k_ec_keyprep_chain<C>, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
+  const dim3 g((n_keys + B - 1) / B);
+  hipLaunchKernelGGL(k_ec_keyprep_decode<C>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.hdr,
                      w.bases);
+  if (decoded) hipEventRecord(decoded, stream);
+  hipLaunchKernelGGL(k_ec_keyprep_chain<C>, g, dim3(B), 0, stream, d_keys, n_keys, w.hdr, w.bases);
   hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3((elanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
                      w.bases, w.tab, w.ecs);
 }
 
-void ec_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream_r1,
-                              hipStream_t stream_k1) {
-  launch_tables<CG_CURVE_R1>(d_keys, n_keys, w, stream_r1);
-  launch_tables<CG_CURVE_K1>(d_keys, n_keys, w, stream_k1);
+void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                       const KeyWs& w, hipStream_t stream_r1, hipStream_t stream_k1, hipEvent_t decoded_r1,
+                       hipEvent_t decoded_k1) {
+  launch_keyprep<CG_CURVE_R1>(d_keys, n_keys, d_arena, arena_len, w, stream_r1, decoded_r1);
+  launch_keyprep<CG_CURVE_K1>(d_keys, n_keys, d_arena, arena_len, w, stream_k1, decoded_k1);
 }
 
 template <int C>
@@ -215,17 +210,19 @@ static void launch_ladder(const cg_item* d_items, uint64_t n_items, uint8_t* d_s
 }
 
 // prep + inversion of both curves first (they need only the decoded keys), then the ladders,
-// each after its curve's key tables are ready
+// each after its curve's key tables are ready (events null: everything is on `stream`)
 void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                      const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
                      const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
-                     hipStream_t stream, hipEvent_t ready_r1, hipEvent_t ready_k1) {
+                     hipStream_t stream, const hipEvent_t decoded[2], const hipEvent_t ready[2]) {
   (void)d_keys;
   (void)n_keys;
+  if (decoded && decoded[0]) hipStreamWaitEvent(stream, decoded[0], 0);
   launch_front<CG_CURVE_R1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
+  if (decoded && decoded[1]) hipStreamWaitEvent(stream, decoded[1], 0);
   launch_front<CG_CURVE_K1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
-  launch_ladder<CG_CURVE_R1>(d_items, n_items, d_status, w, iw, d_btab, stream, ready_r1);
-  launch_ladder<CG_CURVE_K1>(d_items, n_items, d_status, w, iw, d_btab, stream, ready_k1);
+  launch_ladder<CG_CURVE_R1>(d_items, n_items, d_status, w, iw, d_btab, stream, ready ? ready[0] : nullptr);
+  launch_ladder<CG_CURVE_K1>(d_items, n_items, d_status, w, iw, d_btab, stream, ready ? ready[1] : nullptr);
 }
 
 }  // namespace cg

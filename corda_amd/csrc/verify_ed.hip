@@ -1,11 +1,12 @@
 // Ed25519 (EDDSA_ED25519_SHA512) verification kernels, i2p 0.2.0 semantics.
-//   k_ed_keyprep_decode  one lane per distinct key: decode A, canonical Abyte, -A
-//   k_ed_keyprep_chain   one lane per key: row bases 2^{24j} (-A), j = 1..10
-//   k_ed_keyprep_tab     one lane per (key, row, 8 multiples): affine multiples of the row base
-//   k_ed_hash            one lane per item: SHA-512 challenge, scalar prep, radix-64 digits
-//                        (needs only the decoded keys: overlaps the table build)
-//   k_ed_ladder          one lane per item: 4 windows x (11 rows of -A + ~6.5 rows of the
-//                        radix-2^10 B table) mixed additions, 18 doublings
+//   k_ed_key_abyte       one lane per key (main stream): canonical Abyte without decoding
+//   k_ed_keyprep_decode  one lane per key (side stream): decode A -> key status, -A
+//   k_ed_keyprep_chain   one lane per key: row bases 2^{12j} (-A), j = 1..21
+//   k_ed_keyprep_tab     one lane per (key, row): the 32 affine multiples of the row base
+//   k_ed_hash            one lane per item: SHA-512 challenge, scalar prep, signed digits
+//                        (needs only Abyte: overlaps the whole key decode + table build)
+//   k_ed_ladder          one lane per item: key status, then 2 windows x (~21.5 rows of -A +
+//                        13 rows of the radix-2^10 B table) mixed additions, 6 doublings
 //   k_ed_finish          16 items per lane: batch inversion, encode, byte compare
 // Replaces, per item, i2p EdDSAEngine.engineVerify behind Crypto.isValid
 // (core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559, scheme :120-133).
@@ -17,7 +18,45 @@ __constant__ Ed25519Consts c_ed;
 
 static const uint8_t ED_SPKI_PREFIX[12] = {0x30, 0x2a, 0x30, 0x05, 0x06, 0x03, 0x2b, 0x65, 0x70, 0x03, 0x21, 0x00};
 
-// one lane per key: decode A (i2p rules), status, canonical Abyte, row base -A
+// Offset of A's 32 bytes in the arena for a raw or SPKI Ed25519 key; false for a malformed
+// encoding (wrong length / SPKI prefix / outside the arena).
+__device__ __forceinline__ bool ed_key_locate(const cg_key& k, const uint8_t* arena, uint64_t arena_len,
+                                              uint64_t& a_off) {
+  const uint64_t lr = round4(arena_len);
+  a_off = k.off;
+  if (!in_arena(k.off, k.len, arena_len)) return false;
+  if (k.fmt == CG_KEY_RAW) return k.len == 32;
+  if (k.fmt != CG_KEY_SPKI || k.len != 44) return false;
+  for (int b = 0; b < 12; ++b)
+    if ((cg_ld_bytes4(arena, lr, k.off + b) & 0xffu) != ED_SPKI_PREFIX[b]) return false;
+  a_off = k.off + 12;
+  return true;
+}
+
+// one lane per key, main stream: the canonical Abyte k_ed_hash needs, without the square root
+// (ed_abyte_fast), so the challenge hashes run while the keys are still being decoded
+__global__ void __launch_bounds__(64) k_ed_key_abyte(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                     const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                     EdKeyHdr* __restrict__ hdr) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_keys) return;
+  const cg_key k = keys[i];
+  if (k.scheme != CG_EDDSA_ED25519_SHA512) return;
+  uint64_t a_off;
+  uint32_t ab[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (ed_key_locate(k, arena, arena_len, a_off)) {
+    const uint64_t lr = round4(arena_len);
+    uint32_t aw[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) aw[w] = cg_ld_bytes4(arena, lr, a_off + 4 * w);
+    ed_abyte_fast(ab, aw);
+  }
+#pragma unroll
+  for (int w = 0; w < 8; ++w) hdr[i].abyte[w] = ab[w];
+}
+
+// one lane per key, side stream: decode A (i2p rules) -> key status, row base -A. Writes only
+// hdr.status (k_ed_key_abyte owns hdr.abyte).
 __global__ void __launch_bounds__(64) k_ed_keyprep_decode(const cg_key* __restrict__ keys, uint32_t n_keys,
                                                         const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                         EdKeyHdr* __restrict__ hdr, BaseSlot* __restrict__ bases) {
@@ -25,38 +64,22 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_decode(const cg_key* __restri
   if (i >= n_keys) return;
   const cg_key k = keys[i];
   if (k.scheme != CG_EDDSA_ED25519_SHA512) return;
-  const uint64_t lr = round4(arena_len);
-  uint64_t a_off = k.off;
-  bool ok = in_arena(k.off, k.len, arena_len);
-  if (ok && k.fmt == CG_KEY_RAW) {
-    ok = k.len == 32;
-  } else if (ok && k.fmt == CG_KEY_SPKI) {
-    ok = k.len == 44;
-    for (int b = 0; ok && b < 12; ++b) ok = (cg_ld_bytes4(arena, lr, k.off + b) & 0xffu) == ED_SPKI_PREFIX[b];
-    a_off = k.off + 12;
-  } else {
-    ok = false;
-  }
-  EdKeyHdr h;
-  for (int w = 0; w < 7; ++w) h.pad[w] = 0;
-  for (int w = 0; w < 8; ++w) h.abyte[w] = 0;
-  h.status = CG_KEY_INVALID;
-  if (ok) {
+  uint64_t a_off;
+  uint32_t st = CG_KEY_INVALID;
+  if (ed_key_locate(k, arena, arena_len, a_off)) {
+    const uint64_t lr = round4(arena_len);
     uint32_t aw[8];
 #pragma unroll
     for (int w = 0; w < 8; ++w) aw[w] = cg_ld_bytes4(arena, lr, a_off + 4 * w);
     ge_p3 A;
     if (ed_decode_point(A, aw, c_ed) == ED_ST_VALID) {
-      h.status = 0;
-      // canonical Abyte: A comes out of the decode affine (Z = 1), so no inversion is needed
-      fe_tobytes_words(h.abyte, A.Y);
-      h.abyte[7] |= (uint32_t)fe_isnegative(A.X) << 31;
+      st = 0;
       ge_p3 P;
       ed_neg_point(P, A);
-      bases[(size_t)i * EdCfg::kRows].ed = P;
+      bases[(size_t)i * KEY_BASES].ed = P;
     }
   }
-  hdr[i] = h;
+  hdr[i].status = st;
 }
 
 // one lane per key: row bases 2^{24j} (-A), j = 1..10 (a serial chain of 240 doublings)
@@ -66,10 +89,10 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_chain(const cg_key* __restric
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_keys) return;
   if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || hdr[i].status != 0) return;
-  ge_p3 P = bases[(size_t)i * EdCfg::kRows].ed;
+  ge_p3 P = bases[(size_t)i * KEY_BASES].ed;
   for (int j = 1; j < EdCfg::kRows; ++j) {
     ed_dbl_n(P, P, ED_W * ED_K);
-    bases[(size_t)i * EdCfg::kRows + j].ed = P;
+    bases[(size_t)i * KEY_BASES + j].ed = P;
   }
 }
 
@@ -90,31 +113,18 @@ __device__ void ed_small_mul(ge_p3& R, const ge_p3& P, uint32_t m) {
   }
 }
 
-// one lane per (key, row, group of 8 multiples)
+// one lane per (key, row): the 32 affine multiples of the row base, one inversion per row
+// (ed_row_build; Z prefixes in the key's ECDSA scratch, unused by an Ed25519 key)
 __global__ void __launch_bounds__(64) k_ed_keyprep_tab(const cg_key* __restrict__ keys, uint32_t n_keys,
                                                        const EdKeyHdr* __restrict__ hdr,
                                                        const BaseSlot* __restrict__ bases,
-                                                       TabSlot* __restrict__ tabs) {
-  constexpr uint32_t G = EdCfg::kMult / 8;
+                                                       TabSlot* __restrict__ tabs, EcRowScratch* __restrict__ ecs) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = g / (EdCfg::kRows * G);
-  const uint32_t rem = g % (EdCfg::kRows * G);
-  const uint32_t j = rem / G, grp = rem % G;
+  const uint32_t i = g / EdCfg::kRows, j = g % EdCfg::kRows;
   if (i >= n_keys) return;
   if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || hdr[i].status != 0) return;
-  const ge_p3 P = bases[(size_t)i * EdCfg::kRows + j].ed;
-  ge_p3 pts[8];
-  ed_small_mul(pts[0], P, 8 * grp + 1);
-  ge_cached c;
-  ge_p3_to_cached(c, P, c_ed.d2);
-  ge_p1p1 t;
-  for (int k = 1; k < 8; ++k) {
-    ge_add_cached(t, pts[k - 1], c);
-    ge_p1p1_to_p3(pts[k], t);
-  }
-  ge_niels row[8];
-  ed_niels_batch8(row, pts, c_ed.d2);
-  for (int k = 0; k < 8; ++k) tabs[i].ed.t[j][8 * grp + k] = row[k];
+  fe* zpre = (fe*)(ecs + (size_t)i * EC_ROWS) + (size_t)j * EdCfg::kMult;
+  ed_row_build<EdCfg::kMult>(tabs[i].ed.t[j], bases[(size_t)i * KEY_BASES + j].ed, c_ed.d2, zpre);
 }
 
 // The base point B as an extended point (from the constant niels table entry 1*B)
@@ -185,7 +195,7 @@ struct EdDigits {
 };
 static_assert(sizeof(EdDigits) == ITEM_SLOT, "digits must fill one item slot");
 
-// One lane per Ed25519 plan position: status checks, h = SHA-512(R || Abyte || M) mod L,
+// One lane per Ed25519 plan position: item checks, h = SHA-512(R || Abyte || M) mod L,
 // S' = i2p's slide value of S mod L, both recoded to signed radix-64 digits. Needs only the
 // decoded keys (Abyte), so it runs while the key tables are still being built.
 __global__ void __launch_bounds__(256) k_ed_hash(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
@@ -199,10 +209,8 @@ __global__ void __launch_bounds__(256) k_ed_hash(const cg_item* __restrict__ ite
   const uint32_t i = perm[p];
   const cg_item it = items[i];
   const EdKeyHdr* kh = hdr + it.key_idx;
-  uint8_t st;
-  if (kh->status != 0) {
-    st = CG_KEY_INVALID;
-  } else if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
+  uint8_t st;  // a key that does not decode overrides this in k_ed_ladder
+  if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
     st = CG_EMPTY;
   } else if (!in_arena(it.sig_off, it.sig_len, arena_len) ||
              !in_arena(it.msg_off, it.msg_len, item_msg_len(it, arena_len, msgs_len, msgs))) {
@@ -258,16 +266,20 @@ struct PickGlobal {
 // projective in the item slot.
 __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
-    const TabSlot* __restrict__ tabs, const EdBTab* __restrict__ btab, const uint8_t* __restrict__ status,
-    void* __restrict__ slots) {
+    const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBTab* __restrict__ btab,
+    uint8_t* __restrict__ status, void* __restrict__ slots) {
   const uint64_t p = (uint64_t)ranges[PLAN_ED] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ranges[PLAN_ED + 1]) return;
   const uint32_t i = perm[p];
+  const uint32_t key = items[i].key_idx;
+  if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
+    status[i] = CG_KEY_INVALID;
+    return;
+  }
   if (status[i] != ED_PENDING) return;
   const EdDigits d = ((const EdDigits*)slots)[p];
   ge_p2 q;
-  ed_double_scalar_wb<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[items[i].key_idx].ed, *btab, PickGlobal(),
-                                         PickGlobal());
+  ed_double_scalar_wb<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed, *btab, PickGlobal(), PickGlobal());
   ((ge_p2*)slots)[p] = q;
 }
 
@@ -330,20 +342,23 @@ hipError_t ed_init_const(void* d_btab, hipStream_t stream) {
   return hipGetLastError();
 }
 
-void ed_launch_keyprep_decode(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+void ed_launch_key_abyte(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                         const KeyWs& w, hipStream_t stream) {
+  const uint32_t B = 64;
+  hipLaunchKernelGGL(k_ed_key_abyte, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, d_arena,
+                     arena_len, w.hdr);
+}
+
+void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                               const KeyWs& w, hipStream_t stream) {
   const uint32_t B = 64;  // one wave per block: keys are few, spread them over CUs
   hipLaunchKernelGGL(k_ed_keyprep_decode, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, d_arena,
                      arena_len, w.hdr, w.bases);
-}
-
-void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream) {
-  const uint32_t B = 64;
   hipLaunchKernelGGL(k_ed_keyprep_chain, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
                      w.bases);
-  const uint32_t lanes = n_keys * EdCfg::kRows * (EdCfg::kMult / 8);
+  const uint32_t lanes = n_keys * EdCfg::kRows;
   hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((lanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
-                     w.bases, w.tab);
+                     w.bases, w.tab, w.ecs);
 }
 
 void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
@@ -357,8 +372,8 @@ void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_ite
   hipLaunchKernelGGL(k_ed_hash, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
                      arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
   if (tables_ready) hipStreamWaitEvent(stream, tables_ready, 0);
-  hipLaunchKernelGGL(k_ed_ladder, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.tab,
-                     (const EdBTab*)d_btab, (const uint8_t*)d_status, iw.slots);
+  hipLaunchKernelGGL(k_ed_ladder, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
+                     w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
   const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
   hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
                      arena_len, d_status, (const ge_p2*)iw.slots);

@@ -62,6 +62,7 @@ int t_ed_keyprep(const uint32_t* aw, uint32_t* abyte_out) {
   memcpy(abyte_out, kp.abyte, 32);
   return (int)kp.status;
 }
+void t_ed_abyte_fast(const uint32_t* aw, uint32_t* abyte_out) { ed_abyte_fast(abyte_out, aw); }
 int t_ed_verify(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len) {
   init();
   static EdKeyPrep kp;
@@ -211,6 +212,7 @@ extern "C" int t_ed_count_w6(const uint32_t* aw, const uint32_t* sw, const uint8
   (void)verify_w<6, 4>(aw, sw, msg, msg_len);  // builds static tables once
   typedef EdRowsCfg<6, 4> C;
   static EdRowTabW<6, 4> TA;
+  static EdRowTabW<ED_W, ED_K> TP;
   ge_p3 A, N;
   // per key
   g_fe_nmul = g_fe_nsq = 0;
@@ -222,7 +224,7 @@ extern "C" int t_ed_count_w6(const uint32_t* aw, const uint32_t* sw, const uint8
     uint32_t ab[8];
     ed_encode_affine(ab, A.X, A.Y, A.Z);
     ed_neg_point(N, A);
-    ed_rows_w_init<6, 4>(TA, N, g_C.d2);
+    ed_rows_w_init<ED_W, ED_K>(TP, N, g_C.d2);
   }
   out[6] = g_fe_nmul;
   out[7] = g_fe_nsq;
@@ -238,6 +240,7 @@ extern "C" int t_ed_count_w6(const uint32_t* aw, const uint32_t* sw, const uint8
   sc_recode_w<6>(eh, C::kPackedWords, h);
   sc_recode_w<6>(es, C::kPackedWords, sr);
   ge_p2 R;
+  ed_rows_w_init<6, 4>(TA, N, g_C.d2);
   g_fe_nmul = g_fe_nsq = 0;
   ed_double_scalar_w<6, 4>(R, eh, es, TA, TA);
   out[0] = g_fe_nmul;
@@ -338,10 +341,10 @@ extern "C" void t_m29_op(int curve, int n, int op, const uint32_t* a, const uint
 }
 
 // ---------------------------------------------------------------- Ed25519 rows + radix-2^10 B
-static EdBTabW<6, 4, 10>* g_TB10 = nullptr;
+static EdBTabW<ED_W, ED_K, ED_WB>* g_TB10 = nullptr;
 static void tb10_init() {
   if (g_TB10) return;
-  g_TB10 = new EdBTabW<6, 4, 10>;
+  g_TB10 = new EdBTabW<ED_W, ED_K, ED_WB>;
   ge_p3 B;
   fe x, y, two_inv, t;
   fe_sub(x, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
@@ -353,7 +356,7 @@ static void tb10_init() {
   fe_mul(B.Y, y, two_inv);
   fe_1(B.Z);
   fe_mul(B.T, B.X, B.Y);
-  for (int u = 0; u < EdBCfg<6, 4, 10>::kDigits; ++u) ed_btab_wb_row<6, 4, 10>(g_TB10->t[u], B, u, g_C.d2);
+  for (int u = 0; u < EdBCfg<ED_W, ED_K, ED_WB>::kDigits; ++u) ed_btab_wb_row<ED_W, ED_K, ED_WB>(g_TB10->t[u], B, u, g_C.d2);
 }
 static void host_pick(ge_niels& out, const ge_niels* row, int d) { ed_pick_w(out, row, d); }
 
@@ -361,16 +364,16 @@ extern "C" int t_ed_verify_wb(const uint32_t* aw, const uint32_t* sw, const uint
                               uint64_t* counts) {
   init();
   tb10_init();
-  typedef EdRowsCfg<6, 4> C;
-  typedef EdBCfg<6, 4, 10> CB;
-  static EdRowTabW<6, 4> TA;
+  typedef EdRowsCfg<ED_W, ED_K> C;
+  typedef EdBCfg<ED_W, ED_K, ED_WB> CB;
+  static EdRowTabW<ED_W, ED_K> TA;
   static EdKeyPrep kp;
   ed_key_prep(kp, aw, g_C);
   if (kp.status) return (int)kp.status;
   ge_p3 A, N;
   ed_decode_point(A, aw, g_C);
   ed_neg_point(N, A);
-  ed_rows_w_init<6, 4>(TA, N, g_C.d2);
+  ed_rows_w_init<ED_W, ED_K>(TA, N, g_C.d2);
   static uint8_t buf[1 << 20];
   memcpy(buf, msg, msg_len);
   uint32_t pre[16], hw[16], h[8];
@@ -389,13 +392,13 @@ extern "C" int t_ed_verify_wb(const uint32_t* aw, const uint32_t* sw, const uint
     sc_sub(sr, sr, r1);
   }
   uint32_t eh[C::kPackedWords], es[CB::kPackedWords];
-  sc_recode_w<6>(eh, C::kPackedWords, h);
-  sc_recode_w16<10>(es, CB::kPackedWords, sr);
+  sc_recode_w<ED_W>(eh, C::kPackedWords, h);
+  sc_recode_w16<ED_WB>(es, CB::kPackedWords, sr);
   ge_p2 R;
 #ifdef FE_OP_COUNT
   g_fe_nmul = g_fe_nsq = 0;
 #endif
-  ed_double_scalar_wb<6, 4, 10>(R, eh, es, TA, *g_TB10, host_pick, host_pick);
+  ed_double_scalar_wb<ED_W, ED_K, ED_WB>(R, eh, es, TA, *g_TB10, host_pick, host_pick);
 #ifdef FE_OP_COUNT
   if (counts) {
     counts[0] = g_fe_nmul;

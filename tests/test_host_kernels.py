@@ -105,6 +105,33 @@ def test_ed25519_lane_verify_on_fixtures():
     assert n > 200
 
 
+def test_abyte_without_square_root():
+    """k_ed_key_abyte's Abyte (no decode) equals the decoded point's re-encoding for every key
+    that decodes: fixtures, random y, y >= p, y = +-1 (x = 0) with either sign bit."""
+    import ctypes
+    lib = hostk.lib()
+    lib.t_ed_abyte_fast.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.t_ed_keyprep.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    cands = [bytes.fromhex(it["key"]) for it in golden_io.load("ed25519.json")
+             if it["key_fmt"] == 0 and len(bytes.fromhex(it["key"])) == 32]
+    rng = np.random.default_rng(5)
+    cands += [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(400)]
+    P = 2 ** 255 - 19
+    for y in (1, P - 1, P + 1, 2 ** 255 - 1, P, 0, 2 ** 255 - 20):
+        for sign in (0, 1):
+            cands.append(((y % 2 ** 255) | (sign << 255)).to_bytes(32, "little"))
+    n = 0
+    for key in cands:
+        ref = np.zeros(8, dtype=np.uint32)
+        got = np.zeros(8, dtype=np.uint32)
+        st = lib.t_ed_keyprep(ptr(words(key)), ptr(ref))
+        lib.t_ed_abyte_fast(ptr(words(key)), ptr(got))
+        if st == 0:
+            assert got.tobytes() == ref.tobytes(), key.hex()
+            n += 1
+    assert n > 300
+
+
 def test_sha_lane_code():
     import ctypes
     lib = hostk.lib()

@@ -2,8 +2,9 @@
 //
 // Messages are read straight out of the caller's arena with 4-byte loads
 // (unaligned offsets handled by a funnel shift), so nothing is staged per item.
-// SHA-512 runs on 64-bit words (two VGPRs each); on gfx950 a 64-bit rotate is two
-// v_alignbit_b32, a 64-bit add one v_add_co + one v_addc.
+// SHA-512 runs on 64-bit words (two VGPRs each); a 64-bit rotate is written as two
+// v_alignbit_b32 (the compiler otherwise emits two 64-bit shifts + two ORs), Ch and Maj as one
+// v_bfi_b32 per half, a 64-bit add is one v_lshl_add_u64.
 #pragma once
 #include "fe25519.h"
 
@@ -45,7 +46,24 @@ CG_HD uint32_t cg_msg_word_be(const uint8_t* arena, uint64_t len_rounded, uint64
 }
 
 // ----------------------------------------------------------------- SHA-512
-CG_HD uint64_t cg_rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+CG_HD uint64_t cg_rotr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // n is a compile-time constant at every call site
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t a = n < 32 ? hi : lo, b = n < 32 ? lo : hi;
+  const uint32_t r = (uint32_t)n & 31u;
+  return ((uint64_t)__builtin_amdgcn_alignbit(b, a, r) << 32) | __builtin_amdgcn_alignbit(a, b, r);
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
+
+// (e & f) ^ (~e & g) and Maj(a, b, c), each one bitfield select per 32-bit half
+CG_HD uint64_t cg_ch64(uint64_t e, uint64_t f, uint64_t g) { return (e & f) | (~e & g); }
+CG_HD uint64_t cg_maj64(uint64_t a, uint64_t b, uint64_t c) {
+  const uint64_t m = a ^ b;
+  return (m & c) | (~m & b);
+}
 
 CG_HD uint64_t cg_k512(int i) {
   const uint64_t K[80] = {
@@ -97,9 +115,9 @@ CG_HD void sha512_compress(uint64_t s[8], uint64_t w[16]) {
       wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
       w[i & 15] = wi;
     }
-    const uint64_t t1 = h + (cg_rotr64(e, 14) ^ cg_rotr64(e, 18) ^ cg_rotr64(e, 41)) + ((e & f) ^ (~e & g)) +
+    const uint64_t t1 = h + (cg_rotr64(e, 14) ^ cg_rotr64(e, 18) ^ cg_rotr64(e, 41)) + cg_ch64(e, f, g) +
                         cg_k512(i) + wi;
-    const uint64_t t2 = (cg_rotr64(a, 28) ^ cg_rotr64(a, 34) ^ cg_rotr64(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
+    const uint64_t t2 = (cg_rotr64(a, 28) ^ cg_rotr64(a, 34) ^ cg_rotr64(a, 39)) + cg_maj64(a, b, c);
     h = g;
     g = f;
     f = e;

@@ -1,0 +1,60 @@
+"""Per-launch HBM traffic of the Ed25519 item kernels from two rocprofv3 PMC passes
+(tools/profile_r01.sh: --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs), written to
+profiles/r01/pmc_traffic.json for bench.py's roofline.traffic.
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE tallies 128-B requests at 64 B,
+so a wide streaming read reports half its bytes; hbm = 2*FETCH_SIZE + WRITE_SIZE (KB * 1024).
+The doubling is calibrated for streaming reads, not 16-B table gathers, so the figure is an
+upper estimate.
+
+usage: pmc_traffic.py <prof_dir> <kernel_version> <items> <dest_profile_dir>
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+KERNELS = ("cg::k_ed_hash", "cg::k_ed_ladder", "cg::k_ed_finish")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_kernel_kb(path):
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].split("(")[0]
+        if name in KERNELS:
+            acc[name].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    prof, version, items, dest = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+    fetch = per_kernel_kb(os.path.join(prof, "fetch", "run_counter_collection.csv"))
+    write = per_kernel_kb(os.path.join(prof, "write", "run_counter_collection.csv"))
+    assert set(fetch) == set(KERNELS) and set(write) == set(KERNELS), (fetch, write)
+    hbm = int(round((2 * sum(fetch.values()) + sum(write.values())) * 1024))
+    os.makedirs(dest, exist_ok=True)
+    for src, dst in (("trace/run_kernel_stats.csv", "kernel_stats.csv"),
+                     ("fetch/run_counter_collection.csv", "pmc_fetch_size.csv"),
+                     ("write/run_counter_collection.csv", "pmc_write_size.csv"),
+                     ("valu/run_counter_collection.csv", "pmc_valu.csv")):
+        if os.path.exists(os.path.join(prof, src)):
+            shutil.copy(os.path.join(prof, src), os.path.join(dest, dst))
+    rel = os.path.relpath(dest, ROOT)
+    out = {"items": items, "kernel": " + ".join(k.split("::")[1] for k in KERNELS),
+           "source": f"{rel}/pmc_fetch_size.csv, pmc_write_size.csv (rocprofv3 --pmc FETCH_SIZE / "
+                     "WRITE_SIZE, separate passes, bench.py --steps 3)",
+           "fetch_size_kb": fetch, "write_size_kb": write,
+           "correction": "gfx950 FETCH_SIZE reads half the bytes of wide streaming reads "
+                         "(MI355X_MICROARCH.md HBM): hbm = 2*FETCH_SIZE + WRITE_SIZE (KB*1024); "
+                         "uncalibrated for 16-B table gathers, so an upper estimate",
+           "hbm_bytes_per_launch": hbm, "kernel_version": version}
+    with open(os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

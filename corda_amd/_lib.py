@@ -73,7 +73,9 @@ def lib():
                                                  vp, vp]
             L.cg_verify_transactions_device.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp, u64, vp, u32, vp, u64,
                                                         u32, vp, vp, vp, vp]
-            for name in ("cg_verify_transactions", "cg_verify_transactions_device", "cg_reserve", "cg_verify_batch", "cg_verify_batch_device", "cg_sha256_batch",
+            L.cg_verify_filtered.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u64, vp]
+            L.cg_verify_filtered_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u64, vp, vp]
+            for name in ("cg_verify_filtered", "cg_verify_filtered_device", "cg_verify_transactions", "cg_verify_transactions_device", "cg_reserve", "cg_verify_batch", "cg_verify_batch_device", "cg_sha256_batch",
                          "cg_sha512_batch", "cg_sha256_batch_device", "cg_merkle_roots", "cg_tx_ids",
                          "cg_tx_ids_device"):
                 getattr(L, name).restype = i32

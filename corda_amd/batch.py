@@ -18,6 +18,15 @@ TX_DTYPE = np.dtype([("first", "<u8"), ("n", "<u4"), ("reserved", "<u4"), ("salt
 TXSIG_DTYPE = np.dtype([("sig_off", "<u8"), ("tx_idx", "<u4"), ("key_idx", "<u4"), ("sig_len", "<u2"),
                         ("tmpl", "<u2"), ("reserved", "<u4")])
 TMPL_DTYPE = np.dtype([("prefix_off", "<u8"), ("suffix_off", "<u8"), ("prefix_len", "<u4"), ("suffix_len", "<u4")])
+# tear-offs (cg_pmt_node / cg_filtered_leaf / cg_filtered_tx)
+PMT_NODE_DTYPE = np.dtype([("hash_off", "<u8"), ("kind", "<u4"), ("reserved", "<u4")])
+FLEAF_DTYPE = np.dtype([("off", "<u8"), ("nonce_off", "<u8"), ("len", "<u4"), ("flags", "<u4")])
+FTX_DTYPE = np.dtype([("first_node", "<u8"), ("first_leaf", "<u8"), ("root_off", "<u8"), ("n_nodes", "<u4"),
+                      ("n_leaves", "<u4"), ("flags", "<u4"), ("reserved", "<u4")])
+assert PMT_NODE_DTYPE.itemsize == 16 and FLEAF_DTYPE.itemsize == 24 and FTX_DTYPE.itemsize == 40
+PMT_NODE, PMT_LEAF, PMT_INCLUDED = 0, 1, 2
+FLEAF_SALT, FLEAF_HASH = 1, 2
+FTX_FILTERED = 1
 assert TXSIG_DTYPE.itemsize == 24 and TMPL_DTYPE.itemsize == 24
 assert KEY_DTYPE.itemsize == 16 and ITEM_DTYPE.itemsize == 32 and SPAN_DTYPE.itemsize == 16
 assert COMPONENT_DTYPE.itemsize == 16 and TX_DTYPE.itemsize == 24

@@ -70,6 +70,8 @@ struct cg_ctx {
   DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
   // transaction pipeline: verify items, spliced messages, templates; host-entry staging
   DevBuf txitems, msgs, tmpls, h_txs, h_comps, h_sigs, h_ids, h_txst;
+  // tear-offs: leaf-hash workspace
+  DevBuf ftxws;
 };
 
 extern "C" {
@@ -140,7 +142,7 @@ void cg_close(cg_ctx* c) {
   c->aux0.release();
   c->aux1.release();
   c->aux2.release();
-  for (DevBuf* b : {&c->txitems, &c->msgs, &c->tmpls, &c->h_txs, &c->h_comps, &c->h_sigs, &c->h_ids, &c->h_txst})
+  for (DevBuf* b : {&c->txitems, &c->msgs, &c->tmpls, &c->h_txs, &c->h_comps, &c->h_sigs, &c->h_ids, &c->h_txst, &c->ftxws})
     b->release();
   for (int k = 0; k < 3; ++k) {
     if (c->fork.side[k]) {
@@ -501,6 +503,56 @@ int cg_verify_transactions(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_
     HIP_TRY(hipMemcpyAsync(tx_status_out, c->h_txst.p, n_tx, hipMemcpyDeviceToHost, s), "D2H tx status");
   }
   if (n_sigs) HIP_TRY(hipMemcpyAsync(sig_status_out, c->status.p, n_sigs, hipMemcpyDeviceToHost, s), "D2H sig status");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  return CG_OK;
+}
+
+int cg_verify_filtered_device(cg_ctx* c, const cg_filtered_tx* d_ftxs, uint64_t n_ftx, const cg_pmt_node* d_nodes,
+                              uint64_t n_nodes, const cg_filtered_leaf* d_leaves, uint64_t n_leaves,
+                              const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_status, void* hip_stream) {
+  if (!c) return fail(CG_ERR_ARG, "cg_verify_filtered_device: ctx is NULL");
+  if (n_ftx && (!d_ftxs || !d_status)) return fail(CG_ERR_ARG, "cg_verify_filtered_device: NULL buffer");
+  if (n_ftx == 0) return CG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  if (c->ftxws.cap < cg::ftx_ws_bytes(n_leaves)) {
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    HIP_TRY(c->ftxws.ensure(cg::ftx_ws_bytes(n_leaves)), "hipMalloc(filtered ws)");
+  }
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  HIP_TRY(cg::launch_filtered(d_ftxs, n_ftx, d_nodes, n_nodes, d_leaves, n_leaves, d_arena, arena_len, d_status,
+                              (uint8_t*)c->ftxws.p, s), "launch_filtered");
+  return CG_OK;
+}
+
+int cg_verify_filtered(cg_ctx* c, const cg_filtered_tx* ftxs, uint64_t n_ftx, const cg_pmt_node* nodes,
+                       uint64_t n_nodes, const cg_filtered_leaf* leaves, uint64_t n_leaves, const uint8_t* arena,
+                       uint64_t arena_len, uint8_t* status_out) {
+  if (!c) return fail(CG_ERR_ARG, "cg_verify_filtered: ctx is NULL");
+  if (n_ftx && (!ftxs || !status_out)) return fail(CG_ERR_ARG, "cg_verify_filtered: NULL buffer");
+  if ((n_nodes && !nodes) || (n_leaves && !leaves) || (arena_len && !arena))
+    return fail(CG_ERR_ARG, "cg_verify_filtered: NULL table");
+  if (n_ftx == 0) return CG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  hipStream_t s = c->stream;
+  HIP_TRY(c->h_txs.ensure(sizeof(cg_filtered_tx) * n_ftx), "hipMalloc(filtered txs)");
+  HIP_TRY(c->h_comps.ensure(sizeof(cg_pmt_node) * (n_nodes ? n_nodes : 1)), "hipMalloc(nodes)");
+  HIP_TRY(c->h_sigs.ensure(sizeof(cg_filtered_leaf) * (n_leaves ? n_leaves : 1)), "hipMalloc(leaves)");
+  HIP_TRY(c->arena.ensure(((arena_len + 3) & ~(uint64_t)3) + 16), "hipMalloc(arena)");
+  HIP_TRY(c->status.ensure(n_ftx), "hipMalloc(status)");
+  HIP_TRY(c->ftxws.ensure(cg::ftx_ws_bytes(n_leaves)), "hipMalloc(filtered ws)");
+  HIP_TRY(hipMemcpyAsync(c->h_txs.p, ftxs, sizeof(cg_filtered_tx) * n_ftx, hipMemcpyHostToDevice, s), "H2D ftxs");
+  if (n_nodes)
+    HIP_TRY(hipMemcpyAsync(c->h_comps.p, nodes, sizeof(cg_pmt_node) * n_nodes, hipMemcpyHostToDevice, s), "H2D nodes");
+  if (n_leaves)
+    HIP_TRY(hipMemcpyAsync(c->h_sigs.p, leaves, sizeof(cg_filtered_leaf) * n_leaves, hipMemcpyHostToDevice, s),
+            "H2D leaves");
+  if (arena_len) HIP_TRY(hipMemcpyAsync(c->arena.p, arena, arena_len, hipMemcpyHostToDevice, s), "H2D arena");
+  HIP_TRY(cg::launch_filtered((const cg_filtered_tx*)c->h_txs.p, n_ftx, (const cg_pmt_node*)c->h_comps.p, n_nodes,
+                              (const cg_filtered_leaf*)c->h_sigs.p, n_leaves, (const uint8_t*)c->arena.p, arena_len,
+                              (uint8_t*)c->status.p, (uint8_t*)c->ftxws.p, s), "launch_filtered");
+  HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n_ftx, hipMemcpyDeviceToHost, s), "D2H status");
   HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
   return CG_OK;
 }

@@ -74,4 +74,11 @@ hipError_t launch_merkle_roots(const uint8_t* d_leaves, const uint64_t* d_first,
                                uint64_t n, uint8_t* d_roots, uint8_t* d_status, uint8_t* d_ws,
                                const uint64_t* d_wsoff, hipStream_t stream);
 
+// Tear-offs (filtered.hip): leaf hashes, then one lane per filtered transaction. `d_ws` must
+// hold ftx_ws_bytes(n_leaves) bytes.
+size_t ftx_ws_bytes(uint64_t n_leaves);
+hipError_t launch_filtered(const cg_filtered_tx* d_ftxs, uint64_t n_ftx, const cg_pmt_node* d_nodes, uint64_t n_nodes,
+                           const cg_filtered_leaf* d_leaves, uint64_t n_leaves, const uint8_t* d_arena,
+                           uint64_t arena_len, uint8_t* d_status, uint8_t* d_ws, hipStream_t stream);
+
 }  // namespace cg

@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from .batch import COMPONENT_DTYPE, KEY_DTYPE, MODE_DOVERIFY, SPAN_DTYPE, TMPL_DTYPE, TX_DTYPE, TXSIG_DTYPE
+from .batch import COMPONENT_DTYPE, FLEAF_DTYPE, FTX_DTYPE, KEY_DTYPE, PMT_NODE_DTYPE, MODE_DOVERIFY, SPAN_DTYPE, TMPL_DTYPE, TX_DTYPE, TXSIG_DTYPE
 
 
 def _p(a):
@@ -129,6 +129,16 @@ class Engine:
         _lib.check(_lib.lib().cg_tx_ids(self._h, _p(txs), len(txs), _p(comps), len(comps), _p(arena), arena.size,
                                         _p(ids), _p(st)), "cg_tx_ids")
         return ids.reshape(-1, 32), st
+
+    def verify_filtered(self, ftxs, nodes, leaves, arena):
+        """FilteredTransaction.verify / PartialMerkleTree.verify for packed tear-offs
+        (FTX_DTYPE / PMT_NODE_DTYPE / FLEAF_DTYPE / arena, cg_verify_filtered). Returns the
+        per-transaction status bytes (0 true, 1 false, 2 MerkleTreeException, 3 malformed)."""
+        assert ftxs.dtype == FTX_DTYPE and nodes.dtype == PMT_NODE_DTYPE and leaves.dtype == FLEAF_DTYPE
+        st = np.full(len(ftxs), 255, dtype=np.uint8)
+        _lib.check(_lib.lib().cg_verify_filtered(self._h, _p(ftxs), len(ftxs), _p(nodes), len(nodes), _p(leaves),
+                                                 len(leaves), _p(arena), arena.size, _p(st)), "cg_verify_filtered")
+        return st
 
     # ------------------------------------------------------------------ transactions
     def verify_transactions(self, txs, comps, keys, sigs, tmpls, arena, mode=MODE_DOVERIFY):

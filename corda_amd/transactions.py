@@ -15,7 +15,9 @@ serialised with Kryo (Crypto.kt:499-502). ``check_signatures_are_valid_batch`` t
 the caller (``signable_data(tx_id, sig) -> bytes``). ``verify_wire_transactions`` is the
 whole-pipeline form: it takes WireTransaction components, computes every id on the GPU and
 splices the ids into per-metadata SignableData templates (corda_amd/signable.py) on the GPU
-too, so the host never serialises per signature.
+too, so the host never serialises per signature. ``verify_chain`` is
+ResolveTransactionsFlow's whole dependency chain as one such call (SURVEY §8(f2),
+ResolveTransactionsFlow.kt:36-96).
 """
 from dataclasses import dataclass, field
 
@@ -23,7 +25,7 @@ import numpy as np
 
 from . import batch as B
 from . import signable
-from .crypto import BatchItem, Crypto, PublicKey, SCHEME_CODE_NAMES
+from .crypto import BatchItem, Crypto, IllegalArgumentException, PublicKey, SCHEME_CODE_NAMES
 
 
 class SignaturesMissingException(Exception):
@@ -115,6 +117,7 @@ class SignedWireTransaction:
     wtx: WireTransactionData
     sigs: list                       # TransactionSignature
     required_signing_keys: set = field(default_factory=set)
+    inputs: list = field(default_factory=list)   # StateRef.txhash of each input (32-byte ids)
 
 
 def pack_signed_transactions(stxs):
@@ -178,3 +181,83 @@ def verify_wire_transactions(stxs, crypto=Crypto):
         results.append(res)
         pos += len(stx.sigs)
     return out_ids, results
+
+
+# ---------------------------------------------------------------------------------------------
+# Whole-chain resolution: ResolveTransactionsFlow verifies every downloaded
+# dependency in topological order, one SignedTransaction.verify at a time, and each verify
+# checks the signatures twice (checkSignaturesAreValid, then verifyRequiredSignatures ->
+# verifySignaturesExcept -> checkSignaturesAreValid again; SignedTransaction.kt:143-149,
+# TransactionWithSignatures.kt:41-47). Here the whole chain -- every id and every signature --
+# is one GPU call, each signature is verified once, and the ordered walk afterwards throws
+# exactly what the serial loop would have thrown first.
+
+class ExcessivelyLargeTransactionGraph(Exception):
+    """ResolveTransactionsFlow.ExcessivelyLargeTransactionGraph (ResolveTransactionsFlow.kt:66)."""
+
+
+def topological_sort(stxs, ids):
+    """ResolveTransactionsFlow.topologicalSort (ResolveTransactionsFlow.kt:36-62) over
+    transaction indices: dependencies before dependers, deterministic for a given list order
+    (the forward graph keeps insertion order like the LinkedHashSet it restates). Iterative
+    DFS, so chains deeper than Python's recursion limit sort too."""
+    forward = {}
+    for t, stx in enumerate(stxs):
+        for h in stx.inputs:
+            dep = forward.setdefault(bytes(h), {})
+            dep.setdefault(t, None)
+    visited, result = set(), []
+    for root in range(len(stxs)):
+        if ids[root] in visited:
+            continue
+        visited.add(ids[root])
+        stack = [(root, iter(forward.get(ids[root], ())))]
+        while stack:
+            t, it = stack[-1]
+            nxt = None
+            for d in it:
+                if ids[d] not in visited:
+                    nxt = d
+                    break
+            if nxt is None:
+                stack.pop()
+                result.append(t)
+            else:
+                visited.add(ids[nxt])
+                stack.append((nxt, iter(forward.get(ids[nxt], ()))))
+    result.reverse()
+    if len(result) != len(stxs):
+        raise IllegalArgumentException("Failed requirement.")
+    return result
+
+
+def verify_chain(stxs, crypto=Crypto, check_sufficient_signatures=True, on_verified=None, limit=5000):
+    """The signature half of ResolveTransactionsFlow.call's loop (ResolveTransactionsFlow.kt:88-96)
+    for a downloaded set of SignedWireTransactions. Returns the transactions' indices in
+    topological order, all verified. On the first transaction (in that order) whose check fails,
+    raises what its SignedTransaction.verify would have raised first: MerkleTreeException (no
+    id), the first failing signature's exception (SignatureException / InvalidKeyException /
+    IllegalArgumentException, TransactionWithSignatures.kt:58-61) or SignaturesMissingException
+    (:41-47). ``on_verified(index, id)`` runs for each transaction before the next is checked --
+    where the flow records it and runs contract verification (out of scope here)."""
+    if len(stxs) > limit:
+        raise ExcessivelyLargeTransactionGraph()
+    ids, results = verify_wire_transactions(stxs, crypto)
+    if any(i is None for i in ids):
+        # an id-less transaction cannot be placed in the graph: the serial flow fails on it when
+        # it deserialises / hashes it, before any verification
+        t = next(k for k, i in enumerate(ids) if i is None)
+        raise results[t][1]
+    order = topological_sort(stxs, ids)
+    for t in order:
+        stx = stxs[t]
+        if results[t] is not None:
+            raise results[t][1]
+        if check_sufficient_signatures:
+            have = {s.by for s in stx.sigs}
+            missing = {k for k in stx.required_signing_keys if k not in have}
+            if missing:
+                raise SignaturesMissingException(missing, ids[t])
+        if on_verified is not None:
+            on_verified(t, ids[t])
+    return order

@@ -234,6 +234,59 @@ int cg_verify_transactions(cg_ctx* ctx, const cg_tx* txs, uint64_t n_tx, const c
                            uint64_t arena_len, uint32_t mode, uint8_t* ids_out, uint8_t* tx_status_out,
                            uint8_t* sig_status_out);
 
+/* ---- Tear-offs: FilteredTransaction.verify / PartialMerkleTree.verify.
+ * Replaces, for a batch of filtered transactions (the non-validating notary's input,
+ * NonValidatingNotaryFlow.kt:22-27), the serial
+ *   hashes = filteredLeaves.availableComponentHashes   serializedHash(x, nonce) = SHA256(kryo(x) || nonce)
+ *                                                       (MerkleTransaction.kt:23-28,137)
+ *   if (hashes.isEmpty()) throw MerkleTreeException      (MerkleTransaction.kt:173-178)
+ *   partialMerkleTree.verify(rootHash, hashes)          (PartialMerkleTree.kt:130-156)
+ * PartialMerkleTree.verify alone is the same call with precomputed leaf hashes
+ * (CG_FLEAF_HASH) and without the empty check (no CG_FTX_FILTERED flag).
+ *
+ * The PartialTree is passed flattened in post-order (children before their parent):
+ * CG_PMT_LEAF / CG_PMT_INCLUDED push the 32-byte hash at arena[hash_off] (INCLUDED also records
+ * it as a used hash); CG_PMT_NODE pops right then left and pushes hashConcat(left, right). */
+enum { CG_PMT_NODE = 0, CG_PMT_LEAF = 1, CG_PMT_INCLUDED = 2 };
+typedef struct cg_pmt_node {
+  uint64_t hash_off;   /* LEAF / INCLUDED: 32-byte SecureHash at arena[hash_off]; NODE: ignored */
+  uint32_t kind;       /* CG_PMT_* */
+  uint32_t reserved;   /* must be 0 */
+} cg_pmt_node;         /* 16 bytes */
+
+enum { CG_FLEAF_SALT = 1u, /* PrivacySalt component: SHA256(blob), no nonce (MerkleTransaction.kt:23-28) */
+       CG_FLEAF_HASH = 2u  /* the 32 bytes at off are the leaf hash itself (len must be 32) */ };
+typedef struct cg_filtered_leaf {
+  uint64_t off;        /* serialised component bytes at arena[off .. off+len) */
+  uint64_t nonce_off;  /* its 32-byte nonce (FilteredLeaves.nonces[i]) at arena[nonce_off] */
+  uint32_t len;
+  uint32_t flags;      /* CG_FLEAF_* */
+} cg_filtered_leaf;    /* 24 bytes */
+
+enum { CG_FTX_FILTERED = 1u /* FilteredTransaction.verify: no leaves => status 2 */ };
+typedef struct cg_filtered_tx {
+  uint64_t first_node; /* partial tree nodes[first_node .. +n_nodes), post-order */
+  uint64_t first_leaf; /* hashesToCheck: leaves[first_leaf .. +n_leaves), availableComponents order */
+  uint64_t root_off;   /* rootHash (32 bytes) at arena[root_off] */
+  uint32_t n_nodes;
+  uint32_t n_leaves;
+  uint32_t flags;      /* CG_FTX_* */
+  uint32_t reserved;   /* must be 0 */
+} cg_filtered_tx;      /* 40 bytes */
+
+/* status_out per transaction: 0 verify() == true; 1 verify() == false (root differs, or the
+ * used-hash multiset differs from the leaf hashes); 2 MerkleTreeException("Transaction without
+ * included leaves."); 3 malformed input the JVM object cannot express: a node / leaf range or
+ * hash outside the tables / arena, an unknown node kind, a post-order stream that does not
+ * reduce to one root, or a stack deeper than CG_PMT_MAX_DEPTH. */
+#define CG_PMT_MAX_DEPTH 64
+int cg_verify_filtered(cg_ctx* ctx, const cg_filtered_tx* ftxs, uint64_t n_ftx, const cg_pmt_node* nodes,
+                       uint64_t n_nodes, const cg_filtered_leaf* leaves, uint64_t n_leaves, const uint8_t* arena,
+                       uint64_t arena_len, uint8_t* status_out);
+int cg_verify_filtered_device(cg_ctx* ctx, const cg_filtered_tx* d_ftxs, uint64_t n_ftx, const cg_pmt_node* d_nodes,
+                              uint64_t n_nodes, const cg_filtered_leaf* d_leaves, uint64_t n_leaves,
+                              const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_status, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

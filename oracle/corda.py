@@ -149,3 +149,147 @@ def check_signatures_are_valid(tx_id_bytes, sigs, message_of):
         if st != VALID:
             return i, st
     return None, VALID
+
+
+# ---------------- tear-offs: PartialMerkleTree / FilteredTransaction ----------------
+# A MerkleTree / PartialTree is a nested tuple: ("L", hash) leaf, ("I", hash) included leaf
+# (partial trees only), ("N", hash_or_None, left, right) node (full trees carry the node hash).
+
+def merkle_tree(leaves):
+    """MerkleTree.getMerkleTree (MerkleTree.kt:27-66) keeping the whole tree: zero-hash padding
+    to 2^k, then pairwise levels of Node(hashConcat(l, r), l, r)."""
+    if len(leaves) == 0:
+        raise MerkleTreeException("Cannot calculate Merkle root on empty hash list.")
+    lv = [("L", bytes(x)) for x in leaves]
+    while len(lv) & (len(lv) - 1):
+        lv.append(("L", ZERO_HASH))
+    while len(lv) > 1:
+        lv = [("N", hash_concat(_thash(lv[i]), _thash(lv[i + 1])), lv[i], lv[i + 1]) for i in range(0, len(lv), 2)]
+    return lv[0]
+
+
+def _thash(t):
+    return t[1]
+
+
+def partial_tree_build(tree, include_hashes):
+    """PartialMerkleTree.build (PartialMerkleTree.kt:66-123): zero hash not includable
+    (IllegalArgumentException -> ValueError), full-tree check, every leaf whose hash is in
+    include_hashes becomes an IncludedLeaf, subtrees without one are cut to a Leaf of their hash,
+    and the used count must equal len(include_hashes)."""
+    include = [bytes(h) for h in include_hashes]
+    if ZERO_HASH in include:
+        raise ValueError("Zero hashes shouldn't be included in partial tree.")
+
+    def check_full(t, level=0):
+        if t[0] == "L":
+            return level
+        a, b = check_full(t[2], level + 1), check_full(t[3], level + 1)
+        if a != b:
+            raise MerkleTreeException("Got not full binary tree.")
+        return a
+
+    check_full(tree)
+    used = []
+
+    def build(t):
+        if t[0] == "L":
+            if t[1] in include:
+                used.append(t[1])
+                return True, ("I", t[1])
+            return False, ("L", t[1])
+        lf, lt = build(t[2])
+        rf, rt = build(t[3])
+        if lf or rf:
+            return True, ("N", None, lt, rt)
+        return False, ("L", t[1])
+
+    pt = build(tree)[1]
+    if len(include) != len(used):
+        raise MerkleTreeException("Some of the provided hashes are not in the tree.")
+    return pt
+
+
+def partial_tree_verify(ptree, root_hash, hashes_to_check):
+    """PartialMerkleTree.verify (PartialMerkleTree.kt:130-156): recursive root, used hashes in
+    tree order; groupBy equality (multiset) first, then the root."""
+    used = []
+
+    def root(t):
+        if t[0] == "I":
+            used.append(t[1])
+            return t[1]
+        if t[0] == "L":
+            return t[1]
+        return hash_concat(root(t[2]), root(t[3]))
+
+    r = root(ptree)
+    a, b = sorted(bytes(h) for h in hashes_to_check), sorted(used)
+    if a != b:
+        return False
+    return r == bytes(root_hash)
+
+
+def filtered_leaf_hash(blob, nonce):
+    """serializedHash(x, nonce) (MerkleTransaction.kt:23-28): SHA256(kryo(x) || nonce)."""
+    return sha256(bytes(blob) + bytes(nonce))
+
+
+def filtered_tx_verify(root_hash, blobs, nonces, ptree):
+    """FilteredTransaction.verify (MerkleTransaction.kt:173-178) with FilteredLeaves'
+    availableComponentHashes (:137). Raises MerkleTreeException on no leaves."""
+    if len(blobs) != len(nonces):
+        raise ValueError("Each visible component should be accompanied by a nonce.")
+    hashes = [filtered_leaf_hash(b, n) for b, n in zip(blobs, nonces)]
+    if not hashes:
+        raise MerkleTreeException("Transaction without included leaves.")
+    return partial_tree_verify(ptree, root_hash, hashes)
+
+
+def partial_tree_postorder(ptree):
+    """The post-order stream of cg_pmt_node kinds (include/cordagpu.h): [(kind, hash|None)],
+    kind 0 node / 1 leaf / 2 included leaf."""
+    out = []
+
+    def walk(t):
+        if t[0] == "N":
+            walk(t[2])
+            walk(t[3])
+            out.append((0, None))
+        else:
+            out.append((2 if t[0] == "I" else 1, t[1]))
+
+    walk(ptree)
+    return out
+
+
+def partial_tree_from_postorder(stream):
+    """Inverse of partial_tree_postorder: rebuilds the nested PartialTree (raises ValueError on a
+    stream that does not reduce to one tree)."""
+    stk = []
+    for kind, h in stream:
+        if kind == 0:
+            if len(stk) < 2:
+                raise ValueError("node without two children")
+            r, l_ = stk.pop(), stk.pop()
+            stk.append(("N", None, l_, r))
+        elif kind in (1, 2):
+            stk.append(("I" if kind == 2 else "L", bytes(h)))
+        else:
+            raise ValueError("unknown node kind")
+    if len(stk) != 1:
+        raise ValueError("stream does not reduce to one root")
+    return stk[0]
+
+
+def filtered_status(root_hash, leaves, ptree, filtered=True):
+    """Status byte of include/cordagpu.h cg_verify_filtered for one tear-off. ``leaves``:
+    [(blob, nonce)] (FilteredTransaction) or [hash] with filtered=False (PartialMerkleTree.verify)."""
+    if filtered:
+        try:
+            ok = filtered_tx_verify(root_hash, [b for b, _ in leaves], [n for _, n in leaves], ptree)
+        except MerkleTreeException:
+            return 2
+    else:
+        ok = partial_tree_verify(ptree, root_hash, leaves)
+    return 0 if ok else 1

@@ -1,0 +1,111 @@
+"""Verifier batch-signature messages (VerifierApi.kt:10-58, Verifier.kt:69-84).
+
+CPU: the request / response wire format round-trips the C ABI tables, malformed bodies are
+rejected, and workers sharing one request queue answer every request once (host logic, with a
+stand-in engine that records what it was asked). GPU: a worker answers golden-fixture requests
+through cg_verify_batch with the fixtures' expected verdicts.
+"""
+import queue
+import threading
+
+import numpy as np
+import pytest
+
+import golden_io
+from corda_amd import batch as B
+from corda_amd import verifier as V
+
+
+def _batch(n=40, name="ed25519.json"):
+    items = golden_io.load(name)[:n]
+    b, exp, exp_iv = golden_io.sig_batch(items)
+    return b, exp, exp_iv
+
+
+def test_request_round_trip():
+    b, _, _ = _batch()
+    req = V.BatchSignatureRequest.from_batch(1234567890123, b, B.MODE_ISVALID)
+    got = V.BatchSignatureRequest.from_bytes(req.to_bytes())
+    assert got.verification_id == 1234567890123 and got.mode == B.MODE_ISVALID
+    assert got.keys.tobytes() == b.keys.tobytes()
+    assert got.items.tobytes() == b.items.tobytes()
+    assert got.arena.tobytes() == b.arena.tobytes()
+
+
+def test_response_round_trip():
+    st = np.array([0, 1, 2, 3, 4, 5, 255], dtype=np.uint8)
+    r = V.BatchSignatureResponse.from_bytes(V.BatchSignatureResponse(-7, st).to_bytes())
+    assert r.verification_id == -7 and r.status.tolist() == st.tolist() and r.error is None
+    r = V.BatchSignatureResponse.from_bytes(V.BatchSignatureResponse(9, np.zeros(0, np.uint8), "boom").to_bytes())
+    assert r.error == "boom" and r.status.size == 0
+
+
+def test_malformed_requests():
+    b, _, _ = _batch(4)
+    body = V.BatchSignatureRequest.from_batch(5, b).to_bytes()
+    for bad in (body[:10], b"XXXX" + body[4:], body[:-1], body + b"\x00"):
+        with pytest.raises(V.MalformedMessage):
+            V.BatchSignatureRequest.from_bytes(bad)
+    bad_mode = bytearray(body)
+    bad_mode[6] = 9
+    with pytest.raises(V.MalformedMessage):
+        V.BatchSignatureRequest.from_bytes(bytes(bad_mode))
+
+
+class _RecordingEngine:
+    """Stand-in for corda_amd.engine.Engine in host-logic tests: answers NOT_RUN-free statuses
+    derived from the item index, and fails on request."""
+
+    def __init__(self, name):
+        self.name, self.calls = name, 0
+
+    def verify(self, batch, mode):
+        self.calls += 1
+        if batch.n == 3:
+            raise RuntimeError("device lost")
+        return (np.arange(batch.n) % 2).astype(np.uint8)
+
+
+def test_worker_error_paths():
+    w = V.VerifierWorker(_RecordingEngine("a"))
+    r = V.BatchSignatureResponse.from_bytes(w.handle(b"garbage-garbage-garbage"))
+    assert r.error.startswith("MalformedMessage") and r.status.size == 0
+    b, _, _ = _batch(3)
+    r = V.BatchSignatureResponse.from_bytes(w.handle(V.BatchSignatureRequest.from_batch(11, b).to_bytes()))
+    assert r.verification_id == 11 and r.error == "RuntimeError: device lost" and r.status.size == 0
+
+
+def test_workers_share_one_queue():
+    reqs, rsps = queue.Queue(), queue.Queue()
+    engines = [_RecordingEngine("gpu0"), _RecordingEngine("gpu1")]
+    threads = [threading.Thread(target=V.VerifierWorker(e).serve, args=(reqs, rsps)) for e in engines]
+    for t in threads:
+        t.start()
+    b, _, _ = _batch(10)
+    for vid in range(50):
+        reqs.put((f"{V.VERIFICATION_RESPONSES_QUEUE_NAME_PREFIX}.node{vid % 3}",
+                  V.BatchSignatureRequest.from_batch(vid, b).to_bytes()))
+    for _ in threads:
+        reqs.put(None)
+    for t in threads:
+        t.join(30)
+    got = {}
+    while not rsps.empty():
+        reply_to, body = rsps.get()
+        r = V.BatchSignatureResponse.from_bytes(body)
+        assert reply_to.endswith(f"node{r.verification_id % 3}")
+        got[r.verification_id] = r.status
+    assert sorted(got) == list(range(50))
+    assert sum(e.calls for e in engines) == 50
+    assert all(np.array_equal(s, np.arange(10) % 2) for s in got.values())
+
+
+@pytest.mark.gpu
+def test_worker_gpu_golden(engine):
+    w = V.VerifierWorker(engine)
+    for name in ("ed25519.json", "ecdsa.json"):
+        b, exp, exp_iv = _batch(10 ** 6, name)
+        for mode, want in ((B.MODE_DOVERIFY, exp), (B.MODE_ISVALID, exp_iv)):
+            r = V.BatchSignatureResponse.from_bytes(w.handle(V.BatchSignatureRequest.from_batch(3, b, mode).to_bytes()))
+            assert r.error is None and r.verification_id == 3
+            assert np.array_equal(r.status, want)

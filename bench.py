@@ -70,6 +70,8 @@ def parse():
                     help="items of the secondary ECDSA measurement (N = 1 only; 0 disables)")
     ap.add_argument("--pipeline-txs", type=int, default=1 << 18,
                     help="WireTransactions of the secondary config-4 pipeline measurement (N = 1 only; 0 disables)")
+    ap.add_argument("--tear-offs", type=int, default=1 << 18, help="FilteredTransaction.verify secondary (0: off)")
+    ap.add_argument("--host-buffers", type=int, default=1, help="PCIe-inclusive cg_verify_batch secondary (0: off)")
     ap.add_argument("--mixed-items", type=int, default=1 << 20,
                     help="items of the secondary config-5-shaped mixed batch (N = 1 only; 0 disables)")
     return ap.parse_args()
@@ -207,6 +209,65 @@ def bench_pipeline(a, wl, eng, dev, stream, threads):
             "note": "BASELINE configs[3] is 1M txs; default 2^18 keeps host-side signing within the bench budget"}
 
 
+def bench_tear_offs(a, wl, eng, dev, stream):
+    """the non-validating notary's FilteredTransaction.verify for a batch of
+    tear-offs (inputs + notary visible out of ~11 components), one cg_verify_filtered_device call
+    per step. 4096 unique tear-offs are tiled to --tear-offs rows (no deduplication in the
+    engine). Work: SHA-256 compressions (visible leaves + 2 per partial-tree node)."""
+    import torch
+    from corda_amd import merkle as M
+    from corda_amd.batch import PMT_NODE
+    pool, expect = wl.filtered_pool(4096, seed=a.seed + 307)
+    t, n, lv, arena = M.pack_filtered(pool)
+    reps = max(1, a.tear_offs // len(t))
+    tt = np.tile(t, reps)
+    up = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).to(dev)  # noqa: E731
+    td, nd, ld, ad = up(tt), up(n), up(lv), up(arena)
+    sd = torch.full((len(tt),), 255, dtype=torch.uint8, device=dev)
+    sptr = stream.cuda_stream
+
+    def once():
+        eng.verify_filtered_device(td.data_ptr(), len(tt), nd.data_ptr(), len(n), ld.data_ptr(), len(lv),
+                                   ad.data_ptr(), int(arena.size), sd.data_ptr(), sptr)
+
+    once()
+    torch.cuda.synchronize(dev)
+    steps = max(2, a.steps // 2)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        once()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / steps
+    km = e0.elapsed_time(e1) / steps
+    st = sd.cpu().numpy()
+    comp_leaf = int(((lv["len"].astype(np.int64) + 32 + 9 + 63) // 64).sum())
+    comp_node = 2 * int(np.count_nonzero(n["kind"] == PMT_NODE))
+    comp_per = (comp_leaf + comp_node) / len(t)
+    return {"value": round(len(tt) / el, 1), "unit": "tear-offs/s", "tear_offs": len(tt), "unique": len(t),
+            "ms_per_step": round(el * 1e3, 3), "kernel_ms": round(km, 3),
+            "sha256_compressions_per_tear_off": round(comp_per, 2),
+            "sha256_compressions_per_s": round(len(tt) * comp_per / (km * 1e-3), 1),
+            "parity_vs_generator": bool(np.array_equal(st, np.tile(expect, reps)))}
+
+
+def bench_host_buffers(eng, batch, steps=3):
+    """The PCIe-inclusive rate: cg_verify_batch from pageable host buffers (H2D of keys, items
+    and arena, key prep, verify, D2H of the status bytes) on the headline batch."""
+    eng.verify(batch)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.verify(batch)
+    el = (time.perf_counter() - t0) / steps
+    st = eng.last_stats
+    return {"value": round(batch.n / el, 1), "unit": "sigs/s", "items": batch.n,
+            "bytes_h2d": int(batch.arena.size + batch.items.nbytes + batch.keys.nbytes),
+            "ms_per_call": round(el * 1e3, 3), "cg_stats_ms": {k: round(v, 3) for k, v in st.items()
+                                                               if k.startswith("ms_")}}
+
+
 def main():
     a = parse()
     import torch
@@ -250,14 +311,16 @@ def main():
 
         def step(timed, prepare=True):
             if prepare:
-                eng.prepare_keys_device(keys_t.data_ptr(), n_keys_, arena_t.data_ptr(), arena_len_, sptr)
-            if timed:
+                # one-shot cg_verify_batch_device: key prep sized by each key's use count, then items
+                eng.verify_device(keys_t.data_ptr(), n_keys_, items_t.data_ptr(), n_items_, arena_t.data_ptr(),
+                                  arena_len_, status_t.data_ptr(), 0, sptr)
+            else:
+                # item kernels alone against the tables the last one-shot step built
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-            eng.verify_items_device(keys_t.data_ptr(), n_keys_, items_t.data_ptr(), n_items_, arena_t.data_ptr(),
-                                    arena_len_, status_t.data_ptr(), 0, sptr)
-            if timed:
+                eng.verify_items_device(keys_t.data_ptr(), n_keys_, items_t.data_ptr(), n_items_,
+                                        arena_t.data_ptr(), arena_len_, status_t.data_ptr(), 0, sptr)
                 e1.record(stream)
                 ev.append((e0, e1))
             if gather and prepare:
@@ -319,6 +382,10 @@ def main():
         extra["notary_mixed"] = bench_mixed(a, wl, eng, dev, stream, run, threads)
     if world == 1 and a.pipeline_txs > 0:
         extra["tx_pipeline"] = bench_pipeline(a, wl, eng, dev, stream, threads)
+    if world == 1 and a.tear_offs > 0:
+        extra["tear_offs"] = bench_tear_offs(a, wl, eng, dev, stream)
+    if world == 1 and a.host_buffers:
+        extra["host_buffers"] = bench_host_buffers(eng, batch)
 
     st = status_d.cpu().numpy()
     counts = {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}

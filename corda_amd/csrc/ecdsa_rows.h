@@ -416,6 +416,49 @@ CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w&
   return ecdsa_x_check<C>(R, r, K);
 }
 
+// The same check for a key that has only row 0 of its table (few items in the batch,
+// keyws.h): Horner over u2's 43 signed radix-64 digits (252 doublings); G row u is added at
+// digit position ec_g_window(u) < EC_WINDOWS, which is followed by exactly the EC_W * window
+// doublings its row scale expects (as in ecdsa_ladder_check).
+template <int C, class TabG>
+CG_HD uint32_t ecdsa_ladder_check_row0(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG,
+                                       const EcAff* row0, const EcConsts& K) {
+  uint32_t dg[EC_G_PACKED], dq[EC_PACKED];
+  ec_recode_w10(dg, u1);
+  ec_recode_w6(dq, u2);
+  Jac R;
+  jac_set_inf<C>(R, K);
+#pragma unroll 1
+  for (int t = EC_DIGITS - 1; t >= 0; --t) {
+    if (t != EC_DIGITS - 1) {
+#pragma unroll 1
+      for (int d = 0; d < EC_W; ++d) jac_dbl<C>(R, R);
+    }
+    const int b = ec_digit6(dq, t);
+    if (b != 0) {
+      f29 x, y;
+      ec_pick(x, y, row0, b < 0 ? -b : b);
+      if (b < 0) m29_neg<C, 0>(y, y);
+      jac_madd<C>(R, R, x, y, K);
+    }
+    if (t < EC_WINDOWS) {
+      const int u_lo = (t * EC_G_DIGITS + EC_WINDOWS - 1) / EC_WINDOWS;
+      const int u_hi = ((t + 1) * EC_G_DIGITS + EC_WINDOWS - 1) / EC_WINDOWS;
+#pragma unroll 1
+      for (int u = u_lo; u < u_hi; ++u) {
+        const int a = ec_digit10(dg, u);
+        if (a != 0) {
+          f29 x, y;
+          ec_pick(x, y, TG.t[u], a < 0 ? -a : a);
+          if (a < 0) m29_neg<C, 0>(y, y);
+          jac_madd<C>(R, R, x, y, K);
+        }
+      }
+    }
+  }
+  return ecdsa_x_check<C>(R, r, K);
+}
+
 // G rows (per context) from the curve constants.
 template <int C>
 CG_HD void ec_g_rows_init(EcRowTab& T, EcRowScratch& s, const EcConsts& K) {

@@ -294,6 +294,50 @@ CG_HD void ed_double_scalar_wb(ge_p2& out, const uint32_t* eh, const uint32_t* e
   out = q;
 }
 
+// R' = h (-A) + S' B for a key that has only row 0 of its table (a key with few items in the
+// batch, keyws.h): Horner over h's signed radix-2^W digits, W doublings between digits (252 in
+// all), each B row added at the digit position whose remaining doublings its row scale
+// expects (digit position i_u = EdBCfg::window(u) < K is followed by W i_u doublings, as in
+// ed_double_scalar_wb). Same digits, same B table, same result.
+template <int W, int K, int WB, class TabB, class PickA, class PickB>
+CG_HD void ed_double_scalar_row0(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const ge_niels* row0,
+                                 const TabB& TB, PickA pick_a, PickB pick_b) {
+  typedef EdRowsCfg<W, K> C;
+  typedef EdBCfg<W, K, WB> CB;
+  ge_p3 R;
+  ge_p3_0(R);
+  ge_p1p1 t;
+  ge_p2 q;
+  for (int td = C::kDigits - 1; td >= 0; --td) {
+    if (td != C::kDigits - 1) {
+      for (int d = 0; d < W - 1; ++d) {
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+      }
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(R, t);
+    }
+    const int u_lo = td < K ? (td * CB::kDigits + K - 1) / K : 0;
+    const int u_hi = td < K ? ((td + 1) * CB::kDigits + K - 1) / K : 0;
+    const int n_ops = 1 + (u_hi - u_lo);
+    for (int k = 0; k < n_ops; ++k) {
+      ge_niels n;
+      if (k == 0) {
+        pick_a(n, row0, sc_digit_b(eh, td));
+      } else {
+        pick_b(n, TB.t[u_lo + k - 1], sc_digit_h(esb, u_lo + k - 1));
+      }
+      ge_madd(t, R, n);
+      if (k + 1 == n_ops) {
+        ge_p1p1_to_p2(q, t);
+      } else {
+        ge_p1p1_to_p3(R, t);
+      }
+    }
+  }
+  out = q;
+}
+
 // Table rows: row u holds the affine multiples 1..kMult of 2^shift(u) B.
 template <int W, int K, int WB>
 CG_HD void ed_btab_wb_row(ge_niels* row, const ge_p3& B, int u, const fe& d2) {

@@ -40,8 +40,11 @@ size_t btab_bytes();
 hipError_t init_btab(void* d_btab, hipStream_t stream);
 // Bytes of per-item workspace (projective Ed25519 results awaiting the batched inversion).
 size_t item_ws_bytes(uint64_t n_items);
+// With `d_items`, each key's table is sized by the number of items that use it (keyws.h);
+// without (cg_prepare_keys_device), every key gets full tables.
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                          void* d_keyprep, hipStream_t stream, const Fork* fork = nullptr);
+                          void* d_keyprep, hipStream_t stream, const Fork* fork = nullptr,
+                          const cg_item* d_items = nullptr, uint64_t n_items = 0);
 // `d_msgs` (optional): the engine's spliced-message workspace, read by items flagged
 // CG_ITEM_MSG_WS (keyws.h); caller items never carry that flag.
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,

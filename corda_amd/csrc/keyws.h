@@ -87,7 +87,26 @@ struct KeyWs {
   TabSlot* tab;
   BaseSlot* bases;
   EcRowScratch* ecs;
+  uint32_t* uses;  // items per key in this batch, saturating at >= ED_DIRECT_MAX_USES
+                   // (KEY_USES_ALL: unknown -> full tables)
+  uint32_t* full;  // per scheme class c (PLAN_ED / PLAN_R1 / PLAN_K1): the keys that get full
+                   // tables, full[c * n_keys + l] for l < full_count[c] (any order), so the
+                   // chain / row kernels run dense lanes however few keys are hot
+  uint32_t* full_count;
 };
+
+// How much table a key gets, from the number of items that use it in the batch (one-shot entry
+// points count them; cg_prepare_keys_device cannot, and builds every key in full):
+//   0 uses                        decode only (Abyte, status), no rows
+//   1 .. ED_DIRECT_MAX_USES - 1   row 0 only (the 32 affine multiples of -A): the item runs the
+//                                 252-doubling Horner ladder (ed_double_scalar_row0)
+//   more                          all 22 rows: 6 doublings per item (ed_double_scalar_wb)
+// Break-even (measured on MI355X, 2^20 Ed25519 items): a key's full tables cost ~230 ns of
+// GPU time, the row-0 ladder ~7 ns more per item than the full-table one -> ~32 items.
+#define KEY_USES_ALL 0xffffffffu
+#ifndef ED_DIRECT_MAX_USES
+#define ED_DIRECT_MAX_USES 32u
+#endif
 static inline KeyWs key_ws(void* base, uint32_t n_keys) {
   const size_t n = n_keys ? n_keys : 1;
   uint8_t* p = (uint8_t*)base;
@@ -99,12 +118,18 @@ static inline KeyWs key_ws(void* base, uint32_t n_keys) {
   w.bases = (BaseSlot*)p;
   p += al256(n * KEY_BASES * sizeof(BaseSlot));
   w.ecs = (EcRowScratch*)p;
+  p += n * EC_ROWS * sizeof(EcRowScratch);
+  w.uses = (uint32_t*)p;
+  p += al256(n * sizeof(uint32_t));
+  w.full = (uint32_t*)p;
+  p += al256(3 * n * sizeof(uint32_t));
+  w.full_count = (uint32_t*)p;
   return w;
 }
 static inline size_t key_ws_bytes(uint32_t n_keys) {
   const size_t n = n_keys ? n_keys : 1;
   return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(TabSlot)) + al256(n * KEY_BASES * sizeof(BaseSlot)) +
-         n * EC_ROWS * sizeof(EcRowScratch);
+         n * EC_ROWS * sizeof(EcRowScratch) + al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256;
 }
 
 // Per-item workspace slot (indexed by plan position, so the schemes never share one):
@@ -147,7 +172,7 @@ static inline size_t item_ws_total(uint64_t n_items) {
   return al256(n * ITEM_SLOT) + 4 * al256(n * sizeof(uint32_t)) + 256 + al256(plan_sort_temp_bytes(n));
 }
 hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d_keys, uint32_t n_keys,
-                       const ItemWs& iw, hipStream_t stream);
+                       const uint32_t* d_uses, const ItemWs& iw, hipStream_t stream);
 
 // Constant tables per context: [Ed25519 B rows (radix 2^10)][G rows k1][G rows r1][row scratch]
 #define EC_GTAB_LANES (EC_G_DIGITS * (EC_G_MULT / EC_MULT))  // one lane per (row, group of 32)

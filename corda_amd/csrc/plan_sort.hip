@@ -6,8 +6,9 @@
 // on table gathers once the B rows left LDS; key order keeps the -A rows hot in L2). The sort
 // is stable (LSD radix): input order is kept within a key. No per-item atomics, so a hot key
 // (a notary's) costs nothing extra.
-//   k_plan_keys    composite key (class << key_bits | key_idx) and the identity permutation
-//   rocprim::radix_sort_pairs over key_bits + 2 bits
+//   k_plan_keys    composite key (class | table mode | key_idx) and the identity permutation; the
+//                  mode bit (keyws.h) keeps row-0 and full-table items in separate waves
+//   rocprim::radix_sort_pairs over key_bits + 3 bits
 //   k_plan_ranges  class boundaries by binary search in the sorted keys
 #include <hip/hip_runtime.h>
 
@@ -25,12 +26,15 @@ typedef rocprim::radix_sort_config<rocprim::default_config, rocprim::default_con
 
 static uint32_t key_bits(uint32_t n_keys) {
   uint32_t b = 1;
-  while (b < 30 && (1u << b) < n_keys) ++b;
+  while (b < 29 && (1u << b) < n_keys) ++b;  // 2 class bits + the mode bit + 29 key bits
   return b;
 }
 
+// kb = key bits + 1: below the class, the key's table mode (1 = full tables, keyws.h) sits above
+// the key index, so a wave's lanes run one ladder variant, not both
 __global__ void __launch_bounds__(256) k_plan_keys(const cg_item* __restrict__ items, uint64_t n_items,
                                                    const cg_key* __restrict__ keys, uint32_t n_keys, uint32_t kb,
+                                                   const uint32_t* __restrict__ uses,
                                                    uint32_t* __restrict__ skey, uint32_t* __restrict__ sval) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_items) return;
@@ -43,7 +47,8 @@ __global__ void __launch_bounds__(256) k_plan_keys(const cg_item* __restrict__ i
       : s == CG_ECDSA_SECP256K1_SHA256 ? PLAN_K1
                                        : PLAN_CLASSES;
   }
-  skey[i] = (c << kb) | (c < PLAN_CLASSES ? k : 0u);
+  const uint32_t full = (c < PLAN_CLASSES && uses[k] >= ED_DIRECT_MAX_USES) ? 1u : 0u;
+  skey[i] = (c << kb) | (c < PLAN_CLASSES ? (full << (kb - 1)) | k : 0u);
   sval[i] = (uint32_t)i;
 }
 
@@ -70,11 +75,11 @@ size_t plan_sort_temp_bytes(uint64_t n_items) {
 }
 
 hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d_keys, uint32_t n_keys,
-                       const ItemWs& iw, hipStream_t stream) {
-  const uint32_t kb = key_bits(n_keys);
+                       const uint32_t* d_uses, const ItemWs& iw, hipStream_t stream) {
+  const uint32_t kb = key_bits(n_keys) + 1;  // + the table-mode bit
   const uint32_t B = 256;
   hipLaunchKernelGGL(k_plan_keys, dim3((unsigned)((n_items + B - 1) / B)), dim3(B), 0, stream, d_items, n_items,
-                     d_keys, n_keys, kb, iw.skey_in, iw.sval_in);
+                     d_keys, n_keys, kb, d_uses, iw.skey_in, iw.sval_in);
   size_t bytes = iw.sort_temp_bytes;
   hipError_t e = rocprim::radix_sort_pairs<PlanSortConfig>(iw.sort_temp, bytes, (const uint32_t*)iw.skey_in, iw.skey_out,
                                            (const uint32_t*)iw.sval_in, iw.perm, (size_t)n_items, 0u, kb + 2,

@@ -26,6 +26,46 @@ __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_item
     status[i] = CG_UNSUPPORTED;
 }
 
+// Items per key in this batch, saturating near ED_DIRECT_MAX_USES (keyws.h: how much table
+// each key gets). Out-of-range key
+// indices are k_misc_status's (CG_NOT_RUN) and count nowhere.
+__global__ void __launch_bounds__(256) k_key_uses(const cg_item* __restrict__ items, uint64_t n_items,
+                                                  uint32_t n_keys, uint32_t* __restrict__ uses) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items) return;
+  const uint32_t k = items[i].key_idx;
+  // counts only need to reach ED_DIRECT_MAX_USES: a hot key's later items skip the atomic
+  // (racing lanes may overshoot the threshold, which changes nothing)
+  if (k < n_keys && uses[k] < ED_DIRECT_MAX_USES) atomicAdd(&uses[k], 1u);
+}
+
+// Keys that get full tables (uses >= ED_DIRECT_MAX_USES), compacted per scheme class with one
+// atomic per wave and class. One wave per block.
+__global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ keys, uint32_t n_keys,
+                                                     const uint32_t* __restrict__ uses, uint32_t* __restrict__ full,
+                                                     uint32_t* __restrict__ full_count) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t lane = threadIdx.x;
+  int c = -1;
+  if (i < n_keys && uses[i] >= ED_DIRECT_MAX_USES) {
+    const uint8_t s = keys[i].scheme;
+    c = s == CG_EDDSA_ED25519_SHA512 ? PLAN_ED
+      : s == CG_ECDSA_SECP256R1_SHA256 ? PLAN_R1
+      : s == CG_ECDSA_SECP256K1_SHA256 ? PLAN_K1
+                                       : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < PLAN_CLASSES; ++k) {
+    const uint64_t m = __ballot(c == k);
+    if (m == 0) continue;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(&full_count[k], (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (c == k) full[(size_t)k * n_keys + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+  }
+}
+
 hipError_t upload_constants() {
   hipError_t e = ed_upload_constants();
   if (e != hipSuccess) return e;
@@ -43,9 +83,20 @@ hipError_t init_btab(void* d_btab, hipStream_t stream) {
 }
 
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                          void* d_keyprep, hipStream_t stream, const Fork* fork) {
+                          void* d_keyprep, hipStream_t stream, const Fork* fork, const cg_item* d_items,
+                          uint64_t n_items) {
   if (n_keys == 0) return hipSuccess;
   const KeyWs w = key_ws(d_keyprep, n_keys);
+  // use counts first (main stream; the side streams fork after them)
+  hipError_t e0 = hipMemsetAsync(w.uses, d_items ? 0 : 0xff, sizeof(uint32_t) * n_keys, stream);
+  if (e0 != hipSuccess) return e0;
+  if (d_items && n_items)
+    hipLaunchKernelGGL(k_key_uses, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, stream, d_items, n_items,
+                       n_keys, w.uses);
+  e0 = hipMemsetAsync(w.full_count, 0, 256, stream);
+  if (e0 != hipSuccess) return e0;
+  hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys,
+                     (const uint32_t*)w.uses, w.full, w.full_count);
   if (!fork) {
     ed_launch_key_abyte(d_keys, n_keys, d_arena, arena_len, w, stream);
     ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, stream, stream, nullptr, nullptr);
@@ -77,7 +128,7 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
   hipLaunchKernelGGL(k_misc_status, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
                      d_status);
   // plan: items sorted by (scheme class, key) (plan_sort.hip)
-  hipError_t e = launch_plan(d_items, n_items, d_keys, n_keys, iw, stream);
+  hipError_t e = launch_plan(d_items, n_items, d_keys, n_keys, (const uint32_t*)w.uses, iw, stream);
   if (e != hipSuccess) return e;
   ed_launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
                   d_btab, stream, fork ? fork->ready[2] : nullptr);
@@ -91,7 +142,7 @@ hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d
                          void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
                          const uint8_t* d_msgs, uint64_t msgs_len, const Fork* fork) {
   if (n_items == 0) return hipSuccess;
-  hipError_t e = launch_keyprep(d_keys, n_keys, d_arena, arena_len, d_keyprep, stream, fork);
+  hipError_t e = launch_keyprep(d_keys, n_keys, d_arena, arena_len, d_keyprep, stream, fork, d_items, n_items);
   if (e != hipSuccess) return e;
   return launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, d_keyprep, d_item_ws,
                       d_btab, stream, d_msgs, msgs_len, fork);

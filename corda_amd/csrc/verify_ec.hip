@@ -5,7 +5,8 @@
 //   k_ec_keyprep_tab   one lane per (key, row): 32 affine multiples     the ladder for the tab)
 //   k_ec_prep          one lane per item: DER, range checks, SHA-256, e mod n
 //   k_ec_inv           16 items per lane: one shared inversion of s mod n -> u1, u2
-//   k_ec_ladder        one lane per item: u1 G (radix-2^10 constant table) + u2 Q (key rows),
+//   k_ec_ladder        one lane per item: u1 G (radix-2^10 constant table) + u2 Q (key rows;
+//                      row 0 and 252 doublings for a key with few items, keyws.h),
 //                      BC's inversion-free x(R) == r check
 // Replaces, per item, BC DSABase.engineVerify behind Crypto.isValid
 // (core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559, schemes :92-117).
@@ -44,13 +45,17 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_decode(const cg_key* __restri
   hdr[i] = h;
 }
 
+// one lane per full-table key of this curve (keyws.h: the compacted list)
 template <int C>
-__global__ void __launch_bounds__(64) k_ec_keyprep_chain(const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                         const EdKeyHdr* __restrict__ hdr,
+__global__ void __launch_bounds__(64) k_ec_keyprep_chain(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                         const uint32_t* __restrict__ full,
+                                                         const uint32_t* __restrict__ full_count,
                                                          BaseSlot* __restrict__ bases) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_keys) return;
-  if (keys[i].scheme != ec_scheme<C>() || hdr[i].status != 0) return;
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = plan_class_of_curve(C);
+  if (l >= full_count[c]) return;
+  const uint32_t i = full[(size_t)c * n_keys + l];
+  if (hdr[i].status != 0) return;
   Jac P = bases[(size_t)i * KEY_BASES].ec;
   for (int j = 1; j < EC_ROWS; ++j) {
     jac_dbl_n<C>(P, P, EC_W * EC_WINDOWS);
@@ -58,17 +63,32 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_chain(const cg_key* __restric
   }
 }
 
-// one lane per (key, row)
+// Lanes g < n_keys: row 0 of key g (every key of this curve with items); then row-major
+// (row j >= 1, position l of the curve's full-table list): only hot keys' rows 1..10 run.
 template <int C>
 __global__ void __launch_bounds__(64) k_ec_keyprep_tab(const cg_key* __restrict__ keys, uint32_t n_keys,
                                                        const EdKeyHdr* __restrict__ hdr,
-                                                       const BaseSlot* __restrict__ bases, TabSlot* __restrict__ tabs,
-                                                       EcRowScratch* __restrict__ scratch) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = g / EC_ROWS, j = g % EC_ROWS;
-  if (i >= n_keys) return;
-  if (keys[i].scheme != ec_scheme<C>() || hdr[i].status != 0) return;
-  ec_row_build<C>(tabs[i].ec.t[j], bases[(size_t)i * KEY_BASES + j].ec, scratch[g], c_ec[C]);
+                                                       const BaseSlot* __restrict__ bases,
+                                                       const uint32_t* __restrict__ uses,
+                                                       const uint32_t* __restrict__ full,
+                                                       const uint32_t* __restrict__ full_count,
+                                                       TabSlot* __restrict__ tabs, EcRowScratch* __restrict__ scratch) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = plan_class_of_curve(C);
+  uint32_t i, j;
+  if (g < n_keys) {
+    i = (uint32_t)g;
+    j = 0;
+    if (keys[i].scheme != ec_scheme<C>() || uses[i] == 0) return;
+  } else {
+    const uint64_t h = g - n_keys;
+    j = 1 + (uint32_t)(h / n_keys);
+    const uint32_t l = (uint32_t)(h % n_keys);
+    if (j >= (uint32_t)EC_ROWS || l >= full_count[c]) return;
+    i = full[(size_t)c * n_keys + l];
+  }
+  if (hdr[i].status != 0) return;
+  ec_row_build<C>(tabs[i].ec.t[j], bases[(size_t)i * KEY_BASES + j].ec, scratch[(size_t)i * EC_ROWS + j], c_ec[C]);
 }
 
 // one lane per (G row u, group g of 32 multiples)
@@ -137,6 +157,7 @@ __global__ void __launch_bounds__(256) k_ec_inv(const uint32_t* __restrict__ per
 template <int C>
 __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
                                                    const uint32_t* __restrict__ ranges,
+                                                   const uint32_t* __restrict__ uses,
                                                    const TabSlot* __restrict__ tabs,
                                                    const EcGTab* __restrict__ gtab, uint8_t* __restrict__ status,
                                                    const EcItemWs* __restrict__ ws) {
@@ -146,7 +167,12 @@ __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ i
   const uint32_t i = perm[p];
   if (status[i] != EC_PENDING_BASE + C) return;
   const EcItemWs w = ws[p];
-  status[i] = (uint8_t)ecdsa_ladder_check<C>(w.a, w.b, w.r, *gtab, tabs[items[i].key_idx].ec, c_ec[C]);
+  const uint32_t key = items[i].key_idx;
+  if (uses[key] >= ED_DIRECT_MAX_USES) {
+    status[i] = (uint8_t)ecdsa_ladder_check<C>(w.a, w.b, w.r, *gtab, tabs[key].ec, c_ec[C]);
+  } else {  // a key with few items: row 0 only (keyws.h)
+    status[i] = (uint8_t)ecdsa_ladder_check_row0<C>(w.a, w.b, w.r, *gtab, tabs[key].ec.t[0], c_ec[C]);
+  }
 }
 
 hipError_t ec_upload_constants() {
@@ -168,14 +194,17 @@ hipError_t ec_init_const(void* d_btab, hipStream_t stream) {
 template <int C>
 static void launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                            const KeyWs& w, hipStream_t stream, hipEvent_t decoded) {
-  const uint32_t B = 64, elanes = n_keys * EC_ROWS;
+  const uint32_t B = 64;
+  const uint64_t elanes = (uint64_t)n_keys * EC_ROWS;
   const dim3 g((n_keys + B - 1) / B);
   hipLaunchKernelGGL(k_ec_keyprep_decode<C>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.hdr,
                      w.bases);
   if (decoded) hipEventRecord(decoded, stream);
-  hipLaunchKernelGGL(k_ec_keyprep_chain<C>, g, dim3(B), 0, stream, d_keys, n_keys, w.hdr, w.bases);
-  hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3((elanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
-                     w.bases, w.tab, w.ecs);
+  hipLaunchKernelGGL(k_ec_keyprep_chain<C>, g, dim3(B), 0, stream, n_keys, w.hdr, (const uint32_t*)w.full,
+                     (const uint32_t*)w.full_count, w.bases);
+  hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3((unsigned)((elanes + B - 1) / B)), dim3(B), 0, stream, d_keys, n_keys,
+                     w.hdr, w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count,
+                     w.tab, w.ecs);
 }
 
 void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
@@ -205,8 +234,8 @@ static void launch_ladder(const cg_item* d_items, uint64_t n_items, uint8_t* d_s
   if (ready) hipStreamWaitEvent(stream, ready, 0);
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
-  hipLaunchKernelGGL(k_ec_ladder<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.tab,
-                     gtab(d_btab, C), d_status, (const EcItemWs*)iw.slots);
+  hipLaunchKernelGGL(k_ec_ladder<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
+                     (const uint32_t*)w.uses, w.tab, gtab(d_btab, C), d_status, (const EcItemWs*)iw.slots);
 }
 
 // prep + inversion of both curves first (they need only the decoded keys), then the ladders,

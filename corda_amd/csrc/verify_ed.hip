@@ -6,7 +6,9 @@
 //   k_ed_hash            one lane per item: SHA-512 challenge, scalar prep, signed digits
 //                        (needs only Abyte: overlaps the whole key decode + table build)
 //   k_ed_ladder          one lane per item: key status, then 2 windows x (~21.5 rows of -A +
-//                        13 rows of the radix-2^10 B table) mixed additions, 6 doublings
+//                        13 rows of the radix-2^10 B table) mixed additions, 6 doublings; for a
+//                        key with few items in the batch, row 0 of -A and 252 doublings
+//                        (keyws.h ED_DIRECT_MAX_USES)
 //   k_ed_finish          16 items per lane: batch inversion, encode, byte compare
 // Replaces, per item, i2p EdDSAEngine.engineVerify behind Crypto.isValid
 // (core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:553-559, scheme :120-133).
@@ -82,13 +84,16 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_decode(const cg_key* __restri
   hdr[i].status = st;
 }
 
-// one lane per key: row bases 2^{24j} (-A), j = 1..10 (a serial chain of 240 doublings)
-__global__ void __launch_bounds__(64) k_ed_keyprep_chain(const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                         const EdKeyHdr* __restrict__ hdr,
+// one lane per full-table key (keyws.h: the compacted list): row bases 2^{12j} (-A), j = 1..21
+// (a serial chain of 240 doublings)
+__global__ void __launch_bounds__(64) k_ed_keyprep_chain(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                         const uint32_t* __restrict__ full,
+                                                         const uint32_t* __restrict__ full_count,
                                                          BaseSlot* __restrict__ bases) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_keys) return;
-  if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || hdr[i].status != 0) return;
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= full_count[PLAN_ED]) return;
+  const uint32_t i = full[(size_t)PLAN_ED * n_keys + l];
+  if (hdr[i].status != 0) return;
   ge_p3 P = bases[(size_t)i * KEY_BASES].ed;
   for (int j = 1; j < EdCfg::kRows; ++j) {
     ed_dbl_n(P, P, ED_W * ED_K);
@@ -113,16 +118,31 @@ __device__ void ed_small_mul(ge_p3& R, const ge_p3& P, uint32_t m) {
   }
 }
 
-// one lane per (key, row): the 32 affine multiples of the row base, one inversion per row
-// (ed_row_build; Z prefixes in the key's ECDSA scratch, unused by an Ed25519 key)
+// the 32 affine multiples of a row base, one inversion per row (ed_row_build; Z prefixes in the
+// key's ECDSA scratch, unused by an Ed25519 key). Lanes g < n_keys: row 0 of key g (every key
+// with items); then row-major (row j >= 1, position l of the full-table list), so only hot keys'
+// rows 1..21 run, on dense lanes.
 __global__ void __launch_bounds__(64) k_ed_keyprep_tab(const cg_key* __restrict__ keys, uint32_t n_keys,
                                                        const EdKeyHdr* __restrict__ hdr,
                                                        const BaseSlot* __restrict__ bases,
+                                                       const uint32_t* __restrict__ uses,
+                                                       const uint32_t* __restrict__ full,
+                                                       const uint32_t* __restrict__ full_count,
                                                        TabSlot* __restrict__ tabs, EcRowScratch* __restrict__ ecs) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = g / EdCfg::kRows, j = g % EdCfg::kRows;
-  if (i >= n_keys) return;
-  if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || hdr[i].status != 0) return;
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t i, j;
+  if (g < n_keys) {
+    i = (uint32_t)g;
+    j = 0;
+    if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || uses[i] == 0) return;
+  } else {
+    const uint64_t h = g - n_keys;
+    j = 1 + (uint32_t)(h / n_keys);
+    const uint32_t l = (uint32_t)(h % n_keys);
+    if (j >= (uint32_t)EdCfg::kRows || l >= full_count[PLAN_ED]) return;
+    i = full[(size_t)PLAN_ED * n_keys + l];
+  }
+  if (hdr[i].status != 0) return;
   fe* zpre = (fe*)(ecs + (size_t)i * EC_ROWS) + (size_t)j * EdCfg::kMult;
   ed_row_build<EdCfg::kMult>(tabs[i].ed.t[j], bases[(size_t)i * KEY_BASES + j].ed, c_ed.d2, zpre);
 }
@@ -266,8 +286,8 @@ struct PickGlobal {
 // projective in the item slot.
 __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
-    const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBTab* __restrict__ btab,
-    uint8_t* __restrict__ status, void* __restrict__ slots) {
+    const EdKeyHdr* __restrict__ hdr, const uint32_t* __restrict__ uses, const TabSlot* __restrict__ tabs,
+    const EdBTab* __restrict__ btab, uint8_t* __restrict__ status, void* __restrict__ slots) {
   const uint64_t p = (uint64_t)ranges[PLAN_ED] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ranges[PLAN_ED + 1]) return;
   const uint32_t i = perm[p];
@@ -279,7 +299,11 @@ __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
   if (status[i] != ED_PENDING) return;
   const EdDigits d = ((const EdDigits*)slots)[p];
   ge_p2 q;
-  ed_double_scalar_wb<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed, *btab, PickGlobal(), PickGlobal());
+  if (uses[key] >= ED_DIRECT_MAX_USES) {
+    ed_double_scalar_wb<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed, *btab, PickGlobal(), PickGlobal());
+  } else {  // a key with few items: row 0 only (keyws.h)
+    ed_double_scalar_row0<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed.t[0], *btab, PickGlobal(), PickGlobal());
+  }
   ((ge_p2*)slots)[p] = q;
 }
 
@@ -354,11 +378,12 @@ void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const uint8
   const uint32_t B = 64;  // one wave per block: keys are few, spread them over CUs
   hipLaunchKernelGGL(k_ed_keyprep_decode, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, d_arena,
                      arena_len, w.hdr, w.bases);
-  hipLaunchKernelGGL(k_ed_keyprep_chain, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
-                     w.bases);
-  const uint32_t lanes = n_keys * EdCfg::kRows;
-  hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((lanes + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
-                     w.bases, w.tab, w.ecs);
+  hipLaunchKernelGGL(k_ed_keyprep_chain, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
+                     (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.bases);
+  const uint64_t lanes = (uint64_t)n_keys * EdCfg::kRows;
+  hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((unsigned)((lanes + B - 1) / B)), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
+                     w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.tab,
+                     w.ecs);
 }
 
 void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
@@ -373,7 +398,7 @@ void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_ite
                      arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
   if (tables_ready) hipStreamWaitEvent(stream, tables_ready, 0);
   hipLaunchKernelGGL(k_ed_ladder, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                     w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+                     (const uint32_t*)w.uses, w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
   const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
   hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
                      arena_len, d_status, (const ge_p2*)iw.slots);

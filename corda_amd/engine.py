@@ -140,6 +140,13 @@ class Engine:
                                                  len(leaves), _p(arena), arena.size, _p(st)), "cg_verify_filtered")
         return st
 
+    def verify_filtered_device(self, d_ftxs, n_ftx, d_nodes, n_nodes, d_leaves, n_leaves, d_arena, arena_len,
+                               d_status, stream=0):
+        """Asynchronous device form of verify_filtered (every table already in HBM)."""
+        _lib.check(_lib.lib().cg_verify_filtered_device(self._h, d_ftxs, n_ftx, d_nodes, n_nodes, d_leaves, n_leaves,
+                                                        d_arena, arena_len, d_status, stream or None),
+                   "cg_verify_filtered_device")
+
     # ------------------------------------------------------------------ transactions
     def verify_transactions(self, txs, comps, keys, sigs, tmpls, arena, mode=MODE_DOVERIFY):
         """Tx ids + every signature over SignableData(id, metadata) in one call

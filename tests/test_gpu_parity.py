@@ -76,6 +76,43 @@ def test_synthetic_ed25519_vs_c_oracle(engine):
     assert np.all(st[(labels == 7) & kok] == B.SIG_MALFORMED)
 
 
+def test_key_use_modes_vs_c_oracle(engine):
+    """Keys get full row tables, row 0 only, or no rows by how many items use them in the batch
+    (keyws.h ED_DIRECT_MAX_USES): keys around the threshold (30000 items over 512 / 1000 keys), keys with one or two items,
+    hot keys and unused keys in one shuffled batch, all bit-exact against the C oracle."""
+    from tools.workload import wl
+    parts = []
+    for n_items, n_keys, seed in ((30000, 512, 21), (24000, 8000, 22), (30000, 1000, 23), (3000, 3000, 24)):
+        b, _ = wl.ed25519_batch(n_items, n_keys=n_keys, msg_len=200, corrupt_permille=150, seed=seed,
+                                bad_key_every=97, nthreads=16)
+        parts.append(b)
+    b, _ = wl.concat(parts, shuffle_seed=25)
+    uses = np.bincount(b.items["key_idx"], minlength=len(b.keys))
+    assert (uses == 0).any() and (uses == 1).any() and (uses >= 32).any() and ((uses > 1) & (uses < 32)).any()
+    st = engine.verify(b, B.MODE_DOVERIFY)
+    ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
+    assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
+
+
+def test_key_use_modes_ecdsa_vs_c_oracle(engine):
+    """The same table sizing for secp256r1 / secp256k1 keys (row 0 + 252-doubling ladder for keys
+    with few items), mixed with Ed25519 keys in one batch, bit-exact against the C oracle."""
+    from tools.workload import wl
+    parts = []
+    for curve in (0, 1):
+        for n_items, n_keys, seed in ((6000, 64, 31), (5000, 2500, 32), (6000, 200, 33)):
+            b, _ = wl.ecdsa_batch(curve, n_items, n_keys=n_keys, msg_len=150, corrupt_permille=120,
+                                  seed=seed + 10 * curve, nthreads=16)
+            parts.append(b)
+    e, _ = wl.ed25519_batch(5000, n_keys=2000, msg_len=150, corrupt_permille=120, seed=39, nthreads=16)
+    b, _ = wl.concat(parts + [e], shuffle_seed=40)
+    uses = np.bincount(b.items["key_idx"], minlength=len(b.keys))
+    assert (uses == 1).any() and (uses >= 32).any()
+    st = engine.verify(b, B.MODE_DOVERIFY)
+    ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
+    assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
+
+
 def test_edge_batches(engine):
     from corda_amd.batch import BatchBuilder
     items = golden_io.load("ed25519.json")

@@ -180,3 +180,47 @@ def tx_pipeline(n_tx, n_keys=1024, seed=4, corrupt_permille=20, nthreads=8, comp
                  _p(arena[tmpl_base:]), len(pre), _p(arena[tmpl_base + len(pre):]), len(suf), corrupt_permille,
                  seed, _p(ids), _p(labels), nthreads)
     return TxPipeline(txs, comps, keys, sigs, tmpls, arena[:arena_len + 64], ids.reshape(-1, 32), labels)
+
+
+class _Sha256Host:
+    """hashlib stand-in for the engine when building bench inputs (tree node hashes)."""
+
+    @staticmethod
+    def sha256(msgs):
+        import hashlib
+        return [hashlib.sha256(bytes(m)).digest() for m in msgs]
+
+
+def filtered_pool(n_unique, seed=5, comp_len=(80, 600), corrupt_permille=50):
+    """Notary tear-offs (NonValidatingNotaryFlow.kt:22-27): WireTransactions of the
+    config-4 shape (1+Poisson(1) inputs, Poisson(3) outputs, 1+Poisson(3) commands, notary, salt)
+    filtered down to inputs + notary, as a non-validating notary receives them. Returns the list
+    of corda_amd.merkle.FilteredTransaction and the expected status per tear-off (a corrupted
+    one has a flipped bit in a visible component: status 1)."""
+    import hashlib
+    import struct
+    from corda_amd import merkle as M
+    rng = np.random.default_rng(seed)
+    out, expect = [], []
+    for _ in range(n_unique):
+        n_in, n_out, n_cmd = 1 + rng.poisson(1), rng.poisson(3), 1 + rng.poisson(3)
+        n = n_in + n_out + n_cmd + 1
+        blobs = [rng.integers(0, 256, int(rng.integers(comp_len[0], comp_len[1] + 1)), dtype=np.uint8).tobytes()
+                 for _ in range(n)]
+        salt = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        nonces = [hashlib.sha256(salt + struct.pack(">i", i)).digest() for i in range(n)]
+        hashes = [hashlib.sha256(b + x).digest() for b, x in zip(blobs, nonces)]
+        hashes.append(hashlib.sha256(b"\x01" + salt).digest())
+        full = M.merkle_tree(hashes, engine=_Sha256Host)
+        vis = list(range(n_in)) + [n - 1]
+        pmt = M.PartialMerkleTree.build(full, [hashes[i] for i in vis])
+        vb = [blobs[i] for i in vis]
+        bad = rng.integers(0, 1000) < corrupt_permille
+        if bad:
+            j = int(rng.integers(0, len(vb)))
+            b = bytearray(vb[j])
+            b[int(rng.integers(0, len(b)))] ^= 1
+            vb[j] = bytes(b)
+        out.append(M.FilteredTransaction(full.hash, vb, [nonces[i] for i in vis], pmt))
+        expect.append(1 if bad else 0)
+    return out, np.array(expect, dtype=np.uint8)

@@ -93,10 +93,13 @@ struct KeyWs {
                    // tables, full[c * n_keys + l] for l < full_count[c] (any order), so the
                    // chain / row kernels run dense lanes however few keys are hot
   uint32_t* full_count;
+  uint8_t* seen;   // 1 if any item of the batch uses the key (exact; uses is sampled)
 };
 
 // How much table a key gets, from the number of items that use it in the batch (one-shot entry
-// points count them; cg_prepare_keys_device cannot, and builds every key in full):
+// points estimate it from every KEY_USES_SAMPLE-th item, plus an exact "used at all" flag;
+// cg_prepare_keys_device cannot, and builds every key in full). The mode changes only speed,
+// never a verdict: both ladders compute the same point.
 //   0 uses                        decode only (Abyte, status), no rows
 //   1 .. ED_DIRECT_MAX_USES - 1   row 0 only (the 32 affine multiples of -A): the item runs the
 //                                 252-doubling Horner ladder (ed_double_scalar_row0)
@@ -104,6 +107,7 @@ struct KeyWs {
 // Break-even (measured on MI355X, 2^20 Ed25519 items): a key's full tables cost ~230 ns of
 // GPU time, the row-0 ladder ~7 ns more per item than the full-table one -> ~32 items.
 #define KEY_USES_ALL 0xffffffffu
+#define KEY_USES_SAMPLE 4u
 #ifndef ED_DIRECT_MAX_USES
 #define ED_DIRECT_MAX_USES 32u
 #endif
@@ -124,12 +128,14 @@ static inline KeyWs key_ws(void* base, uint32_t n_keys) {
   w.full = (uint32_t*)p;
   p += al256(3 * n * sizeof(uint32_t));
   w.full_count = (uint32_t*)p;
+  p += 256;
+  w.seen = p;
   return w;
 }
 static inline size_t key_ws_bytes(uint32_t n_keys) {
   const size_t n = n_keys ? n_keys : 1;
   return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(TabSlot)) + al256(n * KEY_BASES * sizeof(BaseSlot)) +
-         n * EC_ROWS * sizeof(EcRowScratch) + al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256;
+         n * EC_ROWS * sizeof(EcRowScratch) + al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256 + al256(n);
 }
 
 // Per-item workspace slot (indexed by plan position, so the schemes never share one):

@@ -26,28 +26,46 @@ __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_item
     status[i] = CG_UNSUPPORTED;
 }
 
-// Items per key in this batch, saturating near ED_DIRECT_MAX_USES (keyws.h: how much table
-// each key gets). Out-of-range key
-// indices are k_misc_status's (CG_NOT_RUN) and count nowhere.
+// Per-key use counts, sampled: every KEY_USES_SAMPLE-th item adds KEY_USES_SAMPLE (no-return
+// atomics, a quarter of the traffic of counting all), every item marks its key as used (plain
+// stores: the exact "has items" bit row 0 depends on). Out-of-range key indices are
+// k_misc_status's (CG_NOT_RUN) and count nowhere.
+__global__ void __launch_bounds__(256) k_key_init(uint32_t n_keys, uint32_t all, uint32_t* __restrict__ uses,
+                                                  uint8_t* __restrict__ seen, uint32_t* __restrict__ full_count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < PLAN_CLASSES) full_count[i] = 0;
+  if (i >= n_keys) return;
+  uses[i] = all ? KEY_USES_ALL : 0u;
+  seen[i] = all ? 1 : 0;
+}
+
 __global__ void __launch_bounds__(256) k_key_uses(const cg_item* __restrict__ items, uint64_t n_items,
-                                                  uint32_t n_keys, uint32_t* __restrict__ uses) {
+                                                  uint32_t n_keys, uint32_t* __restrict__ uses,
+                                                  uint8_t* __restrict__ seen) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_items) return;
   const uint32_t k = items[i].key_idx;
-  // counts only need to reach ED_DIRECT_MAX_USES: a hot key's later items skip the atomic
-  // (racing lanes may overshoot the threshold, which changes nothing)
-  if (k < n_keys && uses[k] < ED_DIRECT_MAX_USES) atomicAdd(&uses[k], 1u);
+  if (k >= n_keys) return;
+  seen[k] = 1;
+  if (i % KEY_USES_SAMPLE == 0) atomicAdd(&uses[k], KEY_USES_SAMPLE);
 }
 
 // Keys that get full tables (uses >= ED_DIRECT_MAX_USES), compacted per scheme class with one
 // atomic per wave and class. One wave per block.
 __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                     const uint32_t* __restrict__ uses, uint32_t* __restrict__ full,
-                                                     uint32_t* __restrict__ full_count) {
+                                                     uint32_t* __restrict__ uses, const uint8_t* __restrict__ seen,
+                                                     uint32_t* __restrict__ full, uint32_t* __restrict__ full_count) {
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
   const uint32_t lane = threadIdx.x;
   int c = -1;
-  if (i < n_keys && uses[i] >= ED_DIRECT_MAX_USES) {
+  uint32_t u = 0;
+  if (i < n_keys) {  // the estimate, made exact where it matters: a used key counts >= 1
+    u = uses[i];
+    if (!seen[i]) u = 0;
+    else if (u == 0) u = 1;
+    uses[i] = u;
+  }
+  if (i < n_keys && u >= ED_DIRECT_MAX_USES) {
     const uint8_t s = keys[i].scheme;
     c = s == CG_EDDSA_ED25519_SHA512 ? PLAN_ED
       : s == CG_ECDSA_SECP256R1_SHA256 ? PLAN_R1
@@ -88,15 +106,14 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   if (n_keys == 0) return hipSuccess;
   const KeyWs w = key_ws(d_keyprep, n_keys);
   // use counts first (main stream; the side streams fork after them)
-  hipError_t e0 = hipMemsetAsync(w.uses, d_items ? 0 : 0xff, sizeof(uint32_t) * n_keys, stream);
-  if (e0 != hipSuccess) return e0;
+  const uint32_t kl = n_keys > PLAN_CLASSES ? n_keys : PLAN_CLASSES;
+  hipLaunchKernelGGL(k_key_init, dim3((kl + 255) / 256), dim3(256), 0, stream, n_keys, d_items ? 0u : 1u, w.uses,
+                     w.seen, w.full_count);
   if (d_items && n_items)
     hipLaunchKernelGGL(k_key_uses, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, stream, d_items, n_items,
-                       n_keys, w.uses);
-  e0 = hipMemsetAsync(w.full_count, 0, 256, stream);
-  if (e0 != hipSuccess) return e0;
-  hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys,
-                     (const uint32_t*)w.uses, w.full, w.full_count);
+                       n_keys, w.uses, w.seen);
+  hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys, w.uses,
+                     (const uint8_t*)w.seen, w.full, w.full_count);
   if (!fork) {
     ed_launch_key_abyte(d_keys, n_keys, d_arena, arena_len, w, stream);
     ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, stream, stream, nullptr, nullptr);

@@ -62,6 +62,11 @@ struct DevBuf {
 
 }  // namespace
 
+// cg_verify_batch splits a large host batch into this many consecutive item chunks: the arena
+// bytes chunk k needs go H2D on a copy stream while chunk k-1 verifies.
+#define CG_H2D_CHUNKS 4
+#define CG_H2D_MIN_ITEMS (1u << 17)
+
 struct cg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -72,6 +77,9 @@ struct cg_ctx {
   DevBuf txitems, msgs, tmpls, h_txs, h_comps, h_sigs, h_ids, h_txst;
   // tear-offs: leaf-hash workspace
   DevBuf ftxws;
+  // host-buffer verify: a copy stream and one event per arena segment (chunked H2D / verify)
+  hipStream_t copy = nullptr;
+  hipEvent_t seg[CG_H2D_CHUNKS + 1] = {};
 };
 
 extern "C" {
@@ -115,6 +123,9 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   for (int k = 0; k < 2 && e == hipSuccess; ++k)
     e = hipEventCreateWithFlags(&c->fork.ec_decoded[k], hipEventDisableTiming);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.ready[k], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+  for (int k = 0; k <= CG_H2D_CHUNKS && e == hipSuccess; ++k)
+    e = hipEventCreateWithFlags(&c->seg[k], hipEventDisableTiming);
   if (e == hipSuccess) e = cg::upload_constants();
   if (e == hipSuccess) e = c->btab.ensure(cg::btab_bytes());
   if (e == hipSuccess) e = cg::init_btab(c->btab.p, c->stream);
@@ -152,6 +163,12 @@ void cg_close(cg_ctx* c) {
     if (c->fork.ready[k]) hipEventDestroy(c->fork.ready[k]);
   }
   if (c->fork.start) hipEventDestroy(c->fork.start);
+  if (c->copy) {
+    hipStreamSynchronize(c->copy);
+    hipStreamDestroy(c->copy);
+  }
+  for (int k = 0; k <= CG_H2D_CHUNKS; ++k)
+    if (c->seg[k]) hipEventDestroy(c->seg[k]);
   for (int k = 0; k < 2; ++k)
     if (c->fork.ec_decoded[k]) hipEventDestroy(c->fork.ec_decoded[k]);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -247,15 +264,56 @@ int cg_verify_batch(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_ite
   hipStream_t s = c->stream;
   hipEvent_t ev[4];
   for (auto& e : ev) HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+  // Chunk plan: item chunk k needs arena[0 .. need[k]) (prefix max of its items' extents,
+  // clamped to the arena: an item outside it is CG_NOT_RUN and reads nothing); key prep needs
+  // arena[0 .. key_end). Pipelined only when the keys sit in the first quarter of the arena,
+  // which is how a caller appending (key, sig, clear) in order lays it out; otherwise one copy.
+  uint64_t key_end = 0;
+  for (uint32_t k = 0; k < n_keys; ++k) {
+    const uint64_t e = keys[k].off > arena_len ? arena_len : keys[k].off + keys[k].len;
+    key_end = e > key_end ? e : key_end;
+  }
+  key_end = key_end < arena_len ? key_end : arena_len;
+  int chunks = (n_items >= CG_H2D_MIN_ITEMS && key_end <= arena_len / 4) ? CG_H2D_CHUNKS : 1;
+  uint64_t first[CG_H2D_CHUNKS + 1], need[CG_H2D_CHUNKS];
+  for (int k = 0; k <= chunks; ++k) first[k] = n_items * (uint64_t)k / (uint64_t)chunks;
+  uint64_t run = key_end;
+  for (int k = 0; k < chunks; ++k) {
+    for (uint64_t i = first[k]; i < first[k + 1]; ++i) {
+      const cg_item& it = items[i];
+      const uint64_t se = it.sig_off > arena_len ? 0 : it.sig_off + it.sig_len;
+      const uint64_t me = it.msg_off > arena_len ? 0 : it.msg_off + it.msg_len;
+      const uint64_t e = se > me ? se : me;
+      if (e > run) run = e;
+    }
+    need[k] = run < arena_len ? run : arena_len;
+  }
+  if (chunks == 1) need[0] = arena_len;
   HIP_TRY(hipEventRecord(ev[0], s), "hipEventRecord");
-  if (n_keys) HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, s), "H2D keys");
-  HIP_TRY(hipMemcpyAsync(c->items.p, items, sizeof(cg_item) * n_items, hipMemcpyHostToDevice, s), "H2D items");
-  if (arena_len) HIP_TRY(hipMemcpyAsync(c->arena.p, arena, arena_len, hipMemcpyHostToDevice, s), "H2D arena");
-  HIP_TRY(hipEventRecord(ev[1], s), "hipEventRecord");
-  HIP_TRY(cg::launch_verify((const cg_key*)c->keys.p, n_keys, (const cg_item*)c->items.p, n_items,
-                            (const uint8_t*)c->arena.p, arena_len, mode, (uint8_t*)c->status.p, c->keyprep.p,
-                            c->itemws.p, c->btab.p, s, nullptr, 0, &c->fork),
-          "launch_verify");
+  HIP_TRY(hipStreamWaitEvent(c->copy, ev[0], 0), "hipStreamWaitEvent");
+  if (n_keys)
+    HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, c->copy), "H2D keys");
+  HIP_TRY(hipMemcpyAsync(c->items.p, items, sizeof(cg_item) * n_items, hipMemcpyHostToDevice, c->copy), "H2D items");
+  uint64_t copied = 0;
+  for (int k = 0; k < chunks; ++k) {
+    if (need[k] > copied) {
+      HIP_TRY(hipMemcpyAsync((uint8_t*)c->arena.p + copied, arena + copied, need[k] - copied, hipMemcpyHostToDevice,
+                             c->copy), "H2D arena");
+      copied = need[k];
+    }
+    HIP_TRY(hipEventRecord(c->seg[k], c->copy), "hipEventRecord");
+    HIP_TRY(hipStreamWaitEvent(s, c->seg[k], 0), "hipStreamWaitEvent");
+    if (k == 0) {
+      HIP_TRY(hipEventRecord(ev[1], s), "hipEventRecord");
+      // key tables sized by every item's key (not just chunk 0's)
+      HIP_TRY(cg::launch_keyprep((const cg_key*)c->keys.p, n_keys, (const uint8_t*)c->arena.p, arena_len, c->keyprep.p,
+                                 s, &c->fork, (const cg_item*)c->items.p, n_items), "launch_keyprep");
+    }
+    HIP_TRY(cg::launch_items((const cg_key*)c->keys.p, n_keys, (const cg_item*)c->items.p + first[k],
+                             first[k + 1] - first[k], (const uint8_t*)c->arena.p, arena_len, mode,
+                             (uint8_t*)c->status.p + first[k], c->keyprep.p, c->itemws.p, c->btab.p, s, nullptr, 0,
+                             &c->fork), "launch_items");
+  }
   HIP_TRY(hipEventRecord(ev[2], s), "hipEventRecord");
   HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n_items, hipMemcpyDeviceToHost, s), "D2H status");
   HIP_TRY(hipEventRecord(ev[3], s), "hipEventRecord");

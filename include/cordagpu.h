@@ -151,7 +151,9 @@ const char* cg_last_error(void); /* thread-local message for the last non-OK ret
 int cg_open(cg_ctx** out, const cg_config* cfg);
 void cg_close(cg_ctx* ctx);
 
-/* Host buffers in, host status bytes out (copies through pinned staging). */
+/* Host buffers in, host status bytes out. A batch of >= 2^17 items whose keys sit in the first quarter
+ * of the arena is copied and verified in 4 consecutive item chunks, H2D of chunk k overlapping the
+ * verify of chunk k-1 (stats: ms_h2d = until the first chunk is resident, ms_verify = the rest). */
 int cg_verify_batch(cg_ctx* ctx, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
                     const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
                     cg_stats* stats_opt);

@@ -113,6 +113,36 @@ def test_key_use_modes_ecdsa_vs_c_oracle(engine):
     assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
 
 
+def test_host_buffer_chunked_path(engine):
+    """cg_verify_batch on a batch large enough for the chunked H2D / verify pipeline: verdicts
+    equal the C oracle's, including items whose offsets point outside the arena (CG_NOT_RUN) in a
+    late chunk, and equal the single-copy fallback taken when the keys sit at the arena's end."""
+    from corda_amd.batch import Batch
+    from tools.workload import wl
+    b, _ = wl.ed25519_batch(200000, n_keys=4096, msg_len=120, corrupt_permille=100, seed=51, nthreads=16)
+    items = b.items.copy()
+    items[190000]["msg_off"] = b.arena.size + 7
+    items[199999]["sig_off"] = b.arena.size - 10
+    b = Batch(b.keys, items, b.arena)
+    st = engine.verify(b, B.MODE_DOVERIFY)
+    ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
+    assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
+    assert st[190000] == B.NOT_RUN and st[199999] == B.NOT_RUN
+    # keys moved behind the items: one copy, same verdicts
+    kb = np.concatenate([b.arena, np.zeros((-b.arena.size) % 4, np.uint8)])
+    keys = b.keys.copy()
+    parts = [kb]
+    off = kb.size
+    for j in range(len(keys)):
+        o, n = int(keys[j]["off"]), int(keys[j]["len"])
+        parts.append(b.arena[o:o + n])
+        keys[j]["off"] = off
+        off += n
+    b2 = Batch(keys, items, np.concatenate(parts + [np.zeros(64, np.uint8)]))
+    st2 = engine.verify(b2, B.MODE_DOVERIFY)
+    assert np.array_equal(st2[:190000], st[:190000]) and np.array_equal(st2[190001:199999], st[190001:199999])
+
+
 def test_edge_batches(engine):
     from corda_amd.batch import BatchBuilder
     items = golden_io.load("ed25519.json")

@@ -68,6 +68,7 @@ union BaseSlot {
 #define PLAN_R1 1
 #define PLAN_K1 2
 #define PLAN_CLASSES 3
+#define PLAN_FULL 4  // ranges[PLAN_FULL + c]: first item of class c whose key has full tables
 struct Plan {
   const uint32_t* perm;    // plan position -> item index
   const uint32_t* ranges;  // class c occupies positions [ranges[c], ranges[c + 1])
@@ -97,7 +98,8 @@ struct KeyWs {
 };
 
 // How much table a key gets, from the number of items that use it in the batch (one-shot entry
-// points estimate it from every KEY_USES_SAMPLE-th item, plus an exact "used at all" flag;
+// points estimate it from a hashed 1-in-KEY_USES_SAMPLE sample of the items, plus an exact
+// "used at all" flag;
 // cg_prepare_keys_device cannot, and builds every key in full). The mode changes only speed,
 // never a verdict: both ladders compute the same point.
 //   0 uses                        decode only (Abyte, status), no rows
@@ -107,7 +109,7 @@ struct KeyWs {
 // Break-even (measured on MI355X, 2^20 Ed25519 items): a key's full tables cost ~230 ns of
 // GPU time, the row-0 ladder ~7 ns more per item than the full-table one -> ~32 items.
 #define KEY_USES_ALL 0xffffffffu
-#define KEY_USES_SAMPLE 4u
+#define KEY_USES_SAMPLE 4u  // k_key_uses samples by the top 2 bits of a 32-bit hash: 1 in 4
 #ifndef ED_DIRECT_MAX_USES
 #define ED_DIRECT_MAX_USES 32u
 #endif

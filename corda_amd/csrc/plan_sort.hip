@@ -54,16 +54,19 @@ __global__ void __launch_bounds__(256) k_plan_keys(const cg_item* __restrict__ i
 
 __global__ void k_plan_ranges(const uint32_t* __restrict__ skey, uint64_t n_items, uint32_t kb,
                               uint32_t* __restrict__ ranges) {
-  const uint32_t c = threadIdx.x;
-  if (c > PLAN_CLASSES) return;
-  const uint32_t target = c << kb;
+  // lanes 0..3: class starts ranges[c] (ranges[3] = end of the verified classes); lanes 4..6:
+  // ranges[PLAN_FULL + c] = first full-table item of class c (the mode bit, keyws.h)
+  const uint32_t t = threadIdx.x;
+  if (t > PLAN_CLASSES + PLAN_CLASSES) return;
+  const uint32_t c = t <= PLAN_CLASSES ? t : t - PLAN_CLASSES - 1;
+  const uint32_t target = t <= PLAN_CLASSES ? c << kb : (c << kb) | (1u << (kb - 1));
   uint64_t lo = 0, hi = n_items;  // first position with key >= target
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
     if (skey[mid] < target) lo = mid + 1;
     else hi = mid;
   }
-  ranges[c] = (uint32_t)lo;
+  ranges[t <= PLAN_CLASSES ? c : PLAN_FULL + c] = (uint32_t)lo;
 }
 
 size_t plan_sort_temp_bytes(uint64_t n_items) {

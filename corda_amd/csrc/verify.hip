@@ -26,7 +26,7 @@ __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_item
     status[i] = CG_UNSUPPORTED;
 }
 
-// Per-key use counts, sampled: every KEY_USES_SAMPLE-th item adds KEY_USES_SAMPLE (no-return
+// Per-key use counts, sampled: one item in KEY_USES_SAMPLE adds KEY_USES_SAMPLE (no-return
 // atomics, a quarter of the traffic of counting all), every item marks its key as used (plain
 // stores: the exact "has items" bit row 0 depends on). Out-of-range key indices are
 // k_misc_status's (CG_NOT_RUN) and count nowhere.
@@ -47,7 +47,9 @@ __global__ void __launch_bounds__(256) k_key_uses(const cg_item* __restrict__ it
   const uint32_t k = items[i].key_idx;
   if (k >= n_keys) return;
   seen[k] = 1;
-  if (i % KEY_USES_SAMPLE == 0) atomicAdd(&uses[k], KEY_USES_SAMPLE);
+  // sample by a multiplicative hash of the index, not i % 4: a batch whose items cycle through
+  // the keys with a stride (item j -> key j % n) would otherwise alias whole keys out
+  if (((uint32_t)i * 0x9E3779B1u) >> 30 == 0) atomicAdd(&uses[k], KEY_USES_SAMPLE);
 }
 
 // Keys that get full tables (uses >= ED_DIRECT_MAX_USES), compacted per scheme class with one

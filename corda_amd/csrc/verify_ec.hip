@@ -154,21 +154,25 @@ __global__ void __launch_bounds__(256) k_ec_inv(const uint32_t* __restrict__ per
   ecdsa_batch_inv<C, EC_INV_K>(ws + base, cnt, sel, c_ec[C]);
 }
 
-template <int C>
+// Two launches over the curve's range, one per table mode (the plan keeps the modes in separate
+// waves, so a lane of the other mode exits with its whole wave); separate kernels keep the
+// full-table ladder's register allocation (3 waves/SIMD) free of the row-0 variant's.
+template <int C, bool Full>
 __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
                                                    const uint32_t* __restrict__ ranges,
-                                                   const uint32_t* __restrict__ uses,
                                                    const TabSlot* __restrict__ tabs,
                                                    const EcGTab* __restrict__ gtab, uint8_t* __restrict__ status,
                                                    const EcItemWs* __restrict__ ws) {
-  EC_RANGE(C);
+  const int cls = plan_class_of_curve(C);  // the plan's mode split (plan_sort.hip)
+  const uint32_t beg = Full ? ranges[PLAN_FULL + cls] : ranges[cls];
+  const uint32_t end = Full ? ranges[cls + 1] : ranges[PLAN_FULL + cls];
   const uint64_t p = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= end) return;
   const uint32_t i = perm[p];
   if (status[i] != EC_PENDING_BASE + C) return;
-  const EcItemWs w = ws[p];
   const uint32_t key = items[i].key_idx;
-  if (uses[key] >= ED_DIRECT_MAX_USES) {
+  const EcItemWs w = ws[p];
+  if (Full) {
     status[i] = (uint8_t)ecdsa_ladder_check<C>(w.a, w.b, w.r, *gtab, tabs[key].ec, c_ec[C]);
   } else {  // a key with few items: row 0 only (keyws.h)
     status[i] = (uint8_t)ecdsa_ladder_check_row0<C>(w.a, w.b, w.r, *gtab, tabs[key].ec.t[0], c_ec[C]);
@@ -234,8 +238,10 @@ static void launch_ladder(const cg_item* d_items, uint64_t n_items, uint8_t* d_s
   if (ready) hipStreamWaitEvent(stream, ready, 0);
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
-  hipLaunchKernelGGL(k_ec_ladder<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
-                     (const uint32_t*)w.uses, w.tab, gtab(d_btab, C), d_status, (const EcItemWs*)iw.slots);
+  hipLaunchKernelGGL((k_ec_ladder<C, true>), dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
+                     w.tab, gtab(d_btab, C), d_status, (const EcItemWs*)iw.slots);
+  hipLaunchKernelGGL((k_ec_ladder<C, false>), dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
+                     w.tab, gtab(d_btab, C), d_status, (const EcItemWs*)iw.slots);
 }
 
 // prep + inversion of both curves first (they need only the decoded keys), then the ladders,

@@ -284,12 +284,18 @@ struct PickGlobal {
 // One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the per-key rows and the
 // constant radix-2^10 B table (both in global memory; the B table stays L2-resident), left
 // projective in the item slot.
+// Two launches over the Ed25519 range, one per table mode (the plan keeps the modes in separate
+// waves); separate kernels keep the full-table ladder's registers free of the row-0 variant's.
+template <bool Full>
 __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
-    const EdKeyHdr* __restrict__ hdr, const uint32_t* __restrict__ uses, const TabSlot* __restrict__ tabs,
-    const EdBTab* __restrict__ btab, uint8_t* __restrict__ status, void* __restrict__ slots) {
-  const uint64_t p = (uint64_t)ranges[PLAN_ED] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= ranges[PLAN_ED + 1]) return;
+    const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBTab* __restrict__ btab,
+    uint8_t* __restrict__ status, void* __restrict__ slots) {
+  // the plan's mode split: row-0 keys' items first, then full-table keys' (plan_sort.hip)
+  const uint32_t beg = Full ? ranges[PLAN_FULL + PLAN_ED] : ranges[PLAN_ED];
+  const uint32_t end = Full ? ranges[PLAN_ED + 1] : ranges[PLAN_FULL + PLAN_ED];
+  const uint64_t p = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= end) return;
   const uint32_t i = perm[p];
   const uint32_t key = items[i].key_idx;
   if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
@@ -299,7 +305,7 @@ __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
   if (status[i] != ED_PENDING) return;
   const EdDigits d = ((const EdDigits*)slots)[p];
   ge_p2 q;
-  if (uses[key] >= ED_DIRECT_MAX_USES) {
+  if (Full) {
     ed_double_scalar_wb<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed, *btab, PickGlobal(), PickGlobal());
   } else {  // a key with few items: row 0 only (keyws.h)
     ed_double_scalar_row0<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed.t[0], *btab, PickGlobal(), PickGlobal());
@@ -397,8 +403,10 @@ void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_ite
   hipLaunchKernelGGL(k_ed_hash, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
                      arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
   if (tables_ready) hipStreamWaitEvent(stream, tables_ready, 0);
-  hipLaunchKernelGGL(k_ed_ladder, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                     (const uint32_t*)w.uses, w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+  hipLaunchKernelGGL(k_ed_ladder<true>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
+                     w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+  hipLaunchKernelGGL(k_ed_ladder<false>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
+                     w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
   const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
   hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
                      arena_len, d_status, (const ge_p2*)iw.slots);

@@ -21,12 +21,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def per_kernel_kb(path):
+    """Average KB per launch of each kernel; template instances (k_ed_ladder<true> / <false>, the
+    two table modes, both launched every step) are summed under the kernel's base name."""
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0]
+        full = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        name = full.split("<")[0]
         if name in KERNELS:
-            acc[name].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+            acc[(name, full)].append(float(r["Counter_Value"]))
+    out = collections.defaultdict(float)
+    for (name, _), v in acc.items():
+        out[name] += sum(v) / len(v)
+    return dict(out)
 
 
 def main():

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${1:-v}
 OUT=gpurun_out/prof_r01_$TAG
 mkdir -p $OUT
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --ecdsa-items 0 --mixed-items 0 --pipeline-txs 0"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --ecdsa-items 0 --mixed-items 0 --pipeline-txs 0 --tear-offs 0 --host-buffers 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $B > $OUT/trace.log 2>&1
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- $B > $OUT/fetch.log 2>&1
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- $B > $OUT/write.log 2>&1

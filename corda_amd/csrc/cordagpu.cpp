@@ -70,7 +70,8 @@ struct DevBuf {
 struct cg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  cg::Fork fork = {{nullptr, nullptr, nullptr}, nullptr, {nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+  cg::Fork fork = {{nullptr, nullptr, nullptr}, nullptr, {nullptr, nullptr}, {nullptr, nullptr, nullptr}, nullptr,
+                   {nullptr, nullptr, nullptr}};
   std::mutex mu;
   DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
   // transaction pipeline: verify items, spliced messages, templates; host-entry staging
@@ -123,6 +124,8 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   for (int k = 0; k < 2 && e == hipSuccess; ++k)
     e = hipEventCreateWithFlags(&c->fork.ec_decoded[k], hipEventDisableTiming);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.ready[k], hipEventDisableTiming);
+  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.row0[k], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.front, hipEventDisableTiming);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   for (int k = 0; k <= CG_H2D_CHUNKS && e == hipSuccess; ++k)
     e = hipEventCreateWithFlags(&c->seg[k], hipEventDisableTiming);
@@ -161,8 +164,10 @@ void cg_close(cg_ctx* c) {
       hipStreamDestroy(c->fork.side[k]);
     }
     if (c->fork.ready[k]) hipEventDestroy(c->fork.ready[k]);
+    if (c->fork.row0[k]) hipEventDestroy(c->fork.row0[k]);
   }
   if (c->fork.start) hipEventDestroy(c->fork.start);
+  if (c->fork.front) hipEventDestroy(c->fork.front);
   if (c->copy) {
     hipStreamSynchronize(c->copy);
     hipStreamDestroy(c->copy);

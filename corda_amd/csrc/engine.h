@@ -18,9 +18,13 @@ struct DeviceConsts;  // opaque
 // Key prep fork: side[0] / side[1] build the secp256r1 / secp256k1 keys (decode -> chain -> tab),
 // side[2] the Ed25519 keys; `start` orders them after the main stream's earlier work,
 // ec_decoded[c] / ready[c] are what the item kernels on the main stream wait for.
+// Item stages: the row-0 ladders (keys with few items, keyws.h) run on the side stream that
+// built their class's tables, after `front` (the hashes / ECDSA prep on the main stream), while
+// the main stream runs the full-table ladders; the main stream joins on row0[k]. A few row-0
+// waves (long: 252 doublings) then overlap the full-table launch instead of trailing it.
 struct Fork {
   hipStream_t side[3];
-  hipEvent_t start, ec_decoded[2], ready[3];
+  hipEvent_t start, ec_decoded[2], ready[3], front, row0[3];
 };
 
 // Upload the constant tables (curve constants, base-point tables) for the current device.

@@ -206,19 +206,24 @@ void ed_launch_key_abyte(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d
 // decode -> chain -> tab
 void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                               const KeyWs& w, hipStream_t stream);
-void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
-                     const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
-                     hipStream_t stream, hipEvent_t tables_ready);
+// item stages (verify.hip launch_items orders them across the main and side streams)
+void ed_launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
+                     uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len,
+                     const ItemWs& iw, hipStream_t stream);
+void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                      const ItemWs& iw, const void* d_btab, hipStream_t stream);
+void ed_launch_finish(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
+                      uint8_t* d_status, const ItemWs& iw, hipStream_t stream);
 hipError_t ec_upload_constants();
 hipError_t ec_init_const(void* d_btab, hipStream_t stream);
 // decode (records `decoded`: k_ec_prep needs the key status) -> chain -> tab, per curve
 void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                        const KeyWs& w, hipStream_t stream_r1, hipStream_t stream_k1, hipEvent_t decoded_r1,
                        hipEvent_t decoded_k1);
-void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
-                     const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
-                     hipStream_t stream, const hipEvent_t decoded[2], const hipEvent_t ready[2]);
+void ec_launch_front(int curve, const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena,
+                     uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs,
+                     uint64_t msgs_len, const ItemWs& iw, hipStream_t stream);
+void ec_launch_ladder(int curve, bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status,
+                      const KeyWs& w, const ItemWs& iw, const void* d_btab, hipStream_t stream);
 
 }  // namespace cg

@@ -232,32 +232,33 @@ static void launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t
                      (const uint8_t*)d_status, ws);
 }
 
-template <int C>
-static void launch_ladder(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
-                          const ItemWs& iw, const void* d_btab, hipStream_t stream, hipEvent_t ready) {
-  if (ready) hipStreamWaitEvent(stream, ready, 0);
+void ec_launch_front(int curve, const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena,
+                     uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs,
+                     uint64_t msgs_len, const ItemWs& iw, hipStream_t stream) {
+  if (curve == CG_CURVE_R1)
+    launch_front<CG_CURVE_R1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
+  else
+    launch_front<CG_CURVE_K1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
+}
+
+template <int C, bool Full>
+static void launch_ladder_t(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                            const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
-  hipLaunchKernelGGL((k_ec_ladder<C, true>), dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
-                     w.tab, gtab(d_btab, C), d_status, (const EcItemWs*)iw.slots);
-  hipLaunchKernelGGL((k_ec_ladder<C, false>), dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
+  hipLaunchKernelGGL((k_ec_ladder<C, Full>), dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
                      w.tab, gtab(d_btab, C), d_status, (const EcItemWs*)iw.slots);
 }
 
-// prep + inversion of both curves first (they need only the decoded keys), then the ladders,
-// each after its curve's key tables are ready (events null: everything is on `stream`)
-void ec_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
-                     const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
-                     hipStream_t stream, const hipEvent_t decoded[2], const hipEvent_t ready[2]) {
-  (void)d_keys;
-  (void)n_keys;
-  if (decoded && decoded[0]) hipStreamWaitEvent(stream, decoded[0], 0);
-  launch_front<CG_CURVE_R1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
-  if (decoded && decoded[1]) hipStreamWaitEvent(stream, decoded[1], 0);
-  launch_front<CG_CURVE_K1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
-  launch_ladder<CG_CURVE_R1>(d_items, n_items, d_status, w, iw, d_btab, stream, ready ? ready[0] : nullptr);
-  launch_ladder<CG_CURVE_K1>(d_items, n_items, d_status, w, iw, d_btab, stream, ready ? ready[1] : nullptr);
+void ec_launch_ladder(int curve, bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status,
+                      const KeyWs& w, const ItemWs& iw, const void* d_btab, hipStream_t stream) {
+  if (curve == CG_CURVE_R1) {
+    if (full) launch_ladder_t<CG_CURVE_R1, true>(d_items, n_items, d_status, w, iw, d_btab, stream);
+    else launch_ladder_t<CG_CURVE_R1, false>(d_items, n_items, d_status, w, iw, d_btab, stream);
+  } else {
+    if (full) launch_ladder_t<CG_CURVE_K1, true>(d_items, n_items, d_status, w, iw, d_btab, stream);
+    else launch_ladder_t<CG_CURVE_K1, false>(d_items, n_items, d_status, w, iw, d_btab, stream);
+  }
 }
 
 }  // namespace cg

@@ -392,21 +392,30 @@ void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const uint8
                      w.ecs);
 }
 
-void ed_launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
-                     const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w,
-                     const uint8_t* d_msgs, uint64_t msgs_len, const ItemWs& iw, const void* d_btab,
-                     hipStream_t stream, hipEvent_t tables_ready) {
-  (void)d_keys;
-  (void)n_keys;
+void ed_launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
+                     uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len,
+                     const ItemWs& iw, hipStream_t stream) {
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;  // the Ed25519 range is at most n_items long
   hipLaunchKernelGGL(k_ed_hash, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
                      arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
-  if (tables_ready) hipStreamWaitEvent(stream, tables_ready, 0);
-  hipLaunchKernelGGL(k_ed_ladder<true>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                     w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
-  hipLaunchKernelGGL(k_ed_ladder<false>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                     w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+}
+
+void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                      const ItemWs& iw, const void* d_btab, hipStream_t stream) {
+  const uint32_t B = 256;
+  const uint64_t grid = (n_items + B - 1) / B;
+  if (full)
+    hipLaunchKernelGGL(k_ed_ladder<true>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
+                       w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+  else
+    hipLaunchKernelGGL(k_ed_ladder<false>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
+                       w.hdr, w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+}
+
+void ed_launch_finish(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
+                      uint8_t* d_status, const ItemWs& iw, hipStream_t stream) {
+  const uint32_t B = 256;
   const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
   hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
                      arena_len, d_status, (const ge_p2*)iw.slots);

@@ -255,7 +255,9 @@ CG_HD int sc_digit_h(const uint32_t* packed, int t) {
 
 // R' = h (-A) + S' B: A over the per-key W/K rows, B over the WB table; left projective.
 // `Pick(out, row, digit)` loads a signed niels entry (identity for 0) from either table.
-template <int W, int K, int WB, class RowA, class TabB, class PickA, class PickB>
+// Signed = true: entries are picked by |digit| and the sign goes through ge_madd_signed (the
+// form k_ed_ladder_pf runs; the host tests run it with bounds checks).
+template <int W, int K, int WB, bool Signed = false, class RowA, class TabB, class PickA, class PickB>
 CG_HD void ed_double_scalar_wb(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const RowA& TA, const TabB& TB,
                                PickA pick_a, PickB pick_b) {
   typedef EdRowsCfg<W, K> C;
@@ -278,12 +280,18 @@ CG_HD void ed_double_scalar_wb(ge_p2& out, const uint32_t* eh, const uint32_t* e
     const int n_ops = n_a + (u_hi - u_lo);
     for (int k = 0; k < n_ops; ++k) {
       ge_niels n;
+      const int dg = k < n_a ? sc_digit_b(eh, K * k + i) : sc_digit_h(esb, u_lo + k - n_a);
+      const int dp = Signed && dg < 0 ? -dg : dg;
       if (k < n_a) {
-        pick_a(n, TA.t[k], sc_digit_b(eh, K * k + i));
+        pick_a(n, TA.t[k], dp);
       } else {
-        pick_b(n, TB.t[u_lo + k - n_a], sc_digit_h(esb, u_lo + k - n_a));
+        pick_b(n, TB.t[u_lo + k - n_a], dp);
       }
-      ge_madd(t, R, n);
+      if (Signed) {
+        ge_madd_signed(t, R, n, dg < 0);
+      } else {
+        ge_madd(t, R, n);
+      }
       if (k + 1 == n_ops) {
         ge_p1p1_to_p2(q, t);  // next: doublings (or the end), which need no T
       } else {

@@ -26,15 +26,18 @@ struct ge_niels {  // affine (y+x, y-x, 2dxy), all tight
   fe ypx, ymx, xy2d;
 };
 
+// Operand order shares work between the products: fe_mul(f, g) scales g by 19 and doubles
+// f's odd limbs, so Y = Z * Y and Z = Z * T share f = Z, and X = X * T shares g = T with it.
 CG_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
   fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Y, p.Z, p.Y);
   fe_mul(r.Z, p.Z, p.T);
 }
 
+// (shared operands: g = T for X and Z, g = Y for Y and T, f = X for X and T, f = Z for Y and Z)
 CG_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
   fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Y, p.Z, p.Y);
   fe_mul(r.Z, p.Z, p.T);
   fe_mul(r.T, p.X, p.Y);
 }
@@ -98,6 +101,42 @@ CG_HD void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_niels& q) {
   fe_copy(r.X, r.Z);
   fe_add(r.Z, d, c);
   fe_sub(r.T, d, c);
+  fe_carry(r.T);
+}
+
+// r = p + (-1)^neg q for an affine niels q, without negating q (ge_niels_cneg costs a negation,
+// a carry pass and 30 swaps). With neg, a = Y+X and b = Y-X trade multiplicands, which
+// leaves (Y'-X', X'+Y') for the negated sum's (X'-Y', X'+Y'); the sign goes to Z instead
+// (x = X/Z), and the xy2d product's sign flips Z and T:
+//   neg = 0: (X'-Y', X'+Y', d + c, d - c)     neg = 1: (Y'-X' = -(X'-Y'), X'+Y', c - d, d + c)
+// Bounds: Z <= 5 tight (c + 4p - d), so the next product must take Z as its first operand
+// (ge_p1p1_to_p2 / _p3 do); T is carried (tight).
+CG_HD void ge_madd_signed(ge_p1p1& r, const ge_p3& p, const ge_niels& q, bool neg) {
+  fe a, b, c, d;
+  fe_add(a, p.Y, p.X);
+  fe_sub(b, p.Y, p.X);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t ai = a.v[i], bi = b.v[i];
+    a.v[i] = neg ? bi : ai;
+    b.v[i] = neg ? ai : bi;
+  }
+  fe_mul(r.X, a, q.ypx);
+  fe_mul(r.Y, b, q.ymx);
+  fe_mul(c, q.xy2d, p.T);
+  fe_add(d, p.Z, p.Z);
+  fe_sub(r.Z, r.X, r.Y);
+  fe_add(r.Y, r.X, r.Y);
+  fe_copy(r.X, r.Z);
+  fe s, e, ne;
+  fe_add(s, d, c);
+  fe_sub(e, d, c);
+  fe_sub4(ne, c, d);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    r.Z.v[i] = neg ? ne.v[i] : s.v[i];
+    r.T.v[i] = neg ? s.v[i] : e.v[i];
+  }
   fe_carry(r.T);
 }
 

@@ -5,9 +5,10 @@
 //   k_ed_keyprep_tab     one lane per (key, row): the 32 affine multiples of the row base
 //   k_ed_hash            one lane per item: SHA-512 challenge, scalar prep, signed digits
 //                        (needs only Abyte: overlaps the whole key decode + table build)
-//   k_ed_ladder          one lane per item: key status, then 2 windows x (~21.5 rows of -A +
-//                        13 rows of the radix-2^10 B table) mixed additions, 6 doublings; for a
-//                        key with few items in the batch, row 0 of -A and 252 doublings
+//   k_ed_ladder_pf       one lane per item of a full-table key: key status, then 2 windows x
+//                        (~21.5 rows of -A + 13 rows of the radix-2^10 B table) mixed additions,
+//                        6 doublings; each op's table entry gathered into LDS one op ahead
+//   k_ed_ladder<false>   a key with few items in the batch: row 0 of -A and 252 doublings
 //                        (keyws.h ED_DIRECT_MAX_USES)
 //   k_ed_finish          16 items per lane: batch inversion, encode, byte compare
 // Replaces, per item, i2p EdDSAEngine.engineVerify behind Crypto.isValid
@@ -281,6 +282,167 @@ struct PickGlobal {
 #ifndef ED_LADDER_WAVES_PER_SIMD
 #define ED_LADDER_WAVES_PER_SIMD 3  // 168 VGPRs: 3 waves/SIMD beat 2 (measured, r01)
 #endif
+
+// ---------------------------------------------------------------- pipelined full-table ladder
+// The 69 mixed additions of ed_double_scalar_wb as one flat op sequence (window 1: 21 A rows +
+// B rows 13..25; 6 doublings; window 0: 22 A rows + B rows 0..12). Op o+1's niels entry is
+// gathered straight into LDS (global_load_lds, no VGPR destination) while op o's addition
+// runs, and op o+2's digit word is loaded at the same time: the two dependent memory latencies
+// per op (digit, then entry) leave the critical path. LDS image per wave: 7 x 16-B chunks then
+// 2 x 4-B chunks, chunk c of lane l at wave_base + 64 * off_c + size_c * l (the DMA's
+// lane-linear destination), 7680 B per wave. Only the 16-B and 4-B DMA forms are used: a
+// first cut with 12-B chunks read back wrong entries.
+typedef __attribute__((address_space(3))) void* cg_lds_ptr;
+typedef __attribute__((address_space(1))) void* cg_gbl_ptr;
+
+struct EdOps {
+  static constexpr int kNa1 = (EdCfg::kDigits - 1 + ED_K - 1) / ED_K;  // A rows, window 1
+  static constexpr int kNa0 = (EdCfg::kDigits + ED_K - 1) / ED_K;      // A rows, window 0
+  static constexpr int kUlo1 = (EdBCfgT::kDigits + ED_K - 1) / ED_K;   // B rows [kUlo1, kDigits): window 1
+  static constexpr int kOps1 = kNa1 + (EdBCfgT::kDigits - kUlo1);
+  static constexpr int kOps = kOps1 + kNa0 + kUlo1;
+  static constexpr uint32_t kWaveBytes = 64 * sizeof(ge_niels);
+};
+static_assert(ED_K == 2, "the flat op sequence is written for 2 windows");
+static_assert(sizeof(ge_niels) == 120, "LDS chunking assumes 120-B niels entries");
+
+// op o -> (digit word index in EdDigits, shift, B?, row)
+__device__ __forceinline__ void ed_op_info(int o, int& widx, int& sh, bool& is_b, int& row) {
+  const bool w1 = o < EdOps::kOps1;
+  const int k = w1 ? o : o - EdOps::kOps1;
+  const int n_a = w1 ? EdOps::kNa1 : EdOps::kNa0;
+  if (k < n_a) {
+    const int t = ED_K * k + (w1 ? 1 : 0);
+    widx = t >> 2;
+    sh = (t & 3) * 8;
+    is_b = false;
+    row = k;
+  } else {
+    const int u = (w1 ? EdOps::kUlo1 : 0) + k - n_a;
+    widx = EdCfg::kPackedWords + (u >> 1);
+    sh = (u & 1) * 16;
+    is_b = true;
+    row = u;
+  }
+}
+
+__device__ __forceinline__ int ed_op_digit(uint32_t w, int sh, bool is_b) {
+  return is_b ? (int)(int16_t)(uint16_t)(w >> sh) : (int)(int8_t)(uint8_t)(w >> sh);
+}
+
+__device__ __forceinline__ void ed_glds_niels(const ge_niels* src, uint8_t* wave_lds) {
+  const uint8_t* s = (const uint8_t*)src;
+#pragma unroll
+  for (int c = 0; c < 7; ++c)
+    __builtin_amdgcn_global_load_lds((cg_gbl_ptr)(s + 16 * c), (cg_lds_ptr)(wave_lds + 64 * 16 * c), 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((cg_gbl_ptr)(s + 112), (cg_lds_ptr)(wave_lds + 64 * 112), 4, 0, 0);
+  __builtin_amdgcn_global_load_lds((cg_gbl_ptr)(s + 116), (cg_lds_ptr)(wave_lds + 64 * 116), 4, 0, 0);
+}
+
+__device__ __forceinline__ void ed_lds_niels(ge_niels& n, const uint8_t* wave_lds, uint32_t lane) {
+  uint32_t* d = (uint32_t*)&n;
+#pragma unroll
+  for (int c = 0; c < 7; ++c) {
+    const uint4 v = *(const uint4*)(wave_lds + 64 * 16 * c + 16 * lane);
+    d[4 * c] = v.x;
+    d[4 * c + 1] = v.y;
+    d[4 * c + 2] = v.z;
+    d[4 * c + 3] = v.w;
+  }
+  d[28] = *(const uint32_t*)(wave_lds + 64 * 112 + 4 * lane);
+  d[29] = *(const uint32_t*)(wave_lds + 64 * 116 + 4 * lane);
+}
+
+__device__ __forceinline__ const ge_niels* ed_op_src(const EdTab& TA, const EdBTab& TB, bool is_b, int row, int d) {
+  const int a = d < 0 ? -d : d;
+  const int idx = a > 0 ? a - 1 : 0;
+  return is_b ? &TB.t[row][idx] : &TA.t[row][idx];
+}
+
+__device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* __restrict__ dw, const EdTab& TA,
+                                                    const EdBTab& TB, uint8_t* wave_lds, uint32_t lane) {
+  constexpr int N = EdOps::kOps;
+  int widx, sh, row;
+  bool is_b;
+  // prologue: op 0's digit and entry, op 1's digit word
+  ed_op_info(0, widx, sh, is_b, row);
+  int d_cur = ed_op_digit(dw[widx], sh, is_b);
+  ed_glds_niels(ed_op_src(TA, TB, is_b, row, d_cur), wave_lds);
+  ed_op_info(1, widx, sh, is_b, row);
+  uint32_t w_next = dw[widx];
+  ge_p3 R;
+  ge_p3_0(R);
+  ge_p1p1 t;
+  ge_p2 q;
+  for (int o = 0; o < N; ++o) {
+    if (o == EdOps::kOps1) {  // window 1 -> 0: W doublings while op o's entry is in flight
+      for (int d = 0; d < ED_W - 1; ++d) {
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+      }
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(R, t);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // op o's entry and op o+1's digit word
+    ge_niels n;
+    ed_lds_niels(n, wave_lds, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
+    if (d_cur == 0) ge_niels_identity(n);
+    const bool neg = d_cur < 0;  // the sign goes through the addition, not the entry
+    if (o + 1 < N) {
+      ed_op_info(o + 1, widx, sh, is_b, row);
+      d_cur = ed_op_digit(w_next, sh, is_b);
+      ed_glds_niels(ed_op_src(TA, TB, is_b, row, d_cur), wave_lds);
+      if (o + 2 < N) {
+        ed_op_info(o + 2, widx, sh, is_b, row);
+        w_next = dw[widx];
+      }
+    }
+    ge_madd_signed(t, R, n, neg);
+    if (o + 1 == N || o + 1 == EdOps::kOps1) {
+      ge_p1p1_to_p2(q, t);
+    } else {
+      ge_p1p1_to_p3(R, t);
+    }
+  }
+  out = q;
+}
+
+// A/B on one box (gpurun_out/ab_sw1, profiles/r01/ed25519_v9): the pipelined ladder at 2
+// waves/SIMD (216 VGPRs, no scratch) against k_ed_ladder<true> at 3 waves/SIMD (168 VGPRs,
+// digits and spills in scratch): item kernels 4.24 vs 4.28 ms per 2^20 items. The gain is
+// small because the ladder is VALU-issue-bound, not latency-bound.
+// -DED_LADDER_PF=0 builds the unpipelined ladder for A/B runs (tools/ab.sh).
+#ifndef ED_LADDER_PF
+#define ED_LADDER_PF 1
+#endif
+#ifndef ED_LADDER_PF_WAVES
+#define ED_LADDER_PF_WAVES 2
+#endif
+__global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_pf(
+    const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
+    const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBTab* __restrict__ btab,
+    uint8_t* __restrict__ status, void* __restrict__ slots) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4 * EdOps::kWaveBytes];
+  const uint32_t beg = ranges[PLAN_FULL + PLAN_ED];
+  const uint32_t end = ranges[PLAN_ED + 1];
+  const uint64_t p = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= end) return;
+  const uint32_t i = perm[p];
+  const uint32_t key = items[i].key_idx;
+  if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
+    status[i] = CG_KEY_INVALID;
+    return;
+  }
+  if (status[i] != ED_PENDING) return;
+  // every lane still here runs the same DMA sequence; lanes that left do not take part, and
+  // the LDS image is per lane, so no barrier is needed
+  uint8_t* wave_lds = stage + (threadIdx.x >> 6) * EdOps::kWaveBytes;
+  ge_p2 q;
+  ed_double_scalar_pf(q, (const uint32_t*)((const uint8_t*)slots + (size_t)p * ITEM_SLOT), tabs[key].ed, *btab,
+                      wave_lds, __lane_id());
+  ((ge_p2*)slots)[p] = q;
+}
 // One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the per-key rows and the
 // constant radix-2^10 B table (both in global memory; the B table stays L2-resident), left
 // projective in the item slot.
@@ -405,8 +567,11 @@ void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8
                       const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
-  if (full)
-    hipLaunchKernelGGL(k_ed_ladder<true>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
+  if (full && ED_LADDER_PF)
+    hipLaunchKernelGGL(k_ed_ladder_pf, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
+                       w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+  else if (full)
+    hipLaunchKernelGGL(k_ed_ladder<true>,dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
                        w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
   else
     hipLaunchKernelGGL(k_ed_ladder<false>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,

@@ -360,8 +360,9 @@ static void tb10_init() {
 }
 static void host_pick(ge_niels& out, const ge_niels* row, int d) { ed_pick_w(out, row, d); }
 
-extern "C" int t_ed_verify_wb(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len,
-                              uint64_t* counts) {
+template <bool Signed>
+static int ed_verify_wb(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len,
+                        uint64_t* counts) {
   init();
   tb10_init();
   typedef EdRowsCfg<ED_W, ED_K> C;
@@ -398,7 +399,7 @@ extern "C" int t_ed_verify_wb(const uint32_t* aw, const uint32_t* sw, const uint
 #ifdef FE_OP_COUNT
   g_fe_nmul = g_fe_nsq = 0;
 #endif
-  ed_double_scalar_wb<ED_W, ED_K, ED_WB>(R, eh, es, TA, *g_TB10, host_pick, host_pick);
+  ed_double_scalar_wb<ED_W, ED_K, ED_WB, Signed>(R, eh, es, TA, *g_TB10, host_pick, host_pick);
 #ifdef FE_OP_COUNT
   if (counts) {
     counts[0] = g_fe_nmul;
@@ -408,4 +409,15 @@ extern "C" int t_ed_verify_wb(const uint32_t* aw, const uint32_t* sw, const uint
   fe zi;
   fe_invert(zi, R.Z);
   return ed_encode_cmp(R, zi, sw);
+}
+
+extern "C" int t_ed_verify_wb(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len,
+                              uint64_t* counts) {
+  return ed_verify_wb<false>(aw, sw, msg, msg_len, counts);
+}
+
+// the signed-addition form of k_ed_ladder_pf (ge_madd_signed), bounds-checked
+extern "C" int t_ed_verify_wb_signed(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len,
+                                     uint64_t* counts) {
+  return ed_verify_wb<true>(aw, sw, msg, msg_len, counts);
 }

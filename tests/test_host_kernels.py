@@ -171,18 +171,22 @@ def test_ed25519_row_table_lane_verify_on_fixtures(w):
     assert n > 200
 
 
-def test_ed25519_wide_b_lane_verify_on_fixtures():
-    """k_ed_ladder's arithmetic: -A rows (W=6, K=4) + the radix-2^10 B table (ed25519_rows.h)."""
+@pytest.mark.parametrize("fn", ["t_ed_verify_wb", "t_ed_verify_wb_signed"])
+def test_ed25519_wide_b_lane_verify_on_fixtures(fn):
+    """k_ed_ladder's arithmetic: -A rows (W=6, K=2) + the radix-2^10 B table (ed25519_rows.h);
+    the _signed form is k_ed_ladder_pf's (entries by |digit|, sign through ge_madd_signed), with
+    every limb bound asserted."""
     import ctypes
     lib = hostk.lib()
-    lib.t_ed_verify_wb.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]
+    f = getattr(lib, fn)
+    f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]
     n = 0
     for it in golden_io.load("ed25519.json"):
         key, sig, msg = bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"])
         if it["key_fmt"] != 0 or len(key) != 32 or len(sig) != 64:
             continue
         m = np.frombuffer(msg + bytes(8), dtype=np.uint8).copy()
-        st = lib.t_ed_verify_wb(ptr(words(key)), ptr(words(sig)), ptr(m), len(msg), None)
+        st = f(ptr(words(key)), ptr(words(sig)), ptr(m), len(msg), None)
         got = {0: "VALID", 1: "INVALID", 3: "KEY_INVALID"}[st]
         assert got == it["expect_isvalid"], it["note"]
         n += 1

@@ -15,4 +15,4 @@ for round in 1 2; do
     CORDA_AMD_LIB=$v timeout -k 10 200 $B > $OUT/v${i}_$round.log 2>&1 || exit 1
   done
 done
-for f in $OUT/*.log; do echo "$f $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["kernel_ms"], *[(k, v["value"], v["kernel_ms"]) for k, v in d["secondary"].items()])')"; done
+python3 tools/ab_summary.py $OUT/*.log

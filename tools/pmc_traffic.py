@@ -21,12 +21,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def per_kernel_kb(path):
-    """Average KB per launch of each kernel; template instances (k_ed_ladder<true> / <false>, the
-    two table modes, both launched every step) are summed under the kernel's base name."""
+    """Average KB per launch of each kernel; the two table modes' ladders (k_ed_ladder_pf for
+    full-table keys, k_ed_ladder<false> for row-0 keys, both launched every step) are summed
+    under k_ed_ladder."""
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         full = r["Kernel_Name"].split("(")[0].replace("void ", "")
         name = full.split("<")[0]
+        if name.startswith("cg::k_ed_ladder"):  # k_ed_ladder_pf (full tables) + k_ed_ladder<false>
+            name = "cg::k_ed_ladder"
         if name in KERNELS:
             acc[(name, full)].append(float(r["Counter_Value"]))
     out = collections.defaultdict(float)

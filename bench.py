@@ -50,7 +50,7 @@ MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
 # kernel generation whose PMC traffic profile is committed (profiles/r01/pmc_traffic.json)
-KERNEL_VERSION = "ed25519_v9"
+KERNEL_VERSION = "ed25519_v10"
 
 
 def parse():
@@ -413,6 +413,8 @@ def main():
             tr = json.load(f)
         if tr.get("items") == n_items and tr.get("kernel_version") == KERNEL_VERSION:
             roof["traffic"] = tr.get("hbm_bytes_per_launch")
+            if "valu_issue" in tr:  # PMC SQ pass of the same build: issue-slot occupancy per kernel
+                roof["valu_issue"] = tr["valu_issue"]
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

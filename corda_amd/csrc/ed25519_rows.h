@@ -17,7 +17,9 @@
 // over a constant table (26 rows x 512).
 #define ED_W 6
 #define ED_K 2
+#ifndef ED_WB
 #define ED_WB 10
+#endif
 
 template <int W, int K>
 struct EdRowsCfg {

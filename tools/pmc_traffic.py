@@ -38,6 +38,28 @@ def per_kernel_kb(path):
     return dict(out)
 
 
+def valu_issue(path, items):
+    """VALU issue occupancy of the Ed25519 item kernels from the SQ pass (tools/profile_r01.sh):
+    VALU wave-instructions x 4 cycles (a wave64 VALU op holds a SIMD16 for 4 cycles) over the
+    SIMD-cycles the kernel ran (GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs). ~1.0
+    means the kernel is bound by instruction issue, whatever its MAC fraction."""
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        if name.startswith(("cg::k_ed_ladder_pf", "cg::k_ed_hash", "cg::k_ed_finish")):
+            acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for name, cs in acc.items():
+        m = {k: sum(v) / len(v) for k, v in cs.items()}
+        clk = m["GRBM_GUI_ACTIVE"] / 8
+        out[name.split("::")[1]] = {
+            "valu_insts_per_item": round(m["SQ_INSTS_VALU"] * 64 / items, 1),
+            "xcd_cycles": round(clk),
+            "issue_frac": round(m["SQ_INSTS_VALU"] * 4 / (1024 * clk), 3),
+            "wait_frac": round(m["SQ_WAIT_INST_ANY"] / m["SQ_WAVE_CYCLES"], 3)}
+    return out
+
+
 def main():
     prof, version, items, dest = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
     fetch = per_kernel_kb(os.path.join(prof, "fetch", "run_counter_collection.csv"))
@@ -60,6 +82,9 @@ def main():
                          "(MI355X_MICROARCH.md HBM): hbm = 2*FETCH_SIZE + WRITE_SIZE (KB*1024); "
                          "uncalibrated for 16-B table gathers, so an upper estimate",
            "hbm_bytes_per_launch": hbm, "kernel_version": version}
+    vpath = os.path.join(prof, "valu", "run_counter_collection.csv")
+    if os.path.exists(vpath):
+        out["valu_issue"] = valu_issue(vpath, items)
     with open(os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))

@@ -330,13 +330,18 @@ __device__ __forceinline__ int ed_op_digit(uint32_t w, int sh, bool is_b) {
   return is_b ? (int)(int16_t)(uint16_t)(w >> sh) : (int)(int8_t)(uint8_t)(w >> sh);
 }
 
-__device__ __forceinline__ void ed_glds_niels(const ge_niels* src, uint8_t* wave_lds) {
+// wave_lds_off: the wave's LDS image as a wave-uniform LDS byte offset (readfirstlane'd once
+// by the caller), so the per-chunk M0 values are scalar adds, not VALU readfirstlanes
+__device__ __forceinline__ cg_lds_ptr ed_lds_at(uint32_t wave_lds_off, uint32_t b) {
+  return (cg_lds_ptr)(uintptr_t)(wave_lds_off + b);
+}
+__device__ __forceinline__ void ed_glds_niels(const ge_niels* src, uint32_t wave_lds_off) {
   const uint8_t* s = (const uint8_t*)src;
 #pragma unroll
   for (int c = 0; c < 7; ++c)
-    __builtin_amdgcn_global_load_lds((cg_gbl_ptr)(s + 16 * c), (cg_lds_ptr)(wave_lds + 64 * 16 * c), 16, 0, 0);
-  __builtin_amdgcn_global_load_lds((cg_gbl_ptr)(s + 112), (cg_lds_ptr)(wave_lds + 64 * 112), 4, 0, 0);
-  __builtin_amdgcn_global_load_lds((cg_gbl_ptr)(s + 116), (cg_lds_ptr)(wave_lds + 64 * 116), 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((cg_gbl_ptr)(s + 16 * c), ed_lds_at(wave_lds_off, 64 * 16 * c), 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((cg_gbl_ptr)(s + 112), ed_lds_at(wave_lds_off, 64 * 112), 4, 0, 0);
+  __builtin_amdgcn_global_load_lds((cg_gbl_ptr)(s + 116), ed_lds_at(wave_lds_off, 64 * 116), 4, 0, 0);
 }
 
 __device__ __forceinline__ void ed_lds_niels(ge_niels& n, const uint8_t* wave_lds, uint32_t lane) {
@@ -362,12 +367,13 @@ __device__ __forceinline__ const ge_niels* ed_op_src(const EdTab& TA, const EdBT
 __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* __restrict__ dw, const EdTab& TA,
                                                     const EdBTab& TB, uint8_t* wave_lds, uint32_t lane) {
   constexpr int N = EdOps::kOps;
+  const uint32_t wl = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(cg_lds_ptr)wave_lds);
   int widx, sh, row;
   bool is_b;
   // prologue: op 0's digit and entry, op 1's digit word
   ed_op_info(0, widx, sh, is_b, row);
   int d_cur = ed_op_digit(dw[widx], sh, is_b);
-  ed_glds_niels(ed_op_src(TA, TB, is_b, row, d_cur), wave_lds);
+  ed_glds_niels(ed_op_src(TA, TB, is_b, row, d_cur), wl);
   ed_op_info(1, widx, sh, is_b, row);
   uint32_t w_next = dw[widx];
   ge_p3 R;
@@ -392,7 +398,7 @@ __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* 
     if (o + 1 < N) {
       ed_op_info(o + 1, widx, sh, is_b, row);
       d_cur = ed_op_digit(w_next, sh, is_b);
-      ed_glds_niels(ed_op_src(TA, TB, is_b, row, d_cur), wave_lds);
+      ed_glds_niels(ed_op_src(TA, TB, is_b, row, d_cur), wl);
       if (o + 2 < N) {
         ed_op_info(o + 2, widx, sh, is_b, row);
         w_next = dw[widx];

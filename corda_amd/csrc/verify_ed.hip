@@ -483,7 +483,9 @@ __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
 
 // Encode + compare for 16 consecutive items per lane: one inversion per lane (Montgomery's
 // trick) instead of one per item.
+#ifndef ED_FINISH_K
 #define ED_FINISH_K 16
+#endif
 __global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
                                                    const uint32_t* __restrict__ ranges,
                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,

@@ -50,7 +50,7 @@ MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
 # kernel generation whose PMC traffic profile is committed (profiles/r01/pmc_traffic.json)
-KERNEL_VERSION = "ed25519_v11"
+KERNEL_VERSION = "ed25519_v12"
 
 
 def parse():

@@ -219,7 +219,13 @@ static_assert(sizeof(EdDigits) == ITEM_SLOT, "digits must fill one item slot");
 // One lane per Ed25519 plan position: item checks, h = SHA-512(R || Abyte || M) mod L,
 // S' = i2p's slide value of S mod L, both recoded to signed radix-64 digits. Needs only the
 // decoded keys (Abyte), so it runs while the key tables are still being built.
-__global__ void __launch_bounds__(256) k_ed_hash(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
+// 3 waves/SIMD (168 VGPRs, 16 B of scratch) instead of 2 at 171 VGPRs: the hash shares the chip
+// with the key-table build, and the extra wave per SIMD raised the headline 208 -> 214 M sigs/s
+// (A/B, profiles/r01/ed25519_v12/ab_hash_waves)
+#ifndef ED_HASH_WAVES_PER_SIMD
+#define ED_HASH_WAVES_PER_SIMD 3
+#endif
+__global__ void __launch_bounds__(256, ED_HASH_WAVES_PER_SIMD) k_ed_hash(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
                                                  const uint32_t* __restrict__ ranges,
                                                  const EdKeyHdr* __restrict__ hdr,
                                                  const uint8_t* __restrict__ arena, uint64_t arena_len,

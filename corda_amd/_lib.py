@@ -30,7 +30,16 @@ class cg_stats(ctypes.Structure):
 
 class cg_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32), ("max_items", ctypes.c_uint64),
-                ("max_arena", ctypes.c_uint64)]
+                ("max_arena", ctypes.c_uint64), ("chunk_items", ctypes.c_uint64),
+                ("reserved", ctypes.c_uint64 * 3)]
+
+
+class cg_pool_stats(ctypes.Structure):
+    _fields_ = [("shards", ctypes.c_uint32), ("reruns", ctypes.c_uint32), ("failed_slots", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("not_run", ctypes.c_uint64), ("ms_total", ctypes.c_double)]
+
+
+ABI_VERSION = 2
 
 
 def declared_symbols():
@@ -75,6 +84,20 @@ def lib():
                                                         u32, vp, vp, vp, vp]
             L.cg_verify_filtered.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u64, vp]
             L.cg_verify_filtered_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u64, vp, vp]
+            pool = hasattr(L, "cg_pool_open")  # older builds (A/B variants) lack the pool
+            if pool:
+                L.cg_pool_open.argtypes = [ctypes.POINTER(vp), vp, u32, ctypes.POINTER(cg_config)]
+                L.cg_pool_open.restype = i32
+                L.cg_pool_close.argtypes = [vp]
+                L.cg_pool_close.restype = None
+                L.cg_pool_slots.argtypes = [vp]
+                L.cg_pool_slots.restype = u32
+                L.cg_pool_slot_healthy.argtypes = [vp, u32]
+                L.cg_pool_slot_healthy.restype = i32
+                L.cg_pool_verify_batch.argtypes = [vp, vp, u32, vp, u64, vp, u64, u32, vp, ctypes.POINTER(cg_pool_stats)]
+                L.cg_pool_verify_batch.restype = i32
+                L.cg_pool_inject_fault.argtypes = [vp, u32, i32]
+                L.cg_pool_inject_fault.restype = i32
             for name in ("cg_verify_filtered", "cg_verify_filtered_device", "cg_verify_transactions", "cg_verify_transactions_device", "cg_reserve", "cg_verify_batch", "cg_verify_batch_device", "cg_sha256_batch",
                          "cg_sha512_batch", "cg_sha256_batch_device", "cg_merkle_roots", "cg_tx_ids",
                          "cg_tx_ids_device"):

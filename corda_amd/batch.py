@@ -41,6 +41,75 @@ KEY_RAW, KEY_SPKI, KEY_SEC1 = 0, 1, 2
 MODE_DOVERIFY, MODE_ISVALID = 0, 1
 
 
+# cg_item.sig_len / cg_txsig.sig_len are 16 bits, cg_item.msg_len 32 bits (include/cordagpu.h).
+SIG_LEN_MAX = 0xFFFF
+MSG_LEN_MAX = 0xFFFFFFFF
+# A signature longer than SIG_LEN_MAX cannot be described to the engine. It is packed as a
+# short surrogate whose verdict is the one the JVM gives the real bytes, with the same
+# precedence (unsupported scheme, then key decode, then the signature):
+#   Ed25519: any length != 64 -> SignatureException("signature length is wrong") (SIG_MALFORMED)
+#   ECDSA:   BC 1.57 StdDSAEncoder.decode either rejects the DER (SIG_MALFORMED), or it is a
+#            canonical SEQUENCE{INTEGER r, INTEGER s}, and then one INTEGER has more than 32
+#            thousand content bytes: r or s is outside [1, n-1], isValid == false (INVALID).
+SIG_SURROGATE_MALFORMED = b"\x00"
+SIG_SURROGATE_INVALID = bytes.fromhex("3006020100020101")  # SEQUENCE{INTEGER 0, INTEGER 1}: r = 0
+
+
+def _der_len_at(b, i):
+    """(length, next index) of a minimal definite DER length at b[i], or None."""
+    if i >= len(b):
+        return None
+    l0 = b[i]
+    if l0 < 0x80:
+        return l0, i + 1
+    nb = l0 & 0x7F
+    if nb == 0 or nb > 4 or i + 1 + nb > len(b) or b[i + 1] == 0:
+        return None
+    v = int.from_bytes(b[i + 1:i + 1 + nb], "big")
+    if v < 0x80:
+        return None
+    return v, i + 1 + nb
+
+
+def der_is_two_integers(sig):
+    """True iff ``sig`` is exactly the canonical DER of SEQUENCE{INTEGER, INTEGER} (minimal
+    lengths, minimal non-empty two's-complement contents, nothing trailing): the inputs BC 1.57's
+    decode-and-re-encode check accepts."""
+    b = bytes(sig)
+    if len(b) < 2 or b[0] != 0x30:
+        return False
+    r = _der_len_at(b, 1)
+    if r is None or r[1] + r[0] != len(b):
+        return False
+    i, n = r[1], 0
+    while i < len(b):
+        if b[i] != 0x02:
+            return False
+        r = _der_len_at(b, i + 1)
+        if r is None or r[0] == 0 or r[1] + r[0] > len(b):
+            return False
+        ln, j = r
+        if ln > 1 and ((b[j] == 0 and b[j + 1] < 0x80) or (b[j] == 0xFF and b[j + 1] >= 0x80)):
+            return False
+        i, n = j + ln, n + 1
+    return n == 2
+
+
+def sig_field(scheme, sig):
+    """The bytes to pack for a signature: ``sig`` itself, or its surrogate when it is longer than
+    the ABI's 16-bit length field (see SIG_SURROGATE_*)."""
+    if len(sig) <= SIG_LEN_MAX:
+        return sig
+    if scheme in (ECDSA_SECP256K1_SHA256, ECDSA_SECP256R1_SHA256) and der_is_two_integers(sig):
+        return SIG_SURROGATE_INVALID
+    return SIG_SURROGATE_MALFORMED
+
+
+def check_msg_len(msg):
+    if len(msg) > MSG_LEN_MAX:  # a JVM byte[] holds at most 2^31 - 1 bytes: never a real input
+        raise ValueError(f"clear data of {len(msg)} bytes exceeds the 32-bit cg_item.msg_len")
+
+
 class Batch:
     """Packed batch: ``keys`` (KEY_DTYPE), ``items`` (ITEM_DTYPE), ``arena`` (uint8)."""
 
@@ -78,6 +147,10 @@ class BatchBuilder:
         k = (int(scheme), int(fmt), bytes(key_bytes))
         idx = self._key_index.get(k)
         if idx is None:
+            if len(key_bytes) > SIG_LEN_MAX:
+                # cg_key.len is 16 bits; no key encoding of a GPU scheme is that long, so the key
+                # fails to decode either way: pack one byte, which decodes to KEY_INVALID too
+                key_bytes = b"\x00"
             off = self._append(key_bytes, 4)
             idx = len(self._keys)
             self._keys.append((off, len(key_bytes), scheme, fmt))
@@ -85,6 +158,8 @@ class BatchBuilder:
         return idx
 
     def add(self, key_idx, sig, msg):
+        check_msg_len(msg)
+        sig = sig_field(self._keys[key_idx][2], sig)
         sig_off = self._append(sig, 4)
         msg_off = self._append(msg, 4)
         self._items.append((sig_off, msg_off, len(msg), key_idx, len(sig)))
@@ -100,6 +175,8 @@ class BatchBuilder:
         items = np.zeros(len(self._items), dtype=ITEM_DTYPE)
         if self._items:
             arr = np.array(self._items, dtype=np.uint64)
+            if arr[:, 4].max() > SIG_LEN_MAX or arr[:, 2].max() > MSG_LEN_MAX:
+                raise ValueError("a length exceeds its cg_item field")  # add() never lets one through
             items["sig_off"] = arr[:, 0]
             items["msg_off"] = arr[:, 1]
             items["msg_len"] = arr[:, 2]

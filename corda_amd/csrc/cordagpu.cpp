@@ -6,15 +6,18 @@
 // CG_ERR_DEVICE and the status bytes stay CG_NOT_RUN.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/cordagpu.h"
 #include "engine.h"
+#include "pool.h"
 
 namespace {
 
@@ -62,13 +65,10 @@ struct DevBuf {
 
 }  // namespace
 
-// cg_verify_batch splits a large host batch into this many consecutive item chunks: the arena
-// bytes chunk k needs go H2D on a copy stream while chunk k-1 verifies.
-#define CG_H2D_CHUNKS 4
-#define CG_H2D_MIN_ITEMS (1u << 17)
-
 struct cg_ctx {
   int device = 0;
+  uint64_t chunk = CG_DEFAULT_CHUNK_ITEMS;  // items per verify chunk (cg_config.chunk_items)
+  bool fault = false;                       // cg_pool_inject_fault drill: every call fails
   hipStream_t stream = nullptr;
   cg::Fork fork = {{nullptr, nullptr, nullptr}, nullptr, {nullptr, nullptr}, {nullptr, nullptr, nullptr}, nullptr,
                    {nullptr, nullptr, nullptr}};
@@ -78,10 +78,211 @@ struct cg_ctx {
   DevBuf txitems, msgs, tmpls, h_txs, h_comps, h_sigs, h_ids, h_txst;
   // tear-offs: leaf-hash workspace
   DevBuf ftxws;
-  // host-buffer verify: a copy stream and one event per arena segment (chunked H2D / verify)
+  // host-buffer verify: a copy stream and one event per pipeline chunk (H2D of chunk k+1 overlaps
+  // the verify of chunk k); timing events for cg_stats
   hipStream_t copy = nullptr;
-  hipEvent_t seg[CG_H2D_CHUNKS + 1] = {};
+  std::vector<hipEvent_t> seg;
+  hipEvent_t tev[4] = {};
+  // the end of the last call's device work, whatever stream it ran on: the next call waits for it
+  // before touching the shared workspace (async calls on different streams)
+  hipEvent_t done = nullptr;
+  bool done_rec = false;
 };
+
+namespace {
+
+hipError_t order_in(cg_ctx* c, hipStream_t s) { return c->done_rec ? hipStreamWaitEvent(s, c->done, 0) : hipSuccess; }
+hipError_t order_out(cg_ctx* c, hipStream_t s) {
+  hipError_t e = hipEventRecord(c->done, s);
+  if (e == hipSuccess) c->done_rec = true;
+  return e;
+}
+hipStream_t stream_of(cg_ctx* c, void* hip_stream) { return hip_stream ? (hipStream_t)hip_stream : c->stream; }
+
+// Equal chunks of at most c->chunk items.
+uint64_t chunk_of(const cg_ctx* c, uint64_t n) {
+  if (n <= c->chunk) return n ? n : 1;
+  const uint64_t k = (n + c->chunk - 1) / c->chunk;
+  return (n + k - 1) / k;
+}
+
+// Key and item workspace for n_keys keys and chunks of ws_items items. Growing it waits for the
+// device (cg_reserve ahead of time avoids that).
+hipError_t ensure_ws(cg_ctx* c, uint32_t n_keys, uint64_t ws_items) {
+  if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= cg::item_ws_bytes(ws_items)) return hipSuccess;
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = c->keyprep.ensure(cg::keyprep_bytes(n_keys));
+  if (e == hipSuccess) e = c->itemws.ensure(cg::item_ws_bytes(ws_items));
+  return e;
+}
+
+// Key tables once for the whole call (sized by every item's key use), then the items in chunks.
+hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                          const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, hipStream_t s,
+                          const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0) {
+  if (n_items == 0) return hipSuccess;
+  hipError_t e = cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork, d_items, n_items);
+  const uint64_t per = chunk_of(c, n_items);
+  for (uint64_t f = 0; f < n_items && e == hipSuccess; f += per) {
+    const uint64_t cnt = per < n_items - f ? per : n_items - f;
+    e = cg::launch_items(d_keys, n_keys, d_items + f, cnt, d_arena, arena_len, mode, d_status + f, c->keyprep.p,
+                         c->itemws.p, c->btab.p, s, d_msgs, msgs_len, &c->fork);
+  }
+  return e;
+}
+
+// ---- host-buffer verify: which arena bytes each pipeline chunk needs
+struct Extent {
+  uint64_t lo = UINT64_MAX, hi = 0;
+  void add(uint64_t off, uint64_t len, uint64_t arena_len) {
+    if (off > arena_len) return;  // outside the arena: the kernels never read it (CG_NOT_RUN)
+    const uint64_t e = len > arena_len - off ? arena_len : off + len;
+    if (off < lo) lo = off;
+    if (e > hi) hi = e;
+  }
+  void merge(const Extent& o) {
+    if (o.lo < lo) lo = o.lo;
+    if (o.hi > hi) hi = o.hi;
+  }
+  bool empty() const { return lo >= hi; }
+};
+
+struct HostPlan {
+  std::vector<uint64_t> first;  // chunk k = items [first[k], first[k+1])
+  std::vector<Extent> ext;      // arena bytes chunk k reads
+  Extent keys, win;             // key bytes; everything the call reads
+};
+
+void plan_host(const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items, uint64_t arena_len,
+               uint64_t per, HostPlan& P) {
+  for (uint32_t k = 0; k < n_keys; ++k) P.keys.add(keys[k].off, keys[k].len, arena_len);
+  const uint64_t nch = (n_items + per - 1) / per;
+  P.first.resize(nch + 1);
+  for (uint64_t k = 0; k <= nch; ++k) P.first[k] = n_items * k / nch;
+  P.ext.assign(nch, Extent());
+  // one host thread per chunk (at most 16): the scan reads 32 B per item
+  auto scan = [&](uint64_t k0, uint64_t k1) {
+    for (uint64_t k = k0; k < k1; ++k)
+      for (uint64_t i = P.first[k]; i < P.first[k + 1]; ++i) {
+        P.ext[k].add(items[i].sig_off, items[i].sig_len, arena_len);
+        P.ext[k].add(items[i].msg_off, items[i].msg_len, arena_len);
+      }
+  };
+  const uint64_t nt = nch < 16 ? nch : 16;
+  if (n_items < (1u << 16) || nt < 2) {
+    scan(0, nch);
+  } else {
+    std::vector<std::thread> th;
+    for (uint64_t t = 0; t < nt; ++t) th.emplace_back(scan, nch * t / nt, nch * (t + 1) / nt);
+    for (auto& t : th) t.join();
+  }
+  P.win = P.keys;
+  for (const Extent& e : P.ext) P.win.merge(e);
+  if (P.win.empty()) P.win.lo = P.win.hi = 0;
+  P.win.lo &= ~(uint64_t)15;  // the device window starts 16-aligned (kernels load aligned words)
+}
+
+// Copies the parts of [e.lo, e.hi) not yet resident (`have`: sorted disjoint intervals).
+hipError_t copy_missing(std::vector<std::pair<uint64_t, uint64_t>>& have, const Extent& e, const uint8_t* arena,
+                        uint8_t* dwin, uint64_t win_lo, hipStream_t s) {
+  if (e.empty()) return hipSuccess;
+  uint64_t cur = e.lo;
+  std::vector<std::pair<uint64_t, uint64_t>> gaps;
+  for (const auto& h : have) {
+    if (h.second <= cur) continue;
+    if (h.first >= e.hi) break;
+    if (h.first > cur) gaps.push_back({cur, h.first});
+    cur = h.second > cur ? h.second : cur;
+    if (cur >= e.hi) break;
+  }
+  if (cur < e.hi) gaps.push_back({cur, e.hi});
+  for (const auto& g : gaps) {
+    hipError_t r = hipMemcpyAsync(dwin + (g.first - win_lo), arena + g.first, g.second - g.first,
+                                  hipMemcpyHostToDevice, s);
+    if (r != hipSuccess) return r;
+  }
+  have.push_back({e.lo, e.hi});
+  std::sort(have.begin(), have.end());
+  std::vector<std::pair<uint64_t, uint64_t>> m;
+  for (const auto& h : have) {
+    if (!m.empty() && h.first <= m.back().second) m.back().second = std::max(m.back().second, h.second);
+    else m.push_back(h);
+  }
+  have.swap(m);
+  return hipSuccess;
+}
+
+// cg_verify_batch with the ctx lock held. On failure the status bytes are CG_NOT_RUN.
+int verify_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
+                       const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out, cg_stats* stats) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (c->fault) return fail(CG_ERR_DEVICE, "cg_verify_batch: device fault (injected by cg_pool_inject_fault)");
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  const uint64_t pipe = c->chunk < CG_PIPELINE_CHUNK_ITEMS ? c->chunk : CG_PIPELINE_CHUNK_ITEMS;
+  HostPlan P;
+  plan_host(keys, n_keys, items, n_items, arena_len, pipe, P);
+  const uint64_t nch = P.ext.size();
+  const uint64_t per_max = (n_items + nch - 1) / nch;
+  HIP_TRY(c->keys.ensure(sizeof(cg_key) * (n_keys ? n_keys : 1)), "hipMalloc(keys)");
+  HIP_TRY(c->items.ensure(sizeof(cg_item) * n_items), "hipMalloc(items)");
+  HIP_TRY(c->arena.ensure((P.win.hi - P.win.lo) + 16), "hipMalloc(arena window)");
+  HIP_TRY(c->status.ensure(n_items), "hipMalloc(status)");
+  HIP_TRY(ensure_ws(c, n_keys, per_max), "hipMalloc(workspace)");
+  while (c->seg.size() < nch) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    c->seg.push_back(e);
+  }
+  hipStream_t s = c->stream;
+  uint8_t* dwin = (uint8_t*)c->arena.p;
+  // the kernels index the arena by absolute offsets: hand them the window's base shifted back
+  const uint8_t* dbase = dwin - P.win.lo;
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
+  HIP_TRY(hipEventRecord(c->tev[0], s), "hipEventRecord");
+  HIP_TRY(hipStreamWaitEvent(c->copy, c->tev[0], 0), "hipStreamWaitEvent");
+  std::vector<std::pair<uint64_t, uint64_t>> have;
+  if (n_keys)
+    HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, c->copy), "H2D keys");
+  HIP_TRY(copy_missing(have, P.keys, arena, dwin, P.win.lo, c->copy), "H2D key bytes");
+  HIP_TRY(hipMemcpyAsync(c->items.p, items, sizeof(cg_item) * n_items, hipMemcpyHostToDevice, c->copy), "H2D items");
+  // key tables sized by every item's key, built while chunk 0's arena bytes copy
+  HIP_TRY(hipEventRecord(c->seg[0], c->copy), "hipEventRecord");
+  HIP_TRY(hipStreamWaitEvent(s, c->seg[0], 0), "hipStreamWaitEvent");
+  const cg_key* dk = (const cg_key*)c->keys.p;
+  const cg_item* di = (const cg_item*)c->items.p;
+  uint8_t* ds = (uint8_t*)c->status.p;
+  HIP_TRY(cg::launch_keyprep(dk, n_keys, dbase, arena_len, c->keyprep.p, s, &c->fork, di, n_items), "launch_keyprep");
+  for (uint64_t k = 0; k < nch; ++k) {
+    HIP_TRY(copy_missing(have, P.ext[k], arena, dwin, P.win.lo, c->copy), "H2D arena");
+    HIP_TRY(hipEventRecord(c->seg[k], c->copy), "hipEventRecord");
+    HIP_TRY(hipStreamWaitEvent(s, c->seg[k], 0), "hipStreamWaitEvent");
+    if (k == 0) HIP_TRY(hipEventRecord(c->tev[1], s), "hipEventRecord");
+    const uint64_t f = P.first[k], cnt = P.first[k + 1] - f;
+    HIP_TRY(cg::launch_items(dk, n_keys, di + f, cnt, dbase, arena_len, mode, ds + f, c->keyprep.p, c->itemws.p,
+                             c->btab.p, s, nullptr, 0, &c->fork), "launch_items");
+  }
+  HIP_TRY(hipEventRecord(c->tev[2], s), "hipEventRecord");
+  HIP_TRY(hipMemcpyAsync(status_out, ds, n_items, hipMemcpyDeviceToHost, s), "D2H status");
+  HIP_TRY(hipEventRecord(c->tev[3], s), "hipEventRecord");
+  HIP_TRY(order_out(c, s), "hipEventRecord");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (stats) {
+    float a = 0, b = 0, d = 0;
+    hipEventElapsedTime(&a, c->tev[0], c->tev[1]);
+    hipEventElapsedTime(&b, c->tev[1], c->tev[2]);
+    hipEventElapsedTime(&d, c->tev[2], c->tev[3]);
+    stats->n_items = n_items;
+    stats->n_keys = n_keys;
+    stats->ms_h2d = a;
+    stats->ms_key_prep = 0;
+    stats->ms_verify = b;
+    stats->ms_d2h = d;
+    stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return CG_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -114,6 +315,7 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     return fail(CG_ERR_DEVICE, "cg_open: kernels are built for gfx950, device is %s", prop.gcnArchName);
   cg_ctx* c = new cg_ctx();
   c->device = dev;
+  if (cfg && cfg->chunk_items) c->chunk = cfg->chunk_items;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;
@@ -127,8 +329,8 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.row0[k], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.front, hipEventDisableTiming);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
-  for (int k = 0; k <= CG_H2D_CHUNKS && e == hipSuccess; ++k)
-    e = hipEventCreateWithFlags(&c->seg[k], hipEventDisableTiming);
+  for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&c->tev[k]);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
   if (e == hipSuccess) e = cg::upload_constants();
   if (e == hipSuccess) e = c->btab.ensure(cg::btab_bytes());
   if (e == hipSuccess) e = cg::init_btab(c->btab.p, c->stream);
@@ -172,8 +374,10 @@ void cg_close(cg_ctx* c) {
     hipStreamSynchronize(c->copy);
     hipStreamDestroy(c->copy);
   }
-  for (int k = 0; k <= CG_H2D_CHUNKS; ++k)
-    if (c->seg[k]) hipEventDestroy(c->seg[k]);
+  for (hipEvent_t e : c->seg) hipEventDestroy(e);
+  for (int k = 0; k < 4; ++k)
+    if (c->tev[k]) hipEventDestroy(c->tev[k]);
+  if (c->done) hipEventDestroy(c->done);
   for (int k = 0; k < 2; ++k)
     if (c->fork.ec_decoded[k]) hipEventDestroy(c->fork.ec_decoded[k]);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -184,8 +388,7 @@ int cg_reserve(cg_ctx* c, uint32_t max_keys, uint64_t max_items) {
   if (!c) return fail(CG_ERR_ARG, "cg_reserve: ctx is NULL");
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(max_keys)), "hipMalloc(keyprep)");
-  HIP_TRY(c->itemws.ensure(cg::item_ws_bytes(max_items)), "hipMalloc(item workspace)");
+  HIP_TRY(ensure_ws(c, max_keys, chunk_of(c, max_items)), "hipMalloc(workspace)");
   return CG_OK;
 }
 
@@ -196,17 +399,13 @@ int cg_verify_batch_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   if (n_items && (!d_items || !d_status)) return fail(CG_ERR_ARG, "cg_verify_batch_device: NULL buffer");
   if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_verify_batch_device: bad mode");
   std::lock_guard<std::mutex> g(c->mu);
+  if (c->fault) return fail(CG_ERR_DEVICE, "cg_verify_batch_device: device fault (injected)");
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  if (c->keyprep.cap < cg::keyprep_bytes(n_keys) || c->itemws.cap < cg::item_ws_bytes(n_items)) {
-    // growing the workspace synchronises the device; cg_reserve ahead of time avoids it
-    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
-    HIP_TRY(c->itemws.ensure(cg::item_ws_bytes(n_items)), "hipMalloc(item workspace)");
-  }
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  HIP_TRY(cg::launch_verify(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p,
-                            c->itemws.p, c->btab.p, s, nullptr, 0, &c->fork),
-          "launch_verify");
+  HIP_TRY(ensure_ws(c, n_keys, chunk_of(c, n_items)), "hipMalloc(workspace)");
+  hipStream_t s = stream_of(c, hip_stream);
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
+  HIP_TRY(launch_chunked(c, d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, s), "launch_verify");
+  HIP_TRY(order_out(c, s), "hipEventRecord");
   return CG_OK;
 }
 
@@ -220,8 +419,10 @@ int cg_prepare_keys_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
     HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
   }
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = stream_of(c, hip_stream);
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork), "launch_keyprep");
+  HIP_TRY(order_out(c, s), "hipEventRecord");
   return CG_OK;
 }
 
@@ -235,14 +436,17 @@ int cg_verify_items_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   if (c->keyprep.cap < cg::keyprep_bytes(n_keys))
     return fail(CG_ERR_ARG, "cg_verify_items_device: keys were not prepared (call cg_prepare_keys_device)");
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  if (c->itemws.cap < cg::item_ws_bytes(n_items)) {
-    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    HIP_TRY(c->itemws.ensure(cg::item_ws_bytes(n_items)), "hipMalloc(item workspace)");
+  HIP_TRY(ensure_ws(c, n_keys, chunk_of(c, n_items)), "hipMalloc(item workspace)");
+  hipStream_t s = stream_of(c, hip_stream);
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
+  const uint64_t per = chunk_of(c, n_items);
+  for (uint64_t f = 0; f < n_items; f += per) {
+    const uint64_t cnt = per < n_items - f ? per : n_items - f;
+    HIP_TRY(cg::launch_items(d_keys, n_keys, d_items + f, cnt, d_arena, arena_len, mode, d_status + f, c->keyprep.p,
+                             c->itemws.p, c->btab.p, s, nullptr, 0, &c->fork),
+            "launch_items");
   }
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  HIP_TRY(cg::launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, c->keyprep.p,
-                           c->itemws.p, c->btab.p, s, nullptr, 0, &c->fork),
-          "launch_items");
+  HIP_TRY(order_out(c, s), "hipEventRecord");
   return CG_OK;
 }
 
@@ -254,90 +458,12 @@ int cg_verify_batch(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_ite
   if (n_keys && !keys) return fail(CG_ERR_ARG, "cg_verify_batch: keys is NULL");
   if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_verify_batch: arena is NULL");
   if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_verify_batch: bad mode");
-  for (uint64_t i = 0; i < n_items; ++i) status_out[i] = CG_NOT_RUN;
+  if (n_items) memset(status_out, CG_NOT_RUN, n_items);
   if (n_items == 0) return CG_OK;
-  auto t0 = std::chrono::steady_clock::now();
   std::lock_guard<std::mutex> g(c->mu);
-  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  const size_t arena_alloc = ((arena_len + 3) & ~(uint64_t)3) + 16;
-  HIP_TRY(c->keys.ensure(sizeof(cg_key) * (n_keys ? n_keys : 1)), "hipMalloc(keys)");
-  HIP_TRY(c->items.ensure(sizeof(cg_item) * n_items), "hipMalloc(items)");
-  HIP_TRY(c->arena.ensure(arena_alloc), "hipMalloc(arena)");
-  HIP_TRY(c->status.ensure(n_items), "hipMalloc(status)");
-  HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
-  HIP_TRY(c->itemws.ensure(cg::item_ws_bytes(n_items)), "hipMalloc(item workspace)");
-  hipStream_t s = c->stream;
-  hipEvent_t ev[4];
-  for (auto& e : ev) HIP_TRY(hipEventCreate(&e), "hipEventCreate");
-  // Chunk plan: item chunk k needs arena[0 .. need[k]) (prefix max of its items' extents,
-  // clamped to the arena: an item outside it is CG_NOT_RUN and reads nothing); key prep needs
-  // arena[0 .. key_end). Pipelined only when the keys sit in the first quarter of the arena,
-  // which is how a caller appending (key, sig, clear) in order lays it out; otherwise one copy.
-  uint64_t key_end = 0;
-  for (uint32_t k = 0; k < n_keys; ++k) {
-    const uint64_t e = keys[k].off > arena_len ? arena_len : keys[k].off + keys[k].len;
-    key_end = e > key_end ? e : key_end;
-  }
-  key_end = key_end < arena_len ? key_end : arena_len;
-  int chunks = (n_items >= CG_H2D_MIN_ITEMS && key_end <= arena_len / 4) ? CG_H2D_CHUNKS : 1;
-  uint64_t first[CG_H2D_CHUNKS + 1], need[CG_H2D_CHUNKS];
-  for (int k = 0; k <= chunks; ++k) first[k] = n_items * (uint64_t)k / (uint64_t)chunks;
-  uint64_t run = key_end;
-  for (int k = 0; k < chunks; ++k) {
-    for (uint64_t i = first[k]; i < first[k + 1]; ++i) {
-      const cg_item& it = items[i];
-      const uint64_t se = it.sig_off > arena_len ? 0 : it.sig_off + it.sig_len;
-      const uint64_t me = it.msg_off > arena_len ? 0 : it.msg_off + it.msg_len;
-      const uint64_t e = se > me ? se : me;
-      if (e > run) run = e;
-    }
-    need[k] = run < arena_len ? run : arena_len;
-  }
-  if (chunks == 1) need[0] = arena_len;
-  HIP_TRY(hipEventRecord(ev[0], s), "hipEventRecord");
-  HIP_TRY(hipStreamWaitEvent(c->copy, ev[0], 0), "hipStreamWaitEvent");
-  if (n_keys)
-    HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, c->copy), "H2D keys");
-  HIP_TRY(hipMemcpyAsync(c->items.p, items, sizeof(cg_item) * n_items, hipMemcpyHostToDevice, c->copy), "H2D items");
-  uint64_t copied = 0;
-  for (int k = 0; k < chunks; ++k) {
-    if (need[k] > copied) {
-      HIP_TRY(hipMemcpyAsync((uint8_t*)c->arena.p + copied, arena + copied, need[k] - copied, hipMemcpyHostToDevice,
-                             c->copy), "H2D arena");
-      copied = need[k];
-    }
-    HIP_TRY(hipEventRecord(c->seg[k], c->copy), "hipEventRecord");
-    HIP_TRY(hipStreamWaitEvent(s, c->seg[k], 0), "hipStreamWaitEvent");
-    if (k == 0) {
-      HIP_TRY(hipEventRecord(ev[1], s), "hipEventRecord");
-      // key tables sized by every item's key (not just chunk 0's)
-      HIP_TRY(cg::launch_keyprep((const cg_key*)c->keys.p, n_keys, (const uint8_t*)c->arena.p, arena_len, c->keyprep.p,
-                                 s, &c->fork, (const cg_item*)c->items.p, n_items), "launch_keyprep");
-    }
-    HIP_TRY(cg::launch_items((const cg_key*)c->keys.p, n_keys, (const cg_item*)c->items.p + first[k],
-                             first[k + 1] - first[k], (const uint8_t*)c->arena.p, arena_len, mode,
-                             (uint8_t*)c->status.p + first[k], c->keyprep.p, c->itemws.p, c->btab.p, s, nullptr, 0,
-                             &c->fork), "launch_items");
-  }
-  HIP_TRY(hipEventRecord(ev[2], s), "hipEventRecord");
-  HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n_items, hipMemcpyDeviceToHost, s), "D2H status");
-  HIP_TRY(hipEventRecord(ev[3], s), "hipEventRecord");
-  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
-  if (stats) {
-    float a = 0, b = 0, d = 0;
-    hipEventElapsedTime(&a, ev[0], ev[1]);
-    hipEventElapsedTime(&b, ev[1], ev[2]);
-    hipEventElapsedTime(&d, ev[2], ev[3]);
-    stats->n_items = n_items;
-    stats->n_keys = n_keys;
-    stats->ms_h2d = a;
-    stats->ms_key_prep = 0;
-    stats->ms_verify = b;
-    stats->ms_d2h = d;
-    stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  }
-  for (auto& e : ev) hipEventDestroy(e);
-  return CG_OK;
+  const int rc = verify_host_locked(c, keys, n_keys, items, n_items, arena, arena_len, mode, status_out, stats);
+  if (rc != CG_OK) memset(status_out, CG_NOT_RUN, n_items);
+  return rc;
 }
 
 int cg_sha256_batch_device(cg_ctx* c, const cg_span* d_spans, uint64_t n, const uint8_t* d_arena,
@@ -345,8 +471,10 @@ int cg_sha256_batch_device(cg_ctx* c, const cg_span* d_spans, uint64_t n, const 
   if (!c) return fail(CG_ERR_ARG, "cg_sha256_batch_device: ctx is NULL");
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = stream_of(c, hip_stream);
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(cg::launch_sha256(d_spans, n, d_arena, arena_len, d_digests, s), "launch_sha256");
+  HIP_TRY(order_out(c, s), "hipEventRecord");
   return CG_OK;
 }
 
@@ -359,6 +487,7 @@ static int hash_batch(cg_ctx* c, const cg_span* spans, uint64_t n, const uint8_t
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(c->items.ensure(sizeof(cg_span) * n), "hipMalloc(spans)");
   HIP_TRY(c->arena.ensure(((arena_len + 3) & ~(uint64_t)3) + 16), "hipMalloc(arena)");
   HIP_TRY(c->aux0.ensure(dlen * n), "hipMalloc(digests)");
@@ -394,9 +523,11 @@ int cg_tx_ids_device(cg_ctx* c, const cg_tx* d_txs, uint64_t n_tx, const cg_comp
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
     HIP_TRY(c->aux2.ensure(cg::tx_ws_bytes(n_comps)), "hipMalloc(leaf ws)");
   }
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = stream_of(c, hip_stream);
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(cg::launch_tx_ids(d_txs, n_tx, d_comps, n_comps, d_arena, arena_len, d_ids, d_status,
                             (uint8_t*)c->aux2.p, s), "launch_tx_ids");
+  HIP_TRY(order_out(c, s), "hipEventRecord");
   return CG_OK;
 }
 
@@ -408,6 +539,7 @@ int cg_tx_ids(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_component* co
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(c->keys.ensure(sizeof(cg_tx) * n_tx), "hipMalloc(txs)");
   HIP_TRY(c->items.ensure(sizeof(cg_component) * (n_comps ? n_comps : 1)), "hipMalloc(comps)");
   HIP_TRY(c->arena.ensure(((arena_len + 3) & ~(uint64_t)3) + 16), "hipMalloc(arena)");
@@ -442,6 +574,7 @@ int cg_merkle_roots(cg_ctx* c, const uint8_t* leaves, const uint64_t* first, con
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(c->arena.ensure(32 * (total ? total : 1)), "hipMalloc(leaves)");
   HIP_TRY(c->keys.ensure(8 * n), "hipMalloc(first)");
   HIP_TRY(c->items.ensure(4 * n), "hipMalloc(count)");
@@ -479,29 +612,29 @@ static int verify_transactions_locked(cg_ctx* c, const cg_tx* d_txs, uint64_t n_
   const size_t need_leaf = cg::tx_ws_bytes(n_comps), need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1),
                need_msgs = slot * (n_sigs ? n_sigs : 1), need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
   if (c->aux2.cap < need_leaf || c->txitems.cap < need_items || c->msgs.cap < need_msgs ||
-      c->tmpls.cap < need_tmpl || c->keyprep.cap < cg::keyprep_bytes(n_keys) ||
-      c->itemws.cap < cg::item_ws_bytes(n_sigs)) {
+      c->tmpls.cap < need_tmpl) {
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
     HIP_TRY(c->aux2.ensure(need_leaf), "hipMalloc(leaf ws)");
     HIP_TRY(c->txitems.ensure(need_items), "hipMalloc(tx items)");
     HIP_TRY(c->msgs.ensure(need_msgs), "hipMalloc(spliced messages)");
     HIP_TRY(c->tmpls.ensure(need_tmpl), "hipMalloc(templates)");
-    HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
-    HIP_TRY(c->itemws.ensure(cg::item_ws_bytes(n_sigs)), "hipMalloc(item workspace)");
   }
+  HIP_TRY(ensure_ws(c, n_keys, chunk_of(c, n_sigs)), "hipMalloc(workspace)");
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   if (n_tmpls)
     HIP_TRY(hipMemcpyAsync(c->tmpls.p, tmpls, sizeof(cg_signable_tmpl) * n_tmpls, hipMemcpyHostToDevice, s),
             "H2D templates");
   HIP_TRY(cg::launch_tx_ids(d_txs, n_tx, d_comps, n_comps, d_arena, arena_len, d_ids, d_tx_status,
                             (uint8_t*)c->aux2.p, s), "launch_tx_ids");
-  if (n_sigs == 0) return CG_OK;
-  HIP_TRY(cg::launch_tx_sig_items(d_sigs, n_sigs, (const cg_signable_tmpl*)c->tmpls.p, n_tmpls, d_tx_status, n_tx,
-                                  d_ids, d_arena, arena_len, slot, (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s),
-          "launch_tx_sig_items");
-  HIP_TRY(cg::launch_verify(d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode,
-                            d_sig_status, c->keyprep.p, c->itemws.p, c->btab.p, s, (const uint8_t*)c->msgs.p,
-                            slot * n_sigs, &c->fork),
-          "launch_verify");
+  if (n_sigs) {
+    HIP_TRY(cg::launch_tx_sig_items(d_sigs, n_sigs, (const cg_signable_tmpl*)c->tmpls.p, n_tmpls, d_tx_status, n_tx,
+                                    d_ids, d_arena, arena_len, slot, (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s),
+            "launch_tx_sig_items");
+    HIP_TRY(launch_chunked(c, d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode,
+                           d_sig_status, s, (const uint8_t*)c->msgs.p, slot * n_sigs),
+            "launch_verify");
+  }
+  HIP_TRY(order_out(c, s), "hipEventRecord");
   return CG_OK;
 }
 
@@ -517,7 +650,7 @@ int cg_verify_transactions_device(cg_ctx* c, const cg_tx* d_txs, uint64_t n_tx, 
   if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_verify_transactions_device: bad mode");
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = stream_of(c, hip_stream);
   return verify_transactions_locked(c, d_txs, n_tx, d_comps, n_comps, d_keys, n_keys, d_sigs, n_sigs, tmpls, n_tmpls,
                                     d_arena, arena_len, mode, d_ids, d_tx_status, d_sig_status, s);
 }
@@ -540,6 +673,7 @@ int cg_verify_transactions(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(c->h_txs.ensure(sizeof(cg_tx) * (n_tx ? n_tx : 1)), "hipMalloc(txs)");
   HIP_TRY(c->h_comps.ensure(sizeof(cg_component) * (n_comps ? n_comps : 1)), "hipMalloc(comps)");
   HIP_TRY(c->keys.ensure(sizeof(cg_key) * (n_keys ? n_keys : 1)), "hipMalloc(keys)");
@@ -582,9 +716,11 @@ int cg_verify_filtered_device(cg_ctx* c, const cg_filtered_tx* d_ftxs, uint64_t 
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
     HIP_TRY(c->ftxws.ensure(cg::ftx_ws_bytes(n_leaves)), "hipMalloc(filtered ws)");
   }
-  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  hipStream_t s = stream_of(c, hip_stream);
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(cg::launch_filtered(d_ftxs, n_ftx, d_nodes, n_nodes, d_leaves, n_leaves, d_arena, arena_len, d_status,
                               (uint8_t*)c->ftxws.p, s), "launch_filtered");
+  HIP_TRY(order_out(c, s), "hipEventRecord");
   return CG_OK;
 }
 
@@ -599,6 +735,7 @@ int cg_verify_filtered(cg_ctx* c, const cg_filtered_tx* ftxs, uint64_t n_ftx, co
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(c->h_txs.ensure(sizeof(cg_filtered_tx) * n_ftx), "hipMalloc(filtered txs)");
   HIP_TRY(c->h_comps.ensure(sizeof(cg_pmt_node) * (n_nodes ? n_nodes : 1)), "hipMalloc(nodes)");
   HIP_TRY(c->h_sigs.ensure(sizeof(cg_filtered_leaf) * (n_leaves ? n_leaves : 1)), "hipMalloc(leaves)");
@@ -618,6 +755,99 @@ int cg_verify_filtered(cg_ctx* c, const cg_filtered_tx* ftxs, uint64_t n_ftx, co
   HIP_TRY(hipMemcpyAsync(status_out, c->status.p, n_ftx, hipMemcpyDeviceToHost, s), "D2H status");
   HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
   return CG_OK;
+}
+
+// ---------------------------------------------------------------- several devices (pool.h)
+struct cg_pool {
+  std::vector<cg_ctx*> ctx;
+  std::vector<uint8_t> healthy;
+  std::mutex mu;
+};
+
+int cg_pool_open(cg_pool** out, const int32_t* devices, uint32_t n_slots, const cg_config* cfg) {
+  if (!out) return fail(CG_ERR_ARG, "cg_pool_open: out is NULL");
+  *out = nullptr;
+  if (n_slots == 0 || !devices) return fail(CG_ERR_ARG, "cg_pool_open: no devices");
+  cg_pool* p = new cg_pool();
+  for (uint32_t k = 0; k < n_slots; ++k) {
+    cg_config c = cfg ? *cfg : cg_config{};
+    c.device = devices[k];
+    cg_ctx* x = nullptr;
+    const int rc = cg_open(&x, &c);
+    if (rc != CG_OK) {
+      const std::string why = g_err;
+      cg_pool_close(p);
+      char buf[64];
+      snprintf(buf, sizeof buf, "cg_pool_open: slot %u: ", k);
+      g_err = buf + why;
+      return rc;
+    }
+    p->ctx.push_back(x);
+    p->healthy.push_back(1);
+  }
+  *out = p;
+  return CG_OK;
+}
+
+void cg_pool_close(cg_pool* p) {
+  if (!p) return;
+  for (cg_ctx* c : p->ctx) cg_close(c);
+  delete p;
+}
+
+uint32_t cg_pool_slots(const cg_pool* p) { return p ? (uint32_t)p->ctx.size() : 0; }
+
+int cg_pool_slot_healthy(const cg_pool* p, uint32_t slot) {
+  if (!p || slot >= p->ctx.size()) return -1;
+  return p->healthy[slot] ? 1 : 0;
+}
+
+int cg_pool_inject_fault(cg_pool* p, uint32_t slot, int on) {
+  if (!p || slot >= p->ctx.size()) return fail(CG_ERR_ARG, "cg_pool_inject_fault: bad slot");
+  std::lock_guard<std::mutex> g(p->mu);
+  std::lock_guard<std::mutex> gc(p->ctx[slot]->mu);
+  p->ctx[slot]->fault = on != 0;
+  if (!on) p->healthy[slot] = 1;
+  return CG_OK;
+}
+
+int cg_pool_verify_batch(cg_pool* p, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
+                         const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
+                         cg_pool_stats* stats) {
+  if (!p) return fail(CG_ERR_ARG, "cg_pool_verify_batch: pool is NULL");
+  if (n_items && (!items || !status_out)) return fail(CG_ERR_ARG, "cg_pool_verify_batch: NULL buffer");
+  if (n_keys && !keys) return fail(CG_ERR_ARG, "cg_pool_verify_batch: keys is NULL");
+  if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_pool_verify_batch: arena is NULL");
+  if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_pool_verify_batch: bad mode");
+  const auto t0 = std::chrono::steady_clock::now();
+  std::lock_guard<std::mutex> g(p->mu);
+  std::vector<std::string> errs(p->ctx.size());
+  cg::PoolReport rep;
+  const int rc = cg::pool_run(p->healthy, n_items, status_out,
+                              [&](uint32_t slot, uint64_t first, uint64_t count) {
+                                cg_ctx* c = p->ctx[slot];
+                                std::lock_guard<std::mutex> gc(c->mu);
+                                const int r = verify_host_locked(c, keys, n_keys, items + first, count, arena,
+                                                                 arena_len, mode, status_out + first, nullptr);
+                                if (r != CG_OK) errs[slot] = g_err;  // g_err is this worker thread's
+                                return r;
+                              },
+                              &rep);
+  if (stats) {
+    stats->shards = rep.shards;
+    stats->reruns = rep.reruns;
+    stats->failed_slots = rep.failed_slots;
+    stats->reserved = 0;
+    stats->not_run = rep.not_run;
+    stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  if (rc != CG_OK) {
+    std::string m = "cg_pool_verify_batch: no healthy slot could run every shard;";
+    for (size_t k = 0; k < errs.size(); ++k)
+      if (!errs[k].empty()) m += " [slot " + std::to_string(k) + "] " + errs[k];
+    g_err = m;
+  }
+  return rc;
 }
 
 }  // extern "C"

@@ -13,6 +13,45 @@ namespace cg {
 
 __device__ __forceinline__ uint64_t round4(uint64_t x) { return (x + 3) & ~(uint64_t)3; }
 
+// Persistent, XCD-grouped walk over `n` work units starting at plan position `beg` (a unit is
+// `per` consecutive positions: 1 for the one-lane-per-item stages, K for the batched
+// inversions). Blocks b and b + 8 share an XCD (round-robin dealing, MI355X_MICROARCH.md
+// "Workgroup dispatch"), so group g = b % 8 walks the contiguous g-th eighth of the range with
+// its blocks strided by blockDim lanes: at any moment one XCD's lanes run adjacent, key-sorted
+// positions and share that XCD's L2 for the key's rows. The grid is capped on the host
+// (walk_grid), so a stage whose range is empty costs a few hundred exiting blocks, not
+// n_items / 256 of them, and never competes for dispatch with a concurrent ladder.
+#define CG_XCDS 8u
+struct Walk {
+  uint64_t u, end, step;
+};
+__device__ __forceinline__ Walk walk_units(uint64_t n) {
+  const uint32_t groups = gridDim.x >= CG_XCDS ? CG_XCDS : 1u;
+  const uint32_t g = blockIdx.x % groups;
+  const uint32_t bpg = gridDim.x / groups;  // walk_grid makes gridDim.x a multiple of 8
+  const uint64_t span = (n + groups - 1) / groups;
+  const uint64_t lo = (uint64_t)g * span;
+  const uint64_t hi = lo + span < n ? lo + span : n;
+  Walk w;
+  w.u = lo + (uint64_t)(blockIdx.x / groups) * blockDim.x + threadIdx.x;
+  w.end = hi;
+  w.step = (uint64_t)bpg * blockDim.x;
+  return w;
+}
+// Grid for a walk: enough blocks for `units` (one lane each), at most `cap`, a multiple of 8.
+static inline unsigned walk_grid(uint64_t units, uint32_t block, uint32_t cap) {
+  uint64_t g = (units + block - 1) / block;
+  if (g > cap) g = cap;
+  g = (g + CG_XCDS - 1) / CG_XCDS * CG_XCDS;
+  return (unsigned)(g ? g : CG_XCDS);
+}
+// Grid cap for a 256-lane-block stage at `waves_per_simd`: the resident blocks of the chip
+// (256 CUs x 4 SIMDs x waves / 4 waves per block) times 2, so a block that finishes early
+// (invalid items exit at once) is replaced. Resident blocks of one XCD still run one contiguous
+// window of positions per iteration, so the cap does not cost L2 locality.
+#define CG_CUS 256u
+#define WALK_CAP(waves_per_simd) (CG_CUS * (waves_per_simd) * 2u)
+
 __device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t arena_len) {
   return off <= arena_len && len <= arena_len - off;
 }

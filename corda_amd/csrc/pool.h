@@ -1,0 +1,101 @@
+// One process driving several devices (VERDICT r1 "multi-device inside the
+// library"): the shard plan and the failure handling of cg_pool_verify_batch, with no HIP in
+// it, so tests/native/pool_test.cpp runs exactly this code on the CPU against the C oracle
+// (world sizes 1-4, injected device failures).
+//
+// Plan: the items are cut into contiguous, equal ranges, one per healthy slot (a slot is one
+// cg_ctx: a device, or a second context on the same device). Each shard runs on its own host
+// thread and writes its verdicts straight into its slice of the caller's status buffer (the
+// gather is the D2H copy itself: no collective is needed to assemble a host result).
+//
+// Failure: a shard whose call fails marks its slot unhealthy (skipped by later calls) and has
+// its slice reset to CG_NOT_RUN; failed shards are then re-run on the slots that are still
+// healthy, round-robin, until every shard has run or no healthy slot is left. The reference
+// gets this from Artemis redelivery of the verifier's request (VerifierTests.kt:73-99,
+// OutOfProcessTransactionVerifierService.kt:65-72); here a device fault costs a re-run of its
+// shard, and an item that could not be run anywhere stays CG_NOT_RUN (never "valid"), so the
+// caller can re-queue exactly those.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include <thread>
+#include <vector>
+
+#include "../../include/cordagpu.h"
+
+namespace cg {
+
+struct PoolShard {
+  uint64_t first, count;
+  uint32_t slot;
+  int rc;
+};
+
+struct PoolReport {
+  uint32_t shards = 0;       // shards of the first pass
+  uint32_t reruns = 0;       // shard re-runs after a failure
+  uint32_t failed_slots = 0; // slots marked unhealthy during this call
+  uint64_t not_run = 0;      // items left CG_NOT_RUN
+};
+
+// verify(slot, first, count) -> CG_OK or an error; it writes status[first .. first + count).
+template <class VerifyFn>
+int pool_run(std::vector<uint8_t>& healthy, uint64_t n_items, uint8_t* status, VerifyFn&& verify,
+             PoolReport* rep) {
+  PoolReport r;
+  if (n_items) memset(status, CG_NOT_RUN, n_items);
+  std::vector<uint32_t> live;
+  auto refresh = [&]() {
+    live.clear();
+    for (uint32_t s = 0; s < healthy.size(); ++s)
+      if (healthy[s]) live.push_back(s);
+  };
+  refresh();
+  // first pass: one contiguous shard per healthy slot
+  std::vector<PoolShard> pending;
+  const uint64_t k = live.size();
+  for (uint64_t j = 0; j < k; ++j) {
+    const uint64_t a = n_items * j / k, b = n_items * (j + 1) / k;
+    if (b > a) pending.push_back(PoolShard{a, b - a, 0, CG_OK});
+  }
+  if (n_items && k == 0) {
+    r.not_run = n_items;
+    if (rep) *rep = r;
+    return CG_ERR_DEVICE;
+  }
+  r.shards = (uint32_t)pending.size();
+  bool first = true;
+  while (!pending.empty()) {
+    refresh();
+    if (live.empty()) {
+      for (const PoolShard& sh : pending) r.not_run += sh.count;
+      if (rep) *rep = r;
+      return CG_ERR_DEVICE;
+    }
+    // one shard per healthy slot per pass (a slot's context serialises its calls anyway)
+    const size_t take = pending.size() < live.size() ? pending.size() : live.size();
+    std::vector<PoolShard> pass(pending.begin(), pending.begin() + take);
+    pending.erase(pending.begin(), pending.begin() + take);
+    for (size_t j = 0; j < take; ++j) pass[j].slot = live[j];
+    if (!first) r.reruns += (uint32_t)take;
+    first = false;
+    std::vector<std::thread> th;
+    th.reserve(take);
+    for (PoolShard& sh : pass) th.emplace_back([&sh, &verify]() { sh.rc = verify(sh.slot, sh.first, sh.count); });
+    for (std::thread& t : th) t.join();
+    for (PoolShard& sh : pass) {
+      if (sh.rc == CG_OK) continue;
+      if (healthy[sh.slot]) {
+        healthy[sh.slot] = 0;
+        ++r.failed_slots;
+      }
+      memset(status + sh.first, CG_NOT_RUN, sh.count);
+      pending.push_back(sh);
+    }
+  }
+  if (rep) *rep = r;
+  return CG_OK;
+}
+
+}  // namespace cg

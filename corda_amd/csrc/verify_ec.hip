@@ -114,8 +114,8 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
                                                  uint32_t mode, uint8_t* __restrict__ status,
                                                  EcItemWs* __restrict__ ws) {
   EC_RANGE(C);
-  const uint64_t p = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= end) return;
+  for (Walk wk = walk_units(end - beg); wk.u < wk.end; wk.u += wk.step) {
+  const uint64_t p = beg + wk.u;
   const uint32_t i = perm[p];
   const cg_item it = items[i];
   uint8_t st;
@@ -139,19 +139,20 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
     }
   }
   status[i] = st;
+  }
 }
 
 template <int C>
 __global__ void __launch_bounds__(256) k_ec_inv(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
                                                 const uint8_t* __restrict__ status, EcItemWs* __restrict__ ws) {
   EC_RANGE(C);
-  const uint64_t base = (uint64_t)beg + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * EC_INV_K;
-  if (base >= end) return;
-  const uint32_t cnt = (uint32_t)((end - base) < EC_INV_K ? (end - base) : EC_INV_K);
-  uint32_t sel = 0;
-  for (uint32_t k = 0; k < cnt; ++k) sel |= (uint32_t)(status[perm[base + k]] == EC_PENDING_BASE + C) << k;
-  if (!sel) return;
-  ecdsa_batch_inv<C, EC_INV_K>(ws + base, cnt, sel, c_ec[C]);
+  for (Walk wk = walk_units((end - beg + EC_INV_K - 1) / EC_INV_K); wk.u < wk.end; wk.u += wk.step) {
+    const uint64_t base = beg + wk.u * EC_INV_K;
+    const uint32_t cnt = (uint32_t)((end - base) < EC_INV_K ? (end - base) : EC_INV_K);
+    uint32_t sel = 0;
+    for (uint32_t k = 0; k < cnt; ++k) sel |= (uint32_t)(status[perm[base + k]] == EC_PENDING_BASE + C) << k;
+    if (sel) ecdsa_batch_inv<C, EC_INV_K>(ws + base, cnt, sel, c_ec[C]);
+  }
 }
 
 // Two launches over the curve's range, one per table mode (the plan keeps the modes in separate
@@ -166,16 +167,17 @@ __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ i
   const int cls = plan_class_of_curve(C);  // the plan's mode split (plan_sort.hip)
   const uint32_t beg = Full ? ranges[PLAN_FULL + cls] : ranges[cls];
   const uint32_t end = Full ? ranges[cls + 1] : ranges[PLAN_FULL + cls];
-  const uint64_t p = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= end) return;
-  const uint32_t i = perm[p];
-  if (status[i] != EC_PENDING_BASE + C) return;
-  const uint32_t key = items[i].key_idx;
-  const EcItemWs w = ws[p];
-  if (Full) {
-    status[i] = (uint8_t)ecdsa_ladder_check<C>(w.a, w.b, w.r, *gtab, tabs[key].ec, c_ec[C]);
-  } else {  // a key with few items: row 0 only (keyws.h)
-    status[i] = (uint8_t)ecdsa_ladder_check_row0<C>(w.a, w.b, w.r, *gtab, tabs[key].ec.t[0], c_ec[C]);
+  for (Walk wk = walk_units(end - beg); wk.u < wk.end; wk.u += wk.step) {
+    const uint64_t p = beg + wk.u;
+    const uint32_t i = perm[p];
+    if (status[i] != EC_PENDING_BASE + C) continue;
+    const uint32_t key = items[i].key_idx;
+    const EcItemWs w = ws[p];
+    if (Full) {
+      status[i] = (uint8_t)ecdsa_ladder_check<C>(w.a, w.b, w.r, *gtab, tabs[key].ec, c_ec[C]);
+    } else {  // a key with few items: row 0 only (keyws.h)
+      status[i] = (uint8_t)ecdsa_ladder_check_row0<C>(w.a, w.b, w.r, *gtab, tabs[key].ec.t[0], c_ec[C]);
+    }
   }
 }
 
@@ -222,13 +224,12 @@ template <int C>
 static void launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
                          uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len,
                          const ItemWs& iw, hipStream_t stream) {
-  const uint32_t B = 256;
-  const uint64_t grid = (n_items + B - 1) / B;  // a curve's range is at most n_items long
+  const uint32_t B = 256;  // a curve's range is at most n_items long
   EcItemWs* ws = (EcItemWs*)iw.slots;
-  hipLaunchKernelGGL(k_ec_prep<C>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
+  hipLaunchKernelGGL(k_ec_prep<C>, dim3(walk_grid(n_items, B, WALK_CAP(2))), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
                      d_arena, arena_len, d_msgs, msgs_len, mode, d_status, ws);
-  const uint64_t igrid = (n_items + (uint64_t)B * EC_INV_K - 1) / ((uint64_t)B * EC_INV_K);
-  hipLaunchKernelGGL(k_ec_inv<C>, dim3((unsigned)igrid), dim3(B), 0, stream, iw.perm, iw.ranges,
+  const unsigned igrid = walk_grid((n_items + EC_INV_K - 1) / EC_INV_K, B, WALK_CAP(2));
+  hipLaunchKernelGGL(k_ec_inv<C>, dim3(igrid), dim3(B), 0, stream, iw.perm, iw.ranges,
                      (const uint8_t*)d_status, ws);
 }
 
@@ -245,8 +246,7 @@ template <int C, bool Full>
 static void launch_ladder_t(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
                             const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
-  const uint64_t grid = (n_items + B - 1) / B;
-  hipLaunchKernelGGL((k_ec_ladder<C, Full>), dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
+  hipLaunchKernelGGL((k_ec_ladder<C, Full>), dim3(walk_grid(n_items, B, WALK_CAP(2))), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
                      w.tab, gtab(d_btab, C), d_status, (const EcItemWs*)iw.slots);
 }
 

@@ -225,14 +225,11 @@ static_assert(sizeof(EdDigits) == ITEM_SLOT, "digits must fill one item slot");
 #ifndef ED_HASH_WAVES_PER_SIMD
 #define ED_HASH_WAVES_PER_SIMD 3
 #endif
-__global__ void __launch_bounds__(256, ED_HASH_WAVES_PER_SIMD) k_ed_hash(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
-                                                 const uint32_t* __restrict__ ranges,
-                                                 const EdKeyHdr* __restrict__ hdr,
-                                                 const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                 const uint8_t* __restrict__ msgs, uint64_t msgs_len, uint32_t mode,
-                                                 uint8_t* __restrict__ status, EdDigits* __restrict__ dig) {
-  const uint64_t p = (uint64_t)ranges[PLAN_ED] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= ranges[PLAN_ED + 1]) return;
+__device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restrict__ items,
+                                            const uint32_t* __restrict__ perm, const EdKeyHdr* __restrict__ hdr,
+                                            const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                            const uint8_t* __restrict__ msgs, uint64_t msgs_len, uint32_t mode,
+                                            uint8_t* __restrict__ status, EdDigits* __restrict__ dig) {
   const uint32_t i = perm[p];
   const cg_item it = items[i];
   const EdKeyHdr* kh = hdr + it.key_idx;
@@ -277,6 +274,16 @@ __global__ void __launch_bounds__(256, ED_HASH_WAVES_PER_SIMD) k_ed_hash(const c
     st = (uint8_t)ED_PENDING;
   }
   status[i] = st;
+}
+
+__global__ void __launch_bounds__(256, ED_HASH_WAVES_PER_SIMD) k_ed_hash(
+    const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
+    const EdKeyHdr* __restrict__ hdr, const uint8_t* __restrict__ arena, uint64_t arena_len,
+    const uint8_t* __restrict__ msgs, uint64_t msgs_len, uint32_t mode, uint8_t* __restrict__ status,
+    EdDigits* __restrict__ dig) {
+  const uint32_t beg = ranges[PLAN_ED];
+  for (Walk w = walk_units(ranges[PLAN_ED + 1] - beg); w.u < w.end; w.u += w.step)
+    ed_hash_one(beg + w.u, items, perm, hdr, arena, arena_len, msgs, msgs_len, mode, status, dig);
 }
 
 // One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the row tables (B rows
@@ -437,23 +444,23 @@ __global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_pf(
     uint8_t* __restrict__ status, void* __restrict__ slots) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[4 * EdOps::kWaveBytes];
   const uint32_t beg = ranges[PLAN_FULL + PLAN_ED];
-  const uint32_t end = ranges[PLAN_ED + 1];
-  const uint64_t p = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= end) return;
-  const uint32_t i = perm[p];
-  const uint32_t key = items[i].key_idx;
-  if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
-    status[i] = CG_KEY_INVALID;
-    return;
-  }
-  if (status[i] != ED_PENDING) return;
-  // every lane still here runs the same DMA sequence; lanes that left do not take part, and
-  // the LDS image is per lane, so no barrier is needed
   uint8_t* wave_lds = stage + (threadIdx.x >> 6) * EdOps::kWaveBytes;
-  ge_p2 q;
-  ed_double_scalar_pf(q, (const uint32_t*)((const uint8_t*)slots + (size_t)p * ITEM_SLOT), tabs[key].ed, *btab,
-                      wave_lds, __lane_id());
-  ((ge_p2*)slots)[p] = q;
+  for (Walk w = walk_units(ranges[PLAN_ED + 1] - beg); w.u < w.end; w.u += w.step) {
+    const uint64_t p = beg + w.u;
+    const uint32_t i = perm[p];
+    const uint32_t key = items[i].key_idx;
+    if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
+      status[i] = CG_KEY_INVALID;
+      continue;
+    }
+    if (status[i] != ED_PENDING) continue;
+    // every lane still here runs the same DMA sequence; lanes that left do not take part, and
+    // the LDS image is per lane, so no barrier is needed
+    ge_p2 q;
+    ed_double_scalar_pf(q, (const uint32_t*)((const uint8_t*)slots + (size_t)p * ITEM_SLOT), tabs[key].ed, *btab,
+                        wave_lds, __lane_id());
+    ((ge_p2*)slots)[p] = q;
+  }
 }
 // One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the per-key rows and the
 // constant radix-2^10 B table (both in global memory; the B table stays L2-resident), left
@@ -468,23 +475,24 @@ __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
   // the plan's mode split: row-0 keys' items first, then full-table keys' (plan_sort.hip)
   const uint32_t beg = Full ? ranges[PLAN_FULL + PLAN_ED] : ranges[PLAN_ED];
   const uint32_t end = Full ? ranges[PLAN_ED + 1] : ranges[PLAN_FULL + PLAN_ED];
-  const uint64_t p = (uint64_t)beg + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= end) return;
-  const uint32_t i = perm[p];
-  const uint32_t key = items[i].key_idx;
-  if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
-    status[i] = CG_KEY_INVALID;
-    return;
+  for (Walk w = walk_units(end - beg); w.u < w.end; w.u += w.step) {
+    const uint64_t p = beg + w.u;
+    const uint32_t i = perm[p];
+    const uint32_t key = items[i].key_idx;
+    if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
+      status[i] = CG_KEY_INVALID;
+      continue;
+    }
+    if (status[i] != ED_PENDING) continue;
+    const EdDigits d = ((const EdDigits*)slots)[p];
+    ge_p2 q;
+    if (Full) {
+      ed_double_scalar_wb<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed, *btab, PickGlobal(), PickGlobal());
+    } else {  // a key with few items: row 0 only (keyws.h)
+      ed_double_scalar_row0<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed.t[0], *btab, PickGlobal(), PickGlobal());
+    }
+    ((ge_p2*)slots)[p] = q;
   }
-  if (status[i] != ED_PENDING) return;
-  const EdDigits d = ((const EdDigits*)slots)[p];
-  ge_p2 q;
-  if (Full) {
-    ed_double_scalar_wb<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed, *btab, PickGlobal(), PickGlobal());
-  } else {  // a key with few items: row 0 only (keyws.h)
-    ed_double_scalar_row0<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed.t[0], *btab, PickGlobal(), PickGlobal());
-  }
-  ((ge_p2*)slots)[p] = q;
 }
 
 // Encode + compare for 16 consecutive items per lane: one inversion per lane (Montgomery's
@@ -492,13 +500,10 @@ __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
 #ifndef ED_FINISH_K
 #define ED_FINISH_K 16
 #endif
-__global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
-                                                   const uint32_t* __restrict__ ranges,
-                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                   uint8_t* __restrict__ status, const ge_p2* __restrict__ rin) {
-  const uint32_t end = ranges[PLAN_ED + 1];
-  const uint64_t base = (uint64_t)ranges[PLAN_ED] + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * ED_FINISH_K;
-  if (base >= end) return;
+__device__ __forceinline__ void ed_finish_one(uint64_t base, uint32_t end, const cg_item* __restrict__ items,
+                                              const uint32_t* __restrict__ perm, const uint8_t* __restrict__ arena,
+                                              uint64_t arena_len, uint8_t* __restrict__ status,
+                                              const ge_p2* __restrict__ rin) {
   const uint32_t cnt = (uint32_t)((end - base) < ED_FINISH_K ? (end - base) : ED_FINISH_K);
   fe acc[ED_FINISH_K];
   fe run;
@@ -536,6 +541,15 @@ __global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ i
   }
 }
 
+__global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
+                                                   const uint32_t* __restrict__ ranges,
+                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                   uint8_t* __restrict__ status, const ge_p2* __restrict__ rin) {
+  const uint32_t beg = ranges[PLAN_ED], end = ranges[PLAN_ED + 1];
+  for (Walk w = walk_units((end - beg + ED_FINISH_K - 1) / ED_FINISH_K); w.u < w.end; w.u += w.step)
+    ed_finish_one(beg + w.u * ED_FINISH_K, end, items, perm, arena, arena_len, status, rin);
+}
+
 hipError_t ed_upload_constants() {
   Ed25519Consts h;
   ed_consts_init(h);
@@ -571,32 +585,32 @@ void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const uint8
 void ed_launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
                      uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len,
                      const ItemWs& iw, hipStream_t stream) {
-  const uint32_t B = 256;
-  const uint64_t grid = (n_items + B - 1) / B;  // the Ed25519 range is at most n_items long
-  hipLaunchKernelGGL(k_ed_hash, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
+  const uint32_t B = 256;  // the Ed25519 range is at most n_items long
+  const unsigned grid = walk_grid(n_items, B, WALK_CAP(ED_HASH_WAVES_PER_SIMD));
+  hipLaunchKernelGGL(k_ed_hash, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
                      arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
 }
 
 void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
                       const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
-  const uint64_t grid = (n_items + B - 1) / B;
+  const unsigned grid = walk_grid(n_items, B, WALK_CAP(full && ED_LADDER_PF ? ED_LADDER_PF_WAVES : ED_LADDER_WAVES_PER_SIMD));
   if (full && ED_LADDER_PF)
-    hipLaunchKernelGGL(k_ed_ladder_pf, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
+    hipLaunchKernelGGL(k_ed_ladder_pf, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
                        w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
   else if (full)
-    hipLaunchKernelGGL(k_ed_ladder<true>,dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
+    hipLaunchKernelGGL(k_ed_ladder<true>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
                        w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
   else
-    hipLaunchKernelGGL(k_ed_ladder<false>, dim3((unsigned)grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
+    hipLaunchKernelGGL(k_ed_ladder<false>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
                        w.hdr, w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
 }
 
 void ed_launch_finish(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
                       uint8_t* d_status, const ItemWs& iw, hipStream_t stream) {
   const uint32_t B = 256;
-  const uint64_t fgrid = (n_items + (uint64_t)B * ED_FINISH_K - 1) / ((uint64_t)B * ED_FINISH_K);
-  hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
+  const unsigned fgrid = walk_grid((n_items + ED_FINISH_K - 1) / ED_FINISH_K, B, WALK_CAP(2));
+  hipLaunchKernelGGL(k_ed_finish, dim3(fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
                      arena_len, d_status, (const ge_p2*)iw.slots);
 }
 

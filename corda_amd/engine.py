@@ -18,9 +18,9 @@ def _p(a):
 
 
 class Engine:
-    def __init__(self, device=0):
+    def __init__(self, device=0, chunk_items=0):
         L = _lib.lib()
-        cfg = _lib.cg_config(device, 0, 0, 0)
+        cfg = _lib.cg_config(device, 0, 0, 0, chunk_items)
         h = ctypes.c_void_p()
         _lib.check(L.cg_open(ctypes.byref(h), ctypes.byref(cfg)), f"cg_open(device={device})")
         self._h = h
@@ -171,3 +171,53 @@ class Engine:
                                                       n_sigs, _p(tmpls), len(tmpls), d_arena, arena_len, mode, d_ids,
                                                       d_tx_status, d_sig_status, stream or None)
         _lib.check(rc, "cg_verify_transactions_device")
+
+
+class EnginePool:
+    """One process, several devices (cg_pool): ``verify(batch)`` shards the items over the healthy
+    slots, re-runs a failed slot's shard elsewhere, and returns one status byte per item (items
+    no slot could run stay NOT_RUN and raise ``EngineUnavailable`` unless ``allow_partial``)."""
+
+    def __init__(self, devices, chunk_items=0):
+        L = _lib.lib()
+        cfg = _lib.cg_config(0, 0, 0, 0, chunk_items)
+        devs = (ctypes.c_int32 * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        _lib.check(L.cg_pool_open(ctypes.byref(h), devs, len(devices), ctypes.byref(cfg)), "cg_pool_open")
+        self._h = h
+        self.devices = list(devices)
+        self.last_stats = None
+
+    def close(self):
+        if self._h:
+            _lib.lib().cg_pool_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def healthy(self):
+        L = _lib.lib()
+        return [L.cg_pool_slot_healthy(self._h, k) == 1 for k in range(L.cg_pool_slots(self._h))]
+
+    def inject_fault(self, slot, fail=True):
+        _lib.check(_lib.lib().cg_pool_inject_fault(self._h, slot, 1 if fail else 0), "cg_pool_inject_fault")
+
+    def verify(self, batch, mode=MODE_DOVERIFY, allow_partial=False):
+        st = np.full(batch.n, 255, dtype=np.uint8)
+        stats = _lib.cg_pool_stats()
+        rc = _lib.lib().cg_pool_verify_batch(self._h, _p(batch.keys), len(batch.keys), _p(batch.items), batch.n,
+                                             _p(batch.arena), batch.arena.size, mode, _p(st), ctypes.byref(stats))
+        self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_pool_stats._fields_ if k != "reserved"}
+        if rc != 0 and not allow_partial:
+            _lib.check(rc, "cg_pool_verify_batch")
+        return st

@@ -143,8 +143,8 @@ def pack_signed_transactions(stxs):
         tx_rows.append((first, len(w.components) + 1, 0, bb._append(w.salt, 4)))
         for s in stx.sigs:
             k = bb.key(s.by.scheme, s.by.fmt, s.by.encoded)
-            sig_rows.append((bb._append(s.bytes, 4), t, k, len(s.bytes), tmpl_for(s.platform_version,
-                                                                                  s.scheme_number_id), 0))
+            sb = B.sig_field(s.by.scheme, s.bytes)
+            sig_rows.append((bb._append(sb, 4), t, k, len(sb), tmpl_for(s.platform_version, s.scheme_number_id), 0))
     built = bb.build()
     txs = np.array(tx_rows, dtype=B.TX_DTYPE) if tx_rows else np.zeros(0, B.TX_DTYPE)
     c = np.array(comps, dtype=B.COMPONENT_DTYPE) if comps else np.zeros(0, B.COMPONENT_DTYPE)

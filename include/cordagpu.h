@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define CG_ABI_VERSION 1
+#define CG_ABI_VERSION 2
 
 /* Corda SignatureScheme.schemeNumberID (Crypto.kt:78-184). Others => CG_UNSUPPORTED. */
 enum {
@@ -123,12 +123,23 @@ typedef struct cg_tx {
   uint64_t salt_off; /* 32-byte PrivacySalt value at arena[salt_off] (nonce = SHA256(salt||BE32(i))) */
 } cg_tx;             /* 24 bytes */
 
+/* Items per verify chunk when cg_config.chunk_items is 0. A call with more items is verified in
+ * ceil(n / chunk) equal chunks against key tables built once for the whole call (so the per-item
+ * workspace is bounded by the chunk, not the batch: BASELINE configs[4] streams 12.5M items per
+ * GPU through one call). */
+#define CG_DEFAULT_CHUNK_ITEMS (8u << 20)
+/* Host-buffer calls (cg_verify_batch) pipeline H2D of chunk k+1 against the verify of chunk k
+ * in chunks of at most this many items. */
+#define CG_PIPELINE_CHUNK_ITEMS (2u << 20)
+
 typedef struct cg_config {
-  int32_t device;        /* HIP device ordinal */
+  int32_t device;        /* HIP device ordinal (cg_open; cg_pool_open takes a device list) */
   uint32_t flags;        /* reserved, 0 */
   uint64_t max_items;    /* workspace sizing hint (0 = grow on demand) */
   uint64_t max_arena;    /* workspace sizing hint (0 = grow on demand) */
-} cg_config;
+  uint64_t chunk_items;  /* items per verify chunk (0 = CG_DEFAULT_CHUNK_ITEMS) */
+  uint64_t reserved[3];  /* must be 0 */
+} cg_config;             /* 48 bytes */
 
 typedef struct cg_stats {
   uint64_t n_items;
@@ -151,16 +162,26 @@ const char* cg_last_error(void); /* thread-local message for the last non-OK ret
 int cg_open(cg_ctx** out, const cg_config* cfg);
 void cg_close(cg_ctx* ctx);
 
-/* Host buffers in, host status bytes out. A batch of >= 2^17 items whose keys sit in the first quarter
- * of the arena is copied and verified in 4 consecutive item chunks, H2D of chunk k overlapping the
- * verify of chunk k-1 (stats: ms_h2d = until the first chunk is resident, ms_verify = the rest). */
+/* Host buffers in, host status bytes out (what a JNI caller hands over). The key table, the key
+ * bytes and the item table go first; then the items are verified in consecutive chunks of at most
+ * CG_PIPELINE_CHUNK_ITEMS, the arena bytes chunk k+1 needs (the extent of its items' signatures and
+ * messages) copying on a copy stream while chunk k verifies. Only the arena window the keys and
+ * items reference is copied. Best throughput when the caller appends (sig, clear) per item in item
+ * order after the keys (the layout corda_amd/batch.py and INTEGRATION.md use); any layout is
+ * correct. Lengths: sig_len and cg_key.len are 16-bit; a JVM signature longer than 65 535 bytes is
+ * packed as a surrogate with the same verdict. stats: ms_h2d = until the
+ * first chunk is resident, ms_verify = the rest. On CG_ERR_DEVICE every status byte is
+ * CG_NOT_RUN. */
 int cg_verify_batch(cg_ctx* ctx, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
                     const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
                     cg_stats* stats_opt);
 
-/* Device-resident buffers (HBM pointers) on the caller's HIP stream (hipStream_t as void*,
- * NULL = default stream). Asynchronous: returns after enqueueing; status is valid once the
- * stream has reached that point. Workspace comes from the ctx (reserve with cg_reserve). */
+/* Device-resident buffers (HBM pointers) on the caller's HIP stream (hipStream_t as void*; NULL =
+ * the context's own stream, not the legacy default stream). Asynchronous: returns after
+ * enqueueing; status is valid once the stream has reached that point. Workspace comes from the
+ * ctx (reserve with cg_reserve); consecutive calls on one ctx are ordered on the device (each call
+ * waits for the previous call's work, whatever stream either was enqueued on), because they share
+ * that workspace. */
 int cg_reserve(cg_ctx* ctx, uint32_t max_keys, uint64_t max_items);
 int cg_verify_batch_device(cg_ctx* ctx, const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items,
                            uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
@@ -288,6 +309,34 @@ int cg_verify_filtered(cg_ctx* ctx, const cg_filtered_tx* ftxs, uint64_t n_ftx, 
 int cg_verify_filtered_device(cg_ctx* ctx, const cg_filtered_tx* d_ftxs, uint64_t n_ftx, const cg_pmt_node* d_nodes,
                               uint64_t n_nodes, const cg_filtered_leaf* d_leaves, uint64_t n_leaves,
                               const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_status, void* hip_stream);
+
+/* ---- Several devices in one process (the JVM process drives every GPU of the node).
+ * A pool holds one cg_ctx per slot (a slot is a device ordinal; a device may appear twice).
+ * cg_pool_verify_batch cuts the items into contiguous, equal shards, one per healthy slot, runs
+ * each shard as a cg_verify_batch on its own host thread, and each shard's D2H copy lands in its
+ * slice of status_out (that copy is the gather). A shard whose device fails marks its slot
+ * unhealthy and is re-run on a healthy slot; items that could not run anywhere stay CG_NOT_RUN
+ * and the call returns CG_ERR_DEVICE, so the caller re-queues exactly those (the analogue of the
+ * verifier's Artemis redelivery, OutOfProcessTransactionVerifierService.kt:65-72). */
+typedef struct cg_pool cg_pool;
+typedef struct cg_pool_stats {
+  uint32_t shards;        /* shards of the first pass (= healthy slots at the call) */
+  uint32_t reruns;        /* shard re-runs after a failure */
+  uint32_t failed_slots;  /* slots that failed during this call (now unhealthy) */
+  uint32_t reserved;
+  uint64_t not_run;       /* items left CG_NOT_RUN */
+  double ms_total;
+} cg_pool_stats;
+int cg_pool_open(cg_pool** out, const int32_t* devices, uint32_t n_slots, const cg_config* cfg);
+void cg_pool_close(cg_pool* pool);
+uint32_t cg_pool_slots(const cg_pool* pool);
+int cg_pool_slot_healthy(const cg_pool* pool, uint32_t slot);  /* 1 healthy, 0 failed, -1 bad slot */
+int cg_pool_verify_batch(cg_pool* pool, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
+                         const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
+                         cg_pool_stats* stats_opt);
+/* Failure drill: make every later call on `slot` fail as a device fault would (fail = 1), or
+ * clear it and mark the slot healthy again (fail = 0). For tests and operational drills. */
+int cg_pool_inject_fault(cg_pool* pool, uint32_t slot, int fail);
 
 #ifdef __cplusplus
 }

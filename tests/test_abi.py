@@ -16,7 +16,7 @@ def test_library_exports_every_declared_symbol():
     syms = _lib.declared_symbols()
     assert len(syms) >= 17
     assert [s for s in syms if not hasattr(L, s)] == []
-    assert L.cg_abi_version() == 1
+    assert L.cg_abi_version() == 2
     assert b"gfx950" in L.cg_build_info()
 
 

@@ -98,6 +98,51 @@ def concat(batches, shuffle_seed=None):
     return Batch(keys, items, np.concatenate(arenas + [np.zeros(64, dtype=np.uint8)])), perm
 
 
+def notary_pool(n_unique, ed_keys=4096, ec_keys=1024, msg_len=270, seed=9, nthreads=8,
+                mix=(0.7, 0.2, 0.1), ed_corrupt_permille=120, ec_corrupt_permille=100):
+    """BASELINE configs[4]'s unique pool: n_unique items, 70% Ed25519 /
+    20% secp256r1 / 10% secp256k1 by default, every corruption class of Appendix A, shuffled.
+    Returns (Batch, labels, scheme_of_item)."""
+    ne = int(n_unique * mix[0])
+    nr = int(n_unique * mix[1])
+    nk = n_unique - ne - nr
+    parts, labs, sch = [], [], []
+    if ne:
+        e, le = ed25519_batch(ne, n_keys=ed_keys, msg_len=msg_len, corrupt_permille=ed_corrupt_permille, seed=seed,
+                              nthreads=nthreads)
+        parts.append(e), labs.append(le), sch.append(np.full(ne, 4, np.uint8))
+    for curve, cnt, scheme in ((1, nr, 3), (0, nk, 2)):
+        if cnt:
+            b, lb = ecdsa_batch(curve, cnt, n_keys=ec_keys, msg_len=msg_len, corrupt_permille=ec_corrupt_permille,
+                                seed=seed + 1 + curve, nthreads=nthreads)
+            parts.append(b), labs.append(lb), sch.append(np.full(cnt, scheme, np.uint8))
+    b, perm = concat(parts, shuffle_seed=seed + 7)
+    return b, np.concatenate(labs)[perm], np.concatenate(sch)[perm]
+
+
+def index_stream(pool, n_items, seed=10, replicate=False):
+    """n_items items drawn from `pool` by a seeded index stream (the engine sees every draw as
+    its own item: nothing is deduplicated). replicate=False: the items point into the pool's
+    arena. replicate=True: the arena holds one physical copy of the pool per 2^k draws, item i
+    pointing into copy i // len(pool), so every item has its own bytes and a host-buffer call
+    moves ~370 B per item over PCIe, as a real notary batch would. Returns (Batch, pool_index)."""
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, pool.n, n_items)
+    items = pool.items[idx]
+    arena = pool.arena
+    if replicate:
+        n_copies = (n_items + pool.n - 1) // pool.n
+        step = (pool.arena.size + 15) & ~15
+        arena = np.zeros(step * n_copies + 64, np.uint8)
+        for c in range(n_copies):
+            arena[c * step:c * step + pool.arena.size] = pool.arena
+        copy = (np.arange(n_items, dtype=np.uint64) // np.uint64(pool.n)) * np.uint64(step)
+        items["sig_off"] += copy
+        items["msg_off"] += copy
+        # keys stay in copy 0 (key table offsets unchanged)
+    return Batch(pool.keys, items, arena), idx
+
+
 class TxPipeline:
     """A packed config-4 workload: WireTransactions + their signatures (include/cordagpu.h
     layouts) and the generator's own tx ids and corruption labels."""

@@ -1,20 +1,32 @@
 #!/usr/bin/env python3
-"""Headline benchmark: verified signatures / second for the whole node (BASELINE.json).
+"""Headline benchmark: verified signatures / second for the whole node (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): per GPU, a batch of
-2^20 Ed25519 (EDDSA_ED25519_SHA512) signatures over 4096 keys and 270-byte
-SignableData-sized messages, 12% corrupted across Appendix A classes A1-A7, seeded
-synthetic data (no network, no JVM). One step = one full pass of the hot path over the
-batch with every input already resident in HBM: key prep (decode + tables for every key)
--> verify every item -> status bytes in HBM, plus (N > 1) the RCCL all-gather of the
-per-GPU verdict vectors, the engine's only collective.
+Workload (BASELINE configs[4], SURVEY.md §8(d) config 5, one GPU's shard): the notary-style
+mixed batch, 70% Ed25519 / 20% ECDSA secp256r1 / 10% ECDSA secp256k1, 12.5M items per GPU
+(100M over 8 GPUs), drawn by a seeded index stream from a 2^20-item unique pool with every
+Appendix A corruption class (~11% corrupted), 270-byte SignableData-sized messages, 4096 Ed25519
+keys and 1024 keys per curve. The arena holds one physical copy of the pool per 2^20 draws, so
+every item has its own bytes (4.7 GB per GPU). Synthetic data (no network, no JVM).
 
-Launch: ``python bench.py`` (N = 1) or ``torchrun --nproc-per-node N bench.py --gpus N``;
-one process per GPU, each verifying its own shard (weak scaling). Rank 0 prints ONE JSON
-line. ``roofline`` prices the dominant kernel (k_ed_verify) in 32x32->64 multiply-
-accumulates against the measured v_mad_u64_u32 peak (profiles/r01/ubench_int.json);
-``cpu_baseline`` is the C restatement of the reference's algorithms (oracle/c, "port")
-timed on a bounded sample on the host cores (rank 0, N = 1 only).
+One step = ONE cg_verify_batch_device call over the whole shard with every input resident in HBM:
+use counts + key tables (decode and row tables for every key), then the items in 8M-item device
+chunks (two of 6.25M), status bytes in HBM; plus (N > 1) the RCCL all-gather of the per-GPU
+verdict vectors, the engine's only collective. `value` = items of all ranks / max-over-ranks time.
+
+Launch: ``python bench.py`` (N = 1) or ``torchrun --nproc-per-node N bench.py --gpus N``; one
+process per GPU, each verifying its own shard (weak scaling). Rank 0 prints ONE JSON line.
+  roofline      the dominant kernel (k_ed_ladder_pf), priced in the 32x32->64 multiply-accumulates
+                its lane code executes (host-counted) over its per-launch time from HIP events
+                recorded on the stream it runs on, during the timed region (CG_FLAG_STAGE_TIMING);
+                peak = the measured v_mad_u64_u32 chip rate. traffic = PMC FETCH/WRITE bytes per
+                launch (profiles/r02, tools/pmc_traffic.py) when the committed profile matches.
+  cpu_baseline  the C restatement of the reference algorithms (oracle/c, "port") on a bounded sample
+                of the same workload, on the box's CPU quota (16 CPUs of a 256-thread EPYC) and on
+                one thread; plus BASELINE configs[0] (10k SignedTransactions, fail-fast
+                checkSignaturesAreValid) on the port and on OpenSSL, next to the GPU on that shape.
+  secondary     the PCIe-inclusive rate (host arena -> host verdicts through cg_verify_batch, the
+                JNI path) on the same workload, per-stage times, and at N = 1 the other BASELINE
+                configs: [1] 2^20 Ed25519, [2] 2^20 ECDSA 50/50, [3] 1M-transaction pipeline, tear-offs.
 """
 import argparse
 import json
@@ -29,28 +41,40 @@ sys.path.insert(0, ROOT)
 
 METRIC = "verified sigs/sec (whole node), Ed25519 + ECDSA-P256, at 1/2/4/8 MI355X"
 # Reference-algorithm work per Ed25519 verify, frozen from the C restatement of i2p 0.2.0
-# (oracle/c/ed25519_i2p.c counters): 1601 field multiplies + 1258
-# squarings per engineVerify (key decode excluded), each priced at 64 MAC32. Reported as
-# `i2p_equiv`: the rate at which the GPU retires the reference's own work.
+# (oracle/c/ed25519_i2p.c counters): 1601 field multiplies + 1258 squarings
+# per engineVerify (key decode excluded), each priced at 64 MAC32. Reported as `i2p_equiv`.
 N_FE_ED25519 = 2859
 MAC32_PER_ED25519 = N_FE_ED25519 * 64
-# Executed work of the GPU path per Ed25519 item, counted by the host build of the same lane
-# code (tests/native/host_kernels.cpp t_ed_verify_wb / t_ed_count_w6; pinned by
-# tests/test_host_kernels.py::test_executed_work_constants_match_lane_code).
-# (field multiplies, field squarings):
-ED_VERIFY_FE = (500, 24)   # k_ed_ladder: 43 + 26 mixed additions (-A rows W=6 in 2 windows, radix-2^10 B) + 6 doublings
+# Executed work of the GPU path, counted by the host build of the same lane code
+# (tests/native/host_kernels.cpp; pinned by tests/test_host_kernels.py::test_executed_work_*).
+# Ed25519 (field multiplies, squarings) in the radix-2^25.5 representation (fe25519.h):
+ED_VERIFY_FE = (500, 24)   # k_ed_ladder_pf: 43 + 26 mixed additions + 6 doublings
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
 ED_FINISH_K = 16
-# 32x32->64 products per operation in the radix-2^25.5 representation (fe25519.h)
 MAC_PER_MUL, MAC_PER_SQ = 100, 55
+MAC32_ED_LADDER = ED_VERIFY_FE[0] * MAC_PER_MUL + ED_VERIFY_FE[1] * MAC_PER_SQ
 MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
                           (ED_VERIFY_FE[1] + ED_FINISH_FE[1]) * MAC_PER_SQ +
                           (ED_INVERT_FE[0] * MAC_PER_MUL + ED_INVERT_FE[1] * MAC_PER_SQ) / ED_FINISH_K)
+# ECDSA: Montgomery products (mont29.h) per item: (k_ec_ladder full tables mod p, k_ec_inv mod n
+# per 16 items). One product = 81 a*b MACs + 9 per non-zero 29-bit limb of the modulus (q*m).
+# The ladder figure is its full schedule (every digit non-zero): a lane whose digit is zero skips
+# its addition, but the wave issues it for the other 63 lanes, so the full schedule is what the
+# SIMD executes (per-item mean 1% lower).
+EC_LADDER_MUL = {"secp256r1": 895, "secp256k1": 877}
+EC_INV_MUL_16 = {"secp256r1": 536, "secp256k1": 563}
+EC_MAC_PER_MUL_P = {"secp256r1": 144, "secp256k1": 162}
+EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
-# kernel generation whose PMC traffic profile is committed (profiles/r01/pmc_traffic.json)
-KERNEL_VERSION = "ed25519_v12"
+# kernel generation whose PMC traffic profile is committed (profiles/r02/pmc_traffic.json)
+KERNEL_VERSION = "r02_v1"
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+
+# Appendix A labels (tools/workload) -> the verdict Crypto.doVerify gives them (key decodes)
+ED_LABEL_EXPECT = {0: 0, 1: 1, 2: 1, 3: 1, 4: 0, 6: 1, 7: 2}       # A5 (high S) depends on slide()
+EC_LABEL_EXPECT = {0: 0, 1: 1, 2: 0, 3: 1, 6: 2, 7: 2}  # E5 (pad byte) is minimal when r >= 2^255
 
 
 def parse():
@@ -58,35 +82,73 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--items", type=int, default=1 << 20, help="items per GPU")
-    ap.add_argument("--keys", type=int, default=4096)
+    ap.add_argument("--items", type=int, default=12_500_000, help="items per GPU (configs[4]: 100M / 8)")
+    ap.add_argument("--pool", type=int, default=1 << 20, help="unique items the index stream draws from")
+    ap.add_argument("--ed-keys", type=int, default=4096)
+    ap.add_argument("--ec-keys", type=int, default=1024, help="keys per ECDSA curve")
     ap.add_argument("--msg-len", type=int, default=270)
-    ap.add_argument("--corrupt-permille", type=int, default=120)
+    ap.add_argument("--chunk-items", type=int, default=0, help="device chunk (0: CG_DEFAULT_CHUNK_ITEMS = 8M)")
     ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--host-steps", type=int, default=3, help="PCIe-inclusive cg_verify_batch calls (0: off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work for the baseline sample")
-    ap.add_argument("--threads", type=int, default=0, help="host threads for data generation / CPU baseline")
-    ap.add_argument("--ecdsa-items", type=int, default=1 << 18,
-                    help="items of the secondary ECDSA measurement (N = 1 only; 0 disables)")
-    ap.add_argument("--pipeline-txs", type=int, default=1 << 18,
-                    help="WireTransactions of the secondary config-4 pipeline measurement (N = 1 only; 0 disables)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
+    ap.add_argument("--threads", type=int, default=0, help="host threads (0: the CPU quota, at most 16)")
+    ap.add_argument("--configs1-items", type=int, default=1 << 20, help="configs[1] Ed25519 secondary (0: off)")
+    ap.add_argument("--ecdsa-items", type=int, default=1 << 20, help="configs[2] ECDSA 50/50 secondary (0: off)")
+    ap.add_argument("--pipeline-txs", type=int, default=1 << 20, help="configs[3] transaction pipeline (0: off)")
     ap.add_argument("--tear-offs", type=int, default=1 << 18, help="FilteredTransaction.verify secondary (0: off)")
-    ap.add_argument("--host-buffers", type=int, default=1, help="PCIe-inclusive cg_verify_batch secondary (0: off)")
-    ap.add_argument("--mixed-items", type=int, default=1 << 20,
-                    help="items of the secondary config-5-shaped mixed batch (N = 1 only; 0 disables)")
+    ap.add_argument("--configs0-txs", type=int, default=10_000, help="configs[0] SignedTransactions (0: off)")
     return ap.parse_args()
 
 
 def host_threads(req):
     if req > 0:
         return req
+    n = os.cpu_count() or 1
+    try:  # the container's CPU quota (the GPU box: 16 CPUs of a 256-thread host)
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
     env = os.environ.get("OMP_NUM_THREADS")
-    n = int(env) if env and env.isdigit() else 16
-    return max(1, min(n, os.cpu_count() or 1, 16))
+    if env and env.isdigit():
+        n = min(n, int(env))
+    return max(1, min(n, 16))
 
 
-def cpu_baseline(batch, seconds, threads):
-    """oracle/c (C restatement of i2p 0.2.0 / BC 1.57 semantics) on a bounded sample."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        return "unknown"
+
+
+def expected_verdicts(labels, schemes):
+    """Label -> verdict the reference gives (keys all decode in these workloads); 255 = no fixed
+    expectation (A5: the slide() carry rule decides)."""
+    exp = np.full(labels.size, 255, np.uint8)
+    ed = schemes == 4
+    for lab, v in ED_LABEL_EXPECT.items():
+        exp[ed & (labels == lab)] = v
+    for lab, v in EC_LABEL_EXPECT.items():
+        exp[~ed & (labels == lab)] = v
+    return exp
+
+
+def check_verdicts(st, exp):
+    m = exp != 255
+    bad = int(np.count_nonzero(st[m] != exp[m]))
+    return {"counts": {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
+            "checked_vs_labels": int(m.sum()), "label_mismatches": bad,
+            "not_run": int(np.count_nonzero(st == 255))}
+
+
+# ------------------------------------------------------------------------------------ CPU legs
+def cpu_baseline(batch, st_gpu, seconds, threads):
+    """oracle/c (C restatement of i2p 0.2.0 / BC 1.57 semantics) on a bounded sample of the
+    headline items, on `threads` threads and on one thread."""
     from corda_amd.batch import Batch
     from oracle import c_oracle
     probe = min(batch.n, 256 * threads)
@@ -99,65 +161,206 @@ def cpu_baseline(batch, seconds, threads):
     t = time.perf_counter()
     st = c_oracle.verify_batch(sub, 0, threads)
     dt = time.perf_counter() - t
+    n1 = max(64, min(n, int(n / threads / 2)))
+    sub1 = Batch(batch.keys, batch.items[:n1], batch.arena)
+    t = time.perf_counter()
+    c_oracle.verify_batch(sub1, 0, 1)
+    dt1 = time.perf_counter() - t
     return {"value": round(n / dt, 1), "unit": "sigs/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} items of the rank-0 batch (incl. key decode for all {len(batch.keys)} keys), "
-                      f"oracle/c or_verify_batch over {threads} threads, {dt:.1f} s; JVM reference "
-                      f"unavailable (no JDK / i2p / BouncyCastle jars on the box)"}, st
+            "sample": f"first {n} items of the rank-0 headline batch (70/20/10 mix; incl. decoding all "
+                      f"{len(batch.keys)} keys), oracle/c or_verify_batch over {threads} threads, {dt:.1f} s",
+            "host": f"{cpu_model()}; CPU quota {threads} CPUs (cgroup cpu.max) of {os.cpu_count()} hardware threads",
+            "serial_1thread": {"value": round(n1 / dt1, 1), "items": n1, "seconds": round(dt1, 2)},
+            "parity_on_sample": bool(np.array_equal(st, st_gpu[:n])),
+            "jvm": "JVM reference unavailable: no JDK, no i2p / BouncyCastle jars, no network"}
 
 
-def bench_mixed(a, wl, eng, dev, stream, run, threads):
-    """BASELINE configs[4] shape on one GPU: 70% Ed25519 / 20% secp256r1 / 10% secp256k1,
-    shuffled, no deduplication (ECDSA items are tiled from 65 536-item pools)."""
+def configs0(a, eng, wl, threads):
+    """BASELINE configs[0]: 10k SignedTransactions (GeneratedLedger shape: 1+Poisson(3) command
+    signers + the notary, ~5 Ed25519 signatures each over SignableData(id, metadata)), verified
+    with checkSignaturesAreValid semantics (serial per transaction, fail-fast,
+    TransactionWithSignatures.kt:58-61), transactions taken by workers from a shared counter
+    (Injectors.kt:18-55). CPU: oracle/c port and OpenSSL, on the CPU quota and on one thread.
+    GPU: every signature of every transaction in one cg_verify_batch call, the first failure per
+    transaction rebuilt in list order (corda_amd/transactions.py), checked against the port."""
+    import ctypes
+    from oracle import c_oracle
+    c0, tx_first, _ = wl.configs0(a.configs0_txs, seed=a.seed + 401, nthreads=threads)
+    n_tx, n_sig = len(tx_first) - 1, c0.n
+    L = c_oracle.lib()
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    L.or_check_txs.argtypes = [vp, u32, vp, vp, u64, vp, u64, vp, i32]
+    L.or_check_txs.restype = u64
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    tf = np.ascontiguousarray(tx_first, np.uint64)
+
+    def run(fn, nt, ntx):
+        ff = np.zeros(ntx, np.int64)
+        t = time.perf_counter()
+        done = fn(p(c0.keys), len(c0.keys), p(c0.items), p(tf), ntx, p(c0.arena), c0.arena.size, p(ff), nt)
+        return done, time.perf_counter() - t, ff
+
+    out = {"txs": n_tx, "sigs": n_sig, "shape": "GeneratedLedger-like: 1+Poisson(1) inputs, Poisson(3) outputs, "
+                                                 "1+Poisson(3) command signers + notary; Ed25519; 2% corrupted"}
+    done, dt, ff_port = run(L.or_check_txs, threads, n_tx)
+    out["port"] = {"sigs_per_s": round(done / dt, 1), "tx_per_s": round(n_tx / dt, 1), "threads": threads,
+                   "seconds": round(dt, 2)}
+    n1 = max(1, n_tx // 8)
+    done, dt, _ = run(L.or_check_txs, 1, n1)
+    out["port_1thread"] = {"sigs_per_s": round(done / dt, 1), "tx_per_s": round(n1 / dt, 1), "txs": n1}
+    so = os.path.join(ROOT, "tools", "cpu_baseline", "libosslcheck.so")
+    if os.path.exists(so):
+        O = ctypes.CDLL(so)
+        O.ob_check_txs.argtypes = [vp, u32, vp, vp, u64, vp, u64, vp, i32]
+        O.ob_check_txs.restype = ctypes.c_int64
+        done, dt, ff_ossl = run(O.ob_check_txs, threads, n_tx)
+        if done < 0:
+            out["openssl"] = "absent: libcrypto.so.3 could not be loaded"
+        else:
+            d1, dt1, _ = run(O.ob_check_txs, 1, n1)
+            out["openssl"] = {"sigs_per_s": round(done / dt, 1), "tx_per_s": round(n_tx / dt, 1),
+                              "threads": threads, "sigs_per_s_1thread": round(d1 / dt1, 1),
+                              "same_first_failures_as_port": bool(np.array_equal(ff_ossl, ff_port)),
+                              "note": "OpenSSL 3.0.2 EVP_DigestVerify, fresh EVP_PKEY per signature; rejects "
+                                      "S >= L where i2p 0.2.0 accepts it"}
+    else:
+        out["openssl"] = "absent: tools/cpu_baseline not built"
+    # GPU: one batch of all signatures, fail-fast rebuilt per transaction
+    eng.verify(c0)
+    t = time.perf_counter()
+    st = eng.verify(c0)
+    dt = time.perf_counter() - t
+    ff_gpu = np.full(n_tx, -1, np.int64)
+    bad = np.nonzero(st != 0)[0]
+    owner = np.searchsorted(tf, bad, side="right") - 1
+    for i, o in zip(bad[::-1], owner[::-1]):
+        ff_gpu[o] = i - tf[o]
+    out["gpu"] = {"sigs_per_s": round(n_sig / dt, 1), "tx_per_s": round(n_tx / dt, 1), "ms": round(dt * 1e3, 3),
+                  "path": "cg_verify_batch (host buffers, PCIe included), one call",
+                  "first_failures_equal_port": bool(np.array_equal(ff_gpu, ff_port))}
+    return out
+
+
+# ------------------------------------------------------------------------------------ GPU legs
+def upload(dev, b):
     import torch
-    n = a.mixed_items
-    ne, nr = int(n * 0.7), int(n * 0.2)
-    nk = n - ne - nr
-    e, _ = wl.ed25519_batch(ne, n_keys=a.keys, msg_len=a.msg_len, corrupt_permille=a.corrupt_permille,
-                            seed=a.seed + 101, nthreads=threads)
-    parts = [e]
-    for curve, cnt in ((1, nr), (0, nk)):
-        pool, _ = wl.ecdsa_batch(curve, min(cnt, 65536), n_keys=1024, msg_len=a.msg_len, corrupt_permille=100,
-                                 seed=a.seed + 103 + curve, nthreads=threads)
-        pool.items = np.resize(pool.items, cnt)
-        parts.append(pool)
-    b, _ = wl.concat(parts, shuffle_seed=a.seed + 107)
-    kd = torch.from_numpy(b.keys.view(np.uint8)).to(dev)
-    idd = torch.from_numpy(b.items.view(np.uint8)).to(dev)
-    ad = torch.from_numpy(b.arena).to(dev)
-    sd = torch.full((b.n,), 255, dtype=torch.uint8, device=dev)
-    steps = max(2, a.steps // 2)
-    el, km = run(kd, len(b.keys), idd, b.n, ad, int(b.arena.size), sd, steps, 1, False)
-    st = sd.cpu().numpy()
-    return {"value": round(b.n * steps / el, 1), "unit": "sigs/s", "items": b.n, "keys": len(b.keys),
-            "mix": {"ed25519": ne, "secp256r1": nr, "secp256k1": nk}, "kernel_ms": round(km, 3),
-            "ms_per_step": round(el / steps * 1e3, 3),
-            "verdicts": {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
+    up = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).to(dev)  # noqa: E731
+    return up(b.keys), up(b.items), up(b.arena), torch.full((b.n,), 255, dtype=torch.uint8, device=dev)
 
 
-def bench_ecdsa_mixed(a, wl, dev, run, pools, n):
-    """BASELINE configs[2] shape: one shuffled batch of n ECDSA items, half secp256r1 and half
-    secp256k1, 2048 keys per curve, ~10% corrupted (items tiled from the 65 536-item pools)."""
+def timed_device(eng, bufs, b, steps, warmup, stream, dev, gather=None):
     import torch
-    from corda_amd.batch import Batch
-    parts = [Batch(pools[c].keys, np.resize(pools[c].items, n // 2), pools[c].arena) for c in (1, 0)]
-    b, _ = wl.concat(parts, shuffle_seed=a.seed + 29)
-    kd = torch.from_numpy(b.keys.view(np.uint8)).to(dev)
-    idd = torch.from_numpy(b.items.view(np.uint8)).to(dev)
-    ad = torch.from_numpy(b.arena).to(dev)
-    sd = torch.full((b.n,), 255, dtype=torch.uint8, device=dev)
-    steps = max(2, a.steps // 2)
-    el, km = run(kd, len(b.keys), idd, b.n, ad, int(b.arena.size), sd, steps, 1, False)
-    st = sd.cpu().numpy()
-    return {"value": round(b.n * steps / el, 1), "unit": "sigs/s", "items": b.n, "keys": len(b.keys),
-            "kernel_ms": round(km, 3), "ms_per_step": round(el / steps * 1e3, 3),
-            "verdicts": {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
+    kd, idd, ad, sd = bufs
+    sptr = stream.cuda_stream
+
+    def step():
+        eng.verify_device(kd.data_ptr(), len(b.keys), idd.data_ptr(), b.n, ad.data_ptr(), b.arena.size,
+                          sd.data_ptr(), 0, sptr)
+        if gather is not None:
+            gather(sd)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    return step
 
 
-def bench_pipeline(a, wl, eng, dev, stream, threads):
-    """BASELINE configs[3] shape: WireTransaction ids (SHA-256 Merkle) for every transaction,
-    SignableData(id) spliced from the template, every signature verified -- one
-    cg_verify_transactions_device call per step. Also times the id pass alone (cg_tx_ids_device)
-    and reports its input bytes / time."""
+def stage_summary(times, steps_per_read):
+    out = {}
+    for name, (ms, n) in times.items():
+        if n:
+            out[name] = {"ms_per_step": round(ms / steps_per_read, 3), "launches": int(n),
+                         "ms_per_launch": round(ms / n, 3)}
+    return out
+
+
+def ladder_units(b, labels, schemes, chunk):
+    """Items that reach each ladder, per device chunk: Ed25519 items with a 64-byte signature,
+    ECDSA items whose DER parses and whose r, s are in range (labels 0-2)."""
+    sig64 = b.items["sig_len"] == 64
+    ed = (schemes == 4) & sig64
+    ok_ec = np.isin(labels, (0, 1, 2))
+    r1 = (schemes == 3) & ok_ec
+    k1 = (schemes == 2) & ok_ec
+    n = b.n
+    k = max(1, -(-n // chunk)) if chunk else 1
+    per = -(-n // k)
+    f = lambda m: [int(m[i:i + per].sum()) for i in range(0, n, per)]  # noqa: E731
+    return {"ed": f(ed), "r1": f(r1), "k1": f(k1)}
+
+
+def roofline(stages, units, steps):
+    """The dominant kernel's executed MAC32 over its average launch time (HIP events on its
+    stream). Also the ECDSA ladders, for the record."""
+    def block(stage, per_item, unit_counts, label):
+        ms, n = stages.get(stage, (0.0, 0))
+        if not n:
+            return None
+        launch_ms = ms / n
+        items = sum(unit_counts) / len(unit_counts)  # per launch (one launch per chunk per step)
+        ach = items * per_item / (launch_ms * 1e-3)
+        return {"kernel": label, "bound": "valu-int", "achieved": round(ach / 1e12, 3),
+                "peak": round(PEAK_MAC32_PER_S / 1e12, 3), "unit": "TMAC32/s", "frac": round(ach / PEAK_MAC32_PER_S, 4),
+                "launch_ms": round(launch_ms, 3), "launches": int(n), "items_per_launch": int(items),
+                "work_per_item": per_item}
+    ed = block("ed_ladder", MAC32_ED_LADDER, units["ed"], "k_ed_ladder_pf")
+    r1 = block("r1_ladder", EC_LADDER_MUL["secp256r1"] * EC_MAC_PER_MUL_P["secp256r1"], units["r1"],
+               "k_ec_ladder<secp256r1, full>")
+    k1 = block("k1_ladder", EC_LADDER_MUL["secp256k1"] * EC_MAC_PER_MUL_P["secp256k1"], units["k1"],
+               "k_ec_ladder<secp256k1, full>")
+    return ed, {"secp256r1": r1, "secp256k1": k1}
+
+
+def run_secondary_device(eng, dev, stream, b, steps=4):
+    """Device-resident rate of a secondary batch plus its item-kernel time (tables prebuilt)."""
+    import torch
+    bufs = upload(dev, b)
+    step = timed_device(eng, bufs, b, steps, 1, stream, dev)
+    eng.stage_times()
+    t = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t) / steps
+    stg = eng.stage_times()
+    st = bufs[3].cpu().numpy()
+    return el, st, stg
+
+
+def bench_configs1(a, eng, dev, stream, wl, threads):
+    b, labels = wl.ed25519_batch(a.configs1_items, n_keys=4096, msg_len=a.msg_len, corrupt_permille=120,
+                                 seed=a.seed + 7, nthreads=threads)
+    el, st, stg = run_secondary_device(eng, dev, stream, b)
+    units = ladder_units(b, labels, np.full(b.n, 4, np.uint8), eng_chunk(a))
+    ed, _ = roofline(stg, units, 4)
+    ver = check_verdicts(st, expected_verdicts(labels, np.full(b.n, 4, np.uint8)))
+    return {"value": round(b.n / el, 1), "unit": "sigs/s", "items": b.n, "keys": 4096, "ms_per_step": round(el * 1e3, 3),
+            "roofline": ed, "stages": stage_summary(stg, 4), "verdicts": ver}
+
+
+def eng_chunk(a):
+    return a.chunk_items or (8 << 20)
+
+
+def bench_ecdsa(a, eng, dev, stream, wl, threads):
+    """configs[2]: one shuffled batch, half secp256r1 / half secp256k1, 2048 keys per curve, ~10%
+    corrupted, every item unique."""
+    b, labels, schemes = wl.notary_pool(a.ecdsa_items, ec_keys=2048, msg_len=a.msg_len, seed=a.seed + 29,
+                                        nthreads=threads, mix=(0.0, 0.5, 0.5))
+    el, st, stg = run_secondary_device(eng, dev, stream, b)
+    units = ladder_units(b, labels, schemes, eng_chunk(a))
+    _, ec = roofline(stg, units, 4)
+    return {"value": round(b.n / el, 1), "unit": "sigs/s", "items": b.n, "keys": len(b.keys),
+            "ms_per_step": round(el * 1e3, 3), "roofline": ec, "stages": stage_summary(stg, 4),
+            "verdicts": check_verdicts(st, expected_verdicts(labels, schemes)),
+            "work_per_item_mac32": {c: EC_LADDER_MUL[c] * EC_MAC_PER_MUL_P[c] + EC_INV_MUL_16[c] * EC_MAC_PER_MUL_N[c] / 16
+                                    for c in EC_LADDER_MUL}}
+
+
+def bench_pipeline(a, eng, dev, stream, wl, threads):
+    """configs[3]: WireTransaction ids (SHA-256 Merkle) for every transaction, SignableData(id)
+    spliced from the template, every signature verified -- one cg_verify_transactions_device call
+    per step; the id pass alone timed too (SHA-256 compressions/s against the integer-VALU bound)."""
     import torch
     from corda_amd import _lib
     t0 = time.time()
@@ -171,19 +374,16 @@ def bench_pipeline(a, wl, eng, dev, stream, threads):
     ssd = torch.full((n_sig,), 255, dtype=torch.uint8, device=dev)
     sptr = stream.cuda_stream
     L = _lib.lib()
-    steps = max(2, a.steps // 2)
+    steps = 3
 
     def timed(fn):
         fn()
         torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t = time.perf_counter()
-        e0.record(stream)
         for _ in range(steps):
             fn()
-        e1.record(stream)
         torch.cuda.synchronize(dev)
-        return (time.perf_counter() - t) / steps, e0.elapsed_time(e1) / steps
+        return (time.perf_counter() - t) / steps
 
     def ids_only():
         _lib.check(L.cg_tx_ids_device(eng._h, txd.data_ptr(), n_tx, cd.data_ptr(), len(w.comps), ad.data_ptr(),
@@ -194,26 +394,43 @@ def bench_pipeline(a, wl, eng, dev, stream, threads):
                                        sgd.data_ptr(), n_sig, w.tmpls, ad.data_ptr(), len(w.arena), idd.data_ptr(),
                                        tsd.data_ptr(), ssd.data_ptr(), stream=sptr)
 
-    _, ids_ms = timed(ids_only)
-    el, full_ms = timed(full)
+    ids_s = timed(ids_only)
+    eng.stage_times()
+    el = timed(full)
+    stg = eng.stage_times()
     ids = idd.cpu().numpy().reshape(-1, 32)
     sst = ssd.cpu().numpy()
-    comp_bytes = int(w.comps["len"].astype(np.int64).sum())
+    lens = w.comps["len"].astype(np.int64)
+    comp_bytes = int(lens.sum())
+    # SHA-256 compressions of the id pass: per component nonce (1) + leaf (blob || nonce, or the
+    # salt blob alone), then 2 per Merkle node over the padded leaves
+    salt = (w.comps["flags"] & 1) == 1
+    leaf_blocks = np.where(salt, (lens + 9 + 63) // 64, (lens + 32 + 9 + 63) // 64)
+    nonce_blocks = np.where(salt, 0, 1)
+    ncomp = w.txs["n"].astype(np.int64)
+    padded = 1 << np.ceil(np.log2(np.maximum(ncomp, 1))).astype(np.int64)
+    comps_total = int(leaf_blocks.sum() + nonce_blocks.sum() + 2 * (padded - 1).sum())
+    rate = comps_total / ids_s
     parity = bool(np.array_equal(ids, w.ids) and np.all(sst[w.labels == 0] == 0) and np.all(sst[w.labels == 1] == 1))
-    return {"value": round(n_sig / el, 1), "unit": "sigs/s", "txs": n_tx, "sigs": n_sig,
-            "components": len(w.comps), "component_bytes": comp_bytes,
-            "tx_per_s": round(n_tx / el, 1), "ms_per_step": round(el * 1e3, 3), "kernel_ms": round(full_ms, 3),
-            "tx_ids": {"ms": round(ids_ms, 3), "tx_per_s": round(n_tx / (ids_ms * 1e-3), 1),
-                       "input_GBps": round(comp_bytes / (ids_ms * 1e-3) / 1e9, 1)},
-            "parity_vs_generator": parity, "gen_s": round(gen, 1),
-            "note": "BASELINE configs[3] is 1M txs; default 2^18 keeps host-side signing within the bench budget"}
+    return {"value": round(n_sig / el, 1), "unit": "sigs/s", "txs": n_tx, "sigs": n_sig, "components": len(w.comps),
+            "component_bytes": comp_bytes, "tx_per_s": round(n_tx / el, 1), "ms_per_step": round(el * 1e3, 3),
+            "stages": stage_summary(stg, steps),
+            "tx_ids": {"ms": round(ids_s * 1e3, 3), "tx_per_s": round(n_tx / ids_s, 1),
+                       "input_GBps": round(comp_bytes / ids_s / 1e9, 1),
+                       "hbm_frac": round(comp_bytes / ids_s / 8e12, 4),
+                       "sha256_compressions": comps_total,
+                       "valu_roofline": {"bound": "valu-int", "achieved_compressions_per_s": round(rate, 1),
+                                         "int_ops_per_compression": 2720,
+                                         "achieved_Tops": round(rate * 2720 / 1e12, 2),
+                                         "peak_Tops": 59.0, "frac": round(rate * 2720 / 59e12, 4),
+                                         "note": "peak = v_add_u32 chip rate (profiles/r01/ubench_int.json); "
+                                                 "2 720 32-bit ops per SHA-256 compression (SURVEY §8(d))"}},
+            "parity_vs_generator": parity, "gen_s": round(gen, 1)}
 
 
-def bench_tear_offs(a, wl, eng, dev, stream):
+def bench_tear_offs(a, eng, dev, stream, wl):
     """the non-validating notary's FilteredTransaction.verify for a batch of
-    tear-offs (inputs + notary visible out of ~11 components), one cg_verify_filtered_device call
-    per step. 4096 unique tear-offs are tiled to --tear-offs rows (no deduplication in the
-    engine). Work: SHA-256 compressions (visible leaves + 2 per partial-tree node)."""
+    tear-offs, one cg_verify_filtered_device call per step (4096 unique tiled, no dedup)."""
     import torch
     from corda_amd import merkle as M
     from corda_amd.batch import PMT_NODE
@@ -232,40 +449,37 @@ def bench_tear_offs(a, wl, eng, dev, stream):
 
     once()
     torch.cuda.synchronize(dev)
-    steps = max(2, a.steps // 2)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    steps = 4
     t0 = time.perf_counter()
-    e0.record(stream)
     for _ in range(steps):
         once()
-    e1.record(stream)
     torch.cuda.synchronize(dev)
     el = (time.perf_counter() - t0) / steps
-    km = e0.elapsed_time(e1) / steps
     st = sd.cpu().numpy()
     comp_leaf = int(((lv["len"].astype(np.int64) + 32 + 9 + 63) // 64).sum())
     comp_node = 2 * int(np.count_nonzero(n["kind"] == PMT_NODE))
     comp_per = (comp_leaf + comp_node) / len(t)
     return {"value": round(len(tt) / el, 1), "unit": "tear-offs/s", "tear_offs": len(tt), "unique": len(t),
-            "ms_per_step": round(el * 1e3, 3), "kernel_ms": round(km, 3),
-            "sha256_compressions_per_tear_off": round(comp_per, 2),
-            "sha256_compressions_per_s": round(len(tt) * comp_per / (km * 1e-3), 1),
+            "ms_per_step": round(el * 1e3, 3), "sha256_compressions_per_tear_off": round(comp_per, 2),
+            "sha256_compressions_per_s": round(len(tt) * comp_per / el, 1),
             "parity_vs_generator": bool(np.array_equal(st, np.tile(expect, reps)))}
 
 
-def bench_host_buffers(eng, batch, steps=3):
-    """The PCIe-inclusive rate: cg_verify_batch from pageable host buffers (H2D of keys, items
-    and arena, key prep, verify, D2H of the status bytes) on the headline batch."""
-    eng.verify(batch)
+def bench_host(eng, b, st_dev, steps):
+    """PCIe-inclusive: host arena -> host verdicts through cg_verify_batch (the JNI path) on the
+    headline shard: keys, items and ~370 B per item copied, chunk k+1's copy overlapping chunk k."""
+    st = eng.verify(b)
     t0 = time.perf_counter()
     for _ in range(steps):
-        eng.verify(batch)
+        st = eng.verify(b)
     el = (time.perf_counter() - t0) / steps
-    st = eng.last_stats
-    return {"value": round(batch.n / el, 1), "unit": "sigs/s", "items": batch.n,
-            "bytes_h2d": int(batch.arena.size + batch.items.nbytes + batch.keys.nbytes),
-            "ms_per_call": round(el * 1e3, 3), "cg_stats_ms": {k: round(v, 3) for k, v in st.items()
-                                                               if k.startswith("ms_")}}
+    s = eng.last_stats
+    return {"value": round(b.n / el, 1), "unit": "sigs/s", "items": b.n, "ms_per_call": round(el * 1e3, 3),
+            "bytes_h2d": int(b.arena.size + b.items.nbytes + b.keys.nbytes),
+            "h2d_GBps_effective": round((b.arena.size + b.items.nbytes) / el / 1e9, 1),
+            "cg_stats_ms": {k: round(v, 3) for k, v in s.items() if k.startswith("ms_")},
+            "verdicts_equal_device_path": bool(np.array_equal(st, st_dev)),
+            "path": "cg_verify_batch from pageable host memory (what a JNI caller hands over)"}
 
 
 def main():
@@ -287,158 +501,107 @@ def main():
     from corda_amd.engine import Engine
     from tools.workload import wl
 
-    # ---- synthetic shard for this rank (outside the timed region) ----
+    # ---- this rank's shard (outside the timed region)
     t0 = time.time()
-    batch, labels = wl.ed25519_batch(a.items, n_keys=a.keys, msg_len=a.msg_len,
-                                     corrupt_permille=a.corrupt_permille, seed=a.seed + 7919 * rank,
-                                     nthreads=threads)
+    pool, pool_labels, pool_schemes = wl.notary_pool(a.pool, ed_keys=a.ed_keys, ec_keys=a.ec_keys, msg_len=a.msg_len,
+                                                     seed=a.seed + 7919 * rank, nthreads=threads)
+    batch, idx = wl.index_stream(pool, a.items, seed=a.seed + 31 * rank + 1, replicate=True)
+    labels, schemes = pool_labels[idx], pool_schemes[idx]
     gen_s = time.time() - t0
-    eng = Engine(local)
+    eng = Engine(local, chunk_items=a.chunk_items, stage_timing=True)
     eng.reserve(len(batch.keys), batch.n)
-    keys_d = torch.from_numpy(batch.keys.view(np.uint8)).to(dev)
-    items_d = torch.from_numpy(batch.items.view(np.uint8)).to(dev)
-    arena_d = torch.from_numpy(batch.arena).to(dev)
-    status_d = torch.full((batch.n,), 255, dtype=torch.uint8, device=dev)
-    gathered_out = []
-    n_keys, n_items, arena_len = len(batch.keys), batch.n, int(batch.arena.size)
-    # one explicit stream for the engine, the timing events and the RCCL all-gather
     stream = torch.cuda.Stream(device=dev)
-    sptr = stream.cuda_stream
     torch.cuda.set_stream(stream)
+    bufs = upload(dev, batch)
+    gather = None
+    if world > 1:
+        gather = lambda sd: shard.gather_verdicts(sd, world * batch.n, world)  # noqa: E731  RCCL all-gather
+    step = timed_device(eng, bufs, batch, a.steps, a.warmup, stream, dev, gather)
+    eng.stage_times()  # drop the warmup's records
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    stages = eng.stage_times()
+    st = bufs[3].cpu().numpy()
 
-    def run(keys_t, n_keys_, items_t, n_items_, arena_t, arena_len_, status_t, steps, warmup, gather):
-        ev = []
+    # ---- verdict checks: labels, and every draw of a pool item gets that item's verdict
+    ver = check_verdicts(st, expected_verdicts(labels, schemes))
+    per_pool = np.full(pool.n, 255, np.uint8)
+    per_pool[idx] = st
+    ver["draws_consistent"] = bool(np.array_equal(per_pool[idx], st))
 
-        def step(timed, prepare=True):
-            if prepare:
-                # one-shot cg_verify_batch_device: key prep sized by each key's use count, then items
-                eng.verify_device(keys_t.data_ptr(), n_keys_, items_t.data_ptr(), n_items_, arena_t.data_ptr(),
-                                  arena_len_, status_t.data_ptr(), 0, sptr)
-            else:
-                # item kernels alone against the tables the last one-shot step built
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                eng.verify_items_device(keys_t.data_ptr(), n_keys_, items_t.data_ptr(), n_items_,
-                                        arena_t.data_ptr(), arena_len_, status_t.data_ptr(), 0, sptr)
-                e1.record(stream)
-                ev.append((e0, e1))
-            if gather and prepare:
-                # the engine's only collective: RCCL all-gather of the per-GPU verdict bytes
-                gathered_out.append(shard.gather_verdicts(status_t, world * n_items_, world))
+    units = ladder_units(batch, labels, schemes, eng_chunk(a))
+    roof, ec_roof = roofline(stages, units, a.steps)
+    if roof is not None:
+        roof["i2p_equiv_TMAC32"] = round(roof["achieved"] * MAC32_PER_ED25519 / MAC32_ED_LADDER, 3)
+        roof["traffic"] = None
+        if os.path.exists(TRAFFIC_FILE):
+            with open(TRAFFIC_FILE) as f:
+                tr = json.load(f)
+            if tr.get("kernel_version") == KERNEL_VERSION and tr.get("items") == a.items:
+                roof["traffic"] = tr.get("hbm_bytes_per_launch", {}).get("k_ed_ladder_pf")
+                roof["traffic_source"] = tr.get("source")
+                if "valu_issue" in tr:
+                    roof["valu_issue"] = tr["valu_issue"]
 
-        for _ in range(warmup):
-            step(False)
-        torch.cuda.synchronize(dev)
-        if gather:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t = time.perf_counter()
-        for _ in range(steps):
-            step(False)
-        torch.cuda.synchronize(dev)
-        if gather:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        el = time.perf_counter() - t
-        if gather:
-            tt = torch.tensor([el], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el = float(tt.item())
-        # item kernels alone (key tables already built by the last step), HIP events on the
-        # engine stream: the duration the roofline is priced on. Key preparation overlaps the
-        # item work inside a step, so a step's events would mix the two.
-        for _ in range(max(2, steps // 2)):
-            step(True, prepare=False)
-        torch.cuda.synchronize(dev)
-        return el, float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else float("nan")
-
-    elapsed, kern_ms = run(keys_d, n_keys, items_d, n_items, arena_d, arena_len, status_d, a.steps, a.warmup,
-                           world > 1)
-
-    extra = {}
-    if world == 1 and a.ecdsa_items > 0:
-        # BASELINE configs[2] shape (secp256r1 / secp256k1 batches), outside the headline value
-        pools = {}
-        for curve, name in ((1, "ecdsa_secp256r1"), (0, "ecdsa_secp256k1")):
-            pool = min(a.ecdsa_items, 65536)
-            eb, _ = wl.ecdsa_batch(curve, pool, n_keys=2048, msg_len=a.msg_len, corrupt_permille=100,
-                                   seed=a.seed + 17 + curve, nthreads=threads)
-            pools[curve] = eb
-            reps = max(1, a.ecdsa_items // pool)
-            items_rep = np.tile(eb.items, reps)
-            ek = torch.from_numpy(eb.keys.view(np.uint8)).to(dev)
-            ei = torch.from_numpy(items_rep.view(np.uint8)).to(dev)
-            ea = torch.from_numpy(eb.arena).to(dev)
-            es = torch.full((len(items_rep),), 255, dtype=torch.uint8, device=dev)
-            el, km = run(ek, len(eb.keys), ei, len(items_rep), ea, int(eb.arena.size), es, max(2, a.steps // 2), 1,
-                         False)
-            n_e = len(items_rep)
-            extra[name] = {"value": round(n_e * max(2, a.steps // 2) / el, 1), "unit": "sigs/s",
-                           "items": n_e, "unique_items": pool, "kernel_ms": round(km, 3)}
-        # configs[2] proper: one shuffled batch, half secp256r1 / half secp256k1, 4x --ecdsa-items
-        extra["ecdsa_mixed"] = bench_ecdsa_mixed(a, wl, dev, run, pools, 4 * a.ecdsa_items)
-    if world == 1 and a.mixed_items > 0:
-        extra["notary_mixed"] = bench_mixed(a, wl, eng, dev, stream, run, threads)
-    if world == 1 and a.pipeline_txs > 0:
-        extra["tx_pipeline"] = bench_pipeline(a, wl, eng, dev, stream, threads)
-    if world == 1 and a.tear_offs > 0:
-        extra["tear_offs"] = bench_tear_offs(a, wl, eng, dev, stream)
-    if world == 1 and a.host_buffers:
-        extra["host_buffers"] = bench_host_buffers(eng, batch)
-
-    st = status_d.cpu().numpy()
-    counts = {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}
-    # label sanity (full parity lives in tests/test_gpu_parity.py)
-    valid_ok = bool(np.all(st[labels == 0] == 0))
-
-    total_items = n_items * world * a.steps
-    value = total_items / elapsed
-    achieved = n_items * MAC32_EXEC_PER_ED25519 / (kern_ms * 1e-3)
-    i2p_equiv = n_items * MAC32_PER_ED25519 / (kern_ms * 1e-3)
-    roof = {"bound": "valu-int", "achieved": round(achieved / 1e12, 3), "peak": round(PEAK_MAC32_PER_S / 1e12, 3),
-            "unit": "TMAC32/s", "frac": round(achieved / PEAK_MAC32_PER_S, 4), "traffic": None,
-            "kernel": "k_ed_hash + k_ed_ladder + k_ed_finish (+ plan, k_misc_status, empty ECDSA launches)",
-            "kernel_ms": round(kern_ms, 3),
-            "work_per_item": f"executed: {MAC32_EXEC_PER_ED25519:.0f} MAC32 (field products the lane code "
-                             f"runs: {ED_VERIFY_FE[0] + ED_FINISH_FE[0]} mul x {MAC_PER_MUL} + "
-                             f"{ED_VERIFY_FE[1]} sq x {MAC_PER_SQ} + inversion/{ED_FINISH_K})",
-            "i2p_equiv": {"achieved": round(i2p_equiv / 1e12, 3), "unit": "TMAC32/s",
-                          "work_per_item": f"{N_FE_ED25519} i2p field mul/sq x 64 MAC32 = {MAC32_PER_ED25519}",
-                          "note": "reference algorithm's work / GPU time; exceeds peak because the row "
-                                  "tables do ~2.6x less work than i2p's sliding window"}}
-    traffic_file = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
-    if os.path.exists(traffic_file):
-        with open(traffic_file) as f:
-            tr = json.load(f)
-        if tr.get("items") == n_items and tr.get("kernel_version") == KERNEL_VERSION:
-            roof["traffic"] = tr.get("hbm_bytes_per_launch")
-            if "valu_issue" in tr:  # PMC SQ pass of the same build: issue-slot occupancy per kernel
-                roof["valu_issue"] = tr["valu_issue"]
-
+    extra = {"stages": stage_summary(stages, a.steps), "ecdsa_ladders": ec_roof}
+    if rank == 0 and world == 1 and a.host_steps > 0:
+        extra["host_e2e"] = bench_host(eng, batch, st, a.host_steps)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu, cst = cpu_baseline(batch, a.cpu_seconds, threads)
-        cpu["parity_on_sample"] = bool(np.array_equal(cst, st[:cst.size]))
+        cpu = cpu_baseline(batch, st, a.cpu_seconds, threads)
+        if a.configs0_txs > 0:
+            cpu["configs0"] = configs0(a, eng, wl, threads)
+    del bufs
+    torch.cuda.empty_cache()
+    if world == 1:
+        for name, on, fn in (("configs1_ed25519", a.configs1_items, lambda: bench_configs1(a, eng, dev, stream, wl, threads)),
+                             ("configs2_ecdsa", a.ecdsa_items, lambda: bench_ecdsa(a, eng, dev, stream, wl, threads)),
+                             ("configs3_tx_pipeline", a.pipeline_txs,
+                              lambda: bench_pipeline(a, eng, dev, stream, wl, threads)),
+                             ("tear_offs", a.tear_offs, lambda: bench_tear_offs(a, eng, dev, stream, wl))):
+            if on > 0:
+                extra[name] = fn()
+                torch.cuda.empty_cache()
 
     if rank == 0:
+        total = a.items * world * a.steps
+        n_ed, n_r1 = int((schemes == 4).sum()), int((schemes == 3).sum())
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "sigs/s", "n_gpus": world, "steps": a.steps,
+            "metric": METRIC, "value": round(total / elapsed, 1), "unit": "sigs/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic: seeded RFC 8032 Ed25519 signatures (tools/workload), no JVM capture",
-            "config": {"workload": "BASELINE configs[1]: 2^20 Ed25519 sigs per GPU, bit-exact verdicts incl. "
-                                   "corrupted sigs", "items_per_gpu": n_items, "keys": n_keys,
-                       "msg_len": a.msg_len, "corrupt_permille": a.corrupt_permille,
+            "data": "synthetic: seeded RFC 8032 Ed25519 + ECDSA (secp256r1/k1) signatures with every Appendix A "
+                    "corruption class (tools/workload), no JVM capture",
+            "config": {"workload": "BASELINE configs[4] per-GPU shard: notary-style mixed batch, 70% Ed25519 / 20% "
+                                   "secp256r1 / 10% secp256k1, 12.5M items per GPU (100M at 8 GPUs), inputs resident "
+                                   "in HBM, one cg_verify_batch_device call per step",
+                       "items_per_gpu": a.items, "unique_pool": a.pool, "mix": {"ed25519": n_ed, "secp256r1": n_r1,
+                                                                              "secp256k1": a.items - n_ed - n_r1},
+                       "keys": len(batch.keys), "msg_len": a.msg_len, "arena_bytes_per_gpu": int(batch.arena.size),
+                       "device_chunk_items": eng_chunk(a),
                        "parallelism": f"shard{world}" + ("+rccl_allgather(verdicts)" if world > 1 else "")},
-            "roofline": roof, "cpu_baseline": cpu, "secondary": extra,
-            "verdicts": {"counts": counts, "valid_labels_all_valid": valid_ok},
+            "roofline": roof, "cpu_baseline": cpu, "secondary": extra, "verdicts": ver,
             "gen_s": round(gen_s, 1),
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
     eng.close()
+    if ver["label_mismatches"] or ver["not_run"] or not ver["draws_consistent"]:
+        sys.exit(3)  # a wrong verdict voids the number
 
 
 if __name__ == "__main__":

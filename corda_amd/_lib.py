@@ -40,6 +40,9 @@ class cg_pool_stats(ctypes.Structure):
 
 
 ABI_VERSION = 2
+FLAG_STAGE_TIMING = 1
+STAGE_NAMES = ["plan", "ed_hash", "ed_ladder", "ed_ladder_row0", "ed_finish", "r1_front", "r1_ladder",
+               "r1_ladder_row0", "k1_front", "k1_ladder", "k1_ladder_row0"]
 
 
 def declared_symbols():
@@ -84,6 +87,9 @@ def lib():
                                                         u32, vp, vp, vp, vp]
             L.cg_verify_filtered.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u64, vp]
             L.cg_verify_filtered_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u64, vp, vp]
+            if hasattr(L, "cg_stage_times"):
+                L.cg_stage_times.argtypes = [vp, vp, vp, u32]
+                L.cg_stage_times.restype = i32
             pool = hasattr(L, "cg_pool_open")  # older builds (A/B variants) lack the pool
             if pool:
                 L.cg_pool_open.argtypes = [ctypes.POINTER(vp), vp, u32, ctypes.POINTER(cg_config)]

@@ -71,7 +71,7 @@ struct cg_ctx {
   bool fault = false;                       // cg_pool_inject_fault drill: every call fails
   hipStream_t stream = nullptr;
   cg::Fork fork = {{nullptr, nullptr, nullptr}, nullptr, {nullptr, nullptr}, {nullptr, nullptr, nullptr}, nullptr,
-                   {nullptr, nullptr, nullptr}};
+                   {nullptr, nullptr, nullptr}, nullptr};
   std::mutex mu;
   DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
   // transaction pipeline: verify items, spliced messages, templates; host-entry staging
@@ -87,6 +87,7 @@ struct cg_ctx {
   // before touching the shared workspace (async calls on different streams)
   hipEvent_t done = nullptr;
   bool done_rec = false;
+  cg::StageTimer timer;  // used when opened with CG_FLAG_STAGE_TIMING
 };
 
 namespace {
@@ -316,6 +317,7 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   cg_ctx* c = new cg_ctx();
   c->device = dev;
   if (cfg && cfg->chunk_items) c->chunk = cfg->chunk_items;
+  if (cfg && (cfg->flags & CG_FLAG_STAGE_TIMING)) c->fork.timer = &c->timer;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;
@@ -378,10 +380,38 @@ void cg_close(cg_ctx* c) {
   for (int k = 0; k < 4; ++k)
     if (c->tev[k]) hipEventDestroy(c->tev[k]);
   if (c->done) hipEventDestroy(c->done);
+  for (auto& r : c->timer.recs) {
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+  }
   for (int k = 0; k < 2; ++k)
     if (c->fork.ec_decoded[k]) hipEventDestroy(c->fork.ec_decoded[k]);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
+}
+
+int cg_stage_times(cg_ctx* c, double* ms_out, uint32_t* launches_out, uint32_t n) {
+  if (!c || (n && (!ms_out || !launches_out))) return fail(CG_ERR_ARG, "cg_stage_times: NULL argument");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  const uint32_t m = n < CG_STAGES ? n : CG_STAGES;
+  for (uint32_t k = 0; k < m; ++k) {
+    ms_out[k] = 0;
+    launches_out[k] = 0;
+  }
+  int rc = CG_OK;
+  for (auto& r : c->timer.recs) {
+    float ms = 0;
+    if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) rc = CG_ERR_DEVICE;
+    if ((uint32_t)r.stage < m) {
+      ms_out[r.stage] += ms;
+      launches_out[r.stage] += 1;
+    }
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+  }
+  c->timer.recs.clear();
+  return rc == CG_OK ? (int)m : fail(rc, "cg_stage_times: event wait failed");
 }
 
 int cg_reserve(cg_ctx* c, uint32_t max_keys, uint64_t max_items) {

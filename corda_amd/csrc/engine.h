@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/cordagpu.h"
 
 namespace cg {
@@ -22,9 +24,37 @@ struct DeviceConsts;  // opaque
 // built their class's tables, after `front` (the hashes / ECDSA prep on the main stream), while
 // the main stream runs the full-table ladders; the main stream joins on row0[k]. A few row-0
 // waves (long: 252 doublings) then overlap the full-table launch instead of trailing it.
+// Per-stage timing (cg_config.flags & CG_FLAG_STAGE_TIMING): a pair of events around each stage's
+// launches, recorded on the stream the stage runs on, so a stage's duration is measured where it
+// ran even when other stages overlap it on other streams. Read (and reset) with cg_stage_times.
+struct StageTimer {
+  struct Rec {
+    int stage;
+    hipEvent_t a, b;
+  };
+  std::vector<Rec> recs;
+  int mark(int stage, hipStream_t s) {
+    Rec r{stage, nullptr, nullptr};
+    if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return -1;
+    hipEventRecord(r.a, s);
+    recs.push_back(r);
+    return (int)recs.size() - 1;
+  }
+  void done(int idx, hipStream_t s) {
+    if (idx >= 0) hipEventRecord(recs[idx].b, s);
+  }
+};
+#define CG_TIME(fork, stage, stream, launch)                                   \
+  do {                                                                          \
+    const int _t = (fork) && (fork)->timer ? (fork)->timer->mark((stage), (stream)) : -1; \
+    launch;                                                                     \
+    if (_t >= 0) (fork)->timer->done(_t, (stream));                            \
+  } while (0)
+
 struct Fork {
   hipStream_t side[3];
   hipEvent_t start, ec_decoded[2], ready[3], front, row0[3];
+  StageTimer* timer;  // null unless the ctx was opened with CG_FLAG_STAGE_TIMING
 };
 
 // Upload the constant tables (curve constants, base-point tables) for the current device.

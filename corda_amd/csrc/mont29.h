@@ -21,6 +21,15 @@
 
 #define M29_MASK 0x1fffffffu
 
+// Host-build op counter (tests/native/host_kernels.cpp): Montgomery products per (curve, modulus),
+// the executed-work figure bench.py prices the ECDSA kernels with. Compiled out of the device build.
+#ifdef FE_OP_COUNT
+extern uint64_t g_m29_nmul[2][2];
+#define M29_COUNT(C, N) (++g_m29_nmul[C][N])
+#else
+#define M29_COUNT(C, N) ((void)0)
+#endif
+
 struct f29 {
   uint32_t v[9];
 };
@@ -100,6 +109,7 @@ CG_HD void f29_to_words(uint32_t w[8], const f29& a) {
 // r = a b R^-1 mod m, product scanning (bounds: header). r is reduced.
 template <int C, int N>
 CG_HD void m29_mul(f29& r, const f29& a, const f29& b) {
+  M29_COUNT(C, N);
   uint32_t q[9], out[9];
   fe_acc_t acc = 0;
 #pragma unroll

@@ -147,36 +147,47 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
   hipLaunchKernelGGL(k_misc_status, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
                      d_status);
   // plan: items sorted by (scheme class, key) (plan_sort.hip)
-  hipError_t e = launch_plan(d_items, n_items, d_keys, n_keys, (const uint32_t*)w.uses, iw, stream);
+  hipError_t e = hipSuccess;
+  CG_TIME(fork, CG_STAGE_PLAN, stream, e = launch_plan(d_items, n_items, d_keys, n_keys, (const uint32_t*)w.uses, iw, stream));
   if (e != hipSuccess) return e;
   // fronts: Ed25519 challenges (need only Abyte), ECDSA prep + s^-1 per curve (need the decoded key)
-  ed_launch_front(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
+  CG_TIME(fork, CG_STAGE_ED_HASH, stream,
+          ed_launch_front(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream));
   if (fork) hipStreamWaitEvent(stream, fork->ec_decoded[0], 0);
-  ec_launch_front(CG_CURVE_R1, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
+  CG_TIME(fork, CG_STAGE_R1_FRONT, stream,
+          ec_launch_front(CG_CURVE_R1, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
+                          stream));
   if (fork) hipStreamWaitEvent(stream, fork->ec_decoded[1], 0);
-  ec_launch_front(CG_CURVE_K1, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
+  CG_TIME(fork, CG_STAGE_K1_FRONT, stream,
+          ec_launch_front(CG_CURVE_K1, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
+                          stream));
   // row-0 ladders: on the side streams (after their tables) when forked, else first on `stream`
   if (fork) {
     e = hipEventRecord(fork->front, stream);
     for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->front, 0);
     if (e != hipSuccess) return e;
   }
-  ed_launch_ladder(false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[2] : stream);
-  ec_launch_ladder(CG_CURVE_R1, false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[0] : stream);
-  ec_launch_ladder(CG_CURVE_K1, false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[1] : stream);
+  CG_TIME(fork, CG_STAGE_ED_LADDER_ROW0, fork ? fork->side[2] : stream,
+          ed_launch_ladder(false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[2] : stream));
+  CG_TIME(fork, CG_STAGE_R1_LADDER_ROW0, fork ? fork->side[0] : stream,
+          ec_launch_ladder(CG_CURVE_R1, false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[0] : stream));
+  CG_TIME(fork, CG_STAGE_K1_LADDER_ROW0, fork ? fork->side[1] : stream,
+          ec_launch_ladder(CG_CURVE_K1, false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[1] : stream));
   if (fork) {
     for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventRecord(fork->row0[k], fork->side[k]);
     if (e != hipSuccess) return e;
   }
   // full-table ladders on `stream`, each after its tables; Ed25519 finish after both ladders
   if (fork) hipStreamWaitEvent(stream, fork->ready[2], 0);
-  ed_launch_ladder(true, d_items, n_items, d_status, w, iw, d_btab, stream);
+  CG_TIME(fork, CG_STAGE_ED_LADDER, stream, ed_launch_ladder(true, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) hipStreamWaitEvent(stream, fork->row0[2], 0);
-  ed_launch_finish(d_items, n_items, d_arena, arena_len, d_status, iw, stream);
+  CG_TIME(fork, CG_STAGE_ED_FINISH, stream, ed_launch_finish(d_items, n_items, d_arena, arena_len, d_status, iw, stream));
   if (fork) hipStreamWaitEvent(stream, fork->ready[0], 0);
-  ec_launch_ladder(CG_CURVE_R1, true, d_items, n_items, d_status, w, iw, d_btab, stream);
+  CG_TIME(fork, CG_STAGE_R1_LADDER, stream,
+          ec_launch_ladder(CG_CURVE_R1, true, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) hipStreamWaitEvent(stream, fork->ready[1], 0);
-  ec_launch_ladder(CG_CURVE_K1, true, d_items, n_items, d_status, w, iw, d_btab, stream);
+  CG_TIME(fork, CG_STAGE_K1_LADDER, stream,
+          ec_launch_ladder(CG_CURVE_K1, true, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) {
     hipStreamWaitEvent(stream, fork->row0[0], 0);
     hipStreamWaitEvent(stream, fork->row0[1], 0);

@@ -18,9 +18,9 @@ def _p(a):
 
 
 class Engine:
-    def __init__(self, device=0, chunk_items=0):
+    def __init__(self, device=0, chunk_items=0, stage_timing=False):
         L = _lib.lib()
-        cfg = _lib.cg_config(device, 0, 0, 0, chunk_items)
+        cfg = _lib.cg_config(device, _lib.FLAG_STAGE_TIMING if stage_timing else 0, 0, 0, chunk_items)
         h = ctypes.c_void_p()
         _lib.check(L.cg_open(ctypes.byref(h), ctypes.byref(cfg)), f"cg_open(device={device})")
         self._h = h
@@ -43,6 +43,16 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+    def stage_times(self):
+        """{stage: (ms, launches)} since the last read (Engine(stage_timing=True)); waits for the work."""
+        n = len(_lib.STAGE_NAMES)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_uint32 * n)()
+        rc = _lib.lib().cg_stage_times(self._h, ms, cnt, n)
+        if rc < 0:
+            _lib.check(rc, "cg_stage_times")
+        return {name: (ms[k], cnt[k]) for k, name in enumerate(_lib.STAGE_NAMES)}
 
     # ------------------------------------------------------------------ signatures
     def verify(self, batch, mode=MODE_DOVERIFY):

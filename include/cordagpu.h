@@ -132,6 +132,25 @@ typedef struct cg_tx {
  * in chunks of at most this many items. */
 #define CG_PIPELINE_CHUNK_ITEMS (2u << 20)
 
+/* cg_config.flags */
+#define CG_FLAG_STAGE_TIMING 1u /* time every item stage with HIP events on the stream it runs on (cg_stage_times) */
+
+/* Item stages reported by cg_stage_times (one launch per verify chunk each). */
+enum {
+  CG_STAGE_PLAN = 0,           /* k_misc_status + plan sort */
+  CG_STAGE_ED_HASH = 1,        /* k_ed_hash: SHA-512 challenges, scalar recoding */
+  CG_STAGE_ED_LADDER = 2,      /* k_ed_ladder_pf: full-table keys */
+  CG_STAGE_ED_LADDER_ROW0 = 3, /* k_ed_ladder<false>: keys with few items (side stream) */
+  CG_STAGE_ED_FINISH = 4,      /* k_ed_finish: batched inversion, encode, compare */
+  CG_STAGE_R1_FRONT = 5,       /* k_ec_prep + k_ec_inv, secp256r1 */
+  CG_STAGE_R1_LADDER = 6,
+  CG_STAGE_R1_LADDER_ROW0 = 7,
+  CG_STAGE_K1_FRONT = 8,       /* k_ec_prep + k_ec_inv, secp256k1 */
+  CG_STAGE_K1_LADDER = 9,
+  CG_STAGE_K1_LADDER_ROW0 = 10,
+  CG_STAGES = 11
+};
+
 typedef struct cg_config {
   int32_t device;        /* HIP device ordinal (cg_open; cg_pool_open takes a device list) */
   uint32_t flags;        /* reserved, 0 */
@@ -194,6 +213,12 @@ int cg_prepare_keys_device(cg_ctx* ctx, const cg_key* d_keys, uint32_t n_keys, c
 int cg_verify_items_device(cg_ctx* ctx, const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items,
                            uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
                            uint8_t* d_status, void* hip_stream);
+
+/* Per-stage device time since the last call (ctx opened with CG_FLAG_STAGE_TIMING): waits for the
+ * recorded work, then ms_out[stage] = summed event time of that stage's launches and
+ * launches_out[stage] = their number, for stage < min(n, CG_STAGES); resets the record. Returns
+ * the number of stages written. */
+int cg_stage_times(cg_ctx* ctx, double* ms_out, uint32_t* launches_out, uint32_t n);
 
 /* Hashing. digests_out: 32*n (sha256) / 64*n (sha512) bytes. */
 int cg_sha256_batch(cg_ctx* ctx, const cg_span* spans, uint64_t n, const uint8_t* arena, uint64_t arena_len,

@@ -159,6 +159,62 @@ int or_verify_batch(const cg_key* keys, uint32_t n_keys, const cg_item* items, u
   return 0;
 }
 
+/* ---- TransactionWithSignatures.checkSignaturesAreValid (TransactionWithSignatures.kt:58-61) over a
+ * batch of transactions, the BASELINE configs[0] CPU shape: workers take the next transaction from
+ * a shared counter (test-utils Injectors.kt:18-55 startTightLoopInjector style); a transaction's
+ * signatures are verified in list order through Crypto.doVerify semantics and the loop stops at
+ * the first failure (its exception escapes). Each signature's key is decoded with it: the JVM
+ * builds a fresh PublicKey object for TransactionSignature.by when it deserialises the
+ * SignedTransaction (Kryo.kt:330-339), so nothing is cached across transactions. */
+typedef struct {
+  const cg_key* keys;
+  uint32_t n_keys;
+  const cg_item* items;
+  const uint64_t* tx_first;
+  uint64_t n_tx;
+  const uint8_t* arena;
+  uint64_t arena_len;
+  int64_t* first_fail;
+  uint64_t* next;
+  uint64_t verified;
+} ckjob_t;
+
+static void* ck_worker(void* p) {
+  ckjob_t* j = (ckjob_t*)p;
+  uint64_t done = 0;
+  for (;;) {
+    const uint64_t t = __atomic_fetch_add(j->next, 1, __ATOMIC_RELAXED);
+    if (t >= j->n_tx) break;
+    int64_t ff = -1;
+    for (uint64_t i = j->tx_first[t]; i < j->tx_first[t + 1]; ++i) {
+      const cg_item* it = &j->items[i];
+      const int st = it->key_idx < j->n_keys
+                         ? or_verify_item(&j->keys[it->key_idx], it, j->arena, j->arena_len, CG_MODE_DOVERIFY)
+                         : CG_NOT_RUN;
+      ++done;
+      if (st != CG_VALID) {
+        ff = (int64_t)(i - j->tx_first[t]);
+        break;
+      }
+    }
+    j->first_fail[t] = ff;
+  }
+  __atomic_fetch_add(&((ckjob_t*)p)->verified, done, __ATOMIC_RELAXED);
+  return NULL;
+}
+
+uint64_t or_check_txs(const cg_key* keys, uint32_t n_keys, const cg_item* items, const uint64_t* tx_first,
+                      uint64_t n_tx, const uint8_t* arena, uint64_t arena_len, int64_t* first_fail, int nthreads) {
+  nthreads = resolve_threads(nthreads);
+  uint64_t next = 0;
+  ckjob_t j = {keys, n_keys, items, tx_first, n_tx, arena, arena_len, first_fail, &next, 0};
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, ck_worker, &j);
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  return j.verified;
+}
+
 /* ---- Merkle ---- */
 int or_merkle_root(const uint8_t* leaves, size_t n, uint8_t out[32]) {
   if (n == 0) return -1;

@@ -69,6 +69,11 @@ int or_verify_item(const cg_key* key, const cg_item* it, const uint8_t* arena, u
  * a PublicKey object once). Returns 0. */
 int or_verify_batch(const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
                     const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out, int nthreads);
+/* checkSignaturesAreValid over n_tx transactions (tx t = items[tx_first[t] .. tx_first[t+1])):
+ * first_fail[t] = index within the tx of the first signature that does not verify, or -1.
+ * Returns the number of signatures verified (fail-fast stops early). */
+uint64_t or_check_txs(const cg_key* keys, uint32_t n_keys, const cg_item* items, const uint64_t* tx_first,
+                      uint64_t n_tx, const uint8_t* arena, uint64_t arena_len, int64_t* first_fail, int nthreads);
 /* MerkleTree.getMerkleTree(leaves).hash; returns -1 on empty. */
 int or_merkle_root(const uint8_t* leaves, size_t n, uint8_t out[32]);
 /* WireTransaction.id for one tx; comp_offs/comp_lens index `arena`; salt leaf last. */

@@ -7,6 +7,7 @@
 #include "../../corda_amd/csrc/ed25519.h"
 #ifdef FE_OP_COUNT
 uint64_t g_fe_nmul = 0, g_fe_nsq = 0;
+uint64_t g_m29_nmul[2][2] = {{0, 0}, {0, 0}};
 #endif
 
 static Ed25519Consts g_C;
@@ -294,6 +295,60 @@ static int ecdsa_rows_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
   ecdsa_batch_inv<C, 1>(&ws, 1, 1u, K);
   return (int)ecdsa_ladder_check<C>(ws.a, ws.b, ws.r, *TG[C], *TQ, K);
 }
+// Executed Montgomery products per ECDSA item and stage (the GPU path's own lane code, host build):
+// out[0..1] k_ec_prep (mod p, mod n), out[2..3] k_ec_inv per item (one shared inversion over 16
+// items, EC_INV_K), out[4..5] k_ec_ladder with full tables. Returns the verdict.
+template <int C>
+static int ecdsa_count(const uint8_t* arena, uint64_t lr, uint64_t key_off, uint32_t key_len, uint32_t fmt,
+                       uint64_t sig_off, uint32_t sig_len, uint64_t msg_off, uint64_t msg_len, uint64_t* out) {
+#ifdef FE_OP_COUNT
+  (void)ecdsa_rows_verify<C>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len);  // tables
+  kinit();
+  const EcConsts& K = g_K[C];
+  static EcGTab* TG = nullptr;
+  static EcRowTab* TQ = new EcRowTab;
+  static EcRowScratch* S = new EcRowScratch;
+  if (!TG) {
+    TG = new EcGTab;
+    for (int l = 0; l < EC_G_DIGITS * (EC_G_MULT / EC_MULT); ++l)
+      ec_gtab_group<C>(&TG->t[l / (EC_G_MULT / EC_MULT)][(l % (EC_G_MULT / EC_MULT)) * EC_MULT],
+                       l / (EC_G_MULT / EC_MULT), l % (EC_G_MULT / EC_MULT), *S, K);
+  }
+  f29 xm, ym;
+  uint32_t st = ec_key_decode_bytes<C>(xm, ym, arena, lr, key_off, key_len, fmt, K);
+  if (st) return (int)st;
+  Jac bases[EC_ROWS];
+  ec_row_bases<C>(bases, xm, ym, K);
+  for (int j = 0; j < EC_ROWS; ++j) ec_row_build<C>(TQ->t[j], bases[j], *S, K);
+  auto snap = [&](uint64_t* o) {
+    o[0] = g_m29_nmul[C][0];
+    o[1] = g_m29_nmul[C][1];
+    g_m29_nmul[C][0] = g_m29_nmul[C][1] = 0;
+  };
+  g_m29_nmul[C][0] = g_m29_nmul[C][1] = 0;
+  EcItemWs ws[16];
+  st = ecdsa_prep<C>(ws[0], arena, lr, sig_off, sig_len, arena, lr, msg_off, msg_len);
+  snap(out);
+  if (st) return (int)st;
+  for (int k = 1; k < 16; ++k) ws[k] = ws[0];
+  ecdsa_batch_inv<C, 16>(ws, 16, 0xffffu, K);
+  snap(out + 2);
+  st = ecdsa_ladder_check<C>(ws[0].a, ws[0].b, ws[0].r, *TG, *TQ, K);
+  snap(out + 4);
+  return (int)st;
+#else
+  return -1;
+#endif
+}
+extern "C" int t_ecdsa_count(int scheme, const uint8_t* arena, uint64_t arena_len, uint64_t key_off, uint32_t key_len,
+                             uint32_t fmt, uint64_t sig_off, uint32_t sig_len, uint64_t msg_off, uint64_t msg_len,
+                             uint64_t* out) {
+  const uint64_t lr = (arena_len + 3) & ~3ull;
+  if (scheme == 3)
+    return ecdsa_count<CG_CURVE_R1>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len, out);
+  return ecdsa_count<CG_CURVE_K1>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len, out);
+}
+
 extern "C" int t_ecdsa_verify_rows(int scheme, const uint8_t* arena, uint64_t arena_len, uint64_t key_off,
                                    uint32_t key_len, uint32_t fmt, uint64_t sig_off, uint32_t sig_len,
                                    uint64_t msg_off, uint64_t msg_len) {

@@ -214,6 +214,42 @@ def test_executed_work_constants_match_lane_code():
     assert (mul_i, sq_i) == bench.ED_INVERT_FE, (mul_i, sq_i)
 
 
+def test_executed_work_constants_ecdsa():
+    """bench.py prices the ECDSA ladders and batched inversions with the Montgomery products the
+    lane code executes; those constants must equal what the host build counts, and the MACs per
+    product must follow from the moduli's non-zero 29-bit limbs (81 a*b + 9 per limb of q*m)."""
+    import ctypes
+    import bench
+    lib = hostk.lib()
+    lib.t_ecdsa_count.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                  ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                  ctypes.c_void_p]
+    moduli = {"secp256r1": (2**256 - 2**224 + 2**192 + 2**96 - 1,
+                            0xffffffff00000000ffffffffffffffffbce6faada7179e84f3b9cac2fc632551),
+              "secp256k1": (2**256 - 2**32 - 977, 0xfffffffffffffffffffffffffffffffebaaedce6af48a03bbfd25e8cd0364141)}
+    nnz = lambda m: sum(1 for i in range(9) if (m >> (29 * i)) & (2**29 - 1))  # noqa: E731
+    for name, scheme in (("secp256r1", 3), ("secp256k1", 2)):
+        p, n = moduli[name]
+        assert bench.EC_MAC_PER_MUL_P[name] == 81 + 9 * nnz(p)
+        assert bench.EC_MAC_PER_MUL_N[name] == 81 + 9 * nnz(n)
+        from tools.workload import wl
+        b, _ = wl.ecdsa_batch(1 if scheme == 3 else 0, 256, n_keys=8, corrupt_permille=0, seed=3, nthreads=4)
+        lad = []
+        for i in range(b.n):
+            it = b.items[i]
+            k = b.keys[it["key_idx"]]
+            out = np.zeros(6, np.uint64)
+            assert lib.t_ecdsa_count(scheme, ptr(b.arena), b.arena.size, int(k["off"]), int(k["len"]), int(k["fmt"]),
+                                     int(it["sig_off"]), int(it["sig_len"]), int(it["msg_off"]), int(it["msg_len"]),
+                                     ptr(out)) == 0
+            assert int(out[5]) == 0 and int(out[2]) == 0 and int(out[0]) == 0 and int(out[1]) == 0, (name, out)
+            assert int(out[3]) == bench.EC_INV_MUL_16[name], (name, out)
+            lad.append(int(out[4]))
+        # the wave's schedule: a mixed addition is skipped only when all 64 lanes' digits are zero,
+        # so a wave issues the per-item maximum over random items (the mean is ~1% lower)
+        assert max(lad) == bench.EC_LADDER_MUL[name] and np.mean(lad) > 0.97 * max(lad), (name, lad)
+
+
 @pytest.mark.parametrize("fn", ["t_ecdsa_verify_rows"])
 def test_ecdsa_lane_verify_on_fixtures(fn):
     """ECDSA lane code (the row-table pipeline: key decode -> rows -> prep -> batched

@@ -1,0 +1,106 @@
+/* BASELINE configs[0] CPU reference point with OpenSSL (bench.py cpu_baseline.configs0.openssl):
+ * the same checkSignaturesAreValid loop as oracle/c or_check_txs (fail-fast per transaction,
+ * workers pulling the next transaction from a shared counter), each Ed25519 signature verified
+ * with EVP_DigestVerify on a fresh EVP_PKEY (the JVM builds a fresh PublicKey per deserialised
+ * transaction). An industrial point of comparison, NOT the oracle: OpenSSL rejects S >= L, which
+ * i2p 0.2.0 accepts. libcrypto is loaded with dlopen; without it the entry
+ * point returns -1 and bench.py records it as absent. Not product code. */
+#include <dlfcn.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <unistd.h>
+
+#include "../../include/cordagpu.h"
+
+#define NID_ED25519_ 1087
+typedef void* (*pkey_new_raw_fn)(int, void*, const unsigned char*, size_t);
+typedef void* (*md_ctx_new_fn)(void);
+typedef void (*md_ctx_free_fn)(void*);
+typedef void (*pkey_free_fn)(void*);
+typedef int (*dv_init_fn)(void*, void**, const void*, void*, void*);
+typedef int (*dv_fn)(void*, const unsigned char*, size_t, const unsigned char*, size_t);
+
+static struct {
+  pkey_new_raw_fn pkey_new_raw;
+  md_ctx_new_fn md_ctx_new;
+  md_ctx_free_fn md_ctx_free;
+  pkey_free_fn pkey_free;
+  dv_init_fn dv_init;
+  dv_fn dv;
+  int ok;
+} F;
+
+static int load(void) {
+  if (F.ok) return 1;
+  void* h = dlopen("libcrypto.so.3", RTLD_NOW | RTLD_LOCAL);
+  if (!h) return 0;
+  F.pkey_new_raw = (pkey_new_raw_fn)dlsym(h, "EVP_PKEY_new_raw_public_key");
+  F.md_ctx_new = (md_ctx_new_fn)dlsym(h, "EVP_MD_CTX_new");
+  F.md_ctx_free = (md_ctx_free_fn)dlsym(h, "EVP_MD_CTX_free");
+  F.pkey_free = (pkey_free_fn)dlsym(h, "EVP_PKEY_free");
+  F.dv_init = (dv_init_fn)dlsym(h, "EVP_DigestVerifyInit");
+  F.dv = (dv_fn)dlsym(h, "EVP_DigestVerify");
+  F.ok = F.pkey_new_raw && F.md_ctx_new && F.md_ctx_free && F.pkey_free && F.dv_init && F.dv;
+  return F.ok;
+}
+
+/* 1 valid, 0 not (any failure: OpenSSL has no exception split) */
+static int verify_one(const cg_key* k, const cg_item* it, const uint8_t* arena, uint64_t arena_len) {
+  if (k->scheme != CG_EDDSA_ED25519_SHA512 || k->fmt != CG_KEY_RAW || k->len != 32) return 0;
+  if (k->off + 32 > arena_len || it->sig_off + it->sig_len > arena_len || it->msg_off + it->msg_len > arena_len)
+    return 0;
+  void* pk = F.pkey_new_raw(NID_ED25519_, NULL, arena + k->off, 32);
+  if (!pk) return 0;
+  void* ctx = F.md_ctx_new();
+  int ok = ctx && F.dv_init(ctx, NULL, NULL, NULL, pk) == 1 &&
+           F.dv(ctx, arena + it->sig_off, it->sig_len, arena + it->msg_off, it->msg_len) == 1;
+  if (ctx) F.md_ctx_free(ctx);
+  F.pkey_free(pk);
+  return ok;
+}
+
+typedef struct {
+  const cg_key* keys;
+  uint32_t n_keys;
+  const cg_item* items;
+  const uint64_t* tx_first;
+  uint64_t n_tx;
+  const uint8_t* arena;
+  uint64_t arena_len;
+  int64_t* first_fail;
+  uint64_t next, verified;
+} job_t;
+
+static void* worker(void* p) {
+  job_t* j = (job_t*)p;
+  uint64_t done = 0;
+  for (;;) {
+    const uint64_t t = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+    if (t >= j->n_tx) break;
+    int64_t ff = -1;
+    for (uint64_t i = j->tx_first[t]; i < j->tx_first[t + 1]; ++i) {
+      const cg_item* it = &j->items[i];
+      ++done;
+      if (it->key_idx >= j->n_keys || !verify_one(&j->keys[it->key_idx], it, j->arena, j->arena_len)) {
+        ff = (int64_t)(i - j->tx_first[t]);
+        break;
+      }
+    }
+    j->first_fail[t] = ff;
+  }
+  __atomic_fetch_add(&j->verified, done, __ATOMIC_RELAXED);
+  return NULL;
+}
+
+int64_t ob_check_txs(const cg_key* keys, uint32_t n_keys, const cg_item* items, const uint64_t* tx_first,
+                     uint64_t n_tx, const uint8_t* arena, uint64_t arena_len, int64_t* first_fail, int nthreads) {
+  if (!load()) return -1;
+  if (nthreads <= 0) nthreads = 1;
+  job_t j = {keys, n_keys, items, tx_first, n_tx, arena, arena_len, first_fail, 0, 0};
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, worker, &j);
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  return (int64_t)j.verified;
+}

@@ -227,6 +227,38 @@ def tx_pipeline(n_tx, n_keys=1024, seed=4, corrupt_permille=20, nthreads=8, comp
     return TxPipeline(txs, comps, keys, sigs, tmpls, arena[:arena_len + 64], ids.reshape(-1, 32), labels)
 
 
+def configs0(n_tx, seed=11, nthreads=8, n_keys=1024, corrupt_permille=20):
+    """BASELINE configs[0]: n_tx SignedTransactions of the tx_pipeline shape, each signature's
+    clear data materialised as SignableData(id, metadata) bytes (prefix || id || suffix), items of
+    a transaction contiguous and in list order. Returns (Batch, tx_first [n_tx + 1], labels)."""
+    from corda_amd.batch import ITEM_DTYPE
+    w = tx_pipeline(n_tx, n_keys=n_keys, seed=seed, corrupt_permille=corrupt_permille, nthreads=nthreads)
+    t = w.tmpls[0]
+    pre = w.arena[int(t["prefix_off"]):int(t["prefix_off"]) + int(t["prefix_len"])]
+    suf = w.arena[int(t["suffix_off"]):int(t["suffix_off"]) + int(t["suffix_len"])]
+    mlen = pre.size + 32 + suf.size
+    stride = (64 + mlen + 3) & ~3
+    n = len(w.sigs)
+    kbytes = 32 * n_keys
+    base = (kbytes + 15) & ~15
+    rows = np.zeros((n, stride), np.uint8)
+    so = w.sigs["sig_off"].astype(np.int64)
+    rows[:, :64] = w.arena[so[:, None] + np.arange(64)]
+    rows[:, 64:64 + pre.size] = pre
+    rows[:, 64 + pre.size:64 + pre.size + 32] = w.ids[w.sigs["tx_idx"]]
+    rows[:, 64 + pre.size + 32:64 + mlen] = suf
+    arena = np.concatenate([w.arena[:kbytes], np.zeros(base - kbytes, np.uint8), rows.reshape(-1),
+                            np.zeros(64, np.uint8)])
+    items = np.zeros(n, ITEM_DTYPE)
+    items["sig_off"] = base + stride * np.arange(n)
+    items["msg_off"] = items["sig_off"] + 64
+    items["msg_len"] = mlen
+    items["key_idx"] = w.sigs["key_idx"]
+    items["sig_len"] = 64
+    tx_first = np.concatenate([[0], np.cumsum(np.bincount(w.sigs["tx_idx"], minlength=n_tx))]).astype(np.uint64)
+    return Batch(w.keys, items, arena), tx_first, w.labels
+
+
 class _Sha256Host:
     """hashlib stand-in for the engine when building bench inputs (tree node hashes)."""
 

@@ -25,23 +25,32 @@ import numpy as np
 
 from . import batch as B
 from . import signable
-from .crypto import BatchItem, Crypto, IllegalArgumentException, PublicKey, SCHEME_CODE_NAMES
+from .composite import is_fulfilled_by
+from .crypto import (BatchItem, Crypto, HOST_EXCEPTION, IllegalArgumentException, PublicKey,  # noqa: F401
+                     SCHEME_CODE_NAMES, GPU_SCHEMES, SignatureException, TransactionSignature)
 
 
-class SignaturesMissingException(Exception):
-    def __init__(self, missing, tx_id):
-        super().__init__(f"Missing signatures for {sorted(k.encoded.hex() for k in missing)} on transaction "
-                         f"{tx_id.hex()}")
-        self.missing = missing
-        self.tx_id = tx_id
+class SignaturesMissingException(SignatureException):
+    """SignedTransaction.SignaturesMissingException (SignedTransaction.kt:171-172): a
+    SignatureException carrying the missing keys, their descriptions and the transaction id."""
+
+    def __init__(self, missing, descriptions, tx_id):
+        super().__init__(f"Missing signatures for {list(descriptions)} on transaction {bytes(tx_id).hex().upper()[:6]} "
+                         f"for {', '.join(repr(k) for k in missing)}")
+        self.missing = set(missing)
+        self.descriptions = list(descriptions)
+        self.id = tx_id
+
+    @property
+    def tx_id(self):
+        return self.id
 
 
 @dataclass(frozen=True)
-class TransactionSignature:
-    bytes: bytes
-    by: PublicKey
-    platform_version: int = 1
-    scheme_number_id: int = 4
+class Command:
+    """A command's value (its toString) and signers (Structures.kt Command(value, signers))."""
+    value: str
+    signers: tuple
 
 
 @dataclass
@@ -49,6 +58,23 @@ class SignedTransaction:
     id: bytes
     sigs: list
     required_signing_keys: set = field(default_factory=set)
+    commands: list = field(default_factory=list)   # Command, for getKeyDescriptions
+    notary: object = None                          # the notary's owning key
+
+
+def get_key_descriptions(stx, keys):
+    """SignedTransaction.getKeyDescriptions (SignedTransaction.kt:65-75)."""
+    out = [c.value for c in getattr(stx, "commands", []) if any(k in keys for k in c.signers)]
+    if getattr(stx, "notary", None) is not None and stx.notary in keys:
+        out.append("notary")
+    return out
+
+
+def get_missing_signatures(stx):
+    """TransactionWithSignatures.getMissingSignatures (TransactionWithSignatures.kt:72-78): the
+    required keys not fulfilled by the signatures' keys (composite-aware, CryptoUtils.kt:88-92)."""
+    sig_keys = {s.by for s in stx.sigs}
+    return {k for k in stx.required_signing_keys if not is_fulfilled_by(k, sig_keys)}
 
 
 def _items(stxs, signable_data):
@@ -60,13 +86,7 @@ def _items(stxs, signable_data):
     return items, owner
 
 
-def check_signatures_are_valid_batch(stxs, signable_data, crypto=Crypto):
-    """Verifies all signatures of all transactions in one GPU batch.
-
-    Returns, per transaction, None if every signature verified, else (index, exception)
-    for the FIRST failing signature in list order (the one the serial loop would throw)."""
-    items, owner = _items(stxs, signable_data)
-    status = crypto.verify_batch(items, B.MODE_DOVERIFY) if items else np.zeros(0, np.uint8)
+def _first_failures(stxs, status, errors, crypto):
     result = [None] * len(stxs)
     pos = 0
     for t, stx in enumerate(stxs):
@@ -74,11 +94,23 @@ def check_signatures_are_valid_batch(stxs, signable_data, crypto=Crypto):
             st = int(status[pos + i])
             if st != B.VALID and result[t] is None:
                 try:
-                    crypto.raise_for_status(st, SCHEME_CODE_NAMES.get(s.by.scheme, ""), do_verify=True)
+                    crypto.raise_for_status(st, SCHEME_CODE_NAMES.get(s.by.scheme, ""), do_verify=True,
+                                            error=errors.get(pos + i), key=s.by)
                 except Exception as e:  # noqa: BLE001 - mirrored JVM exception
                     result[t] = (i, e)
         pos += len(stx.sigs)
     return result
+
+
+def check_signatures_are_valid_batch(stxs, signable_data, crypto=Crypto):
+    """Verifies all signatures of all transactions in one GPU batch (host-verified schemes and
+    composite leaves routed by Crypto.verify_batch_ex).
+
+    Returns, per transaction, None if every signature verified, else (index, exception)
+    for the FIRST failing signature in list order (the one the serial loop would throw)."""
+    items, owner = _items(stxs, signable_data)
+    status, errors = crypto.verify_batch_ex(items, B.MODE_DOVERIFY) if items else (np.zeros(0, np.uint8), {})
+    return _first_failures(stxs, status, errors, crypto)
 
 
 def check_signatures_are_valid(stx, signable_data, crypto=Crypto):
@@ -88,14 +120,13 @@ def check_signatures_are_valid(stx, signable_data, crypto=Crypto):
 
 
 def verify_signatures_except(stx, signable_data, allowed_to_be_missing=(), crypto=Crypto):
-    """TransactionWithSignatures.verifySignaturesExcept (TransactionWithSignatures.kt:41-47).
-    Composite-key fulfilment (isFulfilledBy) is host logic and out of scope: required keys
-    are matched by identity."""
+    """TransactionWithSignatures.verifySignaturesExcept (TransactionWithSignatures.kt:41-47):
+    the signatures' check, then SignaturesMissingException for required keys the signatures do not
+    fulfil (composite-aware), minus the keys allowed to be missing."""
     check_signatures_are_valid(stx, signable_data, crypto)
-    sig_keys = {s.by for s in stx.sigs}
-    needed = {k for k in stx.required_signing_keys if k not in sig_keys} - set(allowed_to_be_missing)
+    needed = get_missing_signatures(stx) - set(allowed_to_be_missing)
     if needed:
-        raise SignaturesMissingException(needed, stx.id)
+        raise SignaturesMissingException(needed, get_key_descriptions(stx, needed), stx.id)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -118,6 +149,8 @@ class SignedWireTransaction:
     sigs: list                       # TransactionSignature
     required_signing_keys: set = field(default_factory=set)
     inputs: list = field(default_factory=list)   # StateRef.txhash of each input (32-byte ids)
+    commands: list = field(default_factory=list)
+    notary: object = None
 
 
 def pack_signed_transactions(stxs):
@@ -143,7 +176,9 @@ def pack_signed_transactions(stxs):
         tx_rows.append((first, len(w.components) + 1, 0, bb._append(w.salt, 4)))
         for s in stx.sigs:
             k = bb.key(s.by.scheme, s.by.fmt, s.by.encoded)
-            sb = B.sig_field(s.by.scheme, s.bytes)
+            # a scheme the GPU does not run gets CG_UNSUPPORTED whatever its bytes (the host
+            # verifies it afterwards, verify_wire_transactions): pack a 1-byte placeholder
+            sb = B.sig_field(s.by.scheme, s.bytes) if s.by.scheme in GPU_SCHEMES else b"\x00"
             sig_rows.append((bb._append(sb, 4), t, k, len(sb), tmpl_for(s.platform_version, s.scheme_number_id), 0))
     built = bb.build()
     txs = np.array(tx_rows, dtype=B.TX_DTYPE) if tx_rows else np.zeros(0, B.TX_DTYPE)
@@ -162,6 +197,22 @@ def verify_wire_transactions(stxs, crypto=Crypto):
     from .merkle import MerkleTreeException
     txs, comps, keys, sigs, tmpls, arena = pack_signed_transactions(stxs)
     ids, txst, sst = crypto.engine().verify_transactions(txs, comps, keys, sigs, tmpls, arena, B.MODE_DOVERIFY)
+    sst = sst.copy()
+    # signatures the GPU returned CG_UNSUPPORTED for (RSA, SPHINCS, composite keys): the host
+    # fallback over SignableData(id, metadata) with the GPU-computed id
+    errors, fb, pos = {}, [], 0
+    for t, stx in enumerate(stxs):
+        for i, s in enumerate(stx.sigs):
+            if s.by.scheme not in GPU_SCHEMES and txst[t] == 0:
+                pre, suf = signable.template(s.platform_version, s.scheme_number_id)
+                fb.append((pos + i, BatchItem(s.by, s.bytes, pre + bytes(ids[t]) + suf)))
+        pos += len(stx.sigs)
+    if fb:
+        st2, err2 = crypto.verify_batch_ex([b for _, b in fb], B.MODE_DOVERIFY)
+        for j, (p, _) in enumerate(fb):
+            sst[p] = st2[j]
+            if j in err2:
+                errors[p] = err2[j]
     out_ids, results, pos = [], [], 0
     for t, stx in enumerate(stxs):
         if txst[t] != 0:
@@ -175,7 +226,8 @@ def verify_wire_transactions(stxs, crypto=Crypto):
             st = int(sst[pos + i])
             if st != B.VALID and res is None:
                 try:
-                    crypto.raise_for_status(st, SCHEME_CODE_NAMES.get(s.by.scheme, ""), do_verify=True)
+                    crypto.raise_for_status(st, SCHEME_CODE_NAMES.get(s.by.scheme, ""), do_verify=True,
+                                            error=errors.get(pos + i), key=s.by)
                 except Exception as e:  # noqa: BLE001 - mirrored JVM exception
                     res = (i, e)
         results.append(res)
@@ -254,10 +306,9 @@ def verify_chain(stxs, crypto=Crypto, check_sufficient_signatures=True, on_verif
         if results[t] is not None:
             raise results[t][1]
         if check_sufficient_signatures:
-            have = {s.by for s in stx.sigs}
-            missing = {k for k in stx.required_signing_keys if k not in have}
+            missing = get_missing_signatures(stx)
             if missing:
-                raise SignaturesMissingException(missing, ids[t])
+                raise SignaturesMissingException(missing, get_key_descriptions(stx, missing), ids[t])
         if on_verified is not None:
             on_verified(t, ids[t])
     return order

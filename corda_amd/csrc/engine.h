@@ -36,12 +36,12 @@ struct StageTimer {
   int mark(int stage, hipStream_t s) {
     Rec r{stage, nullptr, nullptr};
     if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return -1;
-    hipEventRecord(r.a, s);
+    (void)hipEventRecord(r.a, s);
     recs.push_back(r);
     return (int)recs.size() - 1;
   }
   void done(int idx, hipStream_t s) {
-    if (idx >= 0) hipEventRecord(recs[idx].b, s);
+    if (idx >= 0) (void)hipEventRecord(recs[idx].b, s);
   }
 };
 #define CG_TIME(fork, stage, stream, launch)                                   \

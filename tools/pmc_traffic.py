@@ -1,13 +1,18 @@
-"""Per-launch HBM traffic of the Ed25519 item kernels from two rocprofv3 PMC passes
-(tools/profile_r01.sh: --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs), written to
-profiles/r01/pmc_traffic.json for bench.py's roofline.traffic.
+"""Per-launch HBM traffic and VALU issue of the item kernels from rocprofv3 passes
+(tools/profile_r02.sh: --kernel-trace --stats, then --pmc FETCH_SIZE, --pmc WRITE_SIZE and an SQ pass,
+each its own process), written to profiles/r02/pmc_traffic.json for bench.py's roofline.
 
-gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE tallies 128-B requests at 64 B,
-so a wide streaming read reports half its bytes; hbm = 2*FETCH_SIZE + WRITE_SIZE (KB * 1024).
-The doubling is calibrated for streaming reads, not 16-B table gathers, so the figure is an
-upper estimate.
+HBM bytes (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE tallies 128-B requests at 64 B,
+so a wide streaming read reports half its bytes: hbm = 2*FETCH_SIZE + WRITE_SIZE (KB * 1024). The
+doubling is calibrated for streaming reads, not 16-B table gathers, so the figure is an upper
+estimate.
 
-usage: pmc_traffic.py <prof_dir> <kernel_version> <items> <dest_profile_dir>
+VALU issue: SQ_INSTS_VALU wave-instructions of the kernel priced per opcode (tools/isa_mix.py: the
+hottest loop's static instruction mix x the measured chip rate of each opcode,
+profiles/r01/ubench_int.json) and spread over the 1024 SIMDs, against the kernel's own duration in
+the counter pass. ``issue_frac_4cyc`` keeps round 1's flat 4-cycles-per-op figure for comparison.
+
+usage: pmc_traffic.py <prof_dir> <kernel_version> <items> <dest_profile_dir> [isa_mix.json]
 """
 import collections
 import csv
@@ -16,56 +21,53 @@ import os
 import shutil
 import sys
 
-KERNELS = ("cg::k_ed_hash", "cg::k_ed_ladder", "cg::k_ed_finish")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = ("k_ed_hash", "k_ed_ladder_pf", "k_ed_finish", "k_ec_prep<1>", "k_ec_inv<1>", "k_ec_ladder<1, true>",
+           "k_ec_prep<0>", "k_ec_inv<0>", "k_ec_ladder<0, true>")
 
 
-def per_kernel_kb(path):
-    """Average KB per launch of each kernel; the two table modes' ladders (k_ed_ladder_pf for
-    full-table keys, k_ed_ladder<false> for row-0 keys, both launched every step) are summed
-    under k_ed_ladder."""
-    acc = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        full = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        name = full.split("<")[0]
-        if name.startswith("cg::k_ed_ladder"):  # k_ed_ladder_pf (full tables) + k_ed_ladder<false>
-            name = "cg::k_ed_ladder"
-        if name in KERNELS:
-            acc[(name, full)].append(float(r["Counter_Value"]))
-    out = collections.defaultdict(float)
-    for (name, _), v in acc.items():
-        out[name] += sum(v) / len(v)
-    return dict(out)
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("cg::", "")
 
 
-def valu_issue(path, items):
-    """VALU issue occupancy of the Ed25519 item kernels from the SQ pass (tools/profile_r01.sh):
-    VALU wave-instructions x 4 cycles (a wave64 VALU op holds a SIMD16 for 4 cycles) over the
-    SIMD-cycles the kernel ran (GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024 SIMDs). ~1.0
-    means the kernel is bound by instruction issue, whatever its MAC fraction."""
+def per_launch(path, counter_names):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        if name.startswith(("cg::k_ed_ladder_pf", "cg::k_ed_hash", "cg::k_ed_finish")):
-            acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        n = short(r["Kernel_Name"])
+        if n not in KERNELS or r["Counter_Name"] not in counter_names:
+            continue
+        acc[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if r["Counter_Name"] == counter_names[0]:
+            dur[n].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
     out = {}
-    for name, cs in acc.items():
-        m = {k: sum(v) / len(v) for k, v in cs.items()}
-        clk = m["GRBM_GUI_ACTIVE"] / 8
-        out[name.split("::")[1]] = {
-            "valu_insts_per_item": round(m["SQ_INSTS_VALU"] * 64 / items, 1),
-            "xcd_cycles": round(clk),
-            "issue_frac": round(m["SQ_INSTS_VALU"] * 4 / (1024 * clk), 3),
-            "wait_frac": round(m["SQ_WAIT_INST_ANY"] / m["SQ_WAVE_CYCLES"], 3)}
+    for n, cs in acc.items():
+        out[n] = {k: sum(v) / len(v) for k, v in cs.items()}
+        out[n]["ms"] = sum(dur[n]) / len(dur[n])
+        out[n]["launches"] = len(dur[n])
+    return out
+
+
+def trace_stats(path):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        n = short(r["Name"])
+        if n in KERNELS:
+            out[n] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) * 1e-6,
+                      "min_ms": float(r["MinNs"]) * 1e-6, "max_ms": float(r["MaxNs"]) * 1e-6}
     return out
 
 
 def main():
     prof, version, items, dest = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    fetch = per_kernel_kb(os.path.join(prof, "fetch", "run_counter_collection.csv"))
-    write = per_kernel_kb(os.path.join(prof, "write", "run_counter_collection.csv"))
-    assert set(fetch) == set(KERNELS) and set(write) == set(KERNELS), (fetch, write)
-    hbm = int(round((2 * sum(fetch.values()) + sum(write.values())) * 1024))
+    mixes = json.load(open(sys.argv[5])) if len(sys.argv) > 5 else {}
+    fetch = per_launch(os.path.join(prof, "fetch", "run_counter_collection.csv"), ["FETCH_SIZE"])
+    write = per_launch(os.path.join(prof, "write", "run_counter_collection.csv"), ["WRITE_SIZE"])
+    sq_names = ["SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE", "SQ_WAVES",
+                "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64"]
+    vpath = os.path.join(prof, "valu", "run_counter_collection.csv")
+    valu = per_launch(vpath, sq_names) if os.path.exists(vpath) else {}
+    trace = trace_stats(os.path.join(prof, "trace", "run_kernel_stats.csv"))
     os.makedirs(dest, exist_ok=True)
     for src, dst in (("trace/run_kernel_stats.csv", "kernel_stats.csv"),
                      ("fetch/run_counter_collection.csv", "pmc_fetch_size.csv"),
@@ -73,21 +75,49 @@ def main():
                      ("valu/run_counter_collection.csv", "pmc_valu.csv")):
         if os.path.exists(os.path.join(prof, src)):
             shutil.copy(os.path.join(prof, src), os.path.join(dest, dst))
+    kern = {}
+    for n in KERNELS:
+        k = {}
+        if n in trace:
+            k["trace"] = trace[n]
+        if n in fetch and n in write:
+            k["fetch_kb"] = round(fetch[n]["FETCH_SIZE"], 1)
+            k["write_kb"] = round(write[n]["WRITE_SIZE"], 1)
+            k["hbm_bytes_per_launch"] = int(round((2 * fetch[n]["FETCH_SIZE"] + write[n]["WRITE_SIZE"]) * 1024))
+        if n in valu:
+            v = valu[n]
+            clk = v["GRBM_GUI_ACTIVE"] / 8
+            k["valu"] = {"insts_per_launch": v["SQ_INSTS_VALU"], "ms_in_counter_pass": round(v["ms"], 3),
+                         "clock_GHz": round(clk / (v["ms"] * 1e6), 3),
+                         "issue_frac_4cyc": round(v["SQ_INSTS_VALU"] * 4 / (1024 * clk), 3),
+                         "wait_frac": round(v["SQ_WAIT_INST_ANY"] / v["SQ_WAVE_CYCLES"], 3)}
+            if "SQ_INSTS_VALU_INT64" in v:
+                k["valu"]["int64_frac"] = round(v["SQ_INSTS_VALU_INT64"] / v["SQ_INSTS_VALU"], 3)
+                k["valu"]["int32_frac"] = round(v["SQ_INSTS_VALU_INT32"] / v["SQ_INSTS_VALU"], 3)
+            mix = mixes.get(n)
+            if mix:
+                t = v["SQ_INSTS_VALU"] / 1024 * mix["mean_ns_per_wave_instr"] * 1e-6
+                k["valu"]["issue_ms_per_opcode_model"] = round(t, 3)
+                k["valu"]["issue_frac"] = round(t / v["ms"], 3)
+                k["valu"]["mix"] = mix
+        if k:
+            kern[n] = k
     rel = os.path.relpath(dest, ROOT)
-    out = {"items": items, "kernel": " + ".join(k.split("::")[1] for k in KERNELS),
-           "source": f"{rel}/pmc_fetch_size.csv, pmc_write_size.csv (rocprofv3 --pmc FETCH_SIZE / "
-                     "WRITE_SIZE, separate passes, bench.py --steps 3)",
-           "fetch_size_kb": fetch, "write_size_kb": write,
-           "correction": "gfx950 FETCH_SIZE reads half the bytes of wide streaming reads "
-                         "(MI355X_MICROARCH.md HBM): hbm = 2*FETCH_SIZE + WRITE_SIZE (KB*1024); "
-                         "uncalibrated for 16-B table gathers, so an upper estimate",
-           "hbm_bytes_per_launch": hbm, "kernel_version": version}
-    vpath = os.path.join(prof, "valu", "run_counter_collection.csv")
-    if os.path.exists(vpath):
-        out["valu_issue"] = valu_issue(vpath, items)
-    with open(os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"), "w") as f:
+    out = {"items": items, "kernel_version": version,
+           "source": f"{rel}/ (rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE; SQ pass; "
+                     "separate processes, bench.py --steps 3 on the headline workload)",
+           "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts 128-B requests at 64 B); upper "
+                         "estimate for table gathers",
+           "kernels": kern,
+           "hbm_bytes_per_launch": {n: k["hbm_bytes_per_launch"] for n, k in kern.items() if "hbm_bytes_per_launch" in k},
+           "valu_issue": {n: k["valu"] for n, k in kern.items() if "valu" in k}}
+    with open(os.path.join(dest, "pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
-    print(json.dumps(out))
+    os.makedirs(os.path.join(ROOT, "profiles", "r02"), exist_ok=True)
+    with open(os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({n: (k.get("hbm_bytes_per_launch"), k.get("valu", {}).get("issue_frac"),
+                          k.get("trace", {}).get("avg_ms")) for n, k in kern.items()}))
 
 
 if __name__ == "__main__":

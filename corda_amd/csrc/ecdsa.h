@@ -387,7 +387,8 @@ CG_HD uint32_t der_sig(const uint8_t* arena, uint64_t lr, uint64_t off, uint32_t
 
 // ------------------------------------------------------------------ key bytes
 // Formats (include/cordagpu.h): RAW 64 B X||Y; SPKI (PublicKey.getEncoded(), 91 B r1 /
-// 88 B k1) ending in an uncompressed point; SEC1 04||X||Y or 02/03||X.
+// 88 B k1, or the 59 / 56 B form around a compressed point); SEC1 04||X||Y, 06/07||X||Y (hybrid)
+// or 02/03||X.
 CG_HD void ec_load_be32(u256w& v, const uint8_t* arena, uint64_t lr, uint64_t off) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) v.w[7 - i] = CG_BSWAP32(cg_ld_bytes4(arena, lr, off + 4 * i));
@@ -399,5 +400,13 @@ CG_HD uint32_t ec_spki_prefix_byte(int curve, int i) {
   const uint8_t K1[23] = {0x30, 0x56, 0x30, 0x10, 0x06, 0x07, 0x2a, 0x86, 0x48, 0xce, 0x3d, 0x02,
                           0x01, 0x06, 0x05, 0x2b, 0x81, 0x04, 0x00, 0x0a, 0x03, 0x42, 0x00};
   return curve == CG_CURVE_R1 ? R1[i] : K1[i];
+}
+
+// SPKI header byte i for a point of ptlen bytes (65 or 33): only the outer SEQUENCE length
+// (byte 1) and the BIT STRING length (byte pl - 2) depend on the point's length.
+CG_HD uint32_t ec_spki_header_byte(int curve, int i, uint32_t ptlen) {
+  const int pl = curve == CG_CURVE_R1 ? 26 : 23;
+  const uint32_t b = ec_spki_prefix_byte(curve, i);
+  return (i == 1 || i == pl - 2) ? b - (65u - ptlen) : b;
 }
 

@@ -184,13 +184,14 @@ CG_HD uint32_t ec_key_decode_bytes(f29& xm, f29& ym, const uint8_t* arena, uint6
   u256w x, y;
   uint64_t pt = off;
   uint32_t ptlen = len;
-  if (fmt == 1) {  // SPKI
+  if (fmt == 1) {  // SPKI: this scheme's id-ecPublicKey + named curve, then a 65- or 33-byte point
     const uint32_t pl = C == CG_CURVE_R1 ? 26 : 23;
-    if (len != pl + 65) return 3;
+    if (len == pl + 65) ptlen = 65;
+    else if (len == pl + 33) ptlen = 33;
+    else return 3;
     for (uint32_t i = 0; i < pl; ++i)
-      if (der_byte(arena, lr, off + i) != ec_spki_prefix_byte(C, (int)i)) return 3;
+      if (der_byte(arena, lr, off + i) != ec_spki_header_byte(C, (int)i, ptlen)) return 3;
     pt = off + pl;
-    ptlen = 65;
   } else if (fmt == 0) {  // RAW
     if (len != 64) return 3;
     ec_load_be32(x, arena, lr, off);
@@ -200,9 +201,10 @@ CG_HD uint32_t ec_key_decode_bytes(f29& xm, f29& ym, const uint8_t* arena, uint6
     return 3;
   }
   const uint32_t tag = ptlen ? der_byte(arena, lr, pt) : 0u;
-  if (ptlen == 65 && tag == 4) {
+  if (ptlen == 65 && (tag == 4 || tag == 6 || tag == 7)) {  // uncompressed / hybrid
     ec_load_be32(x, arena, lr, pt + 1);
     ec_load_be32(y, arena, lr, pt + 33);
+    if (tag != 4 && (y.w[0] & 1u) != (tag & 1u)) return 3;  // hybrid tag carries y's parity
     return ec_key_decode_xy<C>(xm, ym, x, y, K);
   }
   if (ptlen == 33 && (tag == 2 || tag == 3)) {

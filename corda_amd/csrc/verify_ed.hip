@@ -20,20 +20,33 @@ namespace cg {
 __constant__ Ed25519Consts c_ed;
 
 static const uint8_t ED_SPKI_PREFIX[12] = {0x30, 0x2a, 0x30, 0x05, 0x06, 0x03, 0x2b, 0x65, 0x70, 0x03, 0x21, 0x00};
+// AlgorithmIdentifier with an explicit NULL parameter (46 bytes): Crypto.findSignatureScheme
+// normalises DERNull away (Crypto.kt:219-228) and i2p 0.2.0 EdDSAPublicKey.decode accepts it.
+static const uint8_t ED_SPKI_PREFIX_NULL[14] = {0x30, 0x2c, 0x30, 0x07, 0x06, 0x03, 0x2b,
+                                                0x65, 0x70, 0x05, 0x00, 0x03, 0x21, 0x00};
 
 // Offset of A's 32 bytes in the arena for a raw or SPKI Ed25519 key; false for a malformed
-// encoding (wrong length / SPKI prefix / outside the arena).
+// encoding (wrong length / SPKI header / outside the arena).
 __device__ __forceinline__ bool ed_key_locate(const cg_key& k, const uint8_t* arena, uint64_t arena_len,
                                               uint64_t& a_off) {
   const uint64_t lr = round4(arena_len);
   a_off = k.off;
   if (!in_arena(k.off, k.len, arena_len)) return false;
   if (k.fmt == CG_KEY_RAW) return k.len == 32;
-  if (k.fmt != CG_KEY_SPKI || k.len != 44) return false;
-  for (int b = 0; b < 12; ++b)
-    if ((cg_ld_bytes4(arena, lr, k.off + b) & 0xffu) != ED_SPKI_PREFIX[b]) return false;
-  a_off = k.off + 12;
-  return true;
+  if (k.fmt != CG_KEY_SPKI) return false;
+  if (k.len == 44) {
+    for (int b = 0; b < 12; ++b)
+      if ((cg_ld_bytes4(arena, lr, k.off + b) & 0xffu) != ED_SPKI_PREFIX[b]) return false;
+    a_off = k.off + 12;
+    return true;
+  }
+  if (k.len == 46) {
+    for (int b = 0; b < 14; ++b)
+      if ((cg_ld_bytes4(arena, lr, k.off + b) & 0xffu) != ED_SPKI_PREFIX_NULL[b]) return false;
+    a_off = k.off + 14;
+    return true;
+  }
+  return false;
 }
 
 // one lane per key, main stream: the canonical Abyte k_ed_hash needs, without the square root

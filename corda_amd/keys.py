@@ -16,13 +16,26 @@ _A = {3: -3, 2: 0}
 KEY_RAW, KEY_SPKI, KEY_SEC1 = 0, 1, 2
 
 
+ED25519_SPKI_PREFIX_NULL = bytes.fromhex("302c300706032b65700500032100")  # NULL parameters
+
+
+def _ec_spki_header(scheme, point_len):
+    pre = bytearray(EC_SPKI_PREFIX[scheme])
+    pre[1] -= 65 - point_len   # outer SEQUENCE length
+    pre[-2] -= 65 - point_len  # BIT STRING length
+    return bytes(pre)
+
+
 def _ec_uncompressed(scheme, b):
-    """04 || X || Y from a raw 64-byte X||Y or a SEC1 point; None if it cannot be formed."""
+    """04 || X || Y from a raw 64-byte X||Y or a SEC1 point (uncompressed, hybrid, compressed);
+    None if it cannot be formed."""
     p = _P[scheme]
     if len(b) == 64:
         return b"\x04" + b
     if len(b) == 65 and b[0] == 4:
         return b
+    if len(b) == 65 and b[0] in (6, 7):
+        return b"\x04" + b[1:] if (b[64] & 1) == (b[0] & 1) else None
     if len(b) == 33 and b[0] in (2, 3):
         x = int.from_bytes(b[1:], "big")
         if x >= p:
@@ -42,6 +55,16 @@ def canonical_spki(scheme, fmt, encoded):
     that form (such a key fails to decode on the JVM and on the GPU alike)."""
     b = bytes(encoded)
     if fmt == KEY_SPKI:
+        # the JVM key object re-encodes the forms Crypto.decodePublicKey accepts canonically
+        # (i2p: absent parameters; BC: uncompressed point)
+        if scheme == 4 and len(b) == 46 and b[:14] == ED25519_SPKI_PREFIX_NULL:
+            return ED25519_SPKI_PREFIX + b[14:]
+        if scheme in EC_SPKI_PREFIX:
+            for plen in (65, 33):
+                h = _ec_spki_header(scheme, plen)
+                if len(b) == len(h) + plen and b[:len(h)] == h:
+                    u = _ec_uncompressed(scheme, b[len(h):])
+                    return EC_SPKI_PREFIX[scheme] + u if u is not None else b
         return b
     if scheme == 4 and fmt == KEY_RAW and len(b) == 32:
         return ED25519_SPKI_PREFIX + b

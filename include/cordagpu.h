@@ -51,8 +51,11 @@ enum {
 /* Public-key byte formats. */
 enum {
   CG_KEY_RAW = 0,  /* Ed25519: 32-byte A (what Kryo writes, Kryo.kt:333); ECDSA: 64-byte X||Y big-endian */
-  CG_KEY_SPKI = 1, /* X.509 SubjectPublicKeyInfo DER == PublicKey.getEncoded() (44 / 91 / 88 bytes) */
-  CG_KEY_SEC1 = 2  /* ECDSA only: 04||X||Y or 02/03||X */
+  CG_KEY_SPKI = 1, /* X.509 SubjectPublicKeyInfo DER == PublicKey.getEncoded() (44 / 91 / 88 bytes);
+                      also the other forms Crypto.decodePublicKey (Crypto.kt:321-325) accepts:
+                      Ed25519 with NULL parameters (46), EC around a compressed point (59 / 56)
+                      or a hybrid one (06/07 tag, 91 / 88). Anything else: CG_KEY_INVALID. */
+  CG_KEY_SEC1 = 2  /* ECDSA only: 04||X||Y, 06/07||X||Y (hybrid) or 02/03||X */
 };
 
 /* Per-item verdicts. */

@@ -235,11 +235,20 @@ int or_ec_key_decode(or_ec_key* k, int scheme, int fmt, const uint8_t* key, size
   uint8_t pt[65];
   size_t plen;
   if (fmt == CG_KEY_SPKI) {
+    /* Crypto.decodePublicKey (Crypto.kt:321-325): this scheme's id-ecPublicKey + named-curve
+       algorithm identifier, then any point ECCurve.decodePoint accepts. The DER header of a
+       33-byte (compressed) point differs in the two length bytes only. */
     const uint8_t* pre = scheme == CG_ECDSA_SECP256K1_SHA256 ? SPKI_K1 : SPKI_R1;
     size_t pl = scheme == CG_ECDSA_SECP256K1_SHA256 ? sizeof SPKI_K1 : sizeof SPKI_R1;
-    if (len != pl + 65 || memcmp(key, pre, pl) != 0) return CG_KEY_INVALID;
-    memcpy(pt, key + pl, 65);
-    plen = 65;
+    if (len == pl + 65) plen = 65;
+    else if (len == pl + 33) plen = 33;
+    else return CG_KEY_INVALID;
+    for (size_t i = 0; i < pl; ++i) {
+      uint8_t want = pre[i];
+      if (i == 1 || i == pl - 2) want = (uint8_t)(want - (65 - plen));
+      if (key[i] != want) return CG_KEY_INVALID;
+    }
+    memcpy(pt, key + pl, plen);
   } else if (fmt == CG_KEY_RAW) {
     if (len != 64) return CG_KEY_INVALID;
     pt[0] = 4;
@@ -254,10 +263,12 @@ int or_ec_key_decode(or_ec_key* k, int scheme, int fmt, const uint8_t* key, size
   }
   u256 x, y;
   if (plen == 65) {
-    if (pt[0] != 4) return CG_KEY_INVALID;
+    /* 04 uncompressed; 06/07 hybrid, whose tag must carry y's parity (ECCurve.decodePoint) */
+    if (pt[0] != 4 && pt[0] != 6 && pt[0] != 7) return CG_KEY_INVALID;
     u256_from_be(&x, pt + 1);
     u256_from_be(&y, pt + 33);
     if (u256_cmp(&x, &c->p_plain) >= 0 || u256_cmp(&y, &c->p_plain) >= 0) return CG_KEY_INVALID;
+    if (pt[0] != 4 && (int)(y.v[0] & 1) != (pt[0] & 1)) return CG_KEY_INVALID;
     mont_to(f, &k->Q.x, &x);
     mont_to(f, &k->Q.y, &y);
     if (!on_curve(c, &k->Q)) return CG_KEY_INVALID;

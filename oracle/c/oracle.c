@@ -39,6 +39,10 @@ static void counters_flush(void) {
 }
 
 static const uint8_t ED_SPKI[12] = {0x30, 0x2a, 0x30, 0x05, 0x06, 0x03, 0x2b, 0x65, 0x70, 0x03, 0x21, 0x00};
+/* explicit NULL parameter: normalised away by Crypto.findSignatureScheme (Crypto.kt:219-228),
+   accepted by i2p 0.2.0 EdDSAPublicKey.decode */
+static const uint8_t ED_SPKI_NULL[14] = {0x30, 0x2c, 0x30, 0x07, 0x06, 0x03, 0x2b, 0x65,
+                                         0x70, 0x05, 0x00, 0x03, 0x21, 0x00};
 
 static int scheme_supported(int s) {
   return s == CG_ECDSA_SECP256K1_SHA256 || s == CG_ECDSA_SECP256R1_SHA256 || s == CG_EDDSA_ED25519_SHA512;
@@ -61,6 +65,7 @@ static void decode_key(keyslot* ks, const cg_key* key, const uint8_t* arena, uin
     const uint8_t* a = NULL;
     if (key->fmt == CG_KEY_RAW && key->len == 32) a = kb;
     else if (key->fmt == CG_KEY_SPKI && key->len == 44 && memcmp(kb, ED_SPKI, 12) == 0) a = kb + 12;
+    else if (key->fmt == CG_KEY_SPKI && key->len == 46 && memcmp(kb, ED_SPKI_NULL, 14) == 0) a = kb + 14;
     if (!a) { ks->status = CG_KEY_INVALID; return; }
     ks->k = malloc(or_ed_key_size());
     ks->status = or_ed_key_decode((or_ed_key*)ks->k, a);

@@ -40,6 +40,20 @@ MODE_DOVERIFY = 0   # Crypto.doVerify semantics: empty sig / clear -> EMPTY
 MODE_ISVALID = 1    # Crypto.isValid semantics: no empty checks
 
 ED25519_SPKI_PREFIX = bytes.fromhex("302a300506032b6570032100")
+# AlgorithmIdentifier with an explicit NULL parameter: Crypto.findSignatureScheme normalises DERNull
+# to absent (Crypto.kt:219-228) and i2p 0.2.0 EdDSAPublicKey.decode accepts this 46-byte form
+# (it reads Java keystore output). The old draft OID 1.3.101.100 form i2p also reads is not in
+# Corda's algorithmMap (Crypto.kt:190-193), so Crypto.decodePublicKey rejects it.
+ED25519_SPKI_PREFIX_NULL = bytes.fromhex("302c300706032b65700500032100")
+
+
+def ed25519_spki_a(key):
+    """The 32-byte A of an Ed25519 SPKI Crypto.decodePublicKey (Crypto.kt:321-325) accepts."""
+    if len(key) == 44 and key[:12] == ED25519_SPKI_PREFIX:
+        return key[12:]
+    if len(key) == 46 and key[:14] == ED25519_SPKI_PREFIX_NULL:
+        return key[14:]
+    raise ed25519_i2p.KeyDecodeError("bad SubjectPublicKeyInfo")
 
 
 def decode_key(scheme, key_fmt, key):
@@ -47,9 +61,7 @@ def decode_key(scheme, key_fmt, key):
     key = bytes(key)
     if scheme == EDDSA_ED25519_SHA512:
         if key_fmt == KEY_SPKI:
-            if len(key) != 44 or key[:12] != ED25519_SPKI_PREFIX:
-                raise ed25519_i2p.KeyDecodeError("bad SubjectPublicKeyInfo")
-            key = key[12:]
+            key = ed25519_spki_a(key)
         elif key_fmt != KEY_RAW:
             raise ed25519_i2p.KeyDecodeError("bad key format")
         return ed25519_i2p.PublicKey(key)

@@ -108,16 +108,19 @@ SPKI_PREFIX = {
 
 
 def decode_point(c, data):
-    """SEC1 point (04||X||Y, 02/03||X) or raw 64-byte X||Y -> affine point.
-    Mirrors ECCurve.decodePoint + validation (coordinates < p, on curve)."""
+    """SEC1 point (04||X||Y, 06/07||X||Y hybrid, 02/03||X) or raw 64-byte X||Y -> affine point.
+    Mirrors ECCurve.decodePoint + validation (coordinates < p, on curve; a hybrid encoding's
+    tag must carry y's parity; the point at infinity (00) is rejected by ECPublicKeyParameters)."""
     p = c.p
     if len(data) == 64:
         data = b"\x04" + bytes(data)
-    if len(data) == 65 and data[0] == 4:
+    if len(data) == 65 and data[0] in (4, 6, 7):
         x = int.from_bytes(data[1:33], "big")
         y = int.from_bytes(data[33:65], "big")
         if x >= p or y >= p:
             raise KeyDecodeError("x value invalid in Fp field element")
+        if data[0] != 4 and (y & 1) != (data[0] & 1):
+            raise KeyDecodeError("Inconsistent Y coordinate in hybrid encoding")
         if not c.on_curve((x, y)):
             raise KeyDecodeError("Invalid point coordinates")
         return (x, y)
@@ -135,11 +138,25 @@ def decode_point(c, data):
     raise KeyDecodeError("Invalid point encoding")
 
 
+def spki_prefix(scheme, point_len):
+    """DER header of SEQUENCE{AlgorithmIdentifier{id-ecPublicKey, namedCurve}, BIT STRING} for a
+    point of point_len bytes (65: uncompressed / hybrid, 33: compressed)."""
+    pre = bytearray(SPKI_PREFIX[scheme])
+    pre[1] -= 65 - point_len          # outer SEQUENCE length
+    pre[-2] -= 65 - point_len         # BIT STRING length (unused-bits byte + point)
+    return bytes(pre)
+
+
 def decode_spki(scheme, data):
-    pre = SPKI_PREFIX[scheme]
-    if len(data) != len(pre) + 65 or bytes(data[: len(pre)]) != pre:
-        raise KeyDecodeError("bad SubjectPublicKeyInfo")
-    return decode_point(CURVES[scheme], data[len(pre):])
+    """Crypto.decodePublicKey (Crypto.kt:321-325) for an EC key: the algorithm identifier must be
+    this scheme's (id-ecPublicKey + its named curve, Crypto.kt:96/110), DER with no trailing data;
+    the point is whatever ECCurve.decodePoint accepts (uncompressed, compressed, hybrid)."""
+    data = bytes(data)
+    for plen in (65, 33):
+        pre = spki_prefix(scheme, plen)
+        if len(data) == len(pre) + plen and data[: len(pre)] == pre:
+            return decode_point(CURVES[scheme], data[len(pre):])
+    raise KeyDecodeError("bad SubjectPublicKeyInfo")
 
 
 # ---------------- DER (StdDSAEncoder.decode, BC 1.57) ----------------

@@ -47,6 +47,32 @@ def test_ecdsa_golden(engine, mode):
     assert len(bad) == 0, "\n".join(msgs)
 
 
+@pytest.mark.parametrize("mode", [B.MODE_DOVERIFY, B.MODE_ISVALID])
+def test_spki_golden(engine, mode):
+    """Every SubjectPublicKeyInfo form of tests/golden/spki.json (accepted variants and malformed
+    encodings, all three schemes; Crypto.kt:321-325) gets the oracle's verdict."""
+    _check(engine, golden_io.load("spki.json"), mode)
+
+
+def test_all_spki_mixed_batch_vs_c_oracle(engine):
+    """A 70/20/10 mixed batch whose keys are all SPKI (what the Kotlin binding sends: canonical
+    forms plus the NULL-parameter / compressed / hybrid variants), bit-exact against the C oracle
+    and equal to the same batch with raw keys."""
+    from tools.workload import wl
+    parts = [wl.ed25519_batch(21000, n_keys=700, msg_len=270, corrupt_permille=120, seed=51, bad_key_every=61,
+                              nthreads=16)[0],
+             wl.ecdsa_batch(0, 6000, n_keys=300, msg_len=270, corrupt_permille=120, seed=52, nthreads=16)[0],
+             wl.ecdsa_batch(1, 3000, n_keys=150, msg_len=270, corrupt_permille=120, seed=53, nthreads=16)[0]]
+    raw, _ = wl.concat(parts, shuffle_seed=54)
+    b = golden_io.spki_rekey(raw)
+    assert np.all(b.keys["fmt"] == B.KEY_SPKI)
+    st = engine.verify(b, B.MODE_DOVERIFY)
+    ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
+    assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
+    assert np.array_equal(st, engine.verify(raw, B.MODE_DOVERIFY))
+    assert (st == B.VALID).sum() > 20000 and (st == B.KEY_INVALID).any()
+
+
 def test_mixed_golden_shuffled(engine):
     """Ed25519 and ECDSA items interleaved in one batch, shuffled, keys shared."""
     items = golden_io.load("ed25519.json") + golden_io.load("ecdsa.json")

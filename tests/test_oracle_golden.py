@@ -49,7 +49,7 @@ def test_fips_sha():
         assert c_oracle.sha512(m).hex() == x["sha512"]
 
 
-@pytest.mark.parametrize("name", ["ed25519.json", "ecdsa.json"])
+@pytest.mark.parametrize("name", ["ed25519.json", "ecdsa.json", "spki.json"])
 def test_c_oracle_matches_golden(name):
     items = golden_io.load(name)
     b, exp, exp_iv = golden_io.sig_batch(items)
@@ -58,9 +58,9 @@ def test_c_oracle_matches_golden(name):
 
 
 def test_python_oracle_matches_golden_sample():
-    for name in ("ed25519.json", "ecdsa.json"):
+    for name, step in (("ed25519.json", 3), ("ecdsa.json", 3), ("spki.json", 1)):
         items = golden_io.load(name)
-        for it in items[::3]:
+        for it in items[::step]:
             st = corda.verify_item(it["scheme"], it["key_fmt"], bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]),
                                    bytes.fromhex(it["msg"]))
             assert corda.STATUS_NAMES[st] == it["expect"], it["note"]
@@ -75,6 +75,48 @@ def test_openssl_crosscheck_recorded():
             if i["openssl"] == "disagree-expected":
                 # only malleable / high-bit S (A4/A5): i2p has no S < L check, OpenSSL does
                 assert i["scheme"] == 4 and i["class"] in ("A4", "A5"), i["note"]
+
+
+def test_spki_fixtures():
+    """SubjectPublicKeyInfo forms (tests/golden/gen_spki.py): every form Crypto.decodePublicKey
+    accepts (Crypto.kt:321-325) is K0 and verifies; everything else is K1 / KEY_INVALID. OpenSSL
+    agreed on each item except the documented cases (NULL parameters, trailing bytes, unused bits)."""
+    items = golden_io.load("spki.json")
+    notes = {(i["scheme"], i["note"]) for i in items}
+    for scheme in (2, 3):
+        assert (scheme, "SPKI around a compressed point") in notes
+        assert (scheme, "SPKI around a hybrid (06/07) point") in notes
+        assert (scheme, "the other curve's OID around this curve's point") in notes
+    assert (4, "46-byte SPKI with NULL parameters") in notes
+    for i in items:
+        assert i["class"] in ("K0", "K1")
+        if i["class"] == "K1":
+            assert i["expect"] == i["expect_isvalid"] == "KEY_INVALID", i["note"]
+        else:
+            assert i["expect"] in ("VALID", "INVALID"), i["note"]
+        if i["openssl"] == "disagree-expected":
+            assert any(w in i["openssl_reason"] for w in ("NULL", "extra data", "unused")), i["note"]
+        else:
+            assert i["openssl"] == "agree", i["note"]
+    lens = {(i["scheme"], len(i["key"]) // 2) for i in items}
+    assert {(4, 43), (4, 45), (3, 90), (3, 92), (2, 87), (2, 89), (3, 59), (2, 56)} <= lens
+
+
+def test_spki_canonical_form_on_host():
+    """The host mirror's key identity (keys.canonical_spki) maps every accepted SPKI variant onto the
+    canonical encoding the JVM key object reports, so equal points compare equal."""
+    from corda_amd import keys as K
+    items = [i for i in golden_io.load("spki.json") if i["class"] == "K0"]
+    for i in items:
+        kb = bytes.fromhex(i["key"])
+        canon = K.canonical_spki(i["scheme"], K.KEY_SPKI, kb)
+        if i["scheme"] == 4:
+            assert len(canon) == 44 and canon[:12] == K.ED25519_SPKI_PREFIX
+            assert canon[12:] == kb[-32:]
+        else:
+            assert canon[:len(K.EC_SPKI_PREFIX[i["scheme"]])] == K.EC_SPKI_PREFIX[i["scheme"]]
+            assert len(canon) == len(K.EC_SPKI_PREFIX[i["scheme"]]) + 65
+            assert canon[-64:-32] == kb[-64:-32] if len(kb) > 70 else canon[-64:-32] == kb[-32:]
 
 
 def test_fixture_classes_cover_appendix_a():

@@ -15,7 +15,8 @@ verdict vectors, the engine's only collective. `value` = items of all ranks / ma
 
 Launch: ``python bench.py`` (N = 1) or ``torchrun --nproc-per-node N bench.py --gpus N``; one
 process per GPU, each verifying its own shard (weak scaling). Rank 0 prints ONE JSON line.
-  roofline      the dominant kernel (k_ed_ladder_pf), priced in the 32x32->64 multiply-accumulates
+  roofline      the dominant kernel (k_ed_ladder_wide: the shard's keys have wide tables; else
+                k_ed_ladder_pf), priced in the 32x32->64 multiply-accumulates
                 its lane code executes (host-counted) over its per-launch time from HIP events
                 recorded on the stream it runs on, during the timed region (CG_FLAG_STAGE_TIMING);
                 peak = the measured v_mad_u64_u32 chip rate. traffic = PMC FETCH/WRITE bytes per
@@ -49,11 +50,14 @@ MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # (tests/native/host_kernels.cpp; pinned by tests/test_host_kernels.py::test_executed_work_*).
 # Ed25519 (field multiplies, squarings) in the radix-2^25.5 representation (fe25519.h):
 ED_VERIFY_FE = (500, 24)   # k_ed_ladder_pf: 43 + 26 mixed additions + 6 doublings
+ED_WIDE_FE = (377, 0)      # k_ed_ladder_wide: 32 + 22 mixed additions, no doublings (keys with wide tables)
+ED_WIDE_BUILD_FE = (62247, 9120)  # one key's wide table: 248-doubling chain + 32 rows x 128 entries
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
 ED_FINISH_K = 16
 MAC_PER_MUL, MAC_PER_SQ = 100, 55
 MAC32_ED_LADDER = ED_VERIFY_FE[0] * MAC_PER_MUL + ED_VERIFY_FE[1] * MAC_PER_SQ
+MAC32_ED_WIDE = ED_WIDE_FE[0] * MAC_PER_MUL + ED_WIDE_FE[1] * MAC_PER_SQ
 MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
                           (ED_VERIFY_FE[1] + ED_FINISH_FE[1]) * MAC_PER_SQ +
                           (ED_INVERT_FE[0] * MAC_PER_MUL + ED_INVERT_FE[1] * MAC_PER_SQ) / ED_FINISH_K)
@@ -63,13 +67,16 @@ MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
 # its addition, but the wave issues it for the other 63 lanes, so the full schedule is what the
 # SIMD executes (per-item mean 1% lower).
 EC_LADDER_MUL = {"secp256r1": 895, "secp256k1": 877}
+EC_WIDE_MUL = {"secp256r1": 586, "secp256k1": 586}  # k_ec_ladder_wide: 32 + 22 mixed additions + x-check
+# table modes (corda_amd/csrc/keyws.h): full tables from 32 items per key, wide from 384
+KEY_FULL_MIN_USES, KEY_WIDE_MIN_USES, KEY_WIDE_MAX = 32, 384, 8192
 EC_INV_MUL_16 = {"secp256r1": 536, "secp256k1": 563}
 EC_MAC_PER_MUL_P = {"secp256r1": 144, "secp256k1": 162}
 EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
 # kernel generation whose PMC traffic profile is committed (profiles/r02/pmc_traffic.json)
-KERNEL_VERSION = "r02_v1"
+KERNEL_VERSION = "r02_v2"
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
 
 # Appendix A labels (tools/workload) -> the verdict Crypto.doVerify gives them (key decodes)
@@ -275,26 +282,38 @@ def stage_summary(times, steps_per_read):
 
 
 def ladder_units(b, labels, schemes, chunk):
-    """Items that reach each ladder, per device chunk: Ed25519 items with a 64-byte signature,
-    ECDSA items whose DER parses and whose r, s are in range (labels 0-2)."""
+    """Items that reach each ladder, per device chunk and table mode: Ed25519 items with a 64-byte
+    signature, ECDSA items whose DER parses and whose r, s are in range (labels 0-2). The mode of a
+    key follows its item count in the call (keyws.h; the engine samples the counts, so a key
+    within 20% of a threshold makes the split approximate: `exact` says whether any is)."""
     sig64 = b.items["sig_len"] == 64
-    ed = (schemes == 4) & sig64
     ok_ec = np.isin(labels, (0, 1, 2))
-    r1 = (schemes == 3) & ok_ec
-    k1 = (schemes == 2) & ok_ec
+    uses = np.bincount(b.items["key_idx"], minlength=len(b.keys))
+    cap = min(len(b.keys), b.n // KEY_WIDE_MIN_USES, KEY_WIDE_MAX)
+    wide_key = uses >= KEY_WIDE_MIN_USES
+    full_key = (uses >= KEY_FULL_MIN_USES) & ~wide_key
+    near = ((np.abs(uses - KEY_WIDE_MIN_USES) < 0.2 * KEY_WIDE_MIN_USES) |
+            (np.abs(uses - KEY_FULL_MIN_USES) < 0.2 * KEY_FULL_MIN_USES)) & (uses > 0)
+    exact = not near.any() and all(int((wide_key & (b.keys["scheme"] == s)).sum()) <= cap for s in (2, 3, 4))
+    kw, kf = wide_key[b.items["key_idx"]], full_key[b.items["key_idx"]]
     n = b.n
     k = max(1, -(-n // chunk)) if chunk else 1
     per = -(-n // k)
     f = lambda m: [int(m[i:i + per].sum()) for i in range(0, n, per)]  # noqa: E731
-    return {"ed": f(ed), "r1": f(r1), "k1": f(k1)}
+    out = {"exact": exact}
+    for name, sel in (("ed", (schemes == 4) & sig64), ("r1", (schemes == 3) & ok_ec), ("k1", (schemes == 2) & ok_ec)):
+        out[name] = f(sel & kf)
+        out[name + "_wide"] = f(sel & kw)
+    return out
 
 
 def roofline(stages, units, steps):
-    """The dominant kernel's executed MAC32 over its average launch time (HIP events on its
-    stream). Also the ECDSA ladders, for the record."""
+    """Each ladder's executed MAC32 over its average launch time (HIP events on its stream). The
+    headline block is the Ed25519 ladder with the most time per step (k_ed_ladder_wide when the
+    keys have wide tables, else k_ed_ladder_pf); the ECDSA ladders are reported beside it."""
     def block(stage, per_item, unit_counts, label):
         ms, n = stages.get(stage, (0.0, 0))
-        if not n:
+        if not n or not sum(unit_counts):
             return None
         launch_ms = ms / n
         items = sum(unit_counts) / len(unit_counts)  # per launch (one launch per chunk per step)
@@ -302,13 +321,17 @@ def roofline(stages, units, steps):
         return {"kernel": label, "bound": "valu-int", "achieved": round(ach / 1e12, 3),
                 "peak": round(PEAK_MAC32_PER_S / 1e12, 3), "unit": "TMAC32/s", "frac": round(ach / PEAK_MAC32_PER_S, 4),
                 "launch_ms": round(launch_ms, 3), "launches": int(n), "items_per_launch": int(items),
-                "work_per_item": per_item}
-    ed = block("ed_ladder", MAC32_ED_LADDER, units["ed"], "k_ed_ladder_pf")
-    r1 = block("r1_ladder", EC_LADDER_MUL["secp256r1"] * EC_MAC_PER_MUL_P["secp256r1"], units["r1"],
-               "k_ec_ladder<secp256r1, full>")
-    k1 = block("k1_ladder", EC_LADDER_MUL["secp256k1"] * EC_MAC_PER_MUL_P["secp256k1"], units["k1"],
-               "k_ec_ladder<secp256k1, full>")
-    return ed, {"secp256r1": r1, "secp256k1": k1}
+                "work_per_item": per_item, "ms_per_step": round(ms / max(steps, 1), 3),
+                "units_exact": units["exact"]}
+    eds = [x for x in (block("ed_ladder", MAC32_ED_LADDER, units["ed"], "k_ed_ladder_pf"),
+                       block("ed_ladder_wide", MAC32_ED_WIDE, units["ed_wide"], "k_ed_ladder_wide")) if x]
+    ed = max(eds, key=lambda x: x["ms_per_step"]) if eds else None
+    ec = {}
+    for c, tag in (("secp256r1", "r1"), ("secp256k1", "k1")):
+        ec[c] = block(tag + "_ladder", EC_LADDER_MUL[c] * EC_MAC_PER_MUL_P[c], units[tag], f"k_ec_ladder<{c}, full>")
+        ec[c + "_wide"] = block(tag + "_ladder_wide", EC_WIDE_MUL[c] * EC_MAC_PER_MUL_P[c], units[tag + "_wide"],
+                                f"k_ec_ladder_wide<{c}>")
+    return ed, ec
 
 
 def run_secondary_device(eng, dev, stream, b, steps=4):
@@ -545,13 +568,13 @@ def main():
     units = ladder_units(batch, labels, schemes, eng_chunk(a))
     roof, ec_roof = roofline(stages, units, a.steps)
     if roof is not None:
-        roof["i2p_equiv_TMAC32"] = round(roof["achieved"] * MAC32_PER_ED25519 / MAC32_ED_LADDER, 3)
+        roof["i2p_equiv_TMAC32"] = round(roof["achieved"] * MAC32_PER_ED25519 / roof["work_per_item"], 3)
         roof["traffic"] = None
         if os.path.exists(TRAFFIC_FILE):
             with open(TRAFFIC_FILE) as f:
                 tr = json.load(f)
             if tr.get("kernel_version") == KERNEL_VERSION and tr.get("items") == a.items:
-                roof["traffic"] = tr.get("hbm_bytes_per_launch", {}).get("k_ed_ladder_pf")
+                roof["traffic"] = tr.get("hbm_bytes_per_launch", {}).get(roof["kernel"])
                 roof["traffic_source"] = tr.get("source")
                 if "valu_issue" in tr:
                     roof["valu_issue"] = tr["valu_issue"]

@@ -42,7 +42,8 @@ class cg_pool_stats(ctypes.Structure):
 ABI_VERSION = 2
 FLAG_STAGE_TIMING = 1
 STAGE_NAMES = ["plan", "ed_hash", "ed_ladder", "ed_ladder_row0", "ed_finish", "r1_front", "r1_ladder",
-               "r1_ladder_row0", "k1_front", "k1_ladder", "k1_ladder_row0"]
+               "r1_ladder_row0", "k1_front", "k1_ladder", "k1_ladder_row0", "ed_ladder_wide", "r1_ladder_wide",
+               "k1_ladder_wide"]
 
 
 def declared_symbols():

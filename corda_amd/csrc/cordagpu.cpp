@@ -56,6 +56,16 @@ struct DevBuf {
     if (e == hipSuccess) cap = want;
     return e;
   }
+  // exactly `bytes` (no growth margin): for the multi-GB wide-table pools
+  hipError_t ensure_exact(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
   void release() {
     if (p) hipFree(p);
     p = nullptr;
@@ -74,6 +84,7 @@ struct cg_ctx {
                    {nullptr, nullptr, nullptr}, nullptr};
   std::mutex mu;
   DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
+  DevBuf wide;  // wide-table pools (keyws.h), sized by the largest call's item count
   // transaction pipeline: verify items, spliced messages, templates; host-entry staging
   DevBuf txitems, msgs, tmpls, h_txs, h_comps, h_sigs, h_ids, h_txst;
   // tear-offs: leaf-hash workspace
@@ -107,14 +118,25 @@ uint64_t chunk_of(const cg_ctx* c, uint64_t n) {
   return (n + k - 1) / k;
 }
 
-// Key and item workspace for n_keys keys and chunks of ws_items items. Growing it waits for the
-// device (cg_reserve ahead of time avoids that).
-hipError_t ensure_ws(cg_ctx* c, uint32_t n_keys, uint64_t ws_items) {
-  if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= cg::item_ws_bytes(ws_items)) return hipSuccess;
+// Key and item workspace for n_keys keys and chunks of ws_items items, plus the wide-table pools
+// for a call of call_items items (0: none). Growing them waits for the device (cg_reserve ahead
+// of time avoids that).
+hipError_t ensure_ws(cg_ctx* c, uint32_t n_keys, uint64_t ws_items, uint64_t call_items = 0) {
+  const size_t wide = cg::wide_bytes(n_keys, call_items);
+  if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= cg::item_ws_bytes(ws_items) &&
+      c->wide.cap >= wide)
+    return hipSuccess;
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess) e = c->keyprep.ensure(cg::keyprep_bytes(n_keys));
   if (e == hipSuccess) e = c->itemws.ensure(cg::item_ws_bytes(ws_items));
+  if (e == hipSuccess) e = c->wide.ensure_exact(wide);
   return e;
+}
+
+// The wide pools a call may use: what ensure_ws reserved for it (none if the buffer is short).
+cg::WidePool wide_for(cg_ctx* c, uint32_t n_keys, uint64_t n_items) {
+  if (c->wide.cap < cg::wide_bytes(n_keys, n_items)) return cg::WidePool{};
+  return cg::make_wide_pool(c->wide.p, n_keys, n_items);
 }
 
 // Key tables once for the whole call (sized by every item's key use), then the items in chunks.
@@ -122,12 +144,14 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
                           const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, hipStream_t s,
                           const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0) {
   if (n_items == 0) return hipSuccess;
-  hipError_t e = cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork, d_items, n_items);
+  const cg::WidePool wp = wide_for(c, n_keys, n_items);
+  hipError_t e =
+      cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork, d_items, n_items, &wp);
   const uint64_t per = chunk_of(c, n_items);
   for (uint64_t f = 0; f < n_items && e == hipSuccess; f += per) {
     const uint64_t cnt = per < n_items - f ? per : n_items - f;
     e = cg::launch_items(d_keys, n_keys, d_items + f, cnt, d_arena, arena_len, mode, d_status + f, c->keyprep.p,
-                         c->itemws.p, c->btab.p, s, d_msgs, msgs_len, &c->fork);
+                         c->itemws.p, c->btab.p, s, d_msgs, msgs_len, &c->fork, &wp);
   }
   return e;
 }
@@ -228,7 +252,7 @@ int verify_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_
   HIP_TRY(c->items.ensure(sizeof(cg_item) * n_items), "hipMalloc(items)");
   HIP_TRY(c->arena.ensure((P.win.hi - P.win.lo) + 16), "hipMalloc(arena window)");
   HIP_TRY(c->status.ensure(n_items), "hipMalloc(status)");
-  HIP_TRY(ensure_ws(c, n_keys, per_max), "hipMalloc(workspace)");
+  HIP_TRY(ensure_ws(c, n_keys, per_max, n_items), "hipMalloc(workspace)");
   while (c->seg.size() < nch) {
     hipEvent_t e;
     HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
@@ -252,7 +276,9 @@ int verify_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_
   const cg_key* dk = (const cg_key*)c->keys.p;
   const cg_item* di = (const cg_item*)c->items.p;
   uint8_t* ds = (uint8_t*)c->status.p;
-  HIP_TRY(cg::launch_keyprep(dk, n_keys, dbase, arena_len, c->keyprep.p, s, &c->fork, di, n_items), "launch_keyprep");
+  const cg::WidePool wp = wide_for(c, n_keys, n_items);
+  HIP_TRY(cg::launch_keyprep(dk, n_keys, dbase, arena_len, c->keyprep.p, s, &c->fork, di, n_items, &wp),
+          "launch_keyprep");
   for (uint64_t k = 0; k < nch; ++k) {
     HIP_TRY(copy_missing(have, P.ext[k], arena, dwin, P.win.lo, c->copy), "H2D arena");
     HIP_TRY(hipEventRecord(c->seg[k], c->copy), "hipEventRecord");
@@ -260,7 +286,7 @@ int verify_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_
     if (k == 0) HIP_TRY(hipEventRecord(c->tev[1], s), "hipEventRecord");
     const uint64_t f = P.first[k], cnt = P.first[k + 1] - f;
     HIP_TRY(cg::launch_items(dk, n_keys, di + f, cnt, dbase, arena_len, mode, ds + f, c->keyprep.p, c->itemws.p,
-                             c->btab.p, s, nullptr, 0, &c->fork), "launch_items");
+                             c->btab.p, s, nullptr, 0, &c->fork, &wp), "launch_items");
   }
   HIP_TRY(hipEventRecord(c->tev[2], s), "hipEventRecord");
   HIP_TRY(hipMemcpyAsync(status_out, ds, n_items, hipMemcpyDeviceToHost, s), "D2H status");
@@ -352,6 +378,7 @@ void cg_close(cg_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   c->keyprep.release();
   c->itemws.release();
+  c->wide.release();
   c->btab.release();
   c->keys.release();
   c->items.release();
@@ -418,7 +445,7 @@ int cg_reserve(cg_ctx* c, uint32_t max_keys, uint64_t max_items) {
   if (!c) return fail(CG_ERR_ARG, "cg_reserve: ctx is NULL");
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  HIP_TRY(ensure_ws(c, max_keys, chunk_of(c, max_items)), "hipMalloc(workspace)");
+  HIP_TRY(ensure_ws(c, max_keys, chunk_of(c, max_items), max_items), "hipMalloc(workspace)");
   return CG_OK;
 }
 
@@ -431,7 +458,7 @@ int cg_verify_batch_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   std::lock_guard<std::mutex> g(c->mu);
   if (c->fault) return fail(CG_ERR_DEVICE, "cg_verify_batch_device: device fault (injected)");
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  HIP_TRY(ensure_ws(c, n_keys, chunk_of(c, n_items)), "hipMalloc(workspace)");
+  HIP_TRY(ensure_ws(c, n_keys, chunk_of(c, n_items), n_items), "hipMalloc(workspace)");
   hipStream_t s = stream_of(c, hip_stream);
   HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(launch_chunked(c, d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, s), "launch_verify");
@@ -649,7 +676,7 @@ static int verify_transactions_locked(cg_ctx* c, const cg_tx* d_txs, uint64_t n_
     HIP_TRY(c->msgs.ensure(need_msgs), "hipMalloc(spliced messages)");
     HIP_TRY(c->tmpls.ensure(need_tmpl), "hipMalloc(templates)");
   }
-  HIP_TRY(ensure_ws(c, n_keys, chunk_of(c, n_sigs)), "hipMalloc(workspace)");
+  HIP_TRY(ensure_ws(c, n_keys, chunk_of(c, n_sigs), n_sigs), "hipMalloc(workspace)");
   HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   if (n_tmpls)
     HIP_TRY(hipMemcpyAsync(c->tmpls.p, tmpls, sizeof(cg_signable_tmpl) * n_tmpls, hipMemcpyHostToDevice, s),

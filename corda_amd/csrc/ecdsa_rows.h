@@ -468,3 +468,150 @@ CG_HD void ec_g_rows_init(EcRowTab& T, EcRowScratch& s, const EcConsts& K) {
   ec_row_bases<C>(bases, K.gx, K.gy, K);
   for (int j = 0; j < EC_ROWS; ++j) ec_row_build<C>(T.t[j], bases[j], s, K);
 }
+
+// ---------------------------------------------------------------- wide tables (hot keys)
+// A key with many items in the call (keyws.h KEY_WIDE_MIN_USES) gets one row per signed
+// radix-2^8 digit of u2: row j holds the affine multiples 1..128 of 2^{8j} Q. The top digit
+// (bits 248..255 plus the carry) is left in [0, 256] instead of carrying into a 33rd digit, so
+// row 31 also holds the multiples 129..256, stored as a 33rd row of the table (304 128 B). G
+// gets one row per signed radix-2^12 digit of u1 over a constant table (22 rows x 2048 multiples
+// of 2^{12u} G, 3.2 MB per curve). R = one entry per row: 32 + 22 mixed additions, no doublings,
+// against 69 additions + 18 doublings over the full tables.
+#define EC_WIDE_W 8
+#define EC_WIDE_DIGITS 32
+#define EC_WIDE_ROWS 33   // row 32 = multiples 129..256 of row 31's base
+#define EC_WIDE_MULT 128
+#define EC_WIDE_PACKED 16  // int16 digits (the top one reaches 256)
+#define EC_WIDE_GW 12
+#define EC_WIDE_GDIGITS 22  // 264 bits: the top digit covers bits 252..255 plus the carry
+#define EC_WIDE_GMULT 2048
+#define EC_WIDE_GPACKED 11  // int16 digits
+
+struct EcWideTab {
+  EcAff t[EC_WIDE_ROWS][EC_WIDE_MULT];  // t[j][k-1] = k 2^{8j} Q; t[32][k-1] = (128 + k) 2^{248} Q
+};
+struct EcGWideTab {
+  EcAff t[EC_WIDE_GDIGITS][EC_WIDE_GMULT];  // t[u][k-1] = k 2^{12u} G
+};
+// Batch-inversion scratch of one wide row (the Jacobian X, Y wait in the output entries)
+struct EcWideScratch {
+  f29 z[EC_WIDE_MULT], pre[EC_WIDE_MULT];
+};
+
+// Signed radix-2^W digits of a < 2^256 (D digits), packed as int16. TopUnsigned: the last digit
+// keeps the carry (in [0, 2^W]) instead of being recentred.
+template <int W, int D, bool TopUnsigned = false>
+CG_HD void ec_recode_wide(uint32_t* packed, const u256w& a) {
+  constexpr int per = 2;
+  for (int w = 0; w < (D + per - 1) / per; ++w) packed[w] = 0;
+  int carry = 0;
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+    const int bit = t * W;
+    uint32_t v = 0;
+    if (bit < 256) {
+      const int wi = bit >> 5, sh = bit & 31;
+      uint64_t x = (uint64_t)a.w[wi] >> sh;
+      if (sh + W > 32 && wi + 1 < 8) x |= (uint64_t)a.w[wi + 1] << (32 - sh);
+      v = (uint32_t)x & ((1u << W) - 1);
+    }
+    int e = (int)v + carry;
+    if (!TopUnsigned || t + 1 < D) {
+      carry = (e + (1 << (W - 1))) >> W;
+      e -= carry << W;
+    }
+    packed[t >> 1] |= ((uint32_t)(e & 0xffff)) << ((t & 1) * 16);
+  }
+}
+
+// The affine multiples 1..cnt of `step` starting at `first` (= first + k step), one field
+// inversion for the whole run; X, Y wait in out[k] until the backward pass.
+template <int C>
+CG_HD void ec_multiples_wide(EcAff* out, const Jac& first, const Jac& step, int cnt, f29* z, f29* pre,
+                             const EcConsts& K) {
+  Jac acc = first;
+  for (int k = 0; k < cnt; ++k) {
+    if (k > 0) jac_add<C>(acc, acc, step, K);  // acc == step goes through the doubling branch
+    out[k].x = acc.X;
+    out[k].y = acc.Y;
+    z[k] = acc.Z;
+    if (k == 0) pre[0] = acc.Z;
+    else m29_mul<C, 0>(pre[k], pre[k - 1], acc.Z);
+  }
+  f29 inv;
+  m29_inv<C, 0>(inv, pre[cnt - 1], K.one_p);
+  for (int k = cnt - 1; k >= 0; --k) {
+    f29 zi, zi2, zi3;
+    if (k > 0) {
+      m29_mul<C, 0>(zi, inv, pre[k - 1]);
+      m29_mul<C, 0>(inv, inv, z[k]);
+    } else {
+      zi = inv;
+    }
+    m29_sq<C, 0>(zi2, zi);
+    m29_mul<C, 0>(zi3, zi2, zi);
+    m29_mul<C, 0>(out[k].x, out[k].x, zi2);
+    m29_mul<C, 0>(out[k].y, out[k].y, zi3);
+  }
+}
+
+// Row j of a wide table (j = 32: the multiples 129..256 of base = 2^{248} Q).
+template <int C>
+CG_HD void ec_wide_row(EcAff* out, const Jac& base, int j, f29* z, f29* pre, const EcConsts& K) {
+  if (j < EC_WIDE_DIGITS) {
+    ec_multiples_wide<C>(out, base, base, EC_WIDE_MULT, z, pre, K);
+  } else {
+    Jac F;
+    jac_dbl_n<C>(F, base, 7);  // 128 base
+    jac_add<C>(F, F, base, K);
+    ec_multiples_wide<C>(out, F, base, EC_WIDE_MULT, z, pre, K);
+  }
+}
+
+// R = u1 G + u2 Q over the wide tables, then BC's x-check. Returns 0 VALID / 1 INVALID.
+template <int C, class TabG, class TabQ>
+CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG,
+                                       const TabQ& TQ, const EcConsts& K) {
+  uint32_t dg[EC_WIDE_GPACKED], dq[EC_WIDE_PACKED];
+  ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS>(dg, u1);
+  ec_recode_wide<EC_WIDE_W, EC_WIDE_DIGITS, true>(dq, u2);
+  Jac R;
+  jac_set_inf<C>(R, K);
+#pragma unroll 1
+  for (int j = 0; j < EC_WIDE_DIGITS; ++j) {
+    const int b = ec_digit10(dq, j);  // int16 digits
+    if (b != 0) {
+      f29 x, y;
+      const int a = b < 0 ? -b : b;  // the top digit alone reaches 129..256: row 32
+      if (a > EC_WIDE_MULT) ec_pick(x, y, TQ.t[EC_WIDE_DIGITS], a - EC_WIDE_MULT);
+      else ec_pick(x, y, TQ.t[j], a);
+      if (b < 0) m29_neg<C, 0>(y, y);
+      jac_madd<C>(R, R, x, y, K);
+    }
+  }
+#pragma unroll 1
+  for (int u = 0; u < EC_WIDE_GDIGITS; ++u) {
+    const int a = ec_digit10(dg, u);  // int16 digits
+    if (a != 0) {
+      f29 x, y;
+      ec_pick(x, y, TG.t[u], a < 0 ? -a : a);
+      if (a < 0) m29_neg<C, 0>(y, y);
+      jac_madd<C>(R, R, x, y, K);
+    }
+  }
+  return ecdsa_x_check<C>(R, r, K);
+}
+
+// G wide row u, multiples 32 g + 1 .. 32 g + 32 (one lane of the per-context table build)
+template <int C>
+CG_HD void ec_gwide_group(EcAff* out, int u, int g, EcRowScratch& s, const EcConsts& K) {
+  Jac P = {K.gx, K.gy, K.one_p};
+  if (u > 0) jac_dbl_n<C>(P, P, EC_WIDE_GW * u);
+  const uint32_t m = 32u * (uint32_t)g + 1u;
+  Jac F = P;
+  for (int b = 30 - __builtin_clz(m); b >= 0; --b) {
+    jac_dbl<C>(F, F);
+    if ((m >> b) & 1u) jac_add<C>(F, F, P, K);
+  }
+  ec_multiples<C>(out, F, P, EC_MULT, s, K);
+}

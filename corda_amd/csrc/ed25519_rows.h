@@ -356,3 +356,54 @@ CG_HD void ed_btab_wb_row(ge_niels* row, const ge_p3& B, int u, const fe& d2) {
   if (CB::shift(u) > 0) ed_dbl_n(P, P, CB::shift(u));
   ed_row_multiples<CB::kMult>(row, P, d2);
 }
+
+// ---------------------------------------------------------------- wide tables (hot keys)
+// A key with many items in the call (keyws.h KEY_WIDE_MIN_USES) gets one row per signed
+// radix-2^8 digit of h: row j holds the affine multiples 1..128 of 2^{8j} (-A) (32 rows,
+// 491 520 B). B gets one row per signed radix-2^12 digit of S' over a constant table (row u
+// holds 1..2048 times 2^{12u} B, 22 rows, 5.4 MB). R' = sum of one entry per row: 32 + 22 = 54
+// mixed additions and no doublings, against 69 additions + 6 doublings over the full tables.
+#define ED_WIDE_W 8
+#define ED_WIDE_BW 12
+struct EdWideCfg {
+  static constexpr int kDigits = (253 + ED_WIDE_W - 1) / ED_WIDE_W;  // 32: h < 2^253 leaves the carry room
+  static constexpr int kRows = kDigits;
+  static constexpr int kMult = 1 << (ED_WIDE_W - 1);                 // 128
+  static constexpr int kPackedWords = (kDigits + 3) / 4;             // int8 digits
+  static constexpr int kBDigits = (253 + ED_WIDE_BW - 1) / ED_WIDE_BW;  // 22
+  static constexpr int kBMult = 1 << (ED_WIDE_BW - 1);                // 2048
+  static constexpr int kBPackedWords = (kBDigits + 1) / 2;            // int16 digits
+  static constexpr int kOps = kRows + kBDigits;                       // 54
+};
+static_assert(253 % ED_WIDE_W != 0 && 253 % ED_WIDE_BW != 0, "the top digit keeps headroom for the carry");
+
+struct EdWideTab {
+  ge_niels t[EdWideCfg::kRows][EdWideCfg::kMult];  // t[j][k-1] = k 2^{8j} (-A)
+};
+struct EdBWideTab {
+  ge_niels t[EdWideCfg::kBDigits][EdWideCfg::kBMult];  // t[u][k-1] = k 2^{12u} B
+};
+
+// R' = h (-A) + S' B over the wide tables, digits already recoded (eh: radix 2^8, esb: radix
+// 2^12). Entries by |digit|, the sign through ge_madd_signed (the form k_ed_ladder_wide runs).
+template <class TabA, class TabB, class PickA, class PickB>
+CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const TabA& TA, const TabB& TB,
+                                 PickA pick_a, PickB pick_b) {
+  ge_p3 R;
+  ge_p3_0(R);
+  ge_p1p1 t;
+  for (int o = 0; o < EdWideCfg::kOps; ++o) {
+    const bool is_b = o >= EdWideCfg::kRows;
+    const int dg = is_b ? sc_digit_h(esb, o - EdWideCfg::kRows) : sc_digit_b(eh, o);
+    const int dp = dg < 0 ? -dg : dg;
+    ge_niels n;
+    if (is_b) {
+      pick_b(n, TB.t[o - EdWideCfg::kRows], dp);
+    } else {
+      pick_a(n, TA.t[o], dp);
+    }
+    ge_madd_signed(t, R, n, dg < 0);
+    if (o + 1 < EdWideCfg::kOps) ge_p1p1_to_p3(R, t);
+  }
+  ge_p1p1_to_p2(out, t);
+}

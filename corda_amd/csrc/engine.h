@@ -10,6 +10,13 @@
 namespace cg {
 
 struct DeviceConsts;  // opaque
+// The wide-table pools of a call (keyws.h EdWideSlot / EcWideSlot arrays; host-allocated), one per
+// scheme family; caps 0 = no key gets wide tables.
+struct WidePool {
+  void* ed = nullptr;
+  void* ec = nullptr;
+  uint32_t cap_ed = 0, cap_ec = 0;
+};
 
 // Side streams + events owned by a context. Key preparation forks off the caller's stream:
 // the two ECDSA curves' tables and the Ed25519 row tables are built on side streams (each is a
@@ -62,13 +69,18 @@ hipError_t upload_constants();
 
 // Bytes of per-key workspace for n_keys keys.
 size_t keyprep_bytes(uint32_t n_keys);
+// Wide-table pools for a call of n_items over n_keys (keyws.h: keys with many items get one table
+// row per radix-2^8 digit): bytes, and the pool view over `base` (caps 0 when nothing can be wide).
+size_t wide_bytes(uint32_t n_keys, uint64_t n_items);
+WidePool make_wide_pool(void* base, uint32_t n_keys, uint64_t n_items);
 
 // Enqueue the whole verify pipeline for one batch on `stream`:
 //   key prep (one lane per key) -> per-scheme verify (one lane per item) -> status bytes.
 hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                          const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
                          void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
-                         const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0, const Fork* fork = nullptr);
+                         const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0, const Fork* fork = nullptr,
+                         const WidePool* wide = nullptr);
 // Constant base-point row table: size and one-time initialisation (per context).
 size_t btab_bytes();
 hipError_t init_btab(void* d_btab, hipStream_t stream);
@@ -78,13 +90,14 @@ size_t item_ws_bytes(uint64_t n_items);
 // without (cg_prepare_keys_device), every key gets full tables.
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream, const Fork* fork = nullptr,
-                          const cg_item* d_items = nullptr, uint64_t n_items = 0);
+                          const cg_item* d_items = nullptr, uint64_t n_items = 0, const WidePool* wide = nullptr);
 // `d_msgs` (optional): the engine's spliced-message workspace, read by items flagged
 // CG_ITEM_MSG_WS (keyws.h); caller items never carry that flag.
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
                         const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
-                        const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0, const Fork* fork = nullptr);
+                        const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0, const Fork* fork = nullptr,
+                        const WidePool* wide = nullptr);
 
 // Hashing kernels
 hipError_t launch_sha256(const cg_span* d_spans, uint64_t n, const uint8_t* d_arena, uint64_t arena_len,

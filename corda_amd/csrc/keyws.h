@@ -108,6 +108,7 @@ union BaseSlot {
 #define PLAN_K1 2
 #define PLAN_CLASSES 3
 #define PLAN_FULL 4  // ranges[PLAN_FULL + c]: first item of class c whose key has full tables
+#define PLAN_WIDE 7  // ranges[PLAN_WIDE + c]: first item of class c whose key has wide tables
 struct Plan {
   const uint32_t* perm;    // plan position -> item index
   const uint32_t* ranges;  // class c occupies positions [ranges[c], ranges[c + 1])
@@ -134,6 +135,12 @@ struct KeyWs {
                    // chain / row kernels run dense lanes however few keys are hot
   uint32_t* full_count;
   uint8_t* seen;   // 1 if any item of the batch uses the key (exact; uses is sampled)
+  uint32_t* wide_idx;    // per key: its slot in the scheme's wide pool, or KEY_NOT_WIDE
+  uint32_t* wide;        // per class c: the keys with wide tables, wide[c * n_keys + l]
+  uint32_t* wide_count;  // [c] list lengths; [PLAN_CLASSES + 0 / 1] slots taken in the Ed / EC pool
+  struct EdWideSlot* wed;  // wide pools (WidePool; empty: no key gets wide tables)
+  struct EcWideSlot* wec;
+  uint32_t cap_ed, cap_ec;
 };
 
 // How much table a key gets, from the number of items that use it in the batch (one-shot entry
@@ -147,12 +154,51 @@ struct KeyWs {
 //   more                          all 22 rows: 6 doublings per item (ed_double_scalar_wb)
 // Break-even (measured on MI355X, 2^20 Ed25519 items): a key's full tables cost ~230 ns of
 // GPU time, the row-0 ladder ~7 ns more per item than the full-table one -> ~32 items.
+// A fourth mode, for keys with >= KEY_WIDE_MIN_USES items (and a free slot in the scheme's wide
+// pool, sized by the host from the call's item count): one table row per signed radix-2^8 digit
+// (ed25519_rows.h / ecdsa_rows.h "wide tables"), 54 additions and no doublings per item. Its build
+// (4096 entries per key) pays for itself after a few hundred items.
+#ifndef KEY_WIDE_MIN_USES
+#define KEY_WIDE_MIN_USES 384u
+#endif
+#define KEY_NOT_WIDE 0xffffffffu
+#define KEY_WIDE_MAX 8192u  // wide slots per pool at most (Ed25519 4.9 GB / ECDSA 5.0 GB)
 #define KEY_USES_ALL 0xffffffffu
 #define KEY_USES_SAMPLE 4u  // k_key_uses samples by the top 2 bits of a 32-bit hash: 1 in 4
 #ifndef ED_DIRECT_MAX_USES
 #define ED_DIRECT_MAX_USES 32u
 #endif
-static inline KeyWs key_ws(void* base, uint32_t n_keys) {
+// Wide-table slot of one key: the table, its row bases and the row builds' inversion scratch.
+struct EdWideSlot {
+  EdWideTab tab;
+  ge_p3 bases[EdWideCfg::kRows];
+  fe zpre[EdWideCfg::kRows][EdWideCfg::kMult];
+};
+struct EcWideSlot {
+  EcWideTab tab;
+  Jac bases[EC_WIDE_DIGITS];
+  EcWideScratch s[EC_WIDE_ROWS];
+};
+// Slots for a call of n_items over n_keys: no more keys can reach KEY_WIDE_MIN_USES.
+static inline uint32_t wide_cap(uint32_t n_keys, uint64_t n_items) {
+  uint64_t c = n_items / KEY_WIDE_MIN_USES;
+  if (c > n_keys) c = n_keys;
+  if (c > KEY_WIDE_MAX) c = KEY_WIDE_MAX;
+  return (uint32_t)c;
+}
+static inline size_t wide_pool_bytes(uint32_t cap) {
+  return cap ? al256((size_t)cap * sizeof(EdWideSlot)) + al256((size_t)cap * sizeof(EcWideSlot)) : 0;
+}
+static inline WidePool wide_pool(void* base, uint32_t cap) {
+  WidePool p;
+  if (!base || !cap) return p;
+  p.ed = base;
+  p.ec = (uint8_t*)base + al256((size_t)cap * sizeof(EdWideSlot));
+  p.cap_ed = p.cap_ec = cap;
+  return p;
+}
+
+static inline KeyWs key_ws(void* base, uint32_t n_keys, const WidePool* wp = nullptr) {
   const size_t n = n_keys ? n_keys : 1;
   uint8_t* p = (uint8_t*)base;
   KeyWs w;
@@ -171,12 +217,23 @@ static inline KeyWs key_ws(void* base, uint32_t n_keys) {
   w.full_count = (uint32_t*)p;
   p += 256;
   w.seen = p;
+  p += al256(n);
+  w.wide_idx = (uint32_t*)p;
+  p += al256(n * sizeof(uint32_t));
+  w.wide = (uint32_t*)p;
+  p += al256(3 * n * sizeof(uint32_t));
+  w.wide_count = (uint32_t*)p;
+  w.wed = wp ? (EdWideSlot*)wp->ed : nullptr;
+  w.wec = wp ? (EcWideSlot*)wp->ec : nullptr;
+  w.cap_ed = wp ? wp->cap_ed : 0;
+  w.cap_ec = wp ? wp->cap_ec : 0;
   return w;
 }
 static inline size_t key_ws_bytes(uint32_t n_keys) {
   const size_t n = n_keys ? n_keys : 1;
   return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(TabSlot)) + al256(n * KEY_BASES * sizeof(BaseSlot)) +
-         n * EC_ROWS * sizeof(EcRowScratch) + al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256 + al256(n);
+         n * EC_ROWS * sizeof(EcRowScratch) + al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256 +
+         al256(n) + al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256;
 }
 
 // Per-item workspace slot (indexed by plan position, so the schemes never share one):
@@ -219,18 +276,28 @@ static inline size_t item_ws_total(uint64_t n_items) {
   return al256(n * ITEM_SLOT) + 4 * al256(n * sizeof(uint32_t)) + 256 + al256(plan_sort_temp_bytes(n));
 }
 hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d_keys, uint32_t n_keys,
-                       const uint32_t* d_uses, const ItemWs& iw, hipStream_t stream);
+                       const uint32_t* d_uses, const uint32_t* d_wide_idx, const ItemWs& iw, hipStream_t stream);
 
-// Constant tables per context: [Ed25519 B rows (radix 2^10)][G rows k1][G rows r1][row scratch]
+// Constant tables per context: [Ed25519 B rows (radix 2^10)][G rows k1][G rows r1]
+// [Ed25519 B wide rows (radix 2^12)][G wide rows k1][G wide rows r1][row scratch]
 #define EC_GTAB_LANES (EC_G_DIGITS * (EC_G_MULT / EC_MULT))  // one lane per (row, group of 32)
+#define EC_GWIDE_LANES (EC_WIDE_GDIGITS * (EC_WIDE_GMULT / EC_MULT))
+#define CONST_SCRATCH_LANES (EC_GWIDE_LANES > EC_GTAB_LANES ? EC_GWIDE_LANES : EC_GTAB_LANES)
 static inline size_t const_tab_bytes() {
-  return sizeof(EdBTab) + 2 * sizeof(EcGTab) + EC_GTAB_LANES * sizeof(EcRowScratch);
+  return sizeof(EdBTab) + 2 * sizeof(EcGTab) + sizeof(EdBWideTab) + 2 * sizeof(EcGWideTab) +
+         CONST_SCRATCH_LANES * sizeof(EcRowScratch);
 }
 static inline const EcGTab* gtab(const void* d_btab, int curve) {
   return (const EcGTab*)((const uint8_t*)d_btab + sizeof(EdBTab)) + curve;
 }
+static inline const EdBWideTab* bwide(const void* d_btab) {
+  return (const EdBWideTab*)((const uint8_t*)d_btab + sizeof(EdBTab) + 2 * sizeof(EcGTab));
+}
+static inline const EcGWideTab* gwide(const void* d_btab, int curve) {
+  return (const EcGWideTab*)((const uint8_t*)bwide(d_btab) + sizeof(EdBWideTab)) + curve;
+}
 static inline EcRowScratch* const_scratch(void* d_btab) {
-  return (EcRowScratch*)((uint8_t*)d_btab + sizeof(EdBTab) + 2 * sizeof(EcGTab));
+  return (EcRowScratch*)((uint8_t*)gwide(d_btab, 0) + 2 * sizeof(EcGWideTab));
 }
 
 // Intermediate per-item status codes (never returned to the caller)
@@ -251,6 +318,8 @@ void ed_launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_
                      const ItemWs& iw, hipStream_t stream);
 void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
                       const ItemWs& iw, const void* d_btab, hipStream_t stream);
+void ed_launch_ladder_wide(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                           const ItemWs& iw, const void* d_btab, hipStream_t stream);
 void ed_launch_finish(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
                       uint8_t* d_status, const ItemWs& iw, hipStream_t stream);
 hipError_t ec_upload_constants();
@@ -264,5 +333,7 @@ void ec_launch_front(int curve, const cg_item* d_items, uint64_t n_items, const 
                      uint64_t msgs_len, const ItemWs& iw, hipStream_t stream);
 void ec_launch_ladder(int curve, bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status,
                       const KeyWs& w, const ItemWs& iw, const void* d_btab, hipStream_t stream);
+void ec_launch_ladder_wide(int curve, const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                           const ItemWs& iw, const void* d_btab, hipStream_t stream);
 
 }  // namespace cg

@@ -7,8 +7,8 @@
 // is stable (LSD radix): input order is kept within a key. No per-item atomics, so a hot key
 // (a notary's) costs nothing extra.
 //   k_plan_keys    composite key (class | table mode | key_idx) and the identity permutation; the
-//                  mode bit (keyws.h) keeps row-0 and full-table items in separate waves
-//   rocprim::radix_sort_pairs over key_bits + 3 bits
+//                  mode bits (keyws.h) keep row-0, full- and wide-table items in separate waves
+//   rocprim::radix_sort_pairs over key_bits + 4 bits
 //   k_plan_ranges  class boundaries by binary search in the sorted keys
 #include <hip/hip_runtime.h>
 
@@ -26,15 +26,17 @@ typedef rocprim::radix_sort_config<rocprim::default_config, rocprim::default_con
 
 static uint32_t key_bits(uint32_t n_keys) {
   uint32_t b = 1;
-  while (b < 29 && (1u << b) < n_keys) ++b;  // 2 class bits + the mode bit + 29 key bits
+  while (b < 28 && (1u << b) < n_keys) ++b;  // 2 class bits + 2 mode bits + 28 key bits
   return b;
 }
 
-// kb = key bits + 1: below the class, the key's table mode (1 = full tables, keyws.h) sits above
-// the key index, so a wave's lanes run one ladder variant, not both
+// kb = key bits + 2: below the class, the key's table mode (0 row 0, 1 full, 2 wide tables,
+// keyws.h) sits above the key index, so a wave's lanes run one ladder variant. Keys beyond 2^28
+// share sort positions (the index is masked): locality only, never a verdict.
 __global__ void __launch_bounds__(256) k_plan_keys(const cg_item* __restrict__ items, uint64_t n_items,
                                                    const cg_key* __restrict__ keys, uint32_t n_keys, uint32_t kb,
                                                    const uint32_t* __restrict__ uses,
+                                                   const uint32_t* __restrict__ wide_idx,
                                                    uint32_t* __restrict__ skey, uint32_t* __restrict__ sval) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_items) return;
@@ -47,26 +49,37 @@ __global__ void __launch_bounds__(256) k_plan_keys(const cg_item* __restrict__ i
       : s == CG_ECDSA_SECP256K1_SHA256 ? PLAN_K1
                                        : PLAN_CLASSES;
   }
-  const uint32_t full = (c < PLAN_CLASSES && uses[k] >= ED_DIRECT_MAX_USES) ? 1u : 0u;
-  skey[i] = (c << kb) | (c < PLAN_CLASSES ? (full << (kb - 1)) | k : 0u);
+  uint32_t mode = 0;
+  if (c < PLAN_CLASSES) mode = wide_idx[k] != KEY_NOT_WIDE ? 2u : uses[k] >= ED_DIRECT_MAX_USES ? 1u : 0u;
+  skey[i] = (c << kb) | (c < PLAN_CLASSES ? (mode << (kb - 2)) | (k & ((1u << (kb - 2)) - 1u)) : 0u);
   sval[i] = (uint32_t)i;
 }
 
 __global__ void k_plan_ranges(const uint32_t* __restrict__ skey, uint64_t n_items, uint32_t kb,
                               uint32_t* __restrict__ ranges) {
   // lanes 0..3: class starts ranges[c] (ranges[3] = end of the verified classes); lanes 4..6:
-  // ranges[PLAN_FULL + c] = first full-table item of class c (the mode bit, keyws.h)
+  // ranges[PLAN_FULL + c] = first full-table item of class c; lanes 7..9: ranges[PLAN_WIDE + c] =
+  // first wide-table item of class c (the mode bits, keyws.h)
   const uint32_t t = threadIdx.x;
-  if (t > PLAN_CLASSES + PLAN_CLASSES) return;
-  const uint32_t c = t <= PLAN_CLASSES ? t : t - PLAN_CLASSES - 1;
-  const uint32_t target = t <= PLAN_CLASSES ? c << kb : (c << kb) | (1u << (kb - 1));
+  if (t >= PLAN_WIDE + PLAN_CLASSES) return;
+  uint32_t c, target;
+  if (t <= PLAN_CLASSES) {
+    c = t;
+    target = c << kb;
+  } else if (t < PLAN_WIDE) {
+    c = t - PLAN_FULL;
+    target = (c << kb) | (1u << (kb - 2));
+  } else {
+    c = t - PLAN_WIDE;
+    target = (c << kb) | (2u << (kb - 2));
+  }
   uint64_t lo = 0, hi = n_items;  // first position with key >= target
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
     if (skey[mid] < target) lo = mid + 1;
     else hi = mid;
   }
-  ranges[t <= PLAN_CLASSES ? c : PLAN_FULL + c] = (uint32_t)lo;
+  ranges[t] = (uint32_t)lo;
 }
 
 size_t plan_sort_temp_bytes(uint64_t n_items) {
@@ -78,11 +91,11 @@ size_t plan_sort_temp_bytes(uint64_t n_items) {
 }
 
 hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d_keys, uint32_t n_keys,
-                       const uint32_t* d_uses, const ItemWs& iw, hipStream_t stream) {
-  const uint32_t kb = key_bits(n_keys) + 1;  // + the table-mode bit
+                       const uint32_t* d_uses, const uint32_t* d_wide_idx, const ItemWs& iw, hipStream_t stream) {
+  const uint32_t kb = key_bits(n_keys) + 2;  // + the table-mode bits
   const uint32_t B = 256;
   hipLaunchKernelGGL(k_plan_keys, dim3((unsigned)((n_items + B - 1) / B)), dim3(B), 0, stream, d_items, n_items,
-                     d_keys, n_keys, kb, d_uses, iw.skey_in, iw.sval_in);
+                     d_keys, n_keys, kb, d_uses, d_wide_idx, iw.skey_in, iw.sval_in);
   size_t bytes = iw.sort_temp_bytes;
   hipError_t e = rocprim::radix_sort_pairs<PlanSortConfig>(iw.sort_temp, bytes, (const uint32_t*)iw.skey_in, iw.skey_out,
                                            (const uint32_t*)iw.sval_in, iw.perm, (size_t)n_items, 0u, kb + 2,

@@ -31,12 +31,15 @@ __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_item
 // stores: the exact "has items" bit row 0 depends on). Out-of-range key indices are
 // k_misc_status's (CG_NOT_RUN) and count nowhere.
 __global__ void __launch_bounds__(256) k_key_init(uint32_t n_keys, uint32_t all, uint32_t* __restrict__ uses,
-                                                  uint8_t* __restrict__ seen, uint32_t* __restrict__ full_count) {
+                                                  uint8_t* __restrict__ seen, uint32_t* __restrict__ full_count,
+                                                  uint32_t* __restrict__ wide_idx, uint32_t* __restrict__ wide_count) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < PLAN_CLASSES) full_count[i] = 0;
+  if (i < PLAN_CLASSES + 2) wide_count[i] = 0;
   if (i >= n_keys) return;
   uses[i] = all ? KEY_USES_ALL : 0u;
   seen[i] = all ? 1 : 0;
+  wide_idx[i] = KEY_NOT_WIDE;
 }
 
 __global__ void __launch_bounds__(256) k_key_uses(const cg_item* __restrict__ items, uint64_t n_items,
@@ -52,14 +55,33 @@ __global__ void __launch_bounds__(256) k_key_uses(const cg_item* __restrict__ it
   if (((uint32_t)i * 0x9E3779B1u) >> 30 == 0) atomicAdd(&uses[k], KEY_USES_SAMPLE);
 }
 
-// Keys that get full tables (uses >= ED_DIRECT_MAX_USES), compacted per scheme class with one
-// atomic per wave and class. One wave per block.
+// Append the lanes with c == k to list k (one atomic per wave and class).
+__device__ __forceinline__ void list_append(int c, uint32_t i, uint32_t n_keys, uint32_t* __restrict__ list,
+                                            uint32_t* __restrict__ count) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int k = 0; k < PLAN_CLASSES; ++k) {
+    const uint64_t m = __ballot(c == k);
+    if (m == 0) continue;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(&count[k], (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (c == k) list[(size_t)k * n_keys + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+  }
+}
+
+// Table mode per key: wide tables for keys with >= KEY_WIDE_MIN_USES items while the scheme's
+// wide pool has slots (one atomic per wide key: they are few), else full tables from
+// ED_DIRECT_MAX_USES items; the wide and full keys compacted per scheme class. One wave per block.
 __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ keys, uint32_t n_keys,
                                                      uint32_t* __restrict__ uses, const uint8_t* __restrict__ seen,
-                                                     uint32_t* __restrict__ full, uint32_t* __restrict__ full_count) {
+                                                     uint32_t* __restrict__ full, uint32_t* __restrict__ full_count,
+                                                     uint32_t* __restrict__ wide_idx, uint32_t* __restrict__ wide,
+                                                     uint32_t* __restrict__ wide_count, uint32_t cap_ed,
+                                                     uint32_t cap_ec) {
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  const uint32_t lane = threadIdx.x;
-  int c = -1;
+  int c = -1, cw = -1;
   uint32_t u = 0;
   if (i < n_keys) {  // the estimate, made exact where it matters: a used key counts >= 1
     u = uses[i];
@@ -73,17 +95,22 @@ __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ 
       : s == CG_ECDSA_SECP256R1_SHA256 ? PLAN_R1
       : s == CG_ECDSA_SECP256K1_SHA256 ? PLAN_K1
                                        : -1;
+    // KEY_USES_ALL (cg_prepare_keys_device: uses unknown) never gets wide tables
+    if (c >= 0 && u >= KEY_WIDE_MIN_USES && u != KEY_USES_ALL) {
+      const int pool = c == PLAN_ED ? 0 : 1;
+      const uint32_t cap = pool == 0 ? cap_ed : cap_ec;
+      if (cap) {
+        const uint32_t slot = atomicAdd(&wide_count[PLAN_CLASSES + pool], 1u);
+        if (slot < cap) {
+          wide_idx[i] = slot;
+          cw = c;
+          c = -1;
+        }
+      }
+    }
   }
-#pragma unroll
-  for (int k = 0; k < PLAN_CLASSES; ++k) {
-    const uint64_t m = __ballot(c == k);
-    if (m == 0) continue;
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if ((int)lane == leader) base = atomicAdd(&full_count[k], (uint32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
-    if (c == k) full[(size_t)k * n_keys + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
-  }
+  list_append(c, i, n_keys, full, full_count);
+  list_append(cw, i, n_keys, wide, wide_count);
 }
 
 hipError_t upload_constants() {
@@ -93,6 +120,10 @@ hipError_t upload_constants() {
 }
 
 size_t keyprep_bytes(uint32_t n_keys) { return key_ws_bytes(n_keys); }
+size_t wide_bytes(uint32_t n_keys, uint64_t n_items) { return wide_pool_bytes(wide_cap(n_keys, n_items)); }
+WidePool make_wide_pool(void* base, uint32_t n_keys, uint64_t n_items) {
+  return wide_pool(base, wide_cap(n_keys, n_items));
+}
 size_t item_ws_bytes(uint64_t n_items) { return item_ws_total(n_items); }
 size_t btab_bytes() { return const_tab_bytes(); }
 
@@ -104,18 +135,19 @@ hipError_t init_btab(void* d_btab, hipStream_t stream) {
 
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream, const Fork* fork, const cg_item* d_items,
-                          uint64_t n_items) {
+                          uint64_t n_items, const WidePool* wide) {
   if (n_keys == 0) return hipSuccess;
-  const KeyWs w = key_ws(d_keyprep, n_keys);
+  const KeyWs w = key_ws(d_keyprep, n_keys, d_items ? wide : nullptr);
   // use counts first (main stream; the side streams fork after them)
-  const uint32_t kl = n_keys > PLAN_CLASSES ? n_keys : PLAN_CLASSES;
+  const uint32_t kl = n_keys > PLAN_CLASSES + 2 ? n_keys : PLAN_CLASSES + 2;
   hipLaunchKernelGGL(k_key_init, dim3((kl + 255) / 256), dim3(256), 0, stream, n_keys, d_items ? 0u : 1u, w.uses,
-                     w.seen, w.full_count);
+                     w.seen, w.full_count, w.wide_idx, w.wide_count);
   if (d_items && n_items)
     hipLaunchKernelGGL(k_key_uses, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, stream, d_items, n_items,
                        n_keys, w.uses, w.seen);
   hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys, w.uses,
-                     (const uint8_t*)w.seen, w.full, w.full_count);
+                     (const uint8_t*)w.seen, w.full, w.full_count, w.wide_idx, w.wide, w.wide_count, w.cap_ed,
+                     w.cap_ec);
   if (!fork) {
     ed_launch_key_abyte(d_keys, n_keys, d_arena, arena_len, w, stream);
     ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, stream, stream, nullptr, nullptr);
@@ -138,17 +170,19 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                         const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
                         const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
-                        const uint8_t* d_msgs, uint64_t msgs_len, const Fork* fork) {
+                        const uint8_t* d_msgs, uint64_t msgs_len, const Fork* fork, const WidePool* wide) {
   if (n_items == 0) return hipSuccess;
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
-  const KeyWs w = key_ws((void*)d_keyprep, n_keys);
+  const KeyWs w = key_ws((void*)d_keyprep, n_keys, wide);
   const ItemWs iw = item_ws(d_item_ws, n_items);
   hipLaunchKernelGGL(k_misc_status, dim3((unsigned)grid), dim3(B), 0, stream, d_items, n_items, d_keys, n_keys,
                      d_status);
   // plan: items sorted by (scheme class, key) (plan_sort.hip)
   hipError_t e = hipSuccess;
-  CG_TIME(fork, CG_STAGE_PLAN, stream, e = launch_plan(d_items, n_items, d_keys, n_keys, (const uint32_t*)w.uses, iw, stream));
+  CG_TIME(fork, CG_STAGE_PLAN, stream,
+          e = launch_plan(d_items, n_items, d_keys, n_keys, (const uint32_t*)w.uses, (const uint32_t*)w.wide_idx, iw,
+                          stream));
   if (e != hipSuccess) return e;
   // fronts: Ed25519 challenges (need only Abyte), ECDSA prep + s^-1 per curve (need the decoded key)
   CG_TIME(fork, CG_STAGE_ED_HASH, stream,
@@ -178,16 +212,25 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
     if (e != hipSuccess) return e;
   }
   // full-table ladders on `stream`, each after its tables; Ed25519 finish after both ladders
+  // wide-table ladders right after their class's full-table one (same tables-ready event)
   if (fork) hipStreamWaitEvent(stream, fork->ready[2], 0);
   CG_TIME(fork, CG_STAGE_ED_LADDER, stream, ed_launch_ladder(true, d_items, n_items, d_status, w, iw, d_btab, stream));
+  if (w.cap_ed)
+    CG_TIME(fork, CG_STAGE_ED_LADDER_WIDE, stream, ed_launch_ladder_wide(d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) hipStreamWaitEvent(stream, fork->row0[2], 0);
   CG_TIME(fork, CG_STAGE_ED_FINISH, stream, ed_launch_finish(d_items, n_items, d_arena, arena_len, d_status, iw, stream));
   if (fork) hipStreamWaitEvent(stream, fork->ready[0], 0);
   CG_TIME(fork, CG_STAGE_R1_LADDER, stream,
           ec_launch_ladder(CG_CURVE_R1, true, d_items, n_items, d_status, w, iw, d_btab, stream));
+  if (w.cap_ec)
+    CG_TIME(fork, CG_STAGE_R1_LADDER_WIDE, stream,
+            ec_launch_ladder_wide(CG_CURVE_R1, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) hipStreamWaitEvent(stream, fork->ready[1], 0);
   CG_TIME(fork, CG_STAGE_K1_LADDER, stream,
           ec_launch_ladder(CG_CURVE_K1, true, d_items, n_items, d_status, w, iw, d_btab, stream));
+  if (w.cap_ec)
+    CG_TIME(fork, CG_STAGE_K1_LADDER_WIDE, stream,
+            ec_launch_ladder_wide(CG_CURVE_K1, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) {
     hipStreamWaitEvent(stream, fork->row0[0], 0);
     hipStreamWaitEvent(stream, fork->row0[1], 0);
@@ -198,12 +241,12 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
 hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                          const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
                          void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
-                         const uint8_t* d_msgs, uint64_t msgs_len, const Fork* fork) {
+                         const uint8_t* d_msgs, uint64_t msgs_len, const Fork* fork, const WidePool* wide) {
   if (n_items == 0) return hipSuccess;
-  hipError_t e = launch_keyprep(d_keys, n_keys, d_arena, arena_len, d_keyprep, stream, fork, d_items, n_items);
+  hipError_t e = launch_keyprep(d_keys, n_keys, d_arena, arena_len, d_keyprep, stream, fork, d_items, n_items, wide);
   if (e != hipSuccess) return e;
   return launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, d_keyprep, d_item_ws,
-                      d_btab, stream, d_msgs, msgs_len, fork);
+                      d_btab, stream, d_msgs, msgs_len, fork, wide);
 }
 
 }  // namespace cg

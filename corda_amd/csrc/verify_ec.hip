@@ -72,6 +72,7 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_tab(const cg_key* __restrict_
                                                        const uint32_t* __restrict__ uses,
                                                        const uint32_t* __restrict__ full,
                                                        const uint32_t* __restrict__ full_count,
+                                                       const uint32_t* __restrict__ wide_idx,
                                                        TabSlot* __restrict__ tabs, EcRowScratch* __restrict__ scratch) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int c = plan_class_of_curve(C);
@@ -79,7 +80,8 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_tab(const cg_key* __restrict_
   if (g < n_keys) {
     i = (uint32_t)g;
     j = 0;
-    if (keys[i].scheme != ec_scheme<C>() || uses[i] == 0) return;
+    // a wide key's items run only the wide ladder: no row 0
+    if (keys[i].scheme != ec_scheme<C>() || uses[i] == 0 || wide_idx[i] != KEY_NOT_WIDE) return;
   } else {
     const uint64_t h = g - n_keys;
     j = 1 + (uint32_t)(h / n_keys);
@@ -89,6 +91,54 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_tab(const cg_key* __restrict_
   }
   if (hdr[i].status != 0) return;
   ec_row_build<C>(tabs[i].ec.t[j], bases[(size_t)i * KEY_BASES + j].ec, scratch[(size_t)i * EC_ROWS + j], c_ec[C]);
+}
+
+// Wide tables (ecdsa_rows.h): one lane per wide key of this curve, the 32 row bases 2^{8j} Q
+// (a chain of 248 doublings), then one lane per (wide key, row): 128 affine multiples, one
+// inversion (row 32: the multiples 129..256 of the top row's base).
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_wide_chain(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                      const uint32_t* __restrict__ wide,
+                                                      const uint32_t* __restrict__ wide_count,
+                                                      const uint32_t* __restrict__ wide_idx,
+                                                      const BaseSlot* __restrict__ bases, EcWideSlot* __restrict__ wec) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = plan_class_of_curve(C);
+  if (l >= wide_count[c]) return;
+  const uint32_t i = wide[(size_t)c * n_keys + l];
+  if (hdr[i].status != 0) return;
+  EcWideSlot& ws = wec[wide_idx[i]];
+  Jac P = bases[(size_t)i * KEY_BASES].ec;
+  ws.bases[0] = P;
+  for (int j = 1; j < EC_WIDE_DIGITS; ++j) {
+    jac_dbl_n<C>(P, P, EC_WIDE_W);
+    ws.bases[j] = P;
+  }
+}
+
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_wide_tab(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                    const uint32_t* __restrict__ wide,
+                                                    const uint32_t* __restrict__ wide_count,
+                                                    const uint32_t* __restrict__ wide_idx, EcWideSlot* __restrict__ wec) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = plan_class_of_curve(C);
+  const uint32_t l = (uint32_t)(g / EC_WIDE_ROWS), j = (uint32_t)(g % EC_WIDE_ROWS);
+  if (l >= wide_count[c]) return;
+  const uint32_t i = wide[(size_t)c * n_keys + l];
+  if (hdr[i].status != 0) return;
+  EcWideSlot& ws = wec[wide_idx[i]];
+  ec_wide_row<C>(ws.tab.t[j], ws.bases[j < EC_WIDE_DIGITS ? j : EC_WIDE_DIGITS - 1], (int)j, ws.s[j].z, ws.s[j].pre,
+                 c_ec[C]);
+}
+
+// one lane per (G wide row u, group g of 32 multiples)
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_gwide_init(EcGWideTab* __restrict__ out, EcRowScratch* __restrict__ scratch) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= EC_GWIDE_LANES) return;
+  const int u = (int)(l / (EC_WIDE_GMULT / EC_MULT)), g = (int)(l % (EC_WIDE_GMULT / EC_MULT));
+  ec_gwide_group<C>(&out->t[u][g * EC_MULT], u, g, scratch[l], c_ec[C]);
 }
 
 // one lane per (G row u, group g of 32 multiples)
@@ -166,7 +216,7 @@ __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ i
                                                    const EcItemWs* __restrict__ ws) {
   const int cls = plan_class_of_curve(C);  // the plan's mode split (plan_sort.hip)
   const uint32_t beg = Full ? ranges[PLAN_FULL + cls] : ranges[cls];
-  const uint32_t end = Full ? ranges[cls + 1] : ranges[PLAN_FULL + cls];
+  const uint32_t end = Full ? ranges[PLAN_WIDE + cls] : ranges[PLAN_FULL + cls];
   for (Walk wk = walk_units(end - beg); wk.u < wk.end; wk.u += wk.step) {
     const uint64_t p = beg + wk.u;
     const uint32_t i = perm[p];
@@ -178,6 +228,27 @@ __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ i
     } else {  // a key with few items: row 0 only (keyws.h)
       status[i] = (uint8_t)ecdsa_ladder_check_row0<C>(w.a, w.b, w.r, *gtab, tabs[key].ec.t[0], c_ec[C]);
     }
+  }
+}
+
+// the items of wide-table keys (ecdsa_rows.h ecdsa_ladder_check_wide)
+template <int C>
+__global__ void __launch_bounds__(256) k_ec_ladder_wide(const cg_item* __restrict__ items,
+                                                        const uint32_t* __restrict__ perm,
+                                                        const uint32_t* __restrict__ ranges,
+                                                        const uint32_t* __restrict__ wide_idx,
+                                                        const EcWideSlot* __restrict__ wec,
+                                                        const EcGWideTab* __restrict__ gw, uint8_t* __restrict__ status,
+                                                        const EcItemWs* __restrict__ ws) {
+  const int cls = plan_class_of_curve(C);
+  const uint32_t beg = ranges[PLAN_WIDE + cls], end = ranges[cls + 1];
+  for (Walk wk = walk_units(end - beg); wk.u < wk.end; wk.u += wk.step) {
+    const uint64_t p = beg + wk.u;
+    const uint32_t i = perm[p];
+    if (status[i] != EC_PENDING_BASE + C) continue;
+    const uint32_t key = items[i].key_idx;
+    const EcItemWs w = ws[p];
+    status[i] = (uint8_t)ecdsa_ladder_check_wide<C>(w.a, w.b, w.r, *gw, wec[wide_idx[key]].tab, c_ec[C]);
   }
 }
 
@@ -193,6 +264,11 @@ hipError_t ec_init_const(void* d_btab, hipStream_t stream) {
   hipLaunchKernelGGL(k_ec_gtab_init<CG_CURVE_K1>, g, dim3(64), 0, stream, (EcGTab*)gtab(d_btab, CG_CURVE_K1),
                      const_scratch(d_btab));
   hipLaunchKernelGGL(k_ec_gtab_init<CG_CURVE_R1>, g, dim3(64), 0, stream, (EcGTab*)gtab(d_btab, CG_CURVE_R1),
+                     const_scratch(d_btab));
+  const dim3 gw((EC_GWIDE_LANES + 63) / 64);
+  hipLaunchKernelGGL(k_ec_gwide_init<CG_CURVE_K1>, gw, dim3(64), 0, stream, (EcGWideTab*)gwide(d_btab, CG_CURVE_K1),
+                     const_scratch(d_btab));
+  hipLaunchKernelGGL(k_ec_gwide_init<CG_CURVE_R1>, gw, dim3(64), 0, stream, (EcGWideTab*)gwide(d_btab, CG_CURVE_R1),
                      const_scratch(d_btab));
   return hipGetLastError();
 }
@@ -210,7 +286,15 @@ static void launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t*
                      (const uint32_t*)w.full_count, w.bases);
   hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3((unsigned)((elanes + B - 1) / B)), dim3(B), 0, stream, d_keys, n_keys,
                      w.hdr, w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count,
-                     w.tab, w.ecs);
+                     (const uint32_t*)w.wide_idx, w.tab, w.ecs);
+  if (w.cap_ec) {
+    hipLaunchKernelGGL(k_ec_wide_chain<C>, dim3((w.cap_ec + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
+                       (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx,
+                       (const BaseSlot*)w.bases, w.wec);
+    const uint64_t wl = (uint64_t)w.cap_ec * EC_WIDE_ROWS;
+    hipLaunchKernelGGL(k_ec_wide_tab<C>, dim3((unsigned)((wl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr,
+                       (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx, w.wec);
+  }
 }
 
 void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
@@ -259,6 +343,21 @@ void ec_launch_ladder(int curve, bool full, const cg_item* d_items, uint64_t n_i
     if (full) launch_ladder_t<CG_CURVE_K1, true>(d_items, n_items, d_status, w, iw, d_btab, stream);
     else launch_ladder_t<CG_CURVE_K1, false>(d_items, n_items, d_status, w, iw, d_btab, stream);
   }
+}
+
+template <int C>
+static void launch_ladder_wide_t(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                                 const ItemWs& iw, const void* d_btab, hipStream_t stream) {
+  const uint32_t B = 256;
+  hipLaunchKernelGGL((k_ec_ladder_wide<C>), dim3(walk_grid(n_items, B, WALK_CAP(2))), dim3(B), 0, stream, d_items,
+                     iw.perm, iw.ranges, (const uint32_t*)w.wide_idx, (const EcWideSlot*)w.wec, gwide(d_btab, C),
+                     d_status, (const EcItemWs*)iw.slots);
+}
+
+void ec_launch_ladder_wide(int curve, const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                           const ItemWs& iw, const void* d_btab, hipStream_t stream) {
+  if (curve == CG_CURVE_R1) launch_ladder_wide_t<CG_CURVE_R1>(d_items, n_items, d_status, w, iw, d_btab, stream);
+  else launch_ladder_wide_t<CG_CURVE_K1>(d_items, n_items, d_status, w, iw, d_btab, stream);
 }
 
 }  // namespace cg

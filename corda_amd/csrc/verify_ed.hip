@@ -142,13 +142,15 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_tab(const cg_key* __restrict_
                                                        const uint32_t* __restrict__ uses,
                                                        const uint32_t* __restrict__ full,
                                                        const uint32_t* __restrict__ full_count,
+                                                       const uint32_t* __restrict__ wide_idx,
                                                        TabSlot* __restrict__ tabs, EcRowScratch* __restrict__ ecs) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t i, j;
   if (g < n_keys) {
     i = (uint32_t)g;
     j = 0;
-    if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || uses[i] == 0) return;
+    // a wide key's items run only the wide ladder: no row 0
+    if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || uses[i] == 0 || wide_idx[i] != KEY_NOT_WIDE) return;
   } else {
     const uint64_t h = g - n_keys;
     j = 1 + (uint32_t)(h / n_keys);
@@ -159,6 +161,39 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_tab(const cg_key* __restrict_
   if (hdr[i].status != 0) return;
   fe* zpre = (fe*)(ecs + (size_t)i * EC_ROWS) + (size_t)j * EdCfg::kMult;
   ed_row_build<EdCfg::kMult>(tabs[i].ed.t[j], bases[(size_t)i * KEY_BASES + j].ed, c_ed.d2, zpre);
+}
+
+// Wide tables (ed25519_rows.h): one lane per wide key, the 32 row bases 2^{8j} (-A) (a chain of
+// 248 doublings), then one lane per (wide key, row): the 128 affine multiples, one inversion.
+__global__ void __launch_bounds__(64) k_ed_wide_chain(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                      const uint32_t* __restrict__ wide,
+                                                      const uint32_t* __restrict__ wide_count,
+                                                      const uint32_t* __restrict__ wide_idx,
+                                                      const BaseSlot* __restrict__ bases, EdWideSlot* __restrict__ wed) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= wide_count[PLAN_ED]) return;
+  const uint32_t i = wide[(size_t)PLAN_ED * n_keys + l];
+  if (hdr[i].status != 0) return;
+  EdWideSlot& ws = wed[wide_idx[i]];
+  ge_p3 P = bases[(size_t)i * KEY_BASES].ed;
+  ws.bases[0] = P;
+  for (int j = 1; j < EdWideCfg::kRows; ++j) {
+    ed_dbl_n(P, P, ED_WIDE_W);
+    ws.bases[j] = P;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_ed_wide_tab(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                    const uint32_t* __restrict__ wide,
+                                                    const uint32_t* __restrict__ wide_count,
+                                                    const uint32_t* __restrict__ wide_idx, EdWideSlot* __restrict__ wed) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t l = (uint32_t)(g / EdWideCfg::kRows), j = (uint32_t)(g % EdWideCfg::kRows);
+  if (l >= wide_count[PLAN_ED]) return;
+  const uint32_t i = wide[(size_t)PLAN_ED * n_keys + l];
+  if (hdr[i].status != 0) return;
+  EdWideSlot& ws = wed[wide_idx[i]];
+  ed_row_build<EdWideCfg::kMult>(ws.tab.t[j], ws.bases[j], c_ed.d2, ws.zpre[j]);
 }
 
 // The base point B as an extended point (from the constant niels table entry 1*B)
@@ -184,6 +219,30 @@ __global__ void __launch_bounds__(64) k_ed_btab_init(EdBTab* __restrict__ out) {
   ge_p3 P;
   ed_base_point(P);
   if (EdBCfgT::shift(u) > 0) ed_dbl_n(P, P, EdBCfgT::shift(u));
+  ge_p3 pts[8];
+  ed_small_mul(pts[0], P, 8 * grp + 1);
+  ge_cached c;
+  ge_p3_to_cached(c, P, c_ed.d2);
+  ge_p1p1 t;
+  for (int k = 1; k < 8; ++k) {
+    ge_add_cached(t, pts[k - 1], c);
+    ge_p1p1_to_p3(pts[k], t);
+  }
+  ge_niels row[8];
+  ed_niels_batch8(row, pts, c_ed.d2);
+  for (int k = 0; k < 8; ++k) out->t[u][8 * grp + k] = row[k];
+}
+
+// Wide B rows (radix 2^12, row u = multiples of 2^{12u} B), built once per context: one lane per
+// (row, group of 8 multiples)
+__global__ void __launch_bounds__(64) k_ed_bwide_init(EdBWideTab* __restrict__ out) {
+  constexpr uint32_t G = EdWideCfg::kBMult / 8;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t u = g / G, grp = g % G;
+  if (u >= (uint32_t)EdWideCfg::kBDigits) return;
+  ge_p3 P;
+  ed_base_point(P);
+  if (u > 0) ed_dbl_n(P, P, ED_WIDE_BW * (int)u);
   ge_p3 pts[8];
   ed_small_mul(pts[0], P, 8 * grp + 1);
   ge_cached c;
@@ -228,6 +287,12 @@ struct EdDigits {
   uint32_t pad[(ITEM_SLOT - 4 * (EdCfg::kPackedWords + EdBCfgT::kPackedWords)) / 4];
 };
 static_assert(sizeof(EdDigits) == ITEM_SLOT, "digits must fill one item slot");
+// the same hand-off for an item of a wide-table key: h in radix 2^8, S' in radix 2^12
+struct EdDigitsWide {
+  uint32_t eh[EdWideCfg::kPackedWords], es[EdWideCfg::kBPackedWords];
+  uint32_t pad[(ITEM_SLOT - 4 * (EdWideCfg::kPackedWords + EdWideCfg::kBPackedWords)) / 4];
+};
+static_assert(sizeof(EdDigitsWide) == ITEM_SLOT, "digits must fill one item slot");
 
 // One lane per Ed25519 plan position: item checks, h = SHA-512(R || Abyte || M) mod L,
 // S' = i2p's slide value of S mod L, both recoded to signed radix-64 digits. Needs only the
@@ -242,7 +307,7 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
                                             const uint32_t* __restrict__ perm, const EdKeyHdr* __restrict__ hdr,
                                             const uint8_t* __restrict__ arena, uint64_t arena_len,
                                             const uint8_t* __restrict__ msgs, uint64_t msgs_len, uint32_t mode,
-                                            uint8_t* __restrict__ status, EdDigits* __restrict__ dig) {
+                                            uint8_t* __restrict__ status, EdDigits* __restrict__ dig, bool wide) {
   const uint32_t i = perm[p];
   const cg_item it = items[i];
   const EdKeyHdr* kh = hdr + it.key_idx;
@@ -280,10 +345,17 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
         sc_sub(sr, sr, r1);
       }
     }
-    EdDigits d;
-    sc_recode_w<ED_W>(d.eh, EdCfg::kPackedWords, h);
-    sc_recode_w16<ED_WB>(d.es, EdBCfgT::kPackedWords, sr);
-    dig[p] = d;
+    if (wide) {
+      EdDigitsWide d;
+      sc_recode_w<ED_WIDE_W>(d.eh, EdWideCfg::kPackedWords, h);
+      sc_recode_w16<ED_WIDE_BW>(d.es, EdWideCfg::kBPackedWords, sr);
+      ((EdDigitsWide*)dig)[p] = d;
+    } else {
+      EdDigits d;
+      sc_recode_w<ED_W>(d.eh, EdCfg::kPackedWords, h);
+      sc_recode_w16<ED_WB>(d.es, EdBCfgT::kPackedWords, sr);
+      dig[p] = d;
+    }
     st = (uint8_t)ED_PENDING;
   }
   status[i] = st;
@@ -294,9 +366,9 @@ __global__ void __launch_bounds__(256, ED_HASH_WAVES_PER_SIMD) k_ed_hash(
     const EdKeyHdr* __restrict__ hdr, const uint8_t* __restrict__ arena, uint64_t arena_len,
     const uint8_t* __restrict__ msgs, uint64_t msgs_len, uint32_t mode, uint8_t* __restrict__ status,
     EdDigits* __restrict__ dig) {
-  const uint32_t beg = ranges[PLAN_ED];
+  const uint32_t beg = ranges[PLAN_ED], wbeg = ranges[PLAN_WIDE + PLAN_ED];
   for (Walk w = walk_units(ranges[PLAN_ED + 1] - beg); w.u < w.end; w.u += w.step)
-    ed_hash_one(beg + w.u, items, perm, hdr, arena, arena_len, msgs, msgs_len, mode, status, dig);
+    ed_hash_one(beg + w.u, items, perm, hdr, arena, arena_len, msgs, msgs_len, mode, status, dig, beg + w.u >= wbeg);
 }
 
 // One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the row tables (B rows
@@ -458,7 +530,7 @@ __global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_pf(
   __shared__ __attribute__((aligned(16))) uint8_t stage[4 * EdOps::kWaveBytes];
   const uint32_t beg = ranges[PLAN_FULL + PLAN_ED];
   uint8_t* wave_lds = stage + (threadIdx.x >> 6) * EdOps::kWaveBytes;
-  for (Walk w = walk_units(ranges[PLAN_ED + 1] - beg); w.u < w.end; w.u += w.step) {
+  for (Walk w = walk_units(ranges[PLAN_WIDE + PLAN_ED] - beg); w.u < w.end; w.u += w.step) {
     const uint64_t p = beg + w.u;
     const uint32_t i = perm[p];
     const uint32_t key = items[i].key_idx;
@@ -475,6 +547,91 @@ __global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_pf(
     ((ge_p2*)slots)[p] = q;
   }
 }
+// ---------------------------------------------------------------- wide-table ladder
+// ed_double_scalar_wide as a flat sequence of 54 signed mixed additions (32 rows of the key's
+// wide table, then the 22 radix-2^12 B rows), no doublings; each op's entry gathered into LDS
+// one op ahead exactly as in ed_double_scalar_pf.
+__device__ __forceinline__ void ed_wide_op(int o, int& widx, int& sh, bool& is_b, int& row) {
+  is_b = o >= EdWideCfg::kRows;
+  if (!is_b) {
+    widx = o >> 2;
+    sh = (o & 3) * 8;
+    row = o;
+  } else {
+    const int u = o - EdWideCfg::kRows;
+    widx = EdWideCfg::kPackedWords + (u >> 1);
+    sh = (u & 1) * 16;
+    row = u;
+  }
+}
+
+__device__ __forceinline__ const ge_niels* ed_wide_src(const EdWideTab& TA, const EdBWideTab& TB, bool is_b, int row,
+                                                       int d) {
+  const int a = d < 0 ? -d : d;
+  const int idx = a > 0 ? a - 1 : 0;
+  return is_b ? &TB.t[row][idx] : &TA.t[row][idx];
+}
+
+__device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint32_t* __restrict__ dw,
+                                                         const EdWideTab& TA, const EdBWideTab& TB, uint8_t* wave_lds,
+                                                         uint32_t lane) {
+  constexpr int N = EdWideCfg::kOps;
+  const uint32_t wl = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(cg_lds_ptr)wave_lds);
+  int widx, sh, row;
+  bool is_b;
+  ed_wide_op(0, widx, sh, is_b, row);
+  int d_cur = ed_op_digit(dw[widx], sh, is_b);
+  ed_glds_niels(ed_wide_src(TA, TB, is_b, row, d_cur), wl);
+  ed_wide_op(1, widx, sh, is_b, row);
+  uint32_t w_next = dw[widx];
+  ge_p3 R;
+  ge_p3_0(R);
+  ge_p1p1 t;
+  for (int o = 0; o < N; ++o) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // op o's entry and op o+1's digit word
+    ge_niels n;
+    ed_lds_niels(n, wave_lds, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
+    if (d_cur == 0) ge_niels_identity(n);
+    const bool neg = d_cur < 0;
+    if (o + 1 < N) {
+      ed_wide_op(o + 1, widx, sh, is_b, row);
+      d_cur = ed_op_digit(w_next, sh, is_b);
+      ed_glds_niels(ed_wide_src(TA, TB, is_b, row, d_cur), wl);
+      if (o + 2 < N) {
+        ed_wide_op(o + 2, widx, sh, is_b, row);
+        w_next = dw[widx];
+      }
+    }
+    ge_madd_signed(t, R, n, neg);
+    if (o + 1 < N) ge_p1p1_to_p3(R, t);
+  }
+  ge_p1p1_to_p2(out, t);
+}
+
+__global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_wide(
+    const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
+    const EdKeyHdr* __restrict__ hdr, const uint32_t* __restrict__ wide_idx, const EdWideSlot* __restrict__ wed,
+    const EdBWideTab* __restrict__ btab, uint8_t* __restrict__ status, void* __restrict__ slots) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4 * EdOps::kWaveBytes];
+  const uint32_t beg = ranges[PLAN_WIDE + PLAN_ED];
+  uint8_t* wave_lds = stage + (threadIdx.x >> 6) * EdOps::kWaveBytes;
+  for (Walk w = walk_units(ranges[PLAN_ED + 1] - beg); w.u < w.end; w.u += w.step) {
+    const uint64_t p = beg + w.u;
+    const uint32_t i = perm[p];
+    const uint32_t key = items[i].key_idx;
+    if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
+      status[i] = CG_KEY_INVALID;
+      continue;
+    }
+    if (status[i] != ED_PENDING) continue;
+    ge_p2 q;
+    ed_double_scalar_wide_pf(q, (const uint32_t*)((const uint8_t*)slots + (size_t)p * ITEM_SLOT),
+                             wed[wide_idx[key]].tab, *btab, wave_lds, __lane_id());
+    ((ge_p2*)slots)[p] = q;
+  }
+}
+
 // One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the per-key rows and the
 // constant radix-2^10 B table (both in global memory; the B table stays L2-resident), left
 // projective in the item slot.
@@ -487,7 +644,7 @@ __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
     uint8_t* __restrict__ status, void* __restrict__ slots) {
   // the plan's mode split: row-0 keys' items first, then full-table keys' (plan_sort.hip)
   const uint32_t beg = Full ? ranges[PLAN_FULL + PLAN_ED] : ranges[PLAN_ED];
-  const uint32_t end = Full ? ranges[PLAN_ED + 1] : ranges[PLAN_FULL + PLAN_ED];
+  const uint32_t end = Full ? ranges[PLAN_WIDE + PLAN_ED] : ranges[PLAN_FULL + PLAN_ED];
   for (Walk w = walk_units(end - beg); w.u < w.end; w.u += w.step) {
     const uint64_t p = beg + w.u;
     const uint32_t i = perm[p];
@@ -572,6 +729,8 @@ hipError_t ed_upload_constants() {
 hipError_t ed_init_const(void* d_btab, hipStream_t stream) {
   const uint32_t lanes = EdBCfgT::kDigits * (EdBCfgT::kMult / 8);
   hipLaunchKernelGGL(k_ed_btab_init, dim3((lanes + 63) / 64), dim3(64), 0, stream, (EdBTab*)d_btab);
+  const uint32_t wlanes = EdWideCfg::kBDigits * (EdWideCfg::kBMult / 8);
+  hipLaunchKernelGGL(k_ed_bwide_init, dim3((wlanes + 63) / 64), dim3(64), 0, stream, (EdBWideTab*)bwide(d_btab));
   return hipGetLastError();
 }
 
@@ -591,8 +750,16 @@ void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const uint8
                      (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.bases);
   const uint64_t lanes = (uint64_t)n_keys * EdCfg::kRows;
   hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((unsigned)((lanes + B - 1) / B)), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
-                     w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.tab,
-                     w.ecs);
+                     w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count,
+                     (const uint32_t*)w.wide_idx, w.tab, w.ecs);
+  if (w.cap_ed) {
+    hipLaunchKernelGGL(k_ed_wide_chain, dim3((w.cap_ed + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
+                       (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx,
+                       (const BaseSlot*)w.bases, w.wed);
+    const uint64_t wl = (uint64_t)w.cap_ed * EdWideCfg::kRows;
+    hipLaunchKernelGGL(k_ed_wide_tab, dim3((unsigned)((wl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr,
+                       (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx, w.wed);
+  }
 }
 
 void ed_launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
@@ -617,6 +784,14 @@ void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8
   else
     hipLaunchKernelGGL(k_ed_ladder<false>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
                        w.hdr, w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+}
+
+void ed_launch_ladder_wide(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                           const ItemWs& iw, const void* d_btab, hipStream_t stream) {
+  const uint32_t B = 256;
+  const unsigned grid = walk_grid(n_items, B, WALK_CAP(ED_LADDER_PF_WAVES));
+  hipLaunchKernelGGL(k_ed_ladder_wide, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
+                     (const uint32_t*)w.wide_idx, (const EdWideSlot*)w.wed, bwide(d_btab), d_status, iw.slots);
 }
 
 void ed_launch_finish(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,

@@ -151,7 +151,10 @@ enum {
   CG_STAGE_K1_FRONT = 8,       /* k_ec_prep + k_ec_inv, secp256k1 */
   CG_STAGE_K1_LADDER = 9,
   CG_STAGE_K1_LADDER_ROW0 = 10,
-  CG_STAGES = 11
+  CG_STAGE_ED_LADDER_WIDE = 11, /* k_ed_ladder_wide: keys with wide tables (many items in the call) */
+  CG_STAGE_R1_LADDER_WIDE = 12,
+  CG_STAGE_K1_LADDER_WIDE = 13,
+  CG_STAGES = 14
 };
 
 typedef struct cg_config {

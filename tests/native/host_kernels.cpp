@@ -476,3 +476,161 @@ extern "C" int t_ed_verify_wb_signed(const uint32_t* aw, const uint32_t* sw, con
                                      uint64_t* counts) {
   return ed_verify_wb<true>(aw, sw, msg, msg_len, counts);
 }
+
+// ---------------------------------------------------------------- wide tables (hot keys)
+// k_ed_wide_chain / k_ed_wide_tab / k_ed_bwide_init / k_ed_ladder_wide's arithmetic, bounds-checked.
+static EdBWideTab* g_TBW = nullptr;
+static void tbw_init() {
+  if (g_TBW) return;
+  g_TBW = new EdBWideTab;
+  ge_p3 B;
+  fe x, y, two_inv, t;
+  fe_sub(x, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+  fe_add(y, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+  fe_0(t);
+  t.v[0] = 2;
+  fe_invert(two_inv, t);
+  fe_mul(B.X, x, two_inv);
+  fe_mul(B.Y, y, two_inv);
+  fe_1(B.Z);
+  fe_mul(B.T, B.X, B.Y);
+  ge_p3 P = B;
+  for (int u = 0; u < EdWideCfg::kBDigits; ++u) {
+    if (u > 0) ed_dbl_n(P, P, ED_WIDE_BW);
+    ed_row_multiples<EdWideCfg::kBMult>(g_TBW->t[u], P, g_C.d2);
+  }
+}
+
+// counts (optional): [0..1] ladder fe_mul / fe_sq per item, [2..3] table build per key (chain + rows)
+extern "C" int t_ed_verify_wide(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len,
+                                uint64_t* counts) {
+  init();
+  tbw_init();
+  static EdWideTab* TA = new EdWideTab;
+  static fe (*zpre)[EdWideCfg::kMult] = new fe[EdWideCfg::kRows][EdWideCfg::kMult];
+  static EdKeyPrep kp;
+  ed_key_prep(kp, aw, g_C);
+  if (kp.status) return (int)kp.status;
+  ge_p3 A, P;
+  ed_decode_point(A, aw, g_C);
+  ed_neg_point(P, A);
+  static uint32_t last_key[8];
+  static bool have = false;
+  static uint64_t build_mul = 0, build_sq = 0;
+  if (!have || memcmp(last_key, aw, 32) != 0) {  // the fixtures reuse keys: rebuild on change
+#ifdef FE_OP_COUNT
+    g_fe_nmul = g_fe_nsq = 0;
+#endif
+    for (int j = 0; j < EdWideCfg::kRows; ++j) {  // k_ed_wide_chain, then k_ed_wide_tab per row
+      if (j > 0) ed_dbl_n(P, P, ED_WIDE_W);
+      ed_row_build<EdWideCfg::kMult>(TA->t[j], P, g_C.d2, zpre[j]);
+    }
+#ifdef FE_OP_COUNT
+    build_mul = g_fe_nmul;
+    build_sq = g_fe_nsq;
+#endif
+    memcpy(last_key, aw, 32);
+    have = true;
+  }
+  if (counts) {
+    counts[2] = build_mul;
+    counts[3] = build_sq;
+  }
+  static uint8_t buf[1 << 20];
+  memcpy(buf, msg, msg_len);
+  uint32_t pre[16], hw[16], h[8];
+  for (int i = 0; i < 8; ++i) {
+    pre[i] = sw[i];
+    pre[8 + i] = kp.abyte[i];
+  }
+  sha512_prefix64_msg(hw, pre, buf, (msg_len + 3) & ~3ull, 0, msg_len);
+  sc_reduce512(h, hw);
+  uint32_t s[8], sr[8];
+  for (int i = 0; i < 8; ++i) s[i] = sw[8 + i];
+  sc_reduce256(sr, s);
+  if ((s[7] >> 31) && sc_slide_escapes(s)) {
+    uint32_t r1[8];
+    for (int i = 0; i < 8; ++i) r1[i] = sc_R1w(i);
+    sc_sub(sr, sr, r1);
+  }
+  uint32_t eh[EdWideCfg::kPackedWords], es[EdWideCfg::kBPackedWords];
+  sc_recode_w<ED_WIDE_W>(eh, EdWideCfg::kPackedWords, h);
+  sc_recode_w16<ED_WIDE_BW>(es, EdWideCfg::kBPackedWords, sr);
+  ge_p2 R;
+#ifdef FE_OP_COUNT
+  g_fe_nmul = g_fe_nsq = 0;
+#endif
+  ed_double_scalar_wide(R, eh, es, *TA, *g_TBW, host_pick, host_pick);
+#ifdef FE_OP_COUNT
+  if (counts) {
+    counts[0] = g_fe_nmul;
+    counts[1] = g_fe_nsq;
+  }
+#endif
+  fe zi;
+  fe_invert(zi, R.Z);
+  return ed_encode_cmp(R, zi, sw);
+}
+
+// k_ec_gwide_init / k_ec_wide_chain / k_ec_wide_tab / k_ec_ladder_wide. counts (optional):
+// [0] ladder Montgomery products mod p per item, [1] table build per key (chain + rows).
+template <int C>
+static int ecdsa_wide_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off, uint32_t key_len, uint32_t fmt,
+                             uint64_t sig_off, uint32_t sig_len, uint64_t msg_off, uint64_t msg_len, uint64_t* counts) {
+  kinit();
+  const EcConsts& K = g_K[C];
+  static EcGWideTab* TG[2] = {nullptr, nullptr};
+  static EcWideTab* TQ = new EcWideTab;
+  static EcWideScratch* WS = new EcWideScratch;
+  static EcRowScratch* S = new EcRowScratch;
+  if (!TG[C]) {  // the device table build, lane by lane
+    TG[C] = new EcGWideTab;
+    constexpr int G = EC_WIDE_GMULT / EC_MULT;
+    for (int l = 0; l < EC_WIDE_GDIGITS * G; ++l)
+      ec_gwide_group<C>(&TG[C]->t[l / G][(l % G) * EC_MULT], l / G, l % G, *S, K);
+  }
+  f29 xm, ym;
+  uint32_t st = ec_key_decode_bytes<C>(xm, ym, arena, lr, key_off, key_len, fmt, K);
+  if (st) return (int)st;
+  static f29 last_x, last_y;
+  static int last_c = -1;
+  static uint64_t build_count = 0;
+  if (last_c != C || !f29_eq_raw(last_x, xm) || !f29_eq_raw(last_y, ym)) {  // rebuild on key change
+#ifdef FE_OP_COUNT
+    g_m29_nmul[C][0] = g_m29_nmul[C][1] = 0;
+#endif
+    Jac P = {xm, ym, K.one_p};
+    for (int j = 0; j < EC_WIDE_ROWS; ++j) {
+      if (j > 0 && j < EC_WIDE_DIGITS) jac_dbl_n<C>(P, P, EC_WIDE_W);
+      ec_wide_row<C>(TQ->t[j], P, j, WS->z, WS->pre, K);
+    }
+#ifdef FE_OP_COUNT
+    build_count = g_m29_nmul[C][0];
+#endif
+    last_x = xm;
+    last_y = ym;
+    last_c = C;
+  }
+  if (counts) counts[1] = build_count;
+  EcItemWs ws;
+  st = ecdsa_prep<C>(ws, arena, lr, sig_off, sig_len, arena, lr, msg_off, msg_len);
+  if (st) return (int)st;
+  ecdsa_batch_inv<C, 1>(&ws, 1, 1u, K);
+#ifdef FE_OP_COUNT
+  g_m29_nmul[C][0] = g_m29_nmul[C][1] = 0;
+#endif
+  st = ecdsa_ladder_check_wide<C>(ws.a, ws.b, ws.r, *TG[C], *TQ, K);
+#ifdef FE_OP_COUNT
+  if (counts) counts[0] = g_m29_nmul[C][0];
+#endif
+  return (int)st;
+}
+
+extern "C" int t_ecdsa_verify_wide(int scheme, const uint8_t* arena, uint64_t arena_len, uint64_t key_off,
+                                   uint32_t key_len, uint32_t fmt, uint64_t sig_off, uint32_t sig_len,
+                                   uint64_t msg_off, uint64_t msg_len, uint64_t* counts) {
+  const uint64_t lr = (arena_len + 3) & ~3ull;
+  if (scheme == 3)
+    return ecdsa_wide_verify<CG_CURVE_R1>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len, counts);
+  return ecdsa_wide_verify<CG_CURVE_K1>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len, counts);
+}

@@ -139,6 +139,37 @@ def test_key_use_modes_ecdsa_vs_c_oracle(engine):
     assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
 
 
+def test_wide_tables_vs_c_oracle(engine):
+    """Keys with >= KEY_WIDE_MIN_USES items get wide tables (keyws.h: one row per radix-2^8 digit,
+    the radix-2^12 base-point tables, no doublings) next to full-table, row-0 and invalid keys of
+    all three schemes in one shuffled batch; bit-exact against the C oracle through the host-buffer
+    and the device-resident entry points."""
+    from tools.workload import wl
+    parts = [wl.ed25519_batch(40000, n_keys=40, msg_len=270, corrupt_permille=120, seed=61, bad_key_every=13,
+                              nthreads=16)[0],
+             wl.ed25519_batch(16000, n_keys=40, msg_len=200, corrupt_permille=120, seed=62, nthreads=16)[0],
+             wl.ed25519_batch(3000, n_keys=2000, msg_len=100, corrupt_permille=120, seed=63, nthreads=16)[0],
+             wl.ecdsa_batch(0, 14000, n_keys=14, msg_len=270, corrupt_permille=120, seed=64, nthreads=16)[0],
+             wl.ecdsa_batch(1, 9000, n_keys=9, msg_len=270, corrupt_permille=120, seed=65, nthreads=16)[0],
+             wl.ecdsa_batch(0, 4000, n_keys=100, msg_len=100, corrupt_permille=120, seed=66, nthreads=16)[0]]
+    b, _ = wl.concat(parts, shuffle_seed=67)
+    uses = np.bincount(b.items["key_idx"], minlength=len(b.keys))
+    assert (uses >= 900).sum() >= 60 and ((uses >= 32) & (uses < 384)).any() and (uses == 1).any()
+    st = engine.verify(b, B.MODE_DOVERIFY)
+    ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
+    assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
+    assert (st == B.VALID).sum() > 60000 and (st == B.KEY_INVALID).any()
+    import torch  # the device-resident entry point (HBM buffers, the bench's form)
+    dev = torch.device("cuda", 0)
+    kd = torch.from_numpy(b.keys.view(np.uint8)).to(dev)
+    idd = torch.from_numpy(b.items.view(np.uint8)).to(dev)
+    ad = torch.from_numpy(b.arena).to(dev)
+    sd = torch.full((b.n,), 255, dtype=torch.uint8, device=dev)
+    engine.verify_device(kd.data_ptr(), len(b.keys), idd.data_ptr(), b.n, ad.data_ptr(), b.arena.size, sd.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(sd.cpu().numpy(), ref)
+
+
 def test_host_buffer_chunked_path(engine):
     """cg_verify_batch on a batch large enough for the chunked H2D / verify pipeline: verdicts
     equal the C oracle's, including items whose offsets point outside the arena (CG_NOT_RUN) in a

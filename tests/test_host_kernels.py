@@ -307,3 +307,75 @@ def test_mont29_ops(curve, n):
         assert int.from_bytes(out.tobytes(), "little") == (a + b) % m
         lib.t_m29_op(curve, n, 3, ptr(w(a)), ptr(w(b)), ptr(out))
         assert int.from_bytes(out.tobytes(), "little") == (a - b) % m
+
+
+def test_ed25519_wide_tables_lane_verify_on_fixtures():
+    """k_ed_ladder_wide's arithmetic (keys with many items: 32 rows x 128 multiples of 2^{8j}(-A),
+    B over 22 radix-2^12 rows, 54 signed additions, no doublings) on the fixtures, every limb
+    bound asserted."""
+    import ctypes
+    lib = hostk.lib()
+    lib.t_ed_verify_wide.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]
+    n = 0
+    for it in golden_io.load("ed25519.json"):
+        key, sig, msg = bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"])
+        if it["key_fmt"] != 0 or len(key) != 32 or len(sig) != 64:
+            continue
+        m = np.frombuffer(msg + bytes(8), dtype=np.uint8).copy()
+        st = lib.t_ed_verify_wide(ptr(words(key)), ptr(words(sig)), ptr(m), len(msg), None)
+        got = {0: "VALID", 1: "INVALID", 3: "KEY_INVALID"}[st]
+        assert got == it["expect_isvalid"], it["note"]
+        n += 1
+    assert n > 200
+
+
+def test_ecdsa_wide_tables_lane_verify_on_fixtures():
+    """k_ec_ladder_wide's arithmetic (33 rows x 128 multiples of 2^{8j} Q, G over 22 radix-2^12
+    rows, no doublings) on every ECDSA and SPKI fixture, isValid semantics."""
+    import ctypes
+    lib = hostk.lib()
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    lib.t_ecdsa_verify_wide.argtypes = [i32, vp, u64, u64, u32, u32, u64, u32, u64, u64, vp]
+    names = {0: "VALID", 1: "INVALID", 2: "SIG_MALFORMED", 3: "KEY_INVALID"}
+    n = 0
+    for it in golden_io.load("ecdsa.json") + golden_io.load("spki.json"):
+        key, sig, msg = bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"])
+        if it["scheme"] not in (2, 3):
+            continue
+        arena = np.frombuffer(key + sig + msg + bytes(8), dtype=np.uint8).copy()
+        st = lib.t_ecdsa_verify_wide(it["scheme"], ptr(arena), len(key) + len(sig) + len(msg), 0, len(key),
+                                     it["key_fmt"], len(key), len(sig), len(key) + len(sig), len(msg), None)
+        assert names[st] == it["expect_isvalid"], (it["class"], it["note"])
+        n += 1
+    assert n > 300
+
+
+def test_executed_work_constants_wide():
+    """bench.py prices k_ed_ladder_wide / k_ec_ladder_wide with the products their lane code
+    executes (full schedule: every digit non-zero) and the wide-table build per key."""
+    import ctypes
+    import bench
+    from tools.workload import wl
+    lib = hostk.lib()
+    lib.t_ed_verify_wide.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]
+    it = next(i for i in golden_io.load("ed25519.json") if i["expect"] == "VALID" and i["key_fmt"] == 0)
+    key, sig, msg = bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"])
+    m = np.frombuffer(msg + bytes(8), dtype=np.uint8).copy()
+    out = np.zeros(4, dtype=np.uint64)
+    assert lib.t_ed_verify_wide(ptr(words(key)), ptr(words(sig)), ptr(m), len(msg), ptr(out)) == 0
+    assert (int(out[0]), int(out[1])) == bench.ED_WIDE_FE
+    assert (int(out[2]), int(out[3])) == bench.ED_WIDE_BUILD_FE
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    lib.t_ecdsa_verify_wide.argtypes = [i32, vp, u64, u64, u32, u32, u64, u32, u64, u64, vp]
+    for name, scheme, curve in (("secp256r1", 3, 1), ("secp256k1", 2, 0)):
+        b, _ = wl.ecdsa_batch(curve, 96, n_keys=2, corrupt_permille=0, seed=3, nthreads=4)
+        lad = []
+        for i in range(b.n):
+            itm = b.items[i]
+            k = b.keys[itm["key_idx"]]
+            o = np.zeros(2, np.uint64)
+            assert lib.t_ecdsa_verify_wide(scheme, ptr(b.arena), b.arena.size, int(k["off"]), int(k["len"]),
+                                           int(k["fmt"]), int(itm["sig_off"]), int(itm["sig_len"]),
+                                           int(itm["msg_off"]), int(itm["msg_len"]), ptr(o)) == 0
+            lad.append(int(o[0]))
+        assert max(lad) == bench.EC_WIDE_MUL[name] and np.mean(lad) > 0.97 * max(lad), (name, lad)

@@ -51,7 +51,7 @@ MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # Ed25519 (field multiplies, squarings) in the radix-2^25.5 representation (fe25519.h):
 ED_VERIFY_FE = (500, 24)   # k_ed_ladder_pf: 43 + 26 mixed additions + 6 doublings
 ED_WIDE_FE = (377, 0)      # k_ed_ladder_wide: 32 + 22 mixed additions, no doublings (keys with wide tables)
-ED_WIDE_BUILD_FE = (62247, 9120)  # one key's wide table: 248-doubling chain + 32 rows x 128 entries
+ED_WIDE_BUILD_FE = (64871, 11296)  # one key's wide table: 248-doubling chain, 32 rows x 4 groups of 32 entries, one inversion per row
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
 ED_FINISH_K = 16
@@ -69,7 +69,9 @@ MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
 EC_LADDER_MUL = {"secp256r1": 895, "secp256k1": 877}
 EC_WIDE_MUL = {"secp256r1": 586, "secp256k1": 586}  # k_ec_ladder_wide: 32 + 22 mixed additions + x-check
 # table modes (corda_amd/csrc/keyws.h): full tables from 32 items per key, wide from 384
-KEY_FULL_MIN_USES, KEY_WIDE_MIN_USES, KEY_WIDE_MAX = 32, 384, 8192
+KEY_FULL_MIN_USES, KEY_WIDE_MAX = 32, 8192
+KEY_WIDE_MIN_USES = {4: int(os.environ.get("CG_WIDE_MIN_USES_ED", 4096)), 3: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512)),
+                     2: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512))}
 EC_INV_MUL_16 = {"secp256r1": 536, "secp256k1": 563}
 EC_MAC_PER_MUL_P = {"secp256r1": 144, "secp256k1": 162}
 EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
@@ -289,10 +291,11 @@ def ladder_units(b, labels, schemes, chunk):
     sig64 = b.items["sig_len"] == 64
     ok_ec = np.isin(labels, (0, 1, 2))
     uses = np.bincount(b.items["key_idx"], minlength=len(b.keys))
-    cap = min(len(b.keys), b.n // KEY_WIDE_MIN_USES, KEY_WIDE_MAX)
-    wide_key = uses >= KEY_WIDE_MIN_USES
+    thr = np.array([KEY_WIDE_MIN_USES.get(int(s), 1 << 30) for s in b.keys["scheme"]])
+    cap = min(len(b.keys), b.n // min(KEY_WIDE_MIN_USES.values()), KEY_WIDE_MAX)
+    wide_key = uses >= thr
     full_key = (uses >= KEY_FULL_MIN_USES) & ~wide_key
-    near = ((np.abs(uses - KEY_WIDE_MIN_USES) < 0.2 * KEY_WIDE_MIN_USES) |
+    near = ((np.abs(uses - thr) < 0.2 * thr) |
             (np.abs(uses - KEY_FULL_MIN_USES) < 0.2 * KEY_FULL_MIN_USES)) & (uses > 0)
     exact = not near.any() and all(int((wide_key & (b.keys["scheme"] == s)).sum()) <= cap for s in (2, 3, 4))
     kw, kf = wide_key[b.items["key_idx"]], full_key[b.items["key_idx"]]

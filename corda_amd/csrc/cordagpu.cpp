@@ -135,8 +135,23 @@ hipError_t ensure_ws(cg_ctx* c, uint32_t n_keys, uint64_t ws_items, uint64_t cal
 
 // The wide pools a call may use: what ensure_ws reserved for it (none if the buffer is short).
 cg::WidePool wide_for(cg_ctx* c, uint32_t n_keys, uint64_t n_items) {
-  if (c->wide.cap < cg::wide_bytes(n_keys, n_items)) return cg::WidePool{};
-  return cg::make_wide_pool(c->wide.p, n_keys, n_items);
+  static const bool off = [] {  // CG_NO_WIDE_TABLES=1: never build wide tables (A/B runs)
+    const char* v = getenv("CG_NO_WIDE_TABLES");
+    return v && v[0] == '1';
+  }();
+  if (off || c->wide.cap < cg::wide_bytes(n_keys, n_items)) return cg::WidePool{};
+  cg::WidePool p = cg::make_wide_pool(c->wide.p, n_keys, n_items);
+  static const uint32_t min_ed = [] {  // CG_WIDE_MIN_USES_ED / _EC: override the thresholds (A/B runs)
+    const char* v = getenv("CG_WIDE_MIN_USES_ED");
+    return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
+  }();
+  static const uint32_t min_ec = [] {
+    const char* v = getenv("CG_WIDE_MIN_USES_EC");
+    return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
+  }();
+  if (min_ed) p.min_ed = min_ed;
+  if (min_ec) p.min_ec = min_ec;
+  return p;
 }
 
 // Key tables once for the whole call (sized by every item's key use), then the items in chunks.
@@ -349,13 +364,30 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     delete c;
     return hip_fail(e, "hipStreamCreate");
   }
-  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamCreateWithFlags(&c->fork.side[k], hipStreamNonBlocking);
+  // Side streams: plain by default. CG_MASKED_SIDE_STREAMS=1 creates them with a CU mask covering
+  // every CU, which HIP backs with a hardware queue of their own (no sharing with the caller's
+  // stream under GPU_MAX_HW_QUEUES multiplexing); measured no faster once the table builds start
+  // after the plan sort (gpurun_out/ab_side), kept for A/B runs.
+  {
+    hipDeviceProp_t prop;
+    const char* mk = getenv("CG_MASKED_SIDE_STREAMS");
+    const bool masked = mk && mk[0] == '1' && hipGetDeviceProperties(&prop, c->device) == hipSuccess &&
+                        prop.multiProcessorCount > 0;
+    std::vector<uint32_t> mask(masked ? (prop.multiProcessorCount + 31) / 32 : 0, 0u);
+    for (int cu = 0; masked && cu < prop.multiProcessorCount; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+    for (int k = 0; k < 3 && e == hipSuccess; ++k) {
+      e = masked ? hipExtStreamCreateWithCUMask(&c->fork.side[k], (uint32_t)mask.size(), mask.data())
+                 : hipStreamCreateWithFlags(&c->fork.side[k], hipStreamNonBlocking);
+    }
+  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.start, hipEventDisableTiming);
   for (int k = 0; k < 2 && e == hipSuccess; ++k)
     e = hipEventCreateWithFlags(&c->fork.ec_decoded[k], hipEventDisableTiming);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.ready[k], hipEventDisableTiming);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.row0[k], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.front, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.planned, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.ed_tabs, hipEventDisableTiming);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
   for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&c->tev[k]);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
@@ -399,6 +431,8 @@ void cg_close(cg_ctx* c) {
   }
   if (c->fork.start) hipEventDestroy(c->fork.start);
   if (c->fork.front) hipEventDestroy(c->fork.front);
+  if (c->fork.planned) hipEventDestroy(c->fork.planned);
+  if (c->fork.ed_tabs) hipEventDestroy(c->fork.ed_tabs);
   if (c->copy) {
     hipStreamSynchronize(c->copy);
     hipStreamDestroy(c->copy);

@@ -524,22 +524,27 @@ CG_HD void ec_recode_wide(uint32_t* packed, const u256w& a) {
   }
 }
 
-// The affine multiples 1..cnt of `step` starting at `first` (= first + k step), one field
-// inversion for the whole run; X, Y wait in out[k] until the backward pass.
+// The affine multiples first + k step, k = 0..cnt-1, one field inversion for the whole run. The
+// forward pass leaves X, Y in out[k], Z in z[k] and the running Z products in pre[k]; the backward
+// pass starts from inv = 1 / pre[cnt-1]. `step` is affine (x, y), so each step is a mixed addition.
+// The wide-table build runs the passes as separate kernels with one inversion per row between.
 template <int C>
-CG_HD void ec_multiples_wide(EcAff* out, const Jac& first, const Jac& step, int cnt, f29* z, f29* pre,
-                             const EcConsts& K) {
+CG_HD void ec_multiples_fwd(EcAff* out, const Jac& first, const f29& sx, const f29& sy, int cnt, f29* z, f29* pre,
+                            const EcConsts& K) {
   Jac acc = first;
   for (int k = 0; k < cnt; ++k) {
-    if (k > 0) jac_add<C>(acc, acc, step, K);  // acc == step goes through the doubling branch
+    if (k > 0) jac_madd<C>(acc, acc, sx, sy, K);  // acc == step goes through the doubling branch
     out[k].x = acc.X;
     out[k].y = acc.Y;
     z[k] = acc.Z;
     if (k == 0) pre[0] = acc.Z;
     else m29_mul<C, 0>(pre[k], pre[k - 1], acc.Z);
   }
-  f29 inv;
-  m29_inv<C, 0>(inv, pre[cnt - 1], K.one_p);
+}
+
+template <int C>
+CG_HD void ec_multiples_bwd(EcAff* out, const f29& inv_all, int cnt, const f29* z, const f29* pre) {
+  f29 inv = inv_all;
   for (int k = cnt - 1; k >= 0; --k) {
     f29 zi, zi2, zi3;
     if (k > 0) {
@@ -555,17 +560,63 @@ CG_HD void ec_multiples_wide(EcAff* out, const Jac& first, const Jac& step, int 
   }
 }
 
-// Row j of a wide table (j = 32: the multiples 129..256 of base = 2^{248} Q).
+// m * (x, y) for a small m >= 1 and an affine (x, y) (double-and-add, MSB first)
 template <int C>
-CG_HD void ec_wide_row(EcAff* out, const Jac& base, int j, f29* z, f29* pre, const EcConsts& K) {
-  if (j < EC_WIDE_DIGITS) {
-    ec_multiples_wide<C>(out, base, base, EC_WIDE_MULT, z, pre, K);
-  } else {
-    Jac F;
-    jac_dbl_n<C>(F, base, 7);  // 128 base
-    jac_add<C>(F, F, base, K);
-    ec_multiples_wide<C>(out, F, base, EC_WIDE_MULT, z, pre, K);
+CG_HD void jac_small_mul_aff(Jac& r, const f29& x, const f29& y, uint32_t m, const EcConsts& K) {
+  Jac F = {x, y, K.one_p};
+  for (int b = 30 - __builtin_clz(m); b >= 0; --b) {
+    jac_dbl<C>(F, F);
+    if ((m >> b) & 1u) jac_madd<C>(F, F, x, y, K);
   }
+  r = F;
+}
+
+// Forward pass of multiples g * cnt + 1 .. (g + 1) * cnt of wide row j (row 32: 129..256 times the
+// top row's base 2^{248} Q); `base` is affine (k_ec_wide_chain normalises the row bases).
+template <int C>
+CG_HD void ec_wide_group_fwd(EcAff* out, const EcAff& base, int j, int g, int cnt, f29* z, f29* pre,
+                             const EcConsts& K) {
+  const uint32_t m = (j < EC_WIDE_DIGITS ? 0u : (uint32_t)EC_WIDE_MULT) + (uint32_t)(g * cnt) + 1u;
+  Jac F;
+  jac_small_mul_aff<C>(F, base.x, base.y, m, K);
+  ec_multiples_fwd<C>(out, F, base.x, base.y, cnt, z, pre, K);
+}
+
+// Affine x, y of n finite Jacobian points in place (one inversion; `pre` holds n products).
+template <int C>
+CG_HD void jac_batch_to_affine(EcAff* out, const Jac* P, int n, f29* pre, const EcConsts& K) {
+  pre[0] = P[0].Z;
+  for (int k = 1; k < n; ++k) m29_mul<C, 0>(pre[k], pre[k - 1], P[k].Z);
+  f29 inv;
+  m29_inv<C, 0>(inv, pre[n - 1], K.one_p);
+  for (int k = n - 1; k >= 0; --k) {
+    f29 zi, zi2, zi3;
+    if (k > 0) {
+      m29_mul<C, 0>(zi, inv, pre[k - 1]);
+      m29_mul<C, 0>(inv, inv, P[k].Z);
+    } else {
+      zi = inv;
+    }
+    m29_sq<C, 0>(zi2, zi);
+    m29_mul<C, 0>(zi3, zi2, zi);
+    m29_mul<C, 0>(out[k].x, P[k].X, zi2);
+    m29_mul<C, 0>(out[k].y, P[k].Y, zi3);
+  }
+}
+
+// Inverses of G group products (one inversion): out[g] = 1 / t_g.
+template <int C, int G>
+CG_HD void m29_batch_invert_small(f29* out, const f29* t, const EcConsts& K) {
+  f29 pre[G];
+  pre[0] = t[0];
+  for (int g = 1; g < G; ++g) m29_mul<C, 0>(pre[g], pre[g - 1], t[g]);
+  f29 inv;
+  m29_inv<C, 0>(inv, pre[G - 1], K.one_p);
+  for (int g = G - 1; g > 0; --g) {
+    m29_mul<C, 0>(out[g], inv, pre[g - 1]);
+    m29_mul<C, 0>(inv, inv, t[g]);
+  }
+  out[0] = inv;
 }
 
 // R = u1 G + u2 Q over the wide tables, then BC's x-check. Returns 0 VALID / 1 INVALID.

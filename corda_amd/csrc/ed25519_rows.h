@@ -103,10 +103,22 @@ CG_HD void ed_row_multiples(ge_niels* row, const ge_p3& P, const fe& d2) {
 // backward pass turns 1 / (Z_0 ... Z_{M-1}) into every 1/Z_k. ~23 field ops per entry
 // instead of ~52 for batches of 8.
 template <int M>
+CG_HD void ed_multiples_from(ge_niels* row, const ge_p3& first, const ge_p3& P, const fe& d2, fe* zpre);
+template <int M>
 CG_HD void ed_row_build(ge_niels* row, const ge_p3& P, const fe& d2, fe* zpre) {
+  ed_multiples_from<M>(row, P, P, d2, zpre);
+}
+
+// The affine niels points first + k P, k = 0..M-1, one inversion (ed_row_build's passes).
+// Forward pass: projective X, Y, Z of each point wait in its niels slot, the running Z products in
+// zpre[0..M-1] (zpre[M-1] = the product of all M). Backward pass: from inv = 1 / zpre[M-1], every
+// 1 / Z_k, then the niels form. The wide-table build runs the passes as separate kernels with
+// one shared inversion per row between them (verify_ed.hip).
+template <int M>
+CG_HD void ed_multiples_fwd(ge_niels* row, const ge_p3& first, const ge_p3& P, const fe& d2, fe* zpre) {
   ge_cached c;
   ge_p3_to_cached(c, P, d2);
-  ge_p3 cur = P;
+  ge_p3 cur = first;
   ge_p1p1 t;
   fe run;
   for (int k = 0; k < M; ++k) {
@@ -125,8 +137,12 @@ CG_HD void ed_row_build(ge_niels* row, const ge_p3& P, const fe& d2, fe* zpre) {
     }
     fe_copy(zpre[k], run);
   }
+}
+
+template <int M>
+CG_HD void ed_multiples_bwd(ge_niels* row, const fe& inv_all, const fe* zpre, const fe& d2) {
   fe inv;
-  fe_invert(inv, run);
+  fe_copy(inv, inv_all);
   for (int k = M - 1; k >= 0; --k) {
     ge_niels& s = row[k];
     fe zi;
@@ -146,6 +162,29 @@ CG_HD void ed_row_build(ge_niels* row, const ge_p3& P, const fe& d2, fe* zpre) {
     fe_mul(xy, x, y);
     fe_mul(s.xy2d, xy, d2);
   }
+}
+
+template <int M>
+CG_HD void ed_multiples_from(ge_niels* row, const ge_p3& first, const ge_p3& P, const fe& d2, fe* zpre) {
+  ed_multiples_fwd<M>(row, first, P, d2, zpre);
+  fe inv;
+  fe_invert(inv, zpre[M - 1]);
+  ed_multiples_bwd<M>(row, inv, zpre, d2);
+}
+
+// Inverses of G group products t_g (one inversion, Montgomery's trick): out[g] = 1 / t_g.
+template <int G>
+CG_HD void fe_batch_invert_small(fe* out, const fe* t) {
+  fe pre[G];
+  fe_copy(pre[0], t[0]);
+  for (int g = 1; g < G; ++g) fe_mul(pre[g], pre[g - 1], t[g]);
+  fe inv;
+  fe_invert(inv, pre[G - 1]);
+  for (int g = G - 1; g > 0; --g) {
+    fe_mul(out[g], inv, pre[g - 1]);
+    fe_mul(inv, inv, t[g]);
+  }
+  fe_copy(out[0], inv);
 }
 
 template <int W, int K>

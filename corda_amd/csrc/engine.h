@@ -16,6 +16,7 @@ struct WidePool {
   void* ed = nullptr;
   void* ec = nullptr;
   uint32_t cap_ed = 0, cap_ec = 0;
+  uint32_t min_ed = 0, min_ec = 0;  // items per key from which a key gets wide tables, per family
 };
 
 // Side streams + events owned by a context. Key preparation forks off the caller's stream:
@@ -58,10 +59,22 @@ struct StageTimer {
     if (_t >= 0) (fork)->timer->done(_t, (stream));                            \
   } while (0)
 
+// Key-table builds deferred by launch_keyprep until the first chunk's plan is sorted (the sort's
+// decoupled look-back stalls when the table builds hold the SIMDs), then enqueued by launch_items.
+struct PendingTabs {
+  bool on = false;
+  const cg_key* keys = nullptr;
+  uint32_t n_keys = 0;
+  void* keyprep = nullptr;
+  WidePool wide;
+};
+
 struct Fork {
   hipStream_t side[3];
   hipEvent_t start, ec_decoded[2], ready[3], front, row0[3];
   StageTimer* timer;  // null unless the ctx was opened with CG_FLAG_STAGE_TIMING
+  hipEvent_t planned = nullptr, ed_tabs = nullptr;  // plan sorted (main); Ed25519 tables built (side[2])
+  mutable PendingTabs pending;
 };
 
 // Upload the constant tables (curve constants, base-point tables) for the current device.

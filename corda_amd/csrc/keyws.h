@@ -141,6 +141,7 @@ struct KeyWs {
   struct EdWideSlot* wed;  // wide pools (WidePool; empty: no key gets wide tables)
   struct EcWideSlot* wec;
   uint32_t cap_ed, cap_ec;
+  uint32_t min_ed, min_ec;
 };
 
 // How much table a key gets, from the number of items that use it in the batch (one-shot entry
@@ -154,13 +155,19 @@ struct KeyWs {
 //   more                          all 22 rows: 6 doublings per item (ed_double_scalar_wb)
 // Break-even (measured on MI355X, 2^20 Ed25519 items): a key's full tables cost ~230 ns of
 // GPU time, the row-0 ladder ~7 ns more per item than the full-table one -> ~32 items.
-// A fourth mode, for keys with >= KEY_WIDE_MIN_USES items (and a free slot in the scheme's wide
-// pool, sized by the host from the call's item count): one table row per signed radix-2^8 digit
-// (ed25519_rows.h / ecdsa_rows.h "wide tables"), 54 additions and no doublings per item. Its build
-// (4096 entries per key) pays for itself after a few hundred items.
-#ifndef KEY_WIDE_MIN_USES
-#define KEY_WIDE_MIN_USES 384u
+// A fourth mode, for keys with >= KEY_WIDE_MIN_USES_{ED,EC} items (and a free slot in the family's
+// wide pool, sized by the host from the call's item count): one table row per signed radix-2^8
+// digit (ed25519_rows.h / ecdsa_rows.h "wide tables"), 54 additions and no doublings per item.
+// Break-even, measured on MI355X: a wide table costs ~1.2 us (Ed25519) / ~1 us
+// (ECDSA) of chip time to build and saves ~0.64 ns (Ed25519) / ~2 ns (ECDSA) per item against the
+// full tables, so ~1900 / ~500 items. (Environment CG_WIDE_MIN_USES_ED / _EC override, for A/B.)
+#ifndef KEY_WIDE_MIN_USES_ED
+#define KEY_WIDE_MIN_USES_ED 4096u
 #endif
+#ifndef KEY_WIDE_MIN_USES_EC
+#define KEY_WIDE_MIN_USES_EC 512u
+#endif
+#define KEY_WIDE_MIN_USES (KEY_WIDE_MIN_USES_EC < KEY_WIDE_MIN_USES_ED ? KEY_WIDE_MIN_USES_EC : KEY_WIDE_MIN_USES_ED)
 #define KEY_NOT_WIDE 0xffffffffu
 #define KEY_WIDE_MAX 8192u  // wide slots per pool at most (Ed25519 4.9 GB / ECDSA 5.0 GB)
 #define KEY_USES_ALL 0xffffffffu
@@ -176,12 +183,13 @@ struct EdWideSlot {
 };
 struct EcWideSlot {
   EcWideTab tab;
-  Jac bases[EC_WIDE_DIGITS];
+  EcAff bases[EC_WIDE_DIGITS];  // 2^{8j} Q, affine (the row builds step by mixed additions)
+  Jac jbases[EC_WIDE_DIGITS];   // the chain's Jacobian points
   EcWideScratch s[EC_WIDE_ROWS];
 };
 // Slots for a call of n_items over n_keys: no more keys can reach KEY_WIDE_MIN_USES.
-static inline uint32_t wide_cap(uint32_t n_keys, uint64_t n_items) {
-  uint64_t c = n_items / KEY_WIDE_MIN_USES;
+static inline uint32_t wide_cap(uint32_t n_keys, uint64_t n_items, uint32_t min_uses = KEY_WIDE_MIN_USES) {
+  uint64_t c = n_items / min_uses;
   if (c > n_keys) c = n_keys;
   if (c > KEY_WIDE_MAX) c = KEY_WIDE_MAX;
   return (uint32_t)c;
@@ -191,6 +199,8 @@ static inline size_t wide_pool_bytes(uint32_t cap) {
 }
 static inline WidePool wide_pool(void* base, uint32_t cap) {
   WidePool p;
+  p.min_ed = KEY_WIDE_MIN_USES_ED;
+  p.min_ec = KEY_WIDE_MIN_USES_EC;
   if (!base || !cap) return p;
   p.ed = base;
   p.ec = (uint8_t*)base + al256((size_t)cap * sizeof(EdWideSlot));
@@ -227,6 +237,8 @@ static inline KeyWs key_ws(void* base, uint32_t n_keys, const WidePool* wp = nul
   w.wec = wp ? (EcWideSlot*)wp->ec : nullptr;
   w.cap_ed = wp ? wp->cap_ed : 0;
   w.cap_ec = wp ? wp->cap_ec : 0;
+  w.min_ed = wp && wp->min_ed ? wp->min_ed : KEY_WIDE_MIN_USES_ED;
+  w.min_ec = wp && wp->min_ec ? wp->min_ec : KEY_WIDE_MIN_USES_EC;
   return w;
 }
 static inline size_t key_ws_bytes(uint32_t n_keys) {
@@ -309,9 +321,10 @@ hipError_t ed_upload_constants();
 hipError_t ed_init_const(void* d_btab, hipStream_t stream);
 void ed_launch_key_abyte(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                          const KeyWs& w, hipStream_t stream);
-// decode -> chain -> tab
-void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+// decode -> chains (light), then the row tables (heavy)
+void ed_launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                               const KeyWs& w, hipStream_t stream);
+void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream);
 // item stages (verify.hip launch_items orders them across the main and side streams)
 void ed_launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
                      uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len,
@@ -324,10 +337,10 @@ void ed_launch_finish(const cg_item* d_items, uint64_t n_items, const uint8_t* d
                       uint8_t* d_status, const ItemWs& iw, hipStream_t stream);
 hipError_t ec_upload_constants();
 hipError_t ec_init_const(void* d_btab, hipStream_t stream);
-// decode (records `decoded`: k_ec_prep needs the key status) -> chain -> tab, per curve
-void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                       const KeyWs& w, hipStream_t stream_r1, hipStream_t stream_k1, hipEvent_t decoded_r1,
-                       hipEvent_t decoded_k1);
+// per curve: decode (records `decoded`: k_ec_prep needs the key status) -> chains; then the tables
+void ec_launch_keyprep_chains(int curve, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena,
+                              uint64_t arena_len, const KeyWs& w, hipStream_t stream, hipEvent_t decoded);
+void ec_launch_keyprep_tabs(int curve, const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream);
 void ec_launch_front(int curve, const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena,
                      uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs,
                      uint64_t msgs_len, const ItemWs& iw, hipStream_t stream);

@@ -71,7 +71,7 @@ __device__ __forceinline__ void list_append(int c, uint32_t i, uint32_t n_keys, 
   }
 }
 
-// Table mode per key: wide tables for keys with >= KEY_WIDE_MIN_USES items while the scheme's
+// Table mode per key: wide tables for keys with >= min_ed / min_ec items while the family's
 // wide pool has slots (one atomic per wide key: they are few), else full tables from
 // ED_DIRECT_MAX_USES items; the wide and full keys compacted per scheme class. One wave per block.
 __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ keys, uint32_t n_keys,
@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ 
                                                      uint32_t* __restrict__ full, uint32_t* __restrict__ full_count,
                                                      uint32_t* __restrict__ wide_idx, uint32_t* __restrict__ wide,
                                                      uint32_t* __restrict__ wide_count, uint32_t cap_ed,
-                                                     uint32_t cap_ec) {
+                                                     uint32_t cap_ec, uint32_t min_ed, uint32_t min_ec) {
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
   int c = -1, cw = -1;
   uint32_t u = 0;
@@ -96,8 +96,8 @@ __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ 
       : s == CG_ECDSA_SECP256K1_SHA256 ? PLAN_K1
                                        : -1;
     // KEY_USES_ALL (cg_prepare_keys_device: uses unknown) never gets wide tables
-    if (c >= 0 && u >= KEY_WIDE_MIN_USES && u != KEY_USES_ALL) {
-      const int pool = c == PLAN_ED ? 0 : 1;
+    const int pool = c == PLAN_ED ? 0 : 1;
+    if (c >= 0 && u >= (pool == 0 ? min_ed : min_ec) && u != KEY_USES_ALL) {
       const uint32_t cap = pool == 0 ? cap_ed : cap_ec;
       if (cap) {
         const uint32_t slot = atomicAdd(&wide_count[PLAN_CLASSES + pool], 1u);
@@ -133,6 +133,29 @@ hipError_t init_btab(void* d_btab, hipStream_t stream) {
   return ec_init_const(d_btab, stream);
 }
 
+// The deferred table builds, forked from `stream` at this point: Ed25519 first (its ladder runs
+// first), the two curves after it (their ladders run after the Ed25519 ladder and finish).
+static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
+  PendingTabs& p = fork->pending;
+  if (!p.on) return hipSuccess;
+  p.on = false;
+  const KeyWs w = key_ws(p.keyprep, p.n_keys, &p.wide);
+  hipError_t e = hipEventRecord(fork->planned, stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(fork->side[2], fork->planned, 0);
+  if (e != hipSuccess) return e;
+  ed_launch_keyprep_tabs(p.keys, p.n_keys, w, fork->side[2]);
+  e = hipEventRecord(fork->ed_tabs, fork->side[2]);
+  if (e == hipSuccess) e = hipEventRecord(fork->ready[2], fork->side[2]);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+    e = hipStreamWaitEvent(fork->side[k], fork->planned, 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(fork->side[k], fork->ed_tabs, 0);
+    if (e != hipSuccess) break;
+    ec_launch_keyprep_tabs(k == 0 ? CG_CURVE_R1 : CG_CURVE_K1, p.keys, p.n_keys, w, fork->side[k]);
+    e = hipEventRecord(fork->ready[k], fork->side[k]);
+  }
+  return e;
+}
+
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream, const Fork* fork, const cg_item* d_items,
                           uint64_t n_items, const WidePool* wide) {
@@ -147,20 +170,31 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
                        n_keys, w.uses, w.seen);
   hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys, w.uses,
                      (const uint8_t*)w.seen, w.full, w.full_count, w.wide_idx, w.wide, w.wide_count, w.cap_ed,
-                     w.cap_ec);
+                     w.cap_ec, w.min_ed, w.min_ec);
   if (!fork) {
     ed_launch_key_abyte(d_keys, n_keys, d_arena, arena_len, w, stream);
-    ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, stream, stream, nullptr, nullptr);
-    ed_launch_keyprep_tables(d_keys, n_keys, d_arena, arena_len, w, stream);
+    for (int curve : {CG_CURVE_R1, CG_CURVE_K1}) {
+      ec_launch_keyprep_chains(curve, d_keys, n_keys, d_arena, arena_len, w, stream, nullptr);
+      ec_launch_keyprep_tabs(curve, d_keys, n_keys, w, stream);
+    }
+    ed_launch_keyprep_chains(d_keys, n_keys, d_arena, arena_len, w, stream);
+    ed_launch_keyprep_tabs(d_keys, n_keys, w, stream);
     return hipGetLastError();
   }
   hipError_t e = hipEventRecord(fork->start, stream);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->start, 0);
   if (e != hipSuccess) return e;
-  ec_launch_keyprep(d_keys, n_keys, d_arena, arena_len, w, fork->side[0], fork->side[1], fork->ec_decoded[0],
-                    fork->ec_decoded[1]);
-  ed_launch_keyprep_tables(d_keys, n_keys, d_arena, arena_len, w, fork->side[2]);
-  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventRecord(fork->ready[k], fork->side[k]);
+  // light phase now: decodes and row-base chains (few waves, latency-bound)
+  ec_launch_keyprep_chains(CG_CURVE_R1, d_keys, n_keys, d_arena, arena_len, w, fork->side[0], fork->ec_decoded[0]);
+  ec_launch_keyprep_chains(CG_CURVE_K1, d_keys, n_keys, d_arena, arena_len, w, fork->side[1], fork->ec_decoded[1]);
+  ed_launch_keyprep_chains(d_keys, n_keys, d_arena, arena_len, w, fork->side[2]);
+  // heavy phase (the row tables): after the first chunk's plan when items follow, else now
+  fork->pending.on = true;
+  fork->pending.keys = d_keys;
+  fork->pending.n_keys = n_keys;
+  fork->pending.keyprep = d_keyprep;
+  fork->pending.wide = d_items && wide ? *wide : WidePool{};
+  if (!d_items) e = launch_pending_tabs(fork, stream);
   if (e != hipSuccess) return e;
   // the only key work on the main stream: Abyte for k_ed_hash (no decode)
   ed_launch_key_abyte(d_keys, n_keys, d_arena, arena_len, w, stream);
@@ -183,6 +217,7 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
   CG_TIME(fork, CG_STAGE_PLAN, stream,
           e = launch_plan(d_items, n_items, d_keys, n_keys, (const uint32_t*)w.uses, (const uint32_t*)w.wide_idx, iw,
                           stream));
+  if (e == hipSuccess && fork) e = launch_pending_tabs(fork, stream);  // the first chunk starts the table builds
   if (e != hipSuccess) return e;
   // fronts: Ed25519 challenges (need only Abyte), ECDSA prep + s^-1 per curve (need the decoded key)
   CG_TIME(fork, CG_STAGE_ED_HASH, stream,

@@ -109,27 +109,68 @@ __global__ void __launch_bounds__(64) k_ec_wide_chain(uint32_t n_keys, const EdK
   if (hdr[i].status != 0) return;
   EcWideSlot& ws = wec[wide_idx[i]];
   Jac P = bases[(size_t)i * KEY_BASES].ec;
-  ws.bases[0] = P;
+  ws.jbases[0] = P;
   for (int j = 1; j < EC_WIDE_DIGITS; ++j) {
     jac_dbl_n<C>(P, P, EC_WIDE_W);
-    ws.bases[j] = P;
+    ws.jbases[j] = P;
   }
+  jac_batch_to_affine<C>(ws.bases, ws.jbases, EC_WIDE_DIGITS, ws.s[0].pre, c_ec[C]);
 }
 
+// The row tables in three passes over (wide key, row, group) lanes, as the Ed25519 build
+// (verify_ed.hip k_ed_wide_fwd / _inv / _bwd); the steps are mixed additions of the affine base.
+#define EC_WIDE_GROUP 32
+#define EC_WIDE_GROUPS (EC_WIDE_MULT / EC_WIDE_GROUP)
+struct EcWideLane {
+  uint32_t l, j, g;
+};
+__device__ __forceinline__ EcWideLane ec_wide_lane(uint32_t rows, uint32_t groups) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  return EcWideLane{(uint32_t)(t / (rows * groups)), (uint32_t)(t / groups % rows), (uint32_t)(t % groups)};
+}
+#define EC_WIDE_KEY(C, L)                                  \
+  const int c = plan_class_of_curve(C);                    \
+  if ((L).l >= wide_count[c]) return;                      \
+  const uint32_t i = wide[(size_t)c * n_keys + (L).l];     \
+  if (hdr[i].status != 0) return;                          \
+  EcWideSlot& ws = wec[wide_idx[i]]
+
 template <int C>
-__global__ void __launch_bounds__(64) k_ec_wide_tab(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+__global__ void __launch_bounds__(64) k_ec_wide_fwd(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                     const uint32_t* __restrict__ wide,
                                                     const uint32_t* __restrict__ wide_count,
                                                     const uint32_t* __restrict__ wide_idx, EcWideSlot* __restrict__ wec) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int c = plan_class_of_curve(C);
-  const uint32_t l = (uint32_t)(g / EC_WIDE_ROWS), j = (uint32_t)(g % EC_WIDE_ROWS);
-  if (l >= wide_count[c]) return;
-  const uint32_t i = wide[(size_t)c * n_keys + l];
-  if (hdr[i].status != 0) return;
-  EcWideSlot& ws = wec[wide_idx[i]];
-  ec_wide_row<C>(ws.tab.t[j], ws.bases[j < EC_WIDE_DIGITS ? j : EC_WIDE_DIGITS - 1], (int)j, ws.s[j].z, ws.s[j].pre,
-                 c_ec[C]);
+  const EcWideLane L = ec_wide_lane(EC_WIDE_ROWS, EC_WIDE_GROUPS);
+  EC_WIDE_KEY(C, L);
+  const uint32_t o = EC_WIDE_GROUP * L.g;
+  ec_wide_group_fwd<C>(&ws.tab.t[L.j][o], ws.bases[L.j < EC_WIDE_DIGITS ? L.j : EC_WIDE_DIGITS - 1], (int)L.j,
+                       (int)L.g, EC_WIDE_GROUP, &ws.s[L.j].z[o], &ws.s[L.j].pre[o], c_ec[C]);
+}
+
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_wide_inv(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                    const uint32_t* __restrict__ wide,
+                                                    const uint32_t* __restrict__ wide_count,
+                                                    const uint32_t* __restrict__ wide_idx, EcWideSlot* __restrict__ wec) {
+  const EcWideLane L = ec_wide_lane(EC_WIDE_ROWS, 1);
+  EC_WIDE_KEY(C, L);
+  f29* pre = ws.s[L.j].pre;
+  f29 t[EC_WIDE_GROUPS], inv[EC_WIDE_GROUPS];
+  for (int g = 0; g < EC_WIDE_GROUPS; ++g) t[g] = pre[EC_WIDE_GROUP * g + EC_WIDE_GROUP - 1];
+  m29_batch_invert_small<C, EC_WIDE_GROUPS>(inv, t, c_ec[C]);
+  for (int g = 0; g < EC_WIDE_GROUPS; ++g) pre[EC_WIDE_GROUP * g + EC_WIDE_GROUP - 1] = inv[g];
+}
+
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_wide_bwd(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                    const uint32_t* __restrict__ wide,
+                                                    const uint32_t* __restrict__ wide_count,
+                                                    const uint32_t* __restrict__ wide_idx, EcWideSlot* __restrict__ wec) {
+  const EcWideLane L = ec_wide_lane(EC_WIDE_ROWS, EC_WIDE_GROUPS);
+  EC_WIDE_KEY(C, L);
+  const uint32_t o = EC_WIDE_GROUP * L.g;
+  const f29* pre = &ws.s[L.j].pre[o];
+  ec_multiples_bwd<C>(&ws.tab.t[L.j][o], pre[EC_WIDE_GROUP - 1], EC_WIDE_GROUP, &ws.s[L.j].z[o], pre);
 }
 
 // one lane per (G wide row u, group g of 32 multiples)
@@ -274,34 +315,51 @@ hipError_t ec_init_const(void* d_btab, hipStream_t stream) {
 }
 
 template <int C>
-static void launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                           const KeyWs& w, hipStream_t stream, hipEvent_t decoded) {
+static void launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                                  const KeyWs& w, hipStream_t stream, hipEvent_t decoded) {
   const uint32_t B = 64;
-  const uint64_t elanes = (uint64_t)n_keys * EC_ROWS;
   const dim3 g((n_keys + B - 1) / B);
   hipLaunchKernelGGL(k_ec_keyprep_decode<C>, g, dim3(B), 0, stream, d_keys, n_keys, d_arena, arena_len, w.hdr,
                      w.bases);
   if (decoded) hipEventRecord(decoded, stream);
   hipLaunchKernelGGL(k_ec_keyprep_chain<C>, g, dim3(B), 0, stream, n_keys, w.hdr, (const uint32_t*)w.full,
                      (const uint32_t*)w.full_count, w.bases);
+  if (w.cap_ec)
+    hipLaunchKernelGGL(k_ec_wide_chain<C>, dim3((w.cap_ec + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
+                       (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx,
+                       (const BaseSlot*)w.bases, w.wec);
+}
+
+template <int C>
+static void launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream) {
+  const uint32_t B = 64;
+  const uint64_t elanes = (uint64_t)n_keys * EC_ROWS;
   hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3((unsigned)((elanes + B - 1) / B)), dim3(B), 0, stream, d_keys, n_keys,
                      w.hdr, w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count,
                      (const uint32_t*)w.wide_idx, w.tab, w.ecs);
   if (w.cap_ec) {
-    hipLaunchKernelGGL(k_ec_wide_chain<C>, dim3((w.cap_ec + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
-                       (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx,
-                       (const BaseSlot*)w.bases, w.wec);
-    const uint64_t wl = (uint64_t)w.cap_ec * EC_WIDE_ROWS;
-    hipLaunchKernelGGL(k_ec_wide_tab<C>, dim3((unsigned)((wl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr,
-                       (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx, w.wec);
+    const uint64_t gl = (uint64_t)w.cap_ec * EC_WIDE_ROWS * EC_WIDE_GROUPS, rl = (uint64_t)w.cap_ec * EC_WIDE_ROWS;
+    const uint32_t* wl = (const uint32_t*)w.wide;
+    const uint32_t* wc = (const uint32_t*)w.wide_count;
+    const uint32_t* wi = (const uint32_t*)w.wide_idx;
+    hipLaunchKernelGGL(k_ec_wide_fwd<C>, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
+                       wc, wi, w.wec);
+    hipLaunchKernelGGL(k_ec_wide_inv<C>, dim3((unsigned)((rl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
+                       wc, wi, w.wec);
+    hipLaunchKernelGGL(k_ec_wide_bwd<C>, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
+                       wc, wi, w.wec);
   }
 }
 
-void ec_launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
-                       const KeyWs& w, hipStream_t stream_r1, hipStream_t stream_k1, hipEvent_t decoded_r1,
-                       hipEvent_t decoded_k1) {
-  launch_keyprep<CG_CURVE_R1>(d_keys, n_keys, d_arena, arena_len, w, stream_r1, decoded_r1);
-  launch_keyprep<CG_CURVE_K1>(d_keys, n_keys, d_arena, arena_len, w, stream_k1, decoded_k1);
+void ec_launch_keyprep_chains(int curve, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena,
+                              uint64_t arena_len, const KeyWs& w, hipStream_t stream, hipEvent_t decoded) {
+  if (curve == CG_CURVE_R1) launch_keyprep_chains<CG_CURVE_R1>(d_keys, n_keys, d_arena, arena_len, w, stream, decoded);
+  else launch_keyprep_chains<CG_CURVE_K1>(d_keys, n_keys, d_arena, arena_len, w, stream, decoded);
+}
+
+void ec_launch_keyprep_tabs(int curve, const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream) {
+  if (curve == CG_CURVE_R1) launch_keyprep_tabs<CG_CURVE_R1>(d_keys, n_keys, w, stream);
+  else launch_keyprep_tabs<CG_CURVE_K1>(d_keys, n_keys, w, stream);
 }
 
 template <int C>

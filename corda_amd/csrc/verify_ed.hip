@@ -183,17 +183,61 @@ __global__ void __launch_bounds__(64) k_ed_wide_chain(uint32_t n_keys, const EdK
   }
 }
 
-__global__ void __launch_bounds__(64) k_ed_wide_tab(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+// The row tables in three passes over (wide key, row, group of ED_WIDE_GROUP multiples) lanes:
+// forward (first multiple by double-and-add, 31 additions, running Z products), one inversion per
+// row over its groups' products (a quarter of the lanes), backward (every 1/Z, niels form). A lane's
+// serial chain is a quarter of a whole row's, and the inversions cost a quarter of one per group.
+#define ED_WIDE_GROUP 32
+#define ED_WIDE_GROUPS (EdWideCfg::kMult / ED_WIDE_GROUP)
+struct WideLane {
+  uint32_t l, j, g;
+};
+__device__ __forceinline__ WideLane wide_lane(uint32_t rows, uint32_t groups) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  return WideLane{(uint32_t)(t / (rows * groups)), (uint32_t)(t / groups % rows), (uint32_t)(t % groups)};
+}
+
+__global__ void __launch_bounds__(64) k_ed_wide_fwd(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                     const uint32_t* __restrict__ wide,
                                                     const uint32_t* __restrict__ wide_count,
                                                     const uint32_t* __restrict__ wide_idx, EdWideSlot* __restrict__ wed) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t l = (uint32_t)(g / EdWideCfg::kRows), j = (uint32_t)(g % EdWideCfg::kRows);
-  if (l >= wide_count[PLAN_ED]) return;
-  const uint32_t i = wide[(size_t)PLAN_ED * n_keys + l];
+  const WideLane L = wide_lane(EdWideCfg::kRows, ED_WIDE_GROUPS);
+  if (L.l >= wide_count[PLAN_ED]) return;
+  const uint32_t i = wide[(size_t)PLAN_ED * n_keys + L.l];
   if (hdr[i].status != 0) return;
   EdWideSlot& ws = wed[wide_idx[i]];
-  ed_row_build<EdWideCfg::kMult>(ws.tab.t[j], ws.bases[j], c_ed.d2, ws.zpre[j]);
+  ge_p3 first;
+  ed_small_mul(first, ws.bases[L.j], ED_WIDE_GROUP * L.g + 1);
+  ed_multiples_fwd<ED_WIDE_GROUP>(&ws.tab.t[L.j][ED_WIDE_GROUP * L.g], first, ws.bases[L.j], c_ed.d2,
+                                  &ws.zpre[L.j][ED_WIDE_GROUP * L.g]);
+}
+
+__global__ void __launch_bounds__(64) k_ed_wide_inv(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                    const uint32_t* __restrict__ wide,
+                                                    const uint32_t* __restrict__ wide_count,
+                                                    const uint32_t* __restrict__ wide_idx, EdWideSlot* __restrict__ wed) {
+  const WideLane L = wide_lane(EdWideCfg::kRows, 1);
+  if (L.l >= wide_count[PLAN_ED]) return;
+  const uint32_t i = wide[(size_t)PLAN_ED * n_keys + L.l];
+  if (hdr[i].status != 0) return;
+  fe(&z)[EdWideCfg::kMult] = wed[wide_idx[i]].zpre[L.j];
+  fe t[ED_WIDE_GROUPS], inv[ED_WIDE_GROUPS];
+  for (int g = 0; g < ED_WIDE_GROUPS; ++g) t[g] = z[ED_WIDE_GROUP * g + ED_WIDE_GROUP - 1];
+  fe_batch_invert_small<ED_WIDE_GROUPS>(inv, t);
+  for (int g = 0; g < ED_WIDE_GROUPS; ++g) z[ED_WIDE_GROUP * g + ED_WIDE_GROUP - 1] = inv[g];
+}
+
+__global__ void __launch_bounds__(64) k_ed_wide_bwd(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                    const uint32_t* __restrict__ wide,
+                                                    const uint32_t* __restrict__ wide_count,
+                                                    const uint32_t* __restrict__ wide_idx, EdWideSlot* __restrict__ wed) {
+  const WideLane L = wide_lane(EdWideCfg::kRows, ED_WIDE_GROUPS);
+  if (L.l >= wide_count[PLAN_ED]) return;
+  const uint32_t i = wide[(size_t)PLAN_ED * n_keys + L.l];
+  if (hdr[i].status != 0) return;
+  EdWideSlot& ws = wed[wide_idx[i]];
+  const fe* z = &ws.zpre[L.j][ED_WIDE_GROUP * L.g];
+  ed_multiples_bwd<ED_WIDE_GROUP>(&ws.tab.t[L.j][ED_WIDE_GROUP * L.g], z[ED_WIDE_GROUP - 1], z, c_ed.d2);
 }
 
 // The base point B as an extended point (from the constant niels table entry 1*B)
@@ -741,24 +785,38 @@ void ed_launch_key_abyte(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d
                      arena_len, w.hdr);
 }
 
-void ed_launch_keyprep_tables(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+// Light phase (decode, row-base chains: latency-bound, few waves) and heavy phase (the row tables:
+// throughput-bound), so the host can start the heavy phase after the plan sort (keyws.h).
+void ed_launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                               const KeyWs& w, hipStream_t stream) {
   const uint32_t B = 64;  // one wave per block: keys are few, spread them over CUs
   hipLaunchKernelGGL(k_ed_keyprep_decode, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, d_arena,
                      arena_len, w.hdr, w.bases);
   hipLaunchKernelGGL(k_ed_keyprep_chain, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
                      (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.bases);
+  if (w.cap_ed)
+    hipLaunchKernelGGL(k_ed_wide_chain, dim3((w.cap_ed + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
+                       (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx,
+                       (const BaseSlot*)w.bases, w.wed);
+}
+
+void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream) {
+  const uint32_t B = 64;
   const uint64_t lanes = (uint64_t)n_keys * EdCfg::kRows;
   hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((unsigned)((lanes + B - 1) / B)), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
                      w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count,
                      (const uint32_t*)w.wide_idx, w.tab, w.ecs);
   if (w.cap_ed) {
-    hipLaunchKernelGGL(k_ed_wide_chain, dim3((w.cap_ed + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
-                       (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx,
-                       (const BaseSlot*)w.bases, w.wed);
-    const uint64_t wl = (uint64_t)w.cap_ed * EdWideCfg::kRows;
-    hipLaunchKernelGGL(k_ed_wide_tab, dim3((unsigned)((wl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr,
-                       (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx, w.wed);
+    const uint64_t gl = (uint64_t)w.cap_ed * EdWideCfg::kRows * ED_WIDE_GROUPS, rl = (uint64_t)w.cap_ed * EdWideCfg::kRows;
+    const uint32_t* wl = (const uint32_t*)w.wide;
+    const uint32_t* wc = (const uint32_t*)w.wide_count;
+    const uint32_t* wi = (const uint32_t*)w.wide_idx;
+    hipLaunchKernelGGL(k_ed_wide_fwd, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl, wc,
+                       wi, w.wed);
+    hipLaunchKernelGGL(k_ed_wide_inv, dim3((unsigned)((rl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl, wc,
+                       wi, w.wed);
+    hipLaunchKernelGGL(k_ed_wide_bwd, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl, wc,
+                       wi, w.wed);
   }
 }
 

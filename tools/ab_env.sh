@@ -1,0 +1,21 @@
+#!/bin/bash
+# A/B of environment variants on one GPU box (same library): the headline bench without the
+# secondaries, interleaved, two rounds.  usage: bash tools/ab_env.sh out_tag "ENV=1" ["ENV2=1" ...]
+# ("-" = no extra environment)
+set -o pipefail
+TAG=$1; shift
+OUT=gpurun_out/ab_$TAG
+mkdir -p $OUT
+B="python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --host-steps 0 --configs1-items 0 --ecdsa-items 0 --pipeline-txs 0 --tear-offs 0 --configs0-txs 0"
+for round in 1 2; do
+  i=0
+  for v in "$@"; do
+    i=$((i+1))
+    if [ "$v" = "-" ]; then
+      timeout -k 10 200 $B > $OUT/v${i}_$round.log 2>&1 || exit 1
+    else
+      env $v timeout -k 10 200 $B > $OUT/v${i}_$round.log 2>&1 || exit 1
+    fi
+    echo "v$i ($v) round $round: $(grep -o '"value": [0-9.]*' $OUT/v${i}_$round.log | head -1)"
+  done
+done

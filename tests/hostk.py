@@ -18,8 +18,10 @@ def build():
             os.path.getmtime(os.path.join(HERE, "..", "corda_amd", "csrc", f))
             for f in os.listdir(os.path.join(HERE, "..", "corda_amd", "csrc")) if f.endswith(".h")) or \
             os.path.getmtime(SO) < os.path.getmtime(src):
+        tmp = f"{SO}.{os.getpid()}.tmp"  # build aside and rename: parallel test workers never load a partial .so
         subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-DFE_BOUNDS_CHECK", "-DFE_OP_COUNT", "-fPIC", "-shared",
-                               "-o", SO, src])
+                               "-o", tmp, src])
+        os.replace(tmp, SO)
     return ctypes.CDLL(SO)
 
 

@@ -109,6 +109,9 @@ union BaseSlot {
 #define PLAN_CLASSES 3
 #define PLAN_FULL 4  // ranges[PLAN_FULL + c]: first item of class c whose key has full tables
 #define PLAN_WIDE 7  // ranges[PLAN_WIDE + c]: first item of class c whose key has wide tables
+// Items whose clear data is longer than this sort after the short ones of their class and table
+// mode (plan_sort.hip), so a wave hashes either short or long messages, never both.
+#define ITEM_LONG_MIN 1024u
 struct Plan {
   const uint32_t* perm;    // plan position -> item index
   const uint32_t* ranges;  // class c occupies positions [ranges[c], ranges[c + 1])

@@ -26,13 +26,16 @@ typedef rocprim::radix_sort_config<rocprim::default_config, rocprim::default_con
 
 static uint32_t key_bits(uint32_t n_keys) {
   uint32_t b = 1;
-  while (b < 28 && (1u << b) < n_keys) ++b;  // 2 class bits + 2 mode bits + 28 key bits
+  while (b < 27 && (1u << b) < n_keys) ++b;  // 2 class bits + 2 mode bits + the long bit + 27 key bits
   return b;
 }
 
-// kb = key bits + 2: below the class, the key's table mode (0 row 0, 1 full, 2 wide tables,
-// keyws.h) sits above the key index, so a wave's lanes run one ladder variant. Keys beyond 2^28
-// share sort positions (the index is masked): locality only, never a verdict.
+// kb = key bits + 3: below the class, the key's table mode (0 row 0, 1 full, 2 wide tables,
+// keyws.h), so a wave's lanes run one ladder variant; below the mode the long bit (clear data of
+// more than ITEM_LONG_MIN bytes: its items hash in waves of their own at the end of the mode's
+// range instead of stalling a wave of 64 short ones; SURVEY.md §5 "long-context"); then the key
+// index. Keys beyond 2^27 share sort positions (the index is masked): locality only, never a
+// verdict.
 __global__ void __launch_bounds__(256) k_plan_keys(const cg_item* __restrict__ items, uint64_t n_items,
                                                    const cg_key* __restrict__ keys, uint32_t n_keys, uint32_t kb,
                                                    const uint32_t* __restrict__ uses,
@@ -51,7 +54,9 @@ __global__ void __launch_bounds__(256) k_plan_keys(const cg_item* __restrict__ i
   }
   uint32_t mode = 0;
   if (c < PLAN_CLASSES) mode = wide_idx[k] != KEY_NOT_WIDE ? 2u : uses[k] >= ED_DIRECT_MAX_USES ? 1u : 0u;
-  skey[i] = (c << kb) | (c < PLAN_CLASSES ? (mode << (kb - 2)) | (k & ((1u << (kb - 2)) - 1u)) : 0u);
+  const uint32_t lng = items[i].msg_len > ITEM_LONG_MIN ? 1u : 0u;
+  skey[i] = (c << kb) |
+            (c < PLAN_CLASSES ? (mode << (kb - 2)) | (lng << (kb - 3)) | (k & ((1u << (kb - 3)) - 1u)) : 0u);
   sval[i] = (uint32_t)i;
 }
 
@@ -92,7 +97,7 @@ size_t plan_sort_temp_bytes(uint64_t n_items) {
 
 hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d_keys, uint32_t n_keys,
                        const uint32_t* d_uses, const uint32_t* d_wide_idx, const ItemWs& iw, hipStream_t stream) {
-  const uint32_t kb = key_bits(n_keys) + 2;  // + the table-mode bits
+  const uint32_t kb = key_bits(n_keys) + 3;  // + the table-mode bits + the long bit
   const uint32_t B = 256;
   hipLaunchKernelGGL(k_plan_keys, dim3((unsigned)((n_items + B - 1) / B)), dim3(B), 0, stream, d_items, n_items,
                      d_keys, n_keys, kb, d_uses, d_wide_idx, iw.skey_in, iw.sval_in);

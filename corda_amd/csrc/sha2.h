@@ -101,6 +101,8 @@ CG_HD void sha512_init(uint64_t s[8]) {
   s[7] = 0x5be0cd19137e2179ULL;
 }
 
+// The 80 rounds fully unrolled: K folds into immediates and the a..h / w[i & 15] rotation into
+// register renaming (left rolled, the compiler indexed w through M0 and copied a..h every round).
 CG_HD void sha512_compress(uint64_t s[8], uint64_t w[16]) {
   uint64_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
 #pragma unroll
@@ -139,13 +141,33 @@ CG_HD void sha512_compress(uint64_t s[8], uint64_t w[16]) {
 
 // SHA-512(prefix64 || msg) where prefix64 is 16 little-endian words (e.g. R || Abyte).
 // Output: the 64 digest bytes as 16 little-endian words (ready for sc_reduce512).
+// Big-endian 64-bit word of the message at byte offset `pos` (whole word inside the message)
+CG_HD uint64_t cg_msg_dword_be(const uint8_t* arena, uint64_t len_rounded, uint64_t off) {
+  const uint32_t hi = CG_BSWAP32(cg_ld_bytes4(arena, len_rounded, off));
+  const uint32_t lo = CG_BSWAP32(cg_ld_bytes4(arena, len_rounded, off + 4));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 CG_HD void sha512_prefix64_msg(uint32_t out[16], const uint32_t prefix[16], const uint8_t* arena,
                                uint64_t len_rounded, uint64_t msg_off, uint64_t msg_len) {
   uint64_t s[8];
   sha512_init(s);
   const uint64_t n = 64 + msg_len;
   const uint64_t nblocks = (n + 17 + 127) >> 7;
-  for (uint64_t blk = 0; blk < nblocks; ++blk) {
+  // blocks made of prefix / message bytes only (no padding): straight loads, no per-word
+  // position logic; block 0 is the prefix and the first 64 message bytes
+  const uint64_t nfull = n >> 7;
+  for (uint64_t blk = 0; blk < nfull; ++blk) {
+    uint64_t w[16];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      w[j] = blk == 0 ? ((uint64_t)CG_BSWAP32(prefix[2 * j]) << 32) | CG_BSWAP32(prefix[2 * j + 1])
+                      : cg_msg_dword_be(arena, len_rounded, msg_off + blk * 128 - 64 + 8 * j);
+#pragma unroll
+    for (int j = 8; j < 16; ++j) w[j] = cg_msg_dword_be(arena, len_rounded, msg_off + blk * 128 - 64 + 8 * j);
+    sha512_compress(s, w);
+  }
+  for (uint64_t blk = nfull; blk < nblocks; ++blk) {
     uint64_t w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {

@@ -172,6 +172,28 @@ def test_wide_tables_vs_c_oracle(engine):
     assert np.array_equal(sd.cpu().numpy(), ref)
 
 
+def test_long_messages_vs_c_oracle(engine):
+    """Clear data longer than ITEM_LONG_MIN (1 KB) is hashed in waves of its own (plan_sort.hip:
+    the long bit sorts those items after the short ones of their class and table mode), up to
+    1 MB (CryptoUtilsTest.kt exercises 1 MB messages); every verdict equals the C oracle's, in one
+    shuffled batch with short items of all three schemes."""
+    from tools.workload import wl
+    parts = [wl.ed25519_batch(30000, n_keys=300, msg_len=270, corrupt_permille=120, seed=71, nthreads=16)[0],
+             wl.ed25519_batch(200, n_keys=50, msg_len=65536, corrupt_permille=120, seed=72, nthreads=16)[0],
+             wl.ed25519_batch(300, n_keys=300, msg_len=1500, corrupt_permille=120, seed=73, nthreads=16)[0],
+             wl.ed25519_batch(2, n_keys=2, msg_len=1 << 20, corrupt_permille=0, seed=74, nthreads=2)[0],
+             wl.ecdsa_batch(1, 6000, n_keys=60, msg_len=270, corrupt_permille=120, seed=75, nthreads=16)[0],
+             wl.ecdsa_batch(1, 150, n_keys=30, msg_len=20000, corrupt_permille=120, seed=76, nthreads=16)[0],
+             wl.ecdsa_batch(0, 100, n_keys=100, msg_len=4096, corrupt_permille=120, seed=77, nthreads=16)[0],
+             wl.ecdsa_batch(0, 2, n_keys=2, msg_len=1 << 20, corrupt_permille=0, seed=78, nthreads=2)[0]]
+    b, _ = wl.concat(parts, shuffle_seed=79)
+    assert (b.items["msg_len"] >= (1 << 20)).sum() == 4 and (b.items["msg_len"] > 1024).sum() > 700
+    st = engine.verify(b, B.MODE_DOVERIFY)
+    ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
+    assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} mismatches"
+    assert (st[b.items["msg_len"] >= (1 << 20)] == B.VALID).all()
+
+
 def test_host_buffer_chunked_path(engine):
     """cg_verify_batch on a batch large enough for the chunked H2D / verify pipeline: verdicts
     equal the C oracle's, including items whose offsets point outside the arena (CG_NOT_RUN) in a

@@ -16,6 +16,6 @@ for round in 1 2; do
     else
       env $v timeout -k 10 200 $B > $OUT/v${i}_$round.log 2>&1 || exit 1
     fi
-    echo "v$i ($v) round $round: $(grep -o '"value": [0-9.]*' $OUT/v${i}_$round.log | head -1)"
+    echo "v$i ($v) round $round: $(grep -o '"value": [0-9.]*' $OUT/v${i}_$round.log | head -1) $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print({k: v['ms_per_step'] for k, v in d['secondary']['stages'].items() if v['ms_per_step'] > 0.2})" $OUT/v${i}_$round.log)"
   done
 done

@@ -284,6 +284,35 @@ def test_tx_ids_random_vs_oracle(engine):
     assert np.all(st == 0)
 
 
+def test_tx_ids_of_kryo_encoded_components(engine):
+    """WireTransaction ids over components encoded by the Kryo restatement (corda_amd/kryo.py,
+    SURVEY §8 f1, parity unpinned): the GPU ids equal the oracle's MerkleTransaction.kt rule over
+    the same encoded bytes, for transactions of every component type."""
+    import hashlib
+    from corda_amd import kryo as K, merkle
+    rng = np.random.default_rng(6)
+    txs = []
+    for t in range(500):
+        key = K.PublicKeyRef(4, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+        notary = K.Party(bytes.fromhex("3031310b300906035504061302474231") + bytes([t % 251]), key)
+        h = lambda: K.SecureHash(rng.integers(0, 256, 32, dtype=np.uint8).tobytes())  # noqa: E731
+        wtx = K.WireTransaction(
+            inputs=[K.StateRef(h(), int(i)) for i in range(int(rng.integers(0, 4)))],
+            attachments=[h() for _ in range(int(rng.integers(0, 2)))],
+            outputs=[K.TransactionState("com.example.IOUState", (("value", int(rng.integers(0, 1 << 30))),
+                                                                 ("lender", rng.bytes(44))), "com.example.IOUContract",
+                                        notary) for _ in range(int(rng.integers(1, 4)))],
+            commands=[K.Command("com.example.IOUContract$Commands$Create", (), (key,))],
+            notary=notary, time_window=K.TimeWindow((1_700_000_000 + t, 0), None) if t % 2 else None,
+            privacy_salt=K.PrivacySalt(hashlib.sha256(bytes([t % 256, t // 256])).digest()))
+        d = wtx.data()
+        txs.append((d.components, d.salt, d.salt_blob))
+    ids, st = merkle.tx_ids(txs, engine)
+    assert np.all(st == 0)
+    for (blobs, salt, sb), got in zip(txs, ids):
+        assert got == ocorda.tx_id(blobs, salt, sb)
+
+
 def test_crypto_api_behaviour():
     """The reference's own behavioural tests (CryptoUtilsTest.kt:233-286,
     TransactionSignatureTest.kt:33-40) through the host mirror."""

@@ -70,7 +70,7 @@ EC_LADDER_MUL = {"secp256r1": 895, "secp256k1": 877}
 EC_WIDE_MUL = {"secp256r1": 586, "secp256k1": 586}  # k_ec_ladder_wide: 32 + 22 mixed additions + x-check
 # table modes (corda_amd/csrc/keyws.h): full tables from 32 items per key, wide from 384
 KEY_FULL_MIN_USES, KEY_WIDE_MAX = 32, 8192
-KEY_WIDE_MIN_USES = {4: int(os.environ.get("CG_WIDE_MIN_USES_ED", 4096)), 3: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512)),
+KEY_WIDE_MIN_USES = {4: int(os.environ.get("CG_WIDE_MIN_USES_ED", 1536)), 3: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512)),
                      2: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512))}
 EC_INV_MUL_16 = {"secp256r1": 536, "secp256k1": 563}
 EC_MAC_PER_MUL_P = {"secp256r1": 144, "secp256k1": 162}
@@ -97,6 +97,8 @@ def parse():
     ap.add_argument("--ec-keys", type=int, default=1024, help="keys per ECDSA curve")
     ap.add_argument("--msg-len", type=int, default=270)
     ap.add_argument("--chunk-items", type=int, default=0, help="device chunk (0: CG_DEFAULT_CHUNK_ITEMS = 8M)")
+    ap.add_argument("--stream", choices=("ctx", "torch"), default="ctx",
+                    help="headline calls on the engine context's stream (NULL, as a JNI caller) or torch's")
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--host-steps", type=int, default=3, help="PCIe-inclusive cg_verify_batch calls (0: off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -257,14 +259,18 @@ def upload(dev, b):
     return up(b.keys), up(b.items), up(b.arena), torch.full((b.n,), 255, dtype=torch.uint8, device=dev)
 
 
-def timed_device(eng, bufs, b, steps, warmup, stream, dev, gather=None):
+def timed_device(eng, bufs, b, steps, warmup, stream, dev, gather=None, ctx_stream=False):
+    """ctx_stream: enqueue on the engine context's own stream (hip_stream = NULL, the form a JNI
+    caller uses) instead of torch's; the verdict gather then waits for it (device sync)."""
     import torch
     kd, idd, ad, sd = bufs
-    sptr = stream.cuda_stream
+    sptr = 0 if ctx_stream else stream.cuda_stream
 
     def step():
         eng.verify_device(kd.data_ptr(), len(b.keys), idd.data_ptr(), b.n, ad.data_ptr(), b.arena.size,
                           sd.data_ptr(), 0, sptr)
+        if gather is not None and ctx_stream:
+            torch.cuda.synchronize(dev)
         if gather is not None:
             gather(sd)
 
@@ -542,7 +548,7 @@ def main():
     gather = None
     if world > 1:
         gather = lambda sd: shard.gather_verdicts(sd, world * batch.n, world)  # noqa: E731  RCCL all-gather
-    step = timed_device(eng, bufs, batch, a.steps, a.warmup, stream, dev, gather)
+    step = timed_device(eng, bufs, batch, a.steps, a.warmup, stream, dev, gather, ctx_stream=a.stream == "ctx")
     eng.stage_times()  # drop the warmup's records
     if world > 1:
         dist.barrier()

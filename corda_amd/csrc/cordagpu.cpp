@@ -364,10 +364,14 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     delete c;
     return hip_fail(e, "hipStreamCreate");
   }
-  // Side streams: plain by default. CG_MASKED_SIDE_STREAMS=1 creates them with a CU mask covering
-  // every CU, which HIP backs with a hardware queue of their own (no sharing with the caller's
-  // stream under GPU_MAX_HW_QUEUES multiplexing); measured no faster once the table builds start
-  // after the plan sort (gpurun_out/ab_side), kept for A/B runs.
+  // Side streams: plain, created right after the context's stream. HIP multiplexes plain streams
+  // onto GPU_MAX_HW_QUEUES (4) hardware queues in creation order, so the context's stream (the one a
+  // caller gets with hip_stream = NULL) and the three side streams sit on four distinct queues;
+  // a caller stream created elsewhere may share one with a side stream, whose latency-bound table
+  // chain (milliseconds) then runs ahead of that caller's hashes (profiles/r02/wide_v2).
+  // CG_MASKED_SIDE_STREAMS=1: side streams with an all-CU mask, which HIP backs with queues of
+  // their own; measured slower (their chains and tables take CU share from the plan sort and the
+  // hashes: gpurun_out/ab_mask), kept for A/B runs.
   {
     hipDeviceProp_t prop;
     const char* mk = getenv("CG_MASKED_SIDE_STREAMS");

@@ -165,7 +165,7 @@ struct KeyWs {
 // (ECDSA) of chip time to build and saves ~0.64 ns (Ed25519) / ~2 ns (ECDSA) per item against the
 // full tables, so ~1900 / ~500 items. (Environment CG_WIDE_MIN_USES_ED / _EC override, for A/B.)
 #ifndef KEY_WIDE_MIN_USES_ED
-#define KEY_WIDE_MIN_USES_ED 4096u
+#define KEY_WIDE_MIN_USES_ED 1536u
 #endif
 #ifndef KEY_WIDE_MIN_USES_EC
 #define KEY_WIDE_MIN_USES_EC 512u

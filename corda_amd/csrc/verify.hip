@@ -171,7 +171,14 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys, w.uses,
                      (const uint8_t*)w.seen, w.full, w.full_count, w.wide_idx, w.wide, w.wide_count, w.cap_ed,
                      w.cap_ec, w.min_ed, w.min_ec);
-  if (!fork) {
+  static const bool serial = [] {  // CG_SERIAL_KEYPREP=1: key prep on the caller's stream (A/B runs)
+    const char* v = getenv("CG_SERIAL_KEYPREP");
+    return v && v[0] == '1';
+  }();
+  if (!fork || serial) {
+    if (fork) {  // the item stages still wait for these events
+      fork->pending.on = false;
+    }
     ed_launch_key_abyte(d_keys, n_keys, d_arena, arena_len, w, stream);
     for (int curve : {CG_CURVE_R1, CG_CURVE_K1}) {
       ec_launch_keyprep_chains(curve, d_keys, n_keys, d_arena, arena_len, w, stream, nullptr);
@@ -179,6 +186,12 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
     }
     ed_launch_keyprep_chains(d_keys, n_keys, d_arena, arena_len, w, stream);
     ed_launch_keyprep_tabs(d_keys, n_keys, w, stream);
+    if (fork) {
+      hipError_t e = hipSuccess;
+      for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventRecord(fork->ec_decoded[k], stream);
+      for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventRecord(fork->ready[k], stream);
+      if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
   }
   hipError_t e = hipEventRecord(fork->start, stream);

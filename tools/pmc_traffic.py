@@ -22,8 +22,10 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_ed_hash", "k_ed_ladder_pf", "k_ed_finish", "k_ec_prep<1>", "k_ec_inv<1>", "k_ec_ladder<1, true>",
-           "k_ec_prep<0>", "k_ec_inv<0>", "k_ec_ladder<0, true>")
+KERNELS = ("k_ed_hash", "k_ed_ladder_pf", "k_ed_ladder_wide", "k_ed_finish", "k_ec_prep<1>", "k_ec_inv<1>",
+           "k_ec_ladder<1, true>", "k_ec_ladder_wide<1>", "k_ec_prep<0>", "k_ec_inv<0>", "k_ec_ladder<0, true>",
+           "k_ec_ladder_wide<0>", "k_ed_wide_fwd", "k_ed_wide_inv", "k_ed_wide_bwd", "k_ec_wide_fwd<1>",
+           "k_ec_wide_bwd<1>", "k_ec_wide_fwd<0>", "k_ec_wide_bwd<0>")
 
 
 def short(name):

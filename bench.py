@@ -347,7 +347,7 @@ def run_secondary_device(eng, dev, stream, b, steps=4):
     """Device-resident rate of a secondary batch plus its item-kernel time (tables prebuilt)."""
     import torch
     bufs = upload(dev, b)
-    step = timed_device(eng, bufs, b, steps, 1, stream, dev)
+    step = timed_device(eng, bufs, b, steps, 1, stream, dev, ctx_stream=True)
     eng.stage_times()
     t = time.perf_counter()
     for _ in range(steps):

@@ -327,7 +327,9 @@ void ed_launch_key_abyte(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d
 // decode -> chains (light), then the row tables (heavy)
 void ed_launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                               const KeyWs& w, hipStream_t stream);
-void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream);
+// the full / row-0 tables and / or the wide tables
+void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream, bool full,
+                            bool wide);
 // item stages (verify.hip launch_items orders them across the main and side streams)
 void ed_launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
                      uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len,
@@ -343,7 +345,8 @@ hipError_t ec_init_const(void* d_btab, hipStream_t stream);
 // per curve: decode (records `decoded`: k_ec_prep needs the key status) -> chains; then the tables
 void ec_launch_keyprep_chains(int curve, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena,
                               uint64_t arena_len, const KeyWs& w, hipStream_t stream, hipEvent_t decoded);
-void ec_launch_keyprep_tabs(int curve, const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream);
+void ec_launch_keyprep_tabs(int curve, const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream,
+                            bool full, bool wide);
 void ec_launch_front(int curve, const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena,
                      uint64_t arena_len, uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs,
                      uint64_t msgs_len, const ItemWs& iw, hipStream_t stream);

@@ -133,8 +133,9 @@ hipError_t init_btab(void* d_btab, hipStream_t stream) {
   return ec_init_const(d_btab, stream);
 }
 
-// The deferred table builds, forked from `stream` at this point: Ed25519 first (its ladder runs
-// first), the two curves after it (their ladders run after the Ed25519 ladder and finish).
+// The deferred wide-table builds (the full / row-0 tables start with the chains), forked from
+// `stream` at this point: Ed25519 first (its ladder runs first), the two curves after it (their
+// ladders run after the Ed25519 ladder and finish).
 static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
   PendingTabs& p = fork->pending;
   if (!p.on) return hipSuccess;
@@ -143,14 +144,14 @@ static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
   hipError_t e = hipEventRecord(fork->planned, stream);
   if (e == hipSuccess) e = hipStreamWaitEvent(fork->side[2], fork->planned, 0);
   if (e != hipSuccess) return e;
-  ed_launch_keyprep_tabs(p.keys, p.n_keys, w, fork->side[2]);
+  ed_launch_keyprep_tabs(p.keys, p.n_keys, w, fork->side[2], false, true);
   e = hipEventRecord(fork->ed_tabs, fork->side[2]);
   if (e == hipSuccess) e = hipEventRecord(fork->ready[2], fork->side[2]);
   for (int k = 0; k < 2 && e == hipSuccess; ++k) {
     e = hipStreamWaitEvent(fork->side[k], fork->planned, 0);
     if (e == hipSuccess) e = hipStreamWaitEvent(fork->side[k], fork->ed_tabs, 0);
     if (e != hipSuccess) break;
-    ec_launch_keyprep_tabs(k == 0 ? CG_CURVE_R1 : CG_CURVE_K1, p.keys, p.n_keys, w, fork->side[k]);
+    ec_launch_keyprep_tabs(k == 0 ? CG_CURVE_R1 : CG_CURVE_K1, p.keys, p.n_keys, w, fork->side[k], false, true);
     e = hipEventRecord(fork->ready[k], fork->side[k]);
   }
   return e;
@@ -182,10 +183,10 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
     ed_launch_key_abyte(d_keys, n_keys, d_arena, arena_len, w, stream);
     for (int curve : {CG_CURVE_R1, CG_CURVE_K1}) {
       ec_launch_keyprep_chains(curve, d_keys, n_keys, d_arena, arena_len, w, stream, nullptr);
-      ec_launch_keyprep_tabs(curve, d_keys, n_keys, w, stream);
+      ec_launch_keyprep_tabs(curve, d_keys, n_keys, w, stream, true, true);
     }
     ed_launch_keyprep_chains(d_keys, n_keys, d_arena, arena_len, w, stream);
-    ed_launch_keyprep_tabs(d_keys, n_keys, w, stream);
+    ed_launch_keyprep_tabs(d_keys, n_keys, w, stream, true, true);
     if (fork) {
       hipError_t e = hipSuccess;
       for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventRecord(fork->ec_decoded[k], stream);
@@ -197,11 +198,15 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   hipError_t e = hipEventRecord(fork->start, stream);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->start, 0);
   if (e != hipSuccess) return e;
-  // light phase now: decodes and row-base chains (few waves, latency-bound)
+  // now: decodes, row-base chains (few waves, latency-bound) and the full / row-0 tables
   ec_launch_keyprep_chains(CG_CURVE_R1, d_keys, n_keys, d_arena, arena_len, w, fork->side[0], fork->ec_decoded[0]);
+  ec_launch_keyprep_tabs(CG_CURVE_R1, d_keys, n_keys, w, fork->side[0], true, false);
   ec_launch_keyprep_chains(CG_CURVE_K1, d_keys, n_keys, d_arena, arena_len, w, fork->side[1], fork->ec_decoded[1]);
+  ec_launch_keyprep_tabs(CG_CURVE_K1, d_keys, n_keys, w, fork->side[1], true, false);
   ed_launch_keyprep_chains(d_keys, n_keys, d_arena, arena_len, w, fork->side[2]);
-  // heavy phase (the row tables): after the first chunk's plan when items follow, else now
+  ed_launch_keyprep_tabs(d_keys, n_keys, w, fork->side[2], true, false);
+  // the wide tables (thousands of entries per key, they hold every SIMD for milliseconds): after the
+  // first chunk's plan sort when items follow (its decoupled look-back stalls behind them), else now
   fork->pending.on = true;
   fork->pending.keys = d_keys;
   fork->pending.n_keys = n_keys;

@@ -331,13 +331,15 @@ static void launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const u
 }
 
 template <int C>
-static void launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream) {
+static void launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream, bool full,
+                                bool wide) {
   const uint32_t B = 64;
   const uint64_t elanes = (uint64_t)n_keys * EC_ROWS;
-  hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3((unsigned)((elanes + B - 1) / B)), dim3(B), 0, stream, d_keys, n_keys,
-                     w.hdr, w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count,
-                     (const uint32_t*)w.wide_idx, w.tab, w.ecs);
-  if (w.cap_ec) {
+  if (full)
+    hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3((unsigned)((elanes + B - 1) / B)), dim3(B), 0, stream, d_keys,
+                       n_keys, w.hdr, w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full,
+                       (const uint32_t*)w.full_count, (const uint32_t*)w.wide_idx, w.tab, w.ecs);
+  if (wide && w.cap_ec) {
     const uint64_t gl = (uint64_t)w.cap_ec * EC_WIDE_ROWS * EC_WIDE_GROUPS, rl = (uint64_t)w.cap_ec * EC_WIDE_ROWS;
     const uint32_t* wl = (const uint32_t*)w.wide;
     const uint32_t* wc = (const uint32_t*)w.wide_count;
@@ -357,9 +359,10 @@ void ec_launch_keyprep_chains(int curve, const cg_key* d_keys, uint32_t n_keys, 
   else launch_keyprep_chains<CG_CURVE_K1>(d_keys, n_keys, d_arena, arena_len, w, stream, decoded);
 }
 
-void ec_launch_keyprep_tabs(int curve, const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream) {
-  if (curve == CG_CURVE_R1) launch_keyprep_tabs<CG_CURVE_R1>(d_keys, n_keys, w, stream);
-  else launch_keyprep_tabs<CG_CURVE_K1>(d_keys, n_keys, w, stream);
+void ec_launch_keyprep_tabs(int curve, const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream,
+                            bool full, bool wide) {
+  if (curve == CG_CURVE_R1) launch_keyprep_tabs<CG_CURVE_R1>(d_keys, n_keys, w, stream, full, wide);
+  else launch_keyprep_tabs<CG_CURVE_K1>(d_keys, n_keys, w, stream, full, wide);
 }
 
 template <int C>

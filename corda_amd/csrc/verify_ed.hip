@@ -800,13 +800,15 @@ void ed_launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const uint8
                        (const BaseSlot*)w.bases, w.wed);
 }
 
-void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream) {
+void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream, bool full,
+                            bool wide) {
   const uint32_t B = 64;
   const uint64_t lanes = (uint64_t)n_keys * EdCfg::kRows;
-  hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((unsigned)((lanes + B - 1) / B)), dim3(B), 0, stream, d_keys, n_keys, w.hdr,
-                     w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count,
-                     (const uint32_t*)w.wide_idx, w.tab, w.ecs);
-  if (w.cap_ed) {
+  if (full)
+    hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((unsigned)((lanes + B - 1) / B)), dim3(B), 0, stream, d_keys, n_keys,
+                       w.hdr, w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count,
+                       (const uint32_t*)w.wide_idx, w.tab, w.ecs);
+  if (wide && w.cap_ed) {
     const uint64_t gl = (uint64_t)w.cap_ed * EdWideCfg::kRows * ED_WIDE_GROUPS, rl = (uint64_t)w.cap_ed * EdWideCfg::kRows;
     const uint32_t* wl = (const uint32_t*)w.wide;
     const uint32_t* wc = (const uint32_t*)w.wide_count;

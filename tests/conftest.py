@@ -18,6 +18,15 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def engine():
+    # torch ships its own HIP runtime (ROCm 7.0 libamdhip64.so) beside the system one the engine
+    # links (/opt/rocm libamdhip64.so.7): with both in one process, torch's must open the device
+    # first, or its later init reports "No HIP GPUs are available".
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except ImportError:
+        pass
     from corda_amd.engine import Engine
     e = Engine(0)
     yield e

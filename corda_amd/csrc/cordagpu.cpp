@@ -121,14 +121,17 @@ uint64_t chunk_of(const cg_ctx* c, uint64_t n) {
 // Key and item workspace for n_keys keys and chunks of ws_items items, plus the wide-table pools
 // for a call of call_items items (0: none). Growing them waits for the device (cg_reserve ahead
 // of time avoids that).
+// A call of more than one chunk gets two item workspaces (launch_chunked runs chunk k + 1's front
+// before chunk k's back).
+size_t item_half_bytes(uint64_t ws_items) { return (cg::item_ws_bytes(ws_items) + 255) & ~(size_t)255; }
 hipError_t ensure_ws(cg_ctx* c, uint32_t n_keys, uint64_t ws_items, uint64_t call_items = 0) {
   const size_t wide = cg::wide_bytes(n_keys, call_items);
-  if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= cg::item_ws_bytes(ws_items) &&
-      c->wide.cap >= wide)
+  const size_t items = item_half_bytes(ws_items) * (call_items > ws_items ? 2 : 1);
+  if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= items && c->wide.cap >= wide)
     return hipSuccess;
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess) e = c->keyprep.ensure(cg::keyprep_bytes(n_keys));
-  if (e == hipSuccess) e = c->itemws.ensure(cg::item_ws_bytes(ws_items));
+  if (e == hipSuccess) e = c->itemws.ensure(items);
   if (e == hipSuccess) e = c->wide.ensure_exact(wide);
   return e;
 }
@@ -163,10 +166,24 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   hipError_t e =
       cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork, d_items, n_items, &wp);
   const uint64_t per = chunk_of(c, n_items);
-  for (uint64_t f = 0; f < n_items && e == hipSuccess; f += per) {
-    const uint64_t cnt = per < n_items - f ? per : n_items - f;
-    e = cg::launch_items(d_keys, n_keys, d_items + f, cnt, d_arena, arena_len, mode, d_status + f, c->keyprep.p,
-                         c->itemws.p, c->btab.p, s, d_msgs, msgs_len, &c->fork, &wp);
+  const uint64_t nch = (n_items + per - 1) / per;
+  // chunk k's item workspace: half k % 2 when the buffer holds two (ensure_ws), else the one
+  const bool two = nch > 1 && c->itemws.cap >= 2 * item_half_bytes(per);
+  auto ws = [&](uint64_t k) { return (void*)((uint8_t*)c->itemws.p + (two ? (k & 1) * item_half_bytes(per) : 0)); };
+  auto cnt = [&](uint64_t k) { return per < n_items - k * per ? per : n_items - k * per; };
+  auto front = [&](uint64_t k) {
+    return cg::launch_items_front(d_keys, n_keys, d_items + k * per, cnt(k), d_arena, arena_len, mode,
+                                  d_status + k * per, c->keyprep.p, ws(k), s, d_msgs, msgs_len, &c->fork, &wp);
+  };
+  // chunk k + 1's front (plan, hashes, ECDSA prep) before chunk k's back (ladders): the first
+  // chunk's wait for the key tables is spent on the next chunk's fronts
+  if (e == hipSuccess) e = front(0);
+  for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
+    if (!two && k > 0) e = front(k);
+    if (two && k + 1 < nch && e == hipSuccess) e = front(k + 1);
+    if (e == hipSuccess)
+      e = cg::launch_items_back(d_keys, n_keys, d_items + k * per, cnt(k), d_arena, arena_len, d_status + k * per,
+                                c->keyprep.p, ws(k), c->btab.p, s, &c->fork, &wp);
   }
   return e;
 }

@@ -474,24 +474,27 @@ CG_HD void ec_g_rows_init(EcRowTab& T, EcRowScratch& s, const EcConsts& K) {
 // radix-2^8 digit of u2: row j holds the affine multiples 1..128 of 2^{8j} Q. The top digit
 // (bits 248..255 plus the carry) is left in [0, 256] instead of carrying into a 33rd digit, so
 // row 31 also holds the multiples 129..256, stored as a 33rd row of the table (304 128 B). G
-// gets one row per signed radix-2^12 digit of u1 over a constant table (22 rows x 2048 multiples
-// of 2^{12u} G, 3.2 MB per curve). R = one entry per row: 32 + 22 mixed additions, no doublings,
-// against 69 additions + 18 doublings over the full tables.
+// gets one row per signed radix-2^16 digit of u1 over a constant table built once per context
+// (16 rows x 32768 multiples of 2^{16u} G, plus a 17th row for the recoding carry out of bit 255,
+// whose digit is 0 or 1: 40 MB per curve, MALL-resident). R = one entry per row: 32 + 17 mixed
+// additions, no doublings, against 69 additions + 18 doublings over the full tables (radix 2^12
+// for G took 32 + 22).
 #define EC_WIDE_W 8
 #define EC_WIDE_DIGITS 32
 #define EC_WIDE_ROWS 33   // row 32 = multiples 129..256 of row 31's base
 #define EC_WIDE_MULT 128
 #define EC_WIDE_PACKED 16  // int16 digits (the top one reaches 256)
-#define EC_WIDE_GW 12
-#define EC_WIDE_GDIGITS 22  // 264 bits: the top digit covers bits 252..255 plus the carry
-#define EC_WIDE_GMULT 2048
-#define EC_WIDE_GPACKED 11  // int16 digits
+#define EC_WIDE_GW 16
+#define EC_WIDE_GDIGITS 17  // 272 bits: the 17th digit is the carry out of bits 240..255
+#define EC_WIDE_GMULT 32768
+#define EC_WIDE_GPACKED 9  // int16 digits
+static_assert(EC_WIDE_GW <= 16 && EC_WIDE_GDIGITS * EC_WIDE_GW > 256, "G digits: int16, one digit past bit 255");
 
 struct EcWideTab {
   EcAff t[EC_WIDE_ROWS][EC_WIDE_MULT];  // t[j][k-1] = k 2^{8j} Q; t[32][k-1] = (128 + k) 2^{248} Q
 };
 struct EcGWideTab {
-  EcAff t[EC_WIDE_GDIGITS][EC_WIDE_GMULT];  // t[u][k-1] = k 2^{12u} G
+  EcAff t[EC_WIDE_GDIGITS][EC_WIDE_GMULT];  // t[u][k-1] = k 2^{16u} G
 };
 // Batch-inversion scratch of one wide row (the Jacobian X, Y wait in the output entries)
 struct EcWideScratch {
@@ -654,10 +657,9 @@ CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u
 }
 
 // G wide row u, multiples 32 g + 1 .. 32 g + 32 (one lane of the per-context table build)
+// (the group from the row's base P = 2^{16u} G: the host tests build only the groups their digits touch)
 template <int C>
-CG_HD void ec_gwide_group(EcAff* out, int u, int g, EcRowScratch& s, const EcConsts& K) {
-  Jac P = {K.gx, K.gy, K.one_p};
-  if (u > 0) jac_dbl_n<C>(P, P, EC_WIDE_GW * u);
+CG_HD void ec_gwide_group_from(EcAff* out, const Jac& P, int g, EcRowScratch& s, const EcConsts& K) {
   const uint32_t m = 32u * (uint32_t)g + 1u;
   Jac F = P;
   for (int b = 30 - __builtin_clz(m); b >= 0; --b) {
@@ -665,4 +667,11 @@ CG_HD void ec_gwide_group(EcAff* out, int u, int g, EcRowScratch& s, const EcCon
     if ((m >> b) & 1u) jac_add<C>(F, F, P, K);
   }
   ec_multiples<C>(out, F, P, EC_MULT, s, K);
+}
+
+template <int C>
+CG_HD void ec_gwide_group(EcAff* out, int u, int g, EcRowScratch& s, const EcConsts& K) {
+  Jac P = {K.gx, K.gy, K.one_p};
+  if (u > 0) jac_dbl_n<C>(P, P, EC_WIDE_GW * u);
+  ec_gwide_group_from<C>(out, P, g, s, K);
 }

@@ -399,32 +399,37 @@ CG_HD void ed_btab_wb_row(ge_niels* row, const ge_p3& B, int u, const fe& d2) {
 // ---------------------------------------------------------------- wide tables (hot keys)
 // A key with many items in the call (keyws.h KEY_WIDE_MIN_USES) gets one row per signed
 // radix-2^8 digit of h: row j holds the affine multiples 1..128 of 2^{8j} (-A) (32 rows,
-// 491 520 B). B gets one row per signed radix-2^12 digit of S' over a constant table (row u
-// holds 1..2048 times 2^{12u} B, 22 rows, 5.4 MB). R' = sum of one entry per row: 32 + 22 = 54
-// mixed additions and no doublings, against 69 additions + 6 doublings over the full tables.
+// 491 520 B). B gets one row per signed radix-2^16 digit of S' over a constant table built once
+// per context (row u holds 1..32768 times 2^{16u} B: 16 rows, 62.9 MB, MALL-resident). R' = sum of
+// one entry per row: 32 + 16 = 48 mixed additions and no doublings, against 69 additions + 6
+// doublings over the full tables. (Radix 2^12 for B, 5.4 MB, took 32 + 22 = 54; the B gathers
+// miss the 4 MB per-XCD L2 either way.)
 #define ED_WIDE_W 8
-#define ED_WIDE_BW 12
+#ifndef ED_WIDE_BW
+#define ED_WIDE_BW 16
+#endif
 struct EdWideCfg {
   static constexpr int kDigits = (253 + ED_WIDE_W - 1) / ED_WIDE_W;  // 32: h < 2^253 leaves the carry room
   static constexpr int kRows = kDigits;
   static constexpr int kMult = 1 << (ED_WIDE_W - 1);                 // 128
   static constexpr int kPackedWords = (kDigits + 3) / 4;             // int8 digits
-  static constexpr int kBDigits = (253 + ED_WIDE_BW - 1) / ED_WIDE_BW;  // 22
-  static constexpr int kBMult = 1 << (ED_WIDE_BW - 1);                // 2048
+  static constexpr int kBDigits = (253 + ED_WIDE_BW - 1) / ED_WIDE_BW;  // 16
+  static constexpr int kBMult = 1 << (ED_WIDE_BW - 1);                // 32768 (|digit| <= 2^15)
   static constexpr int kBPackedWords = (kBDigits + 1) / 2;            // int16 digits
-  static constexpr int kOps = kRows + kBDigits;                       // 54
+  static constexpr int kOps = kRows + kBDigits;                       // 48
 };
 static_assert(253 % ED_WIDE_W != 0 && 253 % ED_WIDE_BW != 0, "the top digit keeps headroom for the carry");
+static_assert(ED_WIDE_BW <= 16, "B digits are packed as int16");
 
 struct EdWideTab {
   ge_niels t[EdWideCfg::kRows][EdWideCfg::kMult];  // t[j][k-1] = k 2^{8j} (-A)
 };
 struct EdBWideTab {
-  ge_niels t[EdWideCfg::kBDigits][EdWideCfg::kBMult];  // t[u][k-1] = k 2^{12u} B
+  ge_niels t[EdWideCfg::kBDigits][EdWideCfg::kBMult];  // t[u][k-1] = k 2^{16u} B
 };
 
 // R' = h (-A) + S' B over the wide tables, digits already recoded (eh: radix 2^8, esb: radix
-// 2^12). Entries by |digit|, the sign through ge_madd_signed (the form k_ed_ladder_wide runs).
+// 2^ED_WIDE_BW). Entries by |digit|, the sign through ge_madd_signed (the form k_ed_ladder_wide runs).
 template <class TabA, class TabB, class PickA, class PickB>
 CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const TabA& TA, const TabB& TB,
                                  PickA pick_a, PickB pick_b) {
@@ -445,4 +450,38 @@ CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t*
     if (o + 1 < EdWideCfg::kOps) ge_p1p1_to_p3(R, t);
   }
   ge_p1p1_to_p2(out, t);
+}
+
+// m * P for a small m >= 1 (double-and-add, MSB first)
+CG_HD void ed_small_mul(ge_p3& R, const ge_p3& P, uint32_t m, const fe& d2) {
+  ge_cached c;
+  ge_p3_to_cached(c, P, d2);
+  R = P;
+  ge_p1p1 t;
+  int top = 31 - __builtin_clz(m);
+  for (int b = top - 1; b >= 0; --b) {
+    ge_p3_dbl(t, R);
+    ge_p1p1_to_p3(R, t);
+    if ((m >> b) & 1u) {
+      ge_add_cached(t, R, c);
+      ge_p1p1_to_p3(R, t);
+    }
+  }
+}
+
+// Wide B row u, multiples 8 grp + 1 .. 8 grp + 8 of 2^{ED_WIDE_BW u} B (one lane of the
+// per-context build k_ed_bwide_init; the host tests build the groups their digits touch).
+CG_HD void ed_bwide_group(ge_niels* out8, const ge_p3& B, int u, int grp, const fe& d2) {
+  ge_p3 P = B;
+  if (u > 0) ed_dbl_n(P, P, ED_WIDE_BW * u);
+  ge_p3 pts[8];
+  ed_small_mul(pts[0], P, 8u * (uint32_t)grp + 1u, d2);
+  ge_cached c;
+  ge_p3_to_cached(c, P, d2);
+  ge_p1p1 t;
+  for (int k = 1; k < 8; ++k) {
+    ge_add_cached(t, pts[k - 1], c);
+    ge_p1p1_to_p3(pts[k], t);
+  }
+  ed_niels_batch8(out8, pts, d2);
 }

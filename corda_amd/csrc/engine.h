@@ -111,6 +111,18 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
                         const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
                         const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0, const Fork* fork = nullptr,
                         const WidePool* wide = nullptr);
+// launch_items in two halves: the front (status checks, plan sort, challenge hashes, ECDSA prep and
+// s^-1: needs only the decoded keys) and the back (ladders, finish: need the key tables). Between the
+// two a caller with a second item workspace may enqueue the next chunk's front, so the first chunk's
+// wait for the key tables is spent on the second chunk's fronts (cordagpu.cpp launch_chunked).
+hipError_t launch_items_front(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                              const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
+                              const void* d_keyprep, void* d_item_ws, hipStream_t stream, const uint8_t* d_msgs,
+                              uint64_t msgs_len, const Fork* fork, const WidePool* wide);
+hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                             const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_status, const void* d_keyprep,
+                             void* d_item_ws, const void* d_btab, hipStream_t stream, const Fork* fork,
+                             const WidePool* wide);
 
 // Hashing kernels
 hipError_t launch_sha256(const cg_span* d_spans, uint64_t n, const uint8_t* d_arena, uint64_t arena_len,

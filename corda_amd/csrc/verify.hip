@@ -219,10 +219,10 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   return hipGetLastError();
 }
 
-hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
-                        const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                        const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
-                        const uint8_t* d_msgs, uint64_t msgs_len, const Fork* fork, const WidePool* wide) {
+hipError_t launch_items_front(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                              const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
+                              const void* d_keyprep, void* d_item_ws, hipStream_t stream, const uint8_t* d_msgs,
+                              uint64_t msgs_len, const Fork* fork, const WidePool* wide) {
   if (n_items == 0) return hipSuccess;
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
@@ -248,6 +248,18 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
   CG_TIME(fork, CG_STAGE_K1_FRONT, stream,
           ec_launch_front(CG_CURVE_K1, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
                           stream));
+  return hipGetLastError();
+}
+
+hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                             const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_status, const void* d_keyprep,
+                             void* d_item_ws, const void* d_btab, hipStream_t stream, const Fork* fork,
+                             const WidePool* wide) {
+  if (n_items == 0) return hipSuccess;
+  (void)d_keys;
+  const KeyWs w = key_ws((void*)d_keyprep, n_keys, wide);
+  const ItemWs iw = item_ws(d_item_ws, n_items);
+  hipError_t e = hipSuccess;
   // row-0 ladders: on the side streams (after their tables) when forked, else first on `stream`
   if (fork) {
     e = hipEventRecord(fork->front, stream);
@@ -289,6 +301,17 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
     hipStreamWaitEvent(stream, fork->row0[1], 0);
   }
   return hipGetLastError();
+}
+
+hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                        const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
+                        const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
+                        const uint8_t* d_msgs, uint64_t msgs_len, const Fork* fork, const WidePool* wide) {
+  hipError_t e = launch_items_front(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, d_keyprep,
+                                    d_item_ws, stream, d_msgs, msgs_len, fork, wide);
+  if (e != hipSuccess) return e;
+  return launch_items_back(d_keys, n_keys, d_items, n_items, d_arena, arena_len, d_status, d_keyprep, d_item_ws,
+                           d_btab, stream, fork, wide);
 }
 
 hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,

@@ -115,23 +115,6 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_chain(uint32_t n_keys, const 
   }
 }
 
-// m * P for a small m >= 1 (double-and-add, MSB first)
-__device__ void ed_small_mul(ge_p3& R, const ge_p3& P, uint32_t m) {
-  ge_cached c;
-  ge_p3_to_cached(c, P, c_ed.d2);
-  R = P;
-  ge_p1p1 t;
-  int top = 31 - __builtin_clz(m);
-  for (int b = top - 1; b >= 0; --b) {
-    ge_p3_dbl(t, R);
-    ge_p1p1_to_p3(R, t);
-    if ((m >> b) & 1u) {
-      ge_add_cached(t, R, c);
-      ge_p1p1_to_p3(R, t);
-    }
-  }
-}
-
 // the 32 affine multiples of a row base, one inversion per row (ed_row_build; Z prefixes in the
 // key's ECDSA scratch, unused by an Ed25519 key). Lanes g < n_keys: row 0 of key g (every key
 // with items); then row-major (row j >= 1, position l of the full-table list), so only hot keys'
@@ -207,7 +190,7 @@ __global__ void __launch_bounds__(64) k_ed_wide_fwd(uint32_t n_keys, const EdKey
   if (hdr[i].status != 0) return;
   EdWideSlot& ws = wed[wide_idx[i]];
   ge_p3 first;
-  ed_small_mul(first, ws.bases[L.j], ED_WIDE_GROUP * L.g + 1);
+  ed_small_mul(first, ws.bases[L.j], ED_WIDE_GROUP * L.g + 1, c_ed.d2);
   ed_multiples_fwd<ED_WIDE_GROUP>(&ws.tab.t[L.j][ED_WIDE_GROUP * L.g], first, ws.bases[L.j], c_ed.d2,
                                   &ws.zpre[L.j][ED_WIDE_GROUP * L.g]);
 }
@@ -264,7 +247,7 @@ __global__ void __launch_bounds__(64) k_ed_btab_init(EdBTab* __restrict__ out) {
   ed_base_point(P);
   if (EdBCfgT::shift(u) > 0) ed_dbl_n(P, P, EdBCfgT::shift(u));
   ge_p3 pts[8];
-  ed_small_mul(pts[0], P, 8 * grp + 1);
+  ed_small_mul(pts[0], P, 8 * grp + 1, c_ed.d2);
   ge_cached c;
   ge_p3_to_cached(c, P, c_ed.d2);
   ge_p1p1 t;
@@ -277,28 +260,16 @@ __global__ void __launch_bounds__(64) k_ed_btab_init(EdBTab* __restrict__ out) {
   for (int k = 0; k < 8; ++k) out->t[u][8 * grp + k] = row[k];
 }
 
-// Wide B rows (radix 2^12, row u = multiples of 2^{12u} B), built once per context: one lane per
-// (row, group of 8 multiples)
+// Wide B rows (radix 2^ED_WIDE_BW, row u = multiples of 2^{ED_WIDE_BW u} B), built once per
+// context: one lane per (row, group of 8 multiples)
 __global__ void __launch_bounds__(64) k_ed_bwide_init(EdBWideTab* __restrict__ out) {
   constexpr uint32_t G = EdWideCfg::kBMult / 8;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t u = g / G, grp = g % G;
   if (u >= (uint32_t)EdWideCfg::kBDigits) return;
-  ge_p3 P;
-  ed_base_point(P);
-  if (u > 0) ed_dbl_n(P, P, ED_WIDE_BW * (int)u);
-  ge_p3 pts[8];
-  ed_small_mul(pts[0], P, 8 * grp + 1);
-  ge_cached c;
-  ge_p3_to_cached(c, P, c_ed.d2);
-  ge_p1p1 t;
-  for (int k = 1; k < 8; ++k) {
-    ge_add_cached(t, pts[k - 1], c);
-    ge_p1p1_to_p3(pts[k], t);
-  }
-  ge_niels row[8];
-  ed_niels_batch8(row, pts, c_ed.d2);
-  for (int k = 0; k < 8; ++k) out->t[u][8 * grp + k] = row[k];
+  ge_p3 B;
+  ed_base_point(B);
+  ed_bwide_group(&out->t[u][8 * grp], B, (int)u, (int)grp, c_ed.d2);
 }
 
 __device__ __forceinline__ void ld_niels(ge_niels& n, const ge_niels* src) {

@@ -1,3 +1,4 @@
+#include <vector>
 // Host build of the device lane code (corda_amd/csrc/*.h) with FE_BOUNDS_CHECK on, so the
 // exact arithmetic the HIP kernels run is checked on the CPU against the oracle and every
 // limb bound assumed by fe25519.h is asserted. Test infrastructure only.
@@ -479,10 +480,15 @@ extern "C" int t_ed_verify_wb_signed(const uint32_t* aw, const uint32_t* sw, con
 
 // ---------------------------------------------------------------- wide tables (hot keys)
 // k_ed_wide_chain / k_ed_wide_tab / k_ed_bwide_init / k_ed_ladder_wide's arithmetic, bounds-checked.
+// The constant B table is 62.9 MB (radix 2^16): the host builds, with the device lane's code
+// (ed_bwide_group), only the groups of 8 multiples an item's digits touch.
 static EdBWideTab* g_TBW = nullptr;
+static std::vector<bool> g_TBW_built;
+static ge_p3 g_TBW_base[EdWideCfg::kBDigits];  // 2^{16u} B
 static void tbw_init() {
   if (g_TBW) return;
   g_TBW = new EdBWideTab;
+  g_TBW_built.assign(EdWideCfg::kBDigits * (EdWideCfg::kBMult / 8), false);
   ge_p3 B;
   fe x, y, two_inv, t;
   fe_sub(x, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
@@ -497,7 +503,18 @@ static void tbw_init() {
   ge_p3 P = B;
   for (int u = 0; u < EdWideCfg::kBDigits; ++u) {
     if (u > 0) ed_dbl_n(P, P, ED_WIDE_BW);
-    ed_row_multiples<EdWideCfg::kBMult>(g_TBW->t[u], P, g_C.d2);
+    g_TBW_base[u] = P;
+  }
+}
+static void tbw_touch(const uint32_t* es) {
+  for (int u = 0; u < EdWideCfg::kBDigits; ++u) {
+    const int d = sc_digit_h(es, u), a = d < 0 ? -d : d;
+    if (a == 0) continue;
+    const int grp = (a - 1) / 8;
+    const size_t k = (size_t)u * (EdWideCfg::kBMult / 8) + grp;
+    if (g_TBW_built[k]) continue;
+    ed_bwide_group(&g_TBW->t[u][8 * grp], g_TBW_base[u], 0, grp, g_C.d2);
+    g_TBW_built[k] = true;
   }
 }
 
@@ -577,6 +594,7 @@ extern "C" int t_ed_verify_wide(const uint32_t* aw, const uint32_t* sw, const ui
   uint32_t eh[EdWideCfg::kPackedWords], es[EdWideCfg::kBPackedWords];
   sc_recode_w<ED_WIDE_W>(eh, EdWideCfg::kPackedWords, h);
   sc_recode_w16<ED_WIDE_BW>(es, EdWideCfg::kBPackedWords, sr);
+  tbw_touch(es);
   ge_p2 R;
 #ifdef FE_OP_COUNT
   g_fe_nmul = g_fe_nsq = 0;
@@ -601,14 +619,20 @@ static int ecdsa_wide_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
   kinit();
   const EcConsts& K = g_K[C];
   static EcGWideTab* TG[2] = {nullptr, nullptr};
+  static std::vector<bool> tg_built[2];
+  static Jac tg_base[2][EC_WIDE_GDIGITS];  // 2^{16u} G
   static EcWideTab* TQ = new EcWideTab;
   static EcWideScratch* WS = new EcWideScratch;
   static EcRowScratch* S = new EcRowScratch;
-  if (!TG[C]) {  // the device table build, lane by lane
+  constexpr int GG = EC_WIDE_GMULT / EC_MULT;
+  if (!TG[C]) {  // the device lane's code (ec_gwide_group_from), for the groups the digits touch
     TG[C] = new EcGWideTab;
-    constexpr int G = EC_WIDE_GMULT / EC_MULT;
-    for (int l = 0; l < EC_WIDE_GDIGITS * G; ++l)
-      ec_gwide_group<C>(&TG[C]->t[l / G][(l % G) * EC_MULT], l / G, l % G, *S, K);
+    tg_built[C].assign(EC_WIDE_GDIGITS * GG, false);
+    Jac P = {K.gx, K.gy, K.one_p};
+    for (int u = 0; u < EC_WIDE_GDIGITS; ++u) {
+      if (u > 0) jac_dbl_n<C>(P, P, EC_WIDE_GW);
+      tg_base[C][u] = P;
+    }
   }
   f29 xm, ym;
   uint32_t st = ec_key_decode_bytes<C>(xm, ym, arena, lr, key_off, key_len, fmt, K);
@@ -649,6 +673,17 @@ static int ecdsa_wide_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
   st = ecdsa_prep<C>(ws, arena, lr, sig_off, sig_len, arena, lr, msg_off, msg_len);
   if (st) return (int)st;
   ecdsa_batch_inv<C, 1>(&ws, 1, 1u, K);
+  {
+    uint32_t dg[EC_WIDE_GPACKED];
+    ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS>(dg, ws.a);
+    for (int u = 0; u < EC_WIDE_GDIGITS; ++u) {
+      const int d = ec_digit10(dg, u), a = d < 0 ? -d : d;
+      if (a == 0 || tg_built[C][u * GG + (a - 1) / EC_MULT]) continue;
+      const int g = (a - 1) / EC_MULT;
+      ec_gwide_group_from<C>(&TG[C]->t[u][g * EC_MULT], tg_base[C][u], g, *S, K);
+      tg_built[C][u * GG + g] = true;
+    }
+  }
 #ifdef FE_OP_COUNT
   g_m29_nmul[C][0] = g_m29_nmul[C][1] = 0;
 #endif

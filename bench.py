@@ -72,7 +72,8 @@ EC_WIDE_MUL = {"secp256r1": 531, "secp256k1": 531}  # k_ec_ladder_wide: 32 + 17 
 KEY_FULL_MIN_USES, KEY_WIDE_MAX = 32, 8192
 KEY_WIDE_MIN_USES = {4: int(os.environ.get("CG_WIDE_MIN_USES_ED", 1536)), 3: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512)),
                      2: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512))}
-EC_INV_MUL_16 = {"secp256r1": 536, "secp256k1": 563}
+EC_INV_K = 8  # items per k_ec_inv lane (corda_amd/csrc/ecdsa_rows.h)
+EC_INV_MUL_K = {"secp256r1": 480, "secp256k1": 507}  # products of one lane: prefix, inversion, unwinding
 EC_MAC_PER_MUL_P = {"secp256r1": 144, "secp256k1": 162}
 EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
@@ -385,7 +386,7 @@ def bench_ecdsa(a, eng, dev, stream, wl, threads):
     return {"value": round(b.n / el, 1), "unit": "sigs/s", "items": b.n, "keys": len(b.keys),
             "ms_per_step": round(el * 1e3, 3), "roofline": ec, "stages": stage_summary(stg, 4),
             "verdicts": check_verdicts(st, expected_verdicts(labels, schemes)),
-            "work_per_item_mac32": {c: EC_LADDER_MUL[c] * EC_MAC_PER_MUL_P[c] + EC_INV_MUL_16[c] * EC_MAC_PER_MUL_N[c] / 16
+            "work_per_item_mac32": {c: EC_LADDER_MUL[c] * EC_MAC_PER_MUL_P[c] + EC_INV_MUL_K[c] * EC_MAC_PER_MUL_N[c] / EC_INV_K
                                     for c in EC_LADDER_MUL}}
 
 

@@ -253,6 +253,12 @@ CG_HD uint32_t ecdsa_prep(EcItemWs& ws, const uint8_t* arena, uint64_t lr, uint6
   return 0;
 }
 
+// Items per lane of k_ec_inv, one inversion each (A/B 8 vs 16 vs 32 on MI355X: profiles/r02/sha_v2;
+// 16 left ~1 wave per SIMD on a 1M-item curve range)
+#ifndef EC_INV_K
+#define EC_INV_K 8
+#endif
+
 // Stage 2 (per group): w = s^-1 by one shared inversion (Montgomery's trick); u1 = e w,
 // u2 = r w as canonical plain words. `sel` marks the pending items of this curve among
 // ws[0..cnt).

@@ -65,8 +65,10 @@ CG_HD uint64_t cg_maj64(uint64_t a, uint64_t b, uint64_t c) {
   return (m & c) | (~m & b);
 }
 
-CG_HD uint64_t cg_k512(int i) {
-  const uint64_t K[80] = {
+// Round constants in constant memory: the rounds run in a rolled loop of 16 unrolled rounds
+// (sha512_compress), so the constant of round r + j is a scalar load at a uniform index.
+#if defined(__HIP_DEVICE_COMPILE__)
+static __constant__ const uint64_t CG_K512[80] = {
       0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
       0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
       0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
@@ -87,8 +89,30 @@ CG_HD uint64_t cg_k512(int i) {
       0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
       0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
       0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
-  return K[i];
-}
+#else
+static const uint64_t CG_K512[80] = {
+      0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+      0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+      0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+      0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+      0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+      0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+      0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+      0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+      0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+      0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+      0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+      0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+      0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+      0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+      0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+      0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+      0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+      0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+      0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+      0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+#endif
+CG_HD uint64_t cg_k512(int i) { return CG_K512[i]; }
 
 CG_HD void sha512_init(uint64_t s[8]) {
   s[0] = 0x6a09e667f3bcc908ULL;
@@ -101,33 +125,58 @@ CG_HD void sha512_init(uint64_t s[8]) {
   s[7] = 0x5be0cd19137e2179ULL;
 }
 
-// The 80 rounds fully unrolled: K folds into immediates and the a..h / w[i & 15] rotation into
-// register renaming (left rolled, the compiler indexed w through M0 and copied a..h every round).
+// One SHA-512 round on the working variables named in rotated order (a..h of round i are
+// v[(8 - i) & 7] .. : the caller passes them rotated, so no register moves are needed).
+#define CG_SHA512_ROUND(a, b, c, d, e, f, g, h, k, wi)                                                   \
+  {                                                                                                   \
+    const uint64_t t1 = h + (cg_rotr64(e, 14) ^ cg_rotr64(e, 18) ^ cg_rotr64(e, 41)) + cg_ch64(e, f, g) + \
+                        (k) + (wi);                                                                   \
+    const uint64_t t2 = (cg_rotr64(a, 28) ^ cg_rotr64(a, 34) ^ cg_rotr64(a, 39)) + cg_maj64(a, b, c);   \
+    d += t1;                                                                                          \
+    h = t1 + t2;                                                                                      \
+  }
+
+// 8 rounds: after them the variables are back in their own roles
+#define CG_SHA512_8ROUNDS(i0, W)                                   \
+  CG_SHA512_ROUND(a, b, c, d, e, f, g, h, cg_k512((i0) + 0), W(0)) \
+  CG_SHA512_ROUND(h, a, b, c, d, e, f, g, cg_k512((i0) + 1), W(1)) \
+  CG_SHA512_ROUND(g, h, a, b, c, d, e, f, cg_k512((i0) + 2), W(2)) \
+  CG_SHA512_ROUND(f, g, h, a, b, c, d, e, cg_k512((i0) + 3), W(3)) \
+  CG_SHA512_ROUND(e, f, g, h, a, b, c, d, cg_k512((i0) + 4), W(4)) \
+  CG_SHA512_ROUND(d, e, f, g, h, a, b, c, cg_k512((i0) + 5), W(5)) \
+  CG_SHA512_ROUND(c, d, e, f, g, h, a, b, cg_k512((i0) + 6), W(6)) \
+  CG_SHA512_ROUND(b, c, d, e, f, g, h, a, cg_k512((i0) + 7), W(7))
+
+// message schedule word i = r + j (r a multiple of 16, j < 16) into the circular buffer slot j
+CG_HD uint64_t sha512_sched(uint64_t w[16], int j) {
+  const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+  const uint64_t s0 = cg_rotr64(w15, 1) ^ cg_rotr64(w15, 8) ^ (w15 >> 7);
+  const uint64_t s1 = cg_rotr64(w2, 19) ^ cg_rotr64(w2, 61) ^ (w2 >> 6);
+  w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
+  return w[j];
+}
+
+// Rounds 0..15 straight, then 16..79 as a rolled loop of 16 unrolled rounds: the working
+// variables rotate by renaming inside the body and come back to their roles every 8 rounds, the
+// schedule's circular buffer is indexed statically, the constants are scalar loads. (Fully
+// unrolled, 80 rounds per block spilled and thrashed the instruction cache; rolled round by round,
+// every round paid 8 register moves.)
 CG_HD void sha512_compress(uint64_t s[8], uint64_t w[16]) {
   uint64_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
-#pragma unroll
-  for (int i = 0; i < 80; ++i) {
-    uint64_t wi;
-    if (i < 16) {
-      wi = w[i];
-    } else {
-      const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      const uint64_t s0 = cg_rotr64(w15, 1) ^ cg_rotr64(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = cg_rotr64(w2, 19) ^ cg_rotr64(w2, 61) ^ (w2 >> 6);
-      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-      w[i & 15] = wi;
-    }
-    const uint64_t t1 = h + (cg_rotr64(e, 14) ^ cg_rotr64(e, 18) ^ cg_rotr64(e, 41)) + cg_ch64(e, f, g) +
-                        cg_k512(i) + wi;
-    const uint64_t t2 = (cg_rotr64(a, 28) ^ cg_rotr64(a, 34) ^ cg_rotr64(a, 39)) + cg_maj64(a, b, c);
-    h = g;
-    g = f;
-    f = e;
-    e = d + t1;
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + t2;
+#define CG_W0(j) w[(j)]
+#define CG_W1(j) w[8 + (j)]
+  CG_SHA512_8ROUNDS(0, CG_W0)
+  CG_SHA512_8ROUNDS(8, CG_W1)
+#undef CG_W0
+#undef CG_W1
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) {
+#define CG_S0(j) sha512_sched(w, (j))
+#define CG_S1(j) sha512_sched(w, 8 + (j))
+    CG_SHA512_8ROUNDS(r, CG_S0)
+    CG_SHA512_8ROUNDS(r + 8, CG_S1)
+#undef CG_S0
+#undef CG_S1
   }
   s[0] += a;
   s[1] += b;
@@ -139,58 +188,85 @@ CG_HD void sha512_compress(uint64_t s[8], uint64_t w[16]) {
   s[7] += h;
 }
 
-// SHA-512(prefix64 || msg) where prefix64 is 16 little-endian words (e.g. R || Abyte).
-// Output: the 64 digest bytes as 16 little-endian words (ready for sc_reduce512).
-// Big-endian 64-bit word of the message at byte offset `pos` (whole word inside the message)
-CG_HD uint64_t cg_msg_dword_be(const uint8_t* arena, uint64_t len_rounded, uint64_t off) {
-  const uint32_t hi = CG_BSWAP32(cg_ld_bytes4(arena, len_rounded, off));
-  const uint32_t lo = CG_BSWAP32(cg_ld_bytes4(arena, len_rounded, off + 4));
-  return ((uint64_t)hi << 32) | lo;
+// Four aligned little-endian dwords at arena[addr, addr + 16) (addr a multiple of 4), zero past
+// `len_rounded`: one 16-byte load when the whole span is inside (gfx950 loads need only dword
+// alignment), else dword by dword.
+CG_HD void cg_ld_dwords4(uint32_t out[4], const uint8_t* arena, uint64_t len_rounded, uint64_t addr) {
+  if (addr + 16 <= len_rounded) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+    const u32x4_a4 v = *(const u32x4_a4*)(arena + addr);
+    out[0] = v.x;
+    out[1] = v.y;
+    out[2] = v.z;
+    out[3] = v.w;
+#else
+    for (int q = 0; q < 4; ++q) out[q] = cg_ld32(arena + addr + 4 * q);
+#endif
+  } else {
+    for (int q = 0; q < 4; ++q) out[q] = addr + 4 * q < len_rounded ? cg_ld32(arena + addr + 4 * q) : 0u;
+  }
 }
 
+// SHA-512(prefix64 || msg) where prefix64 is 16 little-endian words (e.g. R || Abyte).
+// Output: the 64 digest bytes as 16 little-endian words (ready for sc_reduce512).
+// The message is read as aligned 16-byte chunks (33 dwords per 128-byte block) and realigned with
+// one funnel shift per word, instead of two dword loads per word (round 1: 136 loads per
+// 270-byte message, the challenge kernel's memory-wait share was ~0.3).
 CG_HD void sha512_prefix64_msg(uint32_t out[16], const uint32_t prefix[16], const uint8_t* arena,
                                uint64_t len_rounded, uint64_t msg_off, uint64_t msg_len) {
   uint64_t s[8];
   sha512_init(s);
   const uint64_t n = 64 + msg_len;
   const uint64_t nblocks = (n + 17 + 127) >> 7;
-  // blocks made of prefix / message bytes only (no padding): straight loads, no per-word
-  // position logic; block 0 is the prefix and the first 64 message bytes
-  const uint64_t nfull = n >> 7;
-  for (uint64_t blk = 0; blk < nfull; ++blk) {
-    uint64_t w[16];
+  const uint64_t base = msg_off & ~(uint64_t)3;
+  const uint32_t sh8 = (uint32_t)(msg_off & 3) * 8u;
+  for (uint64_t blk = 0; blk < nblocks; ++blk) {
+    // message words k0 .. k0 + 31 of this block (k0 = 32 blk - 16; block 0 starts with the prefix)
+    const int64_t k0 = (int64_t)blk * 32 - 16;
+    uint32_t W[36];  // aligned dwords k0 .. k0 + 35
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      w[j] = blk == 0 ? ((uint64_t)CG_BSWAP32(prefix[2 * j]) << 32) | CG_BSWAP32(prefix[2 * j + 1])
-                      : cg_msg_dword_be(arena, len_rounded, msg_off + blk * 128 - 64 + 8 * j);
-#pragma unroll
-    for (int j = 8; j < 16; ++j) w[j] = cg_msg_dword_be(arena, len_rounded, msg_off + blk * 128 - 64 + 8 * j);
-    sha512_compress(s, w);
-  }
-  for (uint64_t blk = nfull; blk < nblocks; ++blk) {
-    uint64_t w[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint64_t pos = blk * 128 + (uint64_t)j * 8;  // stream byte position
-      uint32_t hi, lo;
-      if (pos < 64) {
-        hi = CG_BSWAP32(prefix[pos >> 2]);
-        lo = CG_BSWAP32(prefix[(pos >> 2) + 1]);
+    for (int t = 0; t < 9; ++t) {
+      if (blk == 0 && t < 4) {
+        W[4 * t] = W[4 * t + 1] = W[4 * t + 2] = W[4 * t + 3] = 0u;
       } else {
-        hi = cg_msg_word_be(arena, len_rounded, msg_off, msg_len, pos - 64);
-        lo = cg_msg_word_be(arena, len_rounded, msg_off, msg_len, pos - 60);
+        cg_ld_dwords4(&W[4 * t], arena, len_rounded, base + (uint64_t)(k0 + 4 * t) * 4);
       }
-      // a block's padding words beyond the message read as 0 (or 0x80..); the final 16 bytes
-      // of the last block carry the bit length
-      if (blk == nblocks - 1 && j == 15) {
-        hi = (uint32_t)((n * 8) >> 32);
-        lo = (uint32_t)(n * 8);
-      } else if (blk == nblocks - 1 && j == 14) {
-        hi = 0;
-        lo = 0;
-      }
-      w[j] = ((uint64_t)hi << 32) | lo;
     }
+    const bool last = blk + 1 == nblocks;
+    uint32_t be[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const int64_t k = k0 + j;  // message word (negative: prefix)
+      uint32_t w;
+      if (k < 0) {
+        w = prefix[j];
+      } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint32_t raw = __builtin_amdgcn_alignbit(W[j + 1], W[j], sh8);
+#else
+        const uint32_t raw = (uint32_t)((((uint64_t)W[j + 1] << 32) | W[j]) >> sh8);
+#endif
+        const int64_t rem = (int64_t)msg_len - 4 * k;  // message bytes in this word
+        if (rem >= 4) {
+          w = raw;
+        } else if (rem > 0) {
+          w = (raw & (0xffffffffu >> (32u - 8u * (uint32_t)rem))) | (0x80u << (8u * (uint32_t)rem));
+        } else {
+          w = rem == 0 ? 0x80u : 0u;
+        }
+      }
+      be[j] = CG_BSWAP32(w);
+    }
+    if (last) {  // the 128-bit big-endian bit length ends the last block
+      be[28] = 0;
+      be[29] = 0;
+      be[30] = (uint32_t)((n * 8) >> 32);
+      be[31] = (uint32_t)(n * 8);
+    }
+    uint64_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = ((uint64_t)be[2 * j] << 32) | be[2 * j + 1];
     sha512_compress(s, w);
   }
 #pragma unroll
@@ -230,8 +306,8 @@ CG_HD void sha512_arena(uint64_t s_out[8], const uint8_t* arena, uint64_t len_ro
 // ----------------------------------------------------------------- SHA-256
 CG_HD uint32_t cg_rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
-CG_HD uint32_t cg_k256(int i) {
-  const uint32_t K[64] = {
+#if defined(__HIP_DEVICE_COMPILE__)
+static __constant__ const uint32_t CG_K256[64] = {
       0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
       0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
       0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
@@ -240,8 +316,18 @@ CG_HD uint32_t cg_k256(int i) {
       0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
       0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
       0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
-  return K[i];
-}
+#else
+static const uint32_t CG_K256[64] = {
+      0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+      0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+      0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+      0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+      0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+      0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+      0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+      0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+#endif
+CG_HD uint32_t cg_k256(int i) { return CG_K256[i]; }
 
 CG_HD void sha256_init(uint32_t s[8]) {
   s[0] = 0x6a09e667;
@@ -254,31 +340,49 @@ CG_HD void sha256_init(uint32_t s[8]) {
   s[7] = 0x5be0cd19;
 }
 
+#define CG_SHA256_ROUND(a, b, c, d, e, f, g, h, k, wi)                                                    \
+  {                                                                                                    \
+    const uint32_t t1 =                                                                                \
+        h + (cg_rotr32(e, 6) ^ cg_rotr32(e, 11) ^ cg_rotr32(e, 25)) + ((e & f) ^ (~e & g)) + (k) + (wi); \
+    const uint32_t t2 = (cg_rotr32(a, 2) ^ cg_rotr32(a, 13) ^ cg_rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c)); \
+    d += t1;                                                                                           \
+    h = t1 + t2;                                                                                       \
+  }
+#define CG_SHA256_8ROUNDS(i0, W)                                   \
+  CG_SHA256_ROUND(a, b, c, d, e, f, g, h, cg_k256((i0) + 0), W(0)) \
+  CG_SHA256_ROUND(h, a, b, c, d, e, f, g, cg_k256((i0) + 1), W(1)) \
+  CG_SHA256_ROUND(g, h, a, b, c, d, e, f, cg_k256((i0) + 2), W(2)) \
+  CG_SHA256_ROUND(f, g, h, a, b, c, d, e, cg_k256((i0) + 3), W(3)) \
+  CG_SHA256_ROUND(e, f, g, h, a, b, c, d, cg_k256((i0) + 4), W(4)) \
+  CG_SHA256_ROUND(d, e, f, g, h, a, b, c, cg_k256((i0) + 5), W(5)) \
+  CG_SHA256_ROUND(c, d, e, f, g, h, a, b, cg_k256((i0) + 6), W(6)) \
+  CG_SHA256_ROUND(b, c, d, e, f, g, h, a, cg_k256((i0) + 7), W(7))
+
+CG_HD uint32_t sha256_sched(uint32_t w[16], int j) {
+  const uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+  const uint32_t s0 = cg_rotr32(w15, 7) ^ cg_rotr32(w15, 18) ^ (w15 >> 3);
+  const uint32_t s1 = cg_rotr32(w2, 17) ^ cg_rotr32(w2, 19) ^ (w2 >> 10);
+  w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
+  return w[j];
+}
+
+// Same structure as sha512_compress: rounds 0..15 straight, 16..63 as a rolled loop of 16.
 CG_HD void sha256_compress(uint32_t s[8], uint32_t w[16]) {
   uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
-#pragma unroll
-  for (int i = 0; i < 64; ++i) {
-    uint32_t wi;
-    if (i < 16) {
-      wi = w[i];
-    } else {
-      const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      const uint32_t s0 = cg_rotr32(w15, 7) ^ cg_rotr32(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = cg_rotr32(w2, 17) ^ cg_rotr32(w2, 19) ^ (w2 >> 10);
-      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-      w[i & 15] = wi;
-    }
-    const uint32_t t1 =
-        h + (cg_rotr32(e, 6) ^ cg_rotr32(e, 11) ^ cg_rotr32(e, 25)) + ((e & f) ^ (~e & g)) + cg_k256(i) + wi;
-    const uint32_t t2 = (cg_rotr32(a, 2) ^ cg_rotr32(a, 13) ^ cg_rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
-    h = g;
-    g = f;
-    f = e;
-    e = d + t1;
-    d = c;
-    c = b;
-    b = a;
-    a = t1 + t2;
+#define CG_W0(j) w[(j)]
+#define CG_W1(j) w[8 + (j)]
+  CG_SHA256_8ROUNDS(0, CG_W0)
+  CG_SHA256_8ROUNDS(8, CG_W1)
+#undef CG_W0
+#undef CG_W1
+#pragma unroll 1
+  for (int r = 16; r < 64; r += 16) {
+#define CG_S0(j) sha256_sched(w, (j))
+#define CG_S1(j) sha256_sched(w, 8 + (j))
+    CG_SHA256_8ROUNDS(r, CG_S0)
+    CG_SHA256_8ROUNDS(r + 8, CG_S1)
+#undef CG_S0
+#undef CG_S1
   }
   s[0] += a;
   s[1] += b;
@@ -302,10 +406,20 @@ CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t l
   const uint64_t nblocks = (n + 9 + 63) >> 6;
   // blocks made of message bytes only: straight loads, no per-word position logic
   const uint64_t nfull = len >> 6;
+  const uint64_t base = off & ~(uint64_t)3;
+  const uint32_t sh8 = (uint32_t)(off & 3) * 8u;
   for (uint64_t blk = 0; blk < nfull; ++blk) {
-    uint32_t w[16];
+    uint32_t W[20], w[16];  // aligned dwords of the block (+1 for the realignment), 16-byte loads
 #pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = CG_BSWAP32(cg_ld_bytes4(arena, len_rounded, off + blk * 64 + 4 * j));
+    for (int t = 0; t < 5; ++t) cg_ld_dwords4(&W[4 * t], arena, len_rounded, base + blk * 64 + 16 * t);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      w[j] = CG_BSWAP32(__builtin_amdgcn_alignbit(W[j + 1], W[j], sh8));
+#else
+      w[j] = CG_BSWAP32((uint32_t)((((uint64_t)W[j + 1] << 32) | W[j]) >> sh8));
+#endif
+    }
     sha256_compress(s, w);
   }
   for (uint64_t blk = nfull; blk < nblocks; ++blk) {

@@ -4,7 +4,7 @@
 //   k_ec_keyprep_chain one lane per ECDSA key: row bases 2^{24j} Q      prep waits for the decode,
 //   k_ec_keyprep_tab   one lane per (key, row): 32 affine multiples     the ladder for the tab)
 //   k_ec_prep          one lane per item: DER, range checks, SHA-256, e mod n
-//   k_ec_inv           16 items per lane: one shared inversion of s mod n -> u1, u2
+//   k_ec_inv           EC_INV_K items per lane: one shared inversion of s mod n -> u1, u2
 //   k_ec_ladder        one lane per item: u1 G (radix-2^10 constant table) + u2 Q (key rows;
 //                      row 0 and 252 doublings for a key with few items, keyws.h),
 //                      BC's inversion-free x(R) == r check
@@ -16,7 +16,6 @@ namespace cg {
 
 __constant__ EcConsts c_ec[2];  // [CG_CURVE_K1], [CG_CURVE_R1]
 
-#define EC_INV_K 16
 
 template <int C>
 __device__ __forceinline__ uint8_t ec_scheme() {

@@ -327,12 +327,12 @@ static int ecdsa_count(const uint8_t* arena, uint64_t lr, uint64_t key_off, uint
     g_m29_nmul[C][0] = g_m29_nmul[C][1] = 0;
   };
   g_m29_nmul[C][0] = g_m29_nmul[C][1] = 0;
-  EcItemWs ws[16];
+  EcItemWs ws[EC_INV_K];
   st = ecdsa_prep<C>(ws[0], arena, lr, sig_off, sig_len, arena, lr, msg_off, msg_len);
   snap(out);
   if (st) return (int)st;
-  for (int k = 1; k < 16; ++k) ws[k] = ws[0];
-  ecdsa_batch_inv<C, 16>(ws, 16, 0xffffu, K);
+  for (int k = 1; k < EC_INV_K; ++k) ws[k] = ws[0];
+  ecdsa_batch_inv<C, EC_INV_K>(ws, EC_INV_K, (1u << EC_INV_K) - 1u, K);
   snap(out + 2);
   st = ecdsa_ladder_check<C>(ws[0].a, ws[0].b, ws[0].r, *TG, *TQ, K);
   snap(out + 4);

@@ -243,7 +243,7 @@ def test_executed_work_constants_ecdsa():
                                      int(it["sig_off"]), int(it["sig_len"]), int(it["msg_off"]), int(it["msg_len"]),
                                      ptr(out)) == 0
             assert int(out[5]) == 0 and int(out[2]) == 0 and int(out[0]) == 0 and int(out[1]) == 0, (name, out)
-            assert int(out[3]) == bench.EC_INV_MUL_16[name], (name, out)
+            assert int(out[3]) == bench.EC_INV_MUL_K[name], (name, out)
             lad.append(int(out[4]))
         # the wave's schedule: a mixed addition is skipped only when all 64 lanes' digits are zero,
         # so a wave issues the per-item maximum over random items (the mean is ~1% lower)

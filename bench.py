@@ -50,7 +50,7 @@ MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # (tests/native/host_kernels.cpp; pinned by tests/test_host_kernels.py::test_executed_work_*).
 # Ed25519 (field multiplies, squarings) in the radix-2^25.5 representation (fe25519.h):
 ED_VERIFY_FE = (500, 24)   # k_ed_ladder_pf: 43 + 26 mixed additions + 6 doublings
-ED_WIDE_FE = (335, 0)      # k_ed_ladder_wide: 32 + 16 mixed additions, no doublings (keys with wide tables)
+ED_WIDE_FE = (307, 0)      # k_ed_ladder_wide: 32 + 12 mixed additions, no doublings (keys with wide tables)
 ED_WIDE_BUILD_FE = (64871, 11296)  # one key's wide table: 248-doubling chain, 32 rows x 4 groups of 32 entries, one inversion per row
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
@@ -67,7 +67,7 @@ MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
 # its addition, but the wave issues it for the other 63 lanes, so the full schedule is what the
 # SIMD executes (per-item mean 1% lower).
 EC_LADDER_MUL = {"secp256r1": 895, "secp256k1": 877}
-EC_WIDE_MUL = {"secp256r1": 531, "secp256k1": 531}  # k_ec_ladder_wide: 32 + 17 mixed additions + x-check
+EC_WIDE_MUL = {"secp256r1": 476, "secp256k1": 476}  # k_ec_ladder_wide: 32 + 12 mixed additions + x-check
 # table modes (corda_amd/csrc/keyws.h): full tables from 32 items per key, wide from 384
 KEY_FULL_MIN_USES, KEY_WIDE_MAX = 32, 8192
 KEY_WIDE_MIN_USES = {4: int(os.environ.get("CG_WIDE_MIN_USES_ED", 1536)), 3: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512)),

@@ -414,7 +414,13 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
   if (e == hipSuccess) e = cg::upload_constants();
   if (e == hipSuccess) e = c->btab.ensure(cg::btab_bytes());
-  if (e == hipSuccess) e = cg::init_btab(c->btab.p, c->stream);
+  if (e == hipSuccess) {  // the constant tables (6.6 GB, built once per context) over a temporary scratch
+    DevBuf scratch;
+    e = scratch.ensure(cg::btab_scratch_bytes());
+    if (e == hipSuccess) e = cg::init_btab(c->btab.p, scratch.p, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    scratch.release();
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     const int rc = hip_fail(e, "side streams / upload_constants / base-point tables");

@@ -480,27 +480,32 @@ CG_HD void ec_g_rows_init(EcRowTab& T, EcRowScratch& s, const EcConsts& K) {
 // radix-2^8 digit of u2: row j holds the affine multiples 1..128 of 2^{8j} Q. The top digit
 // (bits 248..255 plus the carry) is left in [0, 256] instead of carrying into a 33rd digit, so
 // row 31 also holds the multiples 129..256, stored as a 33rd row of the table (304 128 B). G
-// gets one row per signed radix-2^16 digit of u1 over a constant table built once per context
-// (16 rows x 32768 multiples of 2^{16u} G, plus a 17th row for the recoding carry out of bit 255,
-// whose digit is 0 or 1: 40 MB per curve, MALL-resident). R = one entry per row: 32 + 17 mixed
-// additions, no doublings, against 69 additions + 18 doublings over the full tables (radix 2^12
-// for G took 32 + 22).
+// gets one row per signed radix-2^22 digit of u1 over a constant table built once per context
+// (12 rows x 2^21 multiples of 2^{22u} G, 1.8 GB per curve in HBM; the last digit carries the
+// recoding carry out of bit 255). R = one entry per row: 32 + 12 mixed additions, no doublings,
+// against 69 additions + 18 doublings over the full tables. The fixed-base radix is an HBM-for-work
+// trade: radix 2^12 / 2^16 / 2^20 / 2^22 took 22 / 17 / 13 / 12 G additions; the 2^22 table's
+// gathers come from HBM, not MALL, and are still hidden (headline A/B on one MI355X: 2^16 227M,
+// 2^20 238M, 2^22 246M sigs/s, profiles/r02/radix_v1).
 #define EC_WIDE_W 8
 #define EC_WIDE_DIGITS 32
 #define EC_WIDE_ROWS 33   // row 32 = multiples 129..256 of row 31's base
 #define EC_WIDE_MULT 128
 #define EC_WIDE_PACKED 16  // int16 digits (the top one reaches 256)
-#define EC_WIDE_GW 16
-#define EC_WIDE_GDIGITS 17  // 272 bits: the 17th digit is the carry out of bits 240..255
-#define EC_WIDE_GMULT 32768
-#define EC_WIDE_GPACKED 9  // int16 digits
-static_assert(EC_WIDE_GW <= 16 && EC_WIDE_GDIGITS * EC_WIDE_GW > 256, "G digits: int16, one digit past bit 255");
+#ifndef EC_WIDE_GW
+#define EC_WIDE_GW 22
+#endif
+#define EC_WIDE_GDIGITS ((257 + EC_WIDE_GW - 1) / EC_WIDE_GW)  // radix 2^16: 17, the last the carry out of bit 255
+#define EC_WIDE_GMULT (1 << (EC_WIDE_GW - 1))
+#define EC_WIDE_GBITS (EC_WIDE_GW <= 16 ? 16 : 32)  // digit slot: int16 or int32
+#define EC_WIDE_GPACKED ((EC_WIDE_GDIGITS * EC_WIDE_GBITS + 31) / 32)
+static_assert(EC_WIDE_GDIGITS * EC_WIDE_GW > 256, "G digits: room for the recoding carry out of bit 255");
 
 struct EcWideTab {
   EcAff t[EC_WIDE_ROWS][EC_WIDE_MULT];  // t[j][k-1] = k 2^{8j} Q; t[32][k-1] = (128 + k) 2^{248} Q
 };
 struct EcGWideTab {
-  EcAff t[EC_WIDE_GDIGITS][EC_WIDE_GMULT];  // t[u][k-1] = k 2^{16u} G
+  EcAff t[EC_WIDE_GDIGITS][EC_WIDE_GMULT];  // t[u][k-1] = k 2^{EC_WIDE_GW u} G
 };
 // Batch-inversion scratch of one wide row (the Jacobian X, Y wait in the output entries)
 struct EcWideScratch {
@@ -509,9 +514,9 @@ struct EcWideScratch {
 
 // Signed radix-2^W digits of a < 2^256 (D digits), packed as int16. TopUnsigned: the last digit
 // keeps the carry (in [0, 2^W]) instead of being recentred.
-template <int W, int D, bool TopUnsigned = false>
+template <int W, int D, bool TopUnsigned = false, int Bits = 16>
 CG_HD void ec_recode_wide(uint32_t* packed, const u256w& a) {
-  constexpr int per = 2;
+  constexpr int per = 32 / Bits;
   for (int w = 0; w < (D + per - 1) / per; ++w) packed[w] = 0;
   int carry = 0;
 #pragma unroll
@@ -529,8 +534,13 @@ CG_HD void ec_recode_wide(uint32_t* packed, const u256w& a) {
       carry = (e + (1 << (W - 1))) >> W;
       e -= carry << W;
     }
-    packed[t >> 1] |= ((uint32_t)(e & 0xffff)) << ((t & 1) * 16);
+    if (Bits == 16) packed[t >> 1] |= ((uint32_t)(e & 0xffff)) << ((t & 1) * 16);
+    else packed[t] = (uint32_t)e;
   }
+}
+template <int Bits>
+CG_HD int ec_digit_at(const uint32_t* packed, int t) {
+  return Bits == 16 ? (int)(int16_t)(uint16_t)(packed[t >> 1] >> ((t & 1) * 16)) : (int)packed[t];
 }
 
 // The affine multiples first + k step, k = 0..cnt-1, one field inversion for the whole run. The
@@ -633,7 +643,7 @@ template <int C, class TabG, class TabQ>
 CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG,
                                        const TabQ& TQ, const EcConsts& K) {
   uint32_t dg[EC_WIDE_GPACKED], dq[EC_WIDE_PACKED];
-  ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS>(dg, u1);
+  ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS, false, EC_WIDE_GBITS>(dg, u1);
   ec_recode_wide<EC_WIDE_W, EC_WIDE_DIGITS, true>(dq, u2);
   Jac R;
   jac_set_inf<C>(R, K);
@@ -651,7 +661,7 @@ CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u
   }
 #pragma unroll 1
   for (int u = 0; u < EC_WIDE_GDIGITS; ++u) {
-    const int a = ec_digit10(dg, u);  // int16 digits
+    const int a = ec_digit_at<EC_WIDE_GBITS>(dg, u);
     if (a != 0) {
       f29 x, y;
       ec_pick(x, y, TG.t[u], a < 0 ? -a : a);
@@ -663,7 +673,7 @@ CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u
 }
 
 // G wide row u, multiples 32 g + 1 .. 32 g + 32 (one lane of the per-context table build)
-// (the group from the row's base P = 2^{16u} G: the host tests build only the groups their digits touch)
+// (the group from the row's base P = 2^{EC_WIDE_GW u} G: the host tests build only the groups their digits touch)
 template <int C>
 CG_HD void ec_gwide_group_from(EcAff* out, const Jac& P, int g, EcRowScratch& s, const EcConsts& K) {
   const uint32_t m = 32u * (uint32_t)g + 1u;

@@ -294,6 +294,37 @@ CG_HD int sc_digit_h(const uint32_t* packed, int t) {
   return (int)(int16_t)(uint16_t)(packed[t >> 1] >> ((t & 1) * 16));
 }
 
+// signed radix-2^WB digits packed in Bits-bit slots (16: two per word, 32: one per word)
+template <int WB, int Bits>
+CG_HD void sc_recode_wb(uint32_t* packed, int nwords, const uint32_t a[8]) {
+  if (Bits == 16) {
+    sc_recode_w16<WB>(packed, nwords, a);
+    return;
+  }
+  constexpr int D = (253 + WB - 1) / WB + (253 % WB == 0 ? 1 : 0);
+  int carry = 0;
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+    const int bit = t * WB;
+    uint32_t v = 0;
+    if (bit < 256) {
+      const int wi = bit >> 5, sh = bit & 31;
+      uint64_t x = (uint64_t)a[wi] >> sh;
+      if (sh + WB > 32 && wi + 1 < 8) x |= (uint64_t)a[wi + 1] << (32 - sh);
+      v = (uint32_t)x & ((1u << WB) - 1);
+    }
+    int e = (int)v + carry;
+    carry = (e + (1 << (WB - 1))) >> WB;
+    e -= carry << WB;
+    packed[t] = (uint32_t)e;
+  }
+  for (int w = D; w < nwords; ++w) packed[w] = 0;
+}
+template <int Bits>
+CG_HD int sc_digit_at(const uint32_t* packed, int t) {
+  return Bits == 16 ? sc_digit_h(packed, t) : (int)packed[t];
+}
+
 // R' = h (-A) + S' B: A over the per-key W/K rows, B over the WB table; left projective.
 // `Pick(out, row, digit)` loads a signed niels entry (identity for 0) from either table.
 // Signed = true: entries are picked by |digit| and the sign goes through ge_madd_signed (the
@@ -399,33 +430,33 @@ CG_HD void ed_btab_wb_row(ge_niels* row, const ge_p3& B, int u, const fe& d2) {
 // ---------------------------------------------------------------- wide tables (hot keys)
 // A key with many items in the call (keyws.h KEY_WIDE_MIN_USES) gets one row per signed
 // radix-2^8 digit of h: row j holds the affine multiples 1..128 of 2^{8j} (-A) (32 rows,
-// 491 520 B). B gets one row per signed radix-2^16 digit of S' over a constant table built once
-// per context (row u holds 1..32768 times 2^{16u} B: 16 rows, 62.9 MB, MALL-resident). R' = sum of
-// one entry per row: 32 + 16 = 48 mixed additions and no doublings, against 69 additions + 6
-// doublings over the full tables. (Radix 2^12 for B, 5.4 MB, took 32 + 22 = 54; the B gathers
-// miss the 4 MB per-XCD L2 either way.)
+// 491 520 B). B gets one row per signed radix-2^22 digit of S' over a constant table built once
+// per context (row u holds 1..2^21 times 2^{22u} B: 12 rows, 3.0 GB in HBM). R' = sum of one entry
+// per row: 32 + 12 = 44 mixed additions and no doublings, against 69 additions + 6 doublings over
+// the full tables. (B radix 2^12 / 2^16 / 2^20 took 22 / 16 / 13 additions; the per-op LDS
+// prefetch hides the HBM gathers of the 3 GB table: ecdsa_rows.h has the A/B.)
 #define ED_WIDE_W 8
 #ifndef ED_WIDE_BW
-#define ED_WIDE_BW 16
+#define ED_WIDE_BW 22
 #endif
 struct EdWideCfg {
   static constexpr int kDigits = (253 + ED_WIDE_W - 1) / ED_WIDE_W;  // 32: h < 2^253 leaves the carry room
   static constexpr int kRows = kDigits;
   static constexpr int kMult = 1 << (ED_WIDE_W - 1);                 // 128
   static constexpr int kPackedWords = (kDigits + 3) / 4;             // int8 digits
-  static constexpr int kBDigits = (253 + ED_WIDE_BW - 1) / ED_WIDE_BW;  // 16
-  static constexpr int kBMult = 1 << (ED_WIDE_BW - 1);                // 32768 (|digit| <= 2^15)
-  static constexpr int kBPackedWords = (kBDigits + 1) / 2;            // int16 digits
-  static constexpr int kOps = kRows + kBDigits;                       // 48
+  static constexpr int kBDigits = (253 + ED_WIDE_BW - 1) / ED_WIDE_BW;  // 12 at radix 2^22
+  static constexpr int kBMult = 1 << (ED_WIDE_BW - 1);                // |digit| <= 2^(BW-1)
+  static constexpr int kBBits = ED_WIDE_BW <= 16 ? 16 : 32;           // B digit slot: int16 or int32
+  static constexpr int kBPackedWords = (kBDigits * kBBits + 31) / 32;
+  static constexpr int kOps = kRows + kBDigits;                       // 44 at radix 2^22
 };
 static_assert(253 % ED_WIDE_W != 0 && 253 % ED_WIDE_BW != 0, "the top digit keeps headroom for the carry");
-static_assert(ED_WIDE_BW <= 16, "B digits are packed as int16");
 
 struct EdWideTab {
   ge_niels t[EdWideCfg::kRows][EdWideCfg::kMult];  // t[j][k-1] = k 2^{8j} (-A)
 };
 struct EdBWideTab {
-  ge_niels t[EdWideCfg::kBDigits][EdWideCfg::kBMult];  // t[u][k-1] = k 2^{16u} B
+  ge_niels t[EdWideCfg::kBDigits][EdWideCfg::kBMult];  // t[u][k-1] = k 2^{ED_WIDE_BW u} B
 };
 
 // R' = h (-A) + S' B over the wide tables, digits already recoded (eh: radix 2^8, esb: radix
@@ -438,7 +469,7 @@ CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t*
   ge_p1p1 t;
   for (int o = 0; o < EdWideCfg::kOps; ++o) {
     const bool is_b = o >= EdWideCfg::kRows;
-    const int dg = is_b ? sc_digit_h(esb, o - EdWideCfg::kRows) : sc_digit_b(eh, o);
+    const int dg = is_b ? sc_digit_at<EdWideCfg::kBBits>(esb, o - EdWideCfg::kRows) : sc_digit_b(eh, o);
     const int dp = dg < 0 ? -dg : dg;
     ge_niels n;
     if (is_b) {

@@ -96,7 +96,8 @@ hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d
                          const WidePool* wide = nullptr);
 // Constant base-point row table: size and one-time initialisation (per context).
 size_t btab_bytes();
-hipError_t init_btab(void* d_btab, hipStream_t stream);
+size_t btab_scratch_bytes();  // temporary scratch of init_btab (free once it has run)
+hipError_t init_btab(void* d_btab, void* d_scratch, hipStream_t stream);
 // Bytes of per-item workspace (projective Ed25519 results awaiting the batched inversion).
 size_t item_ws_bytes(uint64_t n_items);
 // With `d_items`, each key's table is sized by the number of items that use it (keyws.h);

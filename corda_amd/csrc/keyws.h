@@ -297,11 +297,17 @@ hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d
 // [Ed25519 B wide rows (radix 2^12)][G wide rows k1][G wide rows r1][row scratch]
 #define EC_GTAB_LANES (EC_G_DIGITS * (EC_G_MULT / EC_MULT))  // one lane per (row, group of 32)
 #define EC_GWIDE_LANES (EC_WIDE_GDIGITS * (EC_WIDE_GMULT / EC_MULT))
-#define CONST_SCRATCH_LANES (EC_GWIDE_LANES > EC_GTAB_LANES ? EC_GWIDE_LANES : EC_GTAB_LANES)
+// the G-table builds run in batches of at most CONST_SCRATCH_LANES lanes over one scratch
+#define CONST_SCRATCH_MAX 131072
+#define CONST_SCRATCH_LANES                                                                        \
+  ((EC_GWIDE_LANES < CONST_SCRATCH_MAX ? EC_GWIDE_LANES : CONST_SCRATCH_MAX) > EC_GTAB_LANES       \
+       ? (EC_GWIDE_LANES < CONST_SCRATCH_MAX ? EC_GWIDE_LANES : CONST_SCRATCH_MAX)                 \
+       : EC_GTAB_LANES)
 static inline size_t const_tab_bytes() {
-  return sizeof(EdBTab) + 2 * sizeof(EcGTab) + sizeof(EdBWideTab) + 2 * sizeof(EcGWideTab) +
-         CONST_SCRATCH_LANES * sizeof(EcRowScratch);
+  return sizeof(EdBTab) + 2 * sizeof(EcGTab) + sizeof(EdBWideTab) + 2 * sizeof(EcGWideTab);
 }
+// scratch of the one-time builds: allocated by cg_open for init_btab only, then freed
+static inline size_t const_scratch_bytes() { return (size_t)CONST_SCRATCH_LANES * sizeof(EcRowScratch); }
 static inline const EcGTab* gtab(const void* d_btab, int curve) {
   return (const EcGTab*)((const uint8_t*)d_btab + sizeof(EdBTab)) + curve;
 }
@@ -311,9 +317,6 @@ static inline const EdBWideTab* bwide(const void* d_btab) {
 static inline const EcGWideTab* gwide(const void* d_btab, int curve) {
   return (const EcGWideTab*)((const uint8_t*)bwide(d_btab) + sizeof(EdBWideTab)) + curve;
 }
-static inline EcRowScratch* const_scratch(void* d_btab) {
-  return (EcRowScratch*)((uint8_t*)gwide(d_btab, 0) + 2 * sizeof(EcGWideTab));
-}
 
 // Intermediate per-item status codes (never returned to the caller)
 #define ED_PENDING 254u
@@ -321,7 +324,7 @@ static inline EcRowScratch* const_scratch(void* d_btab) {
 
 // Per-scheme halves (verify_ed.hip / verify_ec.hip)
 hipError_t ed_upload_constants();
-hipError_t ed_init_const(void* d_btab, hipStream_t stream);
+hipError_t ed_init_const(void* d_btab, void* d_scratch, hipStream_t stream);
 void ed_launch_key_abyte(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                          const KeyWs& w, hipStream_t stream);
 // decode -> chains (light), then the row tables (heavy)
@@ -341,7 +344,7 @@ void ed_launch_ladder_wide(const cg_item* d_items, uint64_t n_items, uint8_t* d_
 void ed_launch_finish(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
                       uint8_t* d_status, const ItemWs& iw, hipStream_t stream);
 hipError_t ec_upload_constants();
-hipError_t ec_init_const(void* d_btab, hipStream_t stream);
+hipError_t ec_init_const(void* d_btab, void* d_scratch, hipStream_t stream);
 // per curve: decode (records `decoded`: k_ec_prep needs the key status) -> chains; then the tables
 void ec_launch_keyprep_chains(int curve, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena,
                               uint64_t arena_len, const KeyWs& w, hipStream_t stream, hipEvent_t decoded);

@@ -126,16 +126,17 @@ WidePool make_wide_pool(void* base, uint32_t n_keys, uint64_t n_items) {
 }
 size_t item_ws_bytes(uint64_t n_items) { return item_ws_total(n_items); }
 size_t btab_bytes() { return const_tab_bytes(); }
+size_t btab_scratch_bytes() { return const_scratch_bytes(); }
 
-hipError_t init_btab(void* d_btab, hipStream_t stream) {
-  hipError_t e = ed_init_const(d_btab, stream);
+hipError_t init_btab(void* d_btab, void* d_scratch, hipStream_t stream) {
+  hipError_t e = ed_init_const(d_btab, d_scratch, stream);
   if (e != hipSuccess) return e;
-  return ec_init_const(d_btab, stream);
+  return ec_init_const(d_btab, d_scratch, stream);
 }
 
-// The deferred wide-table builds (the full / row-0 tables start with the chains), forked from
-// `stream` at this point: Ed25519 first (its ladder runs first), the two curves after it (their
-// ladders run after the Ed25519 ladder and finish).
+// The deferred table builds, forked from `stream` at this point: Ed25519 first (its ladder runs
+// first), the two curves after it (their ladders run after the Ed25519 ladder and finish); per
+// family the wide tables, then the full / row-0 ones.
 static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
   PendingTabs& p = fork->pending;
   if (!p.on) return hipSuccess;
@@ -146,12 +147,17 @@ static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
   if (e != hipSuccess) return e;
   ed_launch_keyprep_tabs(p.keys, p.n_keys, w, fork->side[2], false, true);
   e = hipEventRecord(fork->ed_tabs, fork->side[2]);
+  // then the full / row-0 tables (usually few keys: launched ahead of the wide builds, their
+  // near-empty grids queued behind the challenge hashes, which hold every SIMD, and stalled the
+  // wide builds behind them by ~1.8 ms per call: profiles/r02/sha_v2/timeline_step.txt)
+  ed_launch_keyprep_tabs(p.keys, p.n_keys, w, fork->side[2], true, false);
   if (e == hipSuccess) e = hipEventRecord(fork->ready[2], fork->side[2]);
   for (int k = 0; k < 2 && e == hipSuccess; ++k) {
     e = hipStreamWaitEvent(fork->side[k], fork->planned, 0);
     if (e == hipSuccess) e = hipStreamWaitEvent(fork->side[k], fork->ed_tabs, 0);
     if (e != hipSuccess) break;
     ec_launch_keyprep_tabs(k == 0 ? CG_CURVE_R1 : CG_CURVE_K1, p.keys, p.n_keys, w, fork->side[k], false, true);
+    ec_launch_keyprep_tabs(k == 0 ? CG_CURVE_R1 : CG_CURVE_K1, p.keys, p.n_keys, w, fork->side[k], true, false);
     e = hipEventRecord(fork->ready[k], fork->side[k]);
   }
   return e;
@@ -198,15 +204,13 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   hipError_t e = hipEventRecord(fork->start, stream);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->start, 0);
   if (e != hipSuccess) return e;
-  // now: decodes, row-base chains (few waves, latency-bound) and the full / row-0 tables
+  // now: decodes and row-base chains (few waves, latency-bound)
   ec_launch_keyprep_chains(CG_CURVE_R1, d_keys, n_keys, d_arena, arena_len, w, fork->side[0], fork->ec_decoded[0]);
-  ec_launch_keyprep_tabs(CG_CURVE_R1, d_keys, n_keys, w, fork->side[0], true, false);
   ec_launch_keyprep_chains(CG_CURVE_K1, d_keys, n_keys, d_arena, arena_len, w, fork->side[1], fork->ec_decoded[1]);
-  ec_launch_keyprep_tabs(CG_CURVE_K1, d_keys, n_keys, w, fork->side[1], true, false);
   ed_launch_keyprep_chains(d_keys, n_keys, d_arena, arena_len, w, fork->side[2]);
-  ed_launch_keyprep_tabs(d_keys, n_keys, w, fork->side[2], true, false);
-  // the wide tables (thousands of entries per key, they hold every SIMD for milliseconds): after the
-  // first chunk's plan sort when items follow (its decoupled look-back stalls behind them), else now
+  // the tables (the wide ones hold every SIMD for milliseconds), wide first, then full / row 0:
+  // after the first chunk's plan sort when items follow (its decoupled look-back stalls behind
+  // them), else now
   fork->pending.on = true;
   fork->pending.keys = d_keys;
   fork->pending.n_keys = n_keys;

@@ -173,12 +173,24 @@ __global__ void __launch_bounds__(64) k_ec_wide_bwd(uint32_t n_keys, const EdKey
 }
 
 // one lane per (G wide row u, group g of 32 multiples)
+// G wide rows: the row bases 2^{EC_WIDE_GW u} G first (one lane per row, into scratch slot 0),
+// then one lane per (row u, group g of 32 multiples) in batches over scratch slots 1..
 template <int C>
-__global__ void __launch_bounds__(64) k_ec_gwide_init(EcGWideTab* __restrict__ out, EcRowScratch* __restrict__ scratch) {
-  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= EC_GWIDE_LANES) return;
+__global__ void __launch_bounds__(64) k_ec_gwide_bases(Jac* __restrict__ bases) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= (uint32_t)EC_WIDE_GDIGITS) return;
+  Jac P = {c_ec[C].gx, c_ec[C].gy, c_ec[C].one_p};
+  if (u > 0) jac_dbl_n<C>(P, P, EC_WIDE_GW * (int)u);
+  bases[u] = P;
+}
+#define EC_GWIDE_BATCH (CONST_SCRATCH_LANES - 1)
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_gwide_init(EcGWideTab* __restrict__ out, EcRowScratch* __restrict__ scratch,
+                                                      uint32_t lane0) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x, l = lane0 + s;
+  if (s >= EC_GWIDE_BATCH || l >= EC_GWIDE_LANES) return;
   const int u = (int)(l / (EC_WIDE_GMULT / EC_MULT)), g = (int)(l % (EC_WIDE_GMULT / EC_MULT));
-  ec_gwide_group<C>(&out->t[u][g * EC_MULT], u, g, scratch[l], c_ec[C]);
+  ec_gwide_group_from<C>(&out->t[u][g * EC_MULT], ((const Jac*)scratch)[u], g, scratch[1 + s], c_ec[C]);
 }
 
 // one lane per (G row u, group g of 32 multiples)
@@ -299,17 +311,25 @@ hipError_t ec_upload_constants() {
   return hipMemcpyToSymbol(HIP_SYMBOL(c_ec), k, sizeof k, 0, hipMemcpyHostToDevice);
 }
 
-hipError_t ec_init_const(void* d_btab, hipStream_t stream) {
+hipError_t ec_init_const(void* d_btab, void* d_scratch, hipStream_t stream) {
   const dim3 g((EC_GTAB_LANES + 63) / 64);
   hipLaunchKernelGGL(k_ec_gtab_init<CG_CURVE_K1>, g, dim3(64), 0, stream, (EcGTab*)gtab(d_btab, CG_CURVE_K1),
-                     const_scratch(d_btab));
+                     (EcRowScratch*)d_scratch);
   hipLaunchKernelGGL(k_ec_gtab_init<CG_CURVE_R1>, g, dim3(64), 0, stream, (EcGTab*)gtab(d_btab, CG_CURVE_R1),
-                     const_scratch(d_btab));
-  const dim3 gw((EC_GWIDE_LANES + 63) / 64);
-  hipLaunchKernelGGL(k_ec_gwide_init<CG_CURVE_K1>, gw, dim3(64), 0, stream, (EcGWideTab*)gwide(d_btab, CG_CURVE_K1),
-                     const_scratch(d_btab));
-  hipLaunchKernelGGL(k_ec_gwide_init<CG_CURVE_R1>, gw, dim3(64), 0, stream, (EcGWideTab*)gwide(d_btab, CG_CURVE_R1),
-                     const_scratch(d_btab));
+                     (EcRowScratch*)d_scratch);
+  // per curve: the row bases, then batches of EC_GWIDE_BATCH lanes over one scratch (stream order
+  // serialises them)
+  static_assert(EC_WIDE_GDIGITS * sizeof(Jac) <= sizeof(EcRowScratch), "G row bases fit scratch slot 0");
+  const dim3 gw((EC_GWIDE_BATCH + 63) / 64);
+  EcRowScratch* sc = (EcRowScratch*)d_scratch;
+  hipLaunchKernelGGL(k_ec_gwide_bases<CG_CURVE_K1>, dim3(1), dim3(64), 0, stream, (Jac*)sc);
+  for (uint32_t l0 = 0; l0 < (uint32_t)EC_GWIDE_LANES; l0 += EC_GWIDE_BATCH)
+    hipLaunchKernelGGL(k_ec_gwide_init<CG_CURVE_K1>, gw, dim3(64), 0, stream, (EcGWideTab*)gwide(d_btab, CG_CURVE_K1),
+                       sc, l0);
+  hipLaunchKernelGGL(k_ec_gwide_bases<CG_CURVE_R1>, dim3(1), dim3(64), 0, stream, (Jac*)sc);
+  for (uint32_t l0 = 0; l0 < (uint32_t)EC_GWIDE_LANES; l0 += EC_GWIDE_BATCH)
+    hipLaunchKernelGGL(k_ec_gwide_init<CG_CURVE_R1>, gw, dim3(64), 0, stream, (EcGWideTab*)gwide(d_btab, CG_CURVE_R1),
+                       sc, l0);
   return hipGetLastError();
 }
 

@@ -261,15 +261,22 @@ __global__ void __launch_bounds__(64) k_ed_btab_init(EdBTab* __restrict__ out) {
 }
 
 // Wide B rows (radix 2^ED_WIDE_BW, row u = multiples of 2^{ED_WIDE_BW u} B), built once per
-// context: one lane per (row, group of 8 multiples)
-__global__ void __launch_bounds__(64) k_ed_bwide_init(EdBWideTab* __restrict__ out) {
-  constexpr uint32_t G = EdWideCfg::kBMult / 8;
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t u = g / G, grp = g % G;
+// context: the row bases first (one lane per row, into the constant-table scratch), then one lane
+// per (row, group of 8 multiples)
+__global__ void __launch_bounds__(64) k_ed_bwide_bases(ge_p3* __restrict__ bases) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= (uint32_t)EdWideCfg::kBDigits) return;
-  ge_p3 B;
-  ed_base_point(B);
-  ed_bwide_group(&out->t[u][8 * grp], B, (int)u, (int)grp, c_ed.d2);
+  ge_p3 P;
+  ed_base_point(P);
+  if (u > 0) ed_dbl_n(P, P, ED_WIDE_BW * (int)u);
+  bases[u] = P;
+}
+__global__ void __launch_bounds__(64) k_ed_bwide_init(EdBWideTab* __restrict__ out, const ge_p3* __restrict__ bases) {
+  constexpr uint32_t G = EdWideCfg::kBMult / 8;
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t u = (uint32_t)(g / G), grp = (uint32_t)(g % G);
+  if (u >= (uint32_t)EdWideCfg::kBDigits) return;
+  ed_bwide_group(&out->t[u][8 * grp], bases[u], 0, (int)grp, c_ed.d2);
 }
 
 __device__ __forceinline__ void ld_niels(ge_niels& n, const ge_niels* src) {
@@ -363,7 +370,7 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
     if (wide) {
       EdDigitsWide d;
       sc_recode_w<ED_WIDE_W>(d.eh, EdWideCfg::kPackedWords, h);
-      sc_recode_w16<ED_WIDE_BW>(d.es, EdWideCfg::kBPackedWords, sr);
+      sc_recode_wb<ED_WIDE_BW, EdWideCfg::kBBits>(d.es, EdWideCfg::kBPackedWords, sr);
       ((EdDigitsWide*)dig)[p] = d;
     } else {
       EdDigits d;
@@ -573,11 +580,16 @@ __device__ __forceinline__ void ed_wide_op(int o, int& widx, int& sh, bool& is_b
     sh = (o & 3) * 8;
     row = o;
   } else {
+    constexpr int per = 32 / EdWideCfg::kBBits;
     const int u = o - EdWideCfg::kRows;
-    widx = EdWideCfg::kPackedWords + (u >> 1);
-    sh = (u & 1) * 16;
+    widx = EdWideCfg::kPackedWords + u / per;
+    sh = (u % per) * EdWideCfg::kBBits;
     row = u;
   }
+}
+__device__ __forceinline__ int ed_wide_digit(uint32_t w, int sh, bool is_b) {
+  if (!is_b) return (int)(int8_t)(uint8_t)(w >> sh);
+  return EdWideCfg::kBBits == 16 ? (int)(int16_t)(uint16_t)(w >> sh) : (int)w;
 }
 
 __device__ __forceinline__ const ge_niels* ed_wide_src(const EdWideTab& TA, const EdBWideTab& TB, bool is_b, int row,
@@ -595,7 +607,7 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
   int widx, sh, row;
   bool is_b;
   ed_wide_op(0, widx, sh, is_b, row);
-  int d_cur = ed_op_digit(dw[widx], sh, is_b);
+  int d_cur = ed_wide_digit(dw[widx], sh, is_b);
   ed_glds_niels(ed_wide_src(TA, TB, is_b, row, d_cur), wl);
   ed_wide_op(1, widx, sh, is_b, row);
   uint32_t w_next = dw[widx];
@@ -611,7 +623,7 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
     const bool neg = d_cur < 0;
     if (o + 1 < N) {
       ed_wide_op(o + 1, widx, sh, is_b, row);
-      d_cur = ed_op_digit(w_next, sh, is_b);
+      d_cur = ed_wide_digit(w_next, sh, is_b);
       ed_glds_niels(ed_wide_src(TA, TB, is_b, row, d_cur), wl);
       if (o + 2 < N) {
         ed_wide_op(o + 2, widx, sh, is_b, row);
@@ -741,11 +753,15 @@ hipError_t ed_upload_constants() {
   return hipMemcpyToSymbol(HIP_SYMBOL(c_ed), &h, sizeof h, 0, hipMemcpyHostToDevice);
 }
 
-hipError_t ed_init_const(void* d_btab, hipStream_t stream) {
+hipError_t ed_init_const(void* d_btab, void* d_scratch, hipStream_t stream) {
   const uint32_t lanes = EdBCfgT::kDigits * (EdBCfgT::kMult / 8);
   hipLaunchKernelGGL(k_ed_btab_init, dim3((lanes + 63) / 64), dim3(64), 0, stream, (EdBTab*)d_btab);
-  const uint32_t wlanes = EdWideCfg::kBDigits * (EdWideCfg::kBMult / 8);
-  hipLaunchKernelGGL(k_ed_bwide_init, dim3((wlanes + 63) / 64), dim3(64), 0, stream, (EdBWideTab*)bwide(d_btab));
+  static_assert(EdWideCfg::kBDigits * sizeof(ge_p3) <= sizeof(EcRowScratch), "B row bases fit the scratch");
+  ge_p3* bases = (ge_p3*)d_scratch;  // free until ec_init_const's G builds (same stream)
+  hipLaunchKernelGGL(k_ed_bwide_bases, dim3(1), dim3(64), 0, stream, bases);
+  const uint64_t wlanes = (uint64_t)EdWideCfg::kBDigits * (EdWideCfg::kBMult / 8);
+  hipLaunchKernelGGL(k_ed_bwide_init, dim3((unsigned)((wlanes + 63) / 64)), dim3(64), 0, stream,
+                     (EdBWideTab*)bwide(d_btab), (const ge_p3*)bases);
   return hipGetLastError();
 }
 

@@ -508,7 +508,7 @@ static void tbw_init() {
 }
 static void tbw_touch(const uint32_t* es) {
   for (int u = 0; u < EdWideCfg::kBDigits; ++u) {
-    const int d = sc_digit_h(es, u), a = d < 0 ? -d : d;
+    const int d = sc_digit_at<EdWideCfg::kBBits>(es, u), a = d < 0 ? -d : d;
     if (a == 0) continue;
     const int grp = (a - 1) / 8;
     const size_t k = (size_t)u * (EdWideCfg::kBMult / 8) + grp;
@@ -593,7 +593,7 @@ extern "C" int t_ed_verify_wide(const uint32_t* aw, const uint32_t* sw, const ui
   }
   uint32_t eh[EdWideCfg::kPackedWords], es[EdWideCfg::kBPackedWords];
   sc_recode_w<ED_WIDE_W>(eh, EdWideCfg::kPackedWords, h);
-  sc_recode_w16<ED_WIDE_BW>(es, EdWideCfg::kBPackedWords, sr);
+  sc_recode_wb<ED_WIDE_BW, EdWideCfg::kBBits>(es, EdWideCfg::kBPackedWords, sr);
   tbw_touch(es);
   ge_p2 R;
 #ifdef FE_OP_COUNT
@@ -675,9 +675,9 @@ static int ecdsa_wide_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
   ecdsa_batch_inv<C, 1>(&ws, 1, 1u, K);
   {
     uint32_t dg[EC_WIDE_GPACKED];
-    ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS>(dg, ws.a);
+    ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS, false, EC_WIDE_GBITS>(dg, ws.a);
     for (int u = 0; u < EC_WIDE_GDIGITS; ++u) {
-      const int d = ec_digit10(dg, u), a = d < 0 ? -d : d;
+      const int d = ec_digit_at<EC_WIDE_GBITS>(dg, u), a = d < 0 ? -d : d;
       if (a == 0 || tg_built[C][u * GG + (a - 1) / EC_MULT]) continue;
       const int g = (a - 1) / EC_MULT;
       ec_gwide_group_from<C>(&TG[C]->t[u][g * EC_MULT], tg_base[C][u], g, *S, K);

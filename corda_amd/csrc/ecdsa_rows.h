@@ -601,6 +601,79 @@ CG_HD void ec_wide_group_fwd(EcAff* out, const EcAff& base, int j, int g, int cn
   ec_multiples_fwd<C>(out, F, base.x, base.y, cnt, z, pre, K);
 }
 
+// ---- wide-table build (as ed25519_rows.h "wide-table build"): one lane per (wide key, row j, group g
+// of 32 multiples), walked twice in chunks of EC_WIDE_CHUNK = 2 points: pass 1 stores each chunk's Z
+// product, one lane per row batch-inverts the row's 64 chunk products, pass 3 recomputes the points
+// and writes the affine entries. Nothing but the chunk products goes through memory between passes.
+#define EC_WIDE_CHUNK 2
+#define EC_WIDE_CHUNKS (EC_WIDE_MULT / EC_WIDE_CHUNK)  // 64 per row
+
+static_assert(EC_WIDE_CHUNK == 2, "ec_wide_chunk_out is written for chunks of 2");
+template <int C>
+CG_HD void ec_aff_from(EcAff& e, const Jac& p, const f29& zi) {
+  f29 zi2, zi3;
+  m29_sq<C, 0>(zi2, zi);
+  m29_mul<C, 0>(zi3, zi2, zi);
+  m29_mul<C, 0>(e.x, p.X, zi2);
+  m29_mul<C, 0>(e.y, p.Y, zi3);
+}
+// the chunk's affine entries from zinv = 1 / (Z_0 Z_1) (straight-line, as ed_wide_chunk_out)
+template <int C>
+CG_HD void ec_wide_chunk_out(EcAff* out, const Jac pts[EC_WIDE_CHUNK], const f29& zinv) {
+  f29 z1i, z0i;
+  m29_mul<C, 0>(z1i, zinv, pts[0].Z);
+  m29_mul<C, 0>(z0i, zinv, pts[1].Z);
+  EcAff e0, e1;
+  ec_aff_from<C>(e0, pts[0], z0i);
+  ec_aff_from<C>(e1, pts[1], z1i);
+  out[0] = e0;
+  out[1] = e1;
+}
+
+// Pass 1 (Out = false): zc[c] = chunk c's Z product; pass 3 (Out = true): the group's 32 entries.
+// Multiples g * 32 + 1 .. (g + 1) * 32 of the row's affine base (row 32: 129.. of the top row's).
+template <int C, bool Out>
+CG_HD void ec_wide_group_pass(EcAff* out, f29* zc, const EcAff& base, int j, int g, const EcConsts& K) {
+  const uint32_t m = (j < EC_WIDE_DIGITS ? 0u : (uint32_t)EC_WIDE_MULT) + 32u * (uint32_t)g + 1u;
+  Jac F;
+  jac_small_mul_aff<C>(F, base.x, base.y, m, K);
+#pragma unroll 1
+  for (int ch = 0; ch < 32 / EC_WIDE_CHUNK; ++ch) {
+    Jac pts[EC_WIDE_CHUNK];
+    f29 zp;
+    if (ch > 0) jac_madd<C>(F, F, base.x, base.y, K);  // the chunk's first point (F == base: doubling branch)
+    if (Out) pts[0] = F;
+    else zp = F.Z;
+#pragma unroll
+    for (int k = 1; k < EC_WIDE_CHUNK; ++k) {
+      jac_madd<C>(F, F, base.x, base.y, K);
+      if (Out) pts[k] = F;
+      else m29_mul<C, 0>(zp, zp, F.Z);
+    }
+    if (Out) ec_wide_chunk_out<C>(out + EC_WIDE_CHUNK * ch, pts, zc[ch]);
+    else zc[ch] = zp;
+  }
+}
+
+// in place: z[g] <- 1 / z[g] mod p for the NG products of one row (prefix products in pre[])
+template <int C, int NG>
+CG_HD void m29_invert_run(f29* z, f29* pre, const EcConsts& K) {
+  f29 run = z[0];
+  pre[0] = run;
+  for (int g = 1; g < NG; ++g) {
+    m29_mul<C, 0>(run, run, z[g]);
+    pre[g] = run;
+  }
+  f29 inv;
+  m29_inv<C, 0>(inv, run, K.one_p);
+  for (int g = NG - 1; g > 0; --g) {
+    const f29 zg = z[g];
+    m29_mul<C, 0>(z[g], inv, pre[g - 1]);
+    m29_mul<C, 0>(inv, inv, zg);
+  }
+  z[0] = inv;
+}
+
 // Affine x, y of n finite Jacobian points in place (one inversion; `pre` holds n products).
 template <int C>
 CG_HD void jac_batch_to_affine(EcAff* out, const Jac* P, int n, f29* pre, const EcConsts& K) {

@@ -516,3 +516,95 @@ CG_HD void ed_bwide_group(ge_niels* out8, const ge_p3& B, int u, int grp, const 
   }
   ed_niels_batch8(out8, pts, d2);
 }
+
+// ---------------------------------------------------------------- wide-table build
+// One lane per (wide key, row j, group g of ED_WIDE_GROUP = 32 consecutive multiples of the row base
+// P), in chunks of ED_WIDE_CHUNK = 2: pass 1 walks the group by additions and stores only each
+// chunk's Z product (16 per lane); pass 2 batch-inverts a row's 64 chunk products (one lane per row);
+// pass 3 walks the group again, keeping a chunk's points in VGPRs, and writes its normalised niels
+// entries (240 contiguous bytes; chunks of 4 spilled at 256 VGPRs). The three-pass form that stored every multiple's projective X, Y, Z
+// and running product in memory between passes moved ~1 KB of uncoalesced traffic per entry (12.6 +
+// 4.2 GB per headline call, profiles/r02/p3/pmc_traffic.json) and stalled the challenge hashes and
+// ECDSA fronts sharing the chip with it; this form moves ~130 B per entry.
+#define ED_WIDE_GROUP 32
+#define ED_WIDE_GROUPS (EdWideCfg::kMult / ED_WIDE_GROUP)  // 4 group lanes per row
+#define ED_WIDE_CHUNK 2
+#define ED_WIDE_CHUNKS (EdWideCfg::kMult / ED_WIDE_CHUNK)  // 64 chunk products per row
+
+// the chunk's niels entries from zinv = 1 / (Z_0 Z_1) (straight-line: a loop here was left rolled
+// and put the points in scratch)
+static_assert(ED_WIDE_CHUNK == 2, "ed_wide_chunk_out is written for chunks of 2");
+CG_HD void ed_niels_from(ge_niels& n, const ge_p2& p, const fe& zi, const fe& d2) {
+  fe x, y, xy;
+  fe_mul(x, p.X, zi);
+  fe_mul(y, p.Y, zi);
+  fe_add(n.ypx, y, x);
+  fe_carry(n.ypx);
+  fe_sub(n.ymx, y, x);
+  fe_carry(n.ymx);
+  fe_mul(xy, x, y);
+  fe_mul(n.xy2d, xy, d2);
+}
+CG_HD void ed_wide_chunk_out(ge_niels* out, const ge_p2 pts[ED_WIDE_CHUNK], const fe& zinv, const fe& d2) {
+  fe z1i, z0i;
+  fe_mul(z1i, zinv, pts[0].Z);  // 1 / Z_1
+  fe_mul(z0i, zinv, pts[1].Z);  // 1 / Z_0
+  ge_niels n0, n1;
+  ed_niels_from(n0, pts[0], z0i, d2);
+  ed_niels_from(n1, pts[1], z1i, d2);
+  out[0] = n0;
+  out[1] = n1;
+}
+
+// Pass 1 (Out = false): zc[c] = chunk c's Z product. Pass 3 (Out = true): the group's 32 entries
+// into out[0..31] from the inverted chunk products zc[c].
+template <bool Out>
+CG_HD void ed_wide_group_pass(ge_niels* out, fe* zc, const ge_p3& P, int g, const fe& d2) {
+  ge_cached c;
+  ge_p3_to_cached(c, P, d2);
+  ge_p3 R;
+  ed_small_mul(R, P, (uint32_t)(ED_WIDE_GROUP * g + 1), d2);
+  ge_p1p1 t;
+#pragma unroll 1
+  for (int ch = 0; ch < ED_WIDE_GROUP / ED_WIDE_CHUNK; ++ch) {
+    ge_p2 pts[ED_WIDE_CHUNK];
+    fe zp;
+    if (ch > 0) {  // the chunk's first point: one addition past the previous chunk's last
+      ge_add_cached(t, R, c);
+      ge_p1p1_to_p3(R, t);
+    }
+    if (Out) ge_p3_to_p2(pts[0], R);
+    else fe_copy(zp, R.Z);
+#pragma unroll
+    for (int k = 1; k < ED_WIDE_CHUNK; ++k) {
+      ge_add_cached(t, R, c);
+      ge_p1p1_to_p3(R, t);
+      if (Out) ge_p3_to_p2(pts[k], R);
+      else fe_mul(zp, zp, R.Z);
+    }
+    if (Out) ed_wide_chunk_out(out + ED_WIDE_CHUNK * ch, pts, zc[ch], d2);
+    else fe_copy(zc[ch], zp);
+  }
+}
+
+// in place: z[g] <- 1 / z[g] for the NG products of one row (prefix products in pre[])
+template <int NG>
+CG_HD void fe_invert_run(fe* z, fe* pre) {
+  fe run;
+  fe_copy(run, z[0]);
+  fe_copy(pre[0], run);
+  for (int g = 1; g < NG; ++g) {
+    fe_mul(run, run, z[g]);
+    fe_copy(pre[g], run);
+  }
+  fe inv;
+  fe_invert(inv, run);
+  for (int g = NG - 1; g > 0; --g) {
+    fe zg, t;
+    fe_copy(zg, z[g]);
+    fe_mul(t, inv, pre[g - 1]);
+    fe_copy(z[g], t);
+    fe_mul(inv, inv, zg);
+  }
+  fe_copy(z[0], inv);
+}

@@ -116,8 +116,9 @@ __global__ void __launch_bounds__(64) k_ec_wide_chain(uint32_t n_keys, const EdK
   jac_batch_to_affine<C>(ws.bases, ws.jbases, EC_WIDE_DIGITS, ws.s[0].pre, c_ec[C]);
 }
 
-// The row tables in three passes over (wide key, row, group) lanes, as the Ed25519 build
-// (verify_ed.hip k_ed_wide_fwd / _inv / _bwd); the steps are mixed additions of the affine base.
+// The row tables in three passes over (wide key, row, group of 32) lanes, as the Ed25519 build
+// (ecdsa_rows.h ec_wide_group_pass): chunk Z products, one inversion per row over its 64 chunk
+// products (in the row's scratch z[0..63], prefixes in pre[0..63]), then the entries.
 #define EC_WIDE_GROUP 32
 #define EC_WIDE_GROUPS (EC_WIDE_MULT / EC_WIDE_GROUP)
 struct EcWideLane {
@@ -133,6 +134,7 @@ __device__ __forceinline__ EcWideLane ec_wide_lane(uint32_t rows, uint32_t group
   const uint32_t i = wide[(size_t)c * n_keys + (L).l];     \
   if (hdr[i].status != 0) return;                          \
   EcWideSlot& ws = wec[wide_idx[i]]
+static_assert(EC_WIDE_CHUNKS <= EC_WIDE_MULT, "chunk products fit a row's scratch");
 
 template <int C>
 __global__ void __launch_bounds__(64) k_ec_wide_fwd(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
@@ -141,9 +143,9 @@ __global__ void __launch_bounds__(64) k_ec_wide_fwd(uint32_t n_keys, const EdKey
                                                     const uint32_t* __restrict__ wide_idx, EcWideSlot* __restrict__ wec) {
   const EcWideLane L = ec_wide_lane(EC_WIDE_ROWS, EC_WIDE_GROUPS);
   EC_WIDE_KEY(C, L);
-  const uint32_t o = EC_WIDE_GROUP * L.g;
-  ec_wide_group_fwd<C>(&ws.tab.t[L.j][o], ws.bases[L.j < EC_WIDE_DIGITS ? L.j : EC_WIDE_DIGITS - 1], (int)L.j,
-                       (int)L.g, EC_WIDE_GROUP, &ws.s[L.j].z[o], &ws.s[L.j].pre[o], c_ec[C]);
+  constexpr int CPG = EC_WIDE_GROUP / EC_WIDE_CHUNK;
+  ec_wide_group_pass<C, false>(nullptr, &ws.s[L.j].z[CPG * L.g],
+                               ws.bases[L.j < EC_WIDE_DIGITS ? L.j : EC_WIDE_DIGITS - 1], (int)L.j, (int)L.g, c_ec[C]);
 }
 
 template <int C>
@@ -153,11 +155,7 @@ __global__ void __launch_bounds__(64) k_ec_wide_inv(uint32_t n_keys, const EdKey
                                                     const uint32_t* __restrict__ wide_idx, EcWideSlot* __restrict__ wec) {
   const EcWideLane L = ec_wide_lane(EC_WIDE_ROWS, 1);
   EC_WIDE_KEY(C, L);
-  f29* pre = ws.s[L.j].pre;
-  f29 t[EC_WIDE_GROUPS], inv[EC_WIDE_GROUPS];
-  for (int g = 0; g < EC_WIDE_GROUPS; ++g) t[g] = pre[EC_WIDE_GROUP * g + EC_WIDE_GROUP - 1];
-  m29_batch_invert_small<C, EC_WIDE_GROUPS>(inv, t, c_ec[C]);
-  for (int g = 0; g < EC_WIDE_GROUPS; ++g) pre[EC_WIDE_GROUP * g + EC_WIDE_GROUP - 1] = inv[g];
+  m29_invert_run<C, EC_WIDE_CHUNKS>(ws.s[L.j].z, ws.s[L.j].pre, c_ec[C]);
 }
 
 template <int C>
@@ -167,12 +165,11 @@ __global__ void __launch_bounds__(64) k_ec_wide_bwd(uint32_t n_keys, const EdKey
                                                     const uint32_t* __restrict__ wide_idx, EcWideSlot* __restrict__ wec) {
   const EcWideLane L = ec_wide_lane(EC_WIDE_ROWS, EC_WIDE_GROUPS);
   EC_WIDE_KEY(C, L);
-  const uint32_t o = EC_WIDE_GROUP * L.g;
-  const f29* pre = &ws.s[L.j].pre[o];
-  ec_multiples_bwd<C>(&ws.tab.t[L.j][o], pre[EC_WIDE_GROUP - 1], EC_WIDE_GROUP, &ws.s[L.j].z[o], pre);
+  constexpr int CPG = EC_WIDE_GROUP / EC_WIDE_CHUNK;
+  ec_wide_group_pass<C, true>(&ws.tab.t[L.j][EC_WIDE_GROUP * L.g], &ws.s[L.j].z[CPG * L.g],
+                              ws.bases[L.j < EC_WIDE_DIGITS ? L.j : EC_WIDE_DIGITS - 1], (int)L.j, (int)L.g, c_ec[C]);
 }
 
-// one lane per (G wide row u, group g of 32 multiples)
 // G wide rows: the row bases 2^{EC_WIDE_GW u} G first (one lane per row, into scratch slot 0),
 // then one lane per (row u, group g of 32 multiples) in batches over scratch slots 1..
 template <int C>

@@ -166,12 +166,9 @@ __global__ void __launch_bounds__(64) k_ed_wide_chain(uint32_t n_keys, const EdK
   }
 }
 
-// The row tables in three passes over (wide key, row, group of ED_WIDE_GROUP multiples) lanes:
-// forward (first multiple by double-and-add, 31 additions, running Z products), one inversion per
-// row over its groups' products (a quarter of the lanes), backward (every 1/Z, niels form). A lane's
-// serial chain is a quarter of a whole row's, and the inversions cost a quarter of one per group.
-#define ED_WIDE_GROUP 32
-#define ED_WIDE_GROUPS (EdWideCfg::kMult / ED_WIDE_GROUP)
+// The row tables in three passes (ed25519_rows.h "wide-table build"): chunk Z products per (wide
+// key, row, group of 32) lane, one batch inversion per (wide key, row) lane over the row's 64 chunk
+// products (kept in the slot's zpre[j][0..63], prefixes in zpre[j][64..127]), then the entries.
 struct WideLane {
   uint32_t l, j, g;
 };
@@ -179,6 +176,7 @@ __device__ __forceinline__ WideLane wide_lane(uint32_t rows, uint32_t groups) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   return WideLane{(uint32_t)(t / (rows * groups)), (uint32_t)(t / groups % rows), (uint32_t)(t % groups)};
 }
+static_assert(2 * ED_WIDE_CHUNKS <= EdWideCfg::kMult, "chunk products and prefixes fit a zpre row");
 
 __global__ void __launch_bounds__(64) k_ed_wide_fwd(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                     const uint32_t* __restrict__ wide,
@@ -189,10 +187,8 @@ __global__ void __launch_bounds__(64) k_ed_wide_fwd(uint32_t n_keys, const EdKey
   const uint32_t i = wide[(size_t)PLAN_ED * n_keys + L.l];
   if (hdr[i].status != 0) return;
   EdWideSlot& ws = wed[wide_idx[i]];
-  ge_p3 first;
-  ed_small_mul(first, ws.bases[L.j], ED_WIDE_GROUP * L.g + 1, c_ed.d2);
-  ed_multiples_fwd<ED_WIDE_GROUP>(&ws.tab.t[L.j][ED_WIDE_GROUP * L.g], first, ws.bases[L.j], c_ed.d2,
-                                  &ws.zpre[L.j][ED_WIDE_GROUP * L.g]);
+  constexpr int CPG = ED_WIDE_GROUP / ED_WIDE_CHUNK;
+  ed_wide_group_pass<false>(nullptr, &ws.zpre[L.j][CPG * L.g], ws.bases[L.j], (int)L.g, c_ed.d2);
 }
 
 __global__ void __launch_bounds__(64) k_ed_wide_inv(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
@@ -203,11 +199,8 @@ __global__ void __launch_bounds__(64) k_ed_wide_inv(uint32_t n_keys, const EdKey
   if (L.l >= wide_count[PLAN_ED]) return;
   const uint32_t i = wide[(size_t)PLAN_ED * n_keys + L.l];
   if (hdr[i].status != 0) return;
-  fe(&z)[EdWideCfg::kMult] = wed[wide_idx[i]].zpre[L.j];
-  fe t[ED_WIDE_GROUPS], inv[ED_WIDE_GROUPS];
-  for (int g = 0; g < ED_WIDE_GROUPS; ++g) t[g] = z[ED_WIDE_GROUP * g + ED_WIDE_GROUP - 1];
-  fe_batch_invert_small<ED_WIDE_GROUPS>(inv, t);
-  for (int g = 0; g < ED_WIDE_GROUPS; ++g) z[ED_WIDE_GROUP * g + ED_WIDE_GROUP - 1] = inv[g];
+  fe* z = wed[wide_idx[i]].zpre[L.j];
+  fe_invert_run<ED_WIDE_CHUNKS>(z, z + ED_WIDE_CHUNKS);
 }
 
 __global__ void __launch_bounds__(64) k_ed_wide_bwd(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
@@ -219,8 +212,9 @@ __global__ void __launch_bounds__(64) k_ed_wide_bwd(uint32_t n_keys, const EdKey
   const uint32_t i = wide[(size_t)PLAN_ED * n_keys + L.l];
   if (hdr[i].status != 0) return;
   EdWideSlot& ws = wed[wide_idx[i]];
-  const fe* z = &ws.zpre[L.j][ED_WIDE_GROUP * L.g];
-  ed_multiples_bwd<ED_WIDE_GROUP>(&ws.tab.t[L.j][ED_WIDE_GROUP * L.g], z[ED_WIDE_GROUP - 1], z, c_ed.d2);
+  constexpr int CPG = ED_WIDE_GROUP / ED_WIDE_CHUNK;
+  ed_wide_group_pass<true>(&ws.tab.t[L.j][ED_WIDE_GROUP * L.g], &ws.zpre[L.j][CPG * L.g], ws.bases[L.j], (int)L.g,
+                           c_ed.d2);
 }
 
 // The base point B as an extended point (from the constant niels table entry 1*B)

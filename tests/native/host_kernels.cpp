@@ -538,30 +538,14 @@ extern "C" int t_ed_verify_wide(const uint32_t* aw, const uint32_t* sw, const ui
 #ifdef FE_OP_COUNT
     g_fe_nmul = g_fe_nsq = 0;
 #endif
-    for (int j = 0; j < EdWideCfg::kRows; ++j) {  // k_ed_wide_chain, then k_ed_wide_tab per (row, group)
+    for (int j = 0; j < EdWideCfg::kRows; ++j) {  // k_ed_wide_chain, then the three build passes per row
       if (j > 0) ed_dbl_n(P, P, ED_WIDE_W);
-      for (int g = 0; g < EdWideCfg::kMult / 32; ++g) {
-        ge_p3 first = P;
-        if (g > 0) {  // ed_small_mul(first, P, 32 g + 1), as the device lane does
-          ge_cached c;
-          ge_p3_to_cached(c, P, g_C.d2);
-          ge_p1p1 t;
-          const uint32_t m = 32u * g + 1u;
-          for (int b = 30 - __builtin_clz(m); b >= 0; --b) {
-            ge_p3_dbl(t, first);
-            ge_p1p1_to_p3(first, t);
-            if ((m >> b) & 1u) {
-              ge_add_cached(t, first, c);
-              ge_p1p1_to_p3(first, t);
-            }
-          }
-        }
-        ed_multiples_fwd<32>(&TA->t[j][32 * g], first, P, g_C.d2, &zpre[j][32 * g]);
-      }
-      fe t[4], inv[4];  // k_ed_wide_inv
-      for (int g = 0; g < 4; ++g) t[g] = zpre[j][32 * g + 31];
-      fe_batch_invert_small<4>(inv, t);
-      for (int g = 0; g < 4; ++g) ed_multiples_bwd<32>(&TA->t[j][32 * g], inv[g], &zpre[j][32 * g], g_C.d2);
+      constexpr int CPG = ED_WIDE_GROUP / ED_WIDE_CHUNK;
+      for (int g = 0; g < ED_WIDE_GROUPS; ++g)  // k_ed_wide_fwd lanes
+        ed_wide_group_pass<false>(nullptr, &zpre[j][CPG * g], P, g, g_C.d2);
+      fe_invert_run<ED_WIDE_CHUNKS>(zpre[j], zpre[j] + ED_WIDE_CHUNKS);  // k_ed_wide_inv
+      for (int g = 0; g < ED_WIDE_GROUPS; ++g)  // k_ed_wide_bwd lanes
+        ed_wide_group_pass<true>(&TA->t[j][ED_WIDE_GROUP * g], &zpre[j][CPG * g], P, g, g_C.d2);
     }
 #ifdef FE_OP_COUNT
     build_mul = g_fe_nmul;
@@ -654,12 +638,11 @@ static int ecdsa_wide_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
     jac_batch_to_affine<C>(ab, jb, EC_WIDE_DIGITS, WS->pre, K);
     for (int j = 0; j < EC_WIDE_ROWS; ++j) {  // k_ec_wide_fwd / _inv / _bwd per row
       const EcAff& base = ab[j < EC_WIDE_DIGITS ? j : EC_WIDE_DIGITS - 1];
+      constexpr int CPG = 32 / EC_WIDE_CHUNK;
+      for (int g = 0; g < EC_WIDE_MULT / 32; ++g) ec_wide_group_pass<C, false>(nullptr, &WS->z[CPG * g], base, j, g, K);
+      m29_invert_run<C, EC_WIDE_CHUNKS>(WS->z, WS->pre, K);
       for (int g = 0; g < EC_WIDE_MULT / 32; ++g)
-        ec_wide_group_fwd<C>(&TQ->t[j][32 * g], base, j, g, 32, &WS->z[32 * g], &WS->pre[32 * g], K);
-      f29 t[4], inv[4];
-      for (int g = 0; g < 4; ++g) t[g] = WS->pre[32 * g + 31];
-      m29_batch_invert_small<C, 4>(inv, t, K);
-      for (int g = 0; g < 4; ++g) ec_multiples_bwd<C>(&TQ->t[j][32 * g], inv[g], 32, &WS->z[32 * g], &WS->pre[32 * g]);
+        ec_wide_group_pass<C, true>(&TQ->t[j][32 * g], &WS->z[CPG * g], base, j, g, K);
     }
 #ifdef FE_OP_COUNT
     build_count = g_m29_nmul[C][0];

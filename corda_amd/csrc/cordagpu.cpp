@@ -171,12 +171,20 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   const bool two = nch > 1 && c->itemws.cap >= 2 * item_half_bytes(per);
   auto ws = [&](uint64_t k) { return (void*)((uint8_t*)c->itemws.p + (two ? (k & 1) * item_half_bytes(per) : 0)); };
   auto cnt = [&](uint64_t k) { return per < n_items - k * per ? per : n_items - k * per; };
+  auto plan = [&](uint64_t k) {
+    return cg::launch_items_plan(d_keys, n_keys, d_items + k * per, cnt(k), d_status + k * per, c->keyprep.p, ws(k),
+                                 s, &c->fork, &wp);
+  };
   auto front = [&](uint64_t k) {
     return cg::launch_items_front(d_keys, n_keys, d_items + k * per, cnt(k), d_arena, arena_len, mode,
-                                  d_status + k * per, c->keyprep.p, ws(k), s, d_msgs, msgs_len, &c->fork, &wp);
+                                  d_status + k * per, c->keyprep.p, ws(k), s, d_msgs, msgs_len, &c->fork, &wp,
+                                  two && k < 2);
   };
   // chunk k + 1's front (plan, hashes, ECDSA prep) before chunk k's back (ladders): the first
-  // chunk's wait for the key tables is spent on the next chunk's fronts
+  // chunk's wait for the key tables is spent on the next chunk's fronts. The first two plans sort
+  // before the table builds start (their look-back stalls behind the builds).
+  if (e == hipSuccess && two) e = plan(0);
+  if (e == hipSuccess && two) e = plan(1);
   if (e == hipSuccess) e = front(0);
   for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
     if (!two && k > 0) e = front(k);

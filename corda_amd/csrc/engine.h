@@ -116,10 +116,16 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
 // s^-1: needs only the decoded keys) and the back (ladders, finish: need the key tables). Between the
 // two a caller with a second item workspace may enqueue the next chunk's front, so the first chunk's
 // wait for the key tables is spent on the second chunk's fronts (cordagpu.cpp launch_chunked).
+// The front's plan sort can be enqueued on its own first (`planned` = true then skips it in the
+// front): onesweep's decoupled look-back stalls when the table builds hold the SIMDs, so a caller
+// with two chunks sorts both before the first front starts the table builds.
+hipError_t launch_items_plan(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                             uint8_t* d_status, const void* d_keyprep, void* d_item_ws, hipStream_t stream,
+                             const Fork* fork, const WidePool* wide);
 hipError_t launch_items_front(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                               const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
                               const void* d_keyprep, void* d_item_ws, hipStream_t stream, const uint8_t* d_msgs,
-                              uint64_t msgs_len, const Fork* fork, const WidePool* wide);
+                              uint64_t msgs_len, const Fork* fork, const WidePool* wide, bool planned);
 hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                              const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_status, const void* d_keyprep,
                              void* d_item_ws, const void* d_btab, hipStream_t stream, const Fork* fork,

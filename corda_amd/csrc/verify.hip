@@ -223,10 +223,9 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   return hipGetLastError();
 }
 
-hipError_t launch_items_front(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
-                              const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
-                              const void* d_keyprep, void* d_item_ws, hipStream_t stream, const uint8_t* d_msgs,
-                              uint64_t msgs_len, const Fork* fork, const WidePool* wide) {
+hipError_t launch_items_plan(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                             uint8_t* d_status, const void* d_keyprep, void* d_item_ws, hipStream_t stream,
+                             const Fork* fork, const WidePool* wide) {
   if (n_items == 0) return hipSuccess;
   const uint32_t B = 256;
   const uint64_t grid = (n_items + B - 1) / B;
@@ -239,7 +238,20 @@ hipError_t launch_items_front(const cg_key* d_keys, uint32_t n_keys, const cg_it
   CG_TIME(fork, CG_STAGE_PLAN, stream,
           e = launch_plan(d_items, n_items, d_keys, n_keys, (const uint32_t*)w.uses, (const uint32_t*)w.wide_idx, iw,
                           stream));
-  if (e == hipSuccess && fork) e = launch_pending_tabs(fork, stream);  // the first chunk starts the table builds
+  return e;
+}
+
+hipError_t launch_items_front(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                              const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
+                              const void* d_keyprep, void* d_item_ws, hipStream_t stream, const uint8_t* d_msgs,
+                              uint64_t msgs_len, const Fork* fork, const WidePool* wide, bool planned) {
+  if (n_items == 0) return hipSuccess;
+  const KeyWs w = key_ws((void*)d_keyprep, n_keys, wide);
+  const ItemWs iw = item_ws(d_item_ws, n_items);
+  hipError_t e = hipSuccess;
+  if (!planned)
+    e = launch_items_plan(d_keys, n_keys, d_items, n_items, d_status, d_keyprep, d_item_ws, stream, fork, wide);
+  if (e == hipSuccess && fork) e = launch_pending_tabs(fork, stream);  // the first front starts the table builds
   if (e != hipSuccess) return e;
   // fronts: Ed25519 challenges (need only Abyte), ECDSA prep + s^-1 per curve (need the decoded key)
   CG_TIME(fork, CG_STAGE_ED_HASH, stream,
@@ -312,7 +324,7 @@ hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_
                         const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
                         const uint8_t* d_msgs, uint64_t msgs_len, const Fork* fork, const WidePool* wide) {
   hipError_t e = launch_items_front(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, d_keyprep,
-                                    d_item_ws, stream, d_msgs, msgs_len, fork, wide);
+                                    d_item_ws, stream, d_msgs, msgs_len, fork, wide, false);
   if (e != hipSuccess) return e;
   return launch_items_back(d_keys, n_keys, d_items, n_items, d_arena, arena_len, d_status, d_keyprep, d_item_ws,
                            d_btab, stream, fork, wide);

@@ -686,44 +686,44 @@ __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
   }
 }
 
-// Encode + compare for 16 consecutive items per lane: one inversion per lane (Montgomery's
-// trick) instead of one per item.
+// Encode + compare for ED_FINISH_K items per lane: one inversion per lane (Montgomery's trick)
+// instead of one per item. A wave takes 64 x K consecutive plan positions, lane l the positions
+// l, l + 64, ... of them, so the slot reads of a wave are contiguous (round 1 gave each lane K
+// consecutive positions: every lane's 120-B slot reads were a separate pair of cache lines).
 #ifndef ED_FINISH_K
 #define ED_FINISH_K 16
 #endif
-__device__ __forceinline__ void ed_finish_one(uint64_t base, uint32_t end, const cg_item* __restrict__ items,
-                                              const uint32_t* __restrict__ perm, const uint8_t* __restrict__ arena,
-                                              uint64_t arena_len, uint8_t* __restrict__ status,
-                                              const ge_p2* __restrict__ rin) {
-  const uint32_t cnt = (uint32_t)((end - base) < ED_FINISH_K ? (end - base) : ED_FINISH_K);
+__device__ __forceinline__ void ed_finish_one(uint64_t unit, uint32_t beg, uint32_t end,
+                                              const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
+                                              const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                              uint8_t* __restrict__ status, const ge_p2* __restrict__ rin) {
+  const uint64_t base = beg + (unit >> 6) * (64 * ED_FINISH_K) + (unit & 63);
   fe acc[ED_FINISH_K];
   fe run;
   fe_1(run);
   uint32_t pend = 0;
-  for (uint32_t k = 0; k < cnt; ++k) {
-    const bool p = status[perm[base + k]] == ED_PENDING;
-    pend |= (uint32_t)p << k;
-    if (p) {
-      fe_mul(run, run, rin[base + k].Z);
-    }
+  for (uint32_t k = 0; k < ED_FINISH_K; ++k) {
+    const uint64_t p = base + 64 * k;
+    const bool pd = p < end && status[perm[p]] == ED_PENDING;
+    pend |= (uint32_t)pd << k;
+    if (pd) fe_mul(run, run, rin[p].Z);
     fe_copy(acc[k], run);
   }
   if (!pend) return;
   fe inv;
   fe_invert(inv, run);
   const uint64_t lr = round4(arena_len);
-  for (int k = (int)cnt - 1; k >= 0; --k) {
+  for (int k = ED_FINISH_K - 1; k >= 0; --k) {
     if (!((pend >> k) & 1u)) continue;
+    const uint64_t p = base + 64 * (uint32_t)k;
+    const ge_p2 P = rin[p];
     fe zi, t;
-    // acc[k] = prod of pending Z up to k; inv = 1 / acc[k]
-    int prev = k - 1;
-    while (prev >= 0 && !((pend >> prev) & 1u)) --prev;
-    if (prev >= 0) fe_mul(zi, inv, acc[prev]);
+    // acc[k - 1] = product of the pending Z before k (entries of non-pending items copy it forward)
+    if (k > 0) fe_mul(zi, inv, acc[k - 1]);
     else fe_copy(zi, inv);
-    fe_mul(t, inv, rin[base + k].Z);
+    fe_mul(t, inv, P.Z);
     fe_copy(inv, t);
-    const ge_p2 P = rin[base + k];
-    const uint32_t i = perm[base + k];
+    const uint32_t i = perm[p];
     uint32_t rw[8];
     const uint64_t so = items[i].sig_off;
 #pragma unroll
@@ -737,8 +737,9 @@ __global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ i
                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                    uint8_t* __restrict__ status, const ge_p2* __restrict__ rin) {
   const uint32_t beg = ranges[PLAN_ED], end = ranges[PLAN_ED + 1];
-  for (Walk w = walk_units((end - beg + ED_FINISH_K - 1) / ED_FINISH_K); w.u < w.end; w.u += w.step)
-    ed_finish_one(beg + w.u * ED_FINISH_K, end, items, perm, arena, arena_len, status, rin);
+  const uint64_t units = ((uint64_t)(end - beg) + 64 * ED_FINISH_K - 1) / (64 * ED_FINISH_K) * 64;
+  for (Walk w = walk_units(units); w.u < w.end; w.u += w.step)
+    ed_finish_one(w.u, beg, end, items, perm, arena, arena_len, status, rin);
 }
 
 hipError_t ed_upload_constants() {
@@ -838,7 +839,8 @@ void ed_launch_ladder_wide(const cg_item* d_items, uint64_t n_items, uint8_t* d_
 void ed_launch_finish(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
                       uint8_t* d_status, const ItemWs& iw, hipStream_t stream) {
   const uint32_t B = 256;
-  const unsigned fgrid = walk_grid((n_items + ED_FINISH_K - 1) / ED_FINISH_K, B, WALK_CAP(2));
+  const uint64_t units = (n_items + 64 * ED_FINISH_K - 1) / (64 * ED_FINISH_K) * 64;
+  const unsigned fgrid = walk_grid(units, B, WALK_CAP(2));
   hipLaunchKernelGGL(k_ed_finish, dim3(fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
                      arena_len, d_status, (const ge_p2*)iw.slots);
 }

@@ -49,7 +49,7 @@ MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # Executed work of the GPU path, counted by the host build of the same lane code
 # (tests/native/host_kernels.cpp; pinned by tests/test_host_kernels.py::test_executed_work_*).
 # Ed25519 (field multiplies, squarings) in the radix-2^25.5 representation (fe25519.h):
-ED_VERIFY_FE = (500, 24)   # k_ed_ladder_pf: 43 + 26 mixed additions + 6 doublings
+ED_VERIFY_FE = (402, 24)   # k_ed_ladder_pf: 43 + 12 mixed additions + 6 doublings
 ED_WIDE_FE = (307, 0)      # k_ed_ladder_wide: 32 + 12 mixed additions, no doublings (keys with wide tables)
 ED_WIDE_BUILD_FE = (100103, 13472)  # one key's wide table: 248-doubling chain, 32 rows x 4 groups of 32 entries walked twice (chunk Z products, then entries), one inversion per row
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
@@ -66,7 +66,7 @@ MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
 # The ladder figure is its full schedule (every digit non-zero): a lane whose digit is zero skips
 # its addition, but the wave issues it for the other 63 lanes, so the full schedule is what the
 # SIMD executes (per-item mean 1% lower).
-EC_LADDER_MUL = {"secp256r1": 895, "secp256k1": 877}
+EC_LADDER_MUL = {"secp256r1": 741, "secp256k1": 723}
 EC_WIDE_MUL = {"secp256r1": 476, "secp256k1": 476}  # k_ec_ladder_wide: 32 + 12 mixed additions + x-check
 # table modes (corda_amd/csrc/keyws.h): full tables from 32 items per key, wide from 384
 KEY_FULL_MIN_USES, KEY_WIDE_MAX = 32, 8192
@@ -79,7 +79,7 @@ EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
 # kernel generation whose PMC traffic profile is committed (profiles/r02/pmc_traffic.json)
-KERNEL_VERSION = "r02_v3"
+KERNEL_VERSION = "r02_v4"
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
 
 # Appendix A labels (tools/workload) -> the verdict Crypto.doVerify gives them (key decodes)

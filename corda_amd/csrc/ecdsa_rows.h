@@ -381,100 +381,6 @@ CG_HD void ec_pick(f29& x, f29& y, const Row* row, int a) {
   y = e.y;
 }
 
-// Stage 3: R = u1 G + u2 Q (Q over the per-key radix-64 rows, G over the radix-2^10 table),
-// then the x-check. Returns 0 VALID / 1 INVALID.
-template <int C, class TabG, class TabQ>
-CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG, const TabQ& TQ,
-                                  const EcConsts& K) {
-  uint32_t dg[EC_G_PACKED], dq[EC_PACKED];
-  ec_recode_w10(dg, u1);
-  ec_recode_w6(dq, u2);
-  Jac R;
-  jac_set_inf<C>(R, K);
-  for (int i = EC_WINDOWS - 1; i >= 0; --i) {
-    if (i != EC_WINDOWS - 1) {
-#pragma unroll 1
-      for (int d = 0; d < EC_W; ++d) jac_dbl<C>(R, R);
-    }
-#pragma unroll 1
-    for (int j = 0; j < EC_ROWS; ++j) {
-      const int t = EC_WINDOWS * j + i;
-      if (t >= EC_DIGITS) continue;
-      const int b = ec_digit6(dq, t);
-      if (b != 0) {
-        f29 x, y;
-        ec_pick(x, y, TQ.t[j], b < 0 ? -b : b);
-        if (b < 0) m29_neg<C, 0>(y, y);
-        jac_madd<C>(R, R, x, y, K);
-      }
-    }
-    const int u_lo = (i * EC_G_DIGITS + EC_WINDOWS - 1) / EC_WINDOWS;
-    const int u_hi = ((i + 1) * EC_G_DIGITS + EC_WINDOWS - 1) / EC_WINDOWS;
-#pragma unroll 1
-    for (int u = u_lo; u < u_hi; ++u) {
-      const int a = ec_digit10(dg, u);
-      if (a != 0) {
-        f29 x, y;
-        ec_pick(x, y, TG.t[u], a < 0 ? -a : a);
-        if (a < 0) m29_neg<C, 0>(y, y);
-        jac_madd<C>(R, R, x, y, K);
-      }
-    }
-  }
-  return ecdsa_x_check<C>(R, r, K);
-}
-
-// The same check for a key that has only row 0 of its table (few items in the batch,
-// keyws.h): Horner over u2's 43 signed radix-64 digits (252 doublings); G row u is added at
-// digit position ec_g_window(u) < EC_WINDOWS, which is followed by exactly the EC_W * window
-// doublings its row scale expects (as in ecdsa_ladder_check).
-template <int C, class TabG>
-CG_HD uint32_t ecdsa_ladder_check_row0(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG,
-                                       const EcAff* row0, const EcConsts& K) {
-  uint32_t dg[EC_G_PACKED], dq[EC_PACKED];
-  ec_recode_w10(dg, u1);
-  ec_recode_w6(dq, u2);
-  Jac R;
-  jac_set_inf<C>(R, K);
-#pragma unroll 1
-  for (int t = EC_DIGITS - 1; t >= 0; --t) {
-    if (t != EC_DIGITS - 1) {
-#pragma unroll 1
-      for (int d = 0; d < EC_W; ++d) jac_dbl<C>(R, R);
-    }
-    const int b = ec_digit6(dq, t);
-    if (b != 0) {
-      f29 x, y;
-      ec_pick(x, y, row0, b < 0 ? -b : b);
-      if (b < 0) m29_neg<C, 0>(y, y);
-      jac_madd<C>(R, R, x, y, K);
-    }
-    if (t < EC_WINDOWS) {
-      const int u_lo = (t * EC_G_DIGITS + EC_WINDOWS - 1) / EC_WINDOWS;
-      const int u_hi = ((t + 1) * EC_G_DIGITS + EC_WINDOWS - 1) / EC_WINDOWS;
-#pragma unroll 1
-      for (int u = u_lo; u < u_hi; ++u) {
-        const int a = ec_digit10(dg, u);
-        if (a != 0) {
-          f29 x, y;
-          ec_pick(x, y, TG.t[u], a < 0 ? -a : a);
-          if (a < 0) m29_neg<C, 0>(y, y);
-          jac_madd<C>(R, R, x, y, K);
-        }
-      }
-    }
-  }
-  return ecdsa_x_check<C>(R, r, K);
-}
-
-// G rows (per context) from the curve constants.
-template <int C>
-CG_HD void ec_g_rows_init(EcRowTab& T, EcRowScratch& s, const EcConsts& K) {
-  Jac bases[EC_ROWS];
-  ec_row_bases<C>(bases, K.gx, K.gy, K);
-  for (int j = 0; j < EC_ROWS; ++j) ec_row_build<C>(T.t[j], bases[j], s, K);
-}
-
 // ---------------------------------------------------------------- wide tables (hot keys)
 // A key with many items in the call (keyws.h KEY_WIDE_MIN_USES) gets one row per signed
 // radix-2^8 digit of u2: row j holds the affine multiples 1..128 of 2^{8j} Q. The top digit
@@ -709,6 +615,82 @@ CG_HD void m29_batch_invert_small(f29* out, const f29* t, const EcConsts& K) {
     m29_mul<C, 0>(inv, inv, t[g]);
   }
   out[0] = inv;
+}
+
+// u1 G over the constant radix-2^EC_WIDE_GW table (no doublings needed: added after the Q part)
+template <int C, class TabG>
+CG_HD void ec_add_g_wide(Jac& R, const u256w& u1, const TabG& TG, const EcConsts& K) {
+  uint32_t dg[EC_WIDE_GPACKED];
+  ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS, false, EC_WIDE_GBITS>(dg, u1);
+#pragma unroll 1
+  for (int u = 0; u < EC_WIDE_GDIGITS; ++u) {
+    const int a = ec_digit_at<EC_WIDE_GBITS>(dg, u);
+    if (a != 0) {
+      f29 x, y;
+      ec_pick(x, y, TG.t[u], a < 0 ? -a : a);
+      if (a < 0) m29_neg<C, 0>(y, y);
+      jac_madd<C>(R, R, x, y, K);
+    }
+  }
+}
+
+// Stage 3: R = u2 Q + u1 G (Q over the per-key radix-64 rows in EC_WINDOWS windows, then G over
+// the constant wide table: 43 + 12 mixed additions, 18 doublings; the round-1 radix-2^10 G table
+// spread 26 additions over the windows), then the x-check. Returns 0 VALID / 1 INVALID.
+template <int C, class TabG, class TabQ>
+CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG, const TabQ& TQ,
+                                  const EcConsts& K) {
+  uint32_t dq[EC_PACKED];
+  ec_recode_w6(dq, u2);
+  Jac R;
+  jac_set_inf<C>(R, K);
+  for (int i = EC_WINDOWS - 1; i >= 0; --i) {
+    if (i != EC_WINDOWS - 1) {
+#pragma unroll 1
+      for (int d = 0; d < EC_W; ++d) jac_dbl<C>(R, R);
+    }
+#pragma unroll 1
+    for (int j = 0; j < EC_ROWS; ++j) {
+      const int t = EC_WINDOWS * j + i;
+      if (t >= EC_DIGITS) continue;
+      const int b = ec_digit6(dq, t);
+      if (b != 0) {
+        f29 x, y;
+        ec_pick(x, y, TQ.t[j], b < 0 ? -b : b);
+        if (b < 0) m29_neg<C, 0>(y, y);
+        jac_madd<C>(R, R, x, y, K);
+      }
+    }
+  }
+  ec_add_g_wide<C>(R, u1, TG, K);
+  return ecdsa_x_check<C>(R, r, K);
+}
+
+// The same check for a key that has only row 0 of its table (few items in the batch,
+// keyws.h): Horner over u2's 43 signed radix-64 digits (252 doublings), then u1 G as above.
+template <int C, class TabG>
+CG_HD uint32_t ecdsa_ladder_check_row0(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG,
+                                       const EcAff* row0, const EcConsts& K) {
+  uint32_t dq[EC_PACKED];
+  ec_recode_w6(dq, u2);
+  Jac R;
+  jac_set_inf<C>(R, K);
+#pragma unroll 1
+  for (int t = EC_DIGITS - 1; t >= 0; --t) {
+    if (t != EC_DIGITS - 1) {
+#pragma unroll 1
+      for (int d = 0; d < EC_W; ++d) jac_dbl<C>(R, R);
+    }
+    const int b = ec_digit6(dq, t);
+    if (b != 0) {
+      f29 x, y;
+      ec_pick(x, y, row0, b < 0 ? -b : b);
+      if (b < 0) m29_neg<C, 0>(y, y);
+      jac_madd<C>(R, R, x, y, K);
+    }
+  }
+  ec_add_g_wide<C>(R, u1, TG, K);
+  return ecdsa_x_check<C>(R, r, K);
 }
 
 // R = u1 G + u2 Q over the wide tables, then BC's x-check. Returns 0 VALID / 1 INVALID.

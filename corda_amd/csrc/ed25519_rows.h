@@ -608,3 +608,84 @@ CG_HD void fe_invert_run(fe* z, fe* pre) {
   }
   fe_copy(z[0], inv);
 }
+
+// ---------------------------------------------------------------- full / row-0 tables + wide B
+// R' = h (-A) + S' B for keys with full tables (W/K rows of -A, K windows, (K-1) W doublings) or
+// row 0 only (Horner, 252 doublings), with S' B from the constant radix-2^ED_WIDE_BW table at the
+// end: the B digits need no doublings, so they all go after the last window (12 additions instead
+// of the 26 of the round-1 radix-2^10 table spread over the windows). `Signed`: entries by |digit|,
+// the sign through ge_madd_signed (the form k_ed_ladder_pf runs).
+template <bool Signed, class PickB>
+CG_HD void ed_add_b_wide(ge_p3& R, ge_p1p1& t, ge_p2& q, const uint32_t* esb, const EdBWideTab& TB, PickB pick_b,
+                         bool last_to_p2) {
+  for (int u = 0; u < EdWideCfg::kBDigits; ++u) {
+    const int dg = sc_digit_at<EdWideCfg::kBBits>(esb, u);
+    const int dp = Signed && dg < 0 ? -dg : dg;
+    ge_niels n;
+    pick_b(n, TB.t[u], dp);
+    if (Signed) ge_madd_signed(t, R, n, dg < 0);
+    else ge_madd(t, R, n);
+    if (last_to_p2 && u + 1 == EdWideCfg::kBDigits) ge_p1p1_to_p2(q, t);
+    else ge_p1p1_to_p3(R, t);
+  }
+}
+
+template <int W, int K, bool Signed = false, class RowA, class PickA, class PickB>
+CG_HD void ed_double_scalar_fw(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const RowA& TA,
+                               const EdBWideTab& TB, PickA pick_a, PickB pick_b) {
+  typedef EdRowsCfg<W, K> C;
+  ge_p3 R;
+  ge_p3_0(R);
+  ge_p1p1 t;
+  ge_p2 q;
+  for (int i = K - 1; i >= 0; --i) {
+    if (i != K - 1) {  // R arrives as p2 (q) from the previous window's last addition
+      for (int d = 0; d < W - 1; ++d) {
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+      }
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(R, t);
+    }
+    const int n_a = (C::kDigits - i + K - 1) / K;  // rows with a digit in this window
+    for (int k = 0; k < n_a; ++k) {
+      const int dg = sc_digit_b(eh, K * k + i);
+      const int dp = Signed && dg < 0 ? -dg : dg;
+      ge_niels n;
+      pick_a(n, TA.t[k], dp);
+      if (Signed) ge_madd_signed(t, R, n, dg < 0);
+      else ge_madd(t, R, n);
+      if (i != 0 && k + 1 == n_a) ge_p1p1_to_p2(q, t);  // next: doublings, which need no T
+      else ge_p1p1_to_p3(R, t);
+    }
+  }
+  ed_add_b_wide<Signed>(R, t, q, esb, TB, pick_b, true);
+  out = q;
+}
+
+template <int W, int K, class PickA, class PickB>
+CG_HD void ed_double_scalar_row0w(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const ge_niels* row0,
+                                  const EdBWideTab& TB, PickA pick_a, PickB pick_b) {
+  typedef EdRowsCfg<W, K> C;
+  ge_p3 R;
+  ge_p3_0(R);
+  ge_p1p1 t;
+  ge_p2 q;
+  for (int td = C::kDigits - 1; td >= 0; --td) {
+    if (td != C::kDigits - 1) {
+      for (int d = 0; d < W - 1; ++d) {
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p2(q, t);
+      }
+      ge_p2_dbl(t, q);
+      ge_p1p1_to_p3(R, t);
+    }
+    ge_niels n;
+    pick_a(n, row0, sc_digit_b(eh, td));
+    ge_madd(t, R, n);
+    if (td != 0) ge_p1p1_to_p2(q, t);
+    else ge_p1p1_to_p3(R, t);
+  }
+  ed_add_b_wide<false>(R, t, q, esb, TB, pick_b, true);
+  out = q;
+}

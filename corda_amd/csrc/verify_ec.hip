@@ -261,7 +261,7 @@ template <int C, bool Full>
 __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
                                                    const uint32_t* __restrict__ ranges,
                                                    const TabSlot* __restrict__ tabs,
-                                                   const EcGTab* __restrict__ gtab, uint8_t* __restrict__ status,
+                                                   const EcGWideTab* __restrict__ gtab, uint8_t* __restrict__ status,
                                                    const EcItemWs* __restrict__ ws) {
   const int cls = plan_class_of_curve(C);  // the plan's mode split (plan_sort.hip)
   const uint32_t beg = Full ? ranges[PLAN_FULL + cls] : ranges[cls];
@@ -408,7 +408,7 @@ static void launch_ladder_t(const cg_item* d_items, uint64_t n_items, uint8_t* d
                             const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
   hipLaunchKernelGGL((k_ec_ladder<C, Full>), dim3(walk_grid(n_items, B, WALK_CAP(2))), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
-                     w.tab, gtab(d_btab, C), d_status, (const EcItemWs*)iw.slots);
+                     w.tab, gwide(d_btab, C), d_status, (const EcItemWs*)iw.slots);
 }
 
 void ec_launch_ladder(int curve, bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status,

@@ -298,9 +298,9 @@ __device__ __forceinline__ void pick(ge_niels& out, const ge_niels* row, int d) 
 
 // Digits handed from k_ed_hash to k_ed_ladder through the item slot (the ladder reads them
 // before it writes R' into the same slot).
-struct EdDigits {
-  uint32_t eh[EdCfg::kPackedWords], es[EdBCfgT::kPackedWords];
-  uint32_t pad[(ITEM_SLOT - 4 * (EdCfg::kPackedWords + EdBCfgT::kPackedWords)) / 4];
+struct EdDigits {  // h in radix 2^6 (int8), S' in radix 2^ED_WIDE_BW (the wide B table's digits)
+  uint32_t eh[EdCfg::kPackedWords], es[EdWideCfg::kBPackedWords];
+  uint32_t pad[(ITEM_SLOT - 4 * (EdCfg::kPackedWords + EdWideCfg::kBPackedWords)) / 4];
 };
 static_assert(sizeof(EdDigits) == ITEM_SLOT, "digits must fill one item slot");
 // the same hand-off for an item of a wide-table key: h in radix 2^8, S' in radix 2^12
@@ -369,7 +369,7 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
     } else {
       EdDigits d;
       sc_recode_w<ED_W>(d.eh, EdCfg::kPackedWords, h);
-      sc_recode_w16<ED_WB>(d.es, EdBCfgT::kPackedWords, sr);
+      sc_recode_wb<ED_WIDE_BW, EdWideCfg::kBBits>(d.es, EdWideCfg::kBPackedWords, sr);
       dig[p] = d;
     }
     st = (uint8_t)ED_PENDING;
@@ -398,8 +398,8 @@ struct PickGlobal {
 #endif
 
 // ---------------------------------------------------------------- pipelined full-table ladder
-// The 69 mixed additions of ed_double_scalar_wb as one flat op sequence (window 1: 21 A rows +
-// B rows 13..25; 6 doublings; window 0: 22 A rows + B rows 0..12). Op o+1's niels entry is
+// The 55 mixed additions of ed_double_scalar_fw as one flat op sequence (window 1: 21 A rows;
+// 6 doublings; window 0: 22 A rows, then the 12 radix-2^22 B rows). Op o+1's niels entry is
 // gathered straight into LDS (global_load_lds, no VGPR destination) while op o's addition
 // runs, and op o+2's digit word is loaded at the same time: the two dependent memory latencies
 // per op (digit, then entry) leave the critical path. LDS image per wave: 7 x 16-B chunks then
@@ -412,9 +412,8 @@ typedef __attribute__((address_space(1))) void* cg_gbl_ptr;
 struct EdOps {
   static constexpr int kNa1 = (EdCfg::kDigits - 1 + ED_K - 1) / ED_K;  // A rows, window 1
   static constexpr int kNa0 = (EdCfg::kDigits + ED_K - 1) / ED_K;      // A rows, window 0
-  static constexpr int kUlo1 = (EdBCfgT::kDigits + ED_K - 1) / ED_K;   // B rows [kUlo1, kDigits): window 1
-  static constexpr int kOps1 = kNa1 + (EdBCfgT::kDigits - kUlo1);
-  static constexpr int kOps = kOps1 + kNa0 + kUlo1;
+  static constexpr int kOps1 = kNa1;
+  static constexpr int kOps = kNa1 + kNa0 + EdWideCfg::kBDigits;
   static constexpr uint32_t kWaveBytes = 64 * sizeof(ge_niels);
 };
 static_assert(ED_K == 2, "the flat op sequence is written for 2 windows");
@@ -422,26 +421,27 @@ static_assert(sizeof(ge_niels) == 120, "LDS chunking assumes 120-B niels entries
 
 // op o -> (digit word index in EdDigits, shift, B?, row)
 __device__ __forceinline__ void ed_op_info(int o, int& widx, int& sh, bool& is_b, int& row) {
-  const bool w1 = o < EdOps::kOps1;
-  const int k = w1 ? o : o - EdOps::kOps1;
-  const int n_a = w1 ? EdOps::kNa1 : EdOps::kNa0;
-  if (k < n_a) {
+  if (o < EdOps::kNa1 + EdOps::kNa0) {
+    const bool w1 = o < EdOps::kOps1;
+    const int k = w1 ? o : o - EdOps::kOps1;
     const int t = ED_K * k + (w1 ? 1 : 0);
     widx = t >> 2;
     sh = (t & 3) * 8;
     is_b = false;
     row = k;
   } else {
-    const int u = (w1 ? EdOps::kUlo1 : 0) + k - n_a;
-    widx = EdCfg::kPackedWords + (u >> 1);
-    sh = (u & 1) * 16;
+    constexpr int per = 32 / EdWideCfg::kBBits;
+    const int u = o - EdOps::kNa1 - EdOps::kNa0;
+    widx = EdCfg::kPackedWords + u / per;
+    sh = (u % per) * EdWideCfg::kBBits;
     is_b = true;
     row = u;
   }
 }
 
 __device__ __forceinline__ int ed_op_digit(uint32_t w, int sh, bool is_b) {
-  return is_b ? (int)(int16_t)(uint16_t)(w >> sh) : (int)(int8_t)(uint8_t)(w >> sh);
+  if (!is_b) return (int)(int8_t)(uint8_t)(w >> sh);
+  return EdWideCfg::kBBits == 16 ? (int)(int16_t)(uint16_t)(w >> sh) : (int)w;
 }
 
 // wave_lds_off: the wave's LDS image as a wave-uniform LDS byte offset (readfirstlane'd once
@@ -472,14 +472,14 @@ __device__ __forceinline__ void ed_lds_niels(ge_niels& n, const uint8_t* wave_ld
   d[29] = *(const uint32_t*)(wave_lds + 64 * 116 + 4 * lane);
 }
 
-__device__ __forceinline__ const ge_niels* ed_op_src(const EdTab& TA, const EdBTab& TB, bool is_b, int row, int d) {
+__device__ __forceinline__ const ge_niels* ed_op_src(const EdTab& TA, const EdBWideTab& TB, bool is_b, int row, int d) {
   const int a = d < 0 ? -d : d;
   const int idx = a > 0 ? a - 1 : 0;
   return is_b ? &TB.t[row][idx] : &TA.t[row][idx];
 }
 
 __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* __restrict__ dw, const EdTab& TA,
-                                                    const EdBTab& TB, uint8_t* wave_lds, uint32_t lane) {
+                                                    const EdBWideTab& TB, uint8_t* wave_lds, uint32_t lane) {
   constexpr int N = EdOps::kOps;
   const uint32_t wl = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(cg_lds_ptr)wave_lds);
   int widx, sh, row;
@@ -541,7 +541,7 @@ __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* 
 #endif
 __global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_pf(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
-    const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBTab* __restrict__ btab,
+    const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBWideTab* __restrict__ btab,
     uint8_t* __restrict__ status, void* __restrict__ slots) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[4 * EdOps::kWaveBytes];
   const uint32_t beg = ranges[PLAN_FULL + PLAN_ED];
@@ -661,7 +661,7 @@ __global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_wide(
 template <bool Full>
 __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
-    const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBTab* __restrict__ btab,
+    const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBWideTab* __restrict__ btab,
     uint8_t* __restrict__ status, void* __restrict__ slots) {
   // the plan's mode split: row-0 keys' items first, then full-table keys' (plan_sort.hip)
   const uint32_t beg = Full ? ranges[PLAN_FULL + PLAN_ED] : ranges[PLAN_ED];
@@ -678,9 +678,9 @@ __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
     const EdDigits d = ((const EdDigits*)slots)[p];
     ge_p2 q;
     if (Full) {
-      ed_double_scalar_wb<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed, *btab, PickGlobal(), PickGlobal());
+      ed_double_scalar_fw<ED_W, ED_K>(q, d.eh, d.es, tabs[key].ed, *btab, PickGlobal(), PickGlobal());
     } else {  // a key with few items: row 0 only (keyws.h)
-      ed_double_scalar_row0<ED_W, ED_K, ED_WB>(q, d.eh, d.es, tabs[key].ed.t[0], *btab, PickGlobal(), PickGlobal());
+      ed_double_scalar_row0w<ED_W, ED_K>(q, d.eh, d.es, tabs[key].ed.t[0], *btab, PickGlobal(), PickGlobal());
     }
     ((ge_p2*)slots)[p] = q;
   }
@@ -819,13 +819,13 @@ void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8
   const unsigned grid = walk_grid(n_items, B, WALK_CAP(full && ED_LADDER_PF ? ED_LADDER_PF_WAVES : ED_LADDER_WAVES_PER_SIMD));
   if (full && ED_LADDER_PF)
     hipLaunchKernelGGL(k_ed_ladder_pf, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                       w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+                       w.tab, bwide(d_btab), d_status, iw.slots);
   else if (full)
     hipLaunchKernelGGL(k_ed_ladder<true>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                       w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+                       w.tab, bwide(d_btab), d_status, iw.slots);
   else
     hipLaunchKernelGGL(k_ed_ladder<false>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
-                       w.hdr, w.tab, (const EdBTab*)d_btab, d_status, iw.slots);
+                       w.hdr, w.tab, bwide(d_btab), d_status, iw.slots);
 }
 
 void ed_launch_ladder_wide(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,

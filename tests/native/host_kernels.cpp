@@ -270,6 +270,48 @@ extern "C" int t_ed_count_w6(const uint32_t* aw, const uint32_t* sw, const uint8
 
 // ---------------------------------------------------------------- ECDSA rows (v2 pipeline)
 #include "../../corda_amd/csrc/ecdsa_rows.h"
+// The constant radix-2^22 G table (1.8 GB per curve): the host builds, with the device lane's code
+// (ec_gwide_group_from), only the groups of 32 multiples the u1 digits touch.
+template <int C>
+static EcGWideTab* ec_gwide_host() {
+  static EcGWideTab* TG = nullptr;
+  if (!TG) TG = new EcGWideTab;
+  return TG;
+}
+template <int C>
+static void ec_gwide_touch(const u256w& u1) {
+  constexpr int GG = EC_WIDE_GMULT / EC_MULT;
+  static std::vector<bool> built;
+  static Jac base[EC_WIDE_GDIGITS];  // 2^{22u} G
+  static EcRowScratch* S = new EcRowScratch;
+  const EcConsts& K = g_K[C];
+  if (built.empty()) {
+    built.assign(EC_WIDE_GDIGITS * GG, false);
+    Jac P = {K.gx, K.gy, K.one_p};
+    for (int u = 0; u < EC_WIDE_GDIGITS; ++u) {
+      if (u > 0) jac_dbl_n<C>(P, P, EC_WIDE_GW);
+      base[u] = P;
+    }
+  }
+  EcGWideTab* TG = ec_gwide_host<C>();
+  uint32_t dg[EC_WIDE_GPACKED];
+  ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS, false, EC_WIDE_GBITS>(dg, u1);
+  for (int u = 0; u < EC_WIDE_GDIGITS; ++u) {
+    const int d = ec_digit_at<EC_WIDE_GBITS>(dg, u), a = d < 0 ? -d : d;
+    if (a == 0 || built[u * GG + (a - 1) / EC_MULT]) continue;
+    const int g = (a - 1) / EC_MULT;
+#ifdef FE_OP_COUNT
+    const uint64_t m0 = g_m29_nmul[C][0], m1 = g_m29_nmul[C][1];  // table build: not item work
+#endif
+    ec_gwide_group_from<C>(&TG->t[u][g * EC_MULT], base[u], g, *S, K);
+#ifdef FE_OP_COUNT
+    g_m29_nmul[C][0] = m0;
+    g_m29_nmul[C][1] = m1;
+#endif
+    built[u * GG + g] = true;
+  }
+}
+
 template <int C>
 static int ecdsa_rows_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off, uint32_t key_len, uint32_t fmt,
                              uint64_t sig_off, uint32_t sig_len, uint64_t msg_off, uint64_t msg_len) {
@@ -294,7 +336,9 @@ static int ecdsa_rows_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
   st = ecdsa_prep<C>(ws, arena, lr, sig_off, sig_len, arena, lr, msg_off, msg_len);
   if (st) return (int)st;
   ecdsa_batch_inv<C, 1>(&ws, 1, 1u, K);
-  return (int)ecdsa_ladder_check<C>(ws.a, ws.b, ws.r, *TG[C], *TQ, K);
+  kinit();
+  ec_gwide_touch<C>(ws.a);
+  return (int)ecdsa_ladder_check<C>(ws.a, ws.b, ws.r, *ec_gwide_host<C>(), *TQ, K);
 }
 // Executed Montgomery products per ECDSA item and stage (the GPU path's own lane code, host build):
 // out[0..1] k_ec_prep (mod p, mod n), out[2..3] k_ec_inv per item (one shared inversion over 16
@@ -334,7 +378,8 @@ static int ecdsa_count(const uint8_t* arena, uint64_t lr, uint64_t key_off, uint
   for (int k = 1; k < EC_INV_K; ++k) ws[k] = ws[0];
   ecdsa_batch_inv<C, EC_INV_K>(ws, EC_INV_K, (1u << EC_INV_K) - 1u, K);
   snap(out + 2);
-  st = ecdsa_ladder_check<C>(ws[0].a, ws[0].b, ws[0].r, *TG, *TQ, K);
+  ec_gwide_touch<C>(ws[0].a);
+  st = ecdsa_ladder_check<C>(ws[0].a, ws[0].b, ws[0].r, *ec_gwide_host<C>(), *TQ, K);
   snap(out + 4);
   return (int)st;
 #else
@@ -397,6 +442,10 @@ extern "C" void t_m29_op(int curve, int n, int op, const uint32_t* a, const uint
 }
 
 // ---------------------------------------------------------------- Ed25519 rows + radix-2^10 B
+struct EdBWideTab;
+static void tbw_init();
+static void tbw_touch(const uint32_t* es);
+static EdBWideTab* g_TBW = nullptr;
 static EdBTabW<ED_W, ED_K, ED_WB>* g_TB10 = nullptr;
 static void tb10_init() {
   if (g_TB10) return;
@@ -448,14 +497,16 @@ static int ed_verify_wb(const uint32_t* aw, const uint32_t* sw, const uint8_t* m
     for (int i = 0; i < 8; ++i) r1[i] = sc_R1w(i);
     sc_sub(sr, sr, r1);
   }
-  uint32_t eh[C::kPackedWords], es[CB::kPackedWords];
+  uint32_t eh[C::kPackedWords], es[EdWideCfg::kBPackedWords];
   sc_recode_w<ED_W>(eh, C::kPackedWords, h);
-  sc_recode_w16<ED_WB>(es, CB::kPackedWords, sr);
+  sc_recode_wb<ED_WIDE_BW, EdWideCfg::kBBits>(es, EdWideCfg::kBPackedWords, sr);
+  tbw_init();
+  tbw_touch(es);
   ge_p2 R;
 #ifdef FE_OP_COUNT
   g_fe_nmul = g_fe_nsq = 0;
 #endif
-  ed_double_scalar_wb<ED_W, ED_K, ED_WB, Signed>(R, eh, es, TA, *g_TB10, host_pick, host_pick);
+  ed_double_scalar_fw<ED_W, ED_K, Signed>(R, eh, es, TA, *g_TBW, host_pick, host_pick);
 #ifdef FE_OP_COUNT
   if (counts) {
     counts[0] = g_fe_nmul;
@@ -482,7 +533,6 @@ extern "C" int t_ed_verify_wb_signed(const uint32_t* aw, const uint32_t* sw, con
 // k_ed_wide_chain / k_ed_wide_tab / k_ed_bwide_init / k_ed_ladder_wide's arithmetic, bounds-checked.
 // The constant B table is 62.9 MB (radix 2^16): the host builds, with the device lane's code
 // (ed_bwide_group), only the groups of 8 multiples an item's digits touch.
-static EdBWideTab* g_TBW = nullptr;
 static std::vector<bool> g_TBW_built;
 static ge_p3 g_TBW_base[EdWideCfg::kBDigits];  // 2^{16u} B
 static void tbw_init() {

@@ -280,7 +280,57 @@ __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ i
   }
 }
 
-// the items of wide-table keys (ecdsa_rows.h ecdsa_ladder_check_wide)
+// The items of wide-table keys: ecdsa_ladder_check_wide's 32 Q rows then 12 G rows as one flat op
+// sequence, each op's affine entry gathered straight into LDS one op ahead (global_load_lds, as
+// k_ed_ladder_wide; the 1.8 GB G table's HBM latency and the Q rows' L2 latency leave the critical
+// path; the plain-load form issued 0.86 / 0.93 of its time for r1 / k1). LDS image per wave: 4 x 16-B
+// chunks then 2 x 4-B chunks of the 72-B entry, chunk c of lane l at wave_base + 64 * off_c +
+// size_c * l (the DMA's lane-linear destination), 4608 B per wave.
+typedef __attribute__((address_space(3))) void* ec_lds_ptr;
+typedef __attribute__((address_space(1))) void* ec_gbl_ptr;
+static_assert(sizeof(EcAff) == 72, "LDS chunking assumes 72-B affine entries");
+#define EC_WAVE_LDS (64 * 72)
+#define EC_WIDE_OPS (EC_WIDE_DIGITS + EC_WIDE_GDIGITS)
+
+__device__ __forceinline__ ec_lds_ptr ec_lds_at(uint32_t wave_lds_off, uint32_t b) {
+  return (ec_lds_ptr)(uintptr_t)(wave_lds_off + b);
+}
+__device__ __forceinline__ void ec_glds_aff(const EcAff* src, uint32_t wl) {
+  const uint8_t* s = (const uint8_t*)src;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    __builtin_amdgcn_global_load_lds((ec_gbl_ptr)(s + 16 * c), ec_lds_at(wl, 64 * 16 * c), 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((ec_gbl_ptr)(s + 64), ec_lds_at(wl, 64 * 64), 4, 0, 0);
+  __builtin_amdgcn_global_load_lds((ec_gbl_ptr)(s + 68), ec_lds_at(wl, 64 * 68), 4, 0, 0);
+}
+__device__ __forceinline__ void ec_lds_aff(f29& x, f29& y, const uint8_t* wave_lds, uint32_t lane) {
+  uint32_t d[18];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint4 v = *(const uint4*)(wave_lds + 64 * 16 * c + 16 * lane);
+    d[4 * c] = v.x;
+    d[4 * c + 1] = v.y;
+    d[4 * c + 2] = v.z;
+    d[4 * c + 3] = v.w;
+  }
+  d[16] = *(const uint32_t*)(wave_lds + 64 * 64 + 4 * lane);
+  d[17] = *(const uint32_t*)(wave_lds + 64 * 68 + 4 * lane);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    x.v[i] = d[i];
+    y.v[i] = d[9 + i];
+  }
+}
+// op o's digit and entry (Q row o, or row 32 for the top digit's 129..256; then G row o - 32)
+__device__ __forceinline__ int ec_wide_digit(const uint32_t* dq, const uint32_t* dg, int o) {
+  return o < EC_WIDE_DIGITS ? ec_digit10(dq, o) : ec_digit_at<EC_WIDE_GBITS>(dg, o - EC_WIDE_DIGITS);
+}
+__device__ __forceinline__ const EcAff* ec_wide_src(const EcWideTab& TQ, const EcGWideTab& TG, int o, int d) {
+  const int a = d < 0 ? -d : d;
+  if (o < EC_WIDE_DIGITS) return a > EC_WIDE_MULT ? &TQ.t[EC_WIDE_DIGITS][a - EC_WIDE_MULT - 1] : &TQ.t[o][a > 0 ? a - 1 : 0];
+  return &TG.t[o - EC_WIDE_DIGITS][a > 0 ? a - 1 : 0];
+}
+
 template <int C>
 __global__ void __launch_bounds__(256) k_ec_ladder_wide(const cg_item* __restrict__ items,
                                                         const uint32_t* __restrict__ perm,
@@ -289,15 +339,46 @@ __global__ void __launch_bounds__(256) k_ec_ladder_wide(const cg_item* __restric
                                                         const EcWideSlot* __restrict__ wec,
                                                         const EcGWideTab* __restrict__ gw, uint8_t* __restrict__ status,
                                                         const EcItemWs* __restrict__ ws) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4 * EC_WAVE_LDS];
   const int cls = plan_class_of_curve(C);
   const uint32_t beg = ranges[PLAN_WIDE + cls], end = ranges[cls + 1];
+  uint8_t* wave_lds = stage + (threadIdx.x >> 6) * EC_WAVE_LDS;
+  const uint32_t wl = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(ec_lds_ptr)wave_lds);
+  const uint32_t lane = __lane_id();
+  const EcConsts& K = c_ec[C];
   for (Walk wk = walk_units(end - beg); wk.u < wk.end; wk.u += wk.step) {
     const uint64_t p = beg + wk.u;
     const uint32_t i = perm[p];
     if (status[i] != EC_PENDING_BASE + C) continue;
+    // every lane still here runs the same DMA sequence; lanes that left do not take part, and the
+    // LDS image is per lane, so no barrier is needed
     const uint32_t key = items[i].key_idx;
     const EcItemWs w = ws[p];
-    status[i] = (uint8_t)ecdsa_ladder_check_wide<C>(w.a, w.b, w.r, *gw, wec[wide_idx[key]].tab, c_ec[C]);
+    const EcWideTab& TQ = wec[wide_idx[key]].tab;
+    uint32_t dg[EC_WIDE_GPACKED], dq[EC_WIDE_PACKED];
+    ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS, false, EC_WIDE_GBITS>(dg, w.a);
+    ec_recode_wide<EC_WIDE_W, EC_WIDE_DIGITS, true>(dq, w.b);
+    Jac R;
+    jac_set_inf<C>(R, K);
+    int d_next = ec_wide_digit(dq, dg, 0);
+    ec_glds_aff(ec_wide_src(TQ, *gw, 0, d_next), wl);
+#pragma unroll 1
+    for (int o = 0; o < EC_WIDE_OPS; ++o) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // op o's entry
+      f29 x, y;
+      ec_lds_aff(x, y, wave_lds, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
+      const int d = d_next;
+      if (o + 1 < EC_WIDE_OPS) {
+        d_next = ec_wide_digit(dq, dg, o + 1);
+        ec_glds_aff(ec_wide_src(TQ, *gw, o + 1, d_next), wl);
+      }
+      if (d != 0) {
+        if (d < 0) m29_neg<C, 0>(y, y);
+        jac_madd<C>(R, R, x, y, K);
+      }
+    }
+    status[i] = (uint8_t)ecdsa_x_check<C>(R, w.r, K);
   }
 }
 

@@ -25,7 +25,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = ("k_ed_hash", "k_ed_ladder_pf", "k_ed_ladder_wide", "k_ed_finish", "k_ec_prep<1>", "k_ec_inv<1>",
            "k_ec_ladder<1, true>", "k_ec_ladder_wide<1>", "k_ec_prep<0>", "k_ec_inv<0>", "k_ec_ladder<0, true>",
            "k_ec_ladder_wide<0>", "k_ed_wide_fwd", "k_ed_wide_inv", "k_ed_wide_bwd", "k_ec_wide_fwd<1>",
-           "k_ec_wide_bwd<1>", "k_ec_wide_fwd<0>", "k_ec_wide_bwd<0>")
+           "k_ec_wide_bwd<1>", "k_ec_wide_fwd<0>", "k_ec_wide_bwd<0>", "k_ec_wide_inv<1>", "k_ec_wide_inv<0>",
+           # configs[3] transaction pipeline (tools/profile_tx.sh)
+           "k_tx_map", "k_tx_leaf_count", "k_tx_leaf_scatter", "k_tx_leaves", "k_tx_roots", "k_txsig_items", "k_splice")
 
 
 def short(name):
@@ -115,9 +117,10 @@ def main():
            "valu_issue": {n: k["valu"] for n, k in kern.items() if "valu" in k}}
     with open(os.path.join(dest, "pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
-    os.makedirs(os.path.join(ROOT, "profiles", "r02"), exist_ok=True)
-    with open(os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"), "w") as f:
-        json.dump(out, f, indent=1)
+    if os.environ.get("PMC_TRAFFIC_HEADLINE", "1") == "1":  # the file bench.py's roofline reads
+        os.makedirs(os.path.join(ROOT, "profiles", "r02"), exist_ok=True)
+        with open(os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"), "w") as f:
+            json.dump(out, f, indent=1)
     print(json.dumps({n: (k.get("hbm_bytes_per_launch"), k.get("valu", {}).get("issue_frac"),
                           k.get("trace", {}).get("avg_ms")) for n, k in kern.items()}))
 

@@ -329,8 +329,15 @@ uint64_t wl_ed25519_arena_bytes(uint64_t n_items, uint32_t n_keys, uint32_t msg_
 
 namespace {
 EcConsts g_K[2];
-EcRowTab g_GT[2];  // G rows (the verify path's own table construction)
+EcRowTab g_GT[2];  // G rows built with the verify path's row construction (ec_row_bases / ec_row_build)
 bool g_ec_init = false;
+
+template <int C>
+void ec_g_rows_init(EcRowTab& T, EcRowScratch& s, const EcConsts& K) {
+  Jac bases[EC_ROWS];
+  ec_row_bases<C>(bases, K.gx, K.gy, K);
+  for (int j = 0; j < EC_ROWS; ++j) ec_row_build<C>(T.t[j], bases[j], s, K);
+}
 
 void ec_init() {
   if (!g_ec_init) {

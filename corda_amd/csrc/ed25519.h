@@ -47,6 +47,12 @@ CG_HD void ge_niels_identity(ge_niels& c) {
   fe_1(c.ymx);
   fe_0(c.xy2d);
 }
+// the identity as a half-scaled entry (ge_madd_half_signed)
+CG_HD void ge_niels_identity_half(ge_niels& c) {
+  fe_half(c.ypx);
+  fe_half(c.ymx);
+  fe_0(c.xy2d);
+}
 
 // i2p GroupElement(curve, byte[] s): y = s with bit 255 masked (y >= p accepted), x from
 // u/v; no square root -> KEY_INVALID; sign fix-up (x = 0 with sign bit 1 is accepted).
@@ -284,12 +290,24 @@ struct Ed25519Rows {
   EdRowTab B;
 };
 
-// Normalise 8 extended points to affine niels with one inversion (Montgomery's trick).
-CG_HD void ed_niels_batch8(ge_niels out[8], const ge_p3 P[8], const fe& d2) {
-  fe acc[8], inv, t;
+// Normalise 8 extended points to affine niels with one inversion (Montgomery's trick). Half:
+// half-scaled entries ((y+x)/2, (y-x)/2, x y d): the inverse carries the 1/2, so x and y come out
+// halved and x y d = (x/2)(y/2) 4d.
+template <bool Half = false>
+CG_HD void ed_niels_batch8(ge_niels out[8], const ge_p3 P[8], const fe& d2_in) {
+  fe acc[8], inv, t, d2;
   fe_copy(acc[0], P[0].Z);
   for (int k = 1; k < 8; ++k) fe_mul(acc[k], acc[k - 1], P[k].Z);
   fe_invert(inv, acc[7]);
+  if (Half) {
+    fe h;
+    fe_half(h);
+    fe_mul(inv, inv, h);
+    fe_add(d2, d2_in, d2_in);
+    fe_carry(d2);
+  } else {
+    fe_copy(d2, d2_in);
+  }
   for (int k = 7; k >= 0; --k) {
     fe zi;
     if (k > 0) {

@@ -452,15 +452,19 @@ struct EdWideCfg {
 };
 static_assert(253 % ED_WIDE_W != 0 && 253 % ED_WIDE_BW != 0, "the top digit keeps headroom for the carry");
 
+// Both wide tables hold half-scaled niels entries ((y+x)/2, (y-x)/2, x y d), added with
+// ge_madd_half_signed (no doubling of Z and no carry pass per addition); digit 0 adds the
+// half-scaled identity (ge_niels_identity_half).
 struct EdWideTab {
-  ge_niels t[EdWideCfg::kRows][EdWideCfg::kMult];  // t[j][k-1] = k 2^{8j} (-A)
+  ge_niels t[EdWideCfg::kRows][EdWideCfg::kMult];  // t[j][k-1] = k 2^{8j} (-A), half-scaled
 };
 struct EdBWideTab {
-  ge_niels t[EdWideCfg::kBDigits][EdWideCfg::kBMult];  // t[u][k-1] = k 2^{ED_WIDE_BW u} B
+  ge_niels t[EdWideCfg::kBDigits][EdWideCfg::kBMult];  // t[u][k-1] = k 2^{ED_WIDE_BW u} B, half-scaled
 };
 
 // R' = h (-A) + S' B over the wide tables, digits already recoded (eh: radix 2^8, esb: radix
-// 2^ED_WIDE_BW). Entries by |digit|, the sign through ge_madd_signed (the form k_ed_ladder_wide runs).
+// 2^ED_WIDE_BW). Entries by |digit|, the sign through ge_madd_half_signed (the form k_ed_ladder_wide
+// runs; `pick_*` may return any entry for digit 0, which is replaced by the half-scaled identity).
 template <class TabA, class TabB, class PickA, class PickB>
 CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const TabA& TA, const TabB& TB,
                                  PickA pick_a, PickB pick_b) {
@@ -477,7 +481,8 @@ CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t*
     } else {
       pick_a(n, TA.t[o], dp);
     }
-    ge_madd_signed(t, R, n, dg < 0);
+    if (dg == 0) ge_niels_identity_half(n);
+    ge_madd_half_signed(t, R, n, dg < 0);
     if (o + 1 < EdWideCfg::kOps) ge_p1p1_to_p3(R, t);
   }
   ge_p1p1_to_p2(out, t);
@@ -514,7 +519,7 @@ CG_HD void ed_bwide_group(ge_niels* out8, const ge_p3& B, int u, int grp, const 
     ge_add_cached(t, pts[k - 1], c);
     ge_p1p1_to_p3(pts[k], t);
   }
-  ed_niels_batch8(out8, pts, d2);
+  ed_niels_batch8<true>(out8, pts, d2);
 }
 
 // ---------------------------------------------------------------- wide-table build
@@ -534,7 +539,8 @@ CG_HD void ed_bwide_group(ge_niels* out8, const ge_p3& B, int u, int grp, const 
 // the chunk's niels entries from zinv = 1 / (Z_0 Z_1) (straight-line: a loop here was left rolled
 // and put the points in scratch)
 static_assert(ED_WIDE_CHUNK == 2, "ed_wide_chunk_out is written for chunks of 2");
-CG_HD void ed_niels_from(ge_niels& n, const ge_p2& p, const fe& zi, const fe& d2) {
+// zi = 1 / (2 Z) and d4 = 4d give the half-scaled entry
+CG_HD void ed_niels_from(ge_niels& n, const ge_p2& p, const fe& zi, const fe& d4) {
   fe x, y, xy;
   fe_mul(x, p.X, zi);
   fe_mul(y, p.Y, zi);
@@ -543,15 +549,18 @@ CG_HD void ed_niels_from(ge_niels& n, const ge_p2& p, const fe& zi, const fe& d2
   fe_sub(n.ymx, y, x);
   fe_carry(n.ymx);
   fe_mul(xy, x, y);
-  fe_mul(n.xy2d, xy, d2);
+  fe_mul(n.xy2d, xy, d4);
 }
+// zinv = 1 / (2 Z_0 Z_1) (fe_invert_run's 1/2 included)
 CG_HD void ed_wide_chunk_out(ge_niels* out, const ge_p2 pts[ED_WIDE_CHUNK], const fe& zinv, const fe& d2) {
-  fe z1i, z0i;
+  fe z1i, z0i, d4;
+  fe_add(d4, d2, d2);
+  fe_carry(d4);
   fe_mul(z1i, zinv, pts[0].Z);  // 1 / Z_1
   fe_mul(z0i, zinv, pts[1].Z);  // 1 / Z_0
   ge_niels n0, n1;
-  ed_niels_from(n0, pts[0], z0i, d2);
-  ed_niels_from(n1, pts[1], z1i, d2);
+  ed_niels_from(n0, pts[0], z0i, d4);
+  ed_niels_from(n1, pts[1], z1i, d4);
   out[0] = n0;
   out[1] = n1;
 }
@@ -587,7 +596,8 @@ CG_HD void ed_wide_group_pass(ge_niels* out, fe* zc, const ge_p3& P, int g, cons
   }
 }
 
-// in place: z[g] <- 1 / z[g] for the NG products of one row (prefix products in pre[])
+// in place: z[g] <- 1 / (2 z[g]) for the NG products of one row (prefix products in pre[]); the 1/2
+// rides on the single inversion and reaches every z[g] once (half-scaled entries)
 template <int NG>
 CG_HD void fe_invert_run(fe* z, fe* pre) {
   fe run;
@@ -597,8 +607,10 @@ CG_HD void fe_invert_run(fe* z, fe* pre) {
     fe_mul(run, run, z[g]);
     fe_copy(pre[g], run);
   }
-  fe inv;
+  fe inv, h;
   fe_invert(inv, run);
+  fe_half(h);
+  fe_mul(inv, inv, h);
   for (int g = NG - 1; g > 0; --g) {
     fe zg, t;
     fe_copy(zg, z[g]);
@@ -614,7 +626,7 @@ CG_HD void fe_invert_run(fe* z, fe* pre) {
 // row 0 only (Horner, 252 doublings), with S' B from the constant radix-2^ED_WIDE_BW table at the
 // end: the B digits need no doublings, so they all go after the last window (12 additions instead
 // of the 26 of the round-1 radix-2^10 table spread over the windows). `Signed`: entries by |digit|,
-// the sign through ge_madd_signed (the form k_ed_ladder_pf runs).
+// the sign through ge_madd_signed / ge_madd_half_signed (the form k_ed_ladder_pf runs).
 template <bool Signed, class PickB>
 CG_HD void ed_add_b_wide(ge_p3& R, ge_p1p1& t, ge_p2& q, const uint32_t* esb, const EdBWideTab& TB, PickB pick_b,
                          bool last_to_p2) {
@@ -622,9 +634,9 @@ CG_HD void ed_add_b_wide(ge_p3& R, ge_p1p1& t, ge_p2& q, const uint32_t* esb, co
     const int dg = sc_digit_at<EdWideCfg::kBBits>(esb, u);
     const int dp = Signed && dg < 0 ? -dg : dg;
     ge_niels n;
-    pick_b(n, TB.t[u], dp);
-    if (Signed) ge_madd_signed(t, R, n, dg < 0);
-    else ge_madd(t, R, n);
+    pick_b(n, TB.t[u], dp);  // Signed: by |digit|; otherwise negated by the pick (same for half entries)
+    if (dg == 0) ge_niels_identity_half(n);
+    ge_madd_half_signed(t, R, n, Signed && dg < 0);
     if (last_to_p2 && u + 1 == EdWideCfg::kBDigits) ge_p1p1_to_p2(q, t);
     else ge_p1p1_to_p3(R, t);
   }

@@ -62,6 +62,13 @@ CG_HD void fe_1(fe& h) {
   fe_0(h);
   h.v[0] = 1;
 }
+// 1/2 = (p + 1) / 2 = 2^254 - 9 (tight)
+CG_HD void fe_half(fe& h) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = (i & 1) ? 0x1ffffffu : 0x3ffffffu;
+  h.v[0] = 0x3fffff7u;
+  h.v[9] = 0xffffffu;
+}
 CG_HD void fe_copy(fe& h, const fe& f) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) h.v[i] = f.v[i];

@@ -140,6 +140,37 @@ CG_HD void ge_madd_signed(ge_p1p1& r, const ge_p3& p, const ge_niels& q, bool ne
   fe_carry(r.T);
 }
 
+// ge_madd_signed for a half-scaled niels entry q = ((y+x)/2, (y-x)/2, x y d) (the wide tables):
+// the sum comes out as ge_madd_signed's divided by 2, so D = Z instead of 2Z, and with Z and T of
+// p tight every output stays <= 3 tight: no doubling of Z, no sub4, no carry pass.
+//   neg = 0: (X'-Y', X'+Y', Z + c, Z - c)     neg = 1: (Y'-X', X'+Y', c - Z, Z + c)
+CG_HD void ge_madd_half_signed(ge_p1p1& r, const ge_p3& p, const ge_niels& q, bool neg) {
+  fe a, b, c;
+  fe_add(a, p.Y, p.X);
+  fe_sub(b, p.Y, p.X);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t ai = a.v[i], bi = b.v[i];
+    a.v[i] = neg ? bi : ai;
+    b.v[i] = neg ? ai : bi;
+  }
+  fe_mul(r.X, a, q.ypx);
+  fe_mul(r.Y, b, q.ymx);
+  fe_mul(c, q.xy2d, p.T);
+  fe_sub(r.Z, r.X, r.Y);
+  fe_add(r.Y, r.X, r.Y);
+  fe_copy(r.X, r.Z);
+  fe s, e, ne;
+  fe_add(s, p.Z, c);
+  fe_sub(e, p.Z, c);
+  fe_sub(ne, c, p.Z);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    r.Z.v[i] = neg ? ne.v[i] : s.v[i];
+    r.T.v[i] = neg ? s.v[i] : e.v[i];
+  }
+}
+
 // Conditionally negate a cached point in place: (YpX, YmX, Z, T2d) -> (YmX, YpX, Z, -T2d)
 CG_HD void ge_cached_cneg(ge_cached& q, uint32_t neg) {
   fe t;

@@ -507,7 +507,11 @@ __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* 
     ge_niels n;
     ed_lds_niels(n, wave_lds, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
-    if (d_cur == 0) ge_niels_identity(n);
+    const bool half = o >= EdOps::kNa1 + EdOps::kNa0;  // B ops: half-scaled wide-table entries
+    if (d_cur == 0) {
+      if (half) ge_niels_identity_half(n);
+      else ge_niels_identity(n);
+    }
     const bool neg = d_cur < 0;  // the sign goes through the addition, not the entry
     if (o + 1 < N) {
       ed_op_info(o + 1, widx, sh, is_b, row);
@@ -518,7 +522,8 @@ __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* 
         w_next = dw[widx];
       }
     }
-    ge_madd_signed(t, R, n, neg);
+    if (half) ge_madd_half_signed(t, R, n, neg);
+    else ge_madd_signed(t, R, n, neg);
     if (o + 1 == N || o + 1 == EdOps::kOps1) {
       ge_p1p1_to_p2(q, t);
     } else {
@@ -613,7 +618,7 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
     ge_niels n;
     ed_lds_niels(n, wave_lds, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
-    if (d_cur == 0) ge_niels_identity(n);
+    if (d_cur == 0) ge_niels_identity_half(n);
     const bool neg = d_cur < 0;
     if (o + 1 < N) {
       ed_wide_op(o + 1, widx, sh, is_b, row);
@@ -624,7 +629,7 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
         w_next = dw[widx];
       }
     }
-    ge_madd_signed(t, R, n, neg);
+    ge_madd_half_signed(t, R, n, neg);
     if (o + 1 < N) ge_p1p1_to_p3(R, t);
   }
   ge_p1p1_to_p2(out, t);

@@ -635,7 +635,13 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
   ge_p1p1_to_p2(out, t);
 }
 
-__global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_wide(
+// A/B (profiles/r02/w4_rejected): forcing 4 waves/SIMD (128 VGPRs, 52 B/lane of scratch) cost 4% of
+// the kernel against the compiler's 144 VGPRs at 3 waves/SIMD (a cap of 2 waves/SIMD leaves the
+// allocation at 144: the loop needs no more).
+#ifndef ED_LADDER_WIDE_WAVES
+#define ED_LADDER_WIDE_WAVES ED_LADDER_PF_WAVES
+#endif
+__global__ void __launch_bounds__(256, ED_LADDER_WIDE_WAVES) k_ed_ladder_wide(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
     const EdKeyHdr* __restrict__ hdr, const uint32_t* __restrict__ wide_idx, const EdWideSlot* __restrict__ wed,
     const EdBWideTab* __restrict__ btab, uint8_t* __restrict__ status, void* __restrict__ slots) {

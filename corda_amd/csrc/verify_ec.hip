@@ -462,15 +462,24 @@ void ec_launch_keyprep_tabs(int curve, const cg_key* d_keys, uint32_t n_keys, co
   else launch_keyprep_tabs<CG_CURVE_K1>(d_keys, n_keys, w, stream, full, wide);
 }
 
+// Walk-grid caps of the front stages, in waves per SIMD (the kernels fit 5 and 6). Raising them to
+// 5 / 6 was neutral on the headline (A/B 259.2 vs 259.0 M sigs/s, profiles/r02/cap_rejected): the
+// r1 front slowed while the concurrent challenge hashes sped up.
+#ifndef EC_PREP_CAP_WAVES
+#define EC_PREP_CAP_WAVES 2
+#endif
+#ifndef EC_INV_CAP_WAVES
+#define EC_INV_CAP_WAVES 2
+#endif
 template <int C>
 static void launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
                          uint32_t mode, uint8_t* d_status, const KeyWs& w, const uint8_t* d_msgs, uint64_t msgs_len,
                          const ItemWs& iw, hipStream_t stream) {
   const uint32_t B = 256;  // a curve's range is at most n_items long
   EcItemWs* ws = (EcItemWs*)iw.slots;
-  hipLaunchKernelGGL(k_ec_prep<C>, dim3(walk_grid(n_items, B, WALK_CAP(2))), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                     d_arena, arena_len, d_msgs, msgs_len, mode, d_status, ws);
-  const unsigned igrid = walk_grid((n_items + EC_INV_K - 1) / EC_INV_K, B, WALK_CAP(2));
+  hipLaunchKernelGGL(k_ec_prep<C>, dim3(walk_grid(n_items, B, WALK_CAP(EC_PREP_CAP_WAVES))), dim3(B), 0, stream, d_items,
+                     iw.perm, iw.ranges, w.hdr, d_arena, arena_len, d_msgs, msgs_len, mode, d_status, ws);
+  const unsigned igrid = walk_grid((n_items + EC_INV_K - 1) / EC_INV_K, B, WALK_CAP(EC_INV_CAP_WAVES));
   hipLaunchKernelGGL(k_ec_inv<C>, dim3(igrid), dim3(B), 0, stream, iw.perm, iw.ranges,
                      (const uint8_t*)d_status, ws);
 }

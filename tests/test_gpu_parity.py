@@ -297,24 +297,25 @@ def test_tx_ids_random_vs_oracle(engine):
 
 
 def test_tx_ids_of_kryo_encoded_components(engine):
-    """WireTransaction ids over components encoded by the Kryo restatement (corda_amd/kryo.py,
-    SURVEY §8 f1, parity unpinned): the GPU ids equal the oracle's MerkleTransaction.kt rule over
-    the same encoded bytes, for transactions of every component type."""
+    """WireTransaction ids over components encoded by the Kryo writer (corda_amd/kryo.py, pinned by
+    the tutorial capture, tests/test_kryo.py): the GPU ids equal the oracle's MerkleTransaction.kt
+    rule over the same encoded bytes, for transactions of every component type."""
     import hashlib
     from corda_amd import kryo as K, merkle
     rng = np.random.default_rng(6)
     txs = []
     for t in range(500):
         key = K.PublicKeyRef(4, rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
-        notary = K.Party(bytes.fromhex("3031310b300906035504061302474231") + bytes([t % 251]), key)
+        notary = K.Party(K.x500_der(f"CN=Notary{t % 7},O=R3,L=London,C=GB"), key)
         h = lambda: K.SecureHash(rng.integers(0, 256, 32, dtype=np.uint8).tobytes())  # noqa: E731
+        iou = lambda: K.CordaObject("com.example.state.IOUState", (  # noqa: E731
+            ("iou", "object", K.CordaObject("com.example.state.IOU", (("value", "int", int(rng.integers(0, 1 << 30))),))),
+            ("recipient", "party", notary), ("sender", "party", notary)))
         wtx = K.WireTransaction(
             inputs=[K.StateRef(h(), int(i)) for i in range(int(rng.integers(0, 4)))],
             attachments=[h() for _ in range(int(rng.integers(0, 2)))],
-            outputs=[K.TransactionState("com.example.IOUState", (("value", int(rng.integers(0, 1 << 30))),
-                                                                 ("lender", rng.bytes(44))), "com.example.IOUContract",
-                                        notary) for _ in range(int(rng.integers(1, 4)))],
-            commands=[K.Command("com.example.IOUContract$Commands$Create", (), (key,))],
+            outputs=[K.TransactionState(iou(), notary) for _ in range(int(rng.integers(1, 4)))],
+            commands=[K.Command(K.CordaObject("com.example.contract.IOUContract$Commands$Create"), (key,))],
             notary=notary, time_window=K.TimeWindow((1_700_000_000 + t, 0), None) if t % 2 else None,
             privacy_salt=K.PrivacySalt(hashlib.sha256(bytes([t % 256, t // 256])).digest()))
         d = wtx.data()
@@ -323,6 +324,35 @@ def test_tx_ids_of_kryo_encoded_components(engine):
     assert np.all(st == 0)
     for (blobs, salt, sb), got in zip(txs, ids):
         assert got == ocorda.tx_id(blobs, salt, sb)
+
+
+def test_tutorial_transaction_end_to_end(engine):
+    """The reference's captured transaction (docs/source/tutorial-cordapp.rst) through the engine:
+    SHA-256 of its six Kryo components (rebuilt by the writer) and their Merkle root give the
+    printed id; the two printed Ed25519 signatures over that id verify (and the swapped pairs do
+    not), with raw and SPKI keys."""
+    from kryo_fixtures import _captures, tutorial_components
+    t = _captures()["tutorial"]
+    leaves = engine.sha256(tutorial_components())
+    roots, st = engine.merkle_roots([leaves])
+    assert st[0] == 0 and roots[0].hex().upper() == t["id"]
+    tx_id = roots[0]
+    keys = [bytes.fromhex(k)[-32:] for k in t["signers"]]
+    sigs = [bytes.fromhex(s) for s in t["sigs"]]
+    b = B.BatchBuilder()
+    for i, k in enumerate(keys):
+        for j, s in enumerate(sigs):
+            b.add_with_key(4, B.KEY_RAW, k, s, tx_id)
+            b.add_with_key(4, B.KEY_SPKI, ocorda.ED25519_SPKI_PREFIX + k, s, tx_id)
+    got = engine.verify(b.build(), B.MODE_DOVERIFY)
+    assert list(got) == [B.VALID, B.VALID, B.INVALID, B.INVALID, B.INVALID, B.INVALID, B.VALID, B.VALID]
+
+
+@pytest.mark.parametrize("mode", [B.MODE_DOVERIFY, B.MODE_ISVALID])
+def test_reference_ed25519_signatures(engine, mode):
+    """The tutorial's i2p-made signatures and builder-made corruptions of them
+    (tests/golden/ref_ed25519.json)."""
+    _check(engine, golden_io.load("ref_ed25519.json"), mode)
 
 
 def test_crypto_api_behaviour():

@@ -54,3 +54,17 @@ def test_openssl_agrees_where_semantics_agree():
             assert it["expect"] == "SIG_MALFORMED"
             continue
         assert (it["openssl"] == "VALID") == (it["expect"] == "VALID"), (it["class"], it["note"])
+
+
+def test_reference_ed25519_vectors():
+    """tests/golden/ref_ed25519.json (tools/gen/kryo_captures.py): the two i2p-made signatures the
+    tutorial prints (over the 32-byte id) and corruptions of them; both oracles agree."""
+    items = golden_io.load("ref_ed25519.json")
+    genuine = [i for i in items if i["origin"] == "reference"]
+    assert len(genuine) == 2 and all(i["expect"] == "VALID" for i in genuine)
+    b, exp, exp_iv = golden_io.sig_batch(items)
+    assert np.array_equal(c_oracle.verify_batch(b, 0, 4), exp)
+    assert np.array_equal(c_oracle.verify_batch(b, 1, 4), exp_iv)
+    for it in items:
+        st = corda.verify_item(4, 0, bytes.fromhex(it["key"]), bytes.fromhex(it["sig"]), bytes.fromhex(it["msg"]))
+        assert corda.STATUS_NAMES[st] == it["expect"], it["note"]

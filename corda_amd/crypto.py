@@ -198,14 +198,16 @@ class _Crypto:
             try:
                 key = pk if isinstance(pk, C.CompositeKey) else C.CompositeKey.get_instance(pk.encoded)
                 sig = it.signature_data
-                if not isinstance(sig, C.CompositeSignaturesWithKeys):
-                    if mode == B.MODE_DOVERIFY and len(sig) == 0:
-                        st[i] = B.EMPTY
-                        continue
-                    sig = C.CompositeSignaturesWithKeys.deserialize(sig)
+                # doVerify's empty checks come first, signature then clear data (Crypto.kt:476-477),
+                # before the engine deserialises anything
+                if mode == B.MODE_DOVERIFY and not isinstance(sig, C.CompositeSignaturesWithKeys) and len(sig) == 0:
+                    st[i] = B.EMPTY
+                    continue
                 if mode == B.MODE_DOVERIFY and len(it.clear_data) == 0:
                     st[i] = B.EMPTY
                     continue
+                if not isinstance(sig, C.CompositeSignaturesWithKeys):
+                    sig = C.CompositeSignaturesWithKeys.deserialize(sig)
                 if not key.is_fulfilled_by([s.by for s in sig.sigs]):
                     st[i] = B.INVALID
                     continue

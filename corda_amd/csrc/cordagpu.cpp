@@ -34,7 +34,7 @@ int hip_fail(hipError_t e, const char* where) {
   char buf[512];
   snprintf(buf, sizeof buf, "%s: %s", where, hipGetErrorString(e));
   g_err = buf;
-  return CG_ERR_DEVICE;
+  return e == hipErrorOutOfMemory ? CG_ERR_NOMEM : CG_ERR_DEVICE;
 }
 
 #define HIP_TRY(expr, where)               \
@@ -368,9 +368,15 @@ int cg_device_count(void) {
 
 const char* cg_last_error(void) { return g_err.c_str(); }
 
+static_assert(sizeof(cg_config) == 56, "cg_config is 56 bytes in ABI v2");
+static_assert(sizeof(cg_item) == 32 && sizeof(cg_key) == 16 && sizeof(cg_txsig) == 24, "ABI struct sizes");
+
 int cg_open(cg_ctx** out, const cg_config* cfg) {
   if (!out) return fail(CG_ERR_ARG, "cg_open: out is NULL");
   *out = nullptr;
+  if (cfg && (cfg->reserved[0] || cfg->reserved[1] || cfg->reserved[2]))
+    return fail(CG_ERR_ARG, "cg_open: cg_config.reserved must be 0 (ABI v2: 56-byte cg_config)");
+  if (cfg && (cfg->flags & ~CG_FLAG_STAGE_TIMING)) return fail(CG_ERR_ARG, "cg_open: unknown cg_config.flags bits");
   int dev = cfg ? cfg->device : 0;
   int n = 0;
   HIP_TRY(hipGetDeviceCount(&n), "hipGetDeviceCount");
@@ -476,10 +482,11 @@ void cg_close(cg_ctx* c) {
   for (int k = 0; k < 4; ++k)
     if (c->tev[k]) hipEventDestroy(c->tev[k]);
   if (c->done) hipEventDestroy(c->done);
-  for (auto& r : c->timer.recs) {
-    hipEventDestroy(r.a);
-    hipEventDestroy(r.b);
-  }
+  for (auto* v : {&c->timer.recs, &c->timer.spare})
+    for (auto& r : *v) {
+      hipEventDestroy(r.a);
+      hipEventDestroy(r.b);
+    }
   for (int k = 0; k < 2; ++k)
     if (c->fork.ec_decoded[k]) hipEventDestroy(c->fork.ec_decoded[k]);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -503,8 +510,7 @@ int cg_stage_times(cg_ctx* c, double* ms_out, uint32_t* launches_out, uint32_t n
       ms_out[r.stage] += ms;
       launches_out[r.stage] += 1;
     }
-    hipEventDestroy(r.a);
-    hipEventDestroy(r.b);
+    c->timer.spare.push_back(r);
   }
   c->timer.recs.clear();
   return rc == CG_OK ? (int)m : fail(rc, "cg_stage_times: event wait failed");
@@ -958,6 +964,13 @@ int cg_pool_verify_batch(cg_pool* p, const cg_key* keys, uint32_t n_keys, const 
                                 if (r != CG_OK) errs[slot] = g_err;  // g_err is this worker thread's
                                 return r;
                               },
+                              [&](uint32_t slot) {  // re-probe: no drill fault, the device answers
+                                cg_ctx* c = p->ctx[slot];
+                                std::lock_guard<std::mutex> gc(c->mu);
+                                if (c->fault || hipSetDevice(c->device) != hipSuccess) return false;
+                                const hipError_t q = hipStreamQuery(c->stream);
+                                return q == hipSuccess || q == hipErrorNotReady;
+                              },
                               &rep);
   if (stats) {
     stats->shards = rep.shards;
@@ -968,7 +981,8 @@ int cg_pool_verify_batch(cg_pool* p, const cg_key* keys, uint32_t n_keys, const 
     stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   if (rc != CG_OK) {
-    std::string m = "cg_pool_verify_batch: no healthy slot could run every shard;";
+    std::string m = rc == CG_ERR_DEVICE ? "cg_pool_verify_batch: no healthy slot could run every shard;"
+                                        : "cg_pool_verify_batch: a shard failed (not a device fault);";
     for (size_t k = 0; k < errs.size(); ++k)
       if (!errs[k].empty()) m += " [slot " + std::to_string(k) + "] " + errs[k];
     g_err = m;

@@ -40,10 +40,25 @@ struct StageTimer {
     int stage;
     hipEvent_t a, b;
   };
-  std::vector<Rec> recs;
+  // At most kMaxRecs launches are recorded between two cg_stage_times calls (later launches are
+  // not timed); event pairs are recycled through `spare`, so a context that never reads its stage
+  // times holds a bounded number of events.
+  static constexpr size_t kMaxRecs = 4096;
+  std::vector<Rec> recs, spare;
   int mark(int stage, hipStream_t s) {
+    if (recs.size() >= kMaxRecs) return -1;
     Rec r{stage, nullptr, nullptr};
-    if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return -1;
+    if (!spare.empty()) {
+      r.a = spare.back().a;
+      r.b = spare.back().b;
+      spare.pop_back();
+    } else {
+      if (hipEventCreate(&r.a) != hipSuccess) return -1;
+      if (hipEventCreate(&r.b) != hipSuccess) {
+        (void)hipEventDestroy(r.a);
+        return -1;
+      }
+    }
     (void)hipEventRecord(r.a, s);
     recs.push_back(r);
     return (int)recs.size() - 1;

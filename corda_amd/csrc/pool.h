@@ -8,9 +8,13 @@
 // thread and writes its verdicts straight into its slice of the caller's status buffer (the
 // gather is the D2H copy itself: no collective is needed to assemble a host result).
 //
-// Failure: a shard whose call fails marks its slot unhealthy (skipped by later calls) and has
-// its slice reset to CG_NOT_RUN; failed shards are then re-run on the slots that are still
-// healthy, round-robin, until every shard has run or no healthy slot is left. The reference
+// Failure: a shard whose call fails with a device fault (CG_ERR_DEVICE) marks its slot unhealthy
+// and has its slice reset to CG_NOT_RUN; failed shards are then re-run on the slots that are still
+// healthy, round-robin, until every shard has run or no healthy slot is left. Argument, range and
+// capacity errors (CG_ERR_ARG / CG_ERR_RANGE / CG_ERR_NOMEM) say nothing about the device: they
+// end the call with that code and leave every slot as it was. An unhealthy slot is
+// re-probed at the start of every call (probe(slot): the context answers and no drill fault is
+// set) and rejoins the plan when it answers. The reference
 // gets this from Artemis redelivery of the verifier's request (VerifierTests.kt:73-99,
 // OutOfProcessTransactionVerifierService.kt:65-72); here a device fault costs a re-run of its
 // shard, and an item that could not be run anywhere stays CG_NOT_RUN (never "valid"), so the
@@ -40,11 +44,14 @@ struct PoolReport {
 };
 
 // verify(slot, first, count) -> CG_OK or an error; it writes status[first .. first + count).
-template <class VerifyFn>
-int pool_run(std::vector<uint8_t>& healthy, uint64_t n_items, uint8_t* status, VerifyFn&& verify,
+// probe(slot) -> true when an unhealthy slot may be used again.
+template <class VerifyFn, class ProbeFn>
+int pool_run(std::vector<uint8_t>& healthy, uint64_t n_items, uint8_t* status, VerifyFn&& verify, ProbeFn&& probe,
              PoolReport* rep) {
   PoolReport r;
   if (n_items) memset(status, CG_NOT_RUN, n_items);
+  for (uint32_t s = 0; s < healthy.size(); ++s)
+    if (!healthy[s] && probe(s)) healthy[s] = 1;
   std::vector<uint32_t> live;
   auto refresh = [&]() {
     live.clear();
@@ -84,14 +91,25 @@ int pool_run(std::vector<uint8_t>& healthy, uint64_t n_items, uint8_t* status, V
     th.reserve(take);
     for (PoolShard& sh : pass) th.emplace_back([&sh, &verify]() { sh.rc = verify(sh.slot, sh.first, sh.count); });
     for (std::thread& t : th) t.join();
+    int hard = CG_OK;
     for (PoolShard& sh : pass) {
       if (sh.rc == CG_OK) continue;
+      memset(status + sh.first, CG_NOT_RUN, sh.count);
+      if (sh.rc != CG_ERR_DEVICE) {  // the caller's input or capacity, not the device
+        if (hard == CG_OK) hard = sh.rc;
+        r.not_run += sh.count;
+        continue;
+      }
       if (healthy[sh.slot]) {
         healthy[sh.slot] = 0;
         ++r.failed_slots;
       }
-      memset(status + sh.first, CG_NOT_RUN, sh.count);
       pending.push_back(sh);
+    }
+    if (hard != CG_OK) {
+      for (const PoolShard& sh : pending) r.not_run += sh.count;
+      if (rep) *rep = r;
+      return hard;
     }
   }
   if (rep) *rep = r;

@@ -159,12 +159,12 @@ enum {
 
 typedef struct cg_config {
   int32_t device;        /* HIP device ordinal (cg_open; cg_pool_open takes a device list) */
-  uint32_t flags;        /* reserved, 0 */
+  uint32_t flags;        /* CG_FLAG_* (other bits: CG_ERR_ARG) */
   uint64_t max_items;    /* workspace sizing hint (0 = grow on demand) */
   uint64_t max_arena;    /* workspace sizing hint (0 = grow on demand) */
   uint64_t chunk_items;  /* items per verify chunk (0 = CG_DEFAULT_CHUNK_ITEMS) */
-  uint64_t reserved[3];  /* must be 0 */
-} cg_config;             /* 48 bytes */
+  uint64_t reserved[3];  /* must be 0: cg_open rejects anything else with CG_ERR_ARG */
+} cg_config;             /* 56 bytes (static_assert in cordagpu.cpp) */
 
 typedef struct cg_stats {
   uint64_t n_items;

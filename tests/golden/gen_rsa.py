@@ -1,10 +1,10 @@
-"""Generates tests/golden/rsa.json: SHA256withRSA (Corda RSA_SHA256, scheme 1) fixtures for the
-host fallback (corda_amd/hostverify.py). Signatures and keys come from the OpenSSL 3 CLI (run here
+"""Generates tests/golden/rsa.json: SHA256WITHRSAANDMGF1 (Corda RSA_SHA256, scheme 1,
+Crypto.kt:78-89) fixtures for the host fallback (corda_amd/hostverify.py): RSASSA-PSS with
+SHA-256, MGF1(SHA-256), 32-byte salt. Signatures and keys come from the OpenSSL 3 CLI (run here
 once; the fixture is committed); every item records OpenSSL's own accept / reject as the pin.
-`expect` is the BC 1.57 restatement's outcome: VALID, INVALID (a well-padded block whose
-DigestInfo differs: isValid == false) or SignatureException (a block BC cannot decode: bad
-padding, input >= n, input longer than the modulus) -- that split is [ext] recall, unpinned;
-OpenSSL rejects all three alike.
+`expect` is the BC 1.57 PSSSigner restatement's outcome: VALID or INVALID (verifySignature
+returns false for every failure, including PKCS#1 v1.5 signatures, inputs >= n and inputs
+longer than the modulus).
 
 usage: python tests/golden/gen_rsa.py  (needs the openssl CLI)
 """
@@ -15,6 +15,7 @@ import subprocess
 import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+PSS = ["-sigopt", "rsa_padding_mode:pss", "-sigopt", "rsa_pss_saltlen:32", "-sigopt", "rsa_mgf1_md:sha256"]
 
 
 def sh(*args, data=None):
@@ -26,8 +27,8 @@ def ossl_verify(pub_der, msg, sig, d):
     open(kp, "wb").write(pub_der)
     open(mp, "wb").write(msg)
     open(sp, "wb").write(sig)
-    r = subprocess.run(["openssl", "dgst", "-sha256", "-keyform", "DER", "-verify", kp, "-signature", sp, mp],
-                       capture_output=True)
+    r = subprocess.run(["openssl", "dgst", "-sha256", "-keyform", "DER", "-verify", kp] + PSS +
+                       ["-signature", sp, mp], capture_output=True)
     return "accept" if r.returncode == 0 else "reject"
 
 
@@ -53,17 +54,20 @@ def main():
                 msg = bytes(rng.randrange(256) for _ in range(rng.choice([1, 32, 270, 700])))
                 mp = os.path.join(d, "m.bin")
                 open(mp, "wb").write(msg)
-                sig = sh("openssl", "dgst", "-sha256", "-sign", key, mp)
-                cases = [("valid", msg, sig, "VALID")]
+                sig = sh("openssl", "dgst", "-sha256", "-sign", key, *PSS, mp)
+                v15 = sh("openssl", "dgst", "-sha256", "-sign", key, mp)
+                cases = [("valid", msg, sig, "VALID"),
+                         ("PKCS#1 v1.5 signature of the same message (not Corda's scheme)", msg, v15, "INVALID")]
                 m2 = bytearray(msg)
                 m2[rng.randrange(len(m2))] ^= 1 << rng.randrange(8)
                 cases.append(("flip message bit", bytes(m2), sig, "INVALID"))
                 s2 = bytearray(sig)
                 s2[rng.randrange(len(s2))] ^= 1 << rng.randrange(8)
-                cases.append(("flip signature bit", msg, bytes(s2), "SignatureException"))
+                cases.append(("flip signature bit", msg, bytes(s2), "INVALID"))
                 if k == 0:
-                    cases.append(("signature longer than the modulus", msg, b"\x00" + sig, "SignatureException"))
-                    cases.append(("signature >= n", msg, b"\xff" * len(sig), "SignatureException"))
+                    cases.append(("signature longer than the modulus", msg, b"\x00" + sig, "INVALID"))
+                    cases.append(("signature >= n", msg, b"\xff" * len(sig), "INVALID"))
+                    cases.append(("empty signature", msg, b"", "INVALID"))
                 for note, m, s, exp in cases:
                     items.append({"scheme": 1, "key_fmt": 1, "key": pub.hex(), "sig": s.hex(), "msg": m.hex(),
                                   "bits": bits, "note": note, "expect": exp,
@@ -71,11 +75,11 @@ def main():
         # the same valid signature against another modulus: decodes to garbage padding
         a, b = items[0], items[len(items) // 2]
         items.append({"scheme": 1, "key_fmt": 1, "key": b["key"], "sig": a["sig"], "msg": a["msg"], "bits": b["bits"],
-                      "note": "signature of another key", "expect": "SignatureException",
+                      "note": "signature of another key", "expect": "INVALID",
                       "openssl": ossl_verify(bytes.fromhex(b["key"]), bytes.fromhex(a["msg"]), bytes.fromhex(a["sig"]),
                                              d)})
     meta = {"generator": "tests/golden/gen_rsa.py", "openssl": sh("openssl", "version").decode().strip(),
-            "note": "expect = BC 1.57 DigestSignatureSpi restatement (hostverify.py); openssl = OpenSSL's verdict"}
+            "note": "expect = BC 1.57 PSSSigner restatement (hostverify.py); openssl = OpenSSL's PSS verdict"}
     with open(os.path.join(HERE, "rsa.json"), "w") as f:
         json.dump({"meta": meta, "test_private_key": private, "items": items}, f, indent=0)
     print(len(items), "items")

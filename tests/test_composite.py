@@ -2,6 +2,8 @@
 fallback for the schemes the GPU does not run, on the CPU: the host logic of corda_amd/composite.py,
 corda_amd/hostverify.py and corda_amd/crypto.py with the C oracle standing in for the GPU engine
 (the same cases run against the real engine in tests/test_gpu_composite.py)."""
+import hashlib
+
 import pytest
 
 import composite_cases as CC
@@ -149,3 +151,47 @@ def test_sphincs_has_no_host_verifier(crypto):
     from corda_amd.crypto import BatchItem, HOST_EXCEPTION, UnsupportedOperationException
     st, err = crypto.verify_batch_ex([BatchItem(PublicKey(5, b"\x00" * 64, B.KEY_SPKI), b"s", b"m")])
     assert st[0] == HOST_EXCEPTION and isinstance(err[0], UnsupportedOperationException)
+
+
+def test_rsa_is_pss_not_pkcs1v15():
+    """RSA_SHA256 is BC "SHA256WITHRSAANDMGF1" (Crypto.kt:85): a PSS signature made here verifies,
+    OpenSSL accepts it with the PSS options, and the PKCS#1 v1.5 signature of the same message is
+    false."""
+    import json
+    import os
+    import subprocess
+    import tempfile
+    from corda_amd import hostverify as H
+    k = json.load(open(os.path.join(CC.GOLDEN, "rsa.json")))["test_private_key"]
+    n, d = int(k["n"], 16), int(k["d"], 16)
+    msg = b"a transaction id signed by an RSA key"
+    sig = H.rsa_pss_sign(n, d, msg, bytes(range(32)))
+    key = H.rsa_decode_key(bytes.fromhex(k["spki"]))
+    assert H.rsa_verify(key, sig, msg) is True
+    assert H.rsa_verify(key, sig, msg + b"!") is False
+    kk = (n.bit_length() + 7) // 8
+    di = bytes.fromhex("3031300d060960864801650304020105000420") + hashlib.sha256(msg).digest()
+    em = b"\x00\x01" + b"\xff" * (kk - 3 - len(di)) + b"\x00" + di
+    v15 = pow(int.from_bytes(em, "big"), d, n).to_bytes(kk, "big")
+    assert H.rsa_verify(key, v15, msg) is False
+    with tempfile.TemporaryDirectory() as t:
+        for name, data in (("k.der", bytes.fromhex(k["spki"])), ("s", sig), ("m", msg)):
+            open(os.path.join(t, name), "wb").write(data)
+        r = subprocess.run(["openssl", "dgst", "-sha256", "-keyform", "DER", "-verify", os.path.join(t, "k.der"),
+                            "-sigopt", "rsa_padding_mode:pss", "-sigopt", "rsa_pss_saltlen:32",
+                            "-sigopt", "rsa_mgf1_md:sha256", "-signature", os.path.join(t, "s"), os.path.join(t, "m")],
+                           capture_output=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_composite_empty_clear_data_checked_before_deserialising(crypto):
+    """doVerify's empty checks run before the composite engine deserialises the signature: a
+    malformed non-empty signature with empty clear data is IllegalArgumentException("Clear data
+    is empty, nothing to verify!"), as on the JVM (Crypto.kt:476-477)."""
+    from corda_amd.composite import CompositeKey
+    (_, a), (_, b) = CC.party(20), CC.party(21)
+    k = CompositeKey.Builder().add_keys(a, b).build(threshold=1)
+    with pytest.raises(IllegalArgumentException, match="Clear data is empty, nothing to verify!"):
+        crypto.do_verify(k, b"\x01not a CompositeSignaturesWithKeys", b"")
+    with pytest.raises(IllegalArgumentException, match="Signature data is empty!"):
+        crypto.do_verify(k, b"", b"")

@@ -42,12 +42,12 @@ def test_composite_notary_gpu(crypto):
 
 
 def _rsa_sign(msg):
+    """SHA256WITHRSAANDMGF1 (PSS) with the fixture's test key and a salt derived from the message."""
+    from corda_amd.hostverify import rsa_pss_sign
     k = json.load(open(os.path.join(CC.GOLDEN, "rsa.json")))["test_private_key"]
     n, d = int(k["n"], 16), int(k["d"], 16)
-    kk = (n.bit_length() + 7) // 8
-    di = bytes.fromhex("3031300d060960864801650304020105000420") + hashlib.sha256(msg).digest()
-    em = b"\x00\x01" + b"\xff" * (kk - 3 - len(di)) + b"\x00" + di
-    return PublicKey(1, bytes.fromhex(k["spki"]), B.KEY_SPKI), pow(int.from_bytes(em, "big"), d, n).to_bytes(kk, "big")
+    salt = hashlib.sha256(b"salt" + bytes(msg)).digest()
+    return PublicKey(1, bytes.fromhex(k["spki"]), B.KEY_SPKI), rsa_pss_sign(n, d, msg, salt)
 
 
 def test_wire_transactions_with_rsa_signers_gpu(crypto):

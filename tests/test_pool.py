@@ -27,7 +27,7 @@ def _lib():
                                "-lpthread"])
     L = ctypes.CDLL(SO)
     vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
-    L.pt_pool_verify.argtypes = [vp, u32, vp, u64, vp, u64, u32, vp, u32, vp, u32, u32, vp, vp]
+    L.pt_pool_verify.argtypes = [vp, u32, vp, u64, vp, u64, u32, vp, u32, vp, u32, u32, u32, u32, vp, vp]
     L.pt_pool_verify.restype = ctypes.c_int
     return L
 
@@ -43,13 +43,13 @@ def batch():
     return b, exp
 
 
-def _run(L, b, n_slots, healthy=None, fail_always=0, fail_once=0):
+def _run(L, b, n_slots, healthy=None, fail_always=0, fail_once=0, fail_arg=0, probe_ok=0):
     st = np.full(b.n, 7, dtype=np.uint8)
     h = np.ones(n_slots, np.uint8) if healthy is None else np.array(healthy, np.uint8)
     calls = np.zeros(n_slots, np.uint32)
     rep = np.zeros(4, np.uint64)
     rc = L.pt_pool_verify(_p(b.keys), len(b.keys), _p(b.items), b.n, _p(b.arena), b.arena.size, 0, _p(st), n_slots,
-                          _p(h), fail_always, fail_once, _p(calls), _p(rep))
+                          _p(h), fail_always, fail_once, fail_arg, probe_ok, _p(calls), _p(rep))
     return rc, st, h, calls, rep
 
 
@@ -114,3 +114,24 @@ def test_empty_batch(batch):
     e = Batch(b.keys, b.items[:0], b.arena)
     rc, st, _, calls, rep = _run(L, e, 2)
     assert rc == 0 and st.size == 0 and int(calls.sum()) == 0
+
+
+def test_capacity_error_does_not_poison_the_slot(batch):
+    """A non-device error (here CG_ERR_NOMEM) ends the call with that code and leaves every slot
+    healthy: one oversized batch cannot kill the pool."""
+    L = _lib()
+    b, exp = batch
+    rc, st, h, calls, rep = _run(L, b, 3, fail_arg=0b010)
+    assert rc == -3 and list(h) == [1, 1, 1] and int(rep[2]) == 0
+    assert int(rep[3]) > 0 and np.all(st[st != 255] == exp[st != 255])
+    rc, st, h, calls, rep = _run(L, b, 3)
+    assert rc == 0 and np.array_equal(st, exp)
+
+
+def test_unhealthy_slot_rejoins_after_probe(batch):
+    """An unhealthy slot is re-probed at the start of a call and rejoins the plan if it answers."""
+    L = _lib()
+    b, exp = batch
+    rc, st, h, calls, rep = _run(L, b, 3, healthy=[1, 0, 0], probe_ok=0b010)
+    assert rc == 0 and np.array_equal(st, exp)
+    assert list(h) == [1, 1, 0] and calls[1] == 1 and calls[2] == 0 and int(rep[0]) == 2

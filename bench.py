@@ -101,7 +101,10 @@ def parse():
     ap.add_argument("--stream", choices=("ctx", "torch"), default="ctx",
                     help="headline calls on the engine context's stream (NULL, as a JNI caller) or torch's")
     ap.add_argument("--seed", type=int, default=20251015)
-    ap.add_argument("--host-steps", type=int, default=3, help="PCIe-inclusive cg_verify_batch calls (0: off)")
+    ap.add_argument("--sigs-per-tx", type=int, default=5,
+                    help="signatures per transaction id (GeneratedLedger: 1+Poisson(3) signers + the notary)")
+    ap.add_argument("--device-steps", type=int, default=4, help="device-resident secondary calls (0: off)")
+    ap.add_argument("--host-steps", type=int, default=3, help="message-form cg_verify_batch calls (0: off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
     ap.add_argument("--threads", type=int, default=0, help="host threads (0: the CPU quota, at most 16)")
@@ -498,9 +501,55 @@ def bench_tear_offs(a, eng, dev, stream, wl):
             "parity_vs_generator": bool(np.array_equal(st, np.tile(expect, reps)))}
 
 
+def bench_device(eng, dev, stream, b, tb, st_ref, steps):
+    """Device-resident forms of the headline shard (inputs already in HBM, status left in HBM):
+    cg_verify_batch_device over the materialised messages, and cg_verify_tx_signatures_device over
+    (id, template) pairs. The PCIe-free ceiling of the whole-node headline."""
+    import torch
+    out = {}
+    bufs = upload(dev, b)
+    step = timed_device(eng, bufs, b, steps, 1, stream, dev, ctx_stream=True)
+    eng.stage_times()
+    t = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t) / steps
+    stg = eng.stage_times()
+    out["message_form"] = {"value": round(b.n / el, 1), "unit": "sigs/s", "ms_per_step": round(el * 1e3, 3),
+                           "path": "cg_verify_batch_device, one call per step (SignableData bytes resident in HBM)",
+                           "stages": stage_summary(stg, steps),
+                           "verdicts_equal_headline": bool(np.array_equal(bufs[3].cpu().numpy(), st_ref))}
+    del bufs
+    up = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).to(dev)  # noqa: E731
+    kd, ijd, sgd, ad = up(tb.keys), up(tb.ids), up(tb.sigs), up(tb.arena)
+    sd = torch.full((tb.n,), 255, dtype=torch.uint8, device=dev)
+
+    def once():
+        eng.verify_tx_signatures_device(kd.data_ptr(), len(tb.keys), ijd.data_ptr(), tb.n_ids, sgd.data_ptr(), tb.n,
+                                        tb.tmpls, ad.data_ptr(), tb.arena.size, sd.data_ptr())
+    once()
+    torch.cuda.synchronize(dev)
+    eng.stage_times()
+    t = time.perf_counter()
+    for _ in range(steps):
+        once()
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t) / steps
+    stg = eng.stage_times()
+    out["tx_signatures"] = {"value": round(tb.n / el, 1), "unit": "sigs/s", "ms_per_step": round(el * 1e3, 3),
+                            "path": "cg_verify_tx_signatures_device, one call per step",
+                            "stages": stage_summary(stg, steps),
+                            "verdicts_equal_headline": bool(np.array_equal(sd.cpu().numpy(), st_ref))}
+    del kd, ijd, sgd, ad, sd
+    torch.cuda.empty_cache()
+    return out
+
+
 def bench_host(eng, b, st_dev, steps):
-    """PCIe-inclusive: host arena -> host verdicts through cg_verify_batch (the JNI path) on the
-    headline shard: keys, items and ~370 B per item copied, chunk k+1's copy overlapping chunk k."""
+    """PCIe-inclusive message form: host arena -> host verdicts through cg_verify_batch on the
+    headline shard with every SignableData materialised: keys, items and ~370 B per item copied,
+    chunk k+1's copy overlapping chunk k."""
     st = eng.verify(b)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -511,8 +560,8 @@ def bench_host(eng, b, st_dev, steps):
             "bytes_h2d": int(b.arena.size + b.items.nbytes + b.keys.nbytes),
             "h2d_GBps_effective": round((b.arena.size + b.items.nbytes) / el / 1e9, 1),
             "cg_stats_ms": {k: round(v, 3) for k, v in s.items() if k.startswith("ms_")},
-            "verdicts_equal_device_path": bool(np.array_equal(st, st_dev)),
-            "path": "cg_verify_batch from pageable host memory (what a JNI caller hands over)"}
+            "verdicts_equal_headline": bool(np.array_equal(st, st_dev)),
+            "path": "cg_verify_batch from pageable host memory, SignableData bytes materialised per signature"}
 
 
 def main():
@@ -536,27 +585,39 @@ def main():
 
     # ---- this rank's shard (outside the timed region)
     t0 = time.time()
+    from corda_amd import signable
     pool, pool_labels, pool_schemes = wl.notary_pool(a.pool, ed_keys=a.ed_keys, ec_keys=a.ec_keys, msg_len=a.msg_len,
-                                                     seed=a.seed + 7919 * rank, nthreads=threads)
+                                                     seed=a.seed + 7919 * rank, nthreads=threads,
+                                                     sig_group=a.sigs_per_tx)
+    ids, id_idx = wl.pool_ids(pool, len(signable.template(1, 4)[0]))
     batch, idx = wl.index_stream(pool, a.items, seed=a.seed + 31 * rank + 1, replicate=True)
+    tb = wl.tx_sig_stream(pool, pool_schemes, idx, ids, id_idx, nthreads=threads)
     labels, schemes = pool_labels[idx], pool_schemes[idx]
     gen_s = time.time() - t0
     eng = Engine(local, chunk_items=a.chunk_items, stage_timing=True)
     eng.reserve(len(batch.keys), batch.n)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-    bufs = upload(dev, batch)
-    gather = None
-    if world > 1:
-        gather = lambda sd: shard.gather_verdicts(sd, world * batch.n, world)  # noqa: E731  RCCL all-gather
-    step = timed_device(eng, bufs, batch, a.steps, a.warmup, stream, dev, gather, ctx_stream=a.stream == "ctx")
+    holder = {}
+
+    def step():
+        # the whole node: host arena -> host verdicts, one cg_verify_tx_signatures call (synchronous)
+        holder["st"] = eng.verify_tx_signatures(tb)
+        if world > 1:  # RCCL all-gather of the per-GPU verdict vectors
+            holder["all"] = shard.gather_verdicts(torch.from_numpy(holder["st"]).to(dev), world * tb.n, world)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
     eng.stage_times()  # drop the warmup's records
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t = time.perf_counter()
+    cg_ms = []
     for _ in range(a.steps):
         step()
+        cg_ms.append(dict(eng.last_stats))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -567,7 +628,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     stages = eng.stage_times()
-    st = bufs[3].cpu().numpy()
+    st = holder["st"]
 
     # ---- verdict checks: labels, and every draw of a pool item gets that item's verdict
     ver = check_verdicts(st, expected_verdicts(labels, schemes))
@@ -589,15 +650,21 @@ def main():
                 if "valu_issue" in tr:
                     roof["valu_issue"] = tr["valu_issue"]
 
-    extra = {"stages": stage_summary(stages, a.steps), "ecdsa_ladders": ec_roof}
+    h2d_bytes = int(tb.arena.size + tb.sigs.nbytes + tb.ids.nbytes + tb.keys.nbytes)
+    extra = {"stages": stage_summary(stages, a.steps), "ecdsa_ladders": ec_roof,
+             "headline_h2d": {"bytes_per_call": h2d_bytes, "bytes_per_sig": round(h2d_bytes / tb.n, 1),
+                              "GBps_effective": round(h2d_bytes * a.steps / elapsed / 1e9, 1),
+                              "cg_stats_ms_mean": {k: round(float(np.mean([c[k] for c in cg_ms])), 3)
+                                                   for k in ("ms_h2d", "ms_verify", "ms_d2h", "ms_total")}}}
+    if rank == 0 and world == 1 and a.device_steps > 0:
+        extra["device_resident"] = bench_device(eng, dev, stream, batch, tb, st, a.device_steps)
     if rank == 0 and world == 1 and a.host_steps > 0:
-        extra["host_e2e"] = bench_host(eng, batch, st, a.host_steps)
+        extra["host_message_form"] = bench_host(eng, batch, st, a.host_steps)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(batch, st, a.cpu_seconds, threads)
         if a.configs0_txs > 0:
             cpu["configs0"] = configs0(a, eng, wl, threads)
-    del bufs
     torch.cuda.empty_cache()
     if world == 1:
         for name, on, fn in (("configs1_ed25519", a.configs1_items, lambda: bench_configs1(a, eng, dev, stream, wl, threads)),
@@ -616,14 +683,18 @@ def main():
             "metric": METRIC, "value": round(total / elapsed, 1), "unit": "sigs/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic: seeded RFC 8032 Ed25519 + ECDSA (secp256r1/k1) signatures with every Appendix A "
-                    "corruption class (tools/workload), no JVM capture",
-            "config": {"workload": "BASELINE configs[4] per-GPU shard: notary-style mixed batch, 70% Ed25519 / 20% "
-                                   "secp256r1 / 10% secp256k1, 12.5M items per GPU (100M at 8 GPUs), inputs resident "
-                                   "in HBM, one cg_verify_batch_device call per step",
+            "data": "synthetic: seeded RFC 8032 Ed25519 + ECDSA (secp256r1/k1) signatures over "
+                    "SignableData(txId, SignatureMetadata(1, scheme)) with every Appendix A corruption class "
+                    "(tools/workload), no JVM capture",
+            "config": {"workload": "BASELINE configs[4] per-GPU shard, whole node: notary-style mixed batch, 70% "
+                                   "Ed25519 / 20% secp256r1 / 10% secp256k1, 12.5M signatures per GPU (100M at 8 GPUs), "
+                                   f"{a.sigs_per_tx} signatures per tx id; host arena -> host verdicts, one "
+                                   "cg_verify_tx_signatures call per step (batch Crypto.doVerify(txId, sig): key table, "
+                                   "ids, signature table and signature bytes copied from pageable host memory, "
+                                   "SignableData spliced on the device, verdicts copied back)",
                        "items_per_gpu": a.items, "unique_pool": a.pool, "mix": {"ed25519": n_ed, "secp256r1": n_r1,
                                                                               "secp256k1": a.items - n_ed - n_r1},
-                       "keys": len(batch.keys), "msg_len": a.msg_len, "arena_bytes_per_gpu": int(batch.arena.size),
+                       "keys": len(batch.keys), "tx_ids_per_gpu": int(tb.n_ids), "h2d_bytes_per_gpu": h2d_bytes,
                        "device_chunk_items": eng_chunk(a),
                        "parallelism": f"shard{world}" + ("+rccl_allgather(verdicts)" if world > 1 else "")},
             "roofline": roof, "cpu_baseline": cpu, "secondary": extra, "verdicts": ver,

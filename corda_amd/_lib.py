@@ -86,6 +86,11 @@ def lib():
                                                  vp, vp]
             L.cg_verify_transactions_device.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp, u64, vp, u32, vp, u64,
                                                         u32, vp, vp, vp, vp]
+            L.cg_verify_tx_signatures.argtypes = [vp, vp, u32, vp, u64, vp, u64, vp, u32, vp, u64, u32, vp,
+                                                  ctypes.POINTER(cg_stats)]
+            L.cg_verify_tx_signatures.restype = i32
+            L.cg_verify_tx_signatures_device.argtypes = [vp, vp, u32, vp, u64, vp, u64, vp, u32, vp, u64, u32, vp, vp]
+            L.cg_verify_tx_signatures_device.restype = i32
             L.cg_verify_filtered.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u64, vp]
             L.cg_verify_filtered_device.argtypes = [vp, vp, u64, vp, u64, vp, u64, vp, u64, vp, vp]
             if hasattr(L, "cg_stage_times"):
@@ -103,6 +108,9 @@ def lib():
                 L.cg_pool_slot_healthy.restype = i32
                 L.cg_pool_verify_batch.argtypes = [vp, vp, u32, vp, u64, vp, u64, u32, vp, ctypes.POINTER(cg_pool_stats)]
                 L.cg_pool_verify_batch.restype = i32
+                L.cg_pool_verify_tx_signatures.argtypes = [vp, vp, u32, vp, u64, vp, u64, vp, u32, vp, u64, u32, vp,
+                                                           ctypes.POINTER(cg_pool_stats)]
+                L.cg_pool_verify_tx_signatures.restype = i32
                 L.cg_pool_inject_fault.argtypes = [vp, u32, i32]
                 L.cg_pool_inject_fault.restype = i32
             for name in ("cg_verify_filtered", "cg_verify_filtered_device", "cg_verify_transactions", "cg_verify_transactions_device", "cg_reserve", "cg_verify_batch", "cg_verify_batch_device", "cg_sha256_batch",

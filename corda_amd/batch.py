@@ -184,3 +184,75 @@ class BatchBuilder:
             items["sig_len"] = arr[:, 4]
         arena = np.frombuffer(b"".join(self._chunks) + bytes(16), dtype=np.uint8).copy()
         return Batch(keys, items, arena)
+
+
+class TxSigBatch:
+    """Signatures over known transaction ids (cg_verify_tx_signatures): ``keys`` (KEY_DTYPE),
+    ``ids`` (uint8 [n_ids * 32], the SecureHash bytes), ``sigs`` (TXSIG_DTYPE: tx_idx indexes ids,
+    tmpl indexes tmpls), ``tmpls`` (TMPL_DTYPE: SignableData prefix / suffix per SignatureMetadata
+    value, bytes in the arena), ``arena`` (uint8: key, template and signature bytes)."""
+
+    def __init__(self, keys, ids, sigs, tmpls, arena):
+        self.keys = keys
+        self.ids = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1)
+        self.sigs = sigs
+        self.tmpls = tmpls
+        self.arena = arena
+
+    @property
+    def n(self):
+        return len(self.sigs)
+
+    @property
+    def n_ids(self):
+        return self.ids.size // 32
+
+
+class TxSigBuilder(BatchBuilder):
+    """Packs (tx id, TransactionSignature) pairs the way a JVM caller of cg_verify_tx_signatures
+    would: one key per distinct PublicKey, one id per distinct tx id, one template per distinct
+    SignatureMetadata (its SignableData prefix / suffix), then the signature bytes."""
+
+    def __init__(self):
+        super().__init__()
+        self._ids, self._id_index = [], {}
+        self._tmpls, self._tmpl_index = [], {}
+        self._sigs = []
+
+    def tx_id(self, tx_id):
+        tx_id = bytes(tx_id)
+        if len(tx_id) != 32:
+            raise ValueError("a SecureHash.SHA256 id is 32 bytes")
+        idx = self._id_index.get(tx_id)
+        if idx is None:
+            idx = self._id_index[tx_id] = len(self._ids)
+            self._ids.append(tx_id)
+        return idx
+
+    def template(self, prefix, suffix):
+        k = (bytes(prefix), bytes(suffix))
+        idx = self._tmpl_index.get(k)
+        if idx is None:
+            if len(self._tmpls) >= 0x10000:
+                raise ValueError("more than 65536 SignatureMetadata templates in one batch")
+            idx = self._tmpl_index[k] = len(self._tmpls)
+            self._tmpls.append((self._append(k[0], 4), self._append(k[1], 4), len(k[0]), len(k[1])))
+        return idx
+
+    def add_signature(self, key_idx, tx_idx, tmpl_idx, sig):
+        sig = sig_field(self._keys[key_idx][2], sig)
+        self._sigs.append((self._append(sig, 4), tx_idx, key_idx, len(sig), tmpl_idx))
+        return len(self._sigs) - 1
+
+    def build(self):
+        b = super().build()
+        sigs = np.zeros(len(self._sigs), dtype=TXSIG_DTYPE)
+        if self._sigs:
+            arr = np.array(self._sigs, dtype=np.uint64)
+            sigs["sig_off"], sigs["tx_idx"], sigs["key_idx"] = arr[:, 0], arr[:, 1], arr[:, 2]
+            sigs["sig_len"], sigs["tmpl"] = arr[:, 3], arr[:, 4]
+        tmpls = np.zeros(len(self._tmpls), dtype=TMPL_DTYPE)
+        for i, t in enumerate(self._tmpls):
+            tmpls[i] = t
+        ids = np.frombuffer(b"".join(self._ids), dtype=np.uint8).copy() if self._ids else np.zeros(0, np.uint8)
+        return TxSigBatch(b.keys, ids, sigs, tmpls, b.arena)

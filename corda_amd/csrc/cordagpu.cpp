@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -160,7 +161,12 @@ cg::WidePool wide_for(cg_ctx* c, uint32_t n_keys, uint64_t n_items) {
 // Key tables once for the whole call (sized by every item's key use), then the items in chunks.
 hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                           const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, hipStream_t s,
-                          const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0) {
+                          const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0,
+                          const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* before_front = nullptr) {
+  // before_front (host-buffer entry points): called with (k, first item, items) just before chunk
+  // k's front is enqueued; it makes chunk k's arena bytes resident and orders `s` after them. The
+  // plans and the key-table builds need only the item table, so they are enqueued first and run
+  // while the host copies the first chunk.
   if (n_items == 0) return hipSuccess;
   const cg::WidePool wp = wide_for(c, n_keys, n_items);
   hipError_t e =
@@ -175,16 +181,22 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
     return cg::launch_items_plan(d_keys, n_keys, d_items + k * per, cnt(k), d_status + k * per, c->keyprep.p, ws(k),
                                  s, &c->fork, &wp);
   };
+  const bool pre_plan = two || before_front;
   auto front = [&](uint64_t k) {
+    if (before_front) {
+      const hipError_t w = (*before_front)(k, k * per, cnt(k));
+      if (w != hipSuccess) return w;
+    }
     return cg::launch_items_front(d_keys, n_keys, d_items + k * per, cnt(k), d_arena, arena_len, mode,
                                   d_status + k * per, c->keyprep.p, ws(k), s, d_msgs, msgs_len, &c->fork, &wp,
-                                  two && k < 2);
+                                  (k == 0 && pre_plan) || (k == 1 && two));
   };
   // chunk k + 1's front (plan, hashes, ECDSA prep) before chunk k's back (ladders): the first
   // chunk's wait for the key tables is spent on the next chunk's fronts. The first two plans sort
   // before the table builds start (their look-back stalls behind the builds).
-  if (e == hipSuccess && two) e = plan(0);
+  if (e == hipSuccess && pre_plan) e = plan(0);
   if (e == hipSuccess && two) e = plan(1);
+  if (e == hipSuccess && before_front) e = cg::launch_key_tables(&c->fork, s);
   if (e == hipSuccess) e = front(0);
   for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
     if (!two && k > 0) e = front(k);
@@ -836,6 +848,208 @@ int cg_verify_transactions(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_
   return CG_OK;
 }
 
+// ---------------------------------------------------------------- signatures over known tx ids
+// The spliced-message slot of a template set: the longest prefix || id || suffix, 16-aligned.
+static uint64_t tmpl_slot(const cg_signable_tmpl* tmpls, uint32_t n_tmpls) {
+  uint64_t maxlen = 0;
+  for (uint32_t k = 0; k < n_tmpls; ++k) {
+    const uint64_t l = (uint64_t)tmpls[k].prefix_len + 32u + tmpls[k].suffix_len;
+    if (l > maxlen) maxlen = l;
+  }
+  const uint64_t slot = (maxlen + 15) & ~(uint64_t)15;
+  return slot ? slot : 16;
+}
+
+// Verify items, spliced messages and the template table of n_sigs signatures (waits for the device
+// when a buffer grows).
+static hipError_t ensure_txsig_ws(cg_ctx* c, uint64_t n_sigs, uint32_t n_tmpls, uint64_t slot) {
+  const size_t need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1), need_msgs = slot * (n_sigs ? n_sigs : 1),
+               need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
+  if (c->txitems.cap >= need_items && c->msgs.cap >= need_msgs && c->tmpls.cap >= need_tmpl) return hipSuccess;
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = c->txitems.ensure(need_items);
+  if (e == hipSuccess) e = c->msgs.ensure(need_msgs);
+  if (e == hipSuccess) e = c->tmpls.ensure(need_tmpl);
+  return e;
+}
+
+// Templates to the device, one verify item + spliced SignableData per signature, then the chunked
+// verify (key tables sized by every signature's key).
+static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_ids, uint64_t n_ids,
+                               const cg_txsig* d_sigs, uint64_t n_sigs, const cg_signable_tmpl* tmpls,
+                               uint32_t n_tmpls, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
+                               uint8_t* d_status, hipStream_t s, uint64_t slot,
+                               const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* before_front) {
+  if (n_sigs == 0) return hipSuccess;
+  hipError_t e = hipSuccess;
+  if (n_tmpls)
+    e = hipMemcpyAsync(c->tmpls.p, tmpls, sizeof(cg_signable_tmpl) * n_tmpls, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = cg::launch_tx_sig_items(d_sigs, n_sigs, (const cg_signable_tmpl*)c->tmpls.p, n_tmpls, nullptr, n_ids, d_ids,
+                                d_arena, arena_len, slot, (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s);
+  if (e == hipSuccess)
+    e = launch_chunked(c, d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode, d_status, s,
+                       (const uint8_t*)c->msgs.p, slot * n_sigs, before_front);
+  return e;
+}
+
+// cg_verify_tx_signatures with the ctx lock held. Host side, in order: the key table and key bytes,
+// the template bytes, the ids and the signature table (everything the key tables and the plans
+// need), then the signature bytes chunk by chunk, each copy issued just before its chunk's front
+// so that the key-table builds and the previous chunk's kernels run during it.
+static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const uint8_t* ids,
+                                    uint64_t n_ids, const cg_txsig* sigs, uint64_t n_sigs,
+                                    const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
+                                    uint64_t arena_len, uint32_t mode, uint8_t* status_out, cg_stats* stats) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (c->fault) return fail(CG_ERR_DEVICE, "cg_verify_tx_signatures: device fault (injected by cg_pool_inject_fault)");
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  const uint64_t per = chunk_of(c, n_sigs);
+  const uint64_t nch = (n_sigs + per - 1) / per;
+  // arena extents: key bytes + template bytes (the header), then each chunk's signature bytes
+  Extent head, win;
+  for (uint32_t k = 0; k < n_keys; ++k) head.add(keys[k].off, keys[k].len, arena_len);
+  for (uint32_t k = 0; k < n_tmpls; ++k) {
+    head.add(tmpls[k].prefix_off, tmpls[k].prefix_len, arena_len);
+    head.add(tmpls[k].suffix_off, tmpls[k].suffix_len, arena_len);
+  }
+  std::vector<Extent> ext(nch);
+  {
+    auto scan = [&](uint64_t k0, uint64_t k1) {
+      for (uint64_t k = k0; k < k1; ++k) {
+        const uint64_t e = (k + 1) * per < n_sigs ? (k + 1) * per : n_sigs;
+        for (uint64_t i = k * per; i < e; ++i) ext[k].add(sigs[i].sig_off, sigs[i].sig_len, arena_len);
+      }
+    };
+    const uint64_t nt = nch < 16 ? nch : 16;
+    if (n_sigs < (1u << 16) || nt < 2) {
+      scan(0, nch);
+    } else {
+      std::vector<std::thread> th;
+      for (uint64_t t = 0; t < nt; ++t) th.emplace_back(scan, nch * t / nt, nch * (t + 1) / nt);
+      for (auto& t : th) t.join();
+    }
+  }
+  win = head;
+  for (const Extent& e : ext) win.merge(e);
+  if (win.empty()) win.lo = win.hi = 0;
+  win.lo &= ~(uint64_t)15;  // the device window starts 16-aligned (kernels load aligned words)
+  const uint64_t slot = tmpl_slot(tmpls, n_tmpls);
+  HIP_TRY(c->keys.ensure(sizeof(cg_key) * (n_keys ? n_keys : 1)), "hipMalloc(keys)");
+  HIP_TRY(c->h_sigs.ensure(sizeof(cg_txsig) * n_sigs), "hipMalloc(sigs)");
+  HIP_TRY(c->h_ids.ensure(32 * (n_ids ? n_ids : 1)), "hipMalloc(ids)");
+  HIP_TRY(c->arena.ensure((win.hi - win.lo) + 16), "hipMalloc(arena window)");
+  HIP_TRY(c->status.ensure(n_sigs), "hipMalloc(status)");
+  HIP_TRY(ensure_txsig_ws(c, n_sigs, n_tmpls, slot), "hipMalloc(tx signature workspace)");
+  HIP_TRY(ensure_ws(c, n_keys, per, n_sigs), "hipMalloc(workspace)");
+  while (c->seg.size() < nch + 1) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    c->seg.push_back(e);
+  }
+  hipStream_t s = c->stream;
+  uint8_t* dwin = (uint8_t*)c->arena.p;
+  const uint8_t* dbase = dwin - win.lo;  // kernels index the arena by absolute offsets
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
+  HIP_TRY(hipEventRecord(c->tev[0], s), "hipEventRecord");
+  HIP_TRY(hipStreamWaitEvent(c->copy, c->tev[0], 0), "hipStreamWaitEvent");
+  std::vector<std::pair<uint64_t, uint64_t>> have;
+  if (n_keys)
+    HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, c->copy), "H2D keys");
+  HIP_TRY(copy_missing(have, head, arena, dwin, win.lo, c->copy), "H2D key / template bytes");
+  if (n_ids) HIP_TRY(hipMemcpyAsync(c->h_ids.p, ids, 32 * n_ids, hipMemcpyHostToDevice, c->copy), "H2D ids");
+  HIP_TRY(hipMemcpyAsync(c->h_sigs.p, sigs, sizeof(cg_txsig) * n_sigs, hipMemcpyHostToDevice, c->copy), "H2D sigs");
+  HIP_TRY(hipEventRecord(c->seg[nch], c->copy), "hipEventRecord");
+  HIP_TRY(hipStreamWaitEvent(s, c->seg[nch], 0), "hipStreamWaitEvent");
+  hipError_t copy_err = hipSuccess;
+  const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t, uint64_t) {
+    hipError_t e = copy_missing(have, ext[k], arena, dwin, win.lo, c->copy);
+    if (e == hipSuccess) e = hipEventRecord(c->seg[k], c->copy);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, c->seg[k], 0);
+    if (e == hipSuccess && k == 0) e = hipEventRecord(c->tev[1], s);
+    if (e != hipSuccess) copy_err = e;
+    return e;
+  };
+  uint8_t* ds = (uint8_t*)c->status.p;
+  const hipError_t le = launch_txsig(c, (const cg_key*)c->keys.p, n_keys, (const uint8_t*)c->h_ids.p, n_ids,
+                                     (const cg_txsig*)c->h_sigs.p, n_sigs, tmpls, n_tmpls, dbase, arena_len, mode, ds,
+                                     s, slot, &before);
+  if (copy_err != hipSuccess) return hip_fail(copy_err, "H2D signature bytes");
+  HIP_TRY(le, "launch_txsig");
+  HIP_TRY(hipEventRecord(c->tev[2], s), "hipEventRecord");
+  HIP_TRY(hipMemcpyAsync(status_out, ds, n_sigs, hipMemcpyDeviceToHost, s), "D2H status");
+  HIP_TRY(hipEventRecord(c->tev[3], s), "hipEventRecord");
+  HIP_TRY(order_out(c, s), "hipEventRecord");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (stats) {
+    float a = 0, b = 0, d = 0;
+    hipEventElapsedTime(&a, c->tev[0], c->tev[1]);
+    hipEventElapsedTime(&b, c->tev[1], c->tev[2]);
+    hipEventElapsedTime(&d, c->tev[2], c->tev[3]);
+    stats->n_items = n_sigs;
+    stats->n_keys = n_keys;
+    stats->ms_h2d = a;
+    stats->ms_key_prep = 0;
+    stats->ms_verify = b;
+    stats->ms_d2h = d;
+    stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return CG_OK;
+}
+
+static int txsig_args(const char* fn, cg_ctx* c, uint32_t n_keys, const void* keys, uint64_t n_ids, const void* ids,
+                      uint64_t n_sigs, const void* sigs, const void* status, uint32_t n_tmpls, const void* tmpls,
+                      uint32_t mode) {
+  if (!c) return fail(CG_ERR_ARG, "%s: ctx is NULL", fn);
+  if (n_sigs && (!sigs || !status)) return fail(CG_ERR_ARG, "%s: NULL signature / status buffer", fn);
+  if (n_keys && !keys) return fail(CG_ERR_ARG, "%s: keys is NULL", fn);
+  if (n_ids && !ids) return fail(CG_ERR_ARG, "%s: ids is NULL", fn);
+  if (n_tmpls && !tmpls) return fail(CG_ERR_ARG, "%s: templates is NULL", fn);
+  if (n_tmpls > 0x10000u) return fail(CG_ERR_ARG, "%s: more than 65536 templates (cg_txsig.tmpl is 16-bit)", fn);
+  if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "%s: bad mode", fn);
+  return CG_OK;
+}
+
+int cg_verify_tx_signatures_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_ids,
+                                   uint64_t n_ids, const cg_txsig* d_sigs, uint64_t n_sigs,
+                                   const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* d_arena,
+                                   uint64_t arena_len, uint32_t mode, uint8_t* d_status, void* hip_stream) {
+  const int a = txsig_args("cg_verify_tx_signatures_device", c, n_keys, d_keys, n_ids, d_ids, n_sigs, d_sigs, d_status,
+                           n_tmpls, tmpls, mode);
+  if (a != CG_OK) return a;
+  if (n_sigs == 0) return CG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->fault) return fail(CG_ERR_DEVICE, "cg_verify_tx_signatures_device: device fault (injected)");
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  const uint64_t slot = tmpl_slot(tmpls, n_tmpls);
+  HIP_TRY(ensure_txsig_ws(c, n_sigs, n_tmpls, slot), "hipMalloc(tx signature workspace)");
+  HIP_TRY(ensure_ws(c, n_keys, chunk_of(c, n_sigs), n_sigs), "hipMalloc(workspace)");
+  hipStream_t s = stream_of(c, hip_stream);
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
+  HIP_TRY(launch_txsig(c, d_keys, n_keys, d_ids, n_ids, d_sigs, n_sigs, tmpls, n_tmpls, d_arena, arena_len, mode,
+                       d_status, s, slot, nullptr),
+          "launch_txsig");
+  HIP_TRY(order_out(c, s), "hipEventRecord");
+  return CG_OK;
+}
+
+int cg_verify_tx_signatures(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const uint8_t* ids, uint64_t n_ids,
+                            const cg_txsig* sigs, uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,
+                            const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
+                            cg_stats* stats) {
+  const int a = txsig_args("cg_verify_tx_signatures", c, n_keys, keys, n_ids, ids, n_sigs, sigs, status_out, n_tmpls,
+                           tmpls, mode);
+  if (a != CG_OK) return a;
+  if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_verify_tx_signatures: arena is NULL");
+  if (n_sigs) memset(status_out, CG_NOT_RUN, n_sigs);
+  if (n_sigs == 0) return CG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  const int rc = verify_txsig_host_locked(c, keys, n_keys, ids, n_ids, sigs, n_sigs, tmpls, n_tmpls, arena, arena_len,
+                                          mode, status_out, stats);
+  if (rc != CG_OK) memset(status_out, CG_NOT_RUN, n_sigs);
+  return rc;
+}
+
 int cg_verify_filtered_device(cg_ctx* c, const cg_filtered_tx* d_ftxs, uint64_t n_ftx, const cg_pmt_node* d_nodes,
                               uint64_t n_nodes, const cg_filtered_leaf* d_leaves, uint64_t n_leaves,
                               const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_status, void* hip_stream) {
@@ -943,14 +1157,9 @@ int cg_pool_inject_fault(cg_pool* p, uint32_t slot, int on) {
   return CG_OK;
 }
 
-int cg_pool_verify_batch(cg_pool* p, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
-                         const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
-                         cg_pool_stats* stats) {
-  if (!p) return fail(CG_ERR_ARG, "cg_pool_verify_batch: pool is NULL");
-  if (n_items && (!items || !status_out)) return fail(CG_ERR_ARG, "cg_pool_verify_batch: NULL buffer");
-  if (n_keys && !keys) return fail(CG_ERR_ARG, "cg_pool_verify_batch: keys is NULL");
-  if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_pool_verify_batch: arena is NULL");
-  if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_pool_verify_batch: bad mode");
+// pool_run over one shard function; stats and the error message as cg_pool_verify_batch
+static int pool_call(cg_pool* p, uint64_t n_items, uint8_t* status_out, cg_pool_stats* stats, const char* name,
+                     const std::function<int(cg_ctx*, uint64_t, uint64_t)>& shard) {
   const auto t0 = std::chrono::steady_clock::now();
   std::lock_guard<std::mutex> g(p->mu);
   std::vector<std::string> errs(p->ctx.size());
@@ -959,8 +1168,7 @@ int cg_pool_verify_batch(cg_pool* p, const cg_key* keys, uint32_t n_keys, const 
                               [&](uint32_t slot, uint64_t first, uint64_t count) {
                                 cg_ctx* c = p->ctx[slot];
                                 std::lock_guard<std::mutex> gc(c->mu);
-                                const int r = verify_host_locked(c, keys, n_keys, items + first, count, arena,
-                                                                 arena_len, mode, status_out + first, nullptr);
+                                const int r = shard(c, first, count);
                                 if (r != CG_OK) errs[slot] = g_err;  // g_err is this worker thread's
                                 return r;
                               },
@@ -981,13 +1189,44 @@ int cg_pool_verify_batch(cg_pool* p, const cg_key* keys, uint32_t n_keys, const 
     stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   if (rc != CG_OK) {
-    std::string m = rc == CG_ERR_DEVICE ? "cg_pool_verify_batch: no healthy slot could run every shard;"
-                                        : "cg_pool_verify_batch: a shard failed (not a device fault);";
+    std::string m = std::string(name) + (rc == CG_ERR_DEVICE ? ": no healthy slot could run every shard;"
+                                                             : ": a shard failed (not a device fault);");
     for (size_t k = 0; k < errs.size(); ++k)
       if (!errs[k].empty()) m += " [slot " + std::to_string(k) + "] " + errs[k];
     g_err = m;
   }
   return rc;
+}
+
+int cg_pool_verify_tx_signatures(cg_pool* p, const cg_key* keys, uint32_t n_keys, const uint8_t* ids, uint64_t n_ids,
+                                 const cg_txsig* sigs, uint64_t n_sigs, const cg_signable_tmpl* tmpls,
+                                 uint32_t n_tmpls, const uint8_t* arena, uint64_t arena_len, uint32_t mode,
+                                 uint8_t* status_out, cg_pool_stats* stats) {
+  if (!p) return fail(CG_ERR_ARG, "cg_pool_verify_tx_signatures: pool is NULL");
+  if (p->ctx.empty()) return fail(CG_ERR_ARG, "cg_pool_verify_tx_signatures: empty pool");
+  const int a = txsig_args("cg_pool_verify_tx_signatures", p->ctx[0], n_keys, keys, n_ids, ids, n_sigs, sigs,
+                           status_out, n_tmpls, tmpls, mode);
+  if (a != CG_OK) return a;
+  if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_pool_verify_tx_signatures: arena is NULL");
+  return pool_call(p, n_sigs, status_out, stats, "cg_pool_verify_tx_signatures",
+                   [&](cg_ctx* c, uint64_t first, uint64_t count) {
+                     return verify_txsig_host_locked(c, keys, n_keys, ids, n_ids, sigs + first, count, tmpls, n_tmpls,
+                                                     arena, arena_len, mode, status_out + first, nullptr);
+                   });
+}
+
+int cg_pool_verify_batch(cg_pool* p, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
+                         const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
+                         cg_pool_stats* stats) {
+  if (!p) return fail(CG_ERR_ARG, "cg_pool_verify_batch: pool is NULL");
+  if (n_items && (!items || !status_out)) return fail(CG_ERR_ARG, "cg_pool_verify_batch: NULL buffer");
+  if (n_keys && !keys) return fail(CG_ERR_ARG, "cg_pool_verify_batch: keys is NULL");
+  if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_pool_verify_batch: arena is NULL");
+  if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_pool_verify_batch: bad mode");
+  return pool_call(p, n_items, status_out, stats, "cg_pool_verify_batch", [&](cg_ctx* c, uint64_t first, uint64_t count) {
+    return verify_host_locked(c, keys, n_keys, items + first, count, arena, arena_len, mode, status_out + first,
+                              nullptr);
+  });
 }
 
 }  // extern "C"

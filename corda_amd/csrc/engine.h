@@ -120,6 +120,9 @@ size_t item_ws_bytes(uint64_t n_items);
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream, const Fork* fork = nullptr,
                           const cg_item* d_items = nullptr, uint64_t n_items = 0, const WidePool* wide = nullptr);
+// Start the table builds launch_keyprep deferred (no-op if already started): a host-buffer call
+// starts them before it blocks on the first chunk's arena copy, so they overlap that copy.
+hipError_t launch_key_tables(const Fork* fork, hipStream_t stream);
 // `d_msgs` (optional): the engine's spliced-message workspace, read by items flagged
 // CG_ITEM_MSG_WS (keyws.h); caller items never carry that flag.
 hipError_t launch_items(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,

@@ -4,7 +4,8 @@
 //   k_txsig_items   one lane per signature: a cg_item whose clear data is its slot in the
 //                   spliced-message workspace (flag CG_ITEM_MSG_WS), or an out-of-range key
 //                   index (-> CG_NOT_RUN) when its transaction has no id or its template /
-//                   transaction index is invalid
+//                   transaction index is invalid. tx_status == nullptr: the ids are the
+//                   caller's (cg_verify_tx_signatures*), every one valid
 //   k_splice        one lane per dword of every message slot: prefix || id || suffix, i.e.
 //                   SignableData(id, metadata).serialize() (Crypto.kt:499-502) for the
 //                   signature's metadata template; coalesced 4-byte stores
@@ -32,7 +33,7 @@ __global__ void __launch_bounds__(256) k_txsig_items(const cg_txsig* __restrict_
   it.sig_len = s.sig_len;
   it.reserved1 = 0;
   bool ok = s.tx_idx < n_tx && s.tmpl < n_tmpls;
-  if (ok) ok = tx_status[s.tx_idx] == 0;
+  if (ok && tx_status) ok = tx_status[s.tx_idx] == 0;
   cg_signable_tmpl t = {0, 0, 0, 0};
   if (ok) {
     t = tmpls[s.tmpl];
@@ -63,7 +64,7 @@ __global__ void __launch_bounds__(256) k_splice(const cg_txsig* __restrict__ sig
   if (j >= n_sigs) return;
   const cg_txsig s = sigs[j];
   uint32_t v = 0;
-  if (s.tx_idx < n_tx && s.tmpl < n_tmpls && tx_status[s.tx_idx] == 0) {
+  if (s.tx_idx < n_tx && s.tmpl < n_tmpls && (!tx_status || tx_status[s.tx_idx] == 0)) {
     const cg_signable_tmpl t = tmpls[s.tmpl];
     if (tmpl_ok(t, arena_len)) {
       const uint64_t n = (uint64_t)t.prefix_len + 32u + t.suffix_len;

@@ -163,6 +163,10 @@ static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
   return e;
 }
 
+hipError_t launch_key_tables(const Fork* fork, hipStream_t stream) {
+  return fork ? launch_pending_tabs(fork, stream) : hipSuccess;
+}
+
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream, const Fork* fork, const cg_item* d_items,
                           uint64_t n_items, const WidePool* wide) {

@@ -182,6 +182,29 @@ class Engine:
                                                       d_tx_status, d_sig_status, stream or None)
         _lib.check(rc, "cg_verify_transactions_device")
 
+    # ------------------------------------------------------------------ signatures over tx ids
+    def verify_tx_signatures(self, tb, mode=MODE_DOVERIFY):
+        """Batch Crypto.doVerify(txId, TransactionSignature) (cg_verify_tx_signatures, Crypto.kt:499-502):
+        ``tb`` is a batch.TxSigBatch; each signature's clear data is SignableData(id, metadata),
+        spliced on the device. Returns one status byte per signature; cg_stats in last_stats."""
+        st = np.full(len(tb.sigs), 255, dtype=np.uint8)
+        stats = _lib.cg_stats()
+        rc = _lib.lib().cg_verify_tx_signatures(self._h, _p(tb.keys), len(tb.keys), _p(tb.ids), tb.n_ids, _p(tb.sigs),
+                                                len(tb.sigs), _p(tb.tmpls), len(tb.tmpls), _p(tb.arena), tb.arena.size,
+                                                mode, _p(st), ctypes.byref(stats))
+        _lib.check(rc, "cg_verify_tx_signatures")
+        self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_stats._fields_}
+        return st
+
+    def verify_tx_signatures_device(self, d_keys, n_keys, d_ids, n_ids, d_sigs, n_sigs, tmpls, d_arena, arena_len,
+                                    d_status, mode=MODE_DOVERIFY, stream=0):
+        """Asynchronous device form; `tmpls` is a host TMPL_DTYPE array (template bytes in the arena)."""
+        assert tmpls.dtype == TMPL_DTYPE
+        rc = _lib.lib().cg_verify_tx_signatures_device(self._h, d_keys, n_keys, d_ids, n_ids, d_sigs, n_sigs,
+                                                       _p(tmpls), len(tmpls), d_arena, arena_len, mode, d_status,
+                                                       stream or None)
+        _lib.check(rc, "cg_verify_tx_signatures_device")
+
 
 class EnginePool:
     """One process, several devices (cg_pool): ``verify(batch)`` shards the items over the healthy
@@ -230,4 +253,16 @@ class EnginePool:
         self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_pool_stats._fields_ if k != "reserved"}
         if rc != 0 and not allow_partial:
             _lib.check(rc, "cg_pool_verify_batch")
+        return st
+
+    def verify_tx_signatures(self, tb, mode=MODE_DOVERIFY, allow_partial=False):
+        """cg_pool_verify_tx_signatures: the signature table sharded over the healthy slots."""
+        st = np.full(len(tb.sigs), 255, dtype=np.uint8)
+        stats = _lib.cg_pool_stats()
+        rc = _lib.lib().cg_pool_verify_tx_signatures(self._h, _p(tb.keys), len(tb.keys), _p(tb.ids), tb.n_ids,
+                                                     _p(tb.sigs), len(tb.sigs), _p(tb.tmpls), len(tb.tmpls),
+                                                     _p(tb.arena), tb.arena.size, mode, _p(st), ctypes.byref(stats))
+        self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_pool_stats._fields_ if k != "reserved"}
+        if rc != 0 and not allow_partial:
+            _lib.check(rc, "cg_pool_verify_tx_signatures")
         return st

@@ -288,6 +288,32 @@ int cg_verify_transactions(cg_ctx* ctx, const cg_tx* txs, uint64_t n_tx, const c
                            uint64_t arena_len, uint32_t mode, uint8_t* ids_out, uint8_t* tx_status_out,
                            uint8_t* sig_status_out);
 
+/* ---- Signatures over known transaction ids: the batch form of
+ *   Crypto.doVerify(txId, transactionSignature)   core/.../crypto/Crypto.kt:499-502
+ *     = doVerify(sig.by, sig.bytes, SignableData(txId, sig.signatureMetadata).serialize().bytes)
+ *   (TransactionSignature.kt:27 carries `by` + `signatureMetadata`), called per signature by
+ *   TransactionWithSignatures.checkSignaturesAreValid (TransactionWithSignatures.kt:58-61) and by
+ *   the out-of-process verifier for each received transaction.
+ * Such a caller holds the tx id and the signature's metadata, not message bytes: per signature it
+ * passes a cg_txsig (24 B) and the signature bytes, per transaction its 32-byte id, and one
+ * cg_signable_tmpl per SignatureMetadata value; the engine splices prefix || id || suffix on the
+ * device. cg_txsig.tx_idx indexes `ids` (32 * n_ids bytes), tmpl indexes `tmpls`. A signature
+ * whose id or template index is out of range, or whose template lies outside the arena, gets
+ * CG_NOT_RUN; every other status as cg_verify_batch.
+ * Host form: the key table, key and template bytes, ids and signature table are copied first
+ * (the key tables build from them), then each verify chunk's signature bytes just before the
+ * chunk runs, overlapping the key-table builds and the previous chunk's kernels. stats: ms_h2d =
+ * until the first chunk's bytes are resident, ms_verify = the rest. */
+int cg_verify_tx_signatures(cg_ctx* ctx, const cg_key* keys, uint32_t n_keys, const uint8_t* ids, uint64_t n_ids,
+                            const cg_txsig* sigs, uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,
+                            const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
+                            cg_stats* stats_opt);
+/* Device buffers in HBM except `tmpls` (a small host array); asynchronous on hip_stream. */
+int cg_verify_tx_signatures_device(cg_ctx* ctx, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_ids,
+                                   uint64_t n_ids, const cg_txsig* d_sigs, uint64_t n_sigs,
+                                   const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* d_arena,
+                                   uint64_t arena_len, uint32_t mode, uint8_t* d_status, void* hip_stream);
+
 /* ---- Tear-offs: FilteredTransaction.verify / PartialMerkleTree.verify.
  * Replaces, for a batch of filtered transactions (the non-validating notary's input,
  * NonValidatingNotaryFlow.kt:22-27), the serial
@@ -365,6 +391,13 @@ int cg_pool_slot_healthy(const cg_pool* pool, uint32_t slot);  /* 1 healthy, 0 f
 int cg_pool_verify_batch(cg_pool* pool, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
                          const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
                          cg_pool_stats* stats_opt);
+/* cg_verify_tx_signatures sharded the same way: contiguous, equal shards of the signature table,
+ * one per healthy slot, each shard a cg_verify_tx_signatures on its device (ids, keys and templates
+ * go to every device; each shard copies only its own signature bytes). */
+int cg_pool_verify_tx_signatures(cg_pool* pool, const cg_key* keys, uint32_t n_keys, const uint8_t* ids,
+                                 uint64_t n_ids, const cg_txsig* sigs, uint64_t n_sigs,
+                                 const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
+                                 uint64_t arena_len, uint32_t mode, uint8_t* status_out, cg_pool_stats* stats_opt);
 /* Failure drill: make every later call on `slot` fail as a device fault would (fail = 1), or
  * clear it and mark the slot healthy again (fail = 0). For tests and operational drills. */
 int cg_pool_inject_fault(cg_pool* pool, uint32_t slot, int fail);

@@ -1,0 +1,147 @@
+"""GPU tests of cg_verify_tx_signatures(_device) / cg_pool_verify_tx_signatures: the batch form of
+Crypto.doVerify(txId, TransactionSignature) (Crypto.kt:499-502), each signature's clear data
+SignableData(id, metadata) = prefix || id || suffix spliced on the device.
+
+Parity: the C oracle verifies the same signatures over the materialised SignableData bytes
+(tests/txsig_util.py); at full size (> 8M signatures, the configs[4] per-GPU shard in one call)
+through idempotence: every draw's verdict equals its pool item's, which equals the oracle's."""
+import numpy as np
+import pytest
+
+from corda_amd import batch as B
+from oracle import c_oracle
+
+import txsig_util
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def spool():
+    from corda_amd import signable
+    from tools.workload import wl
+    b, labels, schemes = wl.notary_pool(1 << 16, ed_keys=512, ec_keys=128, seed=91, nthreads=16, sig_group=4)
+    pre, _ = signable.template(1, 4)
+    ids, id_idx = wl.pool_ids(b, len(pre))
+    ref = c_oracle.verify_batch(b, B.MODE_DOVERIFY, 16)
+    return b, labels, schemes, ids, id_idx, ref
+
+
+def test_tx_signatures_host_and_device_vs_oracle(spool):
+    import torch
+    from corda_amd.engine import Engine
+    from tools.workload import wl
+    b, labels, schemes, ids, id_idx, ref = spool
+    idx = np.random.default_rng(3).integers(0, b.n, 150_000)
+    tb = wl.tx_sig_stream(b, schemes, idx, ids, id_idx, nthreads=16)
+    # the oracle on the materialised messages of a sample agrees with the pool verdicts
+    sub = np.random.default_rng(4).choice(tb.n, 4000, replace=False)
+    tsub = B.TxSigBatch(tb.keys, tb.ids, tb.sigs[sub], tb.tmpls, tb.arena)
+    assert np.array_equal(c_oracle.verify_batch(txsig_util.to_message_batch(tsub), 0, 16), ref[idx[sub]])
+    for chunk in (0, 40_001):
+        with Engine(0, chunk_items=chunk) as eng:
+            st = eng.verify_tx_signatures(tb)
+            assert np.array_equal(st, ref[idx]), f"host path (chunk {chunk}): {np.count_nonzero(st != ref[idx])} differ"
+            dev = torch.device("cuda", 0)
+            up = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).to(dev)  # noqa: E731
+            kd, ijd, sgd, ad = up(tb.keys), up(tb.ids), up(tb.sigs), up(tb.arena)
+            sd = torch.full((tb.n,), 255, dtype=torch.uint8, device=dev)
+            eng.verify_tx_signatures_device(kd.data_ptr(), len(tb.keys), ijd.data_ptr(), tb.n_ids, sgd.data_ptr(), tb.n,
+                                            tb.tmpls, ad.data_ptr(), tb.arena.size, sd.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(sd.cpu().numpy(), ref[idx]), "device path"
+            # message-form call on the same items gives the same verdicts
+            st_m = eng.verify(txsig_util.to_message_batch(B.TxSigBatch(tb.keys, tb.ids, tb.sigs[:20000], tb.tmpls,
+                                                                        tb.arena)))
+            assert np.array_equal(st_m, st[:20000])
+
+
+def test_tx_signatures_edges():
+    """Out-of-range id / template index -> NOT_RUN; templates of any length (odd, empty prefix or
+    suffix); isValid mode; an empty call; signatures before the keys in the arena."""
+    from corda_amd.engine import Engine
+    from corda_amd.batch import TxSigBuilder
+    import golden_io
+    items = [it for it in golden_io.load("ed25519.json") if it["expect"] in ("VALID", "INVALID")][:6]
+    rng = np.random.default_rng(8)
+    bld = TxSigBuilder()
+    tx = [bld.tx_id(rng.integers(0, 256, 32, dtype=np.uint8).tobytes()) for _ in range(3)]
+    tm = [bld.template(b"\x01\x02\x03", b""), bld.template(b"", b"\xfe" * 7), bld.template(b"p" * 233, b"s" * 5)]
+    for it in items:
+        bld.key(4, 0, bytes.fromhex(it["key"]))
+    # synthetic signatures: whatever the verdict, the engine must agree with the oracle on the
+    # materialised bytes
+    for j in range(60):
+        k = bld.key(4, 0, bytes.fromhex(items[j % len(items)]["key"]))
+        bld.add_signature(k, tx[j % 3], tm[j % 3], bytes.fromhex(items[(j * 7) % len(items)]["sig"]))
+    tb = bld.build()
+    tb.sigs[5]["tx_idx"] = 99        # no such id
+    tb.sigs[6]["tmpl"] = 40          # no such template
+    with Engine(0) as eng:
+        for mode in (B.MODE_DOVERIFY, B.MODE_ISVALID):
+            st = eng.verify_tx_signatures(tb, mode)
+            ref = c_oracle.verify_batch(txsig_util.to_message_batch(tb), mode, 4)
+            assert st[5] == B.NOT_RUN and st[6] == B.NOT_RUN
+            assert np.array_equal(st, ref)
+        empty = B.TxSigBatch(tb.keys, tb.ids, tb.sigs[:0], tb.tmpls, tb.arena)
+        assert eng.verify_tx_signatures(empty).size == 0
+
+
+def test_tx_signatures_valid_signable_data():
+    """Real signatures over SignableData(id, SignatureMetadata(1, 4)): VALID through the splice,
+    INVALID under another id or another metadata template."""
+    from corda_amd import signable
+    from corda_amd.batch import TxSigBuilder
+    from corda_amd.engine import Engine
+    from oracle import ed25519_i2p as ed
+    rng = np.random.default_rng(12)
+    bld = TxSigBuilder()
+    pre, suf = signable.template(1, 4)
+    pre3, suf3 = signable.template(1, 3)
+    t4, t3 = bld.template(pre, suf), bld.template(pre3, suf3)
+    expect = []
+    for j in range(24):
+        seed = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        pub = ed.public_from_seed(seed)
+        txid = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        sig = ed.sign(seed, signable.serialize(txid, 1, 4))
+        k = bld.key(4, 0, pub)
+        other = bld.tx_id(rng.integers(0, 256, 32, dtype=np.uint8).tobytes())
+        tid = bld.tx_id(txid)
+        bld.add_signature(k, tid, t4, sig)
+        bld.add_signature(k, other, t4, sig)
+        bld.add_signature(k, tid, t3, sig)
+        expect += [B.VALID, B.INVALID, B.INVALID]
+    with Engine(0) as eng:
+        assert list(eng.verify_tx_signatures(bld.build())) == expect
+
+
+def test_tx_signatures_8m_one_call(spool):
+    """> 8M signatures (configs[4] per-GPU shape) in ONE cg_verify_tx_signatures call from host
+    buffers: two device chunks, signature bytes copied per chunk. Idempotence vs the oracle."""
+    from corda_amd.engine import Engine
+    from tools.workload import wl
+    b, labels, schemes, ids, id_idx, ref = spool
+    n = 8_400_000
+    idx = np.random.default_rng(21).integers(0, b.n, n)
+    tb = wl.tx_sig_stream(b, schemes, idx, ids, id_idx, nthreads=16)
+    with Engine(0) as eng:
+        st = eng.verify_tx_signatures(tb)
+    assert not np.any(st == B.NOT_RUN)
+    bad = np.nonzero(st != ref[idx])[0]
+    assert bad.size == 0, f"{bad.size} of {n} verdicts differ from the oracle's verdict on the same pool item"
+    assert np.all(st[labels[idx] == 0] == B.VALID)
+
+
+def test_pool_tx_signatures(spool):
+    from corda_amd.engine import EnginePool
+    from tools.workload import wl
+    b, labels, schemes, ids, id_idx, ref = spool
+    idx = np.random.default_rng(5).integers(0, b.n, 100_000)
+    tb = wl.tx_sig_stream(b, schemes, idx, ids, id_idx, nthreads=16)
+    with EnginePool([0, 0], chunk_items=30000) as ep:
+        assert np.array_equal(ep.verify_tx_signatures(tb), ref[idx])
+        assert ep.last_stats["shards"] == 2
+        ep.inject_fault(0)
+        assert np.array_equal(ep.verify_tx_signatures(tb), ref[idx])
+        assert ep.last_stats["reruns"] == 1

@@ -31,6 +31,25 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+class signable_mode:
+    """Context manager: items generated inside get SignableData clear data, pre || id || suf
+    (pre, suf = corda_amd.signable.template(...)), `group` consecutive items sharing one 32-byte
+    id derived from id_seed; msg_len must be len(pre) + 32 + len(suf)."""
+
+    def __init__(self, pre, suf, group=4, id_seed=0):
+        self.pre, self.suf, self.group, self.id_seed = bytes(pre), bytes(suf), group, id_seed
+
+    def __enter__(self):
+        L = lib()
+        L.wl_set_signable.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint64]
+        L.wl_set_signable(self.pre, len(self.pre), self.suf, len(self.suf), self.group, self.id_seed)
+        return self
+
+    def __exit__(self, *exc):
+        lib().wl_set_signable(None, 0, None, 0, 1, 0)
+
+
 def ed25519_batch(n_items, n_keys=4096, msg_len=270, corrupt_permille=120, seed=1, bad_key_every=0, nthreads=8):
     """Config 2 shape: n_items Ed25519 items over n_keys keys, ~msg_len-byte
     messages, corrupt_permille/1000 corrupted across classes A1-A7. Returns (Batch, labels)."""
@@ -98,23 +117,40 @@ def concat(batches, shuffle_seed=None):
     return Batch(keys, items, np.concatenate(arenas + [np.zeros(64, dtype=np.uint8)])), perm
 
 
+def _signable_or_not(sig_group, scheme, seed):
+    if not sig_group:
+        import contextlib
+        return contextlib.nullcontext()
+    from corda_amd import signable
+    pre, suf = signable.template(1, scheme)
+    return signable_mode(pre, suf, sig_group, id_seed=(seed * 0x9E3779B1 + scheme) & (2 ** 64 - 1))
+
+
 def notary_pool(n_unique, ed_keys=4096, ec_keys=1024, msg_len=270, seed=9, nthreads=8,
-                mix=(0.7, 0.2, 0.1), ed_corrupt_permille=120, ec_corrupt_permille=100):
+                mix=(0.7, 0.2, 0.1), ed_corrupt_permille=120, ec_corrupt_permille=100, sig_group=0):
     """BASELINE configs[4]'s unique pool: n_unique items, 70% Ed25519 /
     20% secp256r1 / 10% secp256k1 by default, every corruption class of Appendix A, shuffled.
+    sig_group > 0: every item's clear data is SignableData(id, SignatureMetadata(1, scheme)), groups
+    of sig_group items of one scheme signing one id (msg_len is then the template's, 269 bytes).
     Returns (Batch, labels, scheme_of_item)."""
     ne = int(n_unique * mix[0])
     nr = int(n_unique * mix[1])
     nk = n_unique - ne - nr
+    if sig_group:
+        from corda_amd import signable
+        pre, suf = signable.template(1, 4)
+        msg_len = len(pre) + 32 + len(suf)
     parts, labs, sch = [], [], []
     if ne:
-        e, le = ed25519_batch(ne, n_keys=ed_keys, msg_len=msg_len, corrupt_permille=ed_corrupt_permille, seed=seed,
-                              nthreads=nthreads)
+        with _signable_or_not(sig_group, 4, seed):
+            e, le = ed25519_batch(ne, n_keys=ed_keys, msg_len=msg_len, corrupt_permille=ed_corrupt_permille, seed=seed,
+                                  nthreads=nthreads)
         parts.append(e), labs.append(le), sch.append(np.full(ne, 4, np.uint8))
     for curve, cnt, scheme in ((1, nr, 3), (0, nk, 2)):
         if cnt:
-            b, lb = ecdsa_batch(curve, cnt, n_keys=ec_keys, msg_len=msg_len, corrupt_permille=ec_corrupt_permille,
-                                seed=seed + 1 + curve, nthreads=nthreads)
+            with _signable_or_not(sig_group, scheme, seed):
+                b, lb = ecdsa_batch(curve, cnt, n_keys=ec_keys, msg_len=msg_len, corrupt_permille=ec_corrupt_permille,
+                                    seed=seed + 1 + curve, nthreads=nthreads)
             parts.append(b), labs.append(lb), sch.append(np.full(cnt, scheme, np.uint8))
     b, perm = concat(parts, shuffle_seed=seed + 7)
     return b, np.concatenate(labs)[perm], np.concatenate(sch)[perm]
@@ -141,6 +177,61 @@ def index_stream(pool, n_items, seed=10, replicate=False):
         items["msg_off"] += copy
         # keys stay in copy 0 (key table offsets unchanged)
     return Batch(pool.keys, items, arena), idx
+
+
+def pool_ids(pool, pre_len):
+    """The distinct 32-byte ids inside a signable pool's messages: (ids [m, 32], id index per item)."""
+    rows = pool.arena[pool.items["msg_off"].astype(np.int64)[:, None] + pre_len + np.arange(32)]
+    v = np.ascontiguousarray(rows).view(np.dtype((np.void, 32))).reshape(-1)
+    uniq, inv = np.unique(v, return_inverse=True)
+    return np.frombuffer(uniq.tobytes(), np.uint8).reshape(-1, 32), inv.astype(np.uint32)
+
+
+def tx_sig_stream(pool, schemes, idx, ids, id_idx, nthreads=8):
+    """The index stream `idx` over a signable pool, as cg_verify_tx_signatures input (the form a
+    JVM caller of checkSignaturesAreValid holds: tx id + TransactionSignature): a compact arena of
+    key bytes, the three SignatureMetadata(1, scheme) templates and every drawn item's own copy of
+    its signature bytes; one id table copy per pass over the pool (draw i of copy i // pool.n),
+    so no two items share bytes unless they share a transaction. Returns batch.TxSigBatch."""
+    from corda_amd import signable
+    from corda_amd.batch import KEY_DTYPE, TMPL_DTYPE, TXSIG_DTYPE, TxSigBatch
+    L = lib()
+    vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+    L.wl_gather.argtypes = [vp, vp, vp, u64, vp, vp, i32]
+    n, m = len(idx), len(ids)
+    al4 = lambda x: (x.astype(np.uint64) + np.uint64(3)) & ~np.uint64(3)  # noqa: E731
+    # keys
+    keys = pool.keys.copy()
+    klen = keys["len"].astype(np.uint16)
+    koff = np.concatenate([[0], np.cumsum(al4(klen))[:-1]]).astype(np.uint64)
+    kend = int(koff[-1] + al4(klen[-1:])[0]) if len(keys) else 0
+    # templates, one per scheme id (2, 3, 4) -> index scheme - 2
+    parts, tmpls, off = [], np.zeros(3, TMPL_DTYPE), (kend + 15) & ~15
+    for j, sch in enumerate((2, 3, 4)):
+        pre, suf = signable.template(1, sch)
+        tmpls[j] = (off, off + len(pre), len(pre), len(suf))
+        parts.append((off, pre + suf))
+        off += (len(pre) + len(suf) + 3) & ~3
+    sig_base = (off + 15) & ~15
+    it = pool.items[idx]
+    slen = it["sig_len"].astype(np.uint16)
+    soff = np.uint64(sig_base) + np.concatenate([[0], np.cumsum(al4(slen))[:-1]]).astype(np.uint64)
+    total = int(soff[-1] + al4(slen[-1:])[0]) if n else sig_base
+    arena = np.zeros(total + 64, np.uint8)
+    L.wl_gather(_p(pool.arena), _p(np.ascontiguousarray(keys["off"])), _p(klen), len(keys), _p(arena), _p(koff), nthreads)
+    keys["off"] = koff
+    for o, b in parts:
+        arena[o:o + len(b)] = np.frombuffer(b, np.uint8)
+    src = np.ascontiguousarray(it["sig_off"])
+    L.wl_gather(_p(pool.arena), _p(src), _p(slen), n, _p(arena), _p(soff), nthreads)
+    n_copies = max(1, -(-n // pool.n))
+    sigs = np.zeros(n, TXSIG_DTYPE)
+    sigs["sig_off"] = soff
+    sigs["sig_len"] = slen
+    sigs["key_idx"] = it["key_idx"]
+    sigs["tx_idx"] = id_idx[idx].astype(np.uint64) + (np.arange(n, dtype=np.uint64) // np.uint64(pool.n)) * np.uint64(m)
+    sigs["tmpl"] = schemes[idx].astype(np.uint16) - 2
+    return TxSigBatch(keys, np.tile(ids.reshape(-1), n_copies), sigs, tmpls, arena)
 
 
 class TxPipeline:

@@ -201,9 +201,43 @@ void add_L(uint8_t s[32], int k) {
   }
 }
 
+// Signable mode (wl_set_signable): item i's clear data is SignableData(id, metadata) =
+// pre || id(i / group) || suf instead of random bytes, so the same items can be handed to
+// cg_verify_tx_signatures as (id, template) pairs. A message-corruption item (A1 / E1) then signs
+// a flipped copy and keeps the true SignableData bytes (same verdict: INVALID).
+struct Signable {
+  bool on = false;
+  std::vector<uint8_t> pre, suf;
+  uint32_t group = 1;
+  uint64_t seed = 0;
+};
+Signable g_signable;
+
+void signable_msg(uint8_t* msg, uint64_t i) {
+  const Signable& S = g_signable;
+  memcpy(msg, S.pre.data(), S.pre.size());
+  uint64_t s = S.seed ^ ((i / S.group) * 0xa0761d6478bd642fULL);
+  for (int w = 0; w < 4; ++w) {
+    const uint64_t v = splitmix(s);
+    memcpy(msg + S.pre.size() + 8 * w, &v, 8);
+  }
+  memcpy(msg + S.pre.size() + 32, S.suf.data(), S.suf.size());
+}
+
 }  // namespace
 
 extern "C" {
+
+// pre == NULL: back to random messages. Otherwise the item generators write pre || id || suf
+// (msg_len must be pre_len + 32 + suf_len), `group` consecutive items sharing one id.
+void wl_set_signable(const uint8_t* pre, uint32_t pre_len, const uint8_t* suf, uint32_t suf_len, uint32_t group,
+                     uint64_t id_seed) {
+  g_signable.on = pre != nullptr;
+  g_signable.pre.assign(pre, pre ? pre + pre_len : pre);
+  g_signable.suf.assign(suf, suf ? suf + suf_len : suf);
+  g_signable.group = group ? group : 1;
+  g_signable.seed = id_seed;
+}
 
 // n_keys seeds -> public keys (32 B each). Key i's seed is derived from (seed, i).
 // `bad_every` > 0 replaces every bad_every-th key with an undecodable 32-byte string
@@ -276,9 +310,13 @@ void wl_ed25519_items(uint64_t n_items, uint32_t n_keys, const uint8_t* seeds, c
         uint8_t* p = arena + base + stride * i;
         uint8_t* sig = p;
         uint8_t* msg = p + 64;
-        for (uint32_t b = 0; b < msg_len; b += 8) {
-          uint64_t v = splitmix(s);
-          memcpy(msg + b, &v, (msg_len - b) < 8 ? (msg_len - b) : 8);
+        if (g_signable.on) {
+          signable_msg(msg, i);
+        } else {
+          for (uint32_t b = 0; b < msg_len; b += 8) {
+            uint64_t v = splitmix(s);
+            memcpy(msg + b, &v, (msg_len - b) < 8 ? (msg_len - b) : 8);
+          }
         }
         sign(sig, seeds + 32 * (size_t)k, pubs + 32 * (size_t)k, msg, msg_len);
         uint8_t label = 0;
@@ -289,7 +327,13 @@ void wl_ed25519_items(uint64_t n_items, uint32_t n_keys, const uint8_t* seeds, c
           label = (uint8_t)cls;
           const uint64_t rb = splitmix(s);
           switch (cls) {
-            case 1: msg[(rb >> 8) % msg_len] ^= (uint8_t)(1u << (rb & 7)); break;    // A1 message bit
+            case 1:                                                                  // A1 message bit
+              msg[(rb >> 8) % msg_len] ^= (uint8_t)(1u << (rb & 7));
+              if (g_signable.on) {  // sign the flipped copy, keep the true SignableData
+                sign(sig, seeds + 32 * (size_t)k, pubs + 32 * (size_t)k, msg, msg_len);
+                msg[(rb >> 8) % msg_len] ^= (uint8_t)(1u << (rb & 7));
+              }
+              break;
             case 2: sig[(rb >> 8) % 31] ^= (uint8_t)(1u << (rb & 7)); break;         // A2 R bit (not sign)
             case 3: sig[32 + (rb >> 8) % 31] ^= (uint8_t)(1u << (rb & 7)); break;    // A3 S bit (< 2^248)
             case 4: add_L(sig + 32, 1); break;                                       // A4 S + L (valid)
@@ -544,9 +588,13 @@ void wl_ecdsa_items(int curve, uint64_t n_items, uint32_t n_keys, const uint8_t*
         const uint32_t k = (uint32_t)(splitmix(s) % n_keys);
         uint8_t* p = arena + base + stride * i;
         uint8_t* msg = p + 80;
-        for (uint32_t b = 0; b < msg_len; b += 8) {
-          uint64_t v = splitmix(s);
-          memcpy(msg + b, &v, (msg_len - b) < 8 ? (msg_len - b) : 8);
+        if (g_signable.on) {
+          signable_msg(msg, i);
+        } else {
+          for (uint32_t b = 0; b < msg_len; b += 8) {
+            uint64_t v = splitmix(s);
+            memcpy(msg + b, &v, (msg_len - b) < 8 ? (msg_len - b) : 8);
+          }
         }
         int cls = 0;
         if (splitmix(s) % 1000 < corrupt_permille) {
@@ -556,9 +604,18 @@ void wl_ecdsa_items(int curve, uint64_t n_items, uint32_t n_keys, const uint8_t*
         u256w d, r, sv;
         memcpy(d.w, ds + 32 * (size_t)k, 32);
         int n;
+        // E1: the signature is over a message differing in one bit from the stored one (signable
+        // mode flips before signing and restores the true SignableData; else flips after)
+        uint64_t flip_at = 0;
+        uint8_t flip_bit = 0;
+        if (cls == 1) {
+          flip_at = splitmix(s) % msg_len;
+          flip_bit = (uint8_t)(1u << (splitmix(s) & 7));
+          if (g_signable.on) msg[flip_at] ^= flip_bit;
+        }
         if (curve == 1) n = ec_sign<CG_CURVE_R1>(p, d, msg, msg_len, s, cls, r, sv);
         else n = ec_sign<CG_CURVE_K1>(p, d, msg, msg_len, s, cls, r, sv);
-        if (cls == 1) msg[splitmix(s) % msg_len] ^= (uint8_t)(1u << (splitmix(s) & 7));
+        if (cls == 1) msg[flip_at] ^= flip_bit;
         items_out[i].sig_off = base + stride * i;
         items_out[i].msg_off = base + stride * i + 80;
         items_out[i].msg_len = msg_len;
@@ -570,6 +627,22 @@ void wl_ecdsa_items(int curve, uint64_t n_items, uint32_t n_keys, const uint8_t*
       }
     });
   }
+  for (auto& x : th) x.join();
+}
+}
+
+extern "C" {
+// dst[dst_off[i] ..) = src[src_off[i] .. + len[i]) for every i (packing a message-form batch's
+// signature / key bytes into a compact arena, bench.py)
+void wl_gather(const uint8_t* src, const uint64_t* src_off, const uint16_t* len, uint64_t n, uint8_t* dst,
+               const uint64_t* dst_off, int nthreads) {
+  if (nthreads <= 0) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t)
+    th.emplace_back([=]() {
+      const uint64_t a = n * t / nthreads, b = n * (t + 1) / nthreads;
+      for (uint64_t i = a; i < b; ++i) memcpy(dst + dst_off[i], src + src_off[i], len[i]);
+    });
   for (auto& x : th) x.join();
 }
 }

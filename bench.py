@@ -104,6 +104,9 @@ def parse():
     ap.add_argument("--sigs-per-tx", type=int, default=5,
                     help="signatures per transaction id (GeneratedLedger: 1+Poisson(3) signers + the notary)")
     ap.add_argument("--device-steps", type=int, default=4, help="device-resident secondary calls (0: off)")
+    ap.add_argument("--key-dists", default="distinct,zipf",
+                    help="key-distribution secondaries on the headline shape ('' : off): distinct = every pool item "
+                         "its own key (2^20 keys, ~12 uses each), zipf = Zipf(1.1) over 2^20 keys")
     ap.add_argument("--host-steps", type=int, default=3, help="message-form cg_verify_batch calls (0: off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
@@ -546,6 +549,53 @@ def bench_device(eng, dev, stream, b, tb, st_ref, steps):
     return out
 
 
+def table_modes(b, schemes):
+    """Items per key-table mode (keyws.h thresholds on the exact use counts): row 0 (< 32 uses),
+    full (32 .. wide threshold), wide (>= 1536 Ed25519 / 512 ECDSA uses, up to the pool cap)."""
+    uses = np.bincount(b.items["key_idx"], minlength=len(b.keys))
+    thr = np.array([KEY_WIDE_MIN_USES.get(int(s), 1 << 30) for s in b.keys["scheme"]])
+    ku = uses[b.items["key_idx"]]
+    kt = thr[b.items["key_idx"]]
+    out = {}
+    for name, sel in (("ed25519", schemes == 4), ("secp256r1", schemes == 3), ("secp256k1", schemes == 2)):
+        out[name] = {"row0": int((sel & (ku < KEY_FULL_MIN_USES)).sum()),
+                     "full": int((sel & (ku >= KEY_FULL_MIN_USES) & (ku < kt)).sum()),
+                     "wide": int((sel & (ku >= kt)).sum())}
+    out["keys_used"] = int((uses > 0).sum())
+    out["max_uses"] = int(uses.max()) if uses.size else 0
+    return out
+
+
+def bench_key_dist(a, eng, dist, rank, threads, steps):
+    """The headline call (cg_verify_tx_signatures, host arena -> host verdicts) on the headline
+    shape with another key distribution: 'distinct' (every pool item its own key: 2^20 keys, each
+    drawn ~12 times by the 12.5M-item stream) or 'zipf' (Zipf(1.1) over 2^20 keys: a few hot keys,
+    a long tail). GeneratedLedger.kt:48-54 draws the signers per command."""
+    from corda_amd import signable
+    from tools.workload import wl
+    t0 = time.time()
+    pool, pl, ps = wl.notary_pool(a.pool, seed=a.seed + 7919 * rank + 17, nthreads=threads, sig_group=a.sigs_per_tx,
+                                  key_dist=dist)
+    ids, id_idx = wl.pool_ids(pool, len(signable.template(1, 4)[0]))
+    idx = np.random.default_rng(a.seed + 5).integers(0, pool.n, a.items)
+    tb = wl.tx_sig_stream(pool, ps, idx, ids, id_idx, nthreads=threads)
+    gen = time.time() - t0
+    from corda_amd.batch import Batch
+    modes = table_modes(Batch(pool.keys, pool.items[idx], pool.arena), ps[idx])
+    eng.verify_tx_signatures(tb)
+    eng.stage_times()
+    t = time.perf_counter()
+    for _ in range(steps):
+        st = eng.verify_tx_signatures(tb)
+    el = (time.perf_counter() - t) / steps
+    stg = eng.stage_times()
+    ver = check_verdicts(st, expected_verdicts(pl[idx], ps[idx]))
+    return {"value": round(tb.n / el, 1), "unit": "sigs/s", "ms_per_call": round(el * 1e3, 3), "keys": len(pool.keys),
+            "table_modes_items": modes, "stages": stage_summary(stg, steps), "verdicts": ver,
+            "cg_stats_ms": {k: round(v, 3) for k, v in eng.last_stats.items() if k.startswith("ms_")},
+            "gen_s": round(gen, 1)}
+
+
 def bench_host(eng, b, st_dev, steps):
     """PCIe-inclusive message form: host arena -> host verdicts through cg_verify_batch on the
     headline shard with every SignableData materialised: keys, items and ~370 B per item copied,
@@ -660,6 +710,7 @@ def main():
         extra["device_resident"] = bench_device(eng, dev, stream, batch, tb, st, a.device_steps)
     if rank == 0 and world == 1 and a.host_steps > 0:
         extra["host_message_form"] = bench_host(eng, batch, st, a.host_steps)
+    extra["table_modes_items"] = table_modes(batch, schemes)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(batch, st, a.cpu_seconds, threads)
@@ -667,6 +718,12 @@ def main():
             cpu["configs0"] = configs0(a, eng, wl, threads)
     torch.cuda.empty_cache()
     if world == 1:
+        for dist in [d for d in a.key_dists.split(",") if d]:
+            try:
+                extra["key_dist_" + dist] = bench_key_dist(a, eng, dist, rank, threads, 2)
+            except Exception as e:  # a failed secondary must not void the headline line
+                extra["key_dist_" + dist] = {"error": f"{type(e).__name__}: {e}"}
+            torch.cuda.empty_cache()
         for name, on, fn in (("configs1_ed25519", a.configs1_items, lambda: bench_configs1(a, eng, dev, stream, wl, threads)),
                              ("configs2_ecdsa", a.ecdsa_items, lambda: bench_ecdsa(a, eng, dev, stream, wl, threads)),
                              ("configs3_tx_pipeline", a.pipeline_txs,

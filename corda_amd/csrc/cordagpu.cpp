@@ -753,8 +753,9 @@ static int verify_transactions_locked(cg_ctx* c, const cg_tx* d_txs, uint64_t n_
   }
   uint64_t slot = (maxlen + 15) & ~(uint64_t)15;
   if (slot == 0) slot = 16;
+  const uint64_t msgs_len = cg::tx_msgs_head(n_tmpls) + slot * n_sigs;
   const size_t need_leaf = cg::tx_ws_bytes(n_comps), need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1),
-               need_msgs = slot * (n_sigs ? n_sigs : 1), need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
+               need_msgs = msgs_len ? msgs_len : 16, need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
   if (c->aux2.cap < need_leaf || c->txitems.cap < need_items || c->msgs.cap < need_msgs ||
       c->tmpls.cap < need_tmpl) {
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
@@ -775,7 +776,7 @@ static int verify_transactions_locked(cg_ctx* c, const cg_tx* d_txs, uint64_t n_
                                     d_ids, d_arena, arena_len, slot, (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s),
             "launch_tx_sig_items");
     HIP_TRY(launch_chunked(c, d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode,
-                           d_sig_status, s, (const uint8_t*)c->msgs.p, slot * n_sigs),
+                           d_sig_status, s, (const uint8_t*)c->msgs.p, msgs_len),
             "launch_verify");
   }
   HIP_TRY(order_out(c, s), "hipEventRecord");
@@ -863,7 +864,8 @@ static uint64_t tmpl_slot(const cg_signable_tmpl* tmpls, uint32_t n_tmpls) {
 // Verify items, spliced messages and the template table of n_sigs signatures (waits for the device
 // when a buffer grows).
 static hipError_t ensure_txsig_ws(cg_ctx* c, uint64_t n_sigs, uint32_t n_tmpls, uint64_t slot) {
-  const size_t need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1), need_msgs = slot * (n_sigs ? n_sigs : 1),
+  const size_t need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1),
+               need_msgs = cg::tx_msgs_head(n_tmpls) + slot * (n_sigs ? n_sigs : 1),
                need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
   if (c->txitems.cap >= need_items && c->msgs.cap >= need_msgs && c->tmpls.cap >= need_tmpl) return hipSuccess;
   hipError_t e = hipDeviceSynchronize();
@@ -889,7 +891,7 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
                                 d_arena, arena_len, slot, (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s);
   if (e == hipSuccess)
     e = launch_chunked(c, d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode, d_status, s,
-                       (const uint8_t*)c->msgs.p, slot * n_sigs, before_front);
+                       (const uint8_t*)c->msgs.p, cg::tx_msgs_head(n_tmpls) + slot * n_sigs, before_front);
   return e;
 }
 

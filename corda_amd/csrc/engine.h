@@ -162,8 +162,10 @@ hipError_t launch_tx_ids(const cg_tx* d_txs, uint64_t n_tx, const cg_component* 
                          const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids, uint8_t* d_status,
                          uint8_t* d_leaf_ws, hipStream_t stream);
 
-// Transaction pipeline: per-signature verify items + spliced SignableData messages (one
-// `slot`-byte message slot per signature in d_msgs; slot a multiple of 16).
+// Transaction pipeline: per-signature verify items + spliced SignableData messages: d_msgs holds
+// the templates' SHA-256 midstate records (tx_msgs_head(n_tmpls) bytes), then one `slot`-byte
+// message slot per signature (slot a multiple of 16).
+uint64_t tx_msgs_head(uint32_t n_tmpls);
 hipError_t launch_tx_sig_items(const cg_txsig* d_sigs, uint64_t n_sigs, const cg_signable_tmpl* d_tmpls,
                                uint32_t n_tmpls, const uint8_t* d_tx_status, uint64_t n_tx, const uint8_t* d_ids,
                                const uint8_t* d_arena, uint64_t arena_len, uint64_t slot, cg_item* d_items,

@@ -60,6 +60,21 @@ __device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t ar
 // in the engine's spliced-message workspace, not in the caller's arena. Launches without that
 // workspace (every caller-facing entry point) pass msgs = nullptr, and the flag is ignored.
 #define CG_ITEM_MSG_WS 1u
+// With CG_ITEM_MSG_WS: the message is a SignableData splice of template reserved1, whose SHA-256
+// midstate record (the template prefix's full 64-byte blocks) heads the message workspace.
+#define CG_ITEM_TMPL 2u
+struct TmplMid {
+  uint32_t state[8];
+  uint32_t blocks;  // prefix blocks absorbed into state
+  uint32_t pad[3];
+};
+static_assert(sizeof(TmplMid) == 48, "template midstate record");
+static inline uint64_t tmpl_mid_bytes(uint32_t n_tmpls) { return ((uint64_t)n_tmpls * sizeof(TmplMid) + 255) & ~(uint64_t)255; }
+__device__ __forceinline__ const TmplMid* item_tmpl_mid(const cg_item& it, const uint8_t* msgs) {
+  return (it.reserved0 & CG_ITEM_TMPL) && (it.reserved0 & CG_ITEM_MSG_WS) && msgs
+             ? (const TmplMid*)msgs + it.reserved1
+             : nullptr;
+}
 __device__ __forceinline__ bool item_in_ws(const cg_item& it, const uint8_t* msgs) {
   return (it.reserved0 & CG_ITEM_MSG_WS) && msgs != nullptr;
 }

@@ -397,10 +397,19 @@ CG_HD void sha256_compress(uint32_t s[8], uint32_t w[16]) {
 // SHA-256 of arena[off, off+len) || suffix (0 or 32 bytes given as 8 big-endian words;
 // used for serialised-component || nonce, MerkleTransaction.kt:23). Output: the state as
 // 8 big-endian words (the digest).
+// mid (optional): the state after the message's first `mid_blocks` 64-byte blocks (a SignableData
+// template's constant prefix, cg_verify_tx_signatures); hashing resumes at that block.
 CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t len_rounded, uint64_t off,
-                               uint64_t len, const uint32_t* suffix_be /* 8 words or null */) {
+                               uint64_t len, const uint32_t* suffix_be /* 8 words or null */,
+                               const uint32_t* mid = nullptr, uint32_t mid_blocks = 0) {
   uint32_t s[8];
-  sha256_init(s);
+  if (mid) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = mid[k];
+  } else {
+    sha256_init(s);
+    mid_blocks = 0;
+  }
   const uint64_t sfx = suffix_be ? 32 : 0;
   const uint64_t n = len + sfx;
   const uint64_t nblocks = (n + 9 + 63) >> 6;
@@ -408,7 +417,7 @@ CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t l
   const uint64_t nfull = len >> 6;
   const uint64_t base = off & ~(uint64_t)3;
   const uint32_t sh8 = (uint32_t)(off & 3) * 8u;
-  for (uint64_t blk = 0; blk < nfull; ++blk) {
+  for (uint64_t blk = mid_blocks; blk < nfull; ++blk) {
     uint32_t W[20], w[16];  // aligned dwords of the block (+1 for the realignment), 16-byte loads
 #pragma unroll
     for (int t = 0; t < 5; ++t) cg_ld_dwords4(&W[4 * t], arena, len_rounded, base + blk * 64 + 16 * t);
@@ -422,7 +431,7 @@ CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t l
     }
     sha256_compress(s, w);
   }
-  for (uint64_t blk = nfull; blk < nblocks; ++blk) {
+  for (uint64_t blk = nfull > mid_blocks ? nfull : mid_blocks; blk < nblocks; ++blk) {
     uint32_t w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {

@@ -13,6 +13,7 @@
 
 #include "engine.h"
 #include "keyws.h"
+#include "sha2.h"
 
 namespace cg {
 
@@ -23,7 +24,7 @@ __device__ __forceinline__ bool tmpl_ok(const cg_signable_tmpl& t, uint64_t aren
 __global__ void __launch_bounds__(256) k_txsig_items(const cg_txsig* __restrict__ sigs, uint64_t n_sigs,
                                                      const cg_signable_tmpl* __restrict__ tmpls, uint32_t n_tmpls,
                                                      const uint8_t* __restrict__ tx_status, uint64_t n_tx,
-                                                     uint64_t arena_len, uint64_t slot,
+                                                     uint64_t arena_len, uint64_t head, uint64_t slot,
                                                      cg_item* __restrict__ items) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_sigs) return;
@@ -40,10 +41,11 @@ __global__ void __launch_bounds__(256) k_txsig_items(const cg_txsig* __restrict_
     ok = tmpl_ok(t, arena_len);
   }
   if (ok) {
-    it.msg_off = j * slot;
+    it.msg_off = head + j * slot;
     it.msg_len = t.prefix_len + 32u + t.suffix_len;
     it.key_idx = s.key_idx;
-    it.reserved0 = CG_ITEM_MSG_WS;
+    it.reserved0 = CG_ITEM_MSG_WS | CG_ITEM_TMPL;
+    it.reserved1 = s.tmpl;
   } else {
     it.msg_off = 0;
     it.msg_len = 0;
@@ -53,11 +55,40 @@ __global__ void __launch_bounds__(256) k_txsig_items(const cg_txsig* __restrict_
   items[j] = it;
 }
 
+// One lane per template: the SHA-256 state after the prefix's full 64-byte blocks (ECDSA's
+// e = SHA-256(SignableData) resumes from it: 3 of the 5 compressions of a 269-byte message).
+__global__ void __launch_bounds__(64) k_tmpl_mid(const cg_signable_tmpl* __restrict__ tmpls, uint32_t n_tmpls,
+                                                 const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                 TmplMid* __restrict__ out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tmpls) return;
+  const cg_signable_tmpl tm = tmpls[t];
+  TmplMid r;
+  sha256_init(r.state);
+  r.blocks = 0;
+  r.pad[0] = r.pad[1] = r.pad[2] = 0;
+  if (tmpl_ok(tm, arena_len)) {
+    const uint64_t lr = round4(arena_len);
+    for (uint32_t b = 0; b < tm.prefix_len / 64; ++b) {
+      uint32_t w[16];
+      for (int j = 0; j < 16; ++j) {
+        uint32_t v = 0;
+        for (int q = 0; q < 4; ++q) v = (v << 8) | (cg_ld_bytes4(arena, lr, tm.prefix_off + 64u * b + 4u * j + q) & 0xffu);
+        w[j] = v;
+      }
+      sha256_compress(r.state, w);
+      r.blocks = b + 1;
+    }
+  }
+  out[t] = r;
+}
+
 __global__ void __launch_bounds__(256) k_splice(const cg_txsig* __restrict__ sigs, uint64_t n_sigs,
                                                 const cg_signable_tmpl* __restrict__ tmpls, uint32_t n_tmpls,
                                                 const uint8_t* __restrict__ tx_status, uint64_t n_tx,
                                                 const uint8_t* __restrict__ ids, const uint8_t* __restrict__ arena,
-                                                uint64_t arena_len, uint64_t slot, uint8_t* __restrict__ msgs) {
+                                                uint64_t arena_len, uint64_t head, uint64_t slot,
+                                                uint8_t* __restrict__ msgs) {
   const uint64_t wpr = slot >> 2;
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t j = g / wpr, w = g % wpr;
@@ -79,8 +110,10 @@ __global__ void __launch_bounds__(256) k_splice(const cg_txsig* __restrict__ sig
       }
     }
   }
-  ((uint32_t*)msgs)[g] = v;
+  ((uint32_t*)(msgs + head))[g] = v;
 }
+
+uint64_t tx_msgs_head(uint32_t n_tmpls) { return tmpl_mid_bytes(n_tmpls); }
 
 hipError_t launch_tx_sig_items(const cg_txsig* d_sigs, uint64_t n_sigs, const cg_signable_tmpl* d_tmpls,
                                uint32_t n_tmpls, const uint8_t* d_tx_status, uint64_t n_tx, const uint8_t* d_ids,
@@ -88,11 +121,15 @@ hipError_t launch_tx_sig_items(const cg_txsig* d_sigs, uint64_t n_sigs, const cg
                                uint8_t* d_msgs, hipStream_t stream) {
   if (n_sigs == 0) return hipSuccess;
   const uint32_t B = 256;
+  const uint64_t head = tmpl_mid_bytes(n_tmpls);
+  if (n_tmpls)
+    hipLaunchKernelGGL(k_tmpl_mid, dim3((n_tmpls + 63) / 64), dim3(64), 0, stream, d_tmpls, n_tmpls, d_arena,
+                       arena_len, (TmplMid*)d_msgs);
   hipLaunchKernelGGL(k_txsig_items, dim3((unsigned)((n_sigs + B - 1) / B)), dim3(B), 0, stream, d_sigs, n_sigs,
-                     d_tmpls, n_tmpls, d_tx_status, n_tx, arena_len, slot, d_items);
+                     d_tmpls, n_tmpls, d_tx_status, n_tx, arena_len, head, slot, d_items);
   const uint64_t words = n_sigs * (slot >> 2);
   hipLaunchKernelGGL(k_splice, dim3((unsigned)((words + B - 1) / B)), dim3(B), 0, stream, d_sigs, n_sigs, d_tmpls,
-                     n_tmpls, d_tx_status, n_tx, d_ids, d_arena, arena_len, slot, d_msgs);
+                     n_tmpls, d_tx_status, n_tx, d_ids, d_arena, arena_len, head, slot, d_msgs);
   return hipGetLastError();
 }
 

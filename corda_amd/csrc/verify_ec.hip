@@ -227,9 +227,10 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
     st = CG_NOT_RUN;
   } else {
     EcItemWs w;
+    const TmplMid* mid = item_tmpl_mid(it, msgs);
     const uint32_t r = ecdsa_prep<C>(w, arena, round4(arena_len), it.sig_off, it.sig_len,
                                      item_msg_arena(it, arena, msgs), round4(item_msg_len(it, arena_len, msgs_len, msgs)),
-                                     it.msg_off, it.msg_len);
+                                     it.msg_off, it.msg_len, mid ? mid->state : nullptr, mid ? mid->blocks : 0u);
     if (r == 0) {
       ws[p] = w;
       st = (uint8_t)(EC_PENDING_BASE + C);

@@ -1,0 +1,97 @@
+/* cordagpu_jni.c -- JNI shim between net.corda.core.crypto.CryptoBatch (jvm/src/main/kotlin) and
+ * libcordagpu.so (include/cordagpu.h). Plain C, direct ByteBuffers only: the JVM hands over the
+ * addresses of its off-heap buffers, the engine copies what it needs and keeps no pointer after a
+ * call returns.
+ *
+ * Build (on a node with a JDK; this repository's image has none, so it is not compiled here):
+ *   gcc -O2 -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude \
+ *       jvm/jni/cordagpu_jni.c -Lcorda_amd -lcordagpu -o libcordagpu_jni.so
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "cordagpu.h"
+
+#define ADDR(b) ((*env)->GetDirectBufferAddress(env, (b)))
+
+static void throw_state(JNIEnv* env, const char* fn, int rc) {
+  char msg[768];
+  const char* why = cg_last_error();
+  snprintf(msg, sizeof msg, "%s failed (%d): %s", fn, rc, why ? why : "");
+  jclass ex = (*env)->FindClass(env, "java/lang/IllegalStateException");
+  if (ex) (*env)->ThrowNew(env, ex, msg);
+}
+
+JNIEXPORT jlong JNICALL Java_net_corda_core_crypto_CryptoBatch_nativeOpen(JNIEnv* env, jobject self, jint dev) {
+  cg_config cfg = {0}; /* ABI v2: chunk_items 0 = CG_DEFAULT_CHUNK_ITEMS, reserved must be 0 */
+  cfg.device = dev;
+  cg_ctx* ctx = 0;
+  int rc = cg_open(&ctx, &cfg);
+  if (rc != CG_OK) {
+    throw_state(env, "cg_open", rc);
+    return 0;
+  }
+  return (jlong)(intptr_t)ctx;
+}
+
+JNIEXPORT void JNICALL Java_net_corda_core_crypto_CryptoBatch_nativeClose(JNIEnv* env, jobject self, jlong ctx) {
+  cg_close((cg_ctx*)(intptr_t)ctx);
+}
+
+/* One JVM process, every GPU of the node: a pool over the device list. */
+JNIEXPORT jlong JNICALL Java_net_corda_core_crypto_CryptoBatch_nativeOpenPool(JNIEnv* env, jobject self,
+                                                                             jintArray devs) {
+  jsize n = (*env)->GetArrayLength(env, devs);
+  jint* d = (*env)->GetIntArrayElements(env, devs, 0);
+  cg_config cfg = {0};
+  cg_pool* pool = 0;
+  int rc = cg_pool_open(&pool, (const int32_t*)d, (uint32_t)n, &cfg);
+  (*env)->ReleaseIntArrayElements(env, devs, d, JNI_ABORT);
+  if (rc != CG_OK) {
+    throw_state(env, "cg_pool_open", rc);
+    return 0;
+  }
+  return (jlong)(intptr_t)pool;
+}
+
+/* Crypto.doVerify / isValid over (key, sig, clear) items: cg_verify_batch. */
+JNIEXPORT jint JNICALL Java_net_corda_core_crypto_CryptoBatch_nativeVerify(
+    JNIEnv* env, jobject self, jlong ctx, jobject keys, jint n_keys, jobject items, jlong n_items,
+    jobject arena, jlong arena_len, jint mode, jobject status) {
+  return cg_verify_batch((cg_ctx*)(intptr_t)ctx, (const cg_key*)ADDR(keys), (uint32_t)n_keys,
+                         (const cg_item*)ADDR(items), (uint64_t)n_items, (const uint8_t*)ADDR(arena),
+                         (uint64_t)arena_len, (uint32_t)mode, (uint8_t*)ADDR(status), 0);
+}
+
+/* Crypto.doVerify(txId, TransactionSignature) over many transactions: cg_verify_tx_signatures
+ * (pool != 0: cg_pool_verify_tx_signatures over every device of the pool). */
+JNIEXPORT jint JNICALL Java_net_corda_core_crypto_CryptoBatch_nativeVerifyTxSignatures(
+    JNIEnv* env, jobject self, jlong ctx, jlong pool, jobject keys, jint n_keys, jobject ids, jlong n_ids,
+    jobject sigs, jlong n_sigs, jobject tmpls, jint n_tmpls, jobject arena, jlong arena_len, jint mode,
+    jobject status) {
+  if (pool)
+    return cg_pool_verify_tx_signatures((cg_pool*)(intptr_t)pool, (const cg_key*)ADDR(keys), (uint32_t)n_keys,
+                                        (const uint8_t*)ADDR(ids), (uint64_t)n_ids, (const cg_txsig*)ADDR(sigs),
+                                        (uint64_t)n_sigs, (const cg_signable_tmpl*)ADDR(tmpls), (uint32_t)n_tmpls,
+                                        (const uint8_t*)ADDR(arena), (uint64_t)arena_len, (uint32_t)mode,
+                                        (uint8_t*)ADDR(status), 0);
+  return cg_verify_tx_signatures((cg_ctx*)(intptr_t)ctx, (const cg_key*)ADDR(keys), (uint32_t)n_keys,
+                                 (const uint8_t*)ADDR(ids), (uint64_t)n_ids, (const cg_txsig*)ADDR(sigs),
+                                 (uint64_t)n_sigs, (const cg_signable_tmpl*)ADDR(tmpls), (uint32_t)n_tmpls,
+                                 (const uint8_t*)ADDR(arena), (uint64_t)arena_len, (uint32_t)mode,
+                                 (uint8_t*)ADDR(status), 0);
+}
+
+/* WireTransaction ids + every signature (cg_verify_transactions). */
+JNIEXPORT jint JNICALL Java_net_corda_core_crypto_CryptoBatch_nativeVerifyTransactions(
+    JNIEnv* env, jobject self, jlong ctx, jobject txs, jlong n_tx, jobject comps, jlong n_comps, jobject keys,
+    jint n_keys, jobject sigs, jlong n_sigs, jobject tmpls, jint n_tmpls, jobject arena, jlong arena_len, jint mode,
+    jobject ids_out, jobject tx_status_out, jobject sig_status_out) {
+  return cg_verify_transactions((cg_ctx*)(intptr_t)ctx, (const cg_tx*)ADDR(txs), (uint64_t)n_tx,
+                                (const cg_component*)ADDR(comps), (uint64_t)n_comps, (const cg_key*)ADDR(keys),
+                                (uint32_t)n_keys, (const cg_txsig*)ADDR(sigs), (uint64_t)n_sigs,
+                                (const cg_signable_tmpl*)ADDR(tmpls), (uint32_t)n_tmpls, (const uint8_t*)ADDR(arena),
+                                (uint64_t)arena_len, (uint32_t)mode, (uint8_t*)ADDR(ids_out),
+                                (uint8_t*)ADDR(tx_status_out), (uint8_t*)ADDR(sig_status_out));
+}

@@ -145,3 +145,47 @@ def test_pool_tx_signatures(spool):
         ep.inject_fault(0)
         assert np.array_equal(ep.verify_tx_signatures(tb), ref[idx])
         assert ep.last_stats["reruns"] == 1
+
+
+def test_tx_signatures_ecdsa_template_lengths():
+    """ECDSA through the splice with SHA-256 resuming from the template prefix's midstate, for
+    prefixes of 0, 63, 64, 127, 128, 200 and 234 bytes (0, 0, 1, 1, 2, 3, 3 absorbed blocks) and
+    suffixes of 0-9 bytes: verdicts equal the oracle's on the materialised bytes and the labels."""
+    from corda_amd.batch import TMPL_DTYPE, TXSIG_DTYPE
+    from corda_amd.engine import Engine
+    from tools.workload import wl
+    rng = np.random.default_rng(31)
+    parts, tm = [], []
+    lens = [(0, 5), (63, 9), (64, 0), (127, 3), (128, 1), (200, 7), (234, 3)]
+    for j, (pl, sl) in enumerate(lens):
+        pre = rng.integers(0, 256, pl, dtype=np.uint8).tobytes()
+        suf = rng.integers(0, 256, sl, dtype=np.uint8).tobytes()
+        with wl.signable_mode(pre, suf, group=3, id_seed=j + 1):
+            b, lab = wl.ecdsa_batch(j & 1, 400, n_keys=20, msg_len=pl + 32 + sl, corrupt_permille=150, seed=40 + j,
+                                    nthreads=8)
+        parts.append((b, lab, pre, suf))
+    big, _ = wl.concat([p[0] for p in parts])
+    labels = np.concatenate([p[1] for p in parts])
+    # template bytes behind the arena; ids = the 32 bytes after each message's prefix
+    arena = [big.arena]
+    off = big.arena.size
+    tmpls = np.zeros(len(parts), TMPL_DTYPE)
+    for j, (_, _, pre, suf) in enumerate(parts):
+        tmpls[j] = (off, off + len(pre), len(pre), len(suf))
+        arena.append(np.frombuffer(pre + suf, np.uint8))
+        off += len(pre) + len(suf)
+    arena = np.concatenate(arena + [np.zeros(64, np.uint8)])
+    tm = np.repeat(np.arange(len(parts)), [p[0].n for p in parts])
+    pl = np.array([len(parts[t][2]) for t in tm])
+    rows = arena[big.items["msg_off"].astype(np.int64)[:, None] + pl[:, None] + np.arange(32)]
+    sigs = np.zeros(big.n, TXSIG_DTYPE)
+    sigs["sig_off"], sigs["sig_len"], sigs["key_idx"] = big.items["sig_off"], big.items["sig_len"], big.items["key_idx"]
+    sigs["tx_idx"] = np.arange(big.n)
+    sigs["tmpl"] = tm
+    tb = B.TxSigBatch(big.keys, rows.reshape(-1), sigs, tmpls, arena)
+    ref = c_oracle.verify_batch(txsig_util.to_message_batch(tb), B.MODE_DOVERIFY, 8)
+    assert np.array_equal(ref, c_oracle.verify_batch(big, B.MODE_DOVERIFY, 8))
+    assert np.all(ref[labels == 0] == B.VALID) and np.all(ref[labels == 1] == B.INVALID)
+    with Engine(0) as eng:
+        st = eng.verify_tx_signatures(tb)
+    assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} differ"

@@ -117,6 +117,38 @@ def concat(batches, shuffle_seed=None):
     return Batch(keys, items, np.concatenate(arenas + [np.zeros(64, dtype=np.uint8)])), perm
 
 
+class key_choice:
+    """Context manager: items generated inside sign with key k[i] instead of a uniform draw."""
+
+    def __init__(self, k):
+        self.k = None if k is None else np.ascontiguousarray(k, dtype=np.uint32)
+
+    def __enter__(self):
+        L = lib()
+        L.wl_set_key_choice.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        if self.k is not None:
+            L.wl_set_key_choice(_p(self.k), self.k.size)
+        return self
+
+    def __exit__(self, *exc):
+        lib().wl_set_key_choice(None, 0)
+
+
+def _key_draw(dist, n_items, n_keys, seed):
+    """Key index per item: 'uniform' (None: the generator's own draw), 'distinct' (item i -> key i),
+    'zipf' (Zipf(s = 1.1) over n_keys, rank 0 the hottest)."""
+    if dist == "uniform":
+        return None
+    if dist == "distinct":
+        return np.arange(n_items, dtype=np.uint32) % n_keys
+    if dist == "zipf":
+        w = 1.0 / np.arange(1, n_keys + 1, dtype=np.float64) ** 1.1
+        c = np.cumsum(w)
+        u = np.random.default_rng(seed).random(n_items) * c[-1]
+        return np.minimum(np.searchsorted(c, u), n_keys - 1).astype(np.uint32)
+    raise ValueError(dist)
+
+
 def _signable_or_not(sig_group, scheme, seed):
     if not sig_group:
         import contextlib
@@ -127,11 +159,14 @@ def _signable_or_not(sig_group, scheme, seed):
 
 
 def notary_pool(n_unique, ed_keys=4096, ec_keys=1024, msg_len=270, seed=9, nthreads=8,
-                mix=(0.7, 0.2, 0.1), ed_corrupt_permille=120, ec_corrupt_permille=100, sig_group=0):
+                mix=(0.7, 0.2, 0.1), ed_corrupt_permille=120, ec_corrupt_permille=100, sig_group=0,
+                key_dist="uniform"):
     """BASELINE configs[4]'s unique pool: n_unique items, 70% Ed25519 /
     20% secp256r1 / 10% secp256k1 by default, every corruption class of Appendix A, shuffled.
     sig_group > 0: every item's clear data is SignableData(id, SignatureMetadata(1, scheme)), groups
     of sig_group items of one scheme signing one id (msg_len is then the template's, 269 bytes).
+    key_dist: 'uniform' (ed_keys / ec_keys keys drawn uniformly), 'distinct' (ed_keys / ec_keys are
+    ignored: every item its own key) or 'zipf' (Zipf(1.1) over as many keys as the part has items).
     Returns (Batch, labels, scheme_of_item)."""
     ne = int(n_unique * mix[0])
     nr = int(n_unique * mix[1])
@@ -141,15 +176,18 @@ def notary_pool(n_unique, ed_keys=4096, ec_keys=1024, msg_len=270, seed=9, nthre
         pre, suf = signable.template(1, 4)
         msg_len = len(pre) + 32 + len(suf)
     parts, labs, sch = [], [], []
+    if key_dist != "uniform":
+        ed_keys, ec_keys = max(1, ne), max(1, nr, nk)
     if ne:
-        with _signable_or_not(sig_group, 4, seed):
+        with _signable_or_not(sig_group, 4, seed), key_choice(_key_draw(key_dist, ne, ed_keys, seed + 11)):
             e, le = ed25519_batch(ne, n_keys=ed_keys, msg_len=msg_len, corrupt_permille=ed_corrupt_permille, seed=seed,
                                   nthreads=nthreads)
         parts.append(e), labs.append(le), sch.append(np.full(ne, 4, np.uint8))
     for curve, cnt, scheme in ((1, nr, 3), (0, nk, 2)):
         if cnt:
-            with _signable_or_not(sig_group, scheme, seed):
-                b, lb = ecdsa_batch(curve, cnt, n_keys=ec_keys, msg_len=msg_len, corrupt_permille=ec_corrupt_permille,
+            nkc = cnt if key_dist != "uniform" else ec_keys
+            with _signable_or_not(sig_group, scheme, seed), key_choice(_key_draw(key_dist, cnt, nkc, seed + 13 + curve)):
+                b, lb = ecdsa_batch(curve, cnt, n_keys=nkc, msg_len=msg_len, corrupt_permille=ec_corrupt_permille,
                                     seed=seed + 1 + curve, nthreads=nthreads)
             parts.append(b), labs.append(lb), sch.append(np.full(cnt, scheme, np.uint8))
     b, perm = concat(parts, shuffle_seed=seed + 7)

@@ -212,6 +212,9 @@ struct Signable {
   uint64_t seed = 0;
 };
 Signable g_signable;
+// wl_set_key_choice: item i of the next generator call signs with key g_key_choice[i] (key-
+// distribution workloads: every item its own key, Zipf draws) instead of a uniform draw.
+std::vector<uint32_t> g_key_choice;
 
 void signable_msg(uint8_t* msg, uint64_t i) {
   const Signable& S = g_signable;
@@ -238,6 +241,9 @@ void wl_set_signable(const uint8_t* pre, uint32_t pre_len, const uint8_t* suf, u
   g_signable.group = group ? group : 1;
   g_signable.seed = id_seed;
 }
+
+// k == NULL: uniform key draws again. Otherwise item i uses key k[i] (k[i] < n_keys of the call).
+void wl_set_key_choice(const uint32_t* k, uint64_t n) { g_key_choice.assign(k, k ? k + n : k); }
 
 // n_keys seeds -> public keys (32 B each). Key i's seed is derived from (seed, i).
 // `bad_every` > 0 replaces every bad_every-th key with an undecodable 32-byte string
@@ -306,7 +312,8 @@ void wl_ed25519_items(uint64_t n_items, uint32_t n_keys, const uint8_t* seeds, c
     th.emplace_back([=]() {
       for (uint64_t i = (uint64_t)t; i < n_items; i += (uint64_t)nthreads) {
         uint64_t s = seed ^ (i * 0x9e3779b97f4a7c15ULL);
-        const uint32_t k = (uint32_t)(splitmix(s) % n_keys);
+        uint32_t k = (uint32_t)(splitmix(s) % n_keys);
+        if (i < g_key_choice.size()) k = g_key_choice[i] % n_keys;
         uint8_t* p = arena + base + stride * i;
         uint8_t* sig = p;
         uint8_t* msg = p + 64;
@@ -585,7 +592,8 @@ void wl_ecdsa_items(int curve, uint64_t n_items, uint32_t n_keys, const uint8_t*
     th.emplace_back([=]() {
       for (uint64_t i = (uint64_t)t; i < n_items; i += (uint64_t)nthreads) {
         uint64_t s = seed ^ (i * 0xd6e8feb86659fd93ULL);
-        const uint32_t k = (uint32_t)(splitmix(s) % n_keys);
+        uint32_t k = (uint32_t)(splitmix(s) % n_keys);
+        if (i < g_key_choice.size()) k = g_key_choice[i] % n_keys;
         uint8_t* p = arena + base + stride * i;
         uint8_t* msg = p + 80;
         if (g_signable.on) {

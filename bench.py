@@ -2,16 +2,19 @@
 """Headline benchmark: verified signatures / second for the whole node (BASELINE.json metric).
 
 Workload (BASELINE configs[4], SURVEY.md §8(d) config 5, one GPU's shard): the notary-style
-mixed batch, 70% Ed25519 / 20% ECDSA secp256r1 / 10% ECDSA secp256k1, 12.5M items per GPU
+mixed batch, 70% Ed25519 / 20% ECDSA secp256r1 / 10% ECDSA secp256k1, 12.5M signatures per GPU
 (100M over 8 GPUs), drawn by a seeded index stream from a 2^20-item unique pool with every
-Appendix A corruption class (~11% corrupted), 270-byte SignableData-sized messages, 4096 Ed25519
-keys and 1024 keys per curve. The arena holds one physical copy of the pool per 2^20 draws, so
-every item has its own bytes (4.7 GB per GPU). Synthetic data (no network, no JVM).
+Appendix A corruption class (~11% corrupted). Every signature signs SignableData(txId,
+SignatureMetadata(1, scheme)) -- the clear data Crypto.doVerify(txId, sig) checks -- with
+--sigs-per-tx signatures per transaction id, 4096 Ed25519 keys and 1024 keys per curve.
+Synthetic data (no network, no JVM).
 
-One step = ONE cg_verify_batch_device call over the whole shard with every input resident in HBM:
-use counts + key tables (decode and row tables for every key), then the items in 8M-item device
-chunks (two of 6.25M), status bytes in HBM; plus (N > 1) the RCCL all-gather of the per-GPU
-verdict vectors, the engine's only collective. `value` = items of all ranks / max-over-ranks time.
+One step = ONE cg_verify_tx_signatures call over the whole shard, host arena -> host verdicts
+(the whole node: a JVM caller's direct buffers in, status bytes out): the key table, ids and
+exact key-use counts, then per device chunk its signature-table slice and signature bytes over
+PCIe (~97 B per signature, pageable memory), key tables, SignableData spliced on the device,
+verify, D2H of the verdicts; plus (N > 1) the RCCL all-gather of the per-GPU verdict vectors,
+the engine's only collective. `value` = signatures of all ranks / max-over-ranks time.
 
 Launch: ``python bench.py`` (N = 1) or ``torchrun --nproc-per-node N bench.py --gpus N``; one
 process per GPU, each verifying its own shard (weak scaling). Rank 0 prints ONE JSON line.
@@ -20,14 +23,16 @@ process per GPU, each verifying its own shard (weak scaling). Rank 0 prints ONE 
                 its lane code executes (host-counted) over its per-launch time from HIP events
                 recorded on the stream it runs on, during the timed region (CG_FLAG_STAGE_TIMING);
                 peak = the measured v_mad_u64_u32 chip rate. traffic = PMC FETCH/WRITE bytes per
-                launch (profiles/r02, tools/pmc_traffic.py) when the committed profile matches.
+                launch (profiles/, tools/pmc_traffic.py) when the committed profile matches.
   cpu_baseline  the C restatement of the reference algorithms (oracle/c, "port") on a bounded sample
                 of the same workload, on the box's CPU quota (16 CPUs of a 256-thread EPYC) and on
                 one thread; plus BASELINE configs[0] (10k SignedTransactions, fail-fast
                 checkSignaturesAreValid) on the port and on OpenSSL, next to the GPU on that shape.
-  secondary     the PCIe-inclusive rate (host arena -> host verdicts through cg_verify_batch, the
-                JNI path) on the same workload, per-stage times, and at N = 1 the other BASELINE
-                configs: [1] 2^20 Ed25519, [2] 2^20 ECDSA 50/50, [3] 1M-transaction pipeline, tear-offs.
+  secondary     device-resident forms of the same shard (inputs in HBM: cg_verify_batch_device over
+                materialised messages, cg_verify_tx_signatures_device), the message-form host call
+                (cg_verify_batch), per-stage times, key-distribution legs (2^20 distinct keys; Zipf),
+                and at N = 1 the other BASELINE configs: [1] 2^20 Ed25519, [2] 2^20 ECDSA 50/50,
+                [3] 1M-transaction pipeline, tear-offs.
 """
 import argparse
 import json
@@ -98,8 +103,6 @@ def parse():
     ap.add_argument("--ec-keys", type=int, default=1024, help="keys per ECDSA curve")
     ap.add_argument("--msg-len", type=int, default=270)
     ap.add_argument("--chunk-items", type=int, default=0, help="device chunk (0: CG_DEFAULT_CHUNK_ITEMS = 8M)")
-    ap.add_argument("--stream", choices=("ctx", "torch"), default="ctx",
-                    help="headline calls on the engine context's stream (NULL, as a JNI caller) or torch's")
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--sigs-per-tx", type=int, default=5,
                     help="signatures per transaction id (GeneratedLedger: 1+Poisson(3) signers + the notary)")

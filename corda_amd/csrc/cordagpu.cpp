@@ -162,15 +162,16 @@ cg::WidePool wide_for(cg_ctx* c, uint32_t n_keys, uint64_t n_items) {
 hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
                           const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, hipStream_t s,
                           const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0,
-                          const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* before_front = nullptr) {
-  // before_front (host-buffer entry points): called with (k, first item, items) just before chunk
-  // k's front is enqueued; it makes chunk k's arena bytes resident and orders `s` after them. The
-  // plans and the key-table builds need only the item table, so they are enqueued first and run
-  // while the host copies the first chunk.
+                          const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* prepare = nullptr,
+                          const cg::KeyUses* uses = nullptr) {
+  // prepare (the tx-signature entry points): called with (k, first item, items) just before chunk
+  // k's front is enqueued; it makes chunk k's verify items (and, host form, its bytes) and orders
+  // `s` after them. The key tables are then sized from `uses` and start building at once, before
+  // any chunk is prepared (so they overlap the host copies).
   if (n_items == 0) return hipSuccess;
   const cg::WidePool wp = wide_for(c, n_keys, n_items);
-  hipError_t e =
-      cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork, d_items, n_items, &wp);
+  hipError_t e = cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork,
+                                    uses ? nullptr : d_items, n_items, &wp, uses);
   const uint64_t per = chunk_of(c, n_items);
   const uint64_t nch = (n_items + per - 1) / per;
   // chunk k's item workspace: half k % 2 when the buffer holds two (ensure_ws), else the one
@@ -181,22 +182,23 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
     return cg::launch_items_plan(d_keys, n_keys, d_items + k * per, cnt(k), d_status + k * per, c->keyprep.p, ws(k),
                                  s, &c->fork, &wp);
   };
-  const bool pre_plan = two || before_front;
+  const bool pre_plan = two && !prepare;
   auto front = [&](uint64_t k) {
-    if (before_front) {
-      const hipError_t w = (*before_front)(k, k * per, cnt(k));
+    if (prepare) {
+      const hipError_t w = (*prepare)(k, k * per, cnt(k));
       if (w != hipSuccess) return w;
     }
     return cg::launch_items_front(d_keys, n_keys, d_items + k * per, cnt(k), d_arena, arena_len, mode,
                                   d_status + k * per, c->keyprep.p, ws(k), s, d_msgs, msgs_len, &c->fork, &wp,
-                                  (k == 0 && pre_plan) || (k == 1 && two));
+                                  pre_plan && k < 2);
   };
   // chunk k + 1's front (plan, hashes, ECDSA prep) before chunk k's back (ladders): the first
-  // chunk's wait for the key tables is spent on the next chunk's fronts. The first two plans sort
-  // before the table builds start (their look-back stalls behind the builds).
+  // chunk's wait for the key tables is spent on the next chunk's fronts. Without a prepare hook the
+  // first two plans sort before the table builds start (their look-back stalls behind the builds);
+  // with one, the builds start first: they overlap the preparation of the first chunk.
   if (e == hipSuccess && pre_plan) e = plan(0);
-  if (e == hipSuccess && two) e = plan(1);
-  if (e == hipSuccess && before_front) e = cg::launch_key_tables(&c->fork, s);
+  if (e == hipSuccess && pre_plan) e = plan(1);
+  if (e == hipSuccess && prepare) e = cg::launch_key_tables(&c->fork, s);
   if (e == hipSuccess) e = front(0);
   for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
     if (!two && k > 0) e = front(k);
@@ -753,7 +755,7 @@ static int verify_transactions_locked(cg_ctx* c, const cg_tx* d_txs, uint64_t n_
   }
   uint64_t slot = (maxlen + 15) & ~(uint64_t)15;
   if (slot == 0) slot = 16;
-  const uint64_t msgs_len = cg::tx_msgs_head(n_tmpls) + slot * n_sigs;
+  const uint64_t msgs_len = cg::tx_msgs_head(n_tmpls, slot) + slot * n_sigs;
   const size_t need_leaf = cg::tx_ws_bytes(n_comps), need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1),
                need_msgs = msgs_len ? msgs_len : 16, need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
   if (c->aux2.cap < need_leaf || c->txitems.cap < need_items || c->msgs.cap < need_msgs ||
@@ -865,7 +867,7 @@ static uint64_t tmpl_slot(const cg_signable_tmpl* tmpls, uint32_t n_tmpls) {
 // when a buffer grows).
 static hipError_t ensure_txsig_ws(cg_ctx* c, uint64_t n_sigs, uint32_t n_tmpls, uint64_t slot) {
   const size_t need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1),
-               need_msgs = cg::tx_msgs_head(n_tmpls) + slot * (n_sigs ? n_sigs : 1),
+               need_msgs = cg::tx_msgs_head(n_tmpls, slot) + slot * (n_sigs ? n_sigs : 1),
                need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
   if (c->txitems.cap >= need_items && c->msgs.cap >= need_msgs && c->tmpls.cap >= need_tmpl) return hipSuccess;
   hipError_t e = hipDeviceSynchronize();
@@ -875,23 +877,31 @@ static hipError_t ensure_txsig_ws(cg_ctx* c, uint64_t n_sigs, uint32_t n_tmpls, 
   return e;
 }
 
-// Templates to the device, one verify item + spliced SignableData per signature, then the chunked
-// verify (key tables sized by every signature's key).
+// Templates to the device (midstates + images), then the chunked verify: key tables sized from
+// `uses` (sampled from the signature table on the device, or the host's exact counts), each chunk's
+// verify items and spliced SignableData made just before its front (after `ready`, which the host
+// form uses to land the chunk's signature table slice and bytes).
 static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_ids, uint64_t n_ids,
                                const cg_txsig* d_sigs, uint64_t n_sigs, const cg_signable_tmpl* tmpls,
                                uint32_t n_tmpls, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
-                               uint8_t* d_status, hipStream_t s, uint64_t slot,
-                               const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* before_front) {
+                               uint8_t* d_status, hipStream_t s, uint64_t slot, const cg::KeyUses& uses,
+                               const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* ready) {
   if (n_sigs == 0) return hipSuccess;
   hipError_t e = hipSuccess;
-  if (n_tmpls)
-    e = hipMemcpyAsync(c->tmpls.p, tmpls, sizeof(cg_signable_tmpl) * n_tmpls, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess)
-    e = cg::launch_tx_sig_items(d_sigs, n_sigs, (const cg_signable_tmpl*)c->tmpls.p, n_tmpls, nullptr, n_ids, d_ids,
-                                d_arena, arena_len, slot, (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s);
+  const cg_signable_tmpl* dt = (const cg_signable_tmpl*)c->tmpls.p;
+  if (n_tmpls) e = hipMemcpyAsync(c->tmpls.p, tmpls, sizeof(cg_signable_tmpl) * n_tmpls, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = cg::launch_tx_sig_templates(dt, n_tmpls, d_arena, arena_len, slot, (uint8_t*)c->msgs.p, s);
+  const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> prepare = [&](uint64_t k, uint64_t first,
+                                                                               uint64_t cnt) {
+    hipError_t r = ready ? (*ready)(k, first, cnt) : hipSuccess;
+    if (r == hipSuccess)
+      r = cg::launch_tx_sig_range(d_sigs, first, cnt, dt, n_tmpls, nullptr, n_ids, d_ids, arena_len, slot,
+                                  (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s);
+    return r;
+  };
   if (e == hipSuccess)
     e = launch_chunked(c, d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode, d_status, s,
-                       (const uint8_t*)c->msgs.p, cg::tx_msgs_head(n_tmpls) + slot * n_sigs, before_front);
+                       (const uint8_t*)c->msgs.p, cg::tx_msgs_head(n_tmpls, slot) + slot * n_sigs, &prepare, &uses);
   return e;
 }
 
@@ -915,22 +925,38 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     head.add(tmpls[k].prefix_off, tmpls[k].prefix_len, arena_len);
     head.add(tmpls[k].suffix_off, tmpls[k].suffix_len, arena_len);
   }
+  // one pass over the signature table on up to 16 host threads: each chunk's byte extent, and the
+  // exact per-key use counts (so the key tables need no signature table on the device)
   std::vector<Extent> ext(nch);
+  std::vector<uint32_t> counts(n_keys ? n_keys : 1, 0u);
   {
-    auto scan = [&](uint64_t k0, uint64_t k1) {
-      for (uint64_t k = k0; k < k1; ++k) {
-        const uint64_t e = (k + 1) * per < n_sigs ? (k + 1) * per : n_sigs;
-        for (uint64_t i = k * per; i < e; ++i) ext[k].add(sigs[i].sig_off, sigs[i].sig_len, arena_len);
+    const uint64_t nt = n_sigs < (1u << 16) ? 1 : 16;
+    std::vector<std::vector<Extent>> pe(nt, std::vector<Extent>(nch));
+    std::vector<std::vector<uint32_t>> pc(nt > 1 ? nt : 0, std::vector<uint32_t>(n_keys ? n_keys : 1, 0u));
+    auto scan = [&](uint64_t t) {
+      const uint64_t a = n_sigs * t / nt, b = n_sigs * (t + 1) / nt;
+      uint32_t* cnt = nt > 1 ? pc[t].data() : counts.data();
+      for (uint64_t i = a; i < b; ++i) {
+        pe[t][i / per].add(sigs[i].sig_off, sigs[i].sig_len, arena_len);
+        if (sigs[i].key_idx < n_keys) ++cnt[sigs[i].key_idx];
       }
     };
-    const uint64_t nt = nch < 16 ? nch : 16;
-    if (n_sigs < (1u << 16) || nt < 2) {
-      scan(0, nch);
+    if (nt == 1) {
+      scan(0);
     } else {
       std::vector<std::thread> th;
-      for (uint64_t t = 0; t < nt; ++t) th.emplace_back(scan, nch * t / nt, nch * (t + 1) / nt);
+      for (uint64_t t = 0; t < nt; ++t) th.emplace_back(scan, t);
+      for (auto& t : th) t.join();
+      th.clear();
+      for (uint64_t t = 0; t < nt; ++t)  // sum the per-thread counts, key ranges in parallel
+        th.emplace_back([&, t] {
+          for (uint64_t k = n_keys * t / nt; k < n_keys * (t + 1) / nt; ++k)
+            for (uint64_t u = 0; u < nt; ++u) counts[k] += pc[u][k];
+        });
       for (auto& t : th) t.join();
     }
+    for (uint64_t t = 0; t < nt; ++t)
+      for (uint64_t k = 0; k < nch; ++k) ext[k].merge(pe[t][k]);
   }
   win = head;
   for (const Extent& e : ext) win.merge(e);
@@ -939,6 +965,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   const uint64_t slot = tmpl_slot(tmpls, n_tmpls);
   HIP_TRY(c->keys.ensure(sizeof(cg_key) * (n_keys ? n_keys : 1)), "hipMalloc(keys)");
   HIP_TRY(c->h_sigs.ensure(sizeof(cg_txsig) * n_sigs), "hipMalloc(sigs)");
+  HIP_TRY(c->aux1.ensure(sizeof(uint32_t) * counts.size()), "hipMalloc(key use counts)");
   HIP_TRY(c->h_ids.ensure(32 * (n_ids ? n_ids : 1)), "hipMalloc(ids)");
   HIP_TRY(c->arena.ensure((win.hi - win.lo) + 16), "hipMalloc(arena window)");
   HIP_TRY(c->status.ensure(n_sigs), "hipMalloc(status)");
@@ -960,12 +987,17 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, c->copy), "H2D keys");
   HIP_TRY(copy_missing(have, head, arena, dwin, win.lo, c->copy), "H2D key / template bytes");
   if (n_ids) HIP_TRY(hipMemcpyAsync(c->h_ids.p, ids, 32 * n_ids, hipMemcpyHostToDevice, c->copy), "H2D ids");
-  HIP_TRY(hipMemcpyAsync(c->h_sigs.p, sigs, sizeof(cg_txsig) * n_sigs, hipMemcpyHostToDevice, c->copy), "H2D sigs");
+  HIP_TRY(hipMemcpyAsync(c->aux1.p, counts.data(), sizeof(uint32_t) * counts.size(), hipMemcpyHostToDevice, c->copy),
+          "H2D key use counts");
   HIP_TRY(hipEventRecord(c->seg[nch], c->copy), "hipEventRecord");
   HIP_TRY(hipStreamWaitEvent(s, c->seg[nch], 0), "hipStreamWaitEvent");
   hipError_t copy_err = hipSuccess;
-  const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t, uint64_t) {
-    hipError_t e = copy_missing(have, ext[k], arena, dwin, win.lo, c->copy);
+  // chunk k: its slice of the signature table, then its signature bytes
+  const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t first,
+                                                                              uint64_t cnt) {
+    hipError_t e = hipMemcpyAsync((cg_txsig*)c->h_sigs.p + first, sigs + first, sizeof(cg_txsig) * cnt,
+                                  hipMemcpyHostToDevice, c->copy);
+    if (e == hipSuccess) e = copy_missing(have, ext[k], arena, dwin, win.lo, c->copy);
     if (e == hipSuccess) e = hipEventRecord(c->seg[k], c->copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, c->seg[k], 0);
     if (e == hipSuccess && k == 0) e = hipEventRecord(c->tev[1], s);
@@ -973,9 +1005,12 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     return e;
   };
   uint8_t* ds = (uint8_t*)c->status.p;
+  cg::KeyUses uses;
+  uses.counts = (const uint32_t*)c->aux1.p;
+  uses.n = n_sigs;
   const hipError_t le = launch_txsig(c, (const cg_key*)c->keys.p, n_keys, (const uint8_t*)c->h_ids.p, n_ids,
                                      (const cg_txsig*)c->h_sigs.p, n_sigs, tmpls, n_tmpls, dbase, arena_len, mode, ds,
-                                     s, slot, &before);
+                                     s, slot, uses, &before);
   if (copy_err != hipSuccess) return hip_fail(copy_err, "H2D signature bytes");
   HIP_TRY(le, "launch_txsig");
   HIP_TRY(hipEventRecord(c->tev[2], s), "hipEventRecord");
@@ -1028,8 +1063,11 @@ int cg_verify_tx_signatures_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_k
   HIP_TRY(ensure_ws(c, n_keys, chunk_of(c, n_sigs), n_sigs), "hipMalloc(workspace)");
   hipStream_t s = stream_of(c, hip_stream);
   HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
+  cg::KeyUses uses;
+  uses.sigs = d_sigs;
+  uses.n = n_sigs;
   HIP_TRY(launch_txsig(c, d_keys, n_keys, d_ids, n_ids, d_sigs, n_sigs, tmpls, n_tmpls, d_arena, arena_len, mode,
-                       d_status, s, slot, nullptr),
+                       d_status, s, slot, uses, nullptr),
           "launch_txsig");
   HIP_TRY(order_out(c, s), "hipEventRecord");
   return CG_OK;

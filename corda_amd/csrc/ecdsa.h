@@ -203,6 +203,65 @@ CG_HD void jac_madd(Jac& r, const Jac& p, const f29& x2, const f29& y2, const Ec
   r = o;
 }
 
+// r = p + (x2, +-y2) affine for the wide ladder: madd-2007-bl with fewer carry chains.
+//  * `inf` flags p = infinity (the ladder's start, or an exceptional P + (-P)) instead of testing Z;
+//  * the sign rides on S2 = +-y2 Z1^3 (m29_neg2: one chain);
+//  * H = U2 - X1 and V - X3 are semi-reduced (m29_sub2: one chain), both used only as
+//    multiplication operands against values < 4m;
+//  * Z3 = Z1 * 2H (one product) instead of (Z1 + H)^2 - Z1Z1 - HH (a square and two subtractions);
+//  * H == 0 (mod p), i.e. the exceptional cases, behind a limb-0 filter that honest inputs fail
+//    with probability ~3 / 2^29, so the wave skips the exact test.
+// Same point as jac_madd (the exceptional cases included: doubling, P + (-P) -> infinity).
+template <int C>
+CG_HD void jac_madd_w(Jac& r, bool& inf, const f29& x2, const f29& y2, bool neg, const EcConsts& K) {
+  if (inf) {
+    r.X = x2;
+    if (neg) m29_neg2<C, 0>(r.Y, y2);
+    else r.Y = y2;
+    r.Z = K.one_p;
+    inf = false;
+    return;
+  }
+  f29 Z1Z1, U2, S2, H, HH, I, J, rr, V, t;
+  m29_sq<C, 0>(Z1Z1, r.Z);
+  m29_mul<C, 0>(U2, x2, Z1Z1);
+  m29_mul<C, 0>(S2, y2, r.Z);
+  m29_mul<C, 0>(S2, S2, Z1Z1);
+  if (neg) m29_neg2<C, 0>(S2, S2);
+  m29_sub2<C, 0>(H, U2, r.X);
+  m29_sub<C, 0>(rr, S2, r.Y);
+  if (m29_maybe_zero_semi<C, 0>(H)) {
+    if (m29_zero_semi<C, 0>(H)) {
+      if (m29_iszero<C, 0>(rr)) {
+        jac_dbl<C>(r, r);
+      } else {
+        jac_set_inf<C>(r, K);
+        inf = true;
+      }
+      return;
+    }
+  }
+  m29_sq<C, 0>(HH, H);
+  m29_add<C, 0>(I, HH, HH);
+  m29_add_lazy(I, I, I);      // 4 HH (< 4m: multiply operand only)
+  m29_mul<C, 0>(J, H, I);
+  m29_mul<C, 0>(V, r.X, I);
+  m29_add_lazy(rr, rr, rr);   // 2 (S2 - Y1) (multiply operand only)
+  Jac o;
+  m29_sq<C, 0>(o.X, rr);
+  m29_sub<C, 0>(o.X, o.X, J);
+  m29_add<C, 0>(t, V, V);
+  m29_sub<C, 0>(o.X, o.X, t);
+  m29_sub2<C, 0>(t, V, o.X);
+  m29_mul<C, 0>(o.Y, rr, t);
+  m29_add_lazy(t, r.Y, r.Y);
+  m29_mul<C, 0>(t, t, J);
+  m29_sub<C, 0>(o.Y, o.Y, t);
+  m29_add_lazy(H, H, H);      // 2H < 8m, limbs < 2^30: times Z1 < 2m
+  m29_mul<C, 0>(o.Z, r.Z, H);
+  r = o;
+}
+
 // affine (Montgomery) of a finite Jacobian point
 template <int C>
 CG_HD void jac_to_affine(f29& x, f29& y, const Jac& p, const EcConsts& K) {

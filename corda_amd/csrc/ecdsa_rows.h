@@ -703,6 +703,7 @@ CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u
   ec_recode_wide<EC_WIDE_W, EC_WIDE_DIGITS, true>(dq, u2);
   Jac R;
   jac_set_inf<C>(R, K);
+  bool inf = true;
 #pragma unroll 1
   for (int j = 0; j < EC_WIDE_DIGITS; ++j) {
     const int b = ec_digit10(dq, j);  // int16 digits
@@ -711,8 +712,7 @@ CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u
       const int a = b < 0 ? -b : b;  // the top digit alone reaches 129..256: row 32
       if (a > EC_WIDE_MULT) ec_pick(x, y, TQ.t[EC_WIDE_DIGITS], a - EC_WIDE_MULT);
       else ec_pick(x, y, TQ.t[j], a);
-      if (b < 0) m29_neg<C, 0>(y, y);
-      jac_madd<C>(R, R, x, y, K);
+      jac_madd_w<C>(R, inf, x, y, b < 0, K);
     }
   }
 #pragma unroll 1
@@ -721,8 +721,7 @@ CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u
     if (a != 0) {
       f29 x, y;
       ec_pick(x, y, TG.t[u], a < 0 ? -a : a);
-      if (a < 0) m29_neg<C, 0>(y, y);
-      jac_madd<C>(R, R, x, y, K);
+      jac_madd_w<C>(R, inf, x, y, a < 0, K);
     }
   }
   return ecdsa_x_check<C>(R, r, K);

@@ -115,11 +115,19 @@ size_t btab_scratch_bytes();  // temporary scratch of init_btab (free once it ha
 hipError_t init_btab(void* d_btab, void* d_scratch, hipStream_t stream);
 // Bytes of per-item workspace (projective Ed25519 results awaiting the batched inversion).
 size_t item_ws_bytes(uint64_t n_items);
-// With `d_items`, each key's table is sized by the number of items that use it (keyws.h);
-// without (cg_prepare_keys_device), every key gets full tables.
+// Where the per-key use counts come from when there is no verify-item table yet: a cg_txsig table
+// in HBM (sampled on the device) or exact counts (n_keys u32 in HBM, made by the host).
+struct KeyUses {
+  const cg_txsig* sigs = nullptr;
+  const uint32_t* counts = nullptr;
+  uint64_t n = 0;  // signatures the counts cover (sizes the wide pools)
+};
+// With `d_items` (or `src`), each key's table is sized by the number of items that use it
+// (keyws.h); with neither (cg_prepare_keys_device), every key gets full tables.
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream, const Fork* fork = nullptr,
-                          const cg_item* d_items = nullptr, uint64_t n_items = 0, const WidePool* wide = nullptr);
+                          const cg_item* d_items = nullptr, uint64_t n_items = 0, const WidePool* wide = nullptr,
+                          const KeyUses* src = nullptr);
 // Start the table builds launch_keyprep deferred (no-op if already started): a host-buffer call
 // starts them before it blocks on the first chunk's arena copy, so they overlap that copy.
 hipError_t launch_key_tables(const Fork* fork, hipStream_t stream);
@@ -163,13 +171,22 @@ hipError_t launch_tx_ids(const cg_tx* d_txs, uint64_t n_tx, const cg_component* 
                          uint8_t* d_leaf_ws, hipStream_t stream);
 
 // Transaction pipeline: per-signature verify items + spliced SignableData messages: d_msgs holds
-// the templates' SHA-256 midstate records (tx_msgs_head(n_tmpls) bytes), then one `slot`-byte
-// message slot per signature (slot a multiple of 16).
-uint64_t tx_msgs_head(uint32_t n_tmpls);
+// the templates' SHA-256 midstate records and template images (tx_msgs_head(n_tmpls, slot) bytes),
+// then one `slot`-byte message slot per signature (slot a multiple of 16).
+uint64_t tx_msgs_head(uint32_t n_tmpls, uint64_t slot);
 hipError_t launch_tx_sig_items(const cg_txsig* d_sigs, uint64_t n_sigs, const cg_signable_tmpl* d_tmpls,
                                uint32_t n_tmpls, const uint8_t* d_tx_status, uint64_t n_tx, const uint8_t* d_ids,
                                const uint8_t* d_arena, uint64_t arena_len, uint64_t slot, cg_item* d_items,
                                uint8_t* d_msgs, hipStream_t stream);
+// The same in two steps: the templates' midstates + images once per call (tx_sig_templates), then
+// any contiguous range [first, first + n) of the signatures (tx_sig_range: its verify items and
+// spliced messages; every signature keeps its own message slot).
+hipError_t launch_tx_sig_templates(const cg_signable_tmpl* d_tmpls, uint32_t n_tmpls, const uint8_t* d_arena,
+                                   uint64_t arena_len, uint64_t slot, uint8_t* d_msgs, hipStream_t stream);
+hipError_t launch_tx_sig_range(const cg_txsig* d_sigs, uint64_t first, uint64_t n, const cg_signable_tmpl* d_tmpls,
+                               uint32_t n_tmpls, const uint8_t* d_tx_status, uint64_t n_tx, const uint8_t* d_ids,
+                               uint64_t arena_len, uint64_t slot, cg_item* d_items, uint8_t* d_msgs,
+                               hipStream_t stream);
 
 // Merkle roots over independent leaf lists.
 hipError_t launch_merkle_roots(const uint8_t* d_leaves, const uint64_t* d_first, const uint32_t* d_count,

@@ -69,7 +69,7 @@ struct TmplMid {
   uint32_t pad[3];
 };
 static_assert(sizeof(TmplMid) == 48, "template midstate record");
-static inline uint64_t tmpl_mid_bytes(uint32_t n_tmpls) { return ((uint64_t)n_tmpls * sizeof(TmplMid) + 255) & ~(uint64_t)255; }
+CG_HD uint64_t tmpl_mid_bytes(uint32_t n_tmpls) { return ((uint64_t)n_tmpls * sizeof(TmplMid) + 255) & ~(uint64_t)255; }
 __device__ __forceinline__ const TmplMid* item_tmpl_mid(const cg_item& it, const uint8_t* msgs) {
   return (it.reserved0 & CG_ITEM_TMPL) && (it.reserved0 & CG_ITEM_MSG_WS) && msgs
              ? (const TmplMid*)msgs + it.reserved1

@@ -59,6 +59,20 @@ constexpr uint32_t m29_limb(int C, int N, int k, int i) {
                     M29_MASK);
 }
 
+// 29-bit limb i (0..8) of k * m for a small k (k m < 2^261)
+constexpr uint32_t m29_limb_k(int C, int N, uint32_t k, int i) {
+  uint64_t carry = 0;
+  uint32_t w[9] = {};
+  for (int j = 0; j < 9; ++j) {
+    const uint64_t x = (uint64_t)m29_w32(C, N, j) * k + carry;
+    w[j] = (uint32_t)x;
+    carry = x >> 32;
+  }
+  const int bit = 29 * i, wi = bit >> 5, sh = bit & 31;
+  const uint64_t x = ((uint64_t)w[wi] >> sh) | (wi + 1 < 9 ? (uint64_t)w[wi + 1] << (32 - sh) : 0u);
+  return (uint32_t)x & M29_MASK;
+}
+
 // -m^-1 mod 2^29 (Newton iteration for m^-1 mod 2^32)
 constexpr uint32_t m29_ninv(int C, int N) {
   uint32_t inv = 1;
@@ -153,6 +167,16 @@ CG_HD void m29_mul(f29& r, const f29& a, const f29& b) {
     acc >>= 29;
   }
   out[8] = (uint32_t)acc;
+#ifdef FE_BOUNDS_CHECK
+  {  // the output is reduced (< 2m): the inputs respected a b < m R
+    int32_t br = 0;
+    for (int i = 0; i < 9; ++i) {
+      const int32_t d = (int32_t)out[i] - (int32_t)m29_limb(C, N, 2, i) + br;
+      br = d >> 29;
+    }
+    FE_ASSERT(br < 0);
+  }
+#endif
 #pragma unroll
   for (int i = 0; i < 9; ++i) r.v[i] = out[i];
 }
@@ -238,6 +262,55 @@ CG_HD void m29_sub(f29& r, const f29& a, const f29& b) {
     r.v[i] = s & M29_MASK;
     c = s >> 29;
   }
+}
+
+// "Semi-reduced": normalized limbs, value < 4m. A valid m29_mul operand when the other operand is
+// < 4m (16 m^2 < m R), not a valid m29_sub / m29_add input.
+// r = a + 2m - b (a, b reduced): ONE signed carry chain instead of m29_sub's two; r semi-reduced,
+// r in (0, 4m).
+template <int C, int N>
+CG_HD void m29_sub2(f29& r, const f29& a, const f29& b) {
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int32_t s = (int32_t)(a.v[i] + m29_limb(C, N, 2, i)) - (int32_t)b.v[i] + c;
+    r.v[i] = (uint32_t)s & M29_MASK;
+    c = s >> 29;
+  }
+  FE_ASSERT(c == 0);
+}
+
+// r = 2m - a for a reduced and a != 0 (as a value): r in (0, 2m), reduced; one carry chain.
+template <int C, int N>
+CG_HD void m29_neg2(f29& r, const f29& a) {
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int32_t s = (int32_t)m29_limb(C, N, 2, i) - (int32_t)a.v[i] + c;
+    r.v[i] = (uint32_t)s & M29_MASK;
+    c = s >> 29;
+  }
+  FE_ASSERT(c == 0);
+}
+
+// Can a semi-reduced a (value < 4m) be 0 mod m, i.e. one of 0, m, 2m, 3m? A filter on limb 0 (false
+// positives ~3 in 2^29); m29_zero_semi decides.
+template <int C, int N>
+CG_HD bool m29_maybe_zero_semi(const f29& a) {
+  const uint32_t x = a.v[0];
+  return x == 0u || x == m29_limb_k(C, N, 1, 0) || x == m29_limb_k(C, N, 2, 0) || x == m29_limb_k(C, N, 3, 0);
+}
+template <int C, int N>
+CG_HD bool m29_zero_semi(const f29& a) {
+  bool z = false;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o |= a.v[i] ^ m29_limb_k(C, N, k, i);
+    z |= o == 0;
+  }
+  return z;
 }
 
 template <int C, int N>

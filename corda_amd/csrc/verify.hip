@@ -55,6 +55,29 @@ __global__ void __launch_bounds__(256) k_key_uses(const cg_item* __restrict__ it
   if (((uint32_t)i * 0x9E3779B1u) >> 30 == 0) atomicAdd(&uses[k], KEY_USES_SAMPLE);
 }
 
+// The same, from a cg_txsig table (cg_verify_tx_signatures_device: the key tables are sized before
+// any verify item exists, so the per-chunk item builds and splices can follow them).
+__global__ void __launch_bounds__(256) k_key_uses_txsig(const cg_txsig* __restrict__ sigs, uint64_t n,
+                                                        uint32_t n_keys, uint32_t* __restrict__ uses,
+                                                        uint8_t* __restrict__ seen) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = sigs[i].key_idx;
+  if (k >= n_keys) return;
+  seen[k] = 1;
+  if (((uint32_t)i * 0x9E3779B1u) >> 30 == 0) atomicAdd(&uses[k], KEY_USES_SAMPLE);
+}
+
+// Exact counts made by the host (cg_verify_tx_signatures counts while it scans the signature
+// table for the copy extents, so no signature table has to be resident before the key tables).
+__global__ void __launch_bounds__(256) k_key_counts(const uint32_t* __restrict__ counts, uint32_t n_keys,
+                                                    uint32_t* __restrict__ uses, uint8_t* __restrict__ seen) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_keys) return;
+  uses[i] = counts[i];
+  seen[i] = counts[i] != 0;
+}
+
 // Append the lanes with c == k to list k (one atomic per wave and class).
 __device__ __forceinline__ void list_append(int c, uint32_t i, uint32_t n_keys, uint32_t* __restrict__ list,
                                             uint32_t* __restrict__ count) {
@@ -169,16 +192,24 @@ hipError_t launch_key_tables(const Fork* fork, hipStream_t stream) {
 
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream, const Fork* fork, const cg_item* d_items,
-                          uint64_t n_items, const WidePool* wide) {
+                          uint64_t n_items, const WidePool* wide, const KeyUses* src) {
   if (n_keys == 0) return hipSuccess;
-  const KeyWs w = key_ws(d_keyprep, n_keys, d_items ? wide : nullptr);
+  const bool counted = d_items || src;  // tables sized by the call's key uses
+  if (!d_items && src) n_items = src->n;
+  const KeyWs w = key_ws(d_keyprep, n_keys, counted ? wide : nullptr);
   // use counts first (main stream; the side streams fork after them)
   const uint32_t kl = n_keys > PLAN_CLASSES + 2 ? n_keys : PLAN_CLASSES + 2;
-  hipLaunchKernelGGL(k_key_init, dim3((kl + 255) / 256), dim3(256), 0, stream, n_keys, d_items ? 0u : 1u, w.uses,
+  hipLaunchKernelGGL(k_key_init, dim3((kl + 255) / 256), dim3(256), 0, stream, n_keys, counted ? 0u : 1u, w.uses,
                      w.seen, w.full_count, w.wide_idx, w.wide_count);
   if (d_items && n_items)
     hipLaunchKernelGGL(k_key_uses, dim3((unsigned)((n_items + 255) / 256)), dim3(256), 0, stream, d_items, n_items,
                        n_keys, w.uses, w.seen);
+  else if (src && src->counts)
+    hipLaunchKernelGGL(k_key_counts, dim3((n_keys + 255) / 256), dim3(256), 0, stream, src->counts, n_keys, w.uses,
+                       w.seen);
+  else if (src && src->sigs && src->n)
+    hipLaunchKernelGGL(k_key_uses_txsig, dim3((unsigned)((src->n + 255) / 256)), dim3(256), 0, stream, src->sigs,
+                       src->n, n_keys, w.uses, w.seen);
   hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys, w.uses,
                      (const uint8_t*)w.seen, w.full, w.full_count, w.wide_idx, w.wide, w.wide_count, w.cap_ed,
                      w.cap_ec, w.min_ed, w.min_ec);
@@ -219,8 +250,8 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   fork->pending.keys = d_keys;
   fork->pending.n_keys = n_keys;
   fork->pending.keyprep = d_keyprep;
-  fork->pending.wide = d_items && wide ? *wide : WidePool{};
-  if (!d_items) e = launch_pending_tabs(fork, stream);
+  fork->pending.wide = counted && wide ? *wide : WidePool{};
+  if (!counted) e = launch_pending_tabs(fork, stream);
   if (e != hipSuccess) return e;
   // the only key work on the main stream: Abyte for k_ed_hash (no decode)
   ed_launch_key_abyte(d_keys, n_keys, d_arena, arena_len, w, stream);

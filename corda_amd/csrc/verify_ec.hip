@@ -361,6 +361,7 @@ __global__ void __launch_bounds__(256) k_ec_ladder_wide(const cg_item* __restric
     ec_recode_wide<EC_WIDE_W, EC_WIDE_DIGITS, true>(dq, w.b);
     Jac R;
     jac_set_inf<C>(R, K);
+    bool inf = true;
     int d_next = ec_wide_digit(dq, dg, 0);
     ec_glds_aff(ec_wide_src(TQ, *gw, 0, d_next), wl);
 #pragma unroll 1
@@ -374,10 +375,7 @@ __global__ void __launch_bounds__(256) k_ec_ladder_wide(const cg_item* __restric
         d_next = ec_wide_digit(dq, dg, o + 1);
         ec_glds_aff(ec_wide_src(TQ, *gw, o + 1, d_next), wl);
       }
-      if (d != 0) {
-        if (d < 0) m29_neg<C, 0>(y, y);
-        jac_madd<C>(R, R, x, y, K);
-      }
+      if (d != 0) jac_madd_w<C>(R, inf, x, y, d < 0, K);
     }
     status[i] = (uint8_t)ecdsa_x_check<C>(R, w.r, K);
   }

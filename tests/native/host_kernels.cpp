@@ -735,3 +735,58 @@ extern "C" int t_ecdsa_verify_wide(int scheme, const uint8_t* arena, uint64_t ar
     return ecdsa_wide_verify<CG_CURVE_R1>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len, counts);
   return ecdsa_wide_verify<CG_CURVE_K1>(arena, lr, key_off, key_len, fmt, sig_off, sig_len, msg_off, msg_len, counts);
 }
+
+// jac_madd_w (the wide ladder's mixed addition: lazy sums, inf flag, Z3 = Z1 * 2H) against
+// jac_madd on chains of random additions of multiples of G with random signs, plus the exceptional
+// cases: acc + acc (doubling), acc + (-acc) (infinity), infinity + Q. Returns mismatches.
+template <int C>
+static int madd_w_cmp(uint64_t seed, int n) {
+  EcConsts K;
+  ec_consts_init<C>(K);
+  int bad = 0;
+  uint64_t s = seed;
+  auto rnd = [&]() {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    return s;
+  };
+  auto same = [&](const Jac& a, bool ainf, const Jac& b) {
+    const bool binf = m29_iszero<C, 0>(b.Z);
+    if (ainf || binf) return ainf == binf;
+    f29 x1, y1, x2, y2;
+    jac_to_affine<C>(x1, y1, a, K);
+    jac_to_affine<C>(x2, y2, b, K);
+    return m29_eq<C, 0>(x1, x2) && m29_eq<C, 0>(y1, y2);
+  };
+  for (int t = 0; t < n; ++t) {
+    // acc = k G (Jacobian, Z != 1 after the multiplication), q = m G affine
+    Jac acc, q;
+    jac_small_mul_aff<C>(acc, K.gx, K.gy, 2 + (uint32_t)(rnd() % 5000), K);
+    const int kind = t % 4;
+    f29 qx, qy;
+    if (kind == 0) {
+      jac_small_mul_aff<C>(q, K.gx, K.gy, 2 + (uint32_t)(rnd() % 5000), K);
+      jac_to_affine<C>(qx, qy, q, K);
+    } else {  // kinds 1, 2: Q = +-acc (doubling / infinity); kind 3: acc = infinity
+      jac_to_affine<C>(qx, qy, acc, K);
+    }
+    const bool neg = kind == 2 ? true : (kind == 1 ? false : (rnd() & 1));
+    Jac ref = acc, got = acc;
+    bool inf = kind == 3;
+    if (kind == 3) jac_set_inf<C>(ref, K);
+    f29 y = qy;
+    if (neg) m29_neg<C, 0>(y, qy);
+    jac_madd<C>(ref, ref, qx, y, K);
+    jac_madd_w<C>(got, inf, qx, qy, neg, K);
+    // and a second addition on top (the flag and the outputs' bounds carry over)
+    f29 y2 = K.gy;
+    jac_madd<C>(ref, ref, K.gx, y2, K);
+    jac_madd_w<C>(got, inf, K.gx, K.gy, false, K);
+    if (!same(got, inf, ref)) ++bad;
+  }
+  return bad;
+}
+extern "C" int t_ec_madd_w_cmp(int curve, uint64_t seed, int n) {
+  return curve == 1 ? madd_w_cmp<CG_CURVE_R1>(seed, n) : madd_w_cmp<CG_CURVE_K1>(seed, n);
+}

@@ -2,6 +2,7 @@
 host with FE_BOUNDS_CHECK (every limb bound assumed by fe25519.h is asserted; a violated
 bound aborts the process), checked against Python big integers and the oracle.
 CPU only: this is where kernel arithmetic is debugged before it reaches a GPU."""
+import ctypes
 import random
 
 import numpy as np
@@ -379,3 +380,13 @@ def test_executed_work_constants_wide():
                                            int(itm["msg_off"]), int(itm["msg_len"]), ptr(o)) == 0
             lad.append(int(o[0]))
         assert max(lad) == bench.EC_WIDE_MUL[name] and np.mean(lad) > 0.97 * max(lad), (name, lad)
+
+
+@pytest.mark.parametrize("curve", [0, 1])
+def test_ec_madd_w_matches_madd(curve):
+    """The wide ladder's mixed addition (semi-reduced operands, infinity flag, Z3 = Z1 * 2H) gives
+    the same points as the exception-complete jac_madd, including Q = acc (doubling), Q = -acc
+    (infinity) and acc = infinity, under the host build's limb and Montgomery-output bound checks."""
+    lib = hostk.lib()
+    lib.t_ec_madd_w_cmp.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int]
+    assert lib.t_ec_madd_w_cmp(curve, 12345 + curve, 400) == 0

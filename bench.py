@@ -580,7 +580,7 @@ def bench_key_dist(a, eng, dist, rank, threads, steps):
     pool, pl, ps = wl.notary_pool(a.pool, seed=a.seed + 7919 * rank + 17, nthreads=threads, sig_group=a.sigs_per_tx,
                                   key_dist=dist)
     ids, id_idx = wl.pool_ids(pool, len(signable.template(1, 4)[0]))
-    idx = np.random.default_rng(a.seed + 5).integers(0, pool.n, a.items)
+    idx = wl.tx_ordered_draws(pool.n, a.items, id_idx, seed=a.seed + 5)
     tb = wl.tx_sig_stream(pool, ps, idx, ids, id_idx, nthreads=threads)
     gen = time.time() - t0
     from corda_amd.batch import Batch
@@ -643,7 +643,8 @@ def main():
                                                      seed=a.seed + 7919 * rank, nthreads=threads,
                                                      sig_group=a.sigs_per_tx)
     ids, id_idx = wl.pool_ids(pool, len(signable.template(1, 4)[0]))
-    batch, idx = wl.index_stream(pool, a.items, seed=a.seed + 31 * rank + 1, replicate=True)
+    draws = wl.tx_ordered_draws(pool.n, a.items, id_idx, seed=a.seed + 31 * rank + 1)
+    batch, idx = wl.index_stream(pool, a.items, replicate=True, idx=draws)
     tb = wl.tx_sig_stream(pool, pool_schemes, idx, ids, id_idx, nthreads=threads)
     labels, schemes = pool_labels[idx], pool_schemes[idx]
     gen_s = time.time() - t0

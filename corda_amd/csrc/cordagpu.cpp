@@ -79,6 +79,7 @@ struct DevBuf {
 struct cg_ctx {
   int device = 0;
   uint64_t chunk = CG_DEFAULT_CHUNK_ITEMS;  // items per verify chunk (cg_config.chunk_items)
+  bool chunk_set = false;                   // the caller chose it (else the host tx-signature path pipelines finer)
   bool fault = false;                       // cg_pool_inject_fault drill: every call fails
   hipStream_t stream = nullptr;
   cg::Fork fork = {{nullptr, nullptr, nullptr}, nullptr, {nullptr, nullptr}, {nullptr, nullptr, nullptr}, nullptr,
@@ -163,7 +164,7 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
                           const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, hipStream_t s,
                           const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0,
                           const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* prepare = nullptr,
-                          const cg::KeyUses* uses = nullptr) {
+                          const cg::KeyUses* uses = nullptr, uint64_t per_items = 0) {
   // prepare (the tx-signature entry points): called with (k, first item, items) just before chunk
   // k's front is enqueued; it makes chunk k's verify items (and, host form, its bytes) and orders
   // `s` after them. The key tables are then sized from `uses` and start building at once, before
@@ -172,7 +173,7 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   const cg::WidePool wp = wide_for(c, n_keys, n_items);
   hipError_t e = cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork,
                                     uses ? nullptr : d_items, n_items, &wp, uses);
-  const uint64_t per = chunk_of(c, n_items);
+  const uint64_t per = per_items ? per_items : chunk_of(c, n_items);
   const uint64_t nch = (n_items + per - 1) / per;
   // chunk k's item workspace: half k % 2 when the buffer holds two (ensure_ws), else the one
   const bool two = nch > 1 && c->itemws.cap >= 2 * item_half_bytes(per);
@@ -402,7 +403,10 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     return fail(CG_ERR_DEVICE, "cg_open: kernels are built for gfx950, device is %s", prop.gcnArchName);
   cg_ctx* c = new cg_ctx();
   c->device = dev;
-  if (cfg && cfg->chunk_items) c->chunk = cfg->chunk_items;
+  if (cfg && cfg->chunk_items) {
+    c->chunk = cfg->chunk_items;
+    c->chunk_set = true;
+  }
   if (cfg && (cfg->flags & CG_FLAG_STAGE_TIMING)) c->fork.timer = &c->timer;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
@@ -852,6 +856,7 @@ int cg_verify_transactions(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_
 }
 
 // ---------------------------------------------------------------- signatures over known tx ids
+#define CG_TXSIG_MIN_CHUNKS 4u
 // The spliced-message slot of a template set: the longest prefix || id || suffix, 16-aligned.
 static uint64_t tmpl_slot(const cg_signable_tmpl* tmpls, uint32_t n_tmpls) {
   uint64_t maxlen = 0;
@@ -885,7 +890,8 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
                                const cg_txsig* d_sigs, uint64_t n_sigs, const cg_signable_tmpl* tmpls,
                                uint32_t n_tmpls, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
                                uint8_t* d_status, hipStream_t s, uint64_t slot, const cg::KeyUses& uses,
-                               const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* ready) {
+                               const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* ready,
+                               uint64_t per = 0) {
   if (n_sigs == 0) return hipSuccess;
   hipError_t e = hipSuccess;
   const cg_signable_tmpl* dt = (const cg_signable_tmpl*)c->tmpls.p;
@@ -901,7 +907,8 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
   };
   if (e == hipSuccess)
     e = launch_chunked(c, d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode, d_status, s,
-                       (const uint8_t*)c->msgs.p, cg::tx_msgs_head(n_tmpls, slot) + slot * n_sigs, &prepare, &uses);
+                       (const uint8_t*)c->msgs.p, cg::tx_msgs_head(n_tmpls, slot) + slot * n_sigs, &prepare, &uses,
+                       per);
   return e;
 }
 
@@ -916,7 +923,15 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   const auto t0 = std::chrono::steady_clock::now();
   if (c->fault) return fail(CG_ERR_DEVICE, "cg_verify_tx_signatures: device fault (injected by cg_pool_inject_fault)");
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  const uint64_t per = chunk_of(c, n_sigs);
+  // chunks: the device chunk, but at least CG_TXSIG_MIN_CHUNKS of them for a large call unless the
+  // caller set cg_config.chunk_items (the first chunk's copy is the part nothing overlaps; measured on
+  // the configs[4] shard: 2 chunks 190.7M, 3 200.8M, 4 207.7M, 6 190.0M sigs/s,
+  // profiles/r03/chunks_v1)
+  uint64_t per = chunk_of(c, n_sigs);
+  if (!c->chunk_set && n_sigs >= CG_TXSIG_MIN_CHUNKS * (1ull << 20)) {
+    const uint64_t alt = (n_sigs + CG_TXSIG_MIN_CHUNKS - 1) / CG_TXSIG_MIN_CHUNKS;
+    if (alt < per) per = alt;
+  }
   const uint64_t nch = (n_sigs + per - 1) / per;
   // arena extents: key bytes + template bytes (the header), then each chunk's signature bytes
   Extent head, win;
@@ -927,17 +942,18 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   }
   // one pass over the signature table on up to 16 host threads: each chunk's byte extent, and the
   // exact per-key use counts (so the key tables need no signature table on the device)
-  std::vector<Extent> ext(nch);
+  std::vector<Extent> ext(nch), idx(nch);  // arena bytes and id bytes each chunk reads
   std::vector<uint32_t> counts(n_keys ? n_keys : 1, 0u);
   {
     const uint64_t nt = n_sigs < (1u << 16) ? 1 : 16;
-    std::vector<std::vector<Extent>> pe(nt, std::vector<Extent>(nch));
+    std::vector<std::vector<Extent>> pe(nt, std::vector<Extent>(nch)), pi(nt, std::vector<Extent>(nch));
     std::vector<std::vector<uint32_t>> pc(nt > 1 ? nt : 0, std::vector<uint32_t>(n_keys ? n_keys : 1, 0u));
     auto scan = [&](uint64_t t) {
       const uint64_t a = n_sigs * t / nt, b = n_sigs * (t + 1) / nt;
       uint32_t* cnt = nt > 1 ? pc[t].data() : counts.data();
       for (uint64_t i = a; i < b; ++i) {
         pe[t][i / per].add(sigs[i].sig_off, sigs[i].sig_len, arena_len);
+        if (sigs[i].tx_idx < n_ids) pi[t][i / per].add(32ull * sigs[i].tx_idx, 32, 32ull * n_ids);
         if (sigs[i].key_idx < n_keys) ++cnt[sigs[i].key_idx];
       }
     };
@@ -956,7 +972,10 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
       for (auto& t : th) t.join();
     }
     for (uint64_t t = 0; t < nt; ++t)
-      for (uint64_t k = 0; k < nch; ++k) ext[k].merge(pe[t][k]);
+      for (uint64_t k = 0; k < nch; ++k) {
+        ext[k].merge(pe[t][k]);
+        idx[k].merge(pi[t][k]);
+      }
   }
   win = head;
   for (const Extent& e : ext) win.merge(e);
@@ -986,17 +1005,20 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   if (n_keys)
     HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, c->copy), "H2D keys");
   HIP_TRY(copy_missing(have, head, arena, dwin, win.lo, c->copy), "H2D key / template bytes");
-  if (n_ids) HIP_TRY(hipMemcpyAsync(c->h_ids.p, ids, 32 * n_ids, hipMemcpyHostToDevice, c->copy), "H2D ids");
+  std::vector<std::pair<uint64_t, uint64_t>> have_ids;  // id bytes already resident
   HIP_TRY(hipMemcpyAsync(c->aux1.p, counts.data(), sizeof(uint32_t) * counts.size(), hipMemcpyHostToDevice, c->copy),
           "H2D key use counts");
   HIP_TRY(hipEventRecord(c->seg[nch], c->copy), "hipEventRecord");
   HIP_TRY(hipStreamWaitEvent(s, c->seg[nch], 0), "hipStreamWaitEvent");
   hipError_t copy_err = hipSuccess;
-  // chunk k: its slice of the signature table, then its signature bytes
+  // chunk k: its slice of the signature table, the ids it references not yet resident (a caller that
+  // lists each transaction's signatures together ships each id once, with its first chunk), then its
+  // signature bytes
   const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t first,
                                                                               uint64_t cnt) {
     hipError_t e = hipMemcpyAsync((cg_txsig*)c->h_sigs.p + first, sigs + first, sizeof(cg_txsig) * cnt,
                                   hipMemcpyHostToDevice, c->copy);
+    if (e == hipSuccess) e = copy_missing(have_ids, idx[k], ids, (uint8_t*)c->h_ids.p, 0, c->copy);
     if (e == hipSuccess) e = copy_missing(have, ext[k], arena, dwin, win.lo, c->copy);
     if (e == hipSuccess) e = hipEventRecord(c->seg[k], c->copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, c->seg[k], 0);
@@ -1010,7 +1032,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   uses.n = n_sigs;
   const hipError_t le = launch_txsig(c, (const cg_key*)c->keys.p, n_keys, (const uint8_t*)c->h_ids.p, n_ids,
                                      (const cg_txsig*)c->h_sigs.p, n_sigs, tmpls, n_tmpls, dbase, arena_len, mode, ds,
-                                     s, slot, uses, &before);
+                                     s, slot, uses, &before, per);
   if (copy_err != hipSuccess) return hip_fail(copy_err, "H2D signature bytes");
   HIP_TRY(le, "launch_txsig");
   HIP_TRY(hipEventRecord(c->tev[2], s), "hipEventRecord");

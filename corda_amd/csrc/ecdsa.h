@@ -203,6 +203,65 @@ CG_HD void jac_madd(Jac& r, const Jac& p, const f29& x2, const f29& y2, const Ec
   r = o;
 }
 
+// r = 2p with fewer carry chains (the ladders' doublings; p finite or Z = 0, reduced coordinates):
+// X - delta and the Y3 / a = 0 D - X3 factors are semi-reduced (m29_sub2), used only as products'
+// operands; secp256r1's Z3 = 2 Y Z is one product instead of (Y + Z)^2 - gamma - delta. Same point
+// as jac_dbl.
+template <int C>
+CG_HD void jac_dbl_w(Jac& r, const Jac& p) {
+  f29 t1, t2, t3, X3, Y3, Z3;
+  if (C == CG_CURVE_R1) {  // a = -3 : dbl-2001-b
+    f29 delta, gamma, beta, alpha;
+    m29_sq<C, 0>(delta, p.Z);
+    m29_sq<C, 0>(gamma, p.Y);
+    m29_mul<C, 0>(beta, p.X, gamma);
+    m29_sub2<C, 0>(t1, p.X, delta);   // < 4m
+    m29_add_lazy(t2, p.X, delta);     // < 4m
+    m29_mul<C, 0>(alpha, t1, t2);
+    m29_add<C, 0>(t1, alpha, alpha);
+    m29_add<C, 0>(alpha, alpha, t1);  // 3 (X - delta)(X + delta)
+    m29_sq<C, 0>(X3, alpha);
+    m29_add<C, 0>(t1, beta, beta);
+    m29_add<C, 0>(t1, t1, t1);  // 4 beta
+    m29_add<C, 0>(t2, t1, t1);  // 8 beta
+    m29_sub<C, 0>(X3, X3, t2);
+    m29_add_lazy(t3, p.Z, p.Z);       // 2Z < 4m
+    m29_mul<C, 0>(Z3, p.Y, t3);       // 2 Y Z
+    m29_sub2<C, 0>(t1, t1, X3);       // 4 beta - X3, < 4m
+    m29_mul<C, 0>(Y3, alpha, t1);
+    m29_add_lazy(t3, gamma, gamma);
+    m29_sq<C, 0>(t2, t3);      // 4 gamma^2
+    m29_add<C, 0>(t2, t2, t2);  // 8 gamma^2
+    m29_sub<C, 0>(Y3, Y3, t2);
+  } else {  // a = 0 : dbl-2009-l
+    f29 A, B, Cc, D, E, F;
+    m29_sq<C, 0>(A, p.X);
+    m29_sq<C, 0>(B, p.Y);
+    m29_sq<C, 0>(Cc, B);
+    m29_add_lazy(t1, p.X, B);
+    m29_sq<C, 0>(t1, t1);
+    m29_sub<C, 0>(t1, t1, A);
+    m29_sub<C, 0>(t1, t1, Cc);
+    m29_add<C, 0>(D, t1, t1);
+    m29_add<C, 0>(E, A, A);
+    m29_add<C, 0>(E, E, A);
+    m29_sq<C, 0>(F, E);
+    m29_add<C, 0>(t2, D, D);
+    m29_sub<C, 0>(X3, F, t2);
+    m29_sub2<C, 0>(t3, D, X3);        // < 4m
+    m29_mul<C, 0>(Y3, E, t3);
+    m29_add<C, 0>(t2, Cc, Cc);
+    m29_add<C, 0>(t2, t2, t2);
+    m29_add<C, 0>(t2, t2, t2);  // 8 C
+    m29_sub<C, 0>(Y3, Y3, t2);
+    m29_add_lazy(t3, p.Y, p.Y);
+    m29_mul<C, 0>(Z3, t3, p.Z);
+  }
+  r.X = X3;
+  r.Y = Y3;
+  r.Z = Z3;
+}
+
 // r = p + (x2, +-y2) affine for the wide ladder: madd-2007-bl with fewer carry chains.
 //  * `inf` flags p = infinity (the ladder's start, or an exceptional P + (-P)) instead of testing Z;
 //  * the sign rides on S2 = +-y2 Z1^3 (m29_neg2: one chain);

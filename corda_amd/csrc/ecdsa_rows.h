@@ -620,7 +620,7 @@ CG_HD void m29_batch_invert_small(f29* out, const f29* t, const EcConsts& K) {
 
 // u1 G over the constant radix-2^EC_WIDE_GW table (no doublings needed: added after the Q part)
 template <int C, class TabG>
-CG_HD void ec_add_g_wide(Jac& R, const u256w& u1, const TabG& TG, const EcConsts& K) {
+CG_HD void ec_add_g_wide(Jac& R, bool& inf, const u256w& u1, const TabG& TG, const EcConsts& K) {
   uint32_t dg[EC_WIDE_GPACKED];
   ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS, false, EC_WIDE_GBITS>(dg, u1);
 #pragma unroll 1
@@ -629,8 +629,7 @@ CG_HD void ec_add_g_wide(Jac& R, const u256w& u1, const TabG& TG, const EcConsts
     if (a != 0) {
       f29 x, y;
       ec_pick(x, y, TG.t[u], a < 0 ? -a : a);
-      if (a < 0) m29_neg<C, 0>(y, y);
-      jac_madd<C>(R, R, x, y, K);
+      jac_madd_w<C>(R, inf, x, y, a < 0, K);
     }
   }
 }
@@ -645,10 +644,11 @@ CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w&
   ec_recode_w6(dq, u2);
   Jac R;
   jac_set_inf<C>(R, K);
+  bool inf = true;  // R = infinity: doublings skipped, the next addition loads the point
   for (int i = EC_WINDOWS - 1; i >= 0; --i) {
-    if (i != EC_WINDOWS - 1) {
+    if (i != EC_WINDOWS - 1 && !inf) {
 #pragma unroll 1
-      for (int d = 0; d < EC_W; ++d) jac_dbl<C>(R, R);
+      for (int d = 0; d < EC_W; ++d) jac_dbl_w<C>(R, R);
     }
 #pragma unroll 1
     for (int j = 0; j < EC_ROWS; ++j) {
@@ -658,12 +658,11 @@ CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w&
       if (b != 0) {
         f29 x, y;
         ec_pick(x, y, TQ.t[j], b < 0 ? -b : b);
-        if (b < 0) m29_neg<C, 0>(y, y);
-        jac_madd<C>(R, R, x, y, K);
+        jac_madd_w<C>(R, inf, x, y, b < 0, K);
       }
     }
   }
-  ec_add_g_wide<C>(R, u1, TG, K);
+  ec_add_g_wide<C>(R, inf, u1, TG, K);
   return ecdsa_x_check<C>(R, r, K);
 }
 
@@ -676,21 +675,21 @@ CG_HD uint32_t ecdsa_ladder_check_row0(const u256w& u1, const u256w& u2, const u
   ec_recode_w6(dq, u2);
   Jac R;
   jac_set_inf<C>(R, K);
+  bool inf = true;
 #pragma unroll 1
   for (int t = EC_DIGITS - 1; t >= 0; --t) {
-    if (t != EC_DIGITS - 1) {
+    if (t != EC_DIGITS - 1 && !inf) {
 #pragma unroll 1
-      for (int d = 0; d < EC_W; ++d) jac_dbl<C>(R, R);
+      for (int d = 0; d < EC_W; ++d) jac_dbl_w<C>(R, R);
     }
     const int b = ec_digit6(dq, t);
     if (b != 0) {
       f29 x, y;
       ec_pick(x, y, row0, b < 0 ? -b : b);
-      if (b < 0) m29_neg<C, 0>(y, y);
-      jac_madd<C>(R, R, x, y, K);
+      jac_madd_w<C>(R, inf, x, y, b < 0, K);
     }
   }
-  ec_add_g_wide<C>(R, u1, TG, K);
+  ec_add_g_wide<C>(R, inf, u1, TG, K);
   return ecdsa_x_check<C>(R, r, K);
 }
 

@@ -173,29 +173,69 @@ __global__ void __launch_bounds__(PART_B) k_tx_leaf_scatter(const cg_component* 
   part_scatter<TX_LEAF_CLASSES>(ci < n_comps ? tx_leaf_class(map, comps, ci) : -1, (uint32_t)ci, boff, perm);
 }
 
+// Message word j (big-endian) of block `blk` of blob || suffix || padding, the blob's bytes of this
+// block given as 17 aligned dwords W (W[0] at the blob's 4-aligned base + 64 blk) realigned by sh8.
+__device__ __forceinline__ uint32_t tx_block_word(const uint32_t* W, int j, uint32_t sh8, uint64_t blk, uint64_t len,
+                                                  uint64_t n, const uint32_t* suffix_be) {
+  const uint64_t pos = blk * 64 + (uint64_t)j * 4;
+  const uint32_t raw = __builtin_amdgcn_alignbit(W[j + 1], W[j], sh8);  // blob bytes pos .. pos + 3
+  if (pos + 4 <= len) return __builtin_bswap32(raw);
+  if (suffix_be && (len & 3) == 0 && pos >= len && pos + 4 <= n) return suffix_be[(pos - len) >> 2];
+  if (pos > n) return 0u;
+  uint32_t acc = 0;
+  for (int bb = 0; bb < 4; ++bb) {
+    const uint64_t q = pos + (uint64_t)bb;
+    uint32_t byte;
+    if (q < len) {
+      byte = (raw >> (8 * bb)) & 0xffu;
+    } else if (q < n) {
+      const uint64_t r = q - len;
+      byte = (suffix_be[r >> 2] >> (24 - 8 * (r & 3))) & 0xffu;
+    } else {
+      byte = q == n ? 0x80u : 0u;
+    }
+    acc = (acc << 8) | byte;
+  }
+  return acc;
+}
+
+// One lane per component (perm order: a wave's 64 components have the same block count), the
+// blob's bytes staged wave-cooperatively through LDS: for each 64-byte block, 17 consecutive lanes
+// load one component's 68 aligned bytes (coalesced runs instead of 64 scattered 16-byte loads per
+// instruction: round 2 moved ~4x the component bytes, profiles/r02/tx_v4), then every lane reads
+// its own 17 dwords back (stride 17: no bank conflicts).
+#define TX_LDS_DW 17
 __global__ void __launch_bounds__(256) k_tx_leaves(const cg_tx* __restrict__ txs, const cg_component* __restrict__ comps,
                                                    const uint32_t* __restrict__ perm,
                                                    const uint32_t* __restrict__ ranges,
                                                    const uint32_t* __restrict__ map,
                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                    uint8_t* __restrict__ status, uint8_t* __restrict__ ws) {
+  __shared__ uint32_t stage[4][64 * TX_LDS_DW];
+  __shared__ uint64_t sbase[4][64];
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= ranges[TX_LEAF_CLASSES]) return;
-  const uint32_t ci = perm[p];
-  const uint32_t t = map[ci];
-  const cg_tx tx = txs[t];
-  const cg_component c = comps[ci];
+  const uint64_t total = ranges[TX_LEAF_CLASSES];
+  if ((p & ~(uint64_t)63) >= total) return;  // the whole wave is past the end
+  const bool live = p < total;
   const uint64_t lr = r4(arena_len);
-  uint32_t leaf[8];
-  if (c.off > arena_len || c.len > arena_len - c.off) {
-    status[t] = 2;
-    for (int k = 0; k < 8; ++k) leaf[k] = 0;
-  } else if (c.flags & 1u) {
-    sha256_arena_suffix(leaf, arena, lr, c.off, c.len, nullptr);
-  } else {
-    // nonce = SHA256(salt || BE32(i)) : 36 bytes, one block
-    uint32_t s[8], w[16], nonce[8];
-    sha256_init(s);
+  uint32_t ci = 0, t = 0;
+  cg_component c = {0, 0, 0};
+  cg_tx tx = {0, 0, 0, 0};
+  bool inside = false;
+  if (live) {
+    ci = perm[p];
+    t = map[ci];
+    tx = txs[t];
+    c = comps[ci];
+    inside = !(c.off > arena_len || c.len > arena_len - c.off);
+    if (!inside) status[t] = 2;
+  }
+  const bool salt = (c.flags & 1u) != 0;
+  uint32_t nonce[8];
+  if (live && inside && !salt) {  // nonce = SHA256(salt || BE32(i)) : 36 bytes, one block
+    uint32_t s8[8], w[16];
+    sha256_init(s8);
 #pragma unroll
     for (int k = 0; k < 8; ++k) w[k] = __builtin_bswap32(cg_ld_bytes4(arena, lr, tx.salt_off + 4 * k));
     w[8] = (uint32_t)(ci - tx.first);
@@ -203,12 +243,55 @@ __global__ void __launch_bounds__(256) k_tx_leaves(const cg_tx* __restrict__ txs
 #pragma unroll
     for (int k = 10; k < 15; ++k) w[k] = 0;
     w[15] = 36 * 8;
-    sha256_compress(s, w);
+    sha256_compress(s8, w);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) nonce[k] = s[k];
-    sha256_arena_suffix(leaf, arena, lr, c.off, c.len, nonce);
+    for (int k = 0; k < 8; ++k) nonce[k] = s8[k];
   }
-  st_node(ws, ci, leaf);
+  const uint64_t len = live && inside ? c.len : 0;
+  const uint64_t n = len + (salt ? 0 : 32);
+  const uint32_t nbl = live && inside ? (uint32_t)((n + 9 + 63) >> 6) : 0u;
+  uint32_t mbl = nbl;  // the wave's largest block count
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t x = (uint32_t)__shfl_xor((int)mbl, o, 64);
+    mbl = x > mbl ? x : mbl;
+  }
+  sbase[wid][lane] = live && inside ? (c.off & ~(uint64_t)3) : ~(uint64_t)0;
+  const uint32_t sh8 = (uint32_t)(c.off & 3) * 8u;
+  uint32_t h[8];
+  sha256_init(h);
+  uint32_t* st = stage[wid];
+  for (uint32_t blk = 0; blk < mbl; ++blk) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous block's reads (and sbase) are done
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < TX_LDS_DW; ++k) {
+      const uint32_t task = lane + 64u * k, cc = task / TX_LDS_DW, d = task % TX_LDS_DW;
+      const uint64_t base = sbase[wid][cc];
+      const uint64_t addr = base + 64ull * blk + 4ull * d;
+      st[task] = base != ~(uint64_t)0 && addr + 4 <= lr ? *(const uint32_t*)(arena + addr) : 0u;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (blk < nbl) {
+      uint32_t W[TX_LDS_DW], w[16];
+#pragma unroll
+      for (int d = 0; d < TX_LDS_DW; ++d) W[d] = st[lane * TX_LDS_DW + d];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = tx_block_word(W, j, sh8, blk, len, n, salt ? nullptr : nonce);
+      if (blk + 1 == nbl) {
+        w[14] = (uint32_t)((n * 8) >> 32);
+        w[15] = (uint32_t)(n * 8);
+      }
+      sha256_compress(h, w);
+    }
+  }
+  if (!live) return;
+  if (!inside) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = 0;
+  }
+  st_node(ws, ci, h);
 }
 
 __global__ void __launch_bounds__(256) k_tx_roots(const cg_tx* __restrict__ txs, uint64_t n_tx,

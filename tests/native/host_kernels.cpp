@@ -784,6 +784,15 @@ static int madd_w_cmp(uint64_t seed, int n) {
     jac_madd<C>(ref, ref, K.gx, y2, K);
     jac_madd_w<C>(got, inf, K.gx, K.gy, false, K);
     if (!same(got, inf, ref)) ++bad;
+    // doublings: jac_dbl_w against jac_dbl, twice (the second on a semi-lazy-built input)
+    if (!inf) {
+      Jac d1 = got, d2 = got;
+      jac_dbl<C>(d1, d1);
+      jac_dbl<C>(d1, d1);
+      jac_dbl_w<C>(d2, d2);
+      jac_dbl_w<C>(d2, d2);
+      if (!same(d2, false, d1)) ++bad;
+    }
   }
   return bad;
 }

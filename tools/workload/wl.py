@@ -194,14 +194,24 @@ def notary_pool(n_unique, ed_keys=4096, ec_keys=1024, msg_len=270, seed=9, nthre
     return b, np.concatenate(labs)[perm], np.concatenate(sch)[perm]
 
 
-def index_stream(pool, n_items, seed=10, replicate=False):
+def tx_ordered_draws(pool_n, n_items, id_idx, seed):
+    """The index stream's draws (as index_stream draws them), reordered so that within each pass over
+    the pool (draw i belongs to copy i // pool_n) the signatures of one transaction id are adjacent:
+    the layout a caller of cg_verify_tx_signatures produces when it lists each transaction's
+    signatures together (TransactionWithSignatures.checkSignaturesAreValid walks one tx at a time)."""
+    idx = np.random.default_rng(seed).integers(0, pool_n, n_items)
+    copy = np.arange(n_items, dtype=np.int64) // pool_n
+    return idx[np.lexsort((id_idx[idx], copy))]
+
+
+def index_stream(pool, n_items, seed=10, replicate=False, idx=None):
     """n_items items drawn from `pool` by a seeded index stream (the engine sees every draw as
     its own item: nothing is deduplicated). replicate=False: the items point into the pool's
     arena. replicate=True: the arena holds one physical copy of the pool per 2^k draws, item i
     pointing into copy i // len(pool), so every item has its own bytes and a host-buffer call
     moves ~370 B per item over PCIe, as a real notary batch would. Returns (Batch, pool_index)."""
-    rng = np.random.default_rng(seed)
-    idx = rng.integers(0, pool.n, n_items)
+    if idx is None:
+        idx = np.random.default_rng(seed).integers(0, pool.n, n_items)
     items = pool.items[idx]
     arena = pool.arena
     if replicate:

@@ -187,13 +187,47 @@ def cpu_baseline(batch, st_gpu, seconds, threads):
     t = time.perf_counter()
     c_oracle.verify_batch(sub1, 0, 1)
     dt1 = time.perf_counter() - t
+    ossl = openssl_items(sub, st, threads)
     return {"value": round(n / dt, 1), "unit": "sigs/s", "cores": threads, "kind": "port",
             "sample": f"first {n} items of the rank-0 headline batch (70/20/10 mix; incl. decoding all "
                       f"{len(batch.keys)} keys), oracle/c or_verify_batch over {threads} threads, {dt:.1f} s",
             "host": f"{cpu_model()}; CPU quota {threads} CPUs (cgroup cpu.max) of {os.cpu_count()} hardware threads",
             "serial_1thread": {"value": round(n1 / dt1, 1), "items": n1, "seconds": round(dt1, 2)},
             "parity_on_sample": bool(np.array_equal(st, st_gpu[:n])),
+            "openssl": ossl,
             "jvm": "JVM reference unavailable: no JDK, no i2p / BouncyCastle jars, no network"}
+
+
+def openssl_items(sub, st_port, threads):
+    """OpenSSL 3 EVP_DigestVerify on the same headline sample (Ed25519 + both ECDSA curves, a fresh
+    EVP_PKEY per item), on the CPU quota and on one thread: an industrial CPU point beside the port.
+    Its verdicts differ from the reference's where i2p 0.2.0 does (S >= L accepted by i2p)."""
+    import ctypes
+    so = os.path.join(ROOT, "tools", "cpu_baseline", "libosslcheck.so")
+    if not os.path.exists(so):
+        return "absent: tools/cpu_baseline not built"
+    O = ctypes.CDLL(so)
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    O.ob_verify_items.argtypes = [vp, u32, vp, u64, vp, u64, vp, i32]
+    O.ob_verify_items.restype = ctypes.c_int64
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    st = np.zeros(sub.n, np.uint8)
+    t = time.perf_counter()
+    if O.ob_verify_items(p(sub.keys), len(sub.keys), p(sub.items), sub.n, p(sub.arena), sub.arena.size, p(st),
+                         threads) < 0:
+        return "absent: libcrypto.so.3 could not be loaded"
+    dt = time.perf_counter() - t
+    n1 = max(64, sub.n // threads // 2)
+    st1 = np.zeros(n1, np.uint8)
+    t = time.perf_counter()
+    O.ob_verify_items(p(sub.keys), len(sub.keys), p(sub.items[:n1]), n1, p(sub.arena), sub.arena.size, p(st1), 1)
+    dt1 = time.perf_counter() - t
+    valid_port = st_port == 0
+    return {"value": round(sub.n / dt, 1), "unit": "sigs/s", "threads": threads, "items": int(sub.n),
+            "value_1thread": round(n1 / dt1, 1),
+            "valid_verdicts_differing_from_port": int(np.count_nonzero((st == 0) != valid_port)),
+            "note": "OpenSSL 3.0.2 EVP_DigestVerify per item (Ed25519 raw keys; ECDSA raw X||Y wrapped in the "
+                    "curve's SPKI); rejects Ed25519 S >= L, which i2p 0.2.0 accepts"}
 
 
 def configs0(a, eng, wl, threads):
@@ -297,6 +331,17 @@ def stage_summary(times, steps_per_read):
             out[name] = {"ms_per_step": round(ms / steps_per_read, 3), "launches": int(n),
                          "ms_per_launch": round(ms / n, 3)}
     return out
+
+
+def headline_chunk(a, n):
+    """Items per verify chunk of the headline call: cg_verify_tx_signatures splits a large host call
+    into at least 4 chunks unless the caller sets cg_config.chunk_items (cordagpu.cpp)."""
+    chunk = eng_chunk(a)
+    k = max(1, -(-n // chunk))
+    per = -(-n // k)
+    if not a.chunk_items and n >= 4 * (1 << 20):
+        per = min(per, -(-n // 4))
+    return per
 
 
 def ladder_units(b, labels, schemes, chunk):
@@ -690,7 +735,7 @@ def main():
     per_pool[idx] = st
     ver["draws_consistent"] = bool(np.array_equal(per_pool[idx], st))
 
-    units = ladder_units(batch, labels, schemes, eng_chunk(a))
+    units = ladder_units(batch, labels, schemes, headline_chunk(a, batch.n))
     roof, ec_roof = roofline(stages, units, a.steps)
     if roof is not None:
         roof["i2p_equiv_TMAC32"] = round(roof["achieved"] * MAC32_PER_ED25519 / roof["work_per_item"], 3)
@@ -709,7 +754,10 @@ def main():
              "headline_h2d": {"bytes_per_call": h2d_bytes, "bytes_per_sig": round(h2d_bytes / tb.n, 1),
                               "GBps_effective": round(h2d_bytes * a.steps / elapsed / 1e9, 1),
                               "cg_stats_ms_mean": {k: round(float(np.mean([c[k] for c in cg_ms])), 3)
-                                                   for k in ("ms_h2d", "ms_verify", "ms_d2h", "ms_total")}}}
+                                                   for k in ("ms_key_prep", "ms_h2d", "ms_verify", "ms_d2h",
+                                                             "ms_total")},
+                              "note": "ms_key_prep = host-side planning (the key-use sample pass), ms_h2d = until "
+                                      "the first chunk's bytes are resident, ms_verify = the rest"}}
     if rank == 0 and world == 1 and a.device_steps > 0:
         extra["device_resident"] = bench_device(eng, dev, stream, batch, tb, st, a.device_steps)
     if rank == 0 and world == 1 and a.host_steps > 0:
@@ -756,7 +804,7 @@ def main():
                        "items_per_gpu": a.items, "unique_pool": a.pool, "mix": {"ed25519": n_ed, "secp256r1": n_r1,
                                                                               "secp256k1": a.items - n_ed - n_r1},
                        "keys": len(batch.keys), "tx_ids_per_gpu": int(tb.n_ids), "h2d_bytes_per_gpu": h2d_bytes,
-                       "device_chunk_items": eng_chunk(a),
+                       "device_chunk_items": headline_chunk(a, batch.n),
                        "parallelism": f"shard{world}" + ("+rccl_allgather(verdicts)" if world > 1 else "")},
             "roofline": roof, "cpu_baseline": cpu, "secondary": extra, "verdicts": ver,
             "gen_s": round(gen_s, 1),

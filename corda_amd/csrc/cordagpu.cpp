@@ -164,7 +164,7 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
                           const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, hipStream_t s,
                           const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0,
                           const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* prepare = nullptr,
-                          const cg::KeyUses* uses = nullptr, uint64_t per_items = 0) {
+                          const cg::KeyUses* uses = nullptr, const std::vector<uint64_t>* bounds = nullptr) {
   // prepare (the tx-signature entry points): called with (k, first item, items) just before chunk
   // k's front is enqueued; it makes chunk k's verify items (and, host form, its bytes) and orders
   // `s` after them. The key tables are then sized from `uses` and start building at once, before
@@ -173,25 +173,34 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   const cg::WidePool wp = wide_for(c, n_keys, n_items);
   hipError_t e = cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork,
                                     uses ? nullptr : d_items, n_items, &wp, uses);
-  const uint64_t per = per_items ? per_items : chunk_of(c, n_items);
-  const uint64_t nch = (n_items + per - 1) / per;
+  // chunk k = items [at(k), at(k) + cnt(k)): the caller's bounds (bounds[0] = 0, bounds[nch] = n),
+  // else equal chunks of chunk_of(c, n) items; `per` (the largest chunk) sizes the item workspaces
+  uint64_t per = chunk_of(c, n_items);
+  uint64_t nch = (n_items + per - 1) / per;
+  if (bounds) {
+    nch = bounds->size() - 1;
+    per = 0;
+    for (uint64_t k = 0; k < nch; ++k) per = std::max(per, (*bounds)[k + 1] - (*bounds)[k]);
+  }
+  auto at = [&](uint64_t k) { return bounds ? (*bounds)[k] : k * per; };
+  auto cnt = [&](uint64_t k) {
+    return bounds ? (*bounds)[k + 1] - (*bounds)[k] : (per < n_items - k * per ? per : n_items - k * per);
+  };
   // chunk k's item workspace: half k % 2 when the buffer holds two (ensure_ws), else the one
   const bool two = nch > 1 && c->itemws.cap >= 2 * item_half_bytes(per);
   auto ws = [&](uint64_t k) { return (void*)((uint8_t*)c->itemws.p + (two ? (k & 1) * item_half_bytes(per) : 0)); };
-  auto cnt = [&](uint64_t k) { return per < n_items - k * per ? per : n_items - k * per; };
   auto plan = [&](uint64_t k) {
-    return cg::launch_items_plan(d_keys, n_keys, d_items + k * per, cnt(k), d_status + k * per, c->keyprep.p, ws(k),
-                                 s, &c->fork, &wp);
+    return cg::launch_items_plan(d_keys, n_keys, d_items + at(k), cnt(k), d_status + at(k), c->keyprep.p, ws(k), s,
+                                 &c->fork, &wp);
   };
   const bool pre_plan = two && !prepare;
   auto front = [&](uint64_t k) {
     if (prepare) {
-      const hipError_t w = (*prepare)(k, k * per, cnt(k));
+      const hipError_t w = (*prepare)(k, at(k), cnt(k));
       if (w != hipSuccess) return w;
     }
-    return cg::launch_items_front(d_keys, n_keys, d_items + k * per, cnt(k), d_arena, arena_len, mode,
-                                  d_status + k * per, c->keyprep.p, ws(k), s, d_msgs, msgs_len, &c->fork, &wp,
-                                  pre_plan && k < 2);
+    return cg::launch_items_front(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, mode, d_status + at(k),
+                                  c->keyprep.p, ws(k), s, d_msgs, msgs_len, &c->fork, &wp, pre_plan && k < 2);
   };
   // chunk k + 1's front (plan, hashes, ECDSA prep) before chunk k's back (ladders): the first
   // chunk's wait for the key tables is spent on the next chunk's fronts. Without a prepare hook the
@@ -205,7 +214,7 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
     if (!two && k > 0) e = front(k);
     if (two && k + 1 < nch && e == hipSuccess) e = front(k + 1);
     if (e == hipSuccess)
-      e = cg::launch_items_back(d_keys, n_keys, d_items + k * per, cnt(k), d_arena, arena_len, d_status + k * per,
+      e = cg::launch_items_back(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, d_status + at(k),
                                 c->keyprep.p, ws(k), c->btab.p, s, &c->fork, &wp);
   }
   return e;
@@ -857,6 +866,7 @@ int cg_verify_transactions(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_
 
 // ---------------------------------------------------------------- signatures over known tx ids
 #define CG_TXSIG_MIN_CHUNKS 4u
+#define CG_TXSIG_COUNT_SAMPLE 8u
 // The spliced-message slot of a template set: the longest prefix || id || suffix, 16-aligned.
 static uint64_t tmpl_slot(const cg_signable_tmpl* tmpls, uint32_t n_tmpls) {
   uint64_t maxlen = 0;
@@ -891,7 +901,7 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
                                uint32_t n_tmpls, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
                                uint8_t* d_status, hipStream_t s, uint64_t slot, const cg::KeyUses& uses,
                                const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* ready,
-                               uint64_t per = 0) {
+                               const std::vector<uint64_t>* bounds = nullptr) {
   if (n_sigs == 0) return hipSuccess;
   hipError_t e = hipSuccess;
   const cg_signable_tmpl* dt = (const cg_signable_tmpl*)c->tmpls.p;
@@ -908,7 +918,7 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
   if (e == hipSuccess)
     e = launch_chunked(c, d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode, d_status, s,
                        (const uint8_t*)c->msgs.p, cg::tx_msgs_head(n_tmpls, slot) + slot * n_sigs, &prepare, &uses,
-                       per);
+                       bounds);
   return e;
 }
 
@@ -932,7 +942,27 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     const uint64_t alt = (n_sigs + CG_TXSIG_MIN_CHUNKS - 1) / CG_TXSIG_MIN_CHUNKS;
     if (alt < per) per = alt;
   }
-  const uint64_t nch = (n_sigs + per - 1) / per;
+  // chunk bounds: equal chunks of `per`; with CG_TXSIG_FIRST_DIV (env, A/B) > 1 the first chunk is
+  // 1/CG_TXSIG_FIRST_DIV of the call and the rest split equally (its copy is the part nothing hides)
+  std::vector<uint64_t> bounds;
+  {
+    static const uint64_t first_div = [] {
+      const char* v = getenv("CG_TXSIG_FIRST_DIV");
+      return v ? (uint64_t)strtoull(v, nullptr, 10) : 0ull;
+    }();
+    const uint64_t k0 = (n_sigs + per - 1) / per;
+    if (first_div > 1 && k0 > 1) {
+      const uint64_t f0 = n_sigs / first_div, rest = n_sigs - f0, kr = k0;
+      bounds.push_back(0);
+      bounds.push_back(f0);
+      for (uint64_t k = 1; k <= kr; ++k) bounds.push_back(f0 + rest * k / kr);
+    } else {
+      for (uint64_t k = 0; k <= k0; ++k) bounds.push_back(k == k0 ? n_sigs : k * per);
+    }
+    per = 0;
+    for (size_t k = 0; k + 1 < bounds.size(); ++k) per = std::max(per, bounds[k + 1] - bounds[k]);
+  }
+  const uint64_t nch = bounds.size() - 1;
   // arena extents: key bytes + template bytes (the header), then each chunk's signature bytes
   Extent head, win;
   for (uint32_t k = 0; k < n_keys; ++k) head.add(keys[k].off, keys[k].len, arena_len);
@@ -940,21 +970,22 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     head.add(tmpls[k].prefix_off, tmpls[k].prefix_len, arena_len);
     head.add(tmpls[k].suffix_off, tmpls[k].suffix_len, arena_len);
   }
-  // one pass over the signature table on up to 16 host threads: each chunk's byte extent, and the
-  // exact per-key use counts (so the key tables need no signature table on the device)
-  std::vector<Extent> ext(nch), idx(nch);  // arena bytes and id bytes each chunk reads
+  // Key-use counts for the table modes from a 1-in-CG_TXSIG_COUNT_SAMPLE sample of the signature
+  // table (16 host threads; the modes change only speed, never a verdict), every key at least 1 so
+  // that each key an unsampled signature may use has its row-0 table. Each chunk's byte extents are
+  // scanned just before its copy, while the device works on the chunks before it.
   std::vector<uint32_t> counts(n_keys ? n_keys : 1, 0u);
+  const uint64_t nt = n_sigs < (1u << 16) ? 1 : 16;
   {
-    const uint64_t nt = n_sigs < (1u << 16) ? 1 : 16;
-    std::vector<std::vector<Extent>> pe(nt, std::vector<Extent>(nch)), pi(nt, std::vector<Extent>(nch));
+    const uint64_t ns = (n_sigs + CG_TXSIG_COUNT_SAMPLE - 1) / CG_TXSIG_COUNT_SAMPLE;
     std::vector<std::vector<uint32_t>> pc(nt > 1 ? nt : 0, std::vector<uint32_t>(n_keys ? n_keys : 1, 0u));
     auto scan = [&](uint64_t t) {
-      const uint64_t a = n_sigs * t / nt, b = n_sigs * (t + 1) / nt;
       uint32_t* cnt = nt > 1 ? pc[t].data() : counts.data();
-      for (uint64_t i = a; i < b; ++i) {
-        pe[t][i / per].add(sigs[i].sig_off, sigs[i].sig_len, arena_len);
-        if (sigs[i].tx_idx < n_ids) pi[t][i / per].add(32ull * sigs[i].tx_idx, 32, 32ull * n_ids);
-        if (sigs[i].key_idx < n_keys) ++cnt[sigs[i].key_idx];
+      for (uint64_t j = ns * t / nt; j < ns * (t + 1) / nt; ++j) {
+        // one record per group of CG_TXSIG_COUNT_SAMPLE, at a hashed position (no aliasing with a
+        // layout that cycles through the keys)
+        const uint64_t i = j * CG_TXSIG_COUNT_SAMPLE + (((uint32_t)j * 0x9E3779B1u) >> 29) % CG_TXSIG_COUNT_SAMPLE;
+        if (i < n_sigs && sigs[i].key_idx < n_keys) cnt[sigs[i].key_idx] += CG_TXSIG_COUNT_SAMPLE;
       }
     };
     if (nt == 1) {
@@ -971,16 +1002,36 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
         });
       for (auto& t : th) t.join();
     }
-    for (uint64_t t = 0; t < nt; ++t)
-      for (uint64_t k = 0; k < nch; ++k) {
-        ext[k].merge(pe[t][k]);
-        idx[k].merge(pi[t][k]);
-      }
+    for (uint32_t k = 0; k < n_keys; ++k)
+      if (counts[k] == 0) counts[k] = 1;
   }
-  win = head;
-  for (const Extent& e : ext) win.merge(e);
-  if (win.empty()) win.lo = win.hi = 0;
-  win.lo &= ~(uint64_t)15;  // the device window starts 16-aligned (kernels load aligned words)
+  const double ms_plan = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  // chunk k's signature bytes and id bytes (exact: a threaded scan of its slice of the table)
+  auto chunk_extents = [&](uint64_t k, Extent& ext, Extent& idx) {
+    const uint64_t f = bounds[k], e = bounds[k + 1];
+    const uint64_t m = (e - f) < (1u << 16) ? 1 : nt;
+    std::vector<Extent> pe(m), pi(m);
+    auto scan = [&](uint64_t t) {
+      for (uint64_t i = f + (e - f) * t / m; i < f + (e - f) * (t + 1) / m; ++i) {
+        pe[t].add(sigs[i].sig_off, sigs[i].sig_len, arena_len);
+        if (sigs[i].tx_idx < n_ids) pi[t].add(32ull * sigs[i].tx_idx, 32, 32ull * n_ids);
+      }
+    };
+    if (m == 1) {
+      scan(0);
+    } else {
+      std::vector<std::thread> th;
+      for (uint64_t t = 0; t < m; ++t) th.emplace_back(scan, t);
+      for (auto& t : th) t.join();
+    }
+    for (uint64_t t = 0; t < m; ++t) {
+      ext.merge(pe[t]);
+      idx.merge(pi[t]);
+    }
+  };
+  // the device arena mirrors [0, arena_len) (only referenced bytes are copied)
+  win.lo = 0;
+  win.hi = arena_len;
   const uint64_t slot = tmpl_slot(tmpls, n_tmpls);
   HIP_TRY(c->keys.ensure(sizeof(cg_key) * (n_keys ? n_keys : 1)), "hipMalloc(keys)");
   HIP_TRY(c->h_sigs.ensure(sizeof(cg_txsig) * n_sigs), "hipMalloc(sigs)");
@@ -1016,10 +1067,12 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   // signature bytes
   const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t first,
                                                                               uint64_t cnt) {
+    Extent ek, ik;
+    chunk_extents(k, ek, ik);
     hipError_t e = hipMemcpyAsync((cg_txsig*)c->h_sigs.p + first, sigs + first, sizeof(cg_txsig) * cnt,
                                   hipMemcpyHostToDevice, c->copy);
-    if (e == hipSuccess) e = copy_missing(have_ids, idx[k], ids, (uint8_t*)c->h_ids.p, 0, c->copy);
-    if (e == hipSuccess) e = copy_missing(have, ext[k], arena, dwin, win.lo, c->copy);
+    if (e == hipSuccess) e = copy_missing(have_ids, ik, ids, (uint8_t*)c->h_ids.p, 0, c->copy);
+    if (e == hipSuccess) e = copy_missing(have, ek, arena, dwin, win.lo, c->copy);
     if (e == hipSuccess) e = hipEventRecord(c->seg[k], c->copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, c->seg[k], 0);
     if (e == hipSuccess && k == 0) e = hipEventRecord(c->tev[1], s);
@@ -1032,7 +1085,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   uses.n = n_sigs;
   const hipError_t le = launch_txsig(c, (const cg_key*)c->keys.p, n_keys, (const uint8_t*)c->h_ids.p, n_ids,
                                      (const cg_txsig*)c->h_sigs.p, n_sigs, tmpls, n_tmpls, dbase, arena_len, mode, ds,
-                                     s, slot, uses, &before, per);
+                                     s, slot, uses, &before, &bounds);
   if (copy_err != hipSuccess) return hip_fail(copy_err, "H2D signature bytes");
   HIP_TRY(le, "launch_txsig");
   HIP_TRY(hipEventRecord(c->tev[2], s), "hipEventRecord");
@@ -1048,7 +1101,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     stats->n_items = n_sigs;
     stats->n_keys = n_keys;
     stats->ms_h2d = a;
-    stats->ms_key_prep = 0;
+    stats->ms_key_prep = ms_plan;  // host-side planning: the key-use sample pass
     stats->ms_verify = b;
     stats->ms_d2h = d;
     stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

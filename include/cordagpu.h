@@ -300,10 +300,12 @@ int cg_verify_transactions(cg_ctx* ctx, const cg_tx* txs, uint64_t n_tx, const c
  * device. cg_txsig.tx_idx indexes `ids` (32 * n_ids bytes), tmpl indexes `tmpls`. A signature
  * whose id or template index is out of range, or whose template lies outside the arena, gets
  * CG_NOT_RUN; every other status as cg_verify_batch.
- * Host form: the key table, key and template bytes, ids and signature table are copied first
- * (the key tables build from them), then each verify chunk's signature bytes just before the
+ * Host form: the key table, key and template bytes and the sampled key-use counts are copied
+ * first (the key tables build from them), then each verify chunk's slice of the signature table,
+ * the ids it references that are not resident yet, and its signature bytes, just before the
  * chunk runs, overlapping the key-table builds and the previous chunk's kernels. stats: ms_h2d =
- * until the first chunk's bytes are resident, ms_verify = the rest. */
+ * until the first chunk's bytes are resident, ms_verify = the rest, ms_key_prep = the host-side
+ * planning before the first copy (a 1-in-8 sample of the signature table for the key-table modes). */
 int cg_verify_tx_signatures(cg_ctx* ctx, const cg_key* keys, uint32_t n_keys, const uint8_t* ids, uint64_t n_ids,
                             const cg_txsig* sigs, uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,
                             const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,

@@ -95,6 +95,9 @@ EC_LABEL_EXPECT = {0: 0, 1: 1, 2: 0, 3: 1, 6: 2, 7: 2}  # E5 (pad byte) is minim
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--pool-devices", default="",
+                    help="one process drives several devices through cg_pool_verify_tx_signatures (comma-separated "
+                         "device ordinals, a device may repeat; weak scaling: --items per slot). Off: the torchrun form")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--items", type=int, default=12_500_000, help="items per GPU (configs[4]: 100M / 8)")
@@ -662,8 +665,49 @@ def bench_host(eng, b, st_dev, steps):
             "path": "cg_verify_batch from pageable host memory, SignableData bytes materialised per signature"}
 
 
+def main_pool(a):
+    """The library's own multi-device form (one JVM process drives every GPU of the
+    node): cg_pool_verify_tx_signatures over the slots in --pool-devices, contiguous equal shards of
+    one signature table (--items per slot), each slot's H2D, verify and D2H on its own host thread.
+    Prints the same JSON line; `value` = all slots' signatures / call time."""
+    from corda_amd import signable
+    from corda_amd.engine import EnginePool
+    from tools.workload import wl
+    devices = [int(x) for x in a.pool_devices.split(",") if x != ""]
+    threads = host_threads(a.threads)
+    n = a.items * len(devices)
+    t0 = time.time()
+    pool, pl, ps = wl.notary_pool(a.pool, ed_keys=a.ed_keys, ec_keys=a.ec_keys, msg_len=a.msg_len, seed=a.seed,
+                                  nthreads=threads, sig_group=a.sigs_per_tx)
+    ids, id_idx = wl.pool_ids(pool, len(signable.template(1, 4)[0]))
+    idx = wl.tx_ordered_draws(pool.n, n, id_idx, seed=a.seed + 1)
+    tb = wl.tx_sig_stream(pool, ps, idx, ids, id_idx, nthreads=threads)
+    gen_s = time.time() - t0
+    with EnginePool(devices, chunk_items=a.chunk_items) as ep:
+        for _ in range(a.warmup):
+            st = ep.verify_tx_signatures(tb)
+        t = time.perf_counter()
+        for _ in range(a.steps):
+            st = ep.verify_tx_signatures(tb)
+        el = (time.perf_counter() - t) / a.steps
+        stats = dict(ep.last_stats)
+    ver = check_verdicts(st, expected_verdicts(pl[idx], ps[idx]))
+    line = {"metric": METRIC, "value": round(n / el, 1), "unit": "sigs/s", "n_gpus": len(set(devices)),
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic (as the headline)",
+            "config": {"workload": f"BASELINE configs[4], whole node from one process: {a.items} signatures per slot "
+                                   f"over slots {devices} through cg_pool_verify_tx_signatures",
+                       "items": n, "parallelism": f"cg_pool{len(devices)}"},
+            "pool_stats": stats, "verdicts": ver, "gen_s": round(gen_s, 1)}
+    print(json.dumps(line), flush=True)
+    if ver["label_mismatches"] or ver["not_run"]:
+        sys.exit(3)
+
+
 def main():
     a = parse()
+    if a.pool_devices:
+        return main_pool(a)
     import torch
     import torch.distributed as dist
 

@@ -164,7 +164,8 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
                           const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status, hipStream_t s,
                           const uint8_t* d_msgs = nullptr, uint64_t msgs_len = 0,
                           const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* prepare = nullptr,
-                          const cg::KeyUses* uses = nullptr, const std::vector<uint64_t>* bounds = nullptr) {
+                          const cg::KeyUses* uses = nullptr, const std::vector<uint64_t>* bounds = nullptr,
+                          bool prepare_blocks = false) {
   // prepare (the tx-signature entry points): called with (k, first item, items) just before chunk
   // k's front is enqueued; it makes chunk k's verify items (and, host form, its bytes) and orders
   // `s` after them. The key tables are then sized from `uses` and start building at once, before
@@ -209,13 +210,25 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   if (e == hipSuccess && pre_plan) e = plan(0);
   if (e == hipSuccess && pre_plan) e = plan(1);
   if (e == hipSuccess && prepare) e = cg::launch_key_tables(&c->fork, s);
+  auto back = [&](uint64_t k) {
+    return cg::launch_items_back(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, d_status + at(k),
+                                 c->keyprep.p, ws(k), c->btab.p, s, &c->fork, &wp);
+  };
+  if (prepare_blocks) {
+    // host copies in the prepare hook block the enqueuing thread: chunk k's back goes in before
+    // chunk k + 1's copy, so the device runs chunk k's ladders during it (with chunk k + 1's front
+    // first, chunk k's ladders waited for chunk k + 1's copy: profiles/r03/v5 timeline)
+    for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
+      e = front(k);
+      if (e == hipSuccess) e = back(k);
+    }
+    return e;
+  }
   if (e == hipSuccess) e = front(0);
   for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
     if (!two && k > 0) e = front(k);
     if (two && k + 1 < nch && e == hipSuccess) e = front(k + 1);
-    if (e == hipSuccess)
-      e = cg::launch_items_back(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, d_status + at(k),
-                                c->keyprep.p, ws(k), c->btab.p, s, &c->fork, &wp);
+    if (e == hipSuccess) e = back(k);
   }
   return e;
 }
@@ -251,11 +264,14 @@ void plan_host(const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64
   P.ext.assign(nch, Extent());
   // one host thread per chunk (at most 16): the scan reads 32 B per item
   auto scan = [&](uint64_t k0, uint64_t k1) {
-    for (uint64_t k = k0; k < k1; ++k)
+    for (uint64_t k = k0; k < k1; ++k) {
+      Extent x;  // thread-local until the end (neighbouring chunks' slots share cache lines)
       for (uint64_t i = P.first[k]; i < P.first[k + 1]; ++i) {
-        P.ext[k].add(items[i].sig_off, items[i].sig_len, arena_len);
-        P.ext[k].add(items[i].msg_off, items[i].msg_len, arena_len);
+        x.add(items[i].sig_off, items[i].sig_len, arena_len);
+        x.add(items[i].msg_off, items[i].msg_len, arena_len);
       }
+      P.ext[k] = x;
+    }
   };
   const uint64_t nt = nch < 16 ? nch : 16;
   if (n_items < (1u << 16) || nt < 2) {
@@ -417,7 +433,19 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     c->chunk_set = true;
   }
   if (cfg && (cfg->flags & CG_FLAG_STAGE_TIMING)) c->fork.timer = &c->timer;
-  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  // CG_STREAM_PRIORITY=1 (A/B): the context's stream at the device's highest priority, so its
+  // blocks (the plan sort's decoupled look-back above all) dispatch ahead of the side streams'
+  // table builds
+  static const bool prio = [] {
+    const char* v = getenv("CG_STREAM_PRIORITY");
+    return v && v[0] == '1';
+  }();
+  int lo_pri = 0, hi_pri = 0;
+  hipError_t e = hipSuccess;
+  if (prio && hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri) == hipSuccess)
+    e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_pri);
+  else
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;
     return hip_fail(e, "hipStreamCreate");
@@ -768,7 +796,7 @@ static int verify_transactions_locked(cg_ctx* c, const cg_tx* d_txs, uint64_t n_
   }
   uint64_t slot = (maxlen + 15) & ~(uint64_t)15;
   if (slot == 0) slot = 16;
-  const uint64_t msgs_len = cg::tx_msgs_head(n_tmpls, slot) + slot * n_sigs;
+  const uint64_t msgs_len = cg::tx_msgs_head(n_tmpls, slot);
   const size_t need_leaf = cg::tx_ws_bytes(n_comps), need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1),
                need_msgs = msgs_len ? msgs_len : 16, need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
   if (c->aux2.cap < need_leaf || c->txitems.cap < need_items || c->msgs.cap < need_msgs ||
@@ -882,7 +910,7 @@ static uint64_t tmpl_slot(const cg_signable_tmpl* tmpls, uint32_t n_tmpls) {
 // when a buffer grows).
 static hipError_t ensure_txsig_ws(cg_ctx* c, uint64_t n_sigs, uint32_t n_tmpls, uint64_t slot) {
   const size_t need_items = sizeof(cg_item) * (n_sigs ? n_sigs : 1),
-               need_msgs = cg::tx_msgs_head(n_tmpls, slot) + slot * (n_sigs ? n_sigs : 1),
+               need_msgs = cg::tx_msgs_head(n_tmpls, slot),
                need_tmpl = sizeof(cg_signable_tmpl) * (n_tmpls ? n_tmpls : 1);
   if (c->txitems.cap >= need_items && c->msgs.cap >= need_msgs && c->tmpls.cap >= need_tmpl) return hipSuccess;
   hipError_t e = hipDeviceSynchronize();
@@ -906,7 +934,8 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
   hipError_t e = hipSuccess;
   const cg_signable_tmpl* dt = (const cg_signable_tmpl*)c->tmpls.p;
   if (n_tmpls) e = hipMemcpyAsync(c->tmpls.p, tmpls, sizeof(cg_signable_tmpl) * n_tmpls, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = cg::launch_tx_sig_templates(dt, n_tmpls, d_arena, arena_len, slot, (uint8_t*)c->msgs.p, s);
+  if (e == hipSuccess)
+    e = cg::launch_tx_sig_templates(dt, n_tmpls, d_arena, arena_len, slot, d_ids, n_ids, (uint8_t*)c->msgs.p, s);
   const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> prepare = [&](uint64_t k, uint64_t first,
                                                                                uint64_t cnt) {
     hipError_t r = ready ? (*ready)(k, first, cnt) : hipSuccess;
@@ -917,8 +946,8 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
   };
   if (e == hipSuccess)
     e = launch_chunked(c, d_keys, n_keys, (const cg_item*)c->txitems.p, n_sigs, d_arena, arena_len, mode, d_status, s,
-                       (const uint8_t*)c->msgs.p, cg::tx_msgs_head(n_tmpls, slot) + slot * n_sigs, &prepare, &uses,
-                       bounds);
+                       (const uint8_t*)c->msgs.p, cg::tx_msgs_head(n_tmpls, slot), &prepare, &uses,
+                       bounds, ready != nullptr);
   return e;
 }
 
@@ -977,15 +1006,20 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   std::vector<uint32_t> counts(n_keys ? n_keys : 1, 0u);
   const uint64_t nt = n_sigs < (1u << 16) ? 1 : 16;
   {
-    const uint64_t ns = (n_sigs + CG_TXSIG_COUNT_SAMPLE - 1) / CG_TXSIG_COUNT_SAMPLE;
+    static const uint32_t S = [] {  // CG_TXSIG_SAMPLE (A/B): 1 in S signatures counted (power of two)
+      const char* v = getenv("CG_TXSIG_SAMPLE");
+      const uint32_t x = v ? (uint32_t)strtoul(v, nullptr, 10) : CG_TXSIG_COUNT_SAMPLE;
+      return x && (x & (x - 1)) == 0 ? x : CG_TXSIG_COUNT_SAMPLE;
+    }();
+    const uint64_t ns = (n_sigs + S - 1) / S;
     std::vector<std::vector<uint32_t>> pc(nt > 1 ? nt : 0, std::vector<uint32_t>(n_keys ? n_keys : 1, 0u));
     auto scan = [&](uint64_t t) {
       uint32_t* cnt = nt > 1 ? pc[t].data() : counts.data();
       for (uint64_t j = ns * t / nt; j < ns * (t + 1) / nt; ++j) {
         // one record per group of CG_TXSIG_COUNT_SAMPLE, at a hashed position (no aliasing with a
         // layout that cycles through the keys)
-        const uint64_t i = j * CG_TXSIG_COUNT_SAMPLE + (((uint32_t)j * 0x9E3779B1u) >> 29) % CG_TXSIG_COUNT_SAMPLE;
-        if (i < n_sigs && sigs[i].key_idx < n_keys) cnt[sigs[i].key_idx] += CG_TXSIG_COUNT_SAMPLE;
+        const uint64_t i = j * S + (((uint32_t)j * 0x9E3779B1u) >> 24) % S;
+        if (i < n_sigs && sigs[i].key_idx < n_keys) cnt[sigs[i].key_idx] += S;
       }
     };
     if (nt == 1) {
@@ -1012,10 +1046,13 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     const uint64_t m = (e - f) < (1u << 16) ? 1 : nt;
     std::vector<Extent> pe(m), pi(m);
     auto scan = [&](uint64_t t) {
+      Extent a, b;  // thread-local until the end (the vector slots share cache lines)
       for (uint64_t i = f + (e - f) * t / m; i < f + (e - f) * (t + 1) / m; ++i) {
-        pe[t].add(sigs[i].sig_off, sigs[i].sig_len, arena_len);
-        if (sigs[i].tx_idx < n_ids) pi[t].add(32ull * sigs[i].tx_idx, 32, 32ull * n_ids);
+        a.add(sigs[i].sig_off, sigs[i].sig_len, arena_len);
+        if (sigs[i].tx_idx < n_ids) b.add(32ull * sigs[i].tx_idx, 32, 32ull * n_ids);
       }
+      pe[t] = a;
+      pi[t] = b;
     };
     if (m == 1) {
       scan(0);

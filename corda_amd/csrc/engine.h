@@ -170,9 +170,9 @@ hipError_t launch_tx_ids(const cg_tx* d_txs, uint64_t n_tx, const cg_component* 
                          const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_ids, uint8_t* d_status,
                          uint8_t* d_leaf_ws, hipStream_t stream);
 
-// Transaction pipeline: per-signature verify items + spliced SignableData messages: d_msgs holds
-// the templates' SHA-256 midstate records and template images (tx_msgs_head(n_tmpls, slot) bytes),
-// then one `slot`-byte message slot per signature (slot a multiple of 16).
+// Transaction pipeline: per-signature verify items over SignableData splices. d_msgs (the message
+// workspace, tx_msgs_head(n_tmpls, slot) bytes) holds the splice header, the templates' SHA-256
+// midstates and their images (`slot` bytes each, a multiple of 16); no message is materialised.
 uint64_t tx_msgs_head(uint32_t n_tmpls, uint64_t slot);
 hipError_t launch_tx_sig_items(const cg_txsig* d_sigs, uint64_t n_sigs, const cg_signable_tmpl* d_tmpls,
                                uint32_t n_tmpls, const uint8_t* d_tx_status, uint64_t n_tx, const uint8_t* d_ids,
@@ -182,7 +182,8 @@ hipError_t launch_tx_sig_items(const cg_txsig* d_sigs, uint64_t n_sigs, const cg
 // any contiguous range [first, first + n) of the signatures (tx_sig_range: its verify items and
 // spliced messages; every signature keeps its own message slot).
 hipError_t launch_tx_sig_templates(const cg_signable_tmpl* d_tmpls, uint32_t n_tmpls, const uint8_t* d_arena,
-                                   uint64_t arena_len, uint64_t slot, uint8_t* d_msgs, hipStream_t stream);
+                                   uint64_t arena_len, uint64_t slot, const uint8_t* d_ids, uint64_t n_ids,
+                                   uint8_t* d_msgs, hipStream_t stream);
 hipError_t launch_tx_sig_range(const cg_txsig* d_sigs, uint64_t first, uint64_t n, const cg_signable_tmpl* d_tmpls,
                                uint32_t n_tmpls, const uint8_t* d_tx_status, uint64_t n_tx, const uint8_t* d_ids,
                                uint64_t arena_len, uint64_t slot, cg_item* d_items, uint8_t* d_msgs,

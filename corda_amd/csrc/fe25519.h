@@ -24,9 +24,11 @@
 #if defined(__HIPCC__)
 #define CG_HD __host__ __device__ __forceinline__
 #define CG_HDS __host__ __device__ static __forceinline__  // static member functions
+#define CG_HDM __host__ __device__ __forceinline__         // non-static member functions
 #else
 #define CG_HD static inline
 #define CG_HDS static inline
+#define CG_HDM inline
 #endif
 
 #ifdef FE_BOUNDS_CHECK

@@ -8,6 +8,7 @@
 #include "ed25519.h"
 #include "ed25519_rows.h"
 #include "engine.h"
+#include "sha2.h"
 
 namespace cg {
 
@@ -63,17 +64,47 @@ __device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t ar
 // With CG_ITEM_MSG_WS: the message is a SignableData splice of template reserved1, whose SHA-256
 // midstate record (the template prefix's full 64-byte blocks) heads the message workspace.
 #define CG_ITEM_TMPL 2u
+// With CG_ITEM_MSG_WS | CG_ITEM_TMPL: the message is never materialised; msg_off is the tx index and
+// the hash kernels read the splice through SpliceLd (sha2.h) from the workspace head below.
+#define CG_ITEM_FUSED 4u
+// Message workspace head (cg_verify_tx_signatures*, cg_verify_transactions*):
+//   [SpliceHdr, 256 B][TmplMid x n_tmpls, 256-aligned][template images: n_tmpls x slot]
+struct SpliceHdr {
+  uint64_t ids;      // device address of the 32-byte ids
+  uint64_t n_ids;
+  uint64_t img_off;  // byte offset of the images in the workspace
+  uint64_t slot;     // bytes per image (16-aligned, >= the longest message + 16)
+};
+#define SPLICE_HDR_BYTES 256u
 struct TmplMid {
   uint32_t state[8];
-  uint32_t blocks;  // prefix blocks absorbed into state
-  uint32_t pad[3];
+  uint32_t blocks;      // prefix blocks absorbed into state
+  uint32_t prefix_len;  // the id's position in the message
+  uint32_t pad[2];
 };
 static_assert(sizeof(TmplMid) == 48, "template midstate record");
-CG_HD uint64_t tmpl_mid_bytes(uint32_t n_tmpls) { return ((uint64_t)n_tmpls * sizeof(TmplMid) + 255) & ~(uint64_t)255; }
+CG_HD uint64_t tmpl_mid_bytes(uint32_t n_tmpls) {
+  return SPLICE_HDR_BYTES + (((uint64_t)n_tmpls * sizeof(TmplMid) + 255) & ~(uint64_t)255);
+}
+__device__ __forceinline__ bool item_fused(const cg_item& it, const uint8_t* msgs) {
+  return msgs && (it.reserved0 & (CG_ITEM_MSG_WS | CG_ITEM_TMPL | CG_ITEM_FUSED)) ==
+                     (CG_ITEM_MSG_WS | CG_ITEM_TMPL | CG_ITEM_FUSED);
+}
 __device__ __forceinline__ const TmplMid* item_tmpl_mid(const cg_item& it, const uint8_t* msgs) {
   return (it.reserved0 & CG_ITEM_TMPL) && (it.reserved0 & CG_ITEM_MSG_WS) && msgs
-             ? (const TmplMid*)msgs + it.reserved1
+             ? (const TmplMid*)(msgs + SPLICE_HDR_BYTES) + it.reserved1
              : nullptr;
+}
+// The splice of a fused item: its template's image with its tx id
+__device__ __forceinline__ SpliceLd item_splice(const cg_item& it, const uint8_t* msgs) {
+  const SpliceHdr* h = (const SpliceHdr*)msgs;
+  const TmplMid* m = (const TmplMid*)(msgs + SPLICE_HDR_BYTES) + it.reserved1;
+  SpliceLd ld;
+  ld.img = msgs + h->img_off + (uint64_t)it.reserved1 * h->slot;
+  ld.img_len = h->slot;
+  ld.id = (const uint32_t*)(uintptr_t)h->ids + 8ull * it.msg_off;
+  ld.at = m->prefix_len;
+  return ld;
 }
 __device__ __forceinline__ bool item_in_ws(const cg_item& it, const uint8_t* msgs) {
   return (it.reserved0 & CG_ITEM_MSG_WS) && msgs != nullptr;

@@ -208,13 +208,52 @@ CG_HD void cg_ld_dwords4(uint32_t out[4], const uint8_t* arena, uint64_t len_rou
   }
 }
 
+// ---- message sources. A message is read as aligned little-endian dwords at byte offsets relative
+// to its 4-aligned base: ArenaLd over a contiguous arena span, or SpliceLd over a SignableData
+// splice (cg_verify_tx_signatures): the template image prefix || 0^32 || suffix with the 32-byte tx
+// id ORed in at byte `at` (two aligned id dwords and a funnel shift per overlapping word), so the
+// spliced bytes are never written to memory.
+struct ArenaLd {
+  const uint8_t* arena;
+  uint64_t len_rounded;
+  CG_HDM void dwords4(uint32_t out[4], uint64_t addr) const { cg_ld_dwords4(out, arena, len_rounded, addr); }
+  CG_HDM uint32_t bytes4(uint64_t off) const { return cg_ld_bytes4(arena, len_rounded, off); }
+};
+// The id's bytes x .. x + 3 (x may start before or run past the 32 id bytes: those read 0).
+CG_HD uint32_t splice_id_word(const uint32_t* id, int64_t x) {
+  if (x <= -4 || x >= 32) return 0u;
+  const int64_t a = x >= 0 ? x >> 2 : -1;
+  const uint32_t r = (uint32_t)(x - 4 * a);
+  const uint32_t lo = a >= 0 ? id[a] : 0u;
+  const uint32_t hi = a + 1 < 8 ? id[a + 1] : 0u;
+  return r ? (lo >> (8 * r)) | (hi << (32 - 8 * r)) : lo;
+}
+struct SpliceLd {
+  const uint8_t* img;   // template image, 16-aligned
+  uint64_t img_len;     // image bytes (loads past them read 0)
+  const uint32_t* id;   // 8 aligned dwords
+  uint32_t at;          // id position (the prefix length)
+  CG_HDM void dwords4(uint32_t out[4], uint64_t addr) const {
+    cg_ld_dwords4(out, img, img_len, addr);
+    const int64_t x0 = (int64_t)addr - (int64_t)at;
+    if (x0 > -16 && x0 < 32) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) out[q] |= splice_id_word(id, x0 + 4 * q);
+    }
+  }
+  CG_HDM uint32_t bytes4(uint64_t off) const {  // off is 4-aligned for a splice (base 0)
+    return cg_ld_bytes4(img, img_len, off) | splice_id_word(id, (int64_t)off - (int64_t)at);
+  }
+};
+
 // SHA-512(prefix64 || msg) where prefix64 is 16 little-endian words (e.g. R || Abyte).
 // Output: the 64 digest bytes as 16 little-endian words (ready for sc_reduce512).
 // The message is read as aligned 16-byte chunks (33 dwords per 128-byte block) and realigned with
 // one funnel shift per word, instead of two dword loads per word (round 1: 136 loads per
 // 270-byte message, the challenge kernel's memory-wait share was ~0.3).
-CG_HD void sha512_prefix64_msg(uint32_t out[16], const uint32_t prefix[16], const uint8_t* arena,
-                               uint64_t len_rounded, uint64_t msg_off, uint64_t msg_len) {
+template <class Ld>
+CG_HD void sha512_prefix64_ld(uint32_t out[16], const uint32_t prefix[16], const Ld& ld, uint64_t msg_off,
+                              uint64_t msg_len) {
   uint64_t s[8];
   sha512_init(s);
   const uint64_t n = 64 + msg_len;
@@ -230,7 +269,7 @@ CG_HD void sha512_prefix64_msg(uint32_t out[16], const uint32_t prefix[16], cons
       if (blk == 0 && t < 4) {
         W[4 * t] = W[4 * t + 1] = W[4 * t + 2] = W[4 * t + 3] = 0u;
       } else {
-        cg_ld_dwords4(&W[4 * t], arena, len_rounded, base + (uint64_t)(k0 + 4 * t) * 4);
+        ld.dwords4(&W[4 * t], base + (uint64_t)(k0 + 4 * t) * 4);
       }
     }
     const bool last = blk + 1 == nblocks;
@@ -274,6 +313,11 @@ CG_HD void sha512_prefix64_msg(uint32_t out[16], const uint32_t prefix[16], cons
     out[2 * k] = CG_BSWAP32((uint32_t)(s[k] >> 32));
     out[2 * k + 1] = CG_BSWAP32((uint32_t)s[k]);
   }
+}
+
+CG_HD void sha512_prefix64_msg(uint32_t out[16], const uint32_t prefix[16], const uint8_t* arena,
+                               uint64_t len_rounded, uint64_t msg_off, uint64_t msg_len) {
+  sha512_prefix64_ld(out, prefix, ArenaLd{arena, len_rounded}, msg_off, msg_len);
 }
 
 // Plain SHA-512 of arena[off, off+len)
@@ -399,9 +443,10 @@ CG_HD void sha256_compress(uint32_t s[8], uint32_t w[16]) {
 // 8 big-endian words (the digest).
 // mid (optional): the state after the message's first `mid_blocks` 64-byte blocks (a SignableData
 // template's constant prefix, cg_verify_tx_signatures); hashing resumes at that block.
-CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t len_rounded, uint64_t off,
-                               uint64_t len, const uint32_t* suffix_be /* 8 words or null */,
-                               const uint32_t* mid = nullptr, uint32_t mid_blocks = 0) {
+template <class Ld>
+CG_HD void sha256_ld_suffix(uint32_t out[8], const Ld& ld, uint64_t off, uint64_t len,
+                            const uint32_t* suffix_be /* 8 words or null */, const uint32_t* mid = nullptr,
+                            uint32_t mid_blocks = 0) {
   uint32_t s[8];
   if (mid) {
 #pragma unroll
@@ -420,7 +465,7 @@ CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t l
   for (uint64_t blk = mid_blocks; blk < nfull; ++blk) {
     uint32_t W[20], w[16];  // aligned dwords of the block (+1 for the realignment), 16-byte loads
 #pragma unroll
-    for (int t = 0; t < 5; ++t) cg_ld_dwords4(&W[4 * t], arena, len_rounded, base + blk * 64 + 16 * t);
+    for (int t = 0; t < 5; ++t) ld.dwords4(&W[4 * t], base + blk * 64 + 16 * t);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -438,7 +483,7 @@ CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t l
       const uint64_t pos = blk * 64 + (uint64_t)j * 4;
       uint32_t v;
       if (pos + 4 <= len) {
-        v = CG_BSWAP32(cg_ld_bytes4(arena, len_rounded, off + pos));
+        v = CG_BSWAP32(ld.bytes4(off + pos));
       } else if (sfx && (len & 3) == 0 && pos >= len && pos + 4 <= n) {
         v = suffix_be[(pos - len) >> 2];
       } else if (pos > n) {
@@ -449,7 +494,7 @@ CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t l
           const uint64_t p = pos + (uint64_t)bb;
           uint32_t byte;
           if (p < len) {
-            byte = cg_ld_bytes4(arena, len_rounded, off + p) & 0xffu;
+            byte = ld.bytes4(off + p) & 0xffu;
           } else if (p < n) {
             const uint64_t q = p - len;
             byte = (suffix_be[q >> 2] >> (24 - 8 * (q & 3))) & 0xffu;
@@ -470,4 +515,10 @@ CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t l
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) out[k] = s[k];
+}
+
+CG_HD void sha256_arena_suffix(uint32_t out[8], const uint8_t* arena, uint64_t len_rounded, uint64_t off,
+                               uint64_t len, const uint32_t* suffix_be /* 8 words or null */,
+                               const uint32_t* mid = nullptr, uint32_t mid_blocks = 0) {
+  sha256_ld_suffix(out, ArenaLd{arena, len_rounded}, off, len, suffix_be, mid, mid_blocks);
 }

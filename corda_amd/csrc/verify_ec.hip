@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(64) k_ec_gtab_init(EcGTab* __restrict__ out, E
   const int cls = plan_class_of_curve(C);             \
   const uint32_t beg = ranges[cls], end = ranges[cls + 1]
 
-template <int C>
+template <int C, bool Fused>  // Fused: every message is a SignableData splice (the tx-signature paths)
 __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
                                                  const uint32_t* __restrict__ ranges,
                                                  const EdKeyHdr* __restrict__ hdr,
@@ -223,14 +223,18 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
   } else if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
     st = CG_EMPTY;
   } else if (!in_arena(it.sig_off, it.sig_len, arena_len) ||
-             !in_arena(it.msg_off, it.msg_len, item_msg_len(it, arena_len, msgs_len, msgs))) {
+             (Fused ? !item_fused(it, msgs)
+                    : !in_arena(it.msg_off, it.msg_len, item_msg_len(it, arena_len, msgs_len, msgs)))) {
     st = CG_NOT_RUN;
   } else {
     EcItemWs w;
     const TmplMid* mid = item_tmpl_mid(it, msgs);
-    const uint32_t r = ecdsa_prep<C>(w, arena, round4(arena_len), it.sig_off, it.sig_len,
-                                     item_msg_arena(it, arena, msgs), round4(item_msg_len(it, arena_len, msgs_len, msgs)),
-                                     it.msg_off, it.msg_len, mid ? mid->state : nullptr, mid ? mid->blocks : 0u);
+    const uint32_t r =
+        Fused ? ecdsa_prep_ld<C>(w, arena, round4(arena_len), it.sig_off, it.sig_len, item_splice(it, msgs), 0,
+                                 it.msg_len, mid->state, mid->blocks)
+              : ecdsa_prep<C>(w, arena, round4(arena_len), it.sig_off, it.sig_len, item_msg_arena(it, arena, msgs),
+                              round4(item_msg_len(it, arena_len, msgs_len, msgs)), it.msg_off, it.msg_len,
+                              mid ? mid->state : nullptr, mid ? mid->blocks : 0u);
     if (r == 0) {
       ws[p] = w;
       st = (uint8_t)(EC_PENDING_BASE + C);
@@ -476,8 +480,14 @@ static void launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t
                          const ItemWs& iw, hipStream_t stream) {
   const uint32_t B = 256;  // a curve's range is at most n_items long
   EcItemWs* ws = (EcItemWs*)iw.slots;
-  hipLaunchKernelGGL(k_ec_prep<C>, dim3(walk_grid(n_items, B, WALK_CAP(EC_PREP_CAP_WAVES))), dim3(B), 0, stream, d_items,
-                     iw.perm, iw.ranges, w.hdr, d_arena, arena_len, d_msgs, msgs_len, mode, d_status, ws);
+  if (d_msgs)
+    hipLaunchKernelGGL((k_ec_prep<C, true>), dim3(walk_grid(n_items, B, WALK_CAP(EC_PREP_CAP_WAVES))), dim3(B), 0,
+                       stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena, arena_len, d_msgs, msgs_len, mode, d_status,
+                       ws);
+  else
+    hipLaunchKernelGGL((k_ec_prep<C, false>), dim3(walk_grid(n_items, B, WALK_CAP(EC_PREP_CAP_WAVES))), dim3(B), 0,
+                       stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena, arena_len, d_msgs, msgs_len, mode, d_status,
+                       ws);
   const unsigned igrid = walk_grid((n_items + EC_INV_K - 1) / EC_INV_K, B, WALK_CAP(EC_INV_CAP_WAVES));
   hipLaunchKernelGGL(k_ec_inv<C>, dim3(igrid), dim3(B), 0, stream, iw.perm, iw.ranges,
                      (const uint8_t*)d_status, ws);

@@ -319,6 +319,7 @@ static_assert(sizeof(EdDigitsWide) == ITEM_SLOT, "digits must fill one item slot
 #ifndef ED_HASH_WAVES_PER_SIMD
 #define ED_HASH_WAVES_PER_SIMD 3
 #endif
+template <bool Fused>
 __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restrict__ items,
                                             const uint32_t* __restrict__ perm, const EdKeyHdr* __restrict__ hdr,
                                             const uint8_t* __restrict__ arena, uint64_t arena_len,
@@ -331,7 +332,8 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
   if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
     st = CG_EMPTY;
   } else if (!in_arena(it.sig_off, it.sig_len, arena_len) ||
-             !in_arena(it.msg_off, it.msg_len, item_msg_len(it, arena_len, msgs_len, msgs))) {
+             (Fused ? !item_fused(it, msgs)
+                    : !in_arena(it.msg_off, it.msg_len, item_msg_len(it, arena_len, msgs_len, msgs)))) {
     st = CG_NOT_RUN;
   } else if (it.sig_len != 64) {
     st = CG_SIG_MALFORMED;
@@ -346,8 +348,11 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
       pre[w] = sw[w];
       pre[8 + w] = kh->abyte[w];
     }
-    sha512_prefix64_msg(hw, pre, item_msg_arena(it, arena, msgs), round4(item_msg_len(it, arena_len, msgs_len, msgs)),
-                        it.msg_off, it.msg_len);
+    if (Fused)
+      sha512_prefix64_ld(hw, pre, item_splice(it, msgs), 0, it.msg_len);
+    else
+      sha512_prefix64_msg(hw, pre, item_msg_arena(it, arena, msgs),
+                          round4(item_msg_len(it, arena_len, msgs_len, msgs)), it.msg_off, it.msg_len);
     sc_reduce512(h, hw);
     uint32_t s[8], sr[8];
 #pragma unroll
@@ -377,6 +382,7 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
   status[i] = st;
 }
 
+template <bool Fused>  // Fused: every item's message is a SignableData splice (the tx-signature paths)
 __global__ void __launch_bounds__(256, ED_HASH_WAVES_PER_SIMD) k_ed_hash(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
     const EdKeyHdr* __restrict__ hdr, const uint8_t* __restrict__ arena, uint64_t arena_len,
@@ -384,7 +390,8 @@ __global__ void __launch_bounds__(256, ED_HASH_WAVES_PER_SIMD) k_ed_hash(
     EdDigits* __restrict__ dig) {
   const uint32_t beg = ranges[PLAN_ED], wbeg = ranges[PLAN_WIDE + PLAN_ED];
   for (Walk w = walk_units(ranges[PLAN_ED + 1] - beg); w.u < w.end; w.u += w.step)
-    ed_hash_one(beg + w.u, items, perm, hdr, arena, arena_len, msgs, msgs_len, mode, status, dig, beg + w.u >= wbeg);
+    ed_hash_one<Fused>(beg + w.u, items, perm, hdr, arena, arena_len, msgs, msgs_len, mode, status, dig,
+                       beg + w.u >= wbeg);
 }
 
 // One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the row tables (B rows
@@ -820,8 +827,12 @@ void ed_launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_
                      const ItemWs& iw, hipStream_t stream) {
   const uint32_t B = 256;  // the Ed25519 range is at most n_items long
   const unsigned grid = walk_grid(n_items, B, WALK_CAP(ED_HASH_WAVES_PER_SIMD));
-  hipLaunchKernelGGL(k_ed_hash, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
-                     arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
+  if (d_msgs)
+    hipLaunchKernelGGL(k_ed_hash<true>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
+                       arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
+  else
+    hipLaunchKernelGGL(k_ed_hash<false>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
+                       arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
 }
 
 void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,

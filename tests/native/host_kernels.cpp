@@ -799,3 +799,51 @@ static int madd_w_cmp(uint64_t seed, int n) {
 extern "C" int t_ec_madd_w_cmp(int curve, uint64_t seed, int n) {
   return curve == 1 ? madd_w_cmp<CG_CURVE_R1>(seed, n) : madd_w_cmp<CG_CURVE_K1>(seed, n);
 }
+
+// SpliceLd (sha2.h: the hash kernels' view of prefix || id || suffix) against the same bytes
+// materialised: SHA-512 with a 64-byte prefix (the Ed25519 challenge) and SHA-256 from a midstate
+// (ECDSA's e), for prefixes of 0..299 and suffixes of 0..17 bytes. Returns mismatches.
+extern "C" int t_sha_splice_cmp(uint64_t seed, int n) {
+  uint64_t s = seed | 1;
+  auto rnd = [&]() {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    return s;
+  };
+  int bad = 0;
+  for (int t = 0; t < n; ++t) {
+    const uint32_t pl = (uint32_t)(rnd() % 300), sl = (uint32_t)(rnd() % 18), len = pl + 32 + sl;
+    const uint32_t slot = (len + 15) & ~15u;
+    std::vector<uint8_t> img(slot + 64, 0), msg(((len + 3) & ~3u) + 64, 0);
+    uint32_t id[8];
+    for (int k = 0; k < 8; ++k) id[k] = (uint32_t)rnd();
+    for (uint32_t k = 0; k < len; ++k) {
+      uint8_t b = (uint8_t)rnd();
+      if (k >= pl && k < pl + 32) b = ((const uint8_t*)id)[k - pl];
+      else img[k] = b;
+      msg[k] = b;
+    }
+    SpliceLd ld{img.data(), slot, id, pl};
+    uint32_t pre[16], a[16], b[16];
+    for (int k = 0; k < 16; ++k) pre[k] = (uint32_t)rnd();
+    sha512_prefix64_ld(a, pre, ld, 0, len);
+    sha512_prefix64_msg(b, pre, msg.data(), (len + 3) & ~3u, 0, len);
+    if (memcmp(a, b, sizeof a)) ++bad;
+    // SHA-256 from the midstate after the prefix's full blocks
+    uint32_t st[8], w[16];
+    sha256_init(st);
+    const uint32_t blocks = pl / 64;
+    for (uint32_t bl = 0; bl < blocks; ++bl) {
+      for (int j = 0; j < 16; ++j)
+        w[j] = ((uint32_t)msg[64 * bl + 4 * j] << 24) | ((uint32_t)msg[64 * bl + 4 * j + 1] << 16) |
+               ((uint32_t)msg[64 * bl + 4 * j + 2] << 8) | msg[64 * bl + 4 * j + 3];
+      sha256_compress(st, w);
+    }
+    uint32_t h1[8], h2[8];
+    sha256_ld_suffix(h1, ld, 0, len, nullptr, st, blocks);
+    sha256_arena_suffix(h2, msg.data(), (len + 3) & ~3u, 0, len, nullptr);
+    if (memcmp(h1, h2, sizeof h1)) ++bad;
+  }
+  return bad;
+}

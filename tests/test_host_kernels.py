@@ -390,3 +390,12 @@ def test_ec_madd_w_matches_madd(curve):
     lib = hostk.lib()
     lib.t_ec_madd_w_cmp.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int]
     assert lib.t_ec_madd_w_cmp(curve, 12345 + curve, 400) == 0
+
+
+def test_sha_over_splice_matches_materialised():
+    """The hash kernels read SignableData = prefix || id || suffix straight from the template image
+    and the id (no message is written): SHA-512 (challenge form) and SHA-256 resumed from the prefix
+    midstate equal the hashes of the materialised bytes for every prefix length 0..299."""
+    lib = hostk.lib()
+    lib.t_sha_splice_cmp.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    assert lib.t_sha_splice_cmp(99, 3000) == 0

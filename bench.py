@@ -66,8 +66,9 @@ MAC32_ED_WIDE = ED_WIDE_FE[0] * MAC_PER_MUL + ED_WIDE_FE[1] * MAC_PER_SQ
 MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
                           (ED_VERIFY_FE[1] + ED_FINISH_FE[1]) * MAC_PER_SQ +
                           (ED_INVERT_FE[0] * MAC_PER_MUL + ED_INVERT_FE[1] * MAC_PER_SQ) / ED_FINISH_K)
-# ECDSA: Montgomery products (mont29.h) per item: (k_ec_ladder full tables mod p, k_ec_inv mod n
-# per 16 items). One product = 81 a*b MACs + 9 per non-zero 29-bit limb of the modulus (q*m).
+# ECDSA: field products (mont29.h) per item: (k_ec_ladder full tables mod p, k_ec_inv mod n
+# per 16 items). A Montgomery product = 81 a*b MACs + 9 per non-zero 29-bit limb of the modulus
+# (q*m); secp256k1's p is folded instead (pseudo-Mersenne, plain form): 81 + 9 + 2 MACs.
 # The ladder figure is its full schedule (every digit non-zero): a lane whose digit is zero skips
 # its addition, but the wave issues it for the other 63 lanes, so the full schedule is what the
 # SIMD executes (per-item mean 1% lower).
@@ -83,9 +84,9 @@ EC_MAC_PER_MUL_P = {"secp256r1": 144, "secp256k1": 162}
 EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
-# kernel generation whose PMC traffic profile is committed (profiles/r02/pmc_traffic.json)
-KERNEL_VERSION = "r02_v6"
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+# kernel generation whose PMC traffic profile is committed (profiles/r03/pmc_traffic.json)
+KERNEL_VERSION = "r03_v8"
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
 
 # Appendix A labels (tools/workload) -> the verdict Crypto.doVerify gives them (key decodes)
 ED_LABEL_EXPECT = {0: 0, 1: 1, 2: 1, 3: 1, 4: 0, 6: 1, 7: 2}       # A5 (high S) depends on slide()
@@ -202,9 +203,10 @@ def cpu_baseline(batch, st_gpu, seconds, threads):
 
 
 def openssl_items(sub, st_port, threads):
-    """OpenSSL 3 EVP_DigestVerify on the same headline sample (Ed25519 + both ECDSA curves, a fresh
-    EVP_PKEY per item), on the CPU quota and on one thread: an industrial CPU point beside the port.
-    Its verdicts differ from the reference's where i2p 0.2.0 does (S >= L accepted by i2p)."""
+    """OpenSSL 3 EVP_DigestVerify on the same headline sample (Ed25519 + both ECDSA curves, each key
+    decoded once per call and shared by the workers), on the CPU quota and on one thread: an
+    industrial CPU point beside the port. Its verdicts differ from the reference's exactly where
+    i2p 0.2.0 does: Ed25519 signatures with S >= L (workload labels A4 / A5), which i2p accepts."""
     import ctypes
     so = os.path.join(ROOT, "tools", "cpu_baseline", "libosslcheck.so")
     if not os.path.exists(so):
@@ -229,8 +231,9 @@ def openssl_items(sub, st_port, threads):
     return {"value": round(sub.n / dt, 1), "unit": "sigs/s", "threads": threads, "items": int(sub.n),
             "value_1thread": round(n1 / dt1, 1),
             "valid_verdicts_differing_from_port": int(np.count_nonzero((st == 0) != valid_port)),
-            "note": "OpenSSL 3.0.2 EVP_DigestVerify per item (Ed25519 raw keys; ECDSA raw X||Y wrapped in the "
-                    "curve's SPKI); rejects Ed25519 S >= L, which i2p 0.2.0 accepts"}
+            "note": "OpenSSL 3.0.2 EVP_DigestVerify per item, keys decoded once per call (Ed25519 raw keys; "
+                    "ECDSA raw X||Y wrapped in the curve's SPKI); rejects Ed25519 S >= L (labels A4 / A5), "
+                    "which i2p 0.2.0 accepts: the only differing verdicts"}
 
 
 def configs0(a, eng, wl, threads):

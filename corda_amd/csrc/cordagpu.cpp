@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -94,6 +95,11 @@ struct cg_ctx {
   // host-buffer verify: a copy stream and one event per pipeline chunk (H2D of chunk k+1 overlaps
   // the verify of chunk k); timing events for cg_stats
   hipStream_t copy = nullptr;
+  // the tx-signature host path's second copy stream (chunk 0's bytes while the key-use counts are
+  // sampled) and a pinned buffer for those counts (a pinned copy does not queue behind a pageable one)
+  hipStream_t copy2 = nullptr;
+  uint32_t* pin_counts = nullptr;
+  size_t pin_counts_cap = 0;
   std::vector<hipEvent_t> seg;
   hipEvent_t tev[4] = {};
   // the end of the last call's device work, whatever stream it ran on: the next call waits for it
@@ -479,6 +485,7 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.planned, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.ed_tabs, hipEventDisableTiming);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy2, hipStreamNonBlocking);
   for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&c->tev[k]);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
   if (e == hipSuccess) e = cg::upload_constants();
@@ -529,10 +536,12 @@ void cg_close(cg_ctx* c) {
   if (c->fork.front) hipEventDestroy(c->fork.front);
   if (c->fork.planned) hipEventDestroy(c->fork.planned);
   if (c->fork.ed_tabs) hipEventDestroy(c->fork.ed_tabs);
-  if (c->copy) {
-    hipStreamSynchronize(c->copy);
-    hipStreamDestroy(c->copy);
-  }
+  for (hipStream_t* cs : {&c->copy, &c->copy2})
+    if (*cs) {
+      hipStreamSynchronize(*cs);
+      hipStreamDestroy(*cs);
+    }
+  if (c->pin_counts) hipHostFree(c->pin_counts);
   for (hipEvent_t e : c->seg) hipEventDestroy(e);
   for (int k = 0; k < 4; ++k)
     if (c->tev[k]) hipEventDestroy(c->tev[k]);
@@ -1005,7 +1014,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   // scanned just before its copy, while the device works on the chunks before it.
   std::vector<uint32_t> counts(n_keys ? n_keys : 1, 0u);
   const uint64_t nt = n_sigs < (1u << 16) ? 1 : 16;
-  {
+  auto sample_counts = [&] {
     static const uint32_t S = [] {  // CG_TXSIG_SAMPLE (A/B): 1 in S signatures counted (power of two)
       const char* v = getenv("CG_TXSIG_SAMPLE");
       const uint32_t x = v ? (uint32_t)strtoul(v, nullptr, 10) : CG_TXSIG_COUNT_SAMPLE;
@@ -1019,7 +1028,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
         // one record per group of CG_TXSIG_COUNT_SAMPLE, at a hashed position (no aliasing with a
         // layout that cycles through the keys)
         const uint64_t i = j * S + (((uint32_t)j * 0x9E3779B1u) >> 24) % S;
-        if (i < n_sigs && sigs[i].key_idx < n_keys) cnt[sigs[i].key_idx] += S;
+        if (i < n_sigs && sigs[i].key_idx < n_keys) ++cnt[sigs[i].key_idx];
       }
     };
     if (nt == 1) {
@@ -1036,10 +1045,17 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
         });
       for (auto& t : th) t.join();
     }
-    for (uint32_t k = 0; k < n_keys; ++k)
-      if (counts[k] == 0) counts[k] = 1;
-  }
-  const double ms_plan = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    // c sampled uses -> S (c + 2 sqrt(c) + 1): about two standard deviations above the unbiased
+    // S c, so a key whose true count clears a mode threshold is not sampled below it (on the
+    // configs[4] shard the plain estimate put 2 of 4096 Ed25519 keys, true minimum 1 634 uses, under
+    // the 1 536 wide threshold: full tables and a 170 us pf ladder per chunk, profiles/r03/v5); at
+    // least S, so every key has its row-0 table
+    for (uint32_t k = 0; k < n_keys; ++k) {
+      const uint64_t c = counts[k];
+      const uint64_t e = (uint64_t)S * (c + 2 * (uint64_t)std::ceil(std::sqrt((double)c)) + 1);
+      counts[k] = e > 0xfffffff0ull ? 0xfffffff0u : (uint32_t)e;
+    }
+  };
   // chunk k's signature bytes and id bytes (exact: a threaded scan of its slice of the table)
   auto chunk_extents = [&](uint64_t k, Extent& ext, Extent& idx) {
     const uint64_t f = bounds[k], e = bounds[k + 1];
@@ -1078,6 +1094,21 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   HIP_TRY(c->status.ensure(n_sigs), "hipMalloc(status)");
   HIP_TRY(ensure_txsig_ws(c, n_sigs, n_tmpls, slot), "hipMalloc(tx signature workspace)");
   HIP_TRY(ensure_ws(c, n_keys, per, n_sigs), "hipMalloc(workspace)");
+  // CG_TXSIG_OVERLAP_PLAN=1 (A/B): sample the counts while chunk 0 copies. Measured slower on the
+  // configs[4] shard (197 / 205 vs 213 / 220 M sigs/s, profiles/r03/ab_sc): the sample pass slows
+  // 2x beside the pageable copy's staging and the late counts delay the key tables.
+  static const bool overlap = [] {
+    const char* v = getenv("CG_TXSIG_OVERLAP_PLAN");
+    return v && v[0] == '1';
+  }();
+  if (overlap && c->pin_counts_cap < counts.size()) {
+    if (c->pin_counts) HIP_TRY(hipHostFree(c->pin_counts), "hipHostFree");
+    c->pin_counts = nullptr;
+    c->pin_counts_cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&c->pin_counts, sizeof(uint32_t) * counts.size(), hipHostMallocDefault),
+            "hipHostMalloc(key use counts)");
+    c->pin_counts_cap = counts.size();
+  }
   while (c->seg.size() < nch + 1) {
     hipEvent_t e;
     HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
@@ -1089,28 +1120,56 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
   HIP_TRY(hipEventRecord(c->tev[0], s), "hipEventRecord");
   HIP_TRY(hipStreamWaitEvent(c->copy, c->tev[0], 0), "hipStreamWaitEvent");
+  HIP_TRY(hipStreamWaitEvent(c->copy2, c->tev[0], 0), "hipStreamWaitEvent");
   std::vector<std::pair<uint64_t, uint64_t>> have;
   if (n_keys)
     HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, c->copy), "H2D keys");
   HIP_TRY(copy_missing(have, head, arena, dwin, win.lo, c->copy), "H2D key / template bytes");
   std::vector<std::pair<uint64_t, uint64_t>> have_ids;  // id bytes already resident
-  HIP_TRY(hipMemcpyAsync(c->aux1.p, counts.data(), sizeof(uint32_t) * counts.size(), hipMemcpyHostToDevice, c->copy),
-          "H2D key use counts");
+  // chunk k: its slice of the signature table, the ids it references not yet resident (a caller that
+  // lists each transaction's signatures together ships each id once, with its first chunk), then its
+  // signature bytes, on copy stream cs; seg[k] marks the end
+  auto copy_chunk = [&](uint64_t k, hipStream_t cs) {
+    Extent ek, ik;
+    chunk_extents(k, ek, ik);
+    const uint64_t first = bounds[k], cnt = bounds[k + 1] - bounds[k];
+    hipError_t e = hipMemcpyAsync((cg_txsig*)c->h_sigs.p + first, sigs + first, sizeof(cg_txsig) * cnt,
+                                  hipMemcpyHostToDevice, cs);
+    if (e == hipSuccess) e = copy_missing(have_ids, ik, ids, (uint8_t*)c->h_ids.p, 0, cs);
+    if (e == hipSuccess) e = copy_missing(have, ek, arena, dwin, win.lo, cs);
+    if (e == hipSuccess) e = hipEventRecord(c->seg[k], cs);
+    return e;
+  };
+  // The key-use counts gate only the key tables; chunk 0's bytes gate everything else. With
+  // `overlap`, chunk 0's copy (its own thread, second copy stream) runs while this thread samples
+  // the counts, which then go from the pinned buffer behind the key bytes on the first copy stream.
+  hipError_t pre_err = hipSuccess;
+  double ms_plan = 0;
+  if (overlap) {
+    std::thread pre([&] {
+      pre_err = hipSetDevice(c->device);
+      if (pre_err == hipSuccess) pre_err = copy_chunk(0, c->copy2);
+    });
+    sample_counts();
+    ms_plan = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    memcpy(c->pin_counts, counts.data(), sizeof(uint32_t) * counts.size());
+    const hipError_t e = hipMemcpyAsync(c->aux1.p, c->pin_counts, sizeof(uint32_t) * counts.size(),
+                                        hipMemcpyHostToDevice, c->copy);
+    pre.join();
+    HIP_TRY(e, "H2D key use counts");
+    HIP_TRY(pre_err, "H2D chunk 0");
+  } else {
+    sample_counts();
+    ms_plan = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    HIP_TRY(hipMemcpyAsync(c->aux1.p, counts.data(), sizeof(uint32_t) * counts.size(), hipMemcpyHostToDevice,
+                           c->copy),
+            "H2D key use counts");
+  }
   HIP_TRY(hipEventRecord(c->seg[nch], c->copy), "hipEventRecord");
   HIP_TRY(hipStreamWaitEvent(s, c->seg[nch], 0), "hipStreamWaitEvent");
   hipError_t copy_err = hipSuccess;
-  // chunk k: its slice of the signature table, the ids it references not yet resident (a caller that
-  // lists each transaction's signatures together ships each id once, with its first chunk), then its
-  // signature bytes
-  const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t first,
-                                                                              uint64_t cnt) {
-    Extent ek, ik;
-    chunk_extents(k, ek, ik);
-    hipError_t e = hipMemcpyAsync((cg_txsig*)c->h_sigs.p + first, sigs + first, sizeof(cg_txsig) * cnt,
-                                  hipMemcpyHostToDevice, c->copy);
-    if (e == hipSuccess) e = copy_missing(have_ids, ik, ids, (uint8_t*)c->h_ids.p, 0, c->copy);
-    if (e == hipSuccess) e = copy_missing(have, ek, arena, dwin, win.lo, c->copy);
-    if (e == hipSuccess) e = hipEventRecord(c->seg[k], c->copy);
+  const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t, uint64_t) {
+    hipError_t e = overlap && k == 0 ? hipSuccess : copy_chunk(k, c->copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, c->seg[k], 0);
     if (e == hipSuccess && k == 0) e = hipEventRecord(c->tev[1], s);
     if (e != hipSuccess) copy_err = e;

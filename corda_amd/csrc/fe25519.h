@@ -134,6 +134,17 @@ CG_HD void fe_reduce_cols(fe& out, fe_acc_t* h) {
     h[(i) + 1] += c;                          \
     h[i] &= ((fe_acc_t)1 << (sh)) - 1;        \
   }
+#ifdef FE_SINGLE_CARRY_CHAIN  // one chain 0 -> 9 (11 carries): 2% fewer ladder instructions, a longer dependency chain
+  FE_CARRY(0, 26);
+  FE_CARRY(1, 25);
+  FE_CARRY(2, 26);
+  FE_CARRY(3, 25);
+  FE_CARRY(4, 26);
+  FE_CARRY(5, 25);
+  FE_CARRY(6, 26);
+  FE_CARRY(7, 25);
+  FE_CARRY(8, 26);
+#else  // two interleaved chains (ref10 order, 12 carries)
   FE_CARRY(0, 26);
   FE_CARRY(4, 26);
   FE_CARRY(1, 25);
@@ -144,6 +155,7 @@ CG_HD void fe_reduce_cols(fe& out, fe_acc_t* h) {
   FE_CARRY(7, 25);
   FE_CARRY(4, 26);
   FE_CARRY(8, 26);
+#endif
   {
     fe_acc_t c = h[9] >> 25;
     h[9] &= FE_M25;

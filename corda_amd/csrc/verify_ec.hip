@@ -480,14 +480,18 @@ static void launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t
                          const ItemWs& iw, hipStream_t stream) {
   const uint32_t B = 256;  // a curve's range is at most n_items long
   EcItemWs* ws = (EcItemWs*)iw.slots;
+  static const uint32_t prep_waves = [] {  // CG_EC_PREP_WAVES (A/B): waves per SIMD of the prep grid
+    const char* v = getenv("CG_EC_PREP_WAVES");
+    const uint32_t x = v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
+    return x ? x : (uint32_t)EC_PREP_CAP_WAVES;
+  }();
+  const dim3 pgrid(walk_grid(n_items, B, WALK_CAP(prep_waves)));
   if (d_msgs)
-    hipLaunchKernelGGL((k_ec_prep<C, true>), dim3(walk_grid(n_items, B, WALK_CAP(EC_PREP_CAP_WAVES))), dim3(B), 0,
-                       stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena, arena_len, d_msgs, msgs_len, mode, d_status,
-                       ws);
+    hipLaunchKernelGGL((k_ec_prep<C, true>), pgrid, dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
+                       arena_len, d_msgs, msgs_len, mode, d_status, ws);
   else
-    hipLaunchKernelGGL((k_ec_prep<C, false>), dim3(walk_grid(n_items, B, WALK_CAP(EC_PREP_CAP_WAVES))), dim3(B), 0,
-                       stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena, arena_len, d_msgs, msgs_len, mode, d_status,
-                       ws);
+    hipLaunchKernelGGL((k_ec_prep<C, false>), pgrid, dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
+                       arena_len, d_msgs, msgs_len, mode, d_status, ws);
   const unsigned igrid = walk_grid((n_items + EC_INV_K - 1) / EC_INV_K, B, WALK_CAP(EC_INV_CAP_WAVES));
   hipLaunchKernelGGL(k_ec_inv<C>, dim3(igrid), dim3(B), 0, stream, iw.perm, iw.ranges,
                      (const uint8_t*)d_status, ws);

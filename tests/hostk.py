@@ -6,7 +6,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SO = os.path.join(HERE, "native", "libhostkernels.so")
+# CG_HOSTK_DEFS="-DFOO ...": extra defines for a variant's host build (its own .so)
+DEFS = os.environ.get("CG_HOSTK_DEFS", "").split()
+SO = os.path.join(HERE, "native", "libhostkernels%s.so" % ("_" + "_".join(d.lstrip("-D") for d in DEFS) if DEFS else ""))
 P = 2 ** 255 - 19
 L = 2 ** 252 + 27742317777372353535851937790883648493
 OFFS = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
@@ -19,8 +21,8 @@ def build():
             for f in os.listdir(os.path.join(HERE, "..", "corda_amd", "csrc")) if f.endswith(".h")) or \
             os.path.getmtime(SO) < os.path.getmtime(src):
         tmp = f"{SO}.{os.getpid()}.tmp"  # build aside and rename: parallel test workers never load a partial .so
-        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-DFE_BOUNDS_CHECK", "-DFE_OP_COUNT", "-fPIC", "-shared",
-                               "-o", tmp, src])
+        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-DFE_BOUNDS_CHECK", "-DFE_OP_COUNT", *DEFS, "-fPIC",
+                               "-shared", "-o", tmp, src])
         os.replace(tmp, SO)
     return ctypes.CDLL(SO)
 

@@ -33,6 +33,9 @@ static struct {
   dv_fn dv;
   d2i_pubkey_fn d2i_pubkey;
   md_fn sha256;
+  void* (*md_fetch)(void*, const char*, const char*);
+  void (*md_free)(void*);
+  int (*md_ctx_reset)(void*);
   int ok;
 } F;
 
@@ -48,8 +51,11 @@ static int load(void) {
   F.dv = (dv_fn)dlsym(h, "EVP_DigestVerify");
   F.d2i_pubkey = (d2i_pubkey_fn)dlsym(h, "d2i_PUBKEY");
   F.sha256 = (md_fn)dlsym(h, "EVP_sha256");
+  F.md_fetch = (void* (*)(void*, const char*, const char*))dlsym(h, "EVP_MD_fetch");
+  F.md_free = (void (*)(void*))dlsym(h, "EVP_MD_free");
+  F.md_ctx_reset = (int (*)(void*))dlsym(h, "EVP_MD_CTX_reset");
   F.ok = F.pkey_new_raw && F.md_ctx_new && F.md_ctx_free && F.pkey_free && F.dv_init && F.dv && F.d2i_pubkey &&
-         F.sha256;
+         F.sha256 && F.md_fetch && F.md_free && F.md_ctx_reset;
   return F.ok;
 }
 
@@ -114,57 +120,48 @@ int64_t ob_check_txs(const cg_key* keys, uint32_t n_keys, const cg_item* items, 
 }
 
 /* ---- the headline mix (bench.py cpu_baseline.openssl): every item verified independently --------
- * Ed25519 through EVP_PKEY_new_raw_public_key; ECDSA (secp256r1 / secp256k1, raw 64-byte X||Y keys
- * wrapped in the curve's SubjectPublicKeyInfo header, or SPKI keys as given) through d2i_PUBKEY and
- * EVP_DigestVerify with SHA-256 over the DER signature. A fresh EVP_PKEY per item, as the JVM builds
- * a PublicKey per deserialised signature. Status: 0 valid, 1 anything else. */
+ * Ed25519 keys through EVP_PKEY_new_raw_public_key; ECDSA keys (secp256r1 / secp256k1, raw 64-byte
+ * X||Y wrapped in the curve's SubjectPublicKeyInfo header, or SPKI as given) through d2i_PUBKEY;
+ * each key decoded ONCE per call (inside the timed call) and shared read-only by the workers, as
+ * Crypto.doVerify receives an already-decoded PublicKey. A per-item decode serialises on OpenSSL
+ * 3.0's decoder locks (16 threads ran slower than one: profiles/r03/v8/bench_full.json). Then
+ * EVP_DigestVerify, SHA-256 fetched once for ECDSA. Status: 0 valid, 1 anything else. */
 static const uint8_t SPKI_R1[26] = {0x30, 0x59, 0x30, 0x13, 0x06, 0x07, 0x2a, 0x86, 0x48, 0xce, 0x3d, 0x02, 0x01,
                                     0x06, 0x08, 0x2a, 0x86, 0x48, 0xce, 0x3d, 0x03, 0x01, 0x07, 0x03, 0x42, 0x00};
 static const uint8_t SPKI_K1[23] = {0x30, 0x56, 0x30, 0x10, 0x06, 0x07, 0x2a, 0x86, 0x48, 0xce, 0x3d, 0x02,
                                     0x01, 0x06, 0x05, 0x2b, 0x81, 0x04, 0x00, 0x0a, 0x03, 0x42, 0x00};
 
-static int verify_item_any(const cg_key* k, const cg_item* it, const uint8_t* arena, uint64_t arena_len) {
-  if (k->off + k->len > arena_len || it->sig_off + it->sig_len > arena_len || it->msg_off + it->msg_len > arena_len)
-    return 0;
-  void* pk = NULL;
-  const void* md = NULL;
+static void* decode_key(const cg_key* k, const uint8_t* arena, uint64_t arena_len) {
+  if (k->off + k->len > arena_len) return NULL;
   if (k->scheme == CG_EDDSA_ED25519_SHA512) {
-    if (k->fmt != CG_KEY_RAW || k->len != 32) return 0;
-    pk = F.pkey_new_raw(NID_ED25519_, NULL, arena + k->off, 32);
-  } else if (k->scheme == CG_ECDSA_SECP256R1_SHA256 || k->scheme == CG_ECDSA_SECP256K1_SHA256) {
-    uint8_t der[128];
-    const uint8_t* p = der;
-    long n = 0;
-    if (k->fmt == CG_KEY_RAW && k->len == 64) {
-      const uint8_t* hdr = k->scheme == CG_ECDSA_SECP256R1_SHA256 ? SPKI_R1 : SPKI_K1;
-      const int hl = k->scheme == CG_ECDSA_SECP256R1_SHA256 ? 26 : 23;
-      for (int i = 0; i < hl; ++i) der[i] = hdr[i];
-      der[hl] = 0x04;
-      for (int i = 0; i < 64; ++i) der[hl + 1 + i] = arena[k->off + i];
-      n = hl + 65;
-    } else if (k->fmt == CG_KEY_SPKI && k->len <= sizeof der) {
-      for (int i = 0; i < k->len; ++i) der[i] = arena[k->off + i];
-      n = k->len;
-    } else {
-      return 0;
-    }
-    pk = F.d2i_pubkey(NULL, &p, n);
-    md = F.sha256();
-  } else {
-    return 0;
+    if (k->fmt != CG_KEY_RAW || k->len != 32) return NULL;
+    return F.pkey_new_raw(NID_ED25519_, NULL, arena + k->off, 32);
   }
-  if (!pk) return 0;
-  void* ctx = F.md_ctx_new();
-  int ok = ctx && F.dv_init(ctx, NULL, md, NULL, pk) == 1 &&
-           F.dv(ctx, arena + it->sig_off, it->sig_len, arena + it->msg_off, it->msg_len) == 1;
-  if (ctx) F.md_ctx_free(ctx);
-  F.pkey_free(pk);
-  return ok;
+  if (k->scheme != CG_ECDSA_SECP256R1_SHA256 && k->scheme != CG_ECDSA_SECP256K1_SHA256) return NULL;
+  uint8_t der[128];
+  const uint8_t* p = der;
+  long n = 0;
+  if (k->fmt == CG_KEY_RAW && k->len == 64) {
+    const uint8_t* hdr = k->scheme == CG_ECDSA_SECP256R1_SHA256 ? SPKI_R1 : SPKI_K1;
+    const int hl = k->scheme == CG_ECDSA_SECP256R1_SHA256 ? 26 : 23;
+    for (int i = 0; i < hl; ++i) der[i] = hdr[i];
+    der[hl] = 0x04;
+    for (int i = 0; i < 64; ++i) der[hl + 1 + i] = arena[k->off + i];
+    n = hl + 65;
+  } else if (k->fmt == CG_KEY_SPKI && k->len <= sizeof der) {
+    for (int i = 0; i < k->len; ++i) der[i] = arena[k->off + i];
+    n = k->len;
+  } else {
+    return NULL;
+  }
+  return F.d2i_pubkey(NULL, &p, n);
 }
 
 typedef struct {
   const cg_key* keys;
   uint32_t n_keys;
+  void** pkeys;
+  const void* sha256;
   const cg_item* items;
   uint64_t n;
   const uint8_t* arena;
@@ -173,19 +170,46 @@ typedef struct {
   uint64_t next;
 } items_job_t;
 
+static void* keys_worker(void* p) {
+  items_job_t* j = (items_job_t*)p;
+  for (;;) {
+    const uint64_t k = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+    if (k >= j->n_keys) break;
+    j->pkeys[k] = decode_key(&j->keys[k], j->arena, j->arena_len);
+  }
+  return NULL;
+}
+
 static void* items_worker(void* p) {
   items_job_t* j = (items_job_t*)p;
+  void* ctx = F.md_ctx_new();
   for (;;) {
     const uint64_t b = __atomic_fetch_add(&j->next, 256, __ATOMIC_RELAXED);
     if (b >= j->n) break;
     const uint64_t e = b + 256 < j->n ? b + 256 : j->n;
     for (uint64_t i = b; i < e; ++i) {
       const cg_item* it = &j->items[i];
-      j->status[i] = it->key_idx < j->n_keys && verify_item_any(&j->keys[it->key_idx], it, j->arena, j->arena_len)
-                         ? 0 : 1;
+      void* pk = it->key_idx < j->n_keys ? j->pkeys[it->key_idx] : NULL;
+      int ok = 0;
+      if (pk && ctx && it->sig_off + it->sig_len <= j->arena_len && it->msg_off + it->msg_len <= j->arena_len) {
+        const void* md = j->keys[it->key_idx].scheme == CG_EDDSA_ED25519_SHA512 ? NULL : j->sha256;
+        ok = F.dv_init(ctx, NULL, md, NULL, pk) == 1 &&
+             F.dv(ctx, j->arena + it->sig_off, it->sig_len, j->arena + it->msg_off, it->msg_len) == 1;
+        F.md_ctx_reset(ctx);
+      }
+      j->status[i] = ok ? 0 : 1;
     }
   }
+  if (ctx) F.md_ctx_free(ctx);
   return NULL;
+}
+
+static void run_workers(void* (*fn)(void*), items_job_t* j, int nthreads) {
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+  j->next = 0;
+  for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, fn, j);
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  free(th);
 }
 
 /* Returns n, or -1 when libcrypto.so.3 cannot be loaded. */
@@ -193,10 +217,14 @@ int64_t ob_verify_items(const cg_key* keys, uint32_t n_keys, const cg_item* item
                         uint64_t arena_len, uint8_t* status, int nthreads) {
   if (!load()) return -1;
   if (nthreads <= 0) nthreads = 1;
-  items_job_t j = {keys, n_keys, items, n, arena, arena_len, status, 0};
-  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
-  for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, items_worker, &j);
-  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
-  free(th);
+  void* sha256 = F.md_fetch(NULL, "SHA256", NULL);
+  void** pkeys = (void**)calloc(n_keys ? n_keys : 1, sizeof(void*));
+  items_job_t j = {keys, n_keys, pkeys, sha256, items, n, arena, arena_len, status, 0};
+  run_workers(keys_worker, &j, nthreads);
+  run_workers(items_worker, &j, nthreads);
+  for (uint32_t k = 0; k < n_keys; ++k)
+    if (pkeys[k]) F.pkey_free(pkeys[k]);
+  free(pkeys);
+  if (sha256) F.md_free(sha256);
   return (int64_t)n;
 }

@@ -1,6 +1,6 @@
 """Per-launch HBM traffic and VALU issue of the item kernels from rocprofv3 passes
 (tools/profile_r02.sh: --kernel-trace --stats, then --pmc FETCH_SIZE, --pmc WRITE_SIZE and an SQ pass,
-each its own process), written to profiles/r02/pmc_traffic.json for bench.py's roofline.
+each its own process), written to profiles/r03/pmc_traffic.json for bench.py's roofline.
 
 HBM bytes (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE tallies 128-B requests at 64 B,
 so a wide streaming read reports half its bytes: hbm = 2*FETCH_SIZE + WRITE_SIZE (KB * 1024). The
@@ -22,7 +22,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_ed_hash", "k_ed_ladder_pf", "k_ed_ladder_wide", "k_ed_finish", "k_ec_prep<1>", "k_ec_inv<1>",
+KERNELS = ("k_ed_hash", "k_ed_hash<true>", "k_ed_hash<false>", "k_ec_prep<1, true>", "k_ec_prep<0, true>",
+           "k_ec_prep<1, false>", "k_ec_prep<0, false>", "k_ed_ladder_pf", "k_ed_ladder_wide", "k_ed_finish", "k_ec_prep<1>", "k_ec_inv<1>",
            "k_ec_ladder<1, true>", "k_ec_ladder_wide<1>", "k_ec_prep<0>", "k_ec_inv<0>", "k_ec_ladder<0, true>",
            "k_ec_ladder_wide<0>", "k_ed_wide_fwd", "k_ed_wide_inv", "k_ed_wide_bwd", "k_ec_wide_fwd<1>",
            "k_ec_wide_bwd<1>", "k_ec_wide_fwd<0>", "k_ec_wide_bwd<0>", "k_ec_wide_inv<1>", "k_ec_wide_inv<0>",
@@ -98,7 +99,8 @@ def main():
             if "SQ_INSTS_VALU_INT64" in v:
                 k["valu"]["int64_frac"] = round(v["SQ_INSTS_VALU_INT64"] / v["SQ_INSTS_VALU"], 3)
                 k["valu"]["int32_frac"] = round(v["SQ_INSTS_VALU_INT32"] / v["SQ_INSTS_VALU"], 3)
-            mix = mixes.get(n)
+            mix = mixes.get(n) or mixes.get(n.replace(", true>", ">").replace(", false>", ">").replace("<true>", "")
+                                            .replace("<false>", ""))
             if mix:
                 t = v["SQ_INSTS_VALU"] / 1024 * mix["mean_ns_per_wave_instr"] * 1e-6
                 k["valu"]["issue_ms_per_opcode_model"] = round(t, 3)
@@ -118,8 +120,8 @@ def main():
     with open(os.path.join(dest, "pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     if os.environ.get("PMC_TRAFFIC_HEADLINE", "1") == "1":  # the file bench.py's roofline reads
-        os.makedirs(os.path.join(ROOT, "profiles", "r02"), exist_ok=True)
-        with open(os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"), "w") as f:
+        os.makedirs(os.path.join(ROOT, "profiles", "r03"), exist_ok=True)
+        with open(os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"), "w") as f:
             json.dump(out, f, indent=1)
     print(json.dumps({n: (k.get("hbm_bytes_per_launch"), k.get("valu", {}).get("issue_frac"),
                           k.get("trace", {}).get("avg_ms")) for n, k in kern.items()}))

@@ -68,7 +68,8 @@ MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
                           (ED_INVERT_FE[0] * MAC_PER_MUL + ED_INVERT_FE[1] * MAC_PER_SQ) / ED_FINISH_K)
 # ECDSA: field products (mont29.h) per item: (k_ec_ladder full tables mod p, k_ec_inv mod n
 # per 16 items). A Montgomery product = 81 a*b MACs + 9 per non-zero 29-bit limb of the modulus
-# (q*m); secp256k1's p is folded instead (pseudo-Mersenne, plain form): 81 + 9 + 2 MACs.
+# (q*m); secp256r1's p telescopes its all-ones limbs (q*m = 4 MACs: 2^9, 2^18, limbs 7 and 8);
+# secp256k1's p is folded instead (pseudo-Mersenne, plain form): 81 + 9 + 2 MACs.
 # The ladder figure is its full schedule (every digit non-zero): a lane whose digit is zero skips
 # its addition, but the wave issues it for the other 63 lanes, so the full schedule is what the
 # SIMD executes (per-item mean 1% lower).
@@ -80,7 +81,7 @@ KEY_WIDE_MIN_USES = {4: int(os.environ.get("CG_WIDE_MIN_USES_ED", 1536)), 3: int
                      2: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512))}
 EC_INV_K = 8  # items per k_ec_inv lane (corda_amd/csrc/ecdsa_rows.h)
 EC_INV_MUL_K = {"secp256r1": 480, "secp256k1": 507}  # products of one lane: prefix, inversion, unwinding
-EC_MAC_PER_MUL_P = {"secp256r1": 144, "secp256k1": 162}
+EC_MAC_PER_MUL_P = {"secp256r1": 117, "secp256k1": 92}
 EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13

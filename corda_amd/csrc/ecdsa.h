@@ -338,6 +338,10 @@ CG_HD void m29_r2(f29& r) {
   f29 x;
   f29_zero(x);
   x.v[0] = 1;
+  if (m29_plain(C, N)) {  // plain form (mont29.h): R = 1
+    r = x;
+    return;
+  }
   for (int i = 0; i < 522; ++i) m29_add<C, N>(x, x, x);
   m29_canon<C, N>(r, x);
 }

@@ -134,10 +134,109 @@ CG_HD uint32_t m29_opaque(uint32_t v) {
   return v;
 }
 
+// secp256k1's field prime p = 2^256 - 2^32 - 977 is pseudo-Mersenne: its elements are kept in
+// PLAIN form (R = 1 in everything below: m29_r2 gives 1, so the "Montgomery" conversions are
+// identities) and a product is folded instead of Montgomery-reduced. The fold uses
+// 2^261 = 32 * 2^256 = 2^37 + 31264 (mod p): 81 + 11 MACs per product instead of 162.
+#ifndef CG_M29_K1_PLAIN  // 0: secp256k1 p in Montgomery form like the other moduli (A/B builds)
+#define CG_M29_K1_PLAIN 1
+#endif
+constexpr bool m29_plain(int C, int N) { return CG_M29_K1_PLAIN && C == 0 && N == 0; }
+
+// r = a b mod p (p = 2^256 - 2^32 - 977) for limbs < 2^30 (a b < 2^524); r reduced (< 2p). The low nine product columns stay raw 64-bit sums (no carries); the high eight
+// are product-scanned into 29-bit limbs H, folded into the low columns (H_m 31264 into column m,
+// H_m 2^8 into column m + 1), then one carry chain; bits >= 256 fold once more (x 977, x 2^32).
+CG_HD void m29_mul_k1p(f29& r, const f29& a, const f29& b) {
+  fe_acc_t c[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    fe_acc_t s = 0;
+#pragma unroll
+    for (int i = 0; i <= k; ++i) s += (fe_acc_t)((uint64_t)a.v[i] * b.v[k - i]);
+    c[k] = s;
+  }
+  uint32_t H[9];
+  fe_acc_t acc = 0;
+#pragma unroll
+  for (int k = 9; k < 17; ++k) {
+#pragma unroll
+    for (int i = k - 8; i < 9; ++i) acc += (fe_acc_t)((uint64_t)a.v[i] * b.v[k - i]);
+    FE_ASSERT(acc < ((fe_acc_t)1 << 64));
+    H[k - 9] = (uint32_t)acc & M29_MASK;
+    acc >>= 29;
+  }
+  FE_ASSERT(acc < ((fe_acc_t)1 << 31));  // a b < 2^524
+  H[8] = (uint32_t)acc;
+  // 2^261 = 2^37 + 31264 (mod p): H_m 2^{29m} 2^261 -> H_m 31264 (column m) + H_m 2^8 (column m + 1)
+  const uint32_t k31264 = m29_opaque(31264u), k256 = m29_opaque(256u);  // MACs, not shift pairs
+#pragma unroll
+  for (int m = 0; m < 9; ++m) {
+    c[m] += (fe_acc_t)((uint64_t)H[m] * k31264);
+    if (m < 8) c[m + 1] += (fe_acc_t)((uint64_t)H[m] * k256);
+  }
+  uint32_t M[9];
+  acc = 0;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    acc += c[j];
+    FE_ASSERT(acc >= c[j]);  // no 64-bit wrap
+    M[j] = (uint32_t)acc & M29_MASK;
+    acc >>= 29;
+  }
+  acc += (fe_acc_t)H[8] << 8;  // H_8's 2^8 term: weight 2^261 again
+  FE_ASSERT(acc < ((fe_acc_t)1 << 40));
+  // bits >= 256: top 2^261 (31264 into limb 0, 2^8 into limb 1) and M[8] >> 24 (977, 2^3)
+  const fe_acc_t top = acc;
+  const uint32_t t = M[8] >> 24;
+  M[8] &= 0xffffffu;
+  acc = top * 31264u + (fe_acc_t)(t * 977u) + M[0];
+  uint32_t out[9];
+  out[0] = (uint32_t)acc & M29_MASK;
+  acc >>= 29;
+  acc += ((fe_acc_t)top << 8) + (fe_acc_t)(t << 3) + M[1];
+  out[1] = (uint32_t)acc & M29_MASK;
+  uint32_t cy = (uint32_t)(acc >> 29);  // < 2^19: the rest of the chain in 32 bits
+#pragma unroll
+  for (int j = 2; j < 9; ++j) {
+    const uint32_t x = M[j] + cy;
+    out[j] = j < 8 ? x & M29_MASK : x;
+    cy = x >> 29;
+  }
+  FE_ASSERT(out[8] < (1u << 29));
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = out[i];
+}
+
+// secp256r1's p = 2^256 - 2^224 + 2^192 + 2^96 - 1 in 29-bit limbs is (2^29-1, 2^29-1, 2^29-1,
+// 2^9-1, 0, 0, 2^18, 2^29-2^21, 2^24-1): the run of all-ones limbs telescopes, limbs 0..3 being
+// 2^96 - 1. With -p^-1 = 1 (mod 2^29) the Montgomery digit q is the column's low 29 bits, so the -q
+// term only clears bits the column shift drops: q p costs four MACs (2^9, 2^18, limbs 7 and 8)
+// instead of seven.
+#ifndef CG_M29_R1_TELESCOPE  // 0: seven MACs per digit (A/B builds)
+#define CG_M29_R1_TELESCOPE 1
+#endif
+constexpr bool m29_r1p_tel(int C, int N) { return CG_M29_R1_TELESCOPE && C == 1 && N == 0; }
+static_assert(m29_limb(1, 0, 1, 0) == M29_MASK && m29_limb(1, 0, 1, 1) == M29_MASK && m29_limb(1, 0, 1, 2) == M29_MASK &&
+                  m29_limb(1, 0, 1, 3) == 0x1ffu && m29_limb(1, 0, 1, 4) == 0 && m29_limb(1, 0, 1, 5) == 0 &&
+                  m29_limb(1, 0, 1, 6) == (1u << 18) && m29_ninv(1, 0) == 1u,
+              "secp256r1 p limbs as the telescoped reduction assumes");
+
 // r = a b R^-1 mod m, product scanning (bounds: header). r is reduced.
 template <int C, int N>
 CG_HD void m29_mul(f29& r, const f29& a, const f29& b) {
   M29_COUNT(C, N);
+  if constexpr (m29_plain(C, N)) {
+    m29_mul_k1p(r, a, b);
+#ifdef FE_BOUNDS_CHECK
+    int32_t br = 0;
+    for (int i = 0; i < 9; ++i) {
+      const int32_t d = (int32_t)r.v[i] - (int32_t)m29_limb(C, N, 2, i) + br;
+      br = d >> 29;
+    }
+    FE_ASSERT(br < 0);
+#endif
+    return;
+  }
   uint32_t q[9], out[9];
   fe_acc_t acc = 0;
 #pragma unroll
@@ -150,16 +249,23 @@ CG_HD void m29_mul(f29& r, const f29& a, const f29& b) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
       const int j = k - i;
-      if (i < k && j >= 0 && j < 9 && m29_limb(C, N, 1, j) != 0)
+      if (!(i < k && j >= 0 && j < 9)) continue;
+      if (m29_r1p_tel(C, N)) {  // q p = q (2^96 - 1 + 2^192 + p7 2^203 + p8 2^232): see m29_r1p_tel
+        if (j == 3) acc += (fe_acc_t)((uint64_t)q[i] * m29_opaque(1u << 9));  // one MAC, not shift + masks
+        if (j == 6) acc += (fe_acc_t)((uint64_t)q[i] * m29_opaque(1u << 18));
+        if (j >= 7) acc += (fe_acc_t)((uint64_t)q[i] * m29_limb(C, N, 1, j));
+      } else if (m29_limb(C, N, 1, j) != 0) {
         acc += (fe_acc_t)((uint64_t)q[i] *
                           (m29_pow2(m29_limb(C, N, 1, j)) ? m29_opaque(m29_limb(C, N, 1, j)) : m29_limb(C, N, 1, j)));
+      }
     }
     if (k < 9) {
       const uint32_t qk = m29_ninv(C, N) == 1u ? ((uint32_t)acc & M29_MASK)
                                                 : (((uint32_t)acc * m29_ninv(C, N)) & M29_MASK);
       q[k] = qk;
-      acc += (fe_acc_t)((uint64_t)qk * m29_limb(C, N, 1, 0));
-      FE_ASSERT(((uint64_t)acc & M29_MASK) == 0);
+      // telescoped: the -q term clears the low 29 bits, which the shift below drops anyway
+      if (!m29_r1p_tel(C, N)) acc += (fe_acc_t)((uint64_t)qk * m29_limb(C, N, 1, 0));
+      FE_ASSERT(m29_r1p_tel(C, N) || ((uint64_t)acc & M29_MASK) == 0);
     } else {
       out[k - 9] = (uint32_t)acc & M29_MASK;
     }

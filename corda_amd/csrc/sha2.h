@@ -58,11 +58,47 @@ CG_HD uint64_t cg_rotr64(uint64_t x, int n) {
 #endif
 }
 
-// (e & f) ^ (~e & g) and Maj(a, b, c), each one bitfield select per 32-bit half
+// Three-input XOR and Maj(a, b, c): one v_bitop3_b32 per 32-bit word (truth tables 0x96 and 0xE8,
+// symmetric in the operands). The compiler forms bitop3 from some 32-bit expressions but not from
+// the halves of the 64-bit SHA-512 words.
+CG_HD uint32_t cg_xor3_32(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+CG_HD uint32_t cg_maj32(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+#else
+  return (a & b) | (c & (a | b));
+#endif
+}
+CG_HD uint64_t cg_xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+  return ((uint64_t)cg_xor3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
+         cg_xor3_32((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
+// (e & f) ^ (~e & g): one bitfield select per 32-bit half
 CG_HD uint64_t cg_ch64(uint64_t e, uint64_t f, uint64_t g) { return (e & f) | (~e & g); }
+#ifndef CG_SHA512_BITOP3
+#define CG_SHA512_BITOP3 2  // maj only: the 64-bit xor3 form priced 3% worse (more moves), maj 3% better
+#endif
 CG_HD uint64_t cg_maj64(uint64_t a, uint64_t b, uint64_t c) {
+#if CG_SHA512_BITOP3 & 2
+  return ((uint64_t)cg_maj32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
+         cg_maj32((uint32_t)a, (uint32_t)b, (uint32_t)c);
+#else
   const uint64_t m = a ^ b;
   return (m & c) | (~m & b);
+#endif
+}
+CG_HD uint64_t cg_x3_64(uint64_t a, uint64_t b, uint64_t c) {
+#if CG_SHA512_BITOP3 & 1
+  return cg_xor3_64(a, b, c);
+#else
+  return a ^ b ^ c;
+#endif
 }
 
 // Round constants in constant memory: the rounds run in a rolled loop of 16 unrolled rounds
@@ -129,9 +165,9 @@ CG_HD void sha512_init(uint64_t s[8]) {
 // v[(8 - i) & 7] .. : the caller passes them rotated, so no register moves are needed).
 #define CG_SHA512_ROUND(a, b, c, d, e, f, g, h, k, wi)                                                   \
   {                                                                                                   \
-    const uint64_t t1 = h + (cg_rotr64(e, 14) ^ cg_rotr64(e, 18) ^ cg_rotr64(e, 41)) + cg_ch64(e, f, g) + \
-                        (k) + (wi);                                                                   \
-    const uint64_t t2 = (cg_rotr64(a, 28) ^ cg_rotr64(a, 34) ^ cg_rotr64(a, 39)) + cg_maj64(a, b, c);   \
+    const uint64_t t1 = h + cg_x3_64(cg_rotr64(e, 14), cg_rotr64(e, 18), cg_rotr64(e, 41)) +            \
+                        cg_ch64(e, f, g) + (k) + (wi);                                                \
+    const uint64_t t2 = cg_x3_64(cg_rotr64(a, 28), cg_rotr64(a, 34), cg_rotr64(a, 39)) + cg_maj64(a, b, c); \
     d += t1;                                                                                          \
     h = t1 + t2;                                                                                      \
   }
@@ -150,8 +186,8 @@ CG_HD void sha512_init(uint64_t s[8]) {
 // message schedule word i = r + j (r a multiple of 16, j < 16) into the circular buffer slot j
 CG_HD uint64_t sha512_sched(uint64_t w[16], int j) {
   const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-  const uint64_t s0 = cg_rotr64(w15, 1) ^ cg_rotr64(w15, 8) ^ (w15 >> 7);
-  const uint64_t s1 = cg_rotr64(w2, 19) ^ cg_rotr64(w2, 61) ^ (w2 >> 6);
+  const uint64_t s0 = cg_x3_64(cg_rotr64(w15, 1), cg_rotr64(w15, 8), w15 >> 7);
+  const uint64_t s1 = cg_x3_64(cg_rotr64(w2, 19), cg_rotr64(w2, 61), w2 >> 6);
   w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
   return w[j];
 }
@@ -387,8 +423,8 @@ CG_HD void sha256_init(uint32_t s[8]) {
 #define CG_SHA256_ROUND(a, b, c, d, e, f, g, h, k, wi)                                                    \
   {                                                                                                    \
     const uint32_t t1 =                                                                                \
-        h + (cg_rotr32(e, 6) ^ cg_rotr32(e, 11) ^ cg_rotr32(e, 25)) + ((e & f) ^ (~e & g)) + (k) + (wi); \
-    const uint32_t t2 = (cg_rotr32(a, 2) ^ cg_rotr32(a, 13) ^ cg_rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c)); \
+        h + cg_xor3_32(cg_rotr32(e, 6), cg_rotr32(e, 11), cg_rotr32(e, 25)) + ((e & f) ^ (~e & g)) + (k) + (wi); \
+    const uint32_t t2 = cg_xor3_32(cg_rotr32(a, 2), cg_rotr32(a, 13), cg_rotr32(a, 22)) + cg_maj32(a, b, c); \
     d += t1;                                                                                           \
     h = t1 + t2;                                                                                       \
   }
@@ -404,8 +440,8 @@ CG_HD void sha256_init(uint32_t s[8]) {
 
 CG_HD uint32_t sha256_sched(uint32_t w[16], int j) {
   const uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-  const uint32_t s0 = cg_rotr32(w15, 7) ^ cg_rotr32(w15, 18) ^ (w15 >> 3);
-  const uint32_t s1 = cg_rotr32(w2, 17) ^ cg_rotr32(w2, 19) ^ (w2 >> 10);
+  const uint32_t s0 = cg_xor3_32(cg_rotr32(w15, 7), cg_rotr32(w15, 18), w15 >> 3);
+  const uint32_t s1 = cg_xor3_32(cg_rotr32(w2, 17), cg_rotr32(w2, 19), w2 >> 10);
   w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
   return w[j];
 }

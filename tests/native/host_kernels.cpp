@@ -418,6 +418,11 @@ static void m29_mul_words(const uint32_t* a, const uint32_t* b, uint32_t* out, i
   m29_mul<C, N>(r, x, y);
   m29_to_words_canon<C, N>(out, r);
 }
+// 1 if (curve, n) elements are kept in plain form (R = 1, mont29.h m29_plain), else 0 (R = 2^261)
+extern "C" int t_m29_plain(int curve, int n) {
+  return curve == 0 && n == 0 ? m29_plain(0, 0) : curve == 0 ? m29_plain(0, 1) : n == 0 ? m29_plain(1, 0) : m29_plain(1, 1);
+}
+
 extern "C" void t_m29_op(int curve, int n, int op, const uint32_t* a, const uint32_t* b, uint32_t* out) {
   // op 0: a b R^-1; 1: (2a)(2b) R^-1 via lazy sums; 2: a + b; 3: a - b (inputs reduced < 2m)
   if (op <= 1) {

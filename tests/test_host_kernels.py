@@ -218,7 +218,9 @@ def test_executed_work_constants_match_lane_code():
 def test_executed_work_constants_ecdsa():
     """bench.py prices the ECDSA ladders and batched inversions with the Montgomery products the
     lane code executes; those constants must equal what the host build counts, and the MACs per
-    product must follow from the moduli's non-zero 29-bit limbs (81 a*b + 9 per limb of q*m)."""
+    product must follow from the moduli's 29-bit limbs: 81 a*b + 9 per non-zero limb of q*m, except
+    secp256r1's p (the all-ones run telescopes: 4 MACs per digit) and secp256k1's p (folded:
+    81 + 9 + 2, mont29.h)."""
     import ctypes
     import bench
     lib = hostk.lib()
@@ -231,7 +233,7 @@ def test_executed_work_constants_ecdsa():
     nnz = lambda m: sum(1 for i in range(9) if (m >> (29 * i)) & (2**29 - 1))  # noqa: E731
     for name, scheme in (("secp256r1", 3), ("secp256k1", 2)):
         p, n = moduli[name]
-        assert bench.EC_MAC_PER_MUL_P[name] == 81 + 9 * nnz(p)
+        assert bench.EC_MAC_PER_MUL_P[name] == {"secp256r1": 81 + 9 * 4, "secp256k1": 81 + 9 + 2}[name]
         assert bench.EC_MAC_PER_MUL_N[name] == 81 + 9 * nnz(n)
         from tools.workload import wl
         b, _ = wl.ecdsa_batch(1 if scheme == 3 else 0, 256, n_keys=8, corrupt_permille=0, seed=3, nthreads=4)
@@ -280,14 +282,16 @@ M29_MODS = {(1, 0): 2 ** 256 - 2 ** 224 + 2 ** 192 + 2 ** 96 - 1,
 
 @pytest.mark.parametrize("curve,n", sorted(M29_MODS))
 def test_mont29_ops(curve, n):
-    """mont29.h (ECDSA field / scalar arithmetic) against Python integers, including values
+    """mont29.h (ECDSA field / scalar arithmetic; secp256k1's p by the pseudo-Mersenne fold) against
+    Python integers, including values
     in [m, 2m) (the reduced range) and the lazy-sum operands, with every column bound asserted."""
     import ctypes
     lib = hostk.lib()
     lib.t_m29_op.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_void_p]
     m = M29_MODS[(curve, n)]
-    rinv = pow(2 ** 261, -1, m)
+    # R = 2^261 (Montgomery) or 1 (secp256k1 p in plain form, folded products)
+    rinv = 1 if lib.t_m29_plain(curve, n) else pow(2 ** 261, -1, m)
     rng = random.Random(curve * 2 + n)
     edge = [0, 1, m - 1, m, m + 1, 2 * m - 1, 2 ** 256 - 1 if 2 ** 256 - 1 < 2 * m else 2 * m - 2]
     vals = edge + [rng.randrange(0, 2 * m) for _ in range(300)]

@@ -56,7 +56,7 @@ MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # Ed25519 (field multiplies, squarings) in the radix-2^25.5 representation (fe25519.h):
 ED_VERIFY_FE = (402, 24)   # k_ed_ladder_pf: 43 + 12 mixed additions + 6 doublings
 ED_WIDE_FE = (307, 0)      # k_ed_ladder_wide: 32 + 12 mixed additions, no doublings (keys with wide tables)
-ED_WIDE_BUILD_FE = (100135, 13472)  # one key's wide table: 248-doubling chain, 32 rows x 4 groups of 32 entries walked twice (chunk Z products, then entries), one inversion per row
+ED_WIDE_BUILD_FE = (62279, 9120)  # one key's wide table: 248-doubling chain, then per row one lane walking its 128 entries, one inversion, the walk back (k_ed_wide_rows)
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
 ED_FINISH_K = 16
@@ -86,7 +86,7 @@ EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
 # kernel generation whose PMC traffic profile is committed (profiles/r03/pmc_traffic.json)
-KERNEL_VERSION = "r03_v8"
+KERNEL_VERSION = "r03_v9"
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
 
 # Appendix A labels (tools/workload) -> the verdict Crypto.doVerify gives them (key decodes)

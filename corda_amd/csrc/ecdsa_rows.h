@@ -569,6 +569,115 @@ CG_HD void ec_wide_group_pass(EcAff* out, f29* zc, const EcAff& base, int j, int
   }
 }
 
+// ---- wide-table rows by co-Z additions (round 3): one lane per (wide key, row j) walks the row's
+// multiples k B of its affine base B with Meloni's ZADDU, the co-Z addition with update (T + B' and
+// B' re-expressed at the sum's Z, 4M + 2S; "New point addition formulae for ECC applications",
+// WAIFI 2007). The new Z is the old one times lambda = X_B' - X_T, so only the lambdas are kept; one
+// inversion per row then normalises every entry walking back (Z_{k-1}^-1 = lambda_k Z_k^-1, 4
+// products per entry): ~14 products per entry against the three-pass form's ~37, no group-start
+// scalar multiplications, and one launch. The un-normalised X, Y wait in the row's output
+// entries, the lambdas in its scratch. A valid key has prime order n > 256, so T = +-B' never
+// happens (lambda != 0).
+// (T, B') <- (B' + T, B' at the sum's Z); lam = X_B' - X_T
+template <int C>
+CG_HD void ec_zaddu(f29& XT, f29& YT, f29& XB, f29& YB, f29& lam) {
+  f29 c, w1, w2, t, d, a1, u;
+  m29_sub<C, 0>(lam, XB, XT);
+  m29_sq<C, 0>(c, lam);
+  m29_mul<C, 0>(w1, XB, c);
+  m29_mul<C, 0>(w2, XT, c);
+  m29_sub2<C, 0>(t, YB, YT);  // product operand only
+  m29_sq<C, 0>(d, t);
+  m29_sub2<C, 0>(u, w1, w2);
+  m29_mul<C, 0>(a1, YB, u);
+  m29_sub<C, 0>(XT, d, w1);
+  m29_sub<C, 0>(XT, XT, w2);
+  m29_sub2<C, 0>(u, w1, XT);
+  m29_mul<C, 0>(YT, t, u);
+  m29_sub<C, 0>(YT, YT, a1);
+  XB = w1;
+  YB = a1;
+}
+
+// 2B (X, Y at Z = 2y) and B at the same Z from an affine B = (x, y): DBLU, 2M + 4S
+template <int C>
+CG_HD void ec_dblu_aff(f29& XT, f29& YT, f29& XB, f29& YB, f29& Z, const f29& x, const f29& y, const EcConsts& K) {
+  f29 xx, yy, s, l, m, t;
+  m29_sq<C, 0>(xx, x);
+  m29_sq<C, 0>(yy, y);
+  m29_mul<C, 0>(s, x, yy);
+  m29_add<C, 0>(s, s, s);
+  m29_add<C, 0>(s, s, s);  // S = 4 x y^2
+  m29_sq<C, 0>(l, yy);
+  m29_add<C, 0>(l, l, l);
+  m29_add<C, 0>(l, l, l);
+  m29_add<C, 0>(l, l, l);  // 8 y^4
+  if (C == CG_CURVE_R1) {  // M = 3 x^2 + a, a = -3
+    m29_sub<C, 0>(t, xx, K.one_p);
+    m29_add<C, 0>(m, t, t);
+    m29_add<C, 0>(m, m, t);
+  } else {  // a = 0
+    m29_add<C, 0>(m, xx, xx);
+    m29_add<C, 0>(m, m, xx);
+  }
+  m29_sq<C, 0>(XT, m);
+  m29_sub<C, 0>(XT, XT, s);
+  m29_sub<C, 0>(XT, XT, s);  // M^2 - 2S
+  m29_sub2<C, 0>(t, s, XT);
+  m29_mul<C, 0>(YT, m, t);
+  m29_sub<C, 0>(YT, YT, l);  // M (S - X) - 8 y^4
+  XB = s;
+  YB = l;
+  m29_add<C, 0>(Z, y, y);
+}
+
+// Row j's 128 affine multiples into out[0..127] (top = row 32: multiples 129..256 of the top row's
+// base, started from 128 B by seven doublings); lam[0..127] is scratch.
+template <int C>
+CG_HD void ec_wide_row_build(EcAff* out, f29* lam, const EcAff& base, bool top, const EcConsts& K) {
+  f29 XT, YT, XB, YB, Z;
+  int e_lo;  // the first chained entry
+  if (!top) {
+    out[0] = base;
+    ec_dblu_aff<C>(XT, YT, XB, YB, Z, base.x, base.y, K);
+    out[1].x = XT;
+    out[1].y = YT;
+    e_lo = 1;
+  } else {
+    Jac F = {base.x, base.y, K.one_p};
+    for (int i = 0; i < 7; ++i) jac_dbl<C>(F, F);
+    f29 z2, z3;
+    m29_sq<C, 0>(z2, F.Z);
+    m29_mul<C, 0>(z3, z2, F.Z);
+    m29_mul<C, 0>(XB, base.x, z2);
+    m29_mul<C, 0>(YB, base.y, z3);
+    XT = F.X;
+    YT = F.Y;
+    Z = F.Z;
+    e_lo = 0;
+  }
+#pragma unroll 1
+  for (int e = e_lo == 0 ? 0 : 2; e < EC_WIDE_MULT; ++e) {
+    ec_zaddu<C>(XT, YT, XB, YB, lam[e]);  // Z_e = Z_{e-1} lam[e]
+    m29_mul<C, 0>(Z, Z, lam[e]);
+    out[e].x = XT;
+    out[e].y = YT;
+  }
+  f29 inv;
+  m29_inv<C, 0>(inv, Z, K.one_p);
+#pragma unroll 1
+  for (int e = EC_WIDE_MULT - 1; e >= e_lo; --e) {
+    f29 zi2, zi3, x, y;
+    m29_sq<C, 0>(zi2, inv);
+    m29_mul<C, 0>(zi3, zi2, inv);
+    m29_mul<C, 0>(x, out[e].x, zi2);
+    m29_mul<C, 0>(y, out[e].y, zi3);
+    out[e].x = x;
+    out[e].y = y;
+    if (e > e_lo) m29_mul<C, 0>(inv, inv, lam[e]);  // 1 / Z_{e-1}
+  }
+}
+
 // in place: z[g] <- 1 / z[g] mod p for the NG products of one row (prefix products in pre[])
 template <int C, int NG>
 CG_HD void m29_invert_run(f29* z, f29* pre, const EcConsts& K) {

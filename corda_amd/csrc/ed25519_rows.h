@@ -621,6 +621,56 @@ CG_HD void fe_invert_run(fe* z, fe* pre) {
   fe_copy(z[0], inv);
 }
 
+// Wide-table row in one lane (round 3): R walks the row's 128 multiples k P by cached additions,
+// each multiple's X, Y, Z parked in its output entry and the running Z product in pre[k]; one
+// inversion (with the 1/2 of the half-scaled entries), then the walk back writes the normalised
+// entries (zi = inv pre[k-1], inv <- inv Z_k, four products per entry). ~15 products per entry
+// against the three-pass form's ~30 (no group-start scalar multiplications, nothing walked
+// twice), and one launch instead of three.
+CG_HD void ed_wide_row_build(ge_niels* out, fe* pre, const ge_p3& P, const fe& d2) {
+  ge_cached c;
+  ge_p3_to_cached(c, P, d2);
+  ge_p3 R = P;
+  fe run;
+#pragma unroll 1
+  for (int k = 0; k < EdWideCfg::kMult; ++k) {
+    if (k > 0) {
+      ge_p1p1 t;
+      ge_add_cached(t, R, c);
+      ge_p1p1_to_p3(R, t);
+      fe_mul(run, run, R.Z);
+    } else {
+      fe_copy(run, R.Z);
+    }
+    out[k].ypx = R.X;  // un-normalised X, Y, Z until the walk back
+    out[k].ymx = R.Y;
+    out[k].xy2d = R.Z;
+    pre[k] = run;
+  }
+  fe inv, h, d4;
+  fe_invert(inv, run);
+  fe_half(h);
+  fe_mul(inv, inv, h);  // 1 / (2 Z_0 .. Z_127): the half-scaled entries' 1/2
+  fe_add(d4, d2, d2);
+  fe_carry(d4);
+#pragma unroll 1
+  for (int k = EdWideCfg::kMult - 1; k >= 0; --k) {
+    ge_p2 p;
+    p.X = out[k].ypx;
+    p.Y = out[k].ymx;
+    fe zi;
+    if (k > 0) {
+      fe_mul(zi, inv, pre[k - 1]);
+      fe_mul(inv, inv, out[k].xy2d);
+    } else {
+      fe_copy(zi, inv);
+    }
+    ge_niels n;
+    ed_niels_from(n, p, zi, d4);
+    out[k] = n;
+  }
+}
+
 // ---------------------------------------------------------------- full / row-0 tables + wide B
 // R' = h (-A) + S' B for keys with full tables (W/K rows of -A, K windows, (K-1) W doublings) or
 // row 0 only (Horner, 252 doublings), with S' B from the constant radix-2^ED_WIDE_BW table at the

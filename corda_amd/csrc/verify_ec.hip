@@ -170,6 +170,22 @@ __global__ void __launch_bounds__(64) k_ec_wide_bwd(uint32_t n_keys, const EdKey
                               ws.bases[L.j < EC_WIDE_DIGITS ? L.j : EC_WIDE_DIGITS - 1], (int)L.j, (int)L.g, c_ec[C]);
 }
 
+// one lane per (wide key, row): the row's 128 affine multiples by co-Z additions, one launch
+// (ecdsa_rows.h ec_wide_row_build; replaces the three passes above unless CG_EC_WIDE_COZ=0)
+template <int C>
+__global__ void __launch_bounds__(64) k_ec_wide_rows(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                     const uint32_t* __restrict__ wide,
+                                                     const uint32_t* __restrict__ wide_count,
+                                                     const uint32_t* __restrict__ wide_idx, EcWideSlot* __restrict__ wec) {
+  const EcWideLane L = ec_wide_lane(EC_WIDE_ROWS, 1);
+  EC_WIDE_KEY(C, L);
+  ec_wide_row_build<C>(ws.tab.t[L.j], ws.s[L.j].z, ws.bases[L.j < EC_WIDE_DIGITS ? L.j : EC_WIDE_DIGITS - 1],
+                       L.j == EC_WIDE_DIGITS, c_ec[C]);
+}
+#ifndef CG_EC_WIDE_COZ
+#define CG_EC_WIDE_COZ 1
+#endif
+
 // G wide rows: the row bases 2^{EC_WIDE_GW u} G first (one lane per row, into scratch slot 0),
 // then one lane per (row u, group g of 32 multiples) in batches over scratch slots 1..
 template <int C>
@@ -444,12 +460,17 @@ static void launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const Key
     const uint32_t* wl = (const uint32_t*)w.wide;
     const uint32_t* wc = (const uint32_t*)w.wide_count;
     const uint32_t* wi = (const uint32_t*)w.wide_idx;
-    hipLaunchKernelGGL(k_ec_wide_fwd<C>, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
-                       wc, wi, w.wec);
-    hipLaunchKernelGGL(k_ec_wide_inv<C>, dim3((unsigned)((rl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
-                       wc, wi, w.wec);
-    hipLaunchKernelGGL(k_ec_wide_bwd<C>, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
-                       wc, wi, w.wec);
+    if (CG_EC_WIDE_COZ) {
+      hipLaunchKernelGGL(k_ec_wide_rows<C>, dim3((unsigned)((rl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr,
+                         wl, wc, wi, w.wec);
+    } else {
+      hipLaunchKernelGGL(k_ec_wide_fwd<C>, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr,
+                         wl, wc, wi, w.wec);
+      hipLaunchKernelGGL(k_ec_wide_inv<C>, dim3((unsigned)((rl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr,
+                         wl, wc, wi, w.wec);
+      hipLaunchKernelGGL(k_ec_wide_bwd<C>, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr,
+                         wl, wc, wi, w.wec);
+    }
   }
 }
 

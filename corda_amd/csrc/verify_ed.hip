@@ -217,6 +217,23 @@ __global__ void __launch_bounds__(64) k_ed_wide_bwd(uint32_t n_keys, const EdKey
                            c_ed.d2);
 }
 
+// one lane per (wide key, row): the row's 128 multiples, one inversion, one launch
+// (ed25519_rows.h ed_wide_row_build; replaces the three passes above unless CG_ED_WIDE_ROWS=0)
+__global__ void __launch_bounds__(64) k_ed_wide_rows(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                     const uint32_t* __restrict__ wide,
+                                                     const uint32_t* __restrict__ wide_count,
+                                                     const uint32_t* __restrict__ wide_idx, EdWideSlot* __restrict__ wed) {
+  const WideLane L = wide_lane(EdWideCfg::kRows, 1);
+  if (L.l >= wide_count[PLAN_ED]) return;
+  const uint32_t i = wide[(size_t)PLAN_ED * n_keys + L.l];
+  if (hdr[i].status != 0) return;
+  EdWideSlot& ws = wed[wide_idx[i]];
+  ed_wide_row_build(ws.tab.t[L.j], ws.zpre[L.j], ws.bases[L.j], c_ed.d2);
+}
+#ifndef CG_ED_WIDE_ROWS
+#define CG_ED_WIDE_ROWS 1
+#endif
+
 // The base point B as an extended point (from the constant niels table entry 1*B)
 __device__ void ed_base_point(ge_p3& B) {
   fe x, y, two_inv, t;
@@ -813,12 +830,17 @@ void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& 
     const uint32_t* wl = (const uint32_t*)w.wide;
     const uint32_t* wc = (const uint32_t*)w.wide_count;
     const uint32_t* wi = (const uint32_t*)w.wide_idx;
-    hipLaunchKernelGGL(k_ed_wide_fwd, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl, wc,
-                       wi, w.wed);
-    hipLaunchKernelGGL(k_ed_wide_inv, dim3((unsigned)((rl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl, wc,
-                       wi, w.wed);
-    hipLaunchKernelGGL(k_ed_wide_bwd, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl, wc,
-                       wi, w.wed);
+    if (CG_ED_WIDE_ROWS) {
+      hipLaunchKernelGGL(k_ed_wide_rows, dim3((unsigned)((rl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
+                         wc, wi, w.wed);
+    } else {
+      hipLaunchKernelGGL(k_ed_wide_fwd, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
+                         wc, wi, w.wed);
+      hipLaunchKernelGGL(k_ed_wide_inv, dim3((unsigned)((rl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
+                         wc, wi, w.wed);
+      hipLaunchKernelGGL(k_ed_wide_bwd, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
+                         wc, wi, w.wed);
+    }
   }
 }
 

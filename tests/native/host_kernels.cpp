@@ -574,6 +574,48 @@ static void tbw_touch(const uint32_t* es) {
 }
 
 // counts (optional): [0..1] ladder fe_mul / fe_sq per item, [2..3] table build per key (chain + rows)
+// k_ed_wide_rows (one lane per row) against the three-pass build (k_ed_wide_fwd / _inv / _bwd)
+// for the row base P = m B (m >= 1): the number of entries whose canonical encodings differ.
+extern "C" int t_ed_wide_row_cmp(uint32_t m) {
+  init();
+  ge_p3 B, P;
+  {  // B from the constant niels entry 1 B (as t_ed_verify_v2)
+    fe x, y, two_inv, t;
+    fe_sub(x, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+    fe_add(y, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+    fe_0(t);
+    t.v[0] = 2;
+    fe_invert(two_inv, t);
+    fe_mul(B.X, x, two_inv);
+    fe_mul(B.Y, y, two_inv);
+    fe_1(B.Z);
+    fe_mul(B.T, B.X, B.Y);
+  }
+  ed_small_mul(P, B, m, g_C.d2);
+  static ge_niels a[EdWideCfg::kMult], b[EdWideCfg::kMult];
+  static fe pre[EdWideCfg::kMult], zc[EdWideCfg::kMult];
+  ed_wide_row_build(a, pre, P, g_C.d2);
+  constexpr int CPG = ED_WIDE_GROUP / ED_WIDE_CHUNK;
+  for (int g = 0; g < ED_WIDE_GROUPS; ++g) ed_wide_group_pass<false>(nullptr, &zc[CPG * g], P, g, g_C.d2);
+  fe_invert_run<ED_WIDE_CHUNKS>(zc, zc + ED_WIDE_CHUNKS);
+  for (int g = 0; g < ED_WIDE_GROUPS; ++g) ed_wide_group_pass<true>(&b[ED_WIDE_GROUP * g], &zc[CPG * g], P, g, g_C.d2);
+  int bad = 0;
+  for (int k = 0; k < EdWideCfg::kMult; ++k) {
+    uint32_t u[8], v[8];
+    const fe* fa[3] = {&a[k].ypx, &a[k].ymx, &a[k].xy2d};
+    const fe* fb[3] = {&b[k].ypx, &b[k].ymx, &b[k].xy2d};
+    for (int q = 0; q < 3; ++q) {
+      fe_tobytes_words(u, *fa[q]);
+      fe_tobytes_words(v, *fb[q]);
+      if (memcmp(u, v, 32) != 0) {
+        ++bad;
+        break;
+      }
+    }
+  }
+  return bad;
+}
+
 extern "C" int t_ed_verify_wide(const uint32_t* aw, const uint32_t* sw, const uint8_t* msg, uint64_t msg_len,
                                 uint64_t* counts) {
   init();
@@ -593,14 +635,9 @@ extern "C" int t_ed_verify_wide(const uint32_t* aw, const uint32_t* sw, const ui
 #ifdef FE_OP_COUNT
     g_fe_nmul = g_fe_nsq = 0;
 #endif
-    for (int j = 0; j < EdWideCfg::kRows; ++j) {  // k_ed_wide_chain, then the three build passes per row
+    for (int j = 0; j < EdWideCfg::kRows; ++j) {  // k_ed_wide_chain, then the k_ed_wide_rows lanes
       if (j > 0) ed_dbl_n(P, P, ED_WIDE_W);
-      constexpr int CPG = ED_WIDE_GROUP / ED_WIDE_CHUNK;
-      for (int g = 0; g < ED_WIDE_GROUPS; ++g)  // k_ed_wide_fwd lanes
-        ed_wide_group_pass<false>(nullptr, &zpre[j][CPG * g], P, g, g_C.d2);
-      fe_invert_run<ED_WIDE_CHUNKS>(zpre[j], zpre[j] + ED_WIDE_CHUNKS);  // k_ed_wide_inv
-      for (int g = 0; g < ED_WIDE_GROUPS; ++g)  // k_ed_wide_bwd lanes
-        ed_wide_group_pass<true>(&TA->t[j][ED_WIDE_GROUP * g], &zpre[j][CPG * g], P, g, g_C.d2);
+      ed_wide_row_build(TA->t[j], zpre[j], P, g_C.d2);
     }
 #ifdef FE_OP_COUNT
     build_mul = g_fe_nmul;
@@ -691,13 +728,9 @@ static int ecdsa_wide_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
       jb[j] = P;
     }
     jac_batch_to_affine<C>(ab, jb, EC_WIDE_DIGITS, WS->pre, K);
-    for (int j = 0; j < EC_WIDE_ROWS; ++j) {  // k_ec_wide_fwd / _inv / _bwd per row
+    for (int j = 0; j < EC_WIDE_ROWS; ++j) {  // k_ec_wide_rows lanes
       const EcAff& base = ab[j < EC_WIDE_DIGITS ? j : EC_WIDE_DIGITS - 1];
-      constexpr int CPG = 32 / EC_WIDE_CHUNK;
-      for (int g = 0; g < EC_WIDE_MULT / 32; ++g) ec_wide_group_pass<C, false>(nullptr, &WS->z[CPG * g], base, j, g, K);
-      m29_invert_run<C, EC_WIDE_CHUNKS>(WS->z, WS->pre, K);
-      for (int g = 0; g < EC_WIDE_MULT / 32; ++g)
-        ec_wide_group_pass<C, true>(&TQ->t[j][32 * g], &WS->z[CPG * g], base, j, g, K);
+      ec_wide_row_build<C>(TQ->t[j], WS->z, base, j == EC_WIDE_DIGITS, K);
     }
 #ifdef FE_OP_COUNT
     build_count = g_m29_nmul[C][0];
@@ -730,6 +763,37 @@ static int ecdsa_wide_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
   if (counts) counts[0] = g_m29_nmul[C][0];
 #endif
   return (int)st;
+}
+
+// k_ec_wide_rows (co-Z, one lane per row) against the three-pass build (k_ec_wide_fwd / _inv /
+// _bwd) for row base m * G (m >= 1): every entry of rows 0, 1 and 32-style (top) equal after
+// canonicalisation. Returns the number of differing entries.
+template <int C>
+static int ec_wide_row_cmp(uint32_t m) {
+  kinit();
+  const EcConsts& K = g_K[C];
+  Jac P;
+  jac_small_mul_aff<C>(P, K.gx, K.gy, m, K);
+  EcAff base;
+  jac_to_affine<C>(base.x, base.y, P, K);
+  static EcAff a[EC_WIDE_MULT], b[EC_WIDE_MULT];
+  static f29 lam[EC_WIDE_MULT];
+  static EcWideScratch ws;
+  int bad = 0;
+  for (int top = 0; top < 2; ++top) {
+    const int j = top ? EC_WIDE_DIGITS : 0;
+    ec_wide_row_build<C>(a, lam, base, top != 0, K);
+    constexpr int CPG = 32 / EC_WIDE_CHUNK;
+    for (int g = 0; g < EC_WIDE_MULT / 32; ++g) ec_wide_group_pass<C, false>(nullptr, &ws.z[CPG * g], base, j, g, K);
+    m29_invert_run<C, EC_WIDE_CHUNKS>(ws.z, ws.pre, K);
+    for (int g = 0; g < EC_WIDE_MULT / 32; ++g) ec_wide_group_pass<C, true>(&b[32 * g], &ws.z[CPG * g], base, j, g, K);
+    for (int e = 0; e < EC_WIDE_MULT; ++e)
+      if (!m29_eq<C, 0>(a[e].x, b[e].x) || !m29_eq<C, 0>(a[e].y, b[e].y)) ++bad;
+  }
+  return bad;
+}
+extern "C" int t_ec_wide_row_cmp(int curve, uint32_t m) {
+  return curve == CG_CURVE_R1 ? ec_wide_row_cmp<CG_CURVE_R1>(m) : ec_wide_row_cmp<CG_CURVE_K1>(m);
 }
 
 extern "C" int t_ecdsa_verify_wide(int scheme, const uint8_t* arena, uint64_t arena_len, uint64_t key_off,

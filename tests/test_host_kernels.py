@@ -403,3 +403,25 @@ def test_sha_over_splice_matches_materialised():
     lib = hostk.lib()
     lib.t_sha_splice_cmp.argtypes = [ctypes.c_uint64, ctypes.c_int]
     assert lib.t_sha_splice_cmp(99, 3000) == 0
+
+
+@pytest.mark.parametrize("curve", [0, 1])
+def test_ec_wide_row_build_matches_three_pass(curve):
+    """k_ec_wide_rows (co-Z additions, one lane per row, one inversion) builds the same affine
+    entries as the three-pass build it replaced, for rows 0 and 32 (multiples 129..256) of several
+    bases, every product's bound asserted."""
+    import ctypes
+    lib = hostk.lib()
+    lib.t_ec_wide_row_cmp.argtypes = [ctypes.c_int, ctypes.c_uint32]
+    for m in (1, 2, 3, 7, 255, 256, 65537, 0x7fffffff):
+        assert lib.t_ec_wide_row_cmp(curve, m) == 0, m
+
+
+def test_ed_wide_row_build_matches_three_pass():
+    """k_ed_wide_rows (one lane per row, one inversion) builds the same half-scaled niels entries as
+    the three-pass build it replaced, for the row bases m B of several m, limb bounds asserted."""
+    import ctypes
+    lib = hostk.lib()
+    lib.t_ed_wide_row_cmp.argtypes = [ctypes.c_uint32]
+    for m in (1, 2, 3, 8, 255, 4096, 65537, 0x7fffffff):
+        assert lib.t_ed_wide_row_cmp(m) == 0, m

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Headline-only bench under each environment setting given as NAME=VALUE ("-" = none).
-# usage: bash tools/ab_env_headline.sh <tag> <NAME=VALUE|-> [...]
+# usage: bash tools/ab_env_headline.sh <tag> <NAME=VALUE[+NAME=VALUE...]|-> [...]
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; shift
@@ -8,7 +8,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 for kv in "$@"; do
   name=$(echo "$kv" | tr '=' '_')
-  if [ "$kv" = "-" ]; then E=""; else E="$kv"; fi
+  if [ "$kv" = "-" ]; then E=""; else E=$(echo "$kv" | tr '+' ' '); fi
   env $E timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --device-steps 0 --host-steps 0 \
     --key-dists '' --configs1-items 0 --ecdsa-items 0 --pipeline-txs 0 --tear-offs 0 --configs0-txs 0 \
     --no-cpu-baseline > $OUT/h_$name.log 2>&1 || { echo FAIL $kv; tail -20 $OUT/h_$name.log; exit 1; }

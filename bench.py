@@ -56,7 +56,7 @@ MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # Ed25519 (field multiplies, squarings) in the radix-2^25.5 representation (fe25519.h):
 ED_VERIFY_FE = (402, 24)   # k_ed_ladder_pf: 43 + 12 mixed additions + 6 doublings
 ED_WIDE_FE = (307, 0)      # k_ed_ladder_wide: 32 + 12 mixed additions, no doublings (keys with wide tables)
-ED_WIDE_BUILD_FE = (62279, 9120)  # one key's wide table: 248-doubling chain, then per row one lane walking its 128 entries, one inversion, the walk back (k_ed_wide_rows)
+ED_WIDE_BUILD_FE = (63399, 18016)  # one key's wide table: 248-doubling chain, then per row two lanes each walking 64 entries (the second from 65 P), one inversion each, the walk back (k_ed_wide_rows)
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
 ED_FINISH_K = 16

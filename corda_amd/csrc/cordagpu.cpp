@@ -216,6 +216,15 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   if (e == hipSuccess && pre_plan) e = plan(0);
   if (e == hipSuccess && pre_plan) e = plan(1);
   if (e == hipSuccess && prepare) e = cg::launch_key_tables(&c->fork, s);
+  // CG_FRONT_AFTER_TABLES=1 (A/B): the first chunk's front waits for every key table, instead of
+  // sharing the chip with the builds (both run at about half speed together:
+  // profiles/r03/env_chains timelines)
+  static const bool after_tables = [] {
+    const char* v = getenv("CG_FRONT_AFTER_TABLES");
+    return v && v[0] == '1';
+  }();
+  if (e == hipSuccess && prepare && after_tables)
+    for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(s, c->fork.ready[k], 0);
   auto back = [&](uint64_t k) {
     return cg::launch_items_back(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, d_status + at(k),
                                  c->keyprep.p, ws(k), c->btab.p, s, &c->fork, &wp);
@@ -484,8 +493,25 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.front, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.planned, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.ed_tabs, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy2, hipStreamNonBlocking);
+  for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.chains[k], hipEventDisableTiming);
+  // The copy streams on hardware queues of their own (an all-CU mask makes HIP back a stream with a
+  // dedicated queue): multiplexed onto the four default queues, the copy stream shared one with a
+  // side stream, and the first chunk's bytes landed only after that stream's table builds (the
+  // chunk's fronts started right after k_ed_keyprep_tab in every timeline; with
+  // GPU_MAX_HW_QUEUES=8 they started 3 ms earlier: profiles/r03/env_hwq). CG_COPY_QUEUE_SHARED=1:
+  // plain streams (A/B).
+  {
+    hipDeviceProp_t prop;
+    const char* sh = getenv("CG_COPY_QUEUE_SHARED");
+    const bool own = !(sh && sh[0] == '1') && hipGetDeviceProperties(&prop, c->device) == hipSuccess &&
+                     prop.multiProcessorCount > 0;
+    std::vector<uint32_t> mask(own ? (prop.multiProcessorCount + 31) / 32 : 0, 0u);
+    for (int cu = 0; own && cu < prop.multiProcessorCount; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+    for (hipStream_t* cs : {&c->copy, &c->copy2})
+      if (e == hipSuccess)
+        e = own ? hipExtStreamCreateWithCUMask(cs, (uint32_t)mask.size(), mask.data())
+                : hipStreamCreateWithFlags(cs, hipStreamNonBlocking);
+  }
   for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&c->tev[k]);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
   if (e == hipSuccess) e = cg::upload_constants();
@@ -536,6 +562,8 @@ void cg_close(cg_ctx* c) {
   if (c->fork.front) hipEventDestroy(c->fork.front);
   if (c->fork.planned) hipEventDestroy(c->fork.planned);
   if (c->fork.ed_tabs) hipEventDestroy(c->fork.ed_tabs);
+  for (int k = 0; k < 3; ++k)
+    if (c->fork.chains[k]) hipEventDestroy(c->fork.chains[k]);
   for (hipStream_t* cs : {&c->copy, &c->copy2})
     if (*cs) {
       hipStreamSynchronize(*cs);

@@ -631,21 +631,68 @@ CG_HD void ec_dblu_aff(f29& XT, f29& YT, f29& XB, f29& YB, f29& Z, const f29& x,
   m29_add<C, 0>(Z, y, y);
 }
 
-// Row j's 128 affine multiples into out[0..127] (top = row 32: multiples 129..256 of the top row's
-// base, started from 128 B by seven doublings); lam[0..127] is scratch.
-template <int C>
-CG_HD void ec_wide_row_build(EcAff* out, f29* lam, const EcAff& base, bool top, const EcConsts& K) {
-  f29 XT, YT, XB, YB, Z;
-  int e_lo;  // the first chained entry
-  if (!top) {
+// Where a row lane parks its entries' X, Y and lambdas between the walks (k = entry index relative
+// to the lane's first): EcParkRow in the entries + lam[] (host build), EcParkLanes lane-interleaved
+// (the device build, keyws.h EcWideSlot::park).
+#define EC_PARK_DWORDS 27  // X, Y and lambda: 3 x 9 limbs
+struct EcParkRow {
+  EcAff* out;
+  f29* lam;
+  CG_HDM void put(int k, const f29& X, const f29& Y, const f29& l) const {
+    out[k].x = X;
+    out[k].y = Y;
+    lam[k] = l;
+  }
+  CG_HDM void get(int k, f29& X, f29& Y, f29& l) const {
+    X = out[k].x;
+    Y = out[k].y;
+    l = lam[k];
+  }
+};
+struct EcParkLanes {
+  uint32_t* base;
+  uint32_t lane, lanes;
+  CG_HDM void st(int k, int q, const f29& f) const {
+    uint32_t* p = base + (size_t)(k * EC_PARK_DWORDS + q * 9) * lanes + lane;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) p[(size_t)d * lanes] = f.v[d];
+  }
+  CG_HDM void ld(int k, int q, f29& f) const {
+    const uint32_t* p = base + (size_t)(k * EC_PARK_DWORDS + q * 9) * lanes + lane;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) f.v[d] = p[(size_t)d * lanes];
+  }
+  CG_HDM void put(int k, const f29& X, const f29& Y, const f29& l) const {
+    st(k, 0, X);
+    st(k, 1, Y);
+    st(k, 2, l);
+  }
+  CG_HDM void get(int k, f29& X, f29& Y, f29& l) const {
+    ld(k, 0, X);
+    ld(k, 1, Y);
+    ld(k, 2, l);
+  }
+};
+
+// Entries [e0, e1) of row j into out[] (entry e = multiple (top ? 128 : 0) + e + 1; top = row 32,
+// the multiples 129..256 of the top row's base). A lane that does not start at entry 0 starts from
+// its first multiple's predecessor by a scalar multiplication.
+template <int C, class Park>
+CG_HD void ec_wide_row_build(EcAff* out, const Park& pk, const EcAff& base, bool top, int e0, int e1,
+                             const EcConsts& K) {
+  f29 XT, YT, XB, YB, Z, l;
+  int e_first, e_lo;  // the first entry ZADDU produces; the first entry the walk back normalises
+  const uint32_t m0 = (top ? (uint32_t)EC_WIDE_MULT : 0u) + (uint32_t)e0;  // the multiple before entry e0
+  if (m0 == 0) {
     out[0] = base;
     ec_dblu_aff<C>(XT, YT, XB, YB, Z, base.x, base.y, K);
-    out[1].x = XT;
-    out[1].y = YT;
+    f29_zero(l);
+    pk.put(1 - e0, XT, YT, l);  // Z_1 = 2y: no lambda
+    e_first = 2;
     e_lo = 1;
   } else {
-    Jac F = {base.x, base.y, K.one_p};
-    for (int i = 0; i < 7; ++i) jac_dbl<C>(F, F);
+    Jac F;
+    jac_small_mul_aff<C>(F, base.x, base.y, m0, K);
     f29 z2, z3;
     m29_sq<C, 0>(z2, F.Z);
     m29_mul<C, 0>(z3, z2, F.Z);
@@ -654,29 +701,42 @@ CG_HD void ec_wide_row_build(EcAff* out, f29* lam, const EcAff& base, bool top, 
     XT = F.X;
     YT = F.Y;
     Z = F.Z;
-    e_lo = 0;
+    e_first = e_lo = e0;
   }
 #pragma unroll 1
-  for (int e = e_lo == 0 ? 0 : 2; e < EC_WIDE_MULT; ++e) {
-    ec_zaddu<C>(XT, YT, XB, YB, lam[e]);  // Z_e = Z_{e-1} lam[e]
-    m29_mul<C, 0>(Z, Z, lam[e]);
-    out[e].x = XT;
-    out[e].y = YT;
+  for (int e = e_first; e < e1; ++e) {
+    ec_zaddu<C>(XT, YT, XB, YB, l);  // Z_e = Z_{e-1} l
+    m29_mul<C, 0>(Z, Z, l);
+    pk.put(e - e0, XT, YT, l);
   }
   f29 inv;
   m29_inv<C, 0>(inv, Z, K.one_p);
+  // the walk back, each entry's parked X, Y and lambda loaded one entry ahead
+  f29 X, Y;
+  pk.get(e1 - 1 - e0, X, Y, l);
 #pragma unroll 1
-  for (int e = EC_WIDE_MULT - 1; e >= e_lo; --e) {
+  for (int e = e1 - 1; e >= e_lo; --e) {
+    f29 Xn = X, Yn = Y, ln = l;
+    if (e > e_lo) pk.get(e - 1 - e0, Xn, Yn, ln);
     f29 zi2, zi3, x, y;
     m29_sq<C, 0>(zi2, inv);
     m29_mul<C, 0>(zi3, zi2, inv);
-    m29_mul<C, 0>(x, out[e].x, zi2);
-    m29_mul<C, 0>(y, out[e].y, zi3);
+    m29_mul<C, 0>(x, X, zi2);
+    m29_mul<C, 0>(y, Y, zi3);
     out[e].x = x;
     out[e].y = y;
-    if (e > e_lo) m29_mul<C, 0>(inv, inv, lam[e]);  // 1 / Z_{e-1}
+    if (e > e_lo) m29_mul<C, 0>(inv, inv, l);  // 1 / Z_{e-1}
+    X = Xn;
+    Y = Yn;
+    l = ln;
   }
 }
+// lanes per row (each walks 128 / EC_WIDE_ROW_LANES entries with its own inversion): more waves for
+// a latency-bound walk against one more scalar multiplication and inversion per extra lane
+#ifndef EC_WIDE_ROW_LANES
+#define EC_WIDE_ROW_LANES 2  // A/B 1 / 2 / 4 lanes: 218.6 / 226.7 / 226.6 and 222.7 / 234.8 / 223.4 M sigs/s (profiles/r03/ab_lanes)
+#endif
+static_assert(EC_WIDE_MULT % EC_WIDE_ROW_LANES == 0 && EC_WIDE_MULT / EC_WIDE_ROW_LANES >= 2, "row split");
 
 // in place: z[g] <- 1 / z[g] mod p for the NG products of one row (prefix products in pre[])
 template <int C, int NG>

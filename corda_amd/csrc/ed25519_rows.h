@@ -627,14 +627,65 @@ CG_HD void fe_invert_run(fe* z, fe* pre) {
 // entries (zi = inv pre[k-1], inv <- inv Z_k, four products per entry). ~15 products per entry
 // against the three-pass form's ~30 (no group-start scalar multiplications, nothing walked
 // twice), and one launch instead of three.
-CG_HD void ed_wide_row_build(ge_niels* out, fe* pre, const ge_p3& P, const fe& d2) {
+// Where a row lane parks its multiples between the walks (k = entry index relative to the lane's
+// first): EdParkRow in the row's own entries + pre[] (host build), EdParkLanes lane-interleaved
+// (the device build, keyws.h EdWideSlot::park).
+#define ED_PARK_DWORDS 40  // X, Y, Z and the running product: 4 x 10 limbs
+struct EdParkRow {
+  ge_niels* out;
+  fe* pre;
+  CG_HDM void put(int k, const fe& X, const fe& Y, const fe& Z, const fe& run) const {
+    out[k].ypx = X;
+    out[k].ymx = Y;
+    out[k].xy2d = Z;
+    pre[k] = run;
+  }
+  CG_HDM void get(int k, fe& X, fe& Y, fe& Z) const {
+    X = out[k].ypx;
+    Y = out[k].ymx;
+    Z = out[k].xy2d;
+  }
+  CG_HDM void get_run(int k, fe& run) const { run = pre[k]; }
+};
+struct EdParkLanes {
+  uint32_t* base;
+  uint32_t lane, lanes;
+  CG_HDM void st(int k, int q, const fe& f) const {
+    uint32_t* p = base + (size_t)(k * ED_PARK_DWORDS + q * 10) * lanes + lane;
+#pragma unroll
+    for (int d = 0; d < 10; ++d) p[(size_t)d * lanes] = f.v[d];
+  }
+  CG_HDM void ld(int k, int q, fe& f) const {
+    const uint32_t* p = base + (size_t)(k * ED_PARK_DWORDS + q * 10) * lanes + lane;
+#pragma unroll
+    for (int d = 0; d < 10; ++d) f.v[d] = p[(size_t)d * lanes];
+  }
+  CG_HDM void put(int k, const fe& X, const fe& Y, const fe& Z, const fe& run) const {
+    st(k, 0, X);
+    st(k, 1, Y);
+    st(k, 2, Z);
+    st(k, 3, run);
+  }
+  CG_HDM void get(int k, fe& X, fe& Y, fe& Z) const {
+    ld(k, 0, X);
+    ld(k, 1, Y);
+    ld(k, 2, Z);
+  }
+  CG_HDM void get_run(int k, fe& run) const { ld(k, 3, run); }
+};
+
+// Entries [e0, e1) (entry k = (k + 1) P); a lane not starting at 0 starts by a scalar multiplication.
+template <class Park>
+CG_HD void ed_wide_row_build(ge_niels* out, const Park& pk, const ge_p3& P, int e0, int e1, const fe& d2) {
   ge_cached c;
   ge_p3_to_cached(c, P, d2);
-  ge_p3 R = P;
+  ge_p3 R;
+  if (e0 == 0) R = P;
+  else ed_small_mul(R, P, (uint32_t)e0 + 1u, d2);
   fe run;
 #pragma unroll 1
-  for (int k = 0; k < EdWideCfg::kMult; ++k) {
-    if (k > 0) {
+  for (int k = e0; k < e1; ++k) {
+    if (k > e0) {
       ge_p1p1 t;
       ge_add_cached(t, R, c);
       ge_p1p1_to_p3(R, t);
@@ -642,34 +693,50 @@ CG_HD void ed_wide_row_build(ge_niels* out, fe* pre, const ge_p3& P, const fe& d
     } else {
       fe_copy(run, R.Z);
     }
-    out[k].ypx = R.X;  // un-normalised X, Y, Z until the walk back
-    out[k].ymx = R.Y;
-    out[k].xy2d = R.Z;
-    pre[k] = run;
+    pk.put(k - e0, R.X, R.Y, R.Z, run);  // un-normalised until the walk back
   }
   fe inv, h, d4;
   fe_invert(inv, run);
   fe_half(h);
-  fe_mul(inv, inv, h);  // 1 / (2 Z_0 .. Z_127): the half-scaled entries' 1/2
+  fe_mul(inv, inv, h);  // 1 / (2 Z_e0 .. Z_e1-1): the half-scaled entries' 1/2
   fe_add(d4, d2, d2);
   fe_carry(d4);
+  // the walk back, each entry's parked coordinates and the previous running product loaded one
+  // entry ahead
+  fe X, Y, Z, pr;
+  pk.get(e1 - 1 - e0, X, Y, Z);
+  if (e1 - 1 > e0) pk.get_run(e1 - 2 - e0, pr);
 #pragma unroll 1
-  for (int k = EdWideCfg::kMult - 1; k >= 0; --k) {
+  for (int k = e1 - 1; k >= e0; --k) {
+    fe Xn = X, Yn = Y, Zn = Z, prn = pr;
+    if (k > e0) {
+      pk.get(k - 1 - e0, Xn, Yn, Zn);
+      if (k - 1 > e0) pk.get_run(k - 2 - e0, prn);
+    }
     ge_p2 p;
-    p.X = out[k].ypx;
-    p.Y = out[k].ymx;
+    p.X = X;
+    p.Y = Y;
     fe zi;
-    if (k > 0) {
-      fe_mul(zi, inv, pre[k - 1]);
-      fe_mul(inv, inv, out[k].xy2d);
+    if (k > e0) {
+      fe_mul(zi, inv, pr);
+      fe_mul(inv, inv, Z);
     } else {
       fe_copy(zi, inv);
     }
     ge_niels n;
     ed_niels_from(n, p, zi, d4);
     out[k] = n;
+    X = Xn;
+    Y = Yn;
+    Z = Zn;
+    pr = prn;
   }
 }
+
+#ifndef ED_WIDE_ROW_LANES  // lanes per row (as EC_WIDE_ROW_LANES)
+#define ED_WIDE_ROW_LANES 2
+#endif
+static_assert(EdWideCfg::kMult % ED_WIDE_ROW_LANES == 0, "row split");
 
 // ---------------------------------------------------------------- full / row-0 tables + wide B
 // R' = h (-A) + S' B for keys with full tables (W/K rows of -A, K windows, (K-1) W doublings) or

@@ -89,6 +89,7 @@ struct Fork {
   hipEvent_t start, ec_decoded[2], ready[3], front, row0[3];
   StageTimer* timer;  // null unless the ctx was opened with CG_FLAG_STAGE_TIMING
   hipEvent_t planned = nullptr, ed_tabs = nullptr;  // plan sorted (main); Ed25519 tables built (side[2])
+  hipEvent_t chains[3] = {nullptr, nullptr, nullptr};  // each family's row-base chains done (side[k])
   mutable PendingTabs pending;
 };
 

@@ -218,23 +218,33 @@ struct KeyWs {
 #endif
 #define KEY_WIDE_MIN_USES (KEY_WIDE_MIN_USES_EC < KEY_WIDE_MIN_USES_ED ? KEY_WIDE_MIN_USES_EC : KEY_WIDE_MIN_USES_ED)
 #define KEY_NOT_WIDE 0xffffffffu
-#define KEY_WIDE_MAX 8192u  // wide slots per pool at most (Ed25519 4.9 GB / ECDSA 5.0 GB)
+#define KEY_WIDE_MAX 8192u  // wide slots per pool at most (Ed25519 9.4 GB / ECDSA 6.3 GB)
 #define KEY_USES_ALL 0xffffffffu
 #define KEY_USES_SAMPLE 4u  // k_key_uses samples by the top 2 bits of a 32-bit hash: 1 in 4
 #ifndef ED_DIRECT_MAX_USES
 #define ED_DIRECT_MAX_USES 32u
 #endif
-// Wide-table slot of one key: the table, its row bases and the row builds' inversion scratch.
+// Wide-table slot of one key: the table, its row bases and the row builds' scratch. The one-lane-
+// per-row builds park every multiple's un-normalised coordinates between their two walks in
+// `park`, lane-interleaved (dword d of entry i of row lane t at park[(i * fields + d) * lanes + t]:
+// one store of a wave is 64 consecutive dwords, where parking in the entries themselves made every
+// store touch 64 cache lines: the builds ran at about a third of their compute rate).
 struct EdWideSlot {
   EdWideTab tab;
   ge_p3 bases[EdWideCfg::kRows];
-  fe zpre[EdWideCfg::kRows][EdWideCfg::kMult];
+  union {
+    fe zpre[EdWideCfg::kRows][EdWideCfg::kMult];                       // three-pass build
+    uint32_t park[EdWideCfg::kRows * EdWideCfg::kMult * ED_PARK_DWORDS];  // row-lane build
+  };
 };
 struct EcWideSlot {
   EcWideTab tab;
   EcAff bases[EC_WIDE_DIGITS];  // 2^{8j} Q, affine (the row builds step by mixed additions)
   Jac jbases[EC_WIDE_DIGITS];   // the chain's Jacobian points
-  EcWideScratch s[EC_WIDE_ROWS];
+  union {
+    EcWideScratch s[EC_WIDE_ROWS];                                 // three-pass build, the chain
+    uint32_t park[EC_WIDE_ROWS * EC_WIDE_MULT * EC_PARK_DWORDS];   // row-lane build
+  };
 };
 // Slots for a call of n_items over n_keys: no more keys can reach KEY_WIDE_MIN_USES.
 static inline uint32_t wide_cap(uint32_t n_keys, uint64_t n_items, uint32_t min_uses = KEY_WIDE_MIN_USES) {

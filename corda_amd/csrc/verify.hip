@@ -168,6 +168,18 @@ static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
   hipError_t e = hipEventRecord(fork->planned, stream);
   if (e == hipSuccess) e = hipStreamWaitEvent(fork->side[2], fork->planned, 0);
   if (e != hipSuccess) return e;
+  // every family's row builds after ALL the row-base chains: a chain is one lane per key (a few
+  // dozen waves, latency-bound), and beside another family's row builds it ran 4x slower (r1: 5.6
+  // instead of 1.3 ms, then its rows after it: profiles/r03/env_copyq timeline). CG_CHAINS_FIRST=0:
+  // each family's builds right after its own chains (A/B).
+  static const bool chains_first = [] {
+    const char* v = getenv("CG_CHAINS_FIRST");
+    return !(v && v[0] == '0');
+  }();
+  for (int k = 0; k < 3 && e == hipSuccess && chains_first; ++k)
+    for (int q = 0; q < 3 && e == hipSuccess; ++q)
+      if (q != k && fork->chains[q]) e = hipStreamWaitEvent(fork->side[k], fork->chains[q], 0);
+  if (e != hipSuccess) return e;
   ed_launch_keyprep_tabs(p.keys, p.n_keys, w, fork->side[2], false, true);
   e = hipEventRecord(fork->ed_tabs, fork->side[2]);
   // then the full / row-0 tables (usually few keys: launched ahead of the wide builds, their
@@ -251,6 +263,9 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   ec_launch_keyprep_chains(CG_CURVE_R1, d_keys, n_keys, d_arena, arena_len, w, fork->side[0], fork->ec_decoded[0]);
   ec_launch_keyprep_chains(CG_CURVE_K1, d_keys, n_keys, d_arena, arena_len, w, fork->side[1], fork->ec_decoded[1]);
   ed_launch_keyprep_chains(d_keys, n_keys, d_arena, arena_len, w, fork->side[2]);
+  for (int k = 0; k < 3 && e == hipSuccess; ++k)
+    if (fork->chains[k]) e = hipEventRecord(fork->chains[k], fork->side[k]);
+  if (e != hipSuccess) return e;
   // the tables (the wide ones hold every SIMD for milliseconds), wide first, then full / row 0:
   // after the first chunk's plan sort when items follow (its decoupled look-back stalls behind
   // them), else now

@@ -177,10 +177,12 @@ __global__ void __launch_bounds__(64) k_ec_wide_rows(uint32_t n_keys, const EdKe
                                                      const uint32_t* __restrict__ wide,
                                                      const uint32_t* __restrict__ wide_count,
                                                      const uint32_t* __restrict__ wide_idx, EcWideSlot* __restrict__ wec) {
-  const EcWideLane L = ec_wide_lane(EC_WIDE_ROWS, 1);
+  const EcWideLane L = ec_wide_lane(EC_WIDE_ROWS, EC_WIDE_ROW_LANES);
   EC_WIDE_KEY(C, L);
-  ec_wide_row_build<C>(ws.tab.t[L.j], ws.s[L.j].z, ws.bases[L.j < EC_WIDE_DIGITS ? L.j : EC_WIDE_DIGITS - 1],
-                       L.j == EC_WIDE_DIGITS, c_ec[C]);
+  constexpr int per = EC_WIDE_MULT / EC_WIDE_ROW_LANES;
+  const EcParkLanes pk{ws.park, L.j * EC_WIDE_ROW_LANES + L.g, (uint32_t)(EC_WIDE_ROWS * EC_WIDE_ROW_LANES)};
+  ec_wide_row_build<C>(ws.tab.t[L.j], pk, ws.bases[L.j < EC_WIDE_DIGITS ? L.j : EC_WIDE_DIGITS - 1],
+                       L.j == EC_WIDE_DIGITS, per * (int)L.g, per * (int)L.g + per, c_ec[C]);
 }
 #ifndef CG_EC_WIDE_COZ
 #define CG_EC_WIDE_COZ 1
@@ -461,8 +463,8 @@ static void launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const Key
     const uint32_t* wc = (const uint32_t*)w.wide_count;
     const uint32_t* wi = (const uint32_t*)w.wide_idx;
     if (CG_EC_WIDE_COZ) {
-      hipLaunchKernelGGL(k_ec_wide_rows<C>, dim3((unsigned)((rl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr,
-                         wl, wc, wi, w.wec);
+      hipLaunchKernelGGL(k_ec_wide_rows<C>, dim3((unsigned)((rl * EC_WIDE_ROW_LANES + B - 1) / B)), dim3(B), 0, stream,
+                         n_keys, w.hdr, wl, wc, wi, w.wec);
     } else {
       hipLaunchKernelGGL(k_ec_wide_fwd<C>, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr,
                          wl, wc, wi, w.wec);

@@ -217,18 +217,23 @@ __global__ void __launch_bounds__(64) k_ed_wide_bwd(uint32_t n_keys, const EdKey
                            c_ed.d2);
 }
 
+#ifndef ED_WIDE_ROWS_WAVES  // waves per SIMD the register allocation must allow
+#define ED_WIDE_ROWS_WAVES 2  // 3 spills 125 VGPRs
+#endif
 // one lane per (wide key, row): the row's 128 multiples, one inversion, one launch
 // (ed25519_rows.h ed_wide_row_build; replaces the three passes above unless CG_ED_WIDE_ROWS=0)
-__global__ void __launch_bounds__(64) k_ed_wide_rows(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ED_WIDE_ROWS_WAVES))) k_ed_wide_rows(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                      const uint32_t* __restrict__ wide,
                                                      const uint32_t* __restrict__ wide_count,
                                                      const uint32_t* __restrict__ wide_idx, EdWideSlot* __restrict__ wed) {
-  const WideLane L = wide_lane(EdWideCfg::kRows, 1);
+  const WideLane L = wide_lane(EdWideCfg::kRows, ED_WIDE_ROW_LANES);
   if (L.l >= wide_count[PLAN_ED]) return;
   const uint32_t i = wide[(size_t)PLAN_ED * n_keys + L.l];
   if (hdr[i].status != 0) return;
   EdWideSlot& ws = wed[wide_idx[i]];
-  ed_wide_row_build(ws.tab.t[L.j], ws.zpre[L.j], ws.bases[L.j], c_ed.d2);
+  constexpr int per = EdWideCfg::kMult / ED_WIDE_ROW_LANES;
+  const EdParkLanes pk{ws.park, L.j * ED_WIDE_ROW_LANES + L.g, (uint32_t)(EdWideCfg::kRows * ED_WIDE_ROW_LANES)};
+  ed_wide_row_build(ws.tab.t[L.j], pk, ws.bases[L.j], per * (int)L.g, per * (int)L.g + per, c_ed.d2);
 }
 #ifndef CG_ED_WIDE_ROWS
 #define CG_ED_WIDE_ROWS 1
@@ -831,8 +836,8 @@ void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& 
     const uint32_t* wc = (const uint32_t*)w.wide_count;
     const uint32_t* wi = (const uint32_t*)w.wide_idx;
     if (CG_ED_WIDE_ROWS) {
-      hipLaunchKernelGGL(k_ed_wide_rows, dim3((unsigned)((rl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
-                         wc, wi, w.wed);
+      hipLaunchKernelGGL(k_ed_wide_rows, dim3((unsigned)((rl * ED_WIDE_ROW_LANES + B - 1) / B)), dim3(B), 0, stream,
+                         n_keys, w.hdr, wl, wc, wi, w.wed);
     } else {
       hipLaunchKernelGGL(k_ed_wide_fwd, dim3((unsigned)((gl + B - 1) / B)), dim3(B), 0, stream, n_keys, w.hdr, wl,
                          wc, wi, w.wed);

@@ -594,7 +594,15 @@ extern "C" int t_ed_wide_row_cmp(uint32_t m) {
   ed_small_mul(P, B, m, g_C.d2);
   static ge_niels a[EdWideCfg::kMult], b[EdWideCfg::kMult];
   static fe pre[EdWideCfg::kMult], zc[EdWideCfg::kMult];
-  ed_wide_row_build(a, pre, P, g_C.d2);
+  for (int g = 0; g < 4; ++g)  // any split; parked in the entries (the host policy) ...
+    ed_wide_row_build(a, EdParkRow{a + 32 * g, pre + 32 * g}, P, 32 * g, 32 * g + 32, g_C.d2);
+  {  // ... or lane-interleaved (the device policy): the same entries
+    static ge_niels a2[EdWideCfg::kMult];
+    static uint32_t park[EdWideCfg::kMult * ED_PARK_DWORDS];
+    for (int g = 0; g < 4; ++g)
+      ed_wide_row_build(a2, EdParkLanes{park, (uint32_t)g, 4u}, P, 32 * g, 32 * g + 32, g_C.d2);
+    if (memcmp(a, a2, sizeof a) != 0) return -1;
+  }
   constexpr int CPG = ED_WIDE_GROUP / ED_WIDE_CHUNK;
   for (int g = 0; g < ED_WIDE_GROUPS; ++g) ed_wide_group_pass<false>(nullptr, &zc[CPG * g], P, g, g_C.d2);
   fe_invert_run<ED_WIDE_CHUNKS>(zc, zc + ED_WIDE_CHUNKS);
@@ -637,7 +645,11 @@ extern "C" int t_ed_verify_wide(const uint32_t* aw, const uint32_t* sw, const ui
 #endif
     for (int j = 0; j < EdWideCfg::kRows; ++j) {  // k_ed_wide_chain, then the k_ed_wide_rows lanes
       if (j > 0) ed_dbl_n(P, P, ED_WIDE_W);
-      ed_wide_row_build(TA->t[j], zpre[j], P, g_C.d2);
+      for (int g = 0; g < ED_WIDE_ROW_LANES; ++g)
+      {
+        const int e0 = g * (EdWideCfg::kMult / ED_WIDE_ROW_LANES), e1 = e0 + EdWideCfg::kMult / ED_WIDE_ROW_LANES;
+        ed_wide_row_build(TA->t[j], EdParkRow{TA->t[j] + e0, zpre[j] + e0}, P, e0, e1, g_C.d2);
+      }
     }
 #ifdef FE_OP_COUNT
     build_mul = g_fe_nmul;
@@ -730,7 +742,10 @@ static int ecdsa_wide_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
     jac_batch_to_affine<C>(ab, jb, EC_WIDE_DIGITS, WS->pre, K);
     for (int j = 0; j < EC_WIDE_ROWS; ++j) {  // k_ec_wide_rows lanes
       const EcAff& base = ab[j < EC_WIDE_DIGITS ? j : EC_WIDE_DIGITS - 1];
-      ec_wide_row_build<C>(TQ->t[j], WS->z, base, j == EC_WIDE_DIGITS, K);
+      for (int g = 0; g < EC_WIDE_ROW_LANES; ++g) {
+        const int e0 = g * (EC_WIDE_MULT / EC_WIDE_ROW_LANES), e1 = e0 + EC_WIDE_MULT / EC_WIDE_ROW_LANES;
+        ec_wide_row_build<C>(TQ->t[j], EcParkRow{TQ->t[j] + e0, WS->z + e0}, base, j == EC_WIDE_DIGITS, e0, e1, K);
+      }
     }
 #ifdef FE_OP_COUNT
     build_count = g_m29_nmul[C][0];
@@ -782,7 +797,15 @@ static int ec_wide_row_cmp(uint32_t m) {
   int bad = 0;
   for (int top = 0; top < 2; ++top) {
     const int j = top ? EC_WIDE_DIGITS : 0;
-    ec_wide_row_build<C>(a, lam, base, top != 0, K);
+    for (int g = 0; g < 4; ++g)  // split in 4 lanes (the same entries as one lane, or any split)
+      ec_wide_row_build<C>(a, EcParkRow{a + 32 * g, lam + 32 * g}, base, top != 0, 32 * g, 32 * g + 32, K);
+    {  // lane-interleaved parking (the device policy): the same entries
+      static EcAff a2[EC_WIDE_MULT];
+      static uint32_t park[EC_WIDE_MULT * EC_PARK_DWORDS];
+      for (int g = 0; g < 4; ++g)
+        ec_wide_row_build<C>(a2, EcParkLanes{park, (uint32_t)g, 4u}, base, top != 0, 32 * g, 32 * g + 32, K);
+      if (memcmp(a, a2, sizeof a) != 0) ++bad;
+    }
     constexpr int CPG = 32 / EC_WIDE_CHUNK;
     for (int g = 0; g < EC_WIDE_MULT / 32; ++g) ec_wide_group_pass<C, false>(nullptr, &ws.z[CPG * g], base, j, g, K);
     m29_invert_run<C, EC_WIDE_CHUNKS>(ws.z, ws.pre, K);

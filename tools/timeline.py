@@ -8,7 +8,14 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     step = int(sys.argv[2]) if len(sys.argv) > 2 else -2
-    starts = [i for i, r in enumerate(rows) if "keyprep_decode" in r["Kernel_Name"] and not any("keyprep_decode" in q["Kernel_Name"] for q in rows[max(0, i - 1):i])]
+    # a step starts at its first key decode; the three families' decodes of one step lie within 5 ms
+    starts, last = [], None
+    for i, r in enumerate(rows):
+        if "keyprep_decode" in r["Kernel_Name"]:
+            t = int(r["Start_Timestamp"])
+            if last is None or t - last > 5_000_000:
+                starts.append(i)
+            last = t
     j = starts[step]
     end = starts[step + 1] if step + 1 < len(starts) and step != -1 else len(rows)
     t0 = int(rows[j]["Start_Timestamp"])

@@ -931,7 +931,7 @@ int cg_verify_transactions(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_
 
 // ---------------------------------------------------------------- signatures over known tx ids
 #define CG_TXSIG_MIN_CHUNKS 4u
-#define CG_TXSIG_COUNT_SAMPLE 32u  // 1 in 32 (blocks of 8 records): plan 3.0 -> 1.4-1.8 ms, 235 -> 237 / 247 M (profiles/r03/env_fd12)
+#define CG_TXSIG_COUNT_SAMPLE 32u  // hot-key calls: 1 in 32 (blocks of 8 records): plan 3.0 -> 1.4-1.8 ms, 235 -> 237 / 247 M (profiles/r03/env_fd12)
 #define CG_TXSIG_SAMPLE_BLOCK 8u
 // The spliced-message slot of a template set: the longest prefix || id || suffix, 16-aligned.
 static uint64_t tmpl_slot(const cg_signable_tmpl* tmpls, uint32_t n_tmpls) {
@@ -1044,11 +1044,16 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   std::vector<uint32_t> counts(n_keys ? n_keys : 1, 0u);
   const uint64_t nt = n_sigs < (1u << 16) ? 1 : 16;
   auto sample_counts = [&] {
-    static const uint32_t S = [] {  // CG_TXSIG_SAMPLE (A/B): 1 in S signatures counted (power of two)
+    // 1 in S signatures counted (CG_TXSIG_SAMPLE, a power of two, overrides): S = 32 when keys average
+    // at least 256 uses (every key far above the 32-use full-table threshold), else 8: at S = 32 an
+    // unsampled key could not be told from one at the threshold, and a long-tailed key mix (Zipf
+    // over 1M keys) built full tables for every used key (125 -> 55 M sigs/s, profiles/r03/v12)
+    static const uint32_t S_env = [] {
       const char* v = getenv("CG_TXSIG_SAMPLE");
-      const uint32_t x = v ? (uint32_t)strtoul(v, nullptr, 10) : CG_TXSIG_COUNT_SAMPLE;
-      return x && (x & (x - 1)) == 0 ? x : CG_TXSIG_COUNT_SAMPLE;
+      const uint32_t x = v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
+      return x && (x & (x - 1)) == 0 ? x : 0u;
     }();
+    const uint32_t S = S_env ? S_env : n_sigs >= 256ull * (n_keys ? n_keys : 1) ? CG_TXSIG_COUNT_SAMPLE : 8u;
     // CG_TXSIG_SAMPLE_BLOCK (A/B): consecutive records per sample. 8 reads an eighth of the table's
     // cache lines instead of all of them (every 8th 24-B record): the pass went 5.3 -> 2.8 ms on the
     // configs[4] shard, 218 -> 238 M sigs/s (profiles/r03/env_ec3); a key the block sampling
@@ -1087,11 +1092,12 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     // c sampled uses -> S (c + 2 sqrt(c) + 1): about two standard deviations above the unbiased
     // S c, so a key whose true count clears a mode threshold is not sampled below it (on the
     // configs[4] shard the plain estimate put 2 of 4096 Ed25519 keys, true minimum 1 634 uses, under
-    // the 1 536 wide threshold: full tables and a 170 us pf ladder per chunk, profiles/r03/v5); at
-    // least S, so every key has its row-0 table
+    // the 1 536 wide threshold: full tables and a 170 us pf ladder per chunk, profiles/r03/v5); an
+    // unsampled key counts min(S, 8): its row-0 table, so every key a signature may use has one
     for (uint32_t k = 0; k < n_keys; ++k) {
       const uint64_t c = counts[k];
-      const uint64_t e = (uint64_t)S * (c + 2 * (uint64_t)std::ceil(std::sqrt((double)c)) + 1);
+      const uint64_t e = c ? (uint64_t)S * (c + 2 * (uint64_t)std::ceil(std::sqrt((double)c)) + 1)
+                           : (S < 8u ? S : 8u);  // unsampled: row-0 tables (below the 32-use threshold)
       counts[k] = e > 0xfffffff0ull ? 0xfffffff0u : (uint32_t)e;
     }
   };

@@ -334,47 +334,43 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
   const KeyWs w = key_ws((void*)d_keyprep, n_keys, wide);
   const ItemWs iw = item_ws(d_item_ws, n_items);
   hipError_t e = hipSuccess;
-  // row-0 and full-table ladders: on the side streams (after their tables) when forked, else first
-  // on `stream`. Both serve few items per call on a wide-table workload, where on `stream` a launch
-  // holding a handful of items cost its whole latency (k_ed_ladder_pf, 170 us per chunk for 2 keys
-  // under the wide threshold: profiles/r03/v5); on a side stream it runs beside the wide ladders.
+  // row-0 ladders: on the side streams (after their tables) when forked, else first on `stream`.
+  // The full-table ladders stay on `stream`: on a side stream (round 3, for a handful of items per
+  // chunk) a persistent full-GPU grid there held every slot while the main stream's next fronts
+  // waited (Zipf keys: 125 -> 56 M sigs/s, profiles/r03/v12 vs v9); the stray full-table launch it
+  // was meant to hide is gone with the biased count estimate.
   if (fork) {
     e = hipEventRecord(fork->front, stream);
     for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->front, 0);
     if (e != hipSuccess) return e;
   }
-  hipStream_t s_ed = fork ? fork->side[2] : stream, s_r1 = fork ? fork->side[0] : stream,
-              s_k1 = fork ? fork->side[1] : stream;
-  CG_TIME(fork, CG_STAGE_ED_LADDER_ROW0, s_ed, ed_launch_ladder(false, d_items, n_items, d_status, w, iw, d_btab, s_ed));
-  CG_TIME(fork, CG_STAGE_R1_LADDER_ROW0, s_r1,
-          ec_launch_ladder(CG_CURVE_R1, false, d_items, n_items, d_status, w, iw, d_btab, s_r1));
-  CG_TIME(fork, CG_STAGE_K1_LADDER_ROW0, s_k1,
-          ec_launch_ladder(CG_CURVE_K1, false, d_items, n_items, d_status, w, iw, d_btab, s_k1));
-  if (fork) {
-    hipStreamWaitEvent(s_ed, fork->ready[2], 0);
-    hipStreamWaitEvent(s_r1, fork->ready[0], 0);
-    hipStreamWaitEvent(s_k1, fork->ready[1], 0);
-  }
-  CG_TIME(fork, CG_STAGE_ED_LADDER, s_ed, ed_launch_ladder(true, d_items, n_items, d_status, w, iw, d_btab, s_ed));
-  CG_TIME(fork, CG_STAGE_R1_LADDER, s_r1,
-          ec_launch_ladder(CG_CURVE_R1, true, d_items, n_items, d_status, w, iw, d_btab, s_r1));
-  CG_TIME(fork, CG_STAGE_K1_LADDER, s_k1,
-          ec_launch_ladder(CG_CURVE_K1, true, d_items, n_items, d_status, w, iw, d_btab, s_k1));
+  CG_TIME(fork, CG_STAGE_ED_LADDER_ROW0, fork ? fork->side[2] : stream,
+          ed_launch_ladder(false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[2] : stream));
+  CG_TIME(fork, CG_STAGE_R1_LADDER_ROW0, fork ? fork->side[0] : stream,
+          ec_launch_ladder(CG_CURVE_R1, false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[0] : stream));
+  CG_TIME(fork, CG_STAGE_K1_LADDER_ROW0, fork ? fork->side[1] : stream,
+          ec_launch_ladder(CG_CURVE_K1, false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[1] : stream));
   if (fork) {
     for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventRecord(fork->row0[k], fork->side[k]);
     if (e != hipSuccess) return e;
   }
-  // wide-table ladders on `stream`, each after its tables; Ed25519 finish after all its ladders
+  // full-table ladders on `stream`, each after its tables; Ed25519 finish after both ladders
+  // wide-table ladders right after their class's full-table one (same tables-ready event)
   if (fork) hipStreamWaitEvent(stream, fork->ready[2], 0);
+  CG_TIME(fork, CG_STAGE_ED_LADDER, stream, ed_launch_ladder(true, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (w.cap_ed)
     CG_TIME(fork, CG_STAGE_ED_LADDER_WIDE, stream, ed_launch_ladder_wide(d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) hipStreamWaitEvent(stream, fork->row0[2], 0);
   CG_TIME(fork, CG_STAGE_ED_FINISH, stream, ed_launch_finish(d_items, n_items, d_arena, arena_len, d_status, iw, stream));
   if (fork) hipStreamWaitEvent(stream, fork->ready[0], 0);
+  CG_TIME(fork, CG_STAGE_R1_LADDER, stream,
+          ec_launch_ladder(CG_CURVE_R1, true, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (w.cap_ec)
     CG_TIME(fork, CG_STAGE_R1_LADDER_WIDE, stream,
             ec_launch_ladder_wide(CG_CURVE_R1, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) hipStreamWaitEvent(stream, fork->ready[1], 0);
+  CG_TIME(fork, CG_STAGE_K1_LADDER, stream,
+          ec_launch_ladder(CG_CURVE_K1, true, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (w.cap_ec)
     CG_TIME(fork, CG_STAGE_K1_LADDER_WIDE, stream,
             ec_launch_ladder_wide(CG_CURVE_K1, d_items, n_items, d_status, w, iw, d_btab, stream));

@@ -1089,14 +1089,16 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
         });
       for (auto& t : th) t.join();
     }
-    // c sampled uses -> S (c + 2 sqrt(c) + 1): about two standard deviations above the unbiased
-    // S c, so a key whose true count clears a mode threshold is not sampled below it (on the
+    // c sampled uses -> S (c + 3 sqrt(c) + 1): about three standard deviations above the unbiased
+    // S c, so a key whose true count clears a mode threshold is not sampled below it (two were not
+    // enough at 1 in 32: a few keys got full tables and a 0.18 ms full-table ladder per chunk,
+    // profiles/r03/v14; on the
     // configs[4] shard the plain estimate put 2 of 4096 Ed25519 keys, true minimum 1 634 uses, under
     // the 1 536 wide threshold: full tables and a 170 us pf ladder per chunk, profiles/r03/v5); an
     // unsampled key counts min(S, 8): its row-0 table, so every key a signature may use has one
     for (uint32_t k = 0; k < n_keys; ++k) {
       const uint64_t c = counts[k];
-      const uint64_t e = c ? (uint64_t)S * (c + 2 * (uint64_t)std::ceil(std::sqrt((double)c)) + 1)
+      const uint64_t e = c ? (uint64_t)S * (c + 3 * (uint64_t)std::ceil(std::sqrt((double)c)) + 1)
                            : (S < 8u ? S : 8u);  // unsampled: row-0 tables (below the 32-use threshold)
       counts[k] = e > 0xfffffff0ull ? 0xfffffff0u : (uint32_t)e;
     }

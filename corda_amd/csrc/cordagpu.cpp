@@ -1096,10 +1096,16 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     // configs[4] shard the plain estimate put 2 of 4096 Ed25519 keys, true minimum 1 634 uses, under
     // the 1 536 wide threshold: full tables and a 170 us pf ladder per chunk, profiles/r03/v5); an
     // unsampled key counts min(S, 8): its row-0 table, so every key a signature may use has one
+    // In a hot call (1 in 32: keys average 256+ uses) every sampled key is counted up to the wide
+    // threshold: a few keys left in full-table mode cost a serial full-table launch per chunk (0.18
+    // ms, ~1.4% of the headline, profiles/r03/ab_der), a wide table costs about 230 items' work.
+    const cg::WidePool thr = cg::make_wide_pool(nullptr, n_keys, n_sigs);  // the wide thresholds
+    const uint64_t floor_hot = S >= CG_TXSIG_COUNT_SAMPLE ? (uint64_t)std::max(thr.min_ed, thr.min_ec) : 0u;
     for (uint32_t k = 0; k < n_keys; ++k) {
       const uint64_t c = counts[k];
-      const uint64_t e = c ? (uint64_t)S * (c + 3 * (uint64_t)std::ceil(std::sqrt((double)c)) + 1)
-                           : (S < 8u ? S : 8u);  // unsampled: row-0 tables (below the 32-use threshold)
+      uint64_t e = c ? (uint64_t)S * (c + 3 * (uint64_t)std::ceil(std::sqrt((double)c)) + 1)
+                     : (S < 8u ? S : 8u);  // unsampled: row-0 tables (below the 32-use threshold)
+      if (c && e < floor_hot) e = floor_hot;
       counts[k] = e > 0xfffffff0ull ? 0xfffffff0u : (uint32_t)e;
     }
   };

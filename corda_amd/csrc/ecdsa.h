@@ -432,15 +432,30 @@ CG_HD bool ec_decompress(u256w& y, const u256w& x, uint32_t odd, const EcConsts&
 }
 
 // ------------------------------------------------------------------ DER (StdDSAEncoder)
-// Reads one byte of the signature
+// The parser reads the signature through a byte source: DerArena straight from the arena (each byte
+// a dword load: the host build and long signatures), DerStaged from a copy the caller staged (the
+// device stage copies a signature's dwords into LDS with a few 16-byte loads first: read byte by
+// byte from the arena, 64 lanes' scattered signatures cost ~140 loads per item, k_ec_prep ran at
+// 0.15 of its issue rate moving 2.4 KB per item, profiles/r03/v14/pmc_traffic.json).
+// One byte of the arena (key decoding, DerArena)
 CG_HD uint32_t der_byte(const uint8_t* arena, uint64_t lr, uint64_t off) {
   return cg_ld_bytes4(arena, lr, off) & 0xffu;
 }
+struct DerArena {
+  const uint8_t* arena;
+  uint64_t lr, off;
+  CG_HDM uint32_t byte(uint32_t i) const { return der_byte(arena, lr, off + i); }
+};
+struct DerStaged {
+  const uint8_t* p;  // the signature's first byte
+  CG_HDM uint32_t byte(uint32_t i) const { return p[i]; }
+};
 
 // DER length at position *i (within [0, n)); returns false if malformed / not minimal.
-CG_HD bool der_len(const uint8_t* arena, uint64_t lr, uint64_t base, uint32_t n, uint32_t* i, uint32_t* out) {
+template <class Src>
+CG_HD bool der_len(const Src& b, uint32_t n, uint32_t* i, uint32_t* out) {
   if (*i >= n) return false;
-  const uint32_t l0 = der_byte(arena, lr, base + (*i)++);
+  const uint32_t l0 = b.byte((*i)++);
   if (l0 < 0x80u) {
     *out = l0;
     return true;
@@ -448,7 +463,7 @@ CG_HD bool der_len(const uint8_t* arena, uint64_t lr, uint64_t base, uint32_t n,
   const uint32_t nb = l0 & 0x7fu;
   if (nb == 0 || nb > 4 || *i + nb > n) return false;
   uint32_t v = 0;
-  for (uint32_t k = 0; k < nb; ++k) v = (v << 8) | der_byte(arena, lr, base + (*i)++);
+  for (uint32_t k = 0; k < nb; ++k) v = (v << 8) | b.byte((*i)++);
   if (v < 0x80u) return false;
   if (nb > 1 && (v >> (8 * (nb - 1))) == 0) return false;
   *out = v;
@@ -457,15 +472,15 @@ CG_HD bool der_len(const uint8_t* arena, uint64_t lr, uint64_t base, uint32_t n,
 
 // INTEGER at *i: validates strict DER; value (if 0 < v < 2^256) -> out (little-endian words),
 // *in_range = false if negative, zero or >= 2^256.
-CG_HD bool der_int(const uint8_t* arena, uint64_t lr, uint64_t base, uint32_t n, uint32_t* i, u256w& out,
-                   bool* in_range) {
-  if (*i >= n || der_byte(arena, lr, base + *i) != 0x02u) return false;
+template <class Src>
+CG_HD bool der_int(const Src& b, uint32_t n, uint32_t* i, u256w& out, bool* in_range) {
+  if (*i >= n || b.byte(*i) != 0x02u) return false;
   (*i)++;
   uint32_t ln;
-  if (!der_len(arena, lr, base, n, i, &ln)) return false;
+  if (!der_len(b, n, i, &ln)) return false;
   if (ln == 0 || *i + ln > n) return false;
-  const uint32_t c0 = der_byte(arena, lr, base + *i);
-  const uint32_t c1 = ln > 1 ? der_byte(arena, lr, base + *i + 1) : 0;
+  const uint32_t c0 = b.byte(*i);
+  const uint32_t c1 = ln > 1 ? b.byte(*i + 1) : 0;
   if (ln > 1 && ((c0 == 0 && c1 < 0x80u) || (c0 == 0xffu && c1 >= 0x80u))) return false;
   u256_zero(out);
   uint32_t start = *i, len = ln;
@@ -482,29 +497,39 @@ CG_HD bool der_int(const uint8_t* arena, uint64_t lr, uint64_t base, uint32_t n,
     *in_range = false;
     return true;
   }
-  for (uint32_t k = 0; k < len; ++k) {
-    const uint32_t byte = der_byte(arena, lr, base + start + k);
-    const uint32_t pos = len - 1 - k;  // little-endian byte index
-    out.w[pos >> 2] |= byte << (8 * (pos & 3));
+  // word by word with static indices (a per-lane byte position into out.w[] put it in scratch)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t pos = 4 * j + q;  // little-endian byte index
+      if (pos < len) w |= b.byte(start + len - 1 - pos) << (8 * q);
+    }
+    out.w[j] = w;
   }
   *in_range = !u256_iszero(out);
   return true;
 }
 
 // returns 0 ok, 2 malformed; *range_ok false => INVALID
-CG_HD uint32_t der_sig(const uint8_t* arena, uint64_t lr, uint64_t off, uint32_t n, u256w& r, u256w& s,
-                       bool* range_ok) {
-  if (n < 2 || der_byte(arena, lr, off) != 0x30u) return 2;
+template <class Src>
+CG_HD uint32_t der_sig(const Src& b, uint32_t n, u256w& r, u256w& s, bool* range_ok) {
+  if (n < 2 || b.byte(0) != 0x30u) return 2;
   uint32_t i = 1, sl;
-  if (!der_len(arena, lr, off, n, &i, &sl)) return 2;
+  if (!der_len(b, n, &i, &sl)) return 2;
   if (i + sl != n) return 2;
   bool ok1 = false, ok2 = false;
-  if (!der_int(arena, lr, off, n, &i, r, &ok1)) return 2;
+  if (!der_int(b, n, &i, r, &ok1)) return 2;
   if (i >= n) return 2;
-  if (!der_int(arena, lr, off, n, &i, s, &ok2)) return 2;
+  if (!der_int(b, n, &i, s, &ok2)) return 2;
   if (i != n) return 2;
   *range_ok = ok1 && ok2;
   return 0;
+}
+CG_HD uint32_t der_sig(const uint8_t* arena, uint64_t lr, uint64_t off, uint32_t n, u256w& r, u256w& s,
+                       bool* range_ok) {
+  return der_sig(DerArena{arena, lr, off}, n, r, s, range_ok);
 }
 
 // ------------------------------------------------------------------ key bytes

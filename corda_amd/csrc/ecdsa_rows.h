@@ -225,13 +225,12 @@ struct EcItemWs {
 
 // Stage 1: DER, range checks, e = SHA-256(M) mod n. Returns 0 (pending: ws filled),
 // 1 INVALID or 2 SIG_MALFORMED.
-template <int C, class Ld = ArenaLd>
-CG_HD uint32_t ecdsa_prep_ld(EcItemWs& ws, const uint8_t* arena, uint64_t lr, uint64_t sig_off, uint32_t sig_len,
-                             const Ld& mld, uint64_t msg_off, uint64_t msg_len, const uint32_t* mid = nullptr,
-                             uint32_t mid_blocks = 0) {
+template <int C, class Ld = ArenaLd, class Src = DerArena>
+CG_HD uint32_t ecdsa_prep_ld(EcItemWs& ws, const Src& sig, uint32_t sig_len, const Ld& mld, uint64_t msg_off,
+                             uint64_t msg_len, const uint32_t* mid = nullptr, uint32_t mid_blocks = 0) {
   u256w r, s;
   bool range_ok = false;
-  if (der_sig(arena, lr, sig_off, sig_len, r, s, &range_ok)) return 2;
+  if (der_sig(sig, sig_len, r, s, &range_ok)) return 2;
   if (!range_ok) return 1;
   if (!u256_lt_mod<C, 1>(r) || !u256_lt_mod<C, 1>(s)) return 1;
   uint32_t h[8];
@@ -258,7 +257,8 @@ template <int C>
 CG_HD uint32_t ecdsa_prep(EcItemWs& ws, const uint8_t* arena, uint64_t lr, uint64_t sig_off, uint32_t sig_len,
                           const uint8_t* marena, uint64_t mlr, uint64_t msg_off, uint64_t msg_len,
                           const uint32_t* mid = nullptr, uint32_t mid_blocks = 0) {
-  return ecdsa_prep_ld<C>(ws, arena, lr, sig_off, sig_len, ArenaLd{marena, mlr}, msg_off, msg_len, mid, mid_blocks);
+  return ecdsa_prep_ld<C>(ws, DerArena{arena, lr, sig_off}, sig_len, ArenaLd{marena, mlr}, msg_off, msg_len, mid,
+                          mid_blocks);
 }
 
 // Items per lane of k_ec_inv, one inversion each (A/B 8 vs 16 vs 32 on MI355X: profiles/r02/sha_v2;

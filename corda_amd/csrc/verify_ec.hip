@@ -222,6 +222,7 @@ __global__ void __launch_bounds__(64) k_ec_gtab_init(EcGTab* __restrict__ out, E
   const int cls = plan_class_of_curve(C);             \
   const uint32_t beg = ranges[cls], end = ranges[cls + 1]
 
+#define EC_SIG_STAGED 80  // signature bytes k_ec_prep stages (DER for a 256-bit curve is at most 72)
 template <int C, bool Fused>  // Fused: every message is a SignableData splice (the tx-signature paths)
 __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
                                                  const uint32_t* __restrict__ ranges,
@@ -231,6 +232,10 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
                                                  uint32_t mode, uint8_t* __restrict__ status,
                                                  EcItemWs* __restrict__ ws) {
   EC_RANGE(C);
+  // each lane's signature staged in LDS (21 dwords from its 4-aligned start: up to EC_SIG_STAGED
+  // bytes) with six 16-byte loads, then parsed byte by byte from there (ecdsa.h DerStaged)
+  __shared__ uint32_t sig_stage[256 * 21];
+  uint32_t* my = sig_stage + 21 * threadIdx.x;  // odd stride: conflict-free dword accesses
   for (Walk wk = walk_units(end - beg); wk.u < wk.end; wk.u += wk.step) {
   const uint64_t p = beg + wk.u;
   const uint32_t i = perm[p];
@@ -247,12 +252,30 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
   } else {
     EcItemWs w;
     const TmplMid* mid = item_tmpl_mid(it, msgs);
-    const uint32_t r =
-        Fused ? ecdsa_prep_ld<C>(w, arena, round4(arena_len), it.sig_off, it.sig_len, item_splice(it, msgs), 0,
-                                 it.msg_len, mid->state, mid->blocks)
-              : ecdsa_prep<C>(w, arena, round4(arena_len), it.sig_off, it.sig_len, item_msg_arena(it, arena, msgs),
-                              round4(item_msg_len(it, arena_len, msgs_len, msgs)), it.msg_off, it.msg_len,
-                              mid ? mid->state : nullptr, mid ? mid->blocks : 0u);
+    const uint64_t lr = round4(arena_len);
+    uint32_t r;
+    if (it.sig_len <= EC_SIG_STAGED) {
+      const uint64_t a0 = it.sig_off & ~(uint64_t)3;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        uint32_t v[4];
+        cg_ld_dwords4(v, arena, lr, a0 + 16 * q);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) my[4 * q + k] = v[k];  // dword stores: a lane's image is only 4-aligned
+      }
+      my[20] = a0 + 80 < lr ? cg_ld32(arena + a0 + 80) : 0u;
+      const DerStaged sig{(const uint8_t*)my + (it.sig_off & 3)};
+      r = Fused ? ecdsa_prep_ld<C>(w, sig, it.sig_len, item_splice(it, msgs), 0, it.msg_len, mid->state, mid->blocks)
+                : ecdsa_prep_ld<C>(w, sig, it.sig_len, ArenaLd{item_msg_arena(it, arena, msgs),
+                                                               round4(item_msg_len(it, arena_len, msgs_len, msgs))},
+                                   it.msg_off, it.msg_len, mid ? mid->state : nullptr, mid ? mid->blocks : 0u);
+    } else {  // long (malformed or out-of-range) encodings: straight from the arena
+      const DerArena sig{arena, lr, it.sig_off};
+      r = Fused ? ecdsa_prep_ld<C>(w, sig, it.sig_len, item_splice(it, msgs), 0, it.msg_len, mid->state, mid->blocks)
+                : ecdsa_prep_ld<C>(w, sig, it.sig_len, ArenaLd{item_msg_arena(it, arena, msgs),
+                                                               round4(item_msg_len(it, arena_len, msgs_len, msgs))},
+                                   it.msg_off, it.msg_len, mid ? mid->state : nullptr, mid ? mid->blocks : 0u);
+    }
     if (r == 0) {
       ws[p] = w;
       st = (uint8_t)(EC_PENDING_BASE + C);

@@ -314,6 +314,17 @@ static_assert(sizeof(EcItemWs) == ITEM_SLOT, "ECDSA stage hand-off must fill one
 // Item workspace: [slots: n x ITEM_SLOT, by plan position][perm: n x u32][ranges]
 //                 [sort keys in/out, sort values in: 3 x n x u32][radix-sort temporary storage]
 size_t plan_sort_temp_bytes(uint64_t n_items);  // plan_sort.hip
+// Plan-ordered Ed25519 columns k_ed_hash writes for the ladders and the finish, so that they read
+// coalesced instead of items[perm[p]] / status[perm[p]] / the signature's R in the arena (a cache
+// line each per item: k_ed_finish moved 650 B per item at 0.48 of its issue rate,
+// profiles/r03/v14/pmc_traffic.json): R's 8 words (word w of position p at r[w * n + p]), the
+// pending flag, the key index.
+struct EdCols {
+  uint32_t* r;
+  uint8_t* pend;
+  uint32_t* key;
+  uint64_t n;
+};
 struct ItemWs {
   void* slots;
   uint32_t* perm;
@@ -321,6 +332,7 @@ struct ItemWs {
   uint32_t *skey_in, *skey_out, *sval_in;
   void* sort_temp;
   size_t sort_temp_bytes;
+  EdCols ed;
 };
 static inline ItemWs item_ws(void* base, uint64_t n_items) {
   const size_t n = n_items ? n_items : 1;
@@ -340,11 +352,19 @@ static inline ItemWs item_ws(void* base, uint64_t n_items) {
   p += al256(n * sizeof(uint32_t));
   w.sort_temp = p;
   w.sort_temp_bytes = plan_sort_temp_bytes(n);
+  p += al256(w.sort_temp_bytes);
+  w.ed.n = n;
+  w.ed.r = (uint32_t*)p;
+  p += al256(8 * n * sizeof(uint32_t));
+  w.ed.key = (uint32_t*)p;
+  p += al256(n * sizeof(uint32_t));
+  w.ed.pend = p;
   return w;
 }
 static inline size_t item_ws_total(uint64_t n_items) {
   const size_t n = n_items ? n_items : 1;
-  return al256(n * ITEM_SLOT) + 4 * al256(n * sizeof(uint32_t)) + 256 + al256(plan_sort_temp_bytes(n));
+  return al256(n * ITEM_SLOT) + 4 * al256(n * sizeof(uint32_t)) + 256 + al256(plan_sort_temp_bytes(n)) +
+         al256(8 * n * sizeof(uint32_t)) + al256(n * sizeof(uint32_t)) + al256(n);
 }
 hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d_keys, uint32_t n_keys,
                        const uint32_t* d_uses, const uint32_t* d_wide_idx, const ItemWs& iw, hipStream_t stream);

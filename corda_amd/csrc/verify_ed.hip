@@ -346,9 +346,11 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
                                             const uint32_t* __restrict__ perm, const EdKeyHdr* __restrict__ hdr,
                                             const uint8_t* __restrict__ arena, uint64_t arena_len,
                                             const uint8_t* __restrict__ msgs, uint64_t msgs_len, uint32_t mode,
-                                            uint8_t* __restrict__ status, EdDigits* __restrict__ dig, bool wide) {
+                                            uint8_t* __restrict__ status, EdDigits* __restrict__ dig, bool wide,
+                                            const EdCols& ec) {
   const uint32_t i = perm[p];
   const cg_item it = items[i];
+  ec.key[p] = it.key_idx;
   const EdKeyHdr* kh = hdr + it.key_idx;
   uint8_t st;  // a key that does not decode overrides this in k_ed_ladder
   if (mode == CG_MODE_DOVERIFY && (it.sig_len == 0 || it.msg_len == 0)) {
@@ -400,7 +402,10 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
       dig[p] = d;
     }
     st = (uint8_t)ED_PENDING;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) ec.r[(size_t)w * ec.n + p] = sw[w];
   }
+  ec.pend[p] = st == ED_PENDING;
   status[i] = st;
 }
 
@@ -409,11 +414,11 @@ __global__ void __launch_bounds__(256, ED_HASH_WAVES_PER_SIMD) k_ed_hash(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
     const EdKeyHdr* __restrict__ hdr, const uint8_t* __restrict__ arena, uint64_t arena_len,
     const uint8_t* __restrict__ msgs, uint64_t msgs_len, uint32_t mode, uint8_t* __restrict__ status,
-    EdDigits* __restrict__ dig) {
+    EdDigits* __restrict__ dig, EdCols ec) {
   const uint32_t beg = ranges[PLAN_ED], wbeg = ranges[PLAN_WIDE + PLAN_ED];
   for (Walk w = walk_units(ranges[PLAN_ED + 1] - beg); w.u < w.end; w.u += w.step)
     ed_hash_one<Fused>(beg + w.u, items, perm, hdr, arena, arena_len, msgs, msgs_len, mode, status, dig,
-                       beg + w.u >= wbeg);
+                       beg + w.u >= wbeg, ec);
 }
 
 // One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the row tables (B rows
@@ -576,19 +581,19 @@ __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* 
 __global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_pf(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
     const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBWideTab* __restrict__ btab,
-    uint8_t* __restrict__ status, void* __restrict__ slots) {
+    uint8_t* __restrict__ status, void* __restrict__ slots, EdCols ec) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[4 * EdOps::kWaveBytes];
   const uint32_t beg = ranges[PLAN_FULL + PLAN_ED];
   uint8_t* wave_lds = stage + (threadIdx.x >> 6) * EdOps::kWaveBytes;
   for (Walk w = walk_units(ranges[PLAN_WIDE + PLAN_ED] - beg); w.u < w.end; w.u += w.step) {
     const uint64_t p = beg + w.u;
-    const uint32_t i = perm[p];
-    const uint32_t key = items[i].key_idx;
+    const uint32_t key = ec.key[p];
     if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
-      status[i] = CG_KEY_INVALID;
+      status[perm[p]] = CG_KEY_INVALID;
+      ec.pend[p] = 0;
       continue;
     }
-    if (status[i] != ED_PENDING) continue;
+    if (!ec.pend[p]) continue;
     // every lane still here runs the same DMA sequence; lanes that left do not take part, and
     // the LDS image is per lane, so no barrier is needed
     ge_p2 q;
@@ -673,19 +678,19 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
 __global__ void __launch_bounds__(256, ED_LADDER_WIDE_WAVES) k_ed_ladder_wide(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
     const EdKeyHdr* __restrict__ hdr, const uint32_t* __restrict__ wide_idx, const EdWideSlot* __restrict__ wed,
-    const EdBWideTab* __restrict__ btab, uint8_t* __restrict__ status, void* __restrict__ slots) {
+    const EdBWideTab* __restrict__ btab, uint8_t* __restrict__ status, void* __restrict__ slots, EdCols ec) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[4 * EdOps::kWaveBytes];
   const uint32_t beg = ranges[PLAN_WIDE + PLAN_ED];
   uint8_t* wave_lds = stage + (threadIdx.x >> 6) * EdOps::kWaveBytes;
   for (Walk w = walk_units(ranges[PLAN_ED + 1] - beg); w.u < w.end; w.u += w.step) {
     const uint64_t p = beg + w.u;
-    const uint32_t i = perm[p];
-    const uint32_t key = items[i].key_idx;
+    const uint32_t key = ec.key[p];
     if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
-      status[i] = CG_KEY_INVALID;
+      status[perm[p]] = CG_KEY_INVALID;
+      ec.pend[p] = 0;
       continue;
     }
-    if (status[i] != ED_PENDING) continue;
+    if (!ec.pend[p]) continue;
     ge_p2 q;
     ed_double_scalar_wide_pf(q, (const uint32_t*)((const uint8_t*)slots + (size_t)p * ITEM_SLOT),
                              wed[wide_idx[key]].tab, *btab, wave_lds, __lane_id());
@@ -702,19 +707,19 @@ template <bool Full>
 __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
     const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBWideTab* __restrict__ btab,
-    uint8_t* __restrict__ status, void* __restrict__ slots) {
+    uint8_t* __restrict__ status, void* __restrict__ slots, EdCols ec) {
   // the plan's mode split: row-0 keys' items first, then full-table keys' (plan_sort.hip)
   const uint32_t beg = Full ? ranges[PLAN_FULL + PLAN_ED] : ranges[PLAN_ED];
   const uint32_t end = Full ? ranges[PLAN_WIDE + PLAN_ED] : ranges[PLAN_FULL + PLAN_ED];
   for (Walk w = walk_units(end - beg); w.u < w.end; w.u += w.step) {
     const uint64_t p = beg + w.u;
-    const uint32_t i = perm[p];
-    const uint32_t key = items[i].key_idx;
+    const uint32_t key = ec.key[p];
     if (hdr[key].status != 0) {  // the key check comes first in i2p / Crypto.doVerify
-      status[i] = CG_KEY_INVALID;
+      status[perm[p]] = CG_KEY_INVALID;
+      ec.pend[p] = 0;
       continue;
     }
-    if (status[i] != ED_PENDING) continue;
+    if (!ec.pend[p]) continue;
     const EdDigits d = ((const EdDigits*)slots)[p];
     ge_p2 q;
     if (Full) {
@@ -734,9 +739,8 @@ __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
 #define ED_FINISH_K 16
 #endif
 __device__ __forceinline__ void ed_finish_one(uint64_t unit, uint32_t beg, uint32_t end,
-                                              const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
-                                              const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                              uint8_t* __restrict__ status, const ge_p2* __restrict__ rin) {
+                                              const uint32_t* __restrict__ perm, uint8_t* __restrict__ status,
+                                              const ge_p2* __restrict__ rin, const EdCols& ec) {
   const uint64_t base = beg + (unit >> 6) * (64 * ED_FINISH_K) + (unit & 63);
   fe acc[ED_FINISH_K];
   fe run;
@@ -744,7 +748,7 @@ __device__ __forceinline__ void ed_finish_one(uint64_t unit, uint32_t beg, uint3
   uint32_t pend = 0;
   for (uint32_t k = 0; k < ED_FINISH_K; ++k) {
     const uint64_t p = base + 64 * k;
-    const bool pd = p < end && status[perm[p]] == ED_PENDING;
+    const bool pd = p < end && ec.pend[p];
     pend |= (uint32_t)pd << k;
     if (pd) fe_mul(run, run, rin[p].Z);
     fe_copy(acc[k], run);
@@ -752,7 +756,6 @@ __device__ __forceinline__ void ed_finish_one(uint64_t unit, uint32_t beg, uint3
   if (!pend) return;
   fe inv;
   fe_invert(inv, run);
-  const uint64_t lr = round4(arena_len);
   for (int k = ED_FINISH_K - 1; k >= 0; --k) {
     if (!((pend >> k) & 1u)) continue;
     const uint64_t p = base + 64 * (uint32_t)k;
@@ -763,23 +766,20 @@ __device__ __forceinline__ void ed_finish_one(uint64_t unit, uint32_t beg, uint3
     else fe_copy(zi, inv);
     fe_mul(t, inv, P.Z);
     fe_copy(inv, t);
-    const uint32_t i = perm[p];
     uint32_t rw[8];
-    const uint64_t so = items[i].sig_off;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) rw[w] = cg_ld_bytes4(arena, lr, so + 4 * w);
-    status[i] = (uint8_t)ed_encode_cmp(P, zi, rw);
+    for (int w = 0; w < 8; ++w) rw[w] = ec.r[(size_t)w * ec.n + p];
+    status[perm[p]] = (uint8_t)ed_encode_cmp(P, zi, rw);
   }
 }
 
-__global__ void __launch_bounds__(256) k_ed_finish(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
-                                                   const uint32_t* __restrict__ ranges,
-                                                   const uint8_t* __restrict__ arena, uint64_t arena_len,
-                                                   uint8_t* __restrict__ status, const ge_p2* __restrict__ rin) {
+__global__ void __launch_bounds__(256) k_ed_finish(const uint32_t* __restrict__ perm,
+                                                   const uint32_t* __restrict__ ranges, uint8_t* __restrict__ status,
+                                                   const ge_p2* __restrict__ rin, EdCols ec) {
   const uint32_t beg = ranges[PLAN_ED], end = ranges[PLAN_ED + 1];
   const uint64_t units = ((uint64_t)(end - beg) + 64 * ED_FINISH_K - 1) / (64 * ED_FINISH_K) * 64;
   for (Walk w = walk_units(units); w.u < w.end; w.u += w.step)
-    ed_finish_one(w.u, beg, end, items, perm, arena, arena_len, status, rin);
+    ed_finish_one(w.u, beg, end, perm, status, rin, ec);
 }
 
 hipError_t ed_upload_constants() {
@@ -856,10 +856,10 @@ void ed_launch_front(const cg_item* d_items, uint64_t n_items, const uint8_t* d_
   const unsigned grid = walk_grid(n_items, B, WALK_CAP(ED_HASH_WAVES_PER_SIMD));
   if (d_msgs)
     hipLaunchKernelGGL(k_ed_hash<true>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
-                       arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
+                       arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots, iw.ed);
   else
     hipLaunchKernelGGL(k_ed_hash<false>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr, d_arena,
-                       arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots);
+                       arena_len, d_msgs, msgs_len, mode, d_status, (EdDigits*)iw.slots, iw.ed);
 }
 
 void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
@@ -868,13 +868,13 @@ void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8
   const unsigned grid = walk_grid(n_items, B, WALK_CAP(full && ED_LADDER_PF ? ED_LADDER_PF_WAVES : ED_LADDER_WAVES_PER_SIMD));
   if (full && ED_LADDER_PF)
     hipLaunchKernelGGL(k_ed_ladder_pf, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                       w.tab, bwide(d_btab), d_status, iw.slots);
+                       w.tab, bwide(d_btab), d_status, iw.slots, iw.ed);
   else if (full)
     hipLaunchKernelGGL(k_ed_ladder<true>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                       w.tab, bwide(d_btab), d_status, iw.slots);
+                       w.tab, bwide(d_btab), d_status, iw.slots, iw.ed);
   else
     hipLaunchKernelGGL(k_ed_ladder<false>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
-                       w.hdr, w.tab, bwide(d_btab), d_status, iw.slots);
+                       w.hdr, w.tab, bwide(d_btab), d_status, iw.slots, iw.ed);
 }
 
 void ed_launch_ladder_wide(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
@@ -882,7 +882,7 @@ void ed_launch_ladder_wide(const cg_item* d_items, uint64_t n_items, uint8_t* d_
   const uint32_t B = 256;
   const unsigned grid = walk_grid(n_items, B, WALK_CAP(ED_LADDER_PF_WAVES));
   hipLaunchKernelGGL(k_ed_ladder_wide, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                     (const uint32_t*)w.wide_idx, (const EdWideSlot*)w.wed, bwide(d_btab), d_status, iw.slots);
+                     (const uint32_t*)w.wide_idx, (const EdWideSlot*)w.wed, bwide(d_btab), d_status, iw.slots, iw.ed);
 }
 
 void ed_launch_finish(const cg_item* d_items, uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len,
@@ -890,8 +890,11 @@ void ed_launch_finish(const cg_item* d_items, uint64_t n_items, const uint8_t* d
   const uint32_t B = 256;
   const uint64_t units = (n_items + 64 * ED_FINISH_K - 1) / (64 * ED_FINISH_K) * 64;
   const unsigned fgrid = walk_grid(units, B, WALK_CAP(2));
-  hipLaunchKernelGGL(k_ed_finish, dim3(fgrid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, d_arena,
-                     arena_len, d_status, (const ge_p2*)iw.slots);
+  (void)d_items;
+  (void)d_arena;
+  (void)arena_len;
+  hipLaunchKernelGGL(k_ed_finish, dim3(fgrid), dim3(B), 0, stream, iw.perm, iw.ranges, d_status, (const ge_p2*)iw.slots,
+                     iw.ed);
 }
 
 }  // namespace cg

@@ -701,8 +701,10 @@ CG_HD void ed_wide_row_build(ge_niels* out, const Park& pk, const ge_p3& P, int 
   fe_mul(inv, inv, h);  // 1 / (2 Z_e0 .. Z_e1-1): the half-scaled entries' 1/2
   fe_add(d4, d2, d2);
   fe_carry(d4);
-  // the walk back, each entry's parked coordinates and the previous running product loaded one
-  // entry ahead
+#ifndef ED_ROWS_PREFETCH  // 1: the walk back loads each entry's parked values one entry ahead
+#define ED_ROWS_PREFETCH 1
+#endif
+#if ED_ROWS_PREFETCH
   fe X, Y, Z, pr;
   pk.get(e1 - 1 - e0, X, Y, Z);
   if (e1 - 1 > e0) pk.get_run(e1 - 2 - e0, pr);
@@ -713,6 +715,13 @@ CG_HD void ed_wide_row_build(ge_niels* out, const Park& pk, const ge_p3& P, int 
       pk.get(k - 1 - e0, Xn, Yn, Zn);
       if (k - 1 > e0) pk.get_run(k - 2 - e0, prn);
     }
+#else  // parked lane-interleaved, the loads are coalesced: no prefetch registers (occupancy)
+#pragma unroll 1
+  for (int k = e1 - 1; k >= e0; --k) {
+    fe X, Y, Z, pr;
+    pk.get(k - e0, X, Y, Z);
+    if (k > e0) pk.get_run(k - 1 - e0, pr);
+#endif
     ge_p2 p;
     p.X = X;
     p.Y = Y;
@@ -726,10 +735,12 @@ CG_HD void ed_wide_row_build(ge_niels* out, const Park& pk, const ge_p3& P, int 
     ge_niels n;
     ed_niels_from(n, p, zi, d4);
     out[k] = n;
+#if ED_ROWS_PREFETCH
     X = Xn;
     Y = Yn;
     Z = Zn;
     pr = prn;
+#endif
   }
 }
 

@@ -68,24 +68,35 @@ __device__ __forceinline__ bool in_arena(uint64_t off, uint64_t len, uint64_t ar
 // the hash kernels read the splice through SpliceLd (sha2.h) from the workspace head below.
 #define CG_ITEM_FUSED 4u
 // Message workspace head (cg_verify_tx_signatures*, cg_verify_transactions*):
-//   [SpliceHdr, 256 B][TmplMid x n_tmpls, 256-aligned][template images: n_tmpls x slot]
+//   [SpliceHdr, 256 B][TmplMid x n_tmpls, 256-aligned][TmplW512 x n_tmpls][template images: n_tmpls x slot]
 struct SpliceHdr {
-  uint64_t ids;      // device address of the 32-byte ids
+  uint64_t ids;       // device address of the 32-byte ids
   uint64_t n_ids;
-  uint64_t img_off;  // byte offset of the images in the workspace
-  uint64_t slot;     // bytes per image (16-aligned, >= the longest message + 16)
+  uint64_t img_off;   // byte offset of the images in the workspace
+  uint64_t slot;      // bytes per image (16-aligned, >= the longest message + 16)
+  uint64_t w512_off;  // byte offset of the TmplW512 records
 };
 #define SPLICE_HDR_BYTES 256u
 struct TmplMid {
   uint32_t state[8];
   uint32_t blocks;      // prefix blocks absorbed into state
   uint32_t prefix_len;  // the id's position in the message
-  uint32_t pad[2];
+  uint32_t ed_mid;      // 1: the template's TmplW512 record holds the Ed25519 challenge's block 1
+  uint32_t pad;
 };
 static_assert(sizeof(TmplMid) == 48, "template midstate record");
-CG_HD uint64_t tmpl_mid_bytes(uint32_t n_tmpls) {
+// SHA-512(R || Abyte || M)'s block 1 is M[64, 192): with the id at prefix_len >= 192 it is template
+// prefix for every signature of the template, so its message schedule, round constants folded in
+// (wk[t] = W[t] + K[t]), is computed once per template (k_tmpl_prep) and k_ed_hash runs that block's
+// 80 rounds without the schedule (sha512_compress_wk).
+struct TmplW512 {
+  uint64_t wk[80];
+};
+#define TMPL_ED_MID_MIN_PREFIX 192u
+CG_HD uint64_t tmpl_w512_off(uint32_t n_tmpls) {
   return SPLICE_HDR_BYTES + (((uint64_t)n_tmpls * sizeof(TmplMid) + 255) & ~(uint64_t)255);
 }
+CG_HD uint64_t tmpl_mid_bytes(uint32_t n_tmpls) { return tmpl_w512_off(n_tmpls) + (uint64_t)n_tmpls * sizeof(TmplW512); }
 __device__ __forceinline__ bool item_fused(const cg_item& it, const uint8_t* msgs) {
   return msgs && (it.reserved0 & (CG_ITEM_MSG_WS | CG_ITEM_TMPL | CG_ITEM_FUSED)) ==
                      (CG_ITEM_MSG_WS | CG_ITEM_TMPL | CG_ITEM_FUSED);
@@ -95,16 +106,21 @@ __device__ __forceinline__ const TmplMid* item_tmpl_mid(const cg_item& it, const
              ? (const TmplMid*)(msgs + SPLICE_HDR_BYTES) + it.reserved1
              : nullptr;
 }
-// The splice of a fused item: its template's image with its tx id
-__device__ __forceinline__ SpliceLd item_splice(const cg_item& it, const uint8_t* msgs) {
+// The splice of template `tmpl` with tx id `tx` (a fused item: tmpl = reserved1, tx = msg_off). With a
+// wave-uniform tmpl the image address, length and id position are scalars, so SpliceLd's bounds and
+// overlap tests are scalar branches; only the id words are per lane.
+__device__ __forceinline__ SpliceLd tmpl_splice(uint32_t tmpl, uint64_t tx, const uint8_t* msgs) {
   const SpliceHdr* h = (const SpliceHdr*)msgs;
-  const TmplMid* m = (const TmplMid*)(msgs + SPLICE_HDR_BYTES) + it.reserved1;
+  const TmplMid* m = (const TmplMid*)(msgs + SPLICE_HDR_BYTES) + tmpl;
   SpliceLd ld;
-  ld.img = msgs + h->img_off + (uint64_t)it.reserved1 * h->slot;
+  ld.img = msgs + h->img_off + (uint64_t)tmpl * h->slot;
   ld.img_len = h->slot;
-  ld.id = (const uint32_t*)(uintptr_t)h->ids + 8ull * it.msg_off;
+  ld.id = (const uint32_t*)(uintptr_t)h->ids + 8ull * tx;
   ld.at = m->prefix_len;
   return ld;
+}
+__device__ __forceinline__ SpliceLd item_splice(const cg_item& it, const uint8_t* msgs) {
+  return tmpl_splice(it.reserved1, it.msg_off, msgs);
 }
 __device__ __forceinline__ bool item_in_ws(const cg_item& it, const uint8_t* msgs) {
   return (it.reserved0 & CG_ITEM_MSG_WS) && msgs != nullptr;

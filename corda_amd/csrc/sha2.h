@@ -224,6 +224,32 @@ CG_HD void sha512_compress(uint64_t s[8], uint64_t w[16]) {
   s[7] += h;
 }
 
+// The same 80 rounds over a precomputed schedule with the round constants folded in
+// (wk[t] = W[t] + K[t]: a block every lane of the wave shares, keyws.h TmplW512). The caller passes
+// a wave-uniform pointer, so the words are scalar loads, as the round constants are.
+CG_HD void sha512_compress_wk(uint64_t s[8], const uint64_t* __restrict__ wk) {
+  uint64_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll 1
+  for (int r = 0; r < 80; r += 8) {
+    CG_SHA512_ROUND(a, b, c, d, e, f, g, h, wk[r + 0], 0)
+    CG_SHA512_ROUND(h, a, b, c, d, e, f, g, wk[r + 1], 0)
+    CG_SHA512_ROUND(g, h, a, b, c, d, e, f, wk[r + 2], 0)
+    CG_SHA512_ROUND(f, g, h, a, b, c, d, e, wk[r + 3], 0)
+    CG_SHA512_ROUND(e, f, g, h, a, b, c, d, wk[r + 4], 0)
+    CG_SHA512_ROUND(d, e, f, g, h, a, b, c, wk[r + 5], 0)
+    CG_SHA512_ROUND(c, d, e, f, g, h, a, b, wk[r + 6], 0)
+    CG_SHA512_ROUND(b, c, d, e, f, g, h, a, wk[r + 7], 0)
+  }
+  s[0] += a;
+  s[1] += b;
+  s[2] += c;
+  s[3] += d;
+  s[4] += e;
+  s[5] += f;
+  s[6] += g;
+  s[7] += h;
+}
+
 // Four aligned little-endian dwords at arena[addr, addr + 16) (addr a multiple of 4), zero past
 // `len_rounded`: one 16-byte load when the whole span is inside (gfx950 loads need only dword
 // alignment), else dword by dword.
@@ -338,6 +364,59 @@ CG_HD void sha512_prefix64_ld(uint32_t out[16], const uint32_t prefix[16], const
       be[29] = 0;
       be[30] = (uint32_t)((n * 8) >> 32);
       be[31] = (uint32_t)(n * 8);
+    }
+    uint64_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = ((uint64_t)be[2 * j] << 32) | be[2 * j + 1];
+    sha512_compress(s, w);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    out[2 * k] = CG_BSWAP32((uint32_t)(s[k] >> 32));
+    out[2 * k + 1] = CG_BSWAP32((uint32_t)s[k]);
+  }
+}
+
+// SHA-512(prefix64 || M) for M a SignableData splice (SpliceLd: base 0, zero past the message):
+// the padding byte is ORed into its word, so no word tests the length, and with wk1 != nullptr
+// (a wave-uniform TmplW512 record, the template's prefix covering M[64, 192)) block 1 runs from
+// its precomputed schedule (sha512_compress_wk).
+template <class Ld>
+CG_HD void sha512_prefix64_splice(uint32_t out[16], const uint32_t prefix[16], const Ld& ld, uint32_t msg_len,
+                                  const uint64_t* wk1) {
+  uint64_t s[8];
+  sha512_init(s);
+  const uint64_t n = 64ull + msg_len;
+  const uint32_t nblocks = (uint32_t)((n + 17u + 127u) >> 7);
+  const int mw = (int)(msg_len >> 2);
+  const uint32_t mk = 0x80u << (8u * (msg_len & 3u));
+  for (uint32_t blk = 0; blk < nblocks; ++blk) {
+    if (blk == 1 && wk1 != nullptr) {
+      sha512_compress_wk(s, wk1);
+      continue;
+    }
+    const int k0 = (int)blk * 32 - 16;  // message word of the block's first word (block 0: prefix first)
+    uint32_t W[32];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (blk == 0 && q < 4) {
+        W[4 * q] = W[4 * q + 1] = W[4 * q + 2] = W[4 * q + 3] = 0u;
+      } else {
+        ld.dwords4(&W[4 * q], (uint64_t)(k0 + 4 * q) * 4u);
+      }
+    }
+    const int km = mw - k0;  // the padding byte's word in this block (may lie outside it)
+    uint32_t be[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const uint32_t w = (blk == 0 && j < 16) ? prefix[j] : (W[j] | (j == km ? mk : 0u));
+      be[j] = CG_BSWAP32(w);
+    }
+    if (blk + 1 == nblocks) {
+      be[28] = 0;
+      be[29] = 0;
+      be[30] = (uint32_t)((n * 8u) >> 32);
+      be[31] = (uint32_t)(n * 8u);
     }
     uint64_t w[16];
 #pragma unroll

@@ -6,7 +6,8 @@
 //                   index (-> CG_NOT_RUN) when its transaction has no id or its template /
 //                   transaction index is invalid. tx_status == nullptr: the ids are the
 //                   caller's (cg_verify_tx_signatures*), every one valid
-//   k_tmpl_prep     one block per SignableData template: its image and SHA-256 midstate; the
+//   k_tmpl_prep     one block per SignableData template: its image, SHA-256 midstate and the
+//                   Ed25519 challenge's block-1 schedule (keyws.h TmplW512); the
 //                   hash kernels read SignableData(id, metadata).serialize() (Crypto.kt:499-502)
 //                   = prefix || id || suffix straight from the image and the id (SpliceLd)
 #include <hip/hip_runtime.h>
@@ -75,6 +76,7 @@ __global__ void __launch_bounds__(64) k_tmpl_prep(const cg_signable_tmpl* __rest
     h.n_ids = n_ids;
     h.img_off = tx_img_off(n_tmpls);
     h.slot = slot;
+    h.w512_off = tmpl_w512_off(n_tmpls);
     *(SpliceHdr*)msgs = h;
   }
   if (t >= n_tmpls) return;
@@ -95,12 +97,26 @@ __global__ void __launch_bounds__(64) k_tmpl_prep(const cg_signable_tmpl* __rest
     for (int q = 0; q < 4; ++q) v |= byte_at(4ull * w + q) << (8 * q);
     img[w] = v;
   }
+  const bool ed_mid = ok && tm.prefix_len >= TMPL_ED_MID_MIN_PREFIX;
+  if (threadIdx.x == 1) {  // the Ed25519 challenge's block 1 = message bytes 64..191 (keyws.h TmplW512)
+    uint64_t* wk = ((TmplW512*)(msgs + tmpl_w512_off(n_tmpls)) + t)->wk;
+    uint64_t w[16];
+    for (int j = 0; j < 16; ++j) {
+      uint64_t v = 0;
+      for (int q = 0; q < 8; ++q) v = (v << 8) | (ed_mid ? byte_at(64ull + 8u * j + q) : 0u);
+      w[j] = v;
+      wk[j] = v + cg_k512(j);
+    }
+    for (int r = 16; r < 80; r += 16)
+      for (int j = 0; j < 16; ++j) wk[r + j] = sha512_sched(w, j) + cg_k512(r + j);
+  }
   if (threadIdx.x != 0) return;
   TmplMid r;
   sha256_init(r.state);
   r.blocks = 0;
   r.prefix_len = tm.prefix_len;
-  r.pad[0] = r.pad[1] = 0;
+  r.ed_mid = ed_mid ? 1u : 0u;
+  r.pad = 0;
   if (ok) {
     for (uint32_t b = 0; b < tm.prefix_len / 64; ++b) {
       uint32_t w[16];

@@ -341,6 +341,9 @@ static_assert(sizeof(EdDigitsWide) == ITEM_SLOT, "digits must fill one item slot
 #ifndef ED_HASH_WAVES_PER_SIMD
 #define ED_HASH_WAVES_PER_SIMD 3
 #endif
+#ifndef ED_HASH_MID_SCHEDULE
+#define ED_HASH_MID_SCHEDULE 1
+#endif
 template <bool Fused>
 __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restrict__ items,
                                             const uint32_t* __restrict__ perm, const EdKeyHdr* __restrict__ hdr,
@@ -372,9 +375,21 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
       pre[w] = sw[w];
       pre[8 + w] = kh->abyte[w];
     }
-    if (Fused)
-      sha512_prefix64_ld(hw, pre, item_splice(it, msgs), 0, it.msg_len);
-    else
+    if (Fused) {
+      // A wave whose items share one template (the plan groups a scheme's items; one template per
+      // scheme in a notary batch) reads the image with scalar addresses and branches and runs block 1
+      // from the template's precomputed schedule; a mixed wave takes the per-lane form.
+      const uint32_t t0 = __builtin_amdgcn_readfirstlane(it.reserved1);
+      if (__builtin_amdgcn_ballot_w64(it.reserved1 != t0) == 0 && ED_HASH_MID_SCHEDULE) {
+        const TmplMid* m0 = (const TmplMid*)(msgs + SPLICE_HDR_BYTES) + t0;
+        const uint64_t* wk1 =
+            m0->ed_mid ? ((const TmplW512*)(msgs + ((const SpliceHdr*)msgs)->w512_off) + t0)->wk : nullptr;
+        sha512_prefix64_splice(hw, pre, tmpl_splice(t0, it.msg_off, msgs), __builtin_amdgcn_readfirstlane(it.msg_len),
+                               wk1);
+      } else {
+        sha512_prefix64_splice(hw, pre, item_splice(it, msgs), it.msg_len, (const uint64_t*)nullptr);
+      }
+    } else
       sha512_prefix64_msg(hw, pre, item_msg_arena(it, arena, msgs),
                           round4(item_msg_len(it, arena_len, msgs_len, msgs)), it.msg_off, it.msg_len);
     sc_reduce512(h, hw);

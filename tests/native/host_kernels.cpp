@@ -922,6 +922,23 @@ extern "C" int t_sha_splice_cmp(uint64_t seed, int n) {
     sha512_prefix64_ld(a, pre, ld, 0, len);
     sha512_prefix64_msg(b, pre, msg.data(), (len + 3) & ~3u, 0, len);
     if (memcmp(a, b, sizeof a)) ++bad;
+    // the Ed25519 challenge's splice form, with and without block 1's template schedule (k_tmpl_prep)
+    uint32_t c[16];
+    sha512_prefix64_splice(c, pre, ld, len, nullptr);
+    if (memcmp(c, b, sizeof c)) ++bad;
+    if (pl >= 192) {  // keyws.h TMPL_ED_MID_MIN_PREFIX: block 1 is all template prefix
+      uint64_t wk[80], w8[16];
+      for (int j = 0; j < 16; ++j) {
+        uint64_t v = 0;
+        for (int q = 0; q < 8; ++q) v = (v << 8) | img[64 + 8 * j + q];
+        w8[j] = v;
+        wk[j] = v + cg_k512(j);
+      }
+      for (int r = 16; r < 80; r += 16)
+        for (int j = 0; j < 16; ++j) wk[r + j] = sha512_sched(w8, j) + cg_k512(r + j);
+      sha512_prefix64_splice(c, pre, ld, len, wk);
+      if (memcmp(c, b, sizeof c)) ++bad;
+    }
     // SHA-256 from the midstate after the prefix's full blocks
     uint32_t st[8], w[16];
     sha256_init(st);

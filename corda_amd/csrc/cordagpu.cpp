@@ -494,6 +494,9 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.planned, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.ed_tabs, hipEventDisableTiming);
   for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&c->fork.chains[k], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork.ec_front_go, hipEventDisableTiming);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k)
+    e = hipEventCreateWithFlags(&c->fork.ec_front_done[k], hipEventDisableTiming);
   // The copy streams on hardware queues of their own (an all-CU mask makes HIP back a stream with a
   // dedicated queue): multiplexed onto the four default queues, the copy stream shared one with a
   // side stream, and the first chunk's bytes landed only after that stream's table builds (the
@@ -564,6 +567,9 @@ void cg_close(cg_ctx* c) {
   if (c->fork.ed_tabs) hipEventDestroy(c->fork.ed_tabs);
   for (int k = 0; k < 3; ++k)
     if (c->fork.chains[k]) hipEventDestroy(c->fork.chains[k]);
+  if (c->fork.ec_front_go) hipEventDestroy(c->fork.ec_front_go);
+  for (int k = 0; k < 2; ++k)
+    if (c->fork.ec_front_done[k]) hipEventDestroy(c->fork.ec_front_done[k]);
   for (hipStream_t* cs : {&c->copy, &c->copy2})
     if (*cs) {
       hipStreamSynchronize(*cs);

@@ -78,6 +78,7 @@ struct StageTimer {
 // decoupled look-back stalls when the table builds hold the SIMDs), then enqueued by launch_items.
 struct PendingTabs {
   bool on = false;
+  bool ec_front_side = false;  // this call's ECDSA fronts run on the side streams (launch_items_front)
   const cg_key* keys = nullptr;
   uint32_t n_keys = 0;
   void* keyprep = nullptr;
@@ -90,6 +91,8 @@ struct Fork {
   StageTimer* timer;  // null unless the ctx was opened with CG_FLAG_STAGE_TIMING
   hipEvent_t planned = nullptr, ed_tabs = nullptr;  // plan sorted (main); Ed25519 tables built (side[2])
   hipEvent_t chains[3] = {nullptr, nullptr, nullptr};  // each family's row-base chains done (side[k])
+  // ECDSA fronts on side[k] (CG_EC_FRONT_SIDE): main's plan done / curve k's front done
+  hipEvent_t ec_front_go = nullptr, ec_front_done[2] = {nullptr, nullptr};
   mutable PendingTabs pending;
 };
 

@@ -311,7 +311,33 @@ hipError_t launch_items_front(const cg_key* d_keys, uint32_t n_keys, const cg_it
     e = launch_items_plan(d_keys, n_keys, d_items, n_items, d_status, d_keyprep, d_item_ws, stream, fork, wide);
   if (e == hipSuccess && fork) e = launch_pending_tabs(fork, stream);  // the first front starts the table builds
   if (e != hipSuccess) return e;
-  // fronts: Ed25519 challenges (need only Abyte), ECDSA prep + s^-1 per curve (need the decoded key)
+  // fronts: Ed25519 challenges (need only Abyte), ECDSA prep + s^-1 per curve (need the decoded key).
+  // CG_EC_FRONT_SIDE=1: each curve's front on its side stream beside the challenge hashes (its
+  // s^-1 batches leave ~1 wave per SIMD: latency-bound alone), joined before that curve's ladders.
+  // The side stream waits for everything enqueued on `stream` so far: this chunk's plan, and the
+  // ladders of the chunk two back, which read the item workspace this front writes.
+  static const bool ec_side = [] {
+    const char* v = getenv("CG_EC_FRONT_SIDE");
+    return v && v[0] == '1';
+  }();
+  if (fork && ec_side && fork->ec_front_go) {
+    e = hipEventRecord(fork->ec_front_go, stream);
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+      const int curve = k == 0 ? CG_CURVE_R1 : CG_CURVE_K1;
+      e = hipStreamWaitEvent(fork->side[k], fork->ec_front_go, 0);
+      if (e != hipSuccess) break;
+      CG_TIME(fork, k == 0 ? CG_STAGE_R1_FRONT : CG_STAGE_K1_FRONT, fork->side[k],
+              ec_launch_front(curve, d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw,
+                              fork->side[k]));
+      e = hipEventRecord(fork->ec_front_done[k], fork->side[k]);
+    }
+    if (e != hipSuccess) return e;
+    fork->pending.ec_front_side = true;
+    CG_TIME(fork, CG_STAGE_ED_HASH, stream,
+            ed_launch_front(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream));
+    return hipGetLastError();
+  }
+  if (fork) fork->pending.ec_front_side = false;
   CG_TIME(fork, CG_STAGE_ED_HASH, stream,
           ed_launch_front(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream));
   if (fork) hipStreamWaitEvent(stream, fork->ec_decoded[0], 0);
@@ -363,12 +389,14 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
   if (fork) hipStreamWaitEvent(stream, fork->row0[2], 0);
   CG_TIME(fork, CG_STAGE_ED_FINISH, stream, ed_launch_finish(d_items, n_items, d_arena, arena_len, d_status, iw, stream));
   if (fork) hipStreamWaitEvent(stream, fork->ready[0], 0);
+  if (fork && fork->pending.ec_front_side) hipStreamWaitEvent(stream, fork->ec_front_done[0], 0);
   CG_TIME(fork, CG_STAGE_R1_LADDER, stream,
           ec_launch_ladder(CG_CURVE_R1, true, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (w.cap_ec)
     CG_TIME(fork, CG_STAGE_R1_LADDER_WIDE, stream,
             ec_launch_ladder_wide(CG_CURVE_R1, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) hipStreamWaitEvent(stream, fork->ready[1], 0);
+  if (fork && fork->pending.ec_front_side) hipStreamWaitEvent(stream, fork->ec_front_done[1], 0);
   CG_TIME(fork, CG_STAGE_K1_LADDER, stream,
           ec_launch_ladder(CG_CURVE_K1, true, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (w.cap_ec)

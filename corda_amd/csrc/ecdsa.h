@@ -271,6 +271,9 @@ CG_HD void jac_dbl_w(Jac& r, const Jac& p) {
 //  * H == 0 (mod p), i.e. the exceptional cases, behind a limb-0 filter that honest inputs fail
 //    with probability ~3 / 2^29, so the wave skips the exact test.
 // Same point as jac_madd (the exceptional cases included: doubling, P + (-P) -> infinity).
+#ifndef CG_EC_MADD_LAZY  // 0: round-3 v15 chains (A/B)
+#define CG_EC_MADD_LAZY 1
+#endif
 template <int C>
 CG_HD void jac_madd_w(Jac& r, bool& inf, const f29& x2, const f29& y2, bool neg, const EcConsts& K) {
   if (inf) {
@@ -301,16 +304,29 @@ CG_HD void jac_madd_w(Jac& r, bool& inf, const f29& x2, const f29& y2, bool neg,
     }
   }
   m29_sq<C, 0>(HH, H);
+#if CG_EC_MADD_LAZY
+  // 4 HH as lazy sums (< 8m, limbs < 2^31): its products are with H (< 4m) and X1 (< 2m), so
+  // a b < 32 m^2 < m R (m < 2^256), and a column stays below 9 * 2^60 + 9 * 2^58 + 2^35
+  m29_add_lazy(I, HH, HH);
+  m29_add_lazy(I, I, I);
+#else
   m29_add<C, 0>(I, HH, HH);
   m29_add_lazy(I, I, I);      // 4 HH (< 4m: multiply operand only)
+#endif
   m29_mul<C, 0>(J, H, I);
   m29_mul<C, 0>(V, r.X, I);
   m29_add_lazy(rr, rr, rr);   // 2 (S2 - Y1) (multiply operand only)
   Jac o;
   m29_sq<C, 0>(o.X, rr);
+#if CG_EC_MADD_LAZY
+  m29_add_lazy(t, J, V);  // J + 2V < 6m, limbs < 3 * 2^29
+  m29_add_lazy(t, t, V);
+  m29_sub_lazy3<C, 0>(o.X, o.X, t);
+#else
   m29_sub<C, 0>(o.X, o.X, J);
   m29_add<C, 0>(t, V, V);
   m29_sub<C, 0>(o.X, o.X, t);
+#endif
   m29_sub2<C, 0>(t, V, o.X);
   m29_mul<C, 0>(o.Y, rr, t);
   m29_add_lazy(t, r.Y, r.Y);

@@ -370,6 +370,41 @@ CG_HD void m29_sub(f29& r, const f29& a, const f29& b) {
   }
 }
 
+// r = a - K m if a >= K m (a normalized, K any small multiple: m29_limb_k)
+template <int C, int N, uint32_t K>
+CG_HD void m29_csub_k(f29& r, const f29& a) {
+  uint32_t d[9];
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int32_t s = (int32_t)a.v[i] - (int32_t)m29_limb_k(C, N, K, i) + br;
+    d[i] = (uint32_t)s & M29_MASK;
+    br = s >> 29;
+  }
+  const bool take = br == 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = take ? d[i] : a.v[i];
+}
+
+// r = a - b reduced, for a reduced and b a lazy sum of three normalized values below 6m in all
+// (limbs < 3 * 2^29): one signed chain a + 6m - b, in (0, 8m), then the conditional subtractions
+// of 4m and 2m. Three carry chains where sub(sub(a, b1), add(b2, b3)) takes six.
+template <int C, int N>
+CG_HD void m29_sub_lazy3(f29& r, const f29& a, const f29& b) {
+  f29 t;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    FE_ASSERT(b.v[i] < 3u * (1u << 29));
+    const int32_t s = (int32_t)(a.v[i] + m29_limb_k(C, N, 6, i)) - (int32_t)b.v[i] + c;
+    t.v[i] = (uint32_t)s & M29_MASK;
+    c = s >> 29;
+  }
+  FE_ASSERT(c == 0);
+  m29_csub_k<C, N, 4>(t, t);
+  m29_csub_k<C, N, 2>(r, t);
+}
+
 // "Semi-reduced": normalized limbs, value < 4m. A valid m29_mul operand when the other operand is
 // < 4m (16 m^2 < m R), not a valid m29_sub / m29_add input.
 // r = a + 2m - b (a, b reduced): ONE signed carry chain instead of m29_sub's two; r semi-reduced,

@@ -271,8 +271,8 @@ CG_HD void jac_dbl_w(Jac& r, const Jac& p) {
 //  * H == 0 (mod p), i.e. the exceptional cases, behind a limb-0 filter that honest inputs fail
 //    with probability ~3 / 2^29, so the wave skips the exact test.
 // Same point as jac_madd (the exceptional cases included: doubling, P + (-P) -> infinity).
-#ifndef CG_EC_MADD_LAZY  // 0: round-3 v15 chains (A/B)
-#define CG_EC_MADD_LAZY 1
+#ifndef CG_EC_MADD_LAZY  // 0: round-3 v15 chains, 1: lazy 4HH + three-chain X3, 2: madd-2004-hmv (A/B)
+#define CG_EC_MADD_LAZY 2
 #endif
 template <int C>
 CG_HD void jac_madd_w(Jac& r, bool& inf, const f29& x2, const f29& y2, bool neg, const EcConsts& K) {
@@ -291,6 +291,41 @@ CG_HD void jac_madd_w(Jac& r, bool& inf, const f29& x2, const f29& y2, bool neg,
   m29_mul<C, 0>(S2, S2, Z1Z1);
   if (neg) m29_neg2<C, 0>(S2, S2);
   m29_sub2<C, 0>(H, U2, r.X);
+#if CG_EC_MADD_LAZY == 2
+  // madd-2004-hmv: r = S2 - Y1 undoubled, so it may stay semi-reduced (r^2 < 16 m^2); no 4HH, 2Y1
+  // or 2H: HHH = H HH, V = X1 HH, X3 = r^2 - HHH - 2V, Y3 = r (V - X3) - Y1 HHH, Z3 = Z1 H (the
+  // same point as madd-2007-bl's, another Jacobian representative)
+  m29_sub2<C, 0>(rr, S2, r.Y);
+  if (m29_maybe_zero_semi<C, 0>(H)) {
+    if (m29_zero_semi<C, 0>(H)) {
+      if (m29_zero_semi<C, 0>(rr)) {
+        jac_dbl<C>(r, r);
+      } else {
+        jac_set_inf<C>(r, K);
+        inf = true;
+      }
+      return;
+    }
+  }
+  {
+    f29 HHH;
+    m29_sq<C, 0>(HH, H);
+    m29_mul<C, 0>(HHH, H, HH);
+    m29_mul<C, 0>(V, r.X, HH);
+    Jac o;
+    m29_sq<C, 0>(o.X, rr);
+    m29_add_lazy(t, HHH, V);  // HHH + 2V < 6m, limbs < 3 * 2^29
+    m29_add_lazy(t, t, V);
+    m29_sub_lazy3<C, 0>(o.X, o.X, t);
+    m29_sub2<C, 0>(t, V, o.X);
+    m29_mul<C, 0>(o.Y, rr, t);
+    m29_mul<C, 0>(t, r.Y, HHH);
+    m29_sub<C, 0>(o.Y, o.Y, t);
+    m29_mul<C, 0>(o.Z, r.Z, H);
+    r = o;
+    return;
+  }
+#endif
   m29_sub<C, 0>(rr, S2, r.Y);
   if (m29_maybe_zero_semi<C, 0>(H)) {
     if (m29_zero_semi<C, 0>(H)) {

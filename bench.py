@@ -80,7 +80,7 @@ KEY_FULL_MIN_USES, KEY_WIDE_MAX = 32, 8192
 KEY_WIDE_MIN_USES = {4: int(os.environ.get("CG_WIDE_MIN_USES_ED", 1536)), 3: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512)),
                      2: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512))}
 EC_INV_K = 8  # items per k_ec_inv lane (corda_amd/csrc/ecdsa_rows.h)
-EC_INV_MUL_K = {"secp256r1": 480, "secp256k1": 507}  # products of one lane: prefix, inversion, unwinding
+EC_INV_MUL_K = {"secp256r1": 365, "secp256k1": 372}  # products of one lane: prefix, inversion, unwinding
 EC_MAC_PER_MUL_P = {"secp256r1": 117, "secp256k1": 92}
 EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)

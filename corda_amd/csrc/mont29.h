@@ -472,14 +472,112 @@ CG_HD void m29_pow(f29& r, const f29& a, const uint32_t e[8], const f29& one_m) 
   r = acc;
 }
 
-// a^(m-2) = a^-1 (Fermat; a != 0)
+// a^(m-2) = a^-1 (Fermat; a != 0) by a 4-bit sliding window over the constant exponent: the odd
+// powers a, a^3, .., a^15 (8 products), then per window its squarings and one product. The windows
+// are laid out at compile time (M29InvSched: squarings and table index per window, scalar loads in
+// the loop); the table entry is picked by a uniform switch, so every product has static operands.
+// secp256r1 n - 2 has 160 one bits: 416 products by square-and-multiply, ~315 here.
+struct M29InvSched {
+  uint32_t n, tail;  // windows; squarings after the last one
+  uint8_t sq[96];    // squarings before window w's product (w >= 1)
+  uint8_t idx[96];   // window w's odd power a^(2 idx + 1)
+};
+constexpr M29InvSched m29_make_inv_sched(int C, int N) {
+  M29InvSched s{};
+  uint32_t e[8] = {};
+  for (int i = 0; i < 8; ++i) e[i] = m29_w32(C, N, i);
+  e[0] -= 2;  // the low word of every modulus here is >= 2
+  int i = 255;
+  while (i > 0 && !((e[i >> 5] >> (i & 31)) & 1u)) --i;
+  uint32_t zeros = 0;
+  while (i >= 0) {
+    if (!((e[i >> 5] >> (i & 31)) & 1u)) {
+      ++zeros;
+      --i;
+      continue;
+    }
+    int l = i - 3 > 0 ? i - 3 : 0;
+    while (!((e[l >> 5] >> (l & 31)) & 1u)) ++l;
+    uint32_t v = 0;
+    for (int j = i; j >= l; --j) v = (v << 1) | ((e[j >> 5] >> (j & 31)) & 1u);
+    s.sq[s.n] = (uint8_t)(s.n == 0 ? 0u : zeros + (uint32_t)(i - l + 1));
+    s.idx[s.n] = (uint8_t)(v >> 1);
+    ++s.n;
+    zeros = 0;
+    i = l - 1;
+  }
+  s.tail = zeros;
+  return s;
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+static __constant__ const M29InvSched CG_M29_INV_SCHED[2][2] = {
+    {m29_make_inv_sched(0, 0), m29_make_inv_sched(0, 1)}, {m29_make_inv_sched(1, 0), m29_make_inv_sched(1, 1)}};
+#else
+static const M29InvSched CG_M29_INV_SCHED[2][2] = {
+    {m29_make_inv_sched(0, 0), m29_make_inv_sched(0, 1)}, {m29_make_inv_sched(1, 0), m29_make_inv_sched(1, 1)}};
+#endif
+static_assert(m29_make_inv_sched(1, 1).n < 96 && m29_make_inv_sched(0, 1).n < 96 && m29_make_inv_sched(1, 0).n < 96 &&
+                  m29_make_inv_sched(0, 0).n < 96,
+              "inversion windows fit the schedule");
+
+#ifndef CG_M29_INV_WINDOW  // 0: square-and-multiply (A/B)
+#define CG_M29_INV_WINDOW 1
+#endif
+// Windowed for the group order only (k_ec_inv's s^-1, ~1 wave per SIMD: latency-bound, registers
+// to spare); the field inversions of the table builds keep square-and-multiply, whose register
+// footprint keeps those kernels at 3 waves per SIMD (the 8-entry table took k_ec_wide_rows from 155
+// to 216 VGPRs).
 template <int C, int N>
 CG_HD void m29_inv(f29& r, const f29& a, const f29& one_m) {
+  if constexpr (CG_M29_INV_WINDOW && N == 1) {
+  (void)one_m;
+  const M29InvSched& S = CG_M29_INV_SCHED[C][N];
+  // eight named values, not an array: an array of them stayed in scratch for secp256r1
+  f29 a2, t0 = a, t1, t2, t3, t4, t5, t6, t7;
+  m29_sq<C, N>(a2, a);
+  m29_mul<C, N>(t1, t0, a2);
+  m29_mul<C, N>(t2, t1, a2);
+  m29_mul<C, N>(t3, t2, a2);
+  m29_mul<C, N>(t4, t3, a2);
+  m29_mul<C, N>(t5, t4, a2);
+  m29_mul<C, N>(t6, t5, a2);
+  m29_mul<C, N>(t7, t6, a2);
+  f29 acc;
+  switch (S.idx[0]) {
+    case 0: acc = t0; break;
+    case 1: acc = t1; break;
+    case 2: acc = t2; break;
+    case 3: acc = t3; break;
+    case 4: acc = t4; break;
+    case 5: acc = t5; break;
+    case 6: acc = t6; break;
+    default: acc = t7; break;
+  }
+#pragma unroll 1
+  for (uint32_t w = 1; w < S.n; ++w) {
+#pragma unroll 1
+    for (uint32_t j = 0; j < S.sq[w]; ++j) m29_sq<C, N>(acc, acc);
+    switch (S.idx[w]) {  // uniform: the schedule is the same for every lane
+      case 0: m29_mul<C, N>(acc, acc, t0); break;
+      case 1: m29_mul<C, N>(acc, acc, t1); break;
+      case 2: m29_mul<C, N>(acc, acc, t2); break;
+      case 3: m29_mul<C, N>(acc, acc, t3); break;
+      case 4: m29_mul<C, N>(acc, acc, t4); break;
+      case 5: m29_mul<C, N>(acc, acc, t5); break;
+      case 6: m29_mul<C, N>(acc, acc, t6); break;
+      default: m29_mul<C, N>(acc, acc, t7); break;
+    }
+  }
+#pragma unroll 1
+  for (uint32_t j = 0; j < S.tail; ++j) m29_sq<C, N>(acc, acc);
+  r = acc;
+  } else {
   uint32_t e[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) e[i] = m29_w32(C, N, i);
   e[0] -= 2;  // the low word of every modulus here is >= 2
   m29_pow<C, N>(r, a, e, one_m);
+  }
 }
 
 // plain (reduced, Montgomery-free) value -> canonical 8 words

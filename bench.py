@@ -387,7 +387,9 @@ def roofline(stages, units, steps):
         if not n or not sum(unit_counts):
             return None
         launch_ms = ms / n
-        items = sum(unit_counts) / len(unit_counts)  # per launch (one launch per chunk per step)
+        # per launch: the step's items over its launches (the stage timer counts the launches, so a
+        # first chunk of another size, CG_TXSIG_FIRST_DIV, is averaged in correctly)
+        items = sum(unit_counts) * max(steps, 1) / n
         ach = items * per_item / (launch_ms * 1e-3)
         return {"kernel": label, "bound": "valu-int", "achieved": round(ach / 1e12, 3),
                 "peak": round(PEAK_MAC32_PER_S / 1e12, 3), "unit": "TMAC32/s", "frac": round(ach / PEAK_MAC32_PER_S, 4),

@@ -1,5 +1,6 @@
 // Internal interface between the C ABI host code (cordagpu.cpp) and the HIP kernels.
 #pragma once
+#include <stdlib.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -95,6 +96,17 @@ struct Fork {
   hipEvent_t ec_front_go = nullptr, ec_front_done[2] = {nullptr, nullptr};
   mutable PendingTabs pending;
 };
+
+// Dynamic LDS reserved by each row-base chain workgroup (CG_CHAIN_SPREAD=1: more than half a CU's
+// 160 KB, so no two single-wave chain workgroups share a CU and their latency-bound walks never
+// split one SIMD's issue; 0 otherwise). A/B knob.
+inline uint32_t chain_spread_lds() {
+  static const uint32_t b = [] {
+    const char* v = getenv("CG_CHAIN_SPREAD");
+    return v && v[0] == '1' ? 82u * 1024u : 0u;
+  }();
+  return b;
+}
 
 // Upload the constant tables (curve constants, base-point tables) for the current device.
 hipError_t upload_constants();

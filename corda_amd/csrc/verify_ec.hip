@@ -465,10 +465,13 @@ static void launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const u
   if (decoded) hipEventRecord(decoded, stream);
   hipLaunchKernelGGL(k_ec_keyprep_chain<C>, g, dim3(B), 0, stream, n_keys, w.hdr, (const uint32_t*)w.full,
                      (const uint32_t*)w.full_count, w.bases);
-  if (w.cap_ec)
-    hipLaunchKernelGGL(k_ec_wide_chain<C>, dim3((w.cap_ec + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
+  if (w.cap_ec) {
+    const uint32_t lds = chain_spread_lds();
+    if (lds) hipFuncSetAttribute((const void*)k_ec_wide_chain<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_ec_wide_chain<C>, dim3((w.cap_ec + B - 1) / B), dim3(B), lds, stream, n_keys, w.hdr,
                        (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx,
                        (const BaseSlot*)w.bases, w.wec);
+  }
 }
 
 template <int C>

@@ -831,10 +831,13 @@ void ed_launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const uint8
                      arena_len, w.hdr, w.bases);
   hipLaunchKernelGGL(k_ed_keyprep_chain, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
                      (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.bases);
-  if (w.cap_ed)
-    hipLaunchKernelGGL(k_ed_wide_chain, dim3((w.cap_ed + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
+  if (w.cap_ed) {
+    const uint32_t lds = chain_spread_lds();
+    if (lds) hipFuncSetAttribute((const void*)k_ed_wide_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_ed_wide_chain, dim3((w.cap_ed + B - 1) / B), dim3(B), lds, stream, n_keys, w.hdr,
                        (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx,
                        (const BaseSlot*)w.bases, w.wed);
+  }
 }
 
 void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream, bool full,

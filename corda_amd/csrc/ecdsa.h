@@ -207,6 +207,9 @@ CG_HD void jac_madd(Jac& r, const Jac& p, const f29& x2, const f29& y2, const Ec
 // X - delta and the Y3 / a = 0 D - X3 factors are semi-reduced (m29_sub2), used only as products'
 // operands; secp256r1's Z3 = 2 Y Z is one product instead of (Y + Z)^2 - gamma - delta. Same point
 // as jac_dbl.
+#ifndef CG_EC_DBL_LAZY  // 0: the round-3 v16 chains (A/B)
+#define CG_EC_DBL_LAZY 1
+#endif
 template <int C>
 CG_HD void jac_dbl_w(Jac& r, const Jac& p) {
   f29 t1, t2, t3, X3, Y3, Z3;
@@ -218,6 +221,25 @@ CG_HD void jac_dbl_w(Jac& r, const Jac& p) {
     m29_sub2<C, 0>(t1, p.X, delta);   // < 4m
     m29_add_lazy(t2, p.X, delta);     // < 4m
     m29_mul<C, 0>(alpha, t1, t2);
+#if CG_EC_DBL_LAZY
+    // 3 (X - delta)(X + delta) as 2t (reduced) + t lazily: < 4m, a product operand only; 8 beta and
+    // 8 gamma^2 as lazy sums of reduced 4 beta / 4 gamma^2, taken off in m29_sub_lazy3
+    m29_add<C, 0>(t1, alpha, alpha);
+    m29_add_lazy(alpha, alpha, t1);
+    m29_sq<C, 0>(X3, alpha);
+    m29_add<C, 0>(t1, beta, beta);
+    m29_add<C, 0>(t1, t1, t1);  // 4 beta
+    m29_add_lazy(t2, t1, t1);   // 8 beta < 4m, limbs < 2^30
+    m29_sub_lazy3<C, 0>(X3, X3, t2);
+    m29_add_lazy(t3, p.Z, p.Z);       // 2Z < 4m
+    m29_mul<C, 0>(Z3, p.Y, t3);       // 2 Y Z
+    m29_sub2<C, 0>(t1, t1, X3);       // 4 beta - X3, < 4m
+    m29_mul<C, 0>(Y3, alpha, t1);
+    m29_add_lazy(t3, gamma, gamma);
+    m29_sq<C, 0>(t2, t3);       // 4 gamma^2
+    m29_add_lazy(t2, t2, t2);   // 8 gamma^2 < 4m
+    m29_sub_lazy3<C, 0>(Y3, Y3, t2);
+#else
     m29_add<C, 0>(t1, alpha, alpha);
     m29_add<C, 0>(alpha, alpha, t1);  // 3 (X - delta)(X + delta)
     m29_sq<C, 0>(X3, alpha);
@@ -233,6 +255,7 @@ CG_HD void jac_dbl_w(Jac& r, const Jac& p) {
     m29_sq<C, 0>(t2, t3);      // 4 gamma^2
     m29_add<C, 0>(t2, t2, t2);  // 8 gamma^2
     m29_sub<C, 0>(Y3, Y3, t2);
+#endif
   } else {  // a = 0 : dbl-2009-l
     f29 A, B, Cc, D, E, F;
     m29_sq<C, 0>(A, p.X);
@@ -243,6 +266,21 @@ CG_HD void jac_dbl_w(Jac& r, const Jac& p) {
     m29_sub<C, 0>(t1, t1, A);
     m29_sub<C, 0>(t1, t1, Cc);
     m29_add<C, 0>(D, t1, t1);
+#if CG_EC_DBL_LAZY
+    // E = 3A as 2A (reduced) + A lazily (< 4m: F = E^2 and E (D - X3) stay under 16 m^2); 2D and 8C
+    // as lazy sums of reduced values, taken off in m29_sub_lazy3
+    m29_add<C, 0>(E, A, A);
+    m29_add_lazy(E, E, A);
+    m29_sq<C, 0>(F, E);
+    m29_add_lazy(t2, D, D);
+    m29_sub_lazy3<C, 0>(X3, F, t2);
+    m29_sub2<C, 0>(t3, D, X3);        // < 4m
+    m29_mul<C, 0>(Y3, E, t3);
+    m29_add<C, 0>(t2, Cc, Cc);
+    m29_add<C, 0>(t2, t2, t2);  // 4 C
+    m29_add_lazy(t2, t2, t2);   // 8 C < 4m
+    m29_sub_lazy3<C, 0>(Y3, Y3, t2);
+#else
     m29_add<C, 0>(E, A, A);
     m29_add<C, 0>(E, E, A);
     m29_sq<C, 0>(F, E);
@@ -254,6 +292,7 @@ CG_HD void jac_dbl_w(Jac& r, const Jac& p) {
     m29_add<C, 0>(t2, t2, t2);
     m29_add<C, 0>(t2, t2, t2);  // 8 C
     m29_sub<C, 0>(Y3, Y3, t2);
+#endif
     m29_add_lazy(t3, p.Y, p.Y);
     m29_mul<C, 0>(Z3, t3, p.Z);
   }

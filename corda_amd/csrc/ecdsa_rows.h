@@ -105,11 +105,11 @@ CG_HD void jac_add(Jac& r, const Jac& p, const Jac& q, const EcConsts& K) {
   r = o;
 }
 
-// 2^n * P
+// 2^n * P (the row-base chains: jac_dbl_w, fewer carry chains than jac_dbl, same point)
 template <int C>
 CG_HD void jac_dbl_n(Jac& r, const Jac& p, int n) {
   Jac t = p;
-  for (int i = 0; i < n; ++i) jac_dbl<C>(t, t);
+  for (int i = 0; i < n; ++i) jac_dbl_w<C>(t, t);
   r = t;
 }
 

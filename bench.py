@@ -86,7 +86,7 @@ EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
 # kernel generation whose PMC traffic profile is committed (profiles/r03/pmc_traffic.json)
-KERNEL_VERSION = "r03_v16"
+KERNEL_VERSION = "r03_v17"
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
 
 # Appendix A labels (tools/workload) -> the verdict Crypto.doVerify gives them (key decodes)

@@ -35,26 +35,44 @@ def short(name):
     return name.split("(")[0].replace("void ", "").replace("cg::", "")
 
 
+def first_n():
+    """PMC_FIRST_N=N keeps each kernel's first N dispatches: the headline leg runs first in bench.py
+    (warmup + steps calls x chunks), so the averages are the headline's launches only, not a mix with
+    the secondary legs' (device-resident, key-distribution) launches of other sizes."""
+    n = int(os.environ.get("PMC_FIRST_N", "0"))
+    return n if n > 0 else None
+
+
 def per_launch(path, counter_names):
-    acc = collections.defaultdict(lambda: collections.defaultdict(list))
-    dur = collections.defaultdict(list)
+    rows = collections.defaultdict(lambda: collections.defaultdict(dict))
     for r in csv.DictReader(open(path)):
         n = short(r["Kernel_Name"])
         if n not in KERNELS or r["Counter_Name"] not in counter_names:
             continue
-        acc[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
-        if r["Counter_Name"] == counter_names[0]:
-            dur[n].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+        d = rows[n][int(r["Dispatch_Id"])]
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        d["ms"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
     out = {}
-    for n, cs in acc.items():
-        out[n] = {k: sum(v) / len(v) for k, v in cs.items()}
-        out[n]["ms"] = sum(dur[n]) / len(dur[n])
-        out[n]["launches"] = len(dur[n])
+    for n, by_id in rows.items():
+        ds = [by_id[i] for i in sorted(by_id)][:first_n()]
+        out[n] = {k: sum(d.get(k, 0.0) for d in ds) / len(ds) for k in list(counter_names) + ["ms"]}
+        out[n]["launches"] = len(ds)
     return out
 
 
 def trace_stats(path):
     out = {}
+    tpath = path.replace("run_kernel_stats.csv", "run_kernel_trace.csv")
+    if first_n() and os.path.exists(tpath):  # the headline's launches only (see first_n)
+        by = collections.defaultdict(list)
+        for r in csv.DictReader(open(tpath)):
+            n = short(r["Kernel_Name"])
+            if n in KERNELS:
+                by[n].append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6))
+        for n, v in by.items():
+            d = [x[1] for x in sorted(v)][:first_n()]
+            out[n] = {"calls": len(d), "avg_ms": sum(d) / len(d), "min_ms": min(d), "max_ms": max(d)}
+        return out
     for r in csv.DictReader(open(path)):
         n = short(r["Name"])
         if n in KERNELS:
@@ -112,6 +130,7 @@ def main():
     out = {"items": items, "kernel_version": version,
            "source": f"{rel}/ (rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE; SQ pass; "
                      "separate processes, bench.py --steps 3 on the headline workload)",
+           "launches_kept": f"first {first_n()} dispatches per kernel (the headline leg)" if first_n() else "all",
            "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts 128-B requests at 64 B); upper "
                          "estimate for table gathers",
            "kernels": kern,

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${1:-v}; shift
 OUT=gpurun_out/prof_r02_$TAG
 mkdir -p $OUT
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-steps 0 --configs1-items 0 --ecdsa-items 0 --pipeline-txs 0 --tear-offs 0 --configs0-txs 0 $*"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --host-steps 0 --device-steps 0 --key-dists= --configs1-items 0 --ecdsa-items 0 --pipeline-txs 0 --tear-offs 0 --configs0-txs 0 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $B > $OUT/trace.log 2>&1 || { echo TRACE_FAIL; tail -20 $OUT/trace.log; exit 1; }
 echo trace_ok
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- $B > $OUT/fetch.log 2>&1 || { echo FETCH_FAIL; tail -5 $OUT/fetch.log; exit 1; }

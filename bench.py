@@ -16,8 +16,13 @@ PCIe (~97 B per signature, pageable memory), key tables, SignableData spliced on
 verify, D2H of the verdicts; plus (N > 1) the RCCL all-gather of the per-GPU verdict vectors,
 the engine's only collective. `value` = signatures of all ranks / max-over-ranks time.
 
-Launch: ``python bench.py`` (N = 1) or ``torchrun --nproc-per-node N bench.py --gpus N``; one
-process per GPU, each verifying its own shard (weak scaling). Rank 0 prints ONE JSON line.
+Launch: ``python bench.py`` (N = 1), ``python bench.py --gpus N`` (this process checks that N
+devices are visible and starts ``torch.distributed.run --nproc-per-node N`` as a child before
+anything touches the GPU, then exits with its code) or ``torchrun --nproc-per-node N bench.py
+--gpus N`` (the driver's form); one process per GPU, each verifying its own shard (weak scaling).
+Rank 0 prints ONE compact JSON line (<= 4 KB, the last line on stdout): the headline, `roofline`
+and a `cpu_baseline` summary. Everything else (secondary legs, per-stage maps, the full CPU
+baseline) goes to --secondary-out (default gpurun_out/bench_secondary.json) and to stderr.
   roofline      the dominant kernel (k_ed_ladder_wide: the shard's keys have wide tables; else
                 k_ed_ladder_pf), priced in the 32x32->64 multiply-accumulates
                 its lane code executes (host-counted) over its per-launch time from HIP events
@@ -85,6 +90,7 @@ EC_MAC_PER_MUL_P = {"secp256r1": 117, "secp256k1": 92}
 EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
 PEAK_MAC32_PER_S = 2.7944e13
+PEAK_SOURCE = "measured v_mad_u64_u32 chip rate, profiles/r01/ubench_int.json"
 # kernel generation whose PMC traffic profile is committed (profiles/r03/pmc_traffic.json)
 KERNEL_VERSION = "r03_v17"
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
@@ -94,7 +100,7 @@ ED_LABEL_EXPECT = {0: 0, 1: 1, 2: 1, 3: 1, 4: 0, 6: 1, 7: 2}       # A5 (high S)
 EC_LABEL_EXPECT = {0: 0, 1: 1, 2: 0, 3: 1, 6: 2, 7: 2}  # E5 (pad byte) is minimal when r >= 2^255
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--pool-devices", default="",
@@ -124,7 +130,124 @@ def parse():
     ap.add_argument("--pipeline-txs", type=int, default=1 << 20, help="configs[3] transaction pipeline (0: off)")
     ap.add_argument("--tear-offs", type=int, default=1 << 18, help="FilteredTransaction.verify secondary (0: off)")
     ap.add_argument("--configs0-txs", type=int, default=10_000, help="configs[0] SignedTransactions (0: off)")
-    return ap.parse_args()
+    ap.add_argument("--secondary-out", default=os.path.join(ROOT, "gpurun_out", "bench_secondary.json"),
+                    help="where the secondary legs' JSON goes ('' : stderr only)")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------------------------ launcher
+def launch_plan(gpus, env, visible):
+    """How `bench.py --gpus N` runs (no GPU call is made to decide it).
+    -> ("inline", world): this process is one rank of a world of `world` (WORLD_SIZE from torchrun,
+       or N = 1); ("spawn", N): start torch.distributed.run with N processes, one per GPU.
+    Raises SystemExit with a message when the request cannot be met: fewer than N visible devices,
+    or a torchrun world that disagrees with --gpus (never report n_gpus = 1 for --gpus 8)."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus}: need at least 1")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: launch one process per GPU")
+        return "inline", world
+    if visible < gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} requested but only {visible} device(s) are visible")
+    return ("spawn", gpus) if gpus > 1 else ("inline", 1)
+
+
+def spawn_cmd(nproc, argv, port, script=None):
+    """The driver's own N-GPU command line (one rank per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__)] + list(argv)
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_world(nproc, argv):
+    """Start the N-rank world as a CHILD process (this process has not touched the GPU: counting
+    devices does not initialise it) and return its exit code; rank 0's stdout passes through."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(spawn_cmd(nproc, argv, free_port()), env=env)
+
+
+# ------------------------------------------------------------------------------------ the line
+LINE_MAX = 4096
+LINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+ROOF_KEYS = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source", "launch_ms",
+             "items_per_launch", "work_per_item", "peak_source")
+CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "host", "jvm", "parity_on_sample")
+
+
+def _trim(d, keys):
+    return None if d is None else {k: d[k] for k in keys if k in d}
+
+
+def compact_line(head, roof, cpu, summary):
+    """The ONE stdout line the driver parses: headline keys, the dominant kernel's roofline,
+    a cpu_baseline summary and a few secondary values; <= LINE_MAX bytes (BENCH_r03's 17.8-KB
+    line was not parsed). Secondaries are dropped before the required keys are."""
+    line = dict(head)
+    line["roofline"] = _trim(roof, ROOF_KEYS)
+    if cpu is not None and "error" not in cpu:
+        c = _trim(cpu, CPU_KEYS)
+        o = cpu.get("openssl")
+        if isinstance(o, dict):
+            c["openssl"] = {"value": o.get("value"), "threads": o.get("threads"),
+                            "value_1thread": o.get("value_1thread")}
+        if isinstance(cpu.get("serial_1thread"), dict):
+            c["value_1thread"] = cpu["serial_1thread"].get("value")
+        c0 = cpu.get("configs0")
+        if isinstance(c0, dict) and "port" in c0:
+            c["configs0"] = {"port_sigs_per_s": c0["port"]["sigs_per_s"],
+                             "gpu_sigs_per_s": c0.get("gpu", {}).get("sigs_per_s"),
+                             "first_failures_equal_port": c0.get("gpu", {}).get("first_failures_equal_port")}
+        line["cpu_baseline"] = c
+    else:
+        line["cpu_baseline"] = cpu
+    line["summary"] = summary
+    s = json.dumps(line, separators=(",", ":"))
+    for drop in ("summary", ("cpu_baseline", "configs0"), ("cpu_baseline", "openssl"), ("cpu_baseline", "host"),
+                 ("config", "workload")):
+        if len(s) <= LINE_MAX:
+            break
+        if isinstance(drop, tuple):
+            if isinstance(line.get(drop[0]), dict):
+                line[drop[0]].pop(drop[1], None)
+        else:
+            line.pop(drop, None)
+        s = json.dumps(line, separators=(",", ":"))
+    assert len(s) <= LINE_MAX, len(s)
+    return s
+
+
+def write_secondary(path, obj):
+    """Secondary legs: a file (merged back by gpurun from gpurun_out/) and stderr."""
+    s = json.dumps(obj, separators=(",", ":"), default=str)
+    if path:
+        try:
+            os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+            with open(path, "w") as f:
+                f.write(s + "\n")
+        except OSError as e:
+            print(f"bench.py: could not write {path}: {e}", file=sys.stderr)
+    print("SECONDARY " + s, file=sys.stderr, flush=True)
+
+
+def guarded(out, name, fn):
+    """Run one secondary leg; a failure is recorded and never voids the headline line."""
+    try:
+        out[name] = fn()
+    except Exception as e:  # noqa: BLE001
+        out[name] = {"error": f"{type(e).__name__}: {e}"}
 
 
 def host_threads(req):
@@ -183,10 +306,14 @@ def cpu_baseline(batch, st_gpu, seconds, threads):
     c_oracle.verify_batch(sub, 0, threads)
     dt = time.perf_counter() - t
     n = int(min(batch.n, max(probe, probe * seconds / max(dt, 1e-6))))
-    sub = Batch(batch.keys, batch.items[:n], batch.arena)
-    t = time.perf_counter()
-    st = c_oracle.verify_batch(sub, 0, threads)
-    dt = time.perf_counter() - t
+    for _ in range(3):  # the probe includes every key's decode: grow the sample until it fills the target
+        sub = Batch(batch.keys, batch.items[:n], batch.arena)
+        t = time.perf_counter()
+        st = c_oracle.verify_batch(sub, 0, threads)
+        dt = time.perf_counter() - t
+        if dt >= 0.6 * seconds or n >= batch.n:
+            break
+        n = int(min(batch.n, n * seconds / max(dt, 1e-6)))
     n1 = max(64, min(n, int(n / threads / 2)))
     sub1 = Batch(batch.keys, batch.items[:n1], batch.arena)
     t = time.perf_counter()
@@ -710,14 +837,19 @@ def main_pool(a):
         sys.exit(3)
 
 
-def main():
-    a = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
     if a.pool_devices:
         return main_pool(a)
     import torch
+    # decide the world before any GPU call (device_count does not initialise the GPU on this image)
+    visible = torch.cuda.device_count() if "WORLD_SIZE" not in os.environ else a.gpus
+    how, world = launch_plan(a.gpus, os.environ, visible)
+    if how == "spawn":
+        sys.exit(spawn_world(world, argv))
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -784,11 +916,18 @@ def main():
     per_pool = np.full(pool.n, 255, np.uint8)
     per_pool[idx] = st
     ver["draws_consistent"] = bool(np.array_equal(per_pool[idx], st))
+    if world > 1:  # every rank's verdicts are checked; rank 0 reports the worst
+        bad = torch.tensor([ver["label_mismatches"] + ver["not_run"] + (0 if ver["draws_consistent"] else 1)],
+                           dtype=torch.int64, device=dev)
+        dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+        ver["world_bad"] = int(bad.item())
+        ver["gathered_not_run"] = int((holder["all"] == 255).sum().item())
 
     units = ladder_units(batch, labels, schemes, headline_chunk(a, batch.n))
     roof, ec_roof = roofline(stages, units, a.steps)
     if roof is not None:
         roof["i2p_equiv_TMAC32"] = round(roof["achieved"] * MAC32_PER_ED25519 / roof["work_per_item"], 3)
+        roof["peak_source"] = PEAK_SOURCE
         roof["traffic"] = None
         if os.path.exists(TRAFFIC_FILE):
             with open(TRAFFIC_FILE) as f:
@@ -800,7 +939,8 @@ def main():
                     roof["valu_issue"] = tr["valu_issue"]
 
     h2d_bytes = int(tb.arena.size + tb.sigs.nbytes + tb.ids.nbytes + tb.keys.nbytes)
-    extra = {"stages": stage_summary(stages, a.steps), "ecdsa_ladders": ec_roof,
+    extra = {"stages": stage_summary(stages, a.steps), "ecdsa_ladders": ec_roof, "roofline_full": roof,
+             "verdicts": ver, "gen_s": round(gen_s, 1),
              "headline_h2d": {"bytes_per_call": h2d_bytes, "bytes_per_sig": round(h2d_bytes / tb.n, 1),
                               "GBps_effective": round(h2d_bytes * a.steps / elapsed / 1e9, 1),
                               "cg_stats_ms_mean": {k: round(float(np.mean([c[k] for c in cg_ms])), 3)
@@ -808,23 +948,23 @@ def main():
                                                              "ms_total")},
                               "note": "ms_key_prep = host-side planning (the key-use sample pass), ms_h2d = until "
                                       "the first chunk's bytes are resident, ms_verify = the rest"}}
-    if rank == 0 and world == 1 and a.device_steps > 0:
-        extra["device_resident"] = bench_device(eng, dev, stream, batch, tb, st, a.device_steps)
-    if rank == 0 and world == 1 and a.host_steps > 0:
-        extra["host_message_form"] = bench_host(eng, batch, st, a.host_steps)
     extra["table_modes_items"] = table_modes(batch, schemes)
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(batch, st, a.cpu_seconds, threads)
-        if a.configs0_txs > 0:
-            cpu["configs0"] = configs0(a, eng, wl, threads)
-    torch.cuda.empty_cache()
-    if world == 1:
-        for dist in [d for d in a.key_dists.split(",") if d]:
+    if rank == 0 and world == 1:
+        if a.device_steps > 0:
+            guarded(extra, "device_resident", lambda: bench_device(eng, dev, stream, batch, tb, st, a.device_steps))
+        if a.host_steps > 0:
+            guarded(extra, "host_message_form", lambda: bench_host(eng, batch, st, a.host_steps))
+        if not a.no_cpu_baseline:
             try:
-                extra["key_dist_" + dist] = bench_key_dist(a, eng, dist, rank, threads, 2)
-            except Exception as e:  # a failed secondary must not void the headline line
-                extra["key_dist_" + dist] = {"error": f"{type(e).__name__}: {e}"}
+                cpu = cpu_baseline(batch, st, a.cpu_seconds, threads)
+                if a.configs0_txs > 0:
+                    guarded(cpu, "configs0", lambda: configs0(a, eng, wl, threads))
+            except Exception as e:  # noqa: BLE001
+                cpu = {"error": f"{type(e).__name__}: {e}"}
+        torch.cuda.empty_cache()
+        for kd in [d for d in a.key_dists.split(",") if d]:
+            guarded(extra, "key_dist_" + kd, lambda: bench_key_dist(a, eng, kd, rank, threads, 2))
             torch.cuda.empty_cache()
         for name, on, fn in (("configs1_ed25519", a.configs1_items, lambda: bench_configs1(a, eng, dev, stream, wl, threads)),
                              ("configs2_ecdsa", a.ecdsa_items, lambda: bench_ecdsa(a, eng, dev, stream, wl, threads)),
@@ -832,38 +972,46 @@ def main():
                               lambda: bench_pipeline(a, eng, dev, stream, wl, threads)),
                              ("tear_offs", a.tear_offs, lambda: bench_tear_offs(a, eng, dev, stream, wl))):
             if on > 0:
-                extra[name] = fn()
+                guarded(extra, name, fn)
                 torch.cuda.empty_cache()
 
+    failed = bool(ver["label_mismatches"] or ver["not_run"] or not ver["draws_consistent"] or ver.get("world_bad"))
     if rank == 0:
         total = a.items * world * a.steps
         n_ed, n_r1 = int((schemes == 4).sum()), int((schemes == 3).sum())
-        line = {
+        head = {
             "metric": METRIC, "value": round(total / elapsed, 1), "unit": "sigs/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic: seeded RFC 8032 Ed25519 + ECDSA (secp256r1/k1) signatures over "
-                    "SignableData(txId, SignatureMetadata(1, scheme)) with every Appendix A corruption class "
-                    "(tools/workload), no JVM capture",
-            "config": {"workload": "BASELINE configs[4] per-GPU shard, whole node: notary-style mixed batch, 70% "
-                                   "Ed25519 / 20% secp256r1 / 10% secp256k1, 12.5M signatures per GPU (100M at 8 GPUs), "
-                                   f"{a.sigs_per_tx} signatures per tx id; host arena -> host verdicts, one "
-                                   "cg_verify_tx_signatures call per step (batch Crypto.doVerify(txId, sig): key table, "
-                                   "ids, signature table and signature bytes copied from pageable host memory, "
-                                   "SignableData spliced on the device, verdicts copied back)",
-                       "items_per_gpu": a.items, "unique_pool": a.pool, "mix": {"ed25519": n_ed, "secp256r1": n_r1,
-                                                                              "secp256k1": a.items - n_ed - n_r1},
-                       "keys": len(batch.keys), "tx_ids_per_gpu": int(tb.n_ids), "h2d_bytes_per_gpu": h2d_bytes,
-                       "device_chunk_items": headline_chunk(a, batch.n),
+            "data": "synthetic: seeded Ed25519 + ECDSA (secp256r1/k1) signatures over SignableData(txId, "
+                    "SignatureMetadata(1, scheme)) with every Appendix A corruption class (tools/workload)",
+            "config": {"workload": "BASELINE configs[4] per-GPU shard, whole node: notary-style mixed batch 70% "
+                                   "Ed25519 / 20% secp256r1 / 10% secp256k1, host arena -> host verdicts, one "
+                                   "cg_verify_tx_signatures call per step (batch Crypto.doVerify(txId, sig))",
+                       "items_per_gpu": a.items, "unique_pool": a.pool,
+                       "mix": [n_ed, n_r1, a.items - n_ed - n_r1], "keys": len(batch.keys),
+                       "sigs_per_tx": a.sigs_per_tx, "h2d_bytes_per_gpu": h2d_bytes,
                        "parallelism": f"shard{world}" + ("+rccl_allgather(verdicts)" if world > 1 else "")},
-            "roofline": roof, "cpu_baseline": cpu, "secondary": extra, "verdicts": ver,
-            "gen_s": round(gen_s, 1),
         }
-        print(json.dumps(line), flush=True)
+        summary = {"verdicts_checked": ver["checked_vs_labels"], "label_mismatches": ver["label_mismatches"],
+                   "not_run": ver["not_run"], "draws_consistent": ver["draws_consistent"],
+                   "secondary_file": os.path.relpath(a.secondary_out, ROOT) if a.secondary_out else None}
+        if ec_roof:
+            summary["ecdsa_wide_frac"] = {c: (ec_roof.get(c + "_wide") or {}).get("frac") for c in ("secp256r1", "secp256k1")}
+        for k in ("device_resident", "key_dist_distinct", "key_dist_zipf", "configs1_ed25519", "configs2_ecdsa",
+                  "configs3_tx_pipeline", "tear_offs"):
+            v = extra.get(k)
+            if isinstance(v, dict):
+                if k == "device_resident":
+                    v = v.get("tx_signatures", {})
+                summary[k] = v.get("value", v.get("error", "")[:80] if "error" in v else None)
+        extra["cpu_baseline_full"] = cpu
+        write_secondary(a.secondary_out, extra)
+        print(compact_line(head, roof, cpu, summary), flush=True)
     if world > 1:
         dist.destroy_process_group()
     eng.close()
-    if ver["label_mismatches"] or ver["not_run"] or not ver["draws_consistent"]:
+    if failed:
         sys.exit(3)  # a wrong verdict voids the number
 
 

@@ -1,0 +1,91 @@
+"""bench.py's contract with the driver, on CPU: the last stdout line is ONE compact JSON object
+(<= 4 KB, required keys present) however large the secondaries grow, and `--gpus N` means N
+processes, one per GPU (VERDICT r3 missing #1 / #2)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _head():
+    return {"metric": bench.METRIC, "value": 2.6e8, "unit": "sigs/s", "n_gpus": 1, "steps": 20, "warmup": 5,
+            "ms_per_step": 48.0, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic", "config": {"workload": "w" * 400, "items_per_gpu": 12_500_000}}
+
+
+def _roof():
+    return {"kernel": "k_ed_ladder_wide", "bound": "valu-int", "achieved": 16.7, "peak": 27.9, "unit": "TMAC32/s",
+            "frac": 0.6, "launch_ms": 3.1, "launches": 100, "items_per_launch": 1720038, "work_per_item": 30700,
+            "traffic": 5.2e9, "traffic_source": "profiles/r04/x", "units_exact": False, "valu_issue": {"x": 1}}
+
+
+def _cpu(big=0):
+    return {"value": 1.7e5, "unit": "sigs/s", "cores": 16, "kind": "port", "sample": "s" * 200, "host": "h" * 100,
+            "jvm": "none", "parity_on_sample": True, "serial_1thread": {"value": 7e3},
+            "openssl": {"value": 1.8e5, "threads": 16, "value_1thread": 1.4e4, "note": "n" * 300},
+            "configs0": {"port": {"sigs_per_s": 8e4}, "gpu": {"sigs_per_s": 1.4e7, "first_failures_equal_port": True},
+                         "blob": "b" * big}}
+
+
+@pytest.mark.parametrize("big", [0, 20_000])
+def test_line_is_compact_and_complete(big):
+    summary = {"device_resident": 3e8, "pad": "p" * big}
+    s = bench.compact_line(_head(), _roof(), _cpu(big), summary)
+    assert len(s.encode()) <= bench.LINE_MAX
+    d = json.loads(s)
+    for k in bench.LINE_KEYS:
+        assert k in d, k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in d["roofline"], k
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in d["cpu_baseline"], k
+    assert "\n" not in s
+
+
+def test_line_without_cpu_or_roofline():
+    d = json.loads(bench.compact_line(_head(), None, {"error": "RuntimeError: x"}, {}))
+    assert d["roofline"] is None and d["cpu_baseline"] == {"error": "RuntimeError: x"}
+
+
+def test_launch_plan():
+    assert bench.launch_plan(1, {}, 1) == ("inline", 1)
+    assert bench.launch_plan(2, {}, 8) == ("spawn", 2)
+    assert bench.launch_plan(8, {}, 8) == ("spawn", 8)
+    assert bench.launch_plan(2, {"WORLD_SIZE": "2"}, 0) == ("inline", 2)
+    with pytest.raises(SystemExit, match="only 1 device"):
+        bench.launch_plan(8, {}, 1)
+    with pytest.raises(SystemExit, match="WORLD_SIZE=4"):
+        bench.launch_plan(8, {"WORLD_SIZE": "4"}, 8)
+    cmd = bench.spawn_cmd(2, ["--gpus", "2", "--steps", "3"], 29500)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "2", "--steps", "3"]
+
+
+def test_spawned_world_of_two_over_gloo():
+    """The exact launcher command bench.py uses for --gpus 2, pointed at a CPU rank (gloo, oracle
+    as the engine): two processes, shards all-gathered, rank 0's line last on stdout."""
+    probe = os.path.join(ROOT, "tests", "rank_probe.py")
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(bench.spawn_cmd(2, ["--gpus", "2"], bench.free_port(), script=probe), env=env,
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    last = json.loads(r.stdout.strip().splitlines()[-1])
+    assert last == {"n_gpus": 2, "items": last["items"], "equal_unsharded": True} and last["items"] > 100
+
+
+def test_gpus_request_exceeding_devices_fails_before_gpu():
+    """No GPU here: `bench.py --gpus 2` must exit non-zero with a message, not run one GPU."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode != 0
+    assert "only 0 device" in r.stderr

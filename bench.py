@@ -59,16 +59,18 @@ MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # Executed work of the GPU path, counted by the host build of the same lane code
 # (tests/native/host_kernels.cpp; pinned by tests/test_host_kernels.py::test_executed_work_*).
 # Ed25519 (field multiplies, squarings) in the radix-2^25.5 representation (fe25519.h):
-ED_VERIFY_FE = (402, 24)   # k_ed_ladder_pf: 43 + 12 mixed additions + 6 doublings
-ED_WIDE_FE = (307, 0)      # k_ed_ladder_wide: 32 + 12 mixed additions, no doublings (keys with wide tables)
+ED_VERIFY_FE = (319, 24)   # k_ed_ladder_pf: 43 mixed additions + 6 doublings in radix 2^25.5 ...
+ED_VERIFY_FE9 = 83         # ... then the 12 B additions in radix 2^29 (fe9.h products)
+ED_WIDE_FE = (307, 0)      # k_ed_ladder_wide: 32 + 12 mixed additions, no doublings (keys with wide tables), all fe9
 ED_WIDE_BUILD_FE = (63399, 18016)  # one key's wide table: 248-doubling chain, then per row two lanes each walking 64 entries (the second from 65 P), one inversion each, the walk back (k_ed_wide_rows)
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
 ED_FINISH_K = 16
 MAC_PER_MUL, MAC_PER_SQ = 100, 55
-MAC32_ED_LADDER = ED_VERIFY_FE[0] * MAC_PER_MUL + ED_VERIFY_FE[1] * MAC_PER_SQ
-MAC32_ED_WIDE = ED_WIDE_FE[0] * MAC_PER_MUL + ED_WIDE_FE[1] * MAC_PER_SQ
-MAC32_EXEC_PER_ED25519 = ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
+MAC_PER_MUL9 = 81 + 16 + 1  # fe9.h: 81 products, 8 columns x 2 fold MACs, the top carry's 1216 T_lo
+MAC32_ED_LADDER = ED_VERIFY_FE[0] * MAC_PER_MUL + ED_VERIFY_FE[1] * MAC_PER_SQ + ED_VERIFY_FE9 * MAC_PER_MUL9
+MAC32_ED_WIDE = ED_WIDE_FE[0] * MAC_PER_MUL9
+MAC32_EXEC_PER_ED25519 = ED_VERIFY_FE9 * MAC_PER_MUL9 + ((ED_VERIFY_FE[0] + ED_FINISH_FE[0]) * MAC_PER_MUL +
                           (ED_VERIFY_FE[1] + ED_FINISH_FE[1]) * MAC_PER_SQ +
                           (ED_INVERT_FE[0] * MAC_PER_MUL + ED_INVERT_FE[1] * MAC_PER_SQ) / ED_FINISH_K)
 # ECDSA: field products (mont29.h) per item: (k_ec_ladder full tables mod p, k_ec_inv mod n
@@ -88,9 +90,12 @@ EC_INV_K = 8  # items per k_ec_inv lane (corda_amd/csrc/ecdsa_rows.h)
 EC_INV_MUL_K = {"secp256r1": 365, "secp256k1": 372}  # products of one lane: prefix, inversion, unwinding
 EC_MAC_PER_MUL_P = {"secp256r1": 117, "secp256k1": 92}
 EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
-# v_mad_u64_u32 chip throughput measured on MI355X (profiles/r01/ubench_int.json)
-PEAK_MAC32_PER_S = 2.7944e13
-PEAK_SOURCE = "measured v_mad_u64_u32 chip rate, profiles/r01/ubench_int.json"
+# v_mad_u64_u32 chip throughput measured on MI355X (profiles/r04/ubench/ubench_peak_summary.json:
+# 16 independent chains per lane, 8 waves per SIMD: 15.05 lanes/clk/SIMD at the measured shader
+# clock). Round 1's 2.79e13 came from a latency-limited harness (8 chains, short launches).
+PEAK_MAC32_PER_S = 3.6412e13
+PEAK_MAC32_SPEC = 16 * 1024 * 2.4e9  # 4 cycles per wave64 v_mad_u64_u32 on a SIMD-32, 2.4 GHz
+PEAK_SOURCE = "measured v_mad_u64_u32 chip rate, profiles/r04/ubench (spec-derived 3.93e13: frac_spec)"
 # kernel generation whose PMC traffic profile is committed (profiles/r03/pmc_traffic.json)
 KERNEL_VERSION = "r03_v17"
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
@@ -182,7 +187,7 @@ def spawn_world(nproc, argv):
 LINE_MAX = 4096
 LINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
-ROOF_KEYS = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source", "launch_ms",
+ROOF_KEYS = ("kernel", "bound", "achieved", "peak", "unit", "frac", "frac_spec", "traffic", "traffic_source", "launch_ms",
              "items_per_launch", "work_per_item", "peak_source")
 CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "host", "jvm", "parity_on_sample")
 
@@ -520,6 +525,7 @@ def roofline(stages, units, steps):
         ach = items * per_item / (launch_ms * 1e-3)
         return {"kernel": label, "bound": "valu-int", "achieved": round(ach / 1e12, 3),
                 "peak": round(PEAK_MAC32_PER_S / 1e12, 3), "unit": "TMAC32/s", "frac": round(ach / PEAK_MAC32_PER_S, 4),
+                "frac_spec": round(ach / PEAK_MAC32_SPEC, 4),
                 "launch_ms": round(launch_ms, 3), "launches": int(n), "items_per_launch": int(items),
                 "work_per_item": per_item, "ms_per_step": round(ms / max(steps, 1), 3),
                 "units_exact": units["exact"]}

@@ -11,6 +11,7 @@
 // no data-dependent control flow, so the 64 lanes of a wave never diverge.
 #pragma once
 #include "ed25519.h"
+#include "fe9.h"
 
 // Product configuration (k_ed_keyprep_* / k_ed_ladder): -A rows of signed radix-2^6 digits in
 // 2 windows (22 rows x 32 multiples per key, 6 doublings per item), B in signed radix 2^10
@@ -455,37 +456,34 @@ static_assert(253 % ED_WIDE_W != 0 && 253 % ED_WIDE_BW != 0, "the top digit keep
 // Both wide tables hold half-scaled niels entries ((y+x)/2, (y-x)/2, x y d), added with
 // ge_madd_half_signed (no doubling of Z and no carry pass per addition); digit 0 adds the
 // half-scaled identity (ge_niels_identity_half).
+// Entries in the radix-2^29 form (fe9.h: the wide ladders run in it), 112 B each.
 struct EdWideTab {
-  ge_niels t[EdWideCfg::kRows][EdWideCfg::kMult];  // t[j][k-1] = k 2^{8j} (-A), half-scaled
+  ge9_niels t[EdWideCfg::kRows][EdWideCfg::kMult];  // t[j][k-1] = k 2^{8j} (-A), half-scaled
 };
 struct EdBWideTab {
-  ge_niels t[EdWideCfg::kBDigits][EdWideCfg::kBMult];  // t[u][k-1] = k 2^{ED_WIDE_BW u} B, half-scaled
+  ge9_niels t[EdWideCfg::kBDigits][EdWideCfg::kBMult];  // t[u][k-1] = k 2^{ED_WIDE_BW u} B, half-scaled
+  // the half-scaled identity, gathered for a zero digit of either table: a select of constants in
+  // the ladder let the compiler specialise the products on it (64 x 32-bit multiplies, ~+40% VALU)
+  ge9_niels ident;
 };
 
 // R' = h (-A) + S' B over the wide tables, digits already recoded (eh: radix 2^8, esb: radix
-// 2^ED_WIDE_BW). Entries by |digit|, the sign through ge_madd_half_signed (the form k_ed_ladder_wide
-// runs; `pick_*` may return any entry for digit 0, which is replaced by the half-scaled identity).
-template <class TabA, class TabB, class PickA, class PickB>
-CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const TabA& TA, const TabB& TB,
-                                 PickA pick_a, PickB pick_b) {
-  ge_p3 R;
-  ge_p3_0(R);
-  ge_p1p1 t;
+// 2^ED_WIDE_BW): 44 signed mixed additions in the radix-2^29 arithmetic (fe9.h), entries by |digit|
+// (digit 0 adds the half-scaled identity), the sign through ge9_madd_half: the form k_ed_ladder_wide
+// runs.
+CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const EdWideTab& TA,
+                                 const EdBWideTab& TB) {
+  ge9_p3 R;
+  ge9_p3_0(R);
   for (int o = 0; o < EdWideCfg::kOps; ++o) {
     const bool is_b = o >= EdWideCfg::kRows;
     const int dg = is_b ? sc_digit_at<EdWideCfg::kBBits>(esb, o - EdWideCfg::kRows) : sc_digit_b(eh, o);
     const int dp = dg < 0 ? -dg : dg;
-    ge_niels n;
-    if (is_b) {
-      pick_b(n, TB.t[o - EdWideCfg::kRows], dp);
-    } else {
-      pick_a(n, TA.t[o], dp);
-    }
-    if (dg == 0) ge_niels_identity_half(n);
-    ge_madd_half_signed(t, R, n, dg < 0);
-    if (o + 1 < EdWideCfg::kOps) ge_p1p1_to_p3(R, t);
+    const ge9_niels n = dp == 0 ? TB.ident : is_b ? TB.t[o - EdWideCfg::kRows][dp - 1] : TA.t[o][dp - 1];
+    if (o + 1 < EdWideCfg::kOps) ge9_madd_half<true>(R, R, n, dg < 0);
+    else ge9_madd_half<false>(R, R, n, dg < 0);
   }
-  ge_p1p1_to_p2(out, t);
+  ge9_to_p2(out, R);
 }
 
 // m * P for a small m >= 1 (double-and-add, MSB first)
@@ -507,7 +505,8 @@ CG_HD void ed_small_mul(ge_p3& R, const ge_p3& P, uint32_t m, const fe& d2) {
 
 // Wide B row u, multiples 8 grp + 1 .. 8 grp + 8 of 2^{ED_WIDE_BW u} B (one lane of the
 // per-context build k_ed_bwide_init; the host tests build the groups their digits touch).
-CG_HD void ed_bwide_group(ge_niels* out8, const ge_p3& B, int u, int grp, const fe& d2) {
+template <class Out>
+CG_HD void ed_bwide_group(Out* out8, const ge_p3& B, int u, int grp, const fe& d2) {
   ge_p3 P = B;
   if (u > 0) ed_dbl_n(P, P, ED_WIDE_BW * u);
   ge_p3 pts[8];
@@ -519,7 +518,9 @@ CG_HD void ed_bwide_group(ge_niels* out8, const ge_p3& B, int u, int grp, const 
     ge_add_cached(t, pts[k - 1], c);
     ge_p1p1_to_p3(pts[k], t);
   }
-  ed_niels_batch8<true>(out8, pts, d2);
+  ge_niels n8[8];
+  ed_niels_batch8<true>(n8, pts, d2);
+  for (int k = 0; k < 8; ++k) ed_niels_store(out8 + k, n8[k]);
 }
 
 // ---------------------------------------------------------------- wide-table build
@@ -552,7 +553,8 @@ CG_HD void ed_niels_from(ge_niels& n, const ge_p2& p, const fe& zi, const fe& d4
   fe_mul(n.xy2d, xy, d4);
 }
 // zinv = 1 / (2 Z_0 Z_1) (fe_invert_run's 1/2 included)
-CG_HD void ed_wide_chunk_out(ge_niels* out, const ge_p2 pts[ED_WIDE_CHUNK], const fe& zinv, const fe& d2) {
+template <class Out>
+CG_HD void ed_wide_chunk_out(Out* out, const ge_p2 pts[ED_WIDE_CHUNK], const fe& zinv, const fe& d2) {
   fe z1i, z0i, d4;
   fe_add(d4, d2, d2);
   fe_carry(d4);
@@ -561,14 +563,14 @@ CG_HD void ed_wide_chunk_out(ge_niels* out, const ge_p2 pts[ED_WIDE_CHUNK], cons
   ge_niels n0, n1;
   ed_niels_from(n0, pts[0], z0i, d4);
   ed_niels_from(n1, pts[1], z1i, d4);
-  out[0] = n0;
-  out[1] = n1;
+  ed_niels_store(out, n0);
+  ed_niels_store(out + 1, n1);
 }
 
 // Pass 1 (Out = false): zc[c] = chunk c's Z product. Pass 3 (Out = true): the group's 32 entries
 // into out[0..31] from the inverted chunk products zc[c].
-template <bool Out>
-CG_HD void ed_wide_group_pass(ge_niels* out, fe* zc, const ge_p3& P, int g, const fe& d2) {
+template <bool Out, class OutT = ge_niels>
+CG_HD void ed_wide_group_pass(OutT* out, fe* zc, const ge_p3& P, int g, const fe& d2) {
   ge_cached c;
   ge_p3_to_cached(c, P, d2);
   ge_p3 R;
@@ -631,19 +633,18 @@ CG_HD void fe_invert_run(fe* z, fe* pre) {
 // first): EdParkRow in the row's own entries + pre[] (host build), EdParkLanes lane-interleaved
 // (the device build, keyws.h EdWideSlot::park).
 #define ED_PARK_DWORDS 40  // X, Y, Z and the running product: 4 x 10 limbs
-struct EdParkRow {
-  ge_niels* out;
-  fe* pre;
+struct EdParkRow {  // host build: X, Y, Z and the running product in four arrays of fe
+  fe *x, *y, *z, *pre;
   CG_HDM void put(int k, const fe& X, const fe& Y, const fe& Z, const fe& run) const {
-    out[k].ypx = X;
-    out[k].ymx = Y;
-    out[k].xy2d = Z;
+    x[k] = X;
+    y[k] = Y;
+    z[k] = Z;
     pre[k] = run;
   }
   CG_HDM void get(int k, fe& X, fe& Y, fe& Z) const {
-    X = out[k].ypx;
-    Y = out[k].ymx;
-    Z = out[k].xy2d;
+    X = x[k];
+    Y = y[k];
+    Z = z[k];
   }
   CG_HDM void get_run(int k, fe& run) const { run = pre[k]; }
 };
@@ -675,8 +676,8 @@ struct EdParkLanes {
 };
 
 // Entries [e0, e1) (entry k = (k + 1) P); a lane not starting at 0 starts by a scalar multiplication.
-template <class Park>
-CG_HD void ed_wide_row_build(ge_niels* out, const Park& pk, const ge_p3& P, int e0, int e1, const fe& d2) {
+template <class Park, class Out>
+CG_HD void ed_wide_row_build(Out* out, const Park& pk, const ge_p3& P, int e0, int e1, const fe& d2) {
   ge_cached c;
   ge_p3_to_cached(c, P, d2);
   ge_p3 R;
@@ -734,7 +735,7 @@ CG_HD void ed_wide_row_build(ge_niels* out, const Park& pk, const ge_p3& P, int 
     }
     ge_niels n;
     ed_niels_from(n, p, zi, d4);
-    out[k] = n;
+    ed_niels_store(out + k, n);
 #if ED_ROWS_PREFETCH
     X = Xn;
     Y = Yn;
@@ -755,19 +756,20 @@ static_assert(EdWideCfg::kMult % ED_WIDE_ROW_LANES == 0, "row split");
 // end: the B digits need no doublings, so they all go after the last window (12 additions instead
 // of the 26 of the round-1 radix-2^10 table spread over the windows). `Signed`: entries by |digit|,
 // the sign through ge_madd_signed / ge_madd_half_signed (the form k_ed_ladder_pf runs).
-template <bool Signed, class PickB>
-CG_HD void ed_add_b_wide(ge_p3& R, ge_p1p1& t, ge_p2& q, const uint32_t* esb, const EdBWideTab& TB, PickB pick_b,
-                         bool last_to_p2) {
+// S' B over the constant radix-2^ED_WIDE_BW table, in the radix-2^29 arithmetic of its entries
+// (fe9.h): R (extended, radix 2^25.5) in, q (projective, radix 2^25.5) out. Entries by |digit|,
+// the sign through ge9_madd_half.
+CG_HD void ed_add_b_wide9(ge_p2& q, const ge_p3& R, const uint32_t* esb, const EdBWideTab& TB) {
+  ge9_p3 R9;
+  ge9_from_p3(R9, R);
   for (int u = 0; u < EdWideCfg::kBDigits; ++u) {
     const int dg = sc_digit_at<EdWideCfg::kBBits>(esb, u);
-    const int dp = Signed && dg < 0 ? -dg : dg;
-    ge_niels n;
-    pick_b(n, TB.t[u], dp);  // Signed: by |digit|; otherwise negated by the pick (same for half entries)
-    if (dg == 0) ge_niels_identity_half(n);
-    ge_madd_half_signed(t, R, n, Signed && dg < 0);
-    if (last_to_p2 && u + 1 == EdWideCfg::kBDigits) ge_p1p1_to_p2(q, t);
-    else ge_p1p1_to_p3(R, t);
+    const int dp = dg < 0 ? -dg : dg;
+    const ge9_niels n = dp == 0 ? TB.ident : TB.t[u][dp - 1];
+    if (u + 1 < EdWideCfg::kBDigits) ge9_madd_half<true>(R9, R9, n, dg < 0);
+    else ge9_madd_half<false>(R9, R9, n, dg < 0);
   }
+  ge9_to_p2(q, R9);
 }
 
 template <int W, int K, bool Signed = false, class RowA, class PickA, class PickB>
@@ -799,7 +801,8 @@ CG_HD void ed_double_scalar_fw(ge_p2& out, const uint32_t* eh, const uint32_t* e
       else ge_p1p1_to_p3(R, t);
     }
   }
-  ed_add_b_wide<Signed>(R, t, q, esb, TB, pick_b, true);
+  (void)pick_b;
+  ed_add_b_wide9(q, R, esb, TB);
   out = q;
 }
 
@@ -826,6 +829,7 @@ CG_HD void ed_double_scalar_row0w(ge_p2& out, const uint32_t* eh, const uint32_t
     if (td != 0) ge_p1p1_to_p2(q, t);
     else ge_p1p1_to_p3(R, t);
   }
-  ed_add_b_wide<false>(R, t, q, esb, TB, pick_b, true);
+  (void)pick_b;
+  ed_add_b_wide9(q, R, esb, TB);
   out = q;
 }

@@ -1,0 +1,349 @@
+// GF(2^255 - 19) in nine 29-bit limbs, for the wide-table Ed25519 ladders (k_ed_ladder_wide and the
+// fixed-base B part of the other ladders): one element per lane in VGPRs.
+//
+// Why a second representation (fe25519.h keeps radix 2^25.5 for everything else): the wide ladder
+// is VALU-issue-bound and on gfx950 every VALU instruction of a MAC-heavy stream costs ~4 cycles
+// whatever it is (profiles/r04/ubench: a MAC + v_add_u32 mix issues at 15-16 instruction-lanes per
+// clock per SIMD, the same as MACs alone), so the instruction COUNT sets the time. Radix 2^25.5
+// spends 100 MACs, ten x19 multiplies, five doublings and twelve three-instruction 64-bit carries
+// per product, and two instructions per limb per subtraction. Nine 29-bit limbs take 81 MACs; the
+// columns of weight >= 2^261 fold back with 2^261 = 19 * 2^6 = 1216 (mod p) split at their 32-bit
+// halves (lo * 1216 into column k - 9, hi * 1216 * 2^3 = hi * 9728 into column k - 8: two MACs per
+// column and no carries), and the nine low columns are product-scanned (a column's carry is the
+// next column's initial accumulator: two instructions per column). ~121 instructions per product
+// against ~150, and a subtraction is one instruction per limb.
+//
+// The price is headroom: a column of nine 58-bit products is 2^61.2, leaving 2.8 bits below 2^64
+// (1.8 below 2^63 signed). So limbs may be SIGNED (a difference is a plain limb-wise subtraction)
+// and there are two products, both exact for the operand classes below (FE_BOUNDS_CHECK asserts
+// every column on the host, tests/test_host_kernels.py):
+//   fe9_mul<false> (uu): non-negative limbs, unsigned MACs; operand limbs a_i b_j < 2^60.6.
+//   fe9_mul<true>  (ss): signed limbs, signed MACs; |a_i b_j| < 2^59.6. The product may be negative,
+//       so the low columns carry B = 2^40 p = 2^295 - 19 2^40 (2^63 in column 8, -19 2^40 in column
+//       0): column 8's total lies in (0, 2^64) and its carry-out is non-negative, so the output is
+//       non-negative like uu's.
+// Operand classes (limb bounds):
+//   T  (tight: any product's output)   limb_i in [0, 2^29), limb_1 in [0, 2^29 + 2^17)
+//   A2 (T + T)                          [0, 2^30 + 2^18)
+//   S  (T - T, fe9_sub)                 (-2^29 - 2^17, 2^29 + 2^17)
+//   V  (T + 128 p - T, fe9_subk)        [2^28, 2^30 + 2^29 + 2^17)
+//   uu: T x T, A2 x T, A2 x A2, A2 x V (2^60.59 per term, 9 terms 2^63.76 < 2^64)
+//   ss: S x T, S x A2, S x V           (2^59.59 per term, 9 terms 2^62.76 < 2^63)
+#pragma once
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "fe25519.h"
+#include "ge25519.h"
+
+#define FE9_M 0x1fffffffu
+
+struct fe9 {
+  uint32_t v[9];
+};
+
+#ifdef FE_OP_COUNT
+extern uint64_t g_fe9_nmul;
+#define FE9_COUNT() (++g_fe9_nmul)
+#else
+#define FE9_COUNT() ((void)0)
+#endif
+
+// A constant multiplier as an SGPR the compiler cannot fold into shifts (mont29.h m29_opaque).
+CG_HD uint32_t fe9_opaque(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+s"(v));
+#endif
+  return v;
+}
+
+CG_HD void fe9_0(fe9& h) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) h.v[i] = 0;
+}
+CG_HD void fe9_1(fe9& h) {
+  fe9_0(h);
+  h.v[0] = 1;
+}
+// 1/2 = (p + 1) / 2 = 2^254 - 9 (tight)
+CG_HD void fe9_half(fe9& h) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) h.v[i] = FE9_M;
+  h.v[0] = FE9_M - 8u;
+  h.v[8] = (1u << 22) - 1u;
+}
+
+CG_HD void fe9_add(fe9& h, const fe9& f, const fe9& g) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) h.v[i] = f.v[i] + g.v[i];
+}
+// signed difference (class S when f, g are T)
+CG_HD void fe9_sub(fe9& h, const fe9& f, const fe9& g) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) h.v[i] = f.v[i] - g.v[i];
+}
+// f + 128 p - g, non-negative limbs for tight g (class V): 128 p = 2 * (2^261 - 1216) with every
+// 29-bit limb of 64 p doubled, limbs >= 2^30 - 2432 > any tight limb
+CG_HD void fe9_subk(fe9& h, const fe9& f, const fe9& g) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const uint32_t k = i == 0 ? (1u << 30) - 2432u : (1u << 30) - 2u;
+    FE_ASSERT(g.v[i] <= k);
+    h.v[i] = (f.v[i] + k) - g.v[i];
+  }
+}
+CG_HD void fe9_cmov(fe9& h, const fe9& a, const fe9& b, bool take_b) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) h.v[i] = take_b ? b.v[i] : a.v[i];
+}
+
+#ifdef FE_BOUNDS_CHECK
+typedef __int128 fe9_acc;
+#define FE9_IN_RANGE(x, lo, hi) FE_ASSERT((x) >= (fe9_acc)(lo) && (x) < (fe9_acc)(hi))
+#endif
+
+// out = a b mod p, tight. Signed: limbs of a and b are int32 (class S operands), else uint32.
+template <bool Signed>
+CG_HD void fe9_mul(fe9& out, const fe9& a, const fe9& b) {
+  FE9_COUNT();
+  const uint32_t k1216 = fe9_opaque(1216u), k9728 = fe9_opaque(9728u);
+  (void)k9728;
+#ifdef FE_BOUNDS_CHECK
+  // exact model with 128-bit integers: every column of the 64-bit device arithmetic must be exact
+  auto prod = [&](int i, int j) -> fe9_acc {
+    return Signed ? (fe9_acc)(int32_t)a.v[i] * (int32_t)b.v[j] : (fe9_acc)a.v[i] * b.v[j];
+  };
+  const fe9_acc lim = Signed ? ((fe9_acc)1 << 63) : ((fe9_acc)1 << 64);
+  fe9_acc hc[8];
+  for (int k = 9; k < 17; ++k) {
+    fe9_acc s = 0;
+    for (int i = k - 8; i < 9; ++i) {
+      FE9_IN_RANGE(prod(i, k - i), Signed ? -((fe9_acc)1 << 60) : 0, Signed ? ((fe9_acc)1 << 60) : ((fe9_acc)1 << 61));
+      s += prod(i, k - i);
+    }
+    FE9_IN_RANGE(s, Signed ? -lim : 0, lim);
+    hc[k - 9] = s;
+  }
+  uint32_t d[9];
+  fe9_acc acc = Signed ? -(fe9_acc)19 * ((fe9_acc)1 << 40) : 0;
+  for (int m = 0; m < 9; ++m) {
+    for (int i = 0; i <= m; ++i) acc += prod(i, m - i);
+    if (m <= 7) acc += (fe9_acc)(uint32_t)(uint64_t)hc[m] * 1216;  // lo half (two's complement)
+    if (m >= 1) {
+      const fe9_acc h = Signed ? (fe9_acc)(int32_t)(uint32_t)((uint64_t)hc[m - 1] >> 32)
+                               : (fe9_acc)(uint32_t)((uint64_t)hc[m - 1] >> 32);
+      acc += h * 9728;
+    }
+    if (m == 8 && Signed) acc += (fe9_acc)1 << 63;
+    if (m < 8) FE9_IN_RANGE(acc, Signed ? -lim : 0, lim);
+    else FE9_IN_RANGE(acc, 0, (fe9_acc)1 << 64);  // column 8 (ss: biased) is non-negative
+    d[m] = (uint32_t)(acc & FE9_M);
+    acc >>= 29;  // floor division, exact in 128 bits
+  }
+  const uint64_t T = (uint64_t)acc;
+  FE_ASSERT(acc >= 0 && T < (1ull << 35));
+#else
+  typedef typename std::conditional<Signed, int64_t, uint64_t>::type acc_t;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // opaque 32-bit operands: in the ladder loop the compiler otherwise widened loop-carried
+  // differences to 64 bits and emitted 64 x 64-bit multiplies (3 MACs + moves each)
+  fe9 a_, b_;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    a_.v[i] = a.v[i];
+    b_.v[i] = b.v[i];
+    asm volatile("" : "+v"(a_.v[i]), "+v"(b_.v[i]));
+  }
+#define a a_
+#define b b_
+#endif
+  acc_t hc[8];
+#pragma unroll
+  for (int k = 9; k < 17; ++k) {
+    acc_t s = 0;
+#pragma unroll
+    for (int i = k - 8; i < 9; ++i) {
+      if (Signed) s += (acc_t)(int64_t)(int32_t)a.v[i] * (int64_t)(int32_t)b.v[k - i];
+      else s += (acc_t)((uint64_t)a.v[i] * b.v[k - i]);
+    }
+    hc[k - 9] = s;
+  }
+  uint32_t d[9];
+  acc_t acc = Signed ? (acc_t)(-(int64_t)19 * ((int64_t)1 << 40)) : 0;
+#pragma unroll
+  for (int m = 0; m < 9; ++m) {
+#pragma unroll
+    for (int i = 0; i <= m; ++i) {
+      if (Signed) acc += (acc_t)(int64_t)(int32_t)a.v[i] * (int64_t)(int32_t)b.v[m - i];
+      else acc += (acc_t)((uint64_t)a.v[i] * b.v[m - i]);
+    }
+    if (m <= 7) acc += (acc_t)((uint64_t)(uint32_t)hc[m] * k1216);
+    if (m >= 1) {
+      if (Signed) acc += (acc_t)((int64_t)(int32_t)(uint32_t)((uint64_t)hc[m - 1] >> 32) * (int64_t)(int32_t)k9728);
+      else acc += (acc_t)((uint64_t)(uint32_t)((uint64_t)hc[m - 1] >> 32) * k9728);
+    }
+    d[m] = (uint32_t)acc & FE9_M;
+    if (m < 8) {
+      acc = Signed ? (acc_t)((int64_t)acc >> 29) : (acc_t)((uint64_t)acc >> 29);
+    } else {
+      // column 8: ss adds 2^63 (bit 63 flipped), after which the total is read as unsigned
+      uint64_t c8 = (uint64_t)acc;
+      if (Signed) c8 ^= 1ull << 63;
+      d[8] = (uint32_t)c8 & FE9_M;
+      acc = (acc_t)(c8 >> 29);
+    }
+  }
+  const uint64_t T = (uint64_t)acc;
+#if defined(__HIP_DEVICE_COMPILE__)
+#undef a
+#undef b
+#endif
+#endif
+  // T 2^261 = 1216 T: T_lo 1216 into limb 0, T_hi 2^32 1216 = T_hi 9728 2^29 into limb 1
+  const uint64_t x0 = (uint64_t)d[0] + (uint64_t)(uint32_t)T * k1216;
+  out.v[0] = (uint32_t)x0 & FE9_M;
+  out.v[1] = d[1] + (uint32_t)(T >> 32) * 9728u + (uint32_t)(x0 >> 29);
+  FE_ASSERT(out.v[1] < (1u << 29) + (1u << 17));
+#pragma unroll
+  for (int i = 2; i < 9; ++i) out.v[i] = d[i];
+}
+
+// Little-endian 32 bytes (value < 2^256) -> tight limbs
+CG_HD void fe9_from_words(fe9& h, const uint32_t w[8]) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int bit = 29 * i, wi = bit >> 5, sh = bit & 31;
+    uint64_t x = (uint64_t)w[wi] >> sh;
+    if (wi + 1 < 8) x |= (uint64_t)w[wi + 1] << (32 - sh);
+    h.v[i] = (uint32_t)x & FE9_M;
+  }
+}
+
+CG_HD void fe9_from_fe(fe9& h, const fe& f) {
+  uint32_t w[8];
+  fe_tobytes_words(w, f);
+  fe9_from_words(h, w);
+}
+
+// Non-negative limbs (any class but S) -> 8 words of a value < 2^255 congruent mod p (not always
+// canonical: fe_frombytes_words takes it as is)
+CG_HD void fe9_to_words255(uint32_t w[8], const fe9& f) {
+  uint32_t n[9];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    c += f.v[i];
+    n[i] = (uint32_t)c & FE9_M;
+    c >>= 29;
+  }
+  // bits >= 255: n_8 >> 23 and c (weight 2^261 = 2^255 2^6); 2^255 = 19
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const uint64_t t = (uint64_t)(n[8] >> 23) + (c << 6);
+    n[8] &= (1u << 23) - 1u;
+    c = 0;
+    uint64_t x = (uint64_t)n[0] + 19u * t;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      if (i > 0) x = (uint64_t)n[i] + (x >> 29);
+      n[i] = (uint32_t)x & FE9_M;
+    }
+    c = x >> 29;  // 0: n_8 < 2^23 + small
+  }
+  FE_ASSERT(n[8] < (1u << 23));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int bit = 32 * k, li = bit / 29, sh = bit % 29;
+    const uint64_t x = ((uint64_t)n[li] >> sh) | ((uint64_t)n[li + 1] << (29 - sh)) |
+                       (li + 2 < 9 && sh > 26 ? (uint64_t)n[li + 2] << (58 - sh) : 0ull);
+    w[k] = (uint32_t)x;
+  }
+}
+
+CG_HD void fe_from_fe9(fe& h, const fe9& f) {
+  uint32_t w[8];
+  fe9_to_words255(w, f);
+  fe_frombytes_words(h, w);
+}
+
+// ---------------------------------------------------------------- points
+struct ge9_p3 {
+  fe9 X, Y, Z, T;
+};
+// A half-scaled wide-table entry ((y+x)/2, (y-x)/2, x y d), tight; padded to 112 B (7 x 16-B LDS
+// DMA chunks, 16-B aligned rows).
+struct ge9_niels {
+  fe9 ypx, ymx, xy2d;
+  uint32_t pad;
+};
+static_assert(sizeof(ge9_niels) == 112, "ge9_niels layout");
+
+CG_HD void ge9_niels_from(ge9_niels& o, const ge_niels& n) {
+  fe9_from_fe(o.ypx, n.ypx);
+  fe9_from_fe(o.ymx, n.ymx);
+  fe9_from_fe(o.xy2d, n.xy2d);
+  o.pad = 0;
+}
+// store overloads for the table builders (the host tests also build fe tables)
+CG_HD void ed_niels_store(ge_niels* dst, const ge_niels& n) { *dst = n; }
+CG_HD void ed_niels_store(ge9_niels* dst, const ge_niels& n) { ge9_niels_from(*dst, n); }
+
+CG_HD void ge9_niels_identity_half(ge9_niels& n) {
+  fe9_half(n.ypx);
+  fe9_half(n.ymx);
+  fe9_0(n.xy2d);
+}
+
+CG_HD void ge9_p3_0(ge9_p3& h) {
+  fe9_0(h.X);
+  fe9_1(h.Y);
+  fe9_1(h.Z);
+  fe9_0(h.T);
+}
+
+CG_HD void ge9_from_p3(ge9_p3& r, const ge_p3& p) {
+  fe9_from_fe(r.X, p.X);
+  fe9_from_fe(r.Y, p.Y);
+  fe9_from_fe(r.Z, p.Z);
+  fe9_from_fe(r.T, p.T);
+}
+
+// r = p + (-1)^neg q for a half-scaled entry q (HWCD mixed addition; the sums come out halved, so
+// D = Z). The sign goes through the entry: -q swaps (y+x)/2 and (y-x)/2 and negates xyd, i.e.
+// C -> -C, which swaps F = Z - C and G = Z + C. Every product's operand classes (header):
+//   B' = (Y+X) sp   uu A2 x T      A' = (Y-X) sm   ss S x T      C = T xyd   uu T x T
+//   E = B' - A' (S), H = B' + A' (A2), u = Z + C (A2), v = Z + 128p - C (V)
+//   X3 = E F  ss S x {A2, V}   Y3 = G H  uu {V, A2} x A2   Z3 = u v (= F G)  uu   T3 = E H  ss S x A2
+// WithT = false leaves T unset (the last addition of a ladder: projective output).
+template <bool WithT>
+CG_HD void ge9_madd_half(ge9_p3& r, const ge9_p3& p, const ge9_niels& q, bool neg) {
+  fe9 sp, sm;
+  fe9_cmov(sp, q.ypx, q.ymx, neg);
+  fe9_cmov(sm, q.ymx, q.ypx, neg);
+  fe9 a, b;
+  fe9_add(a, p.Y, p.X);
+  fe9_sub(b, p.Y, p.X);
+  fe9 Bp, Ap, C;
+  fe9_mul<false>(Bp, a, sp);
+  fe9_mul<true>(Ap, b, sm);
+  fe9_mul<false>(C, p.T, q.xy2d);
+  fe9 E, H, u, v;
+  fe9_sub(E, Bp, Ap);
+  fe9_add(H, Bp, Ap);
+  fe9_add(u, p.Z, C);
+  fe9_subk(v, p.Z, C);
+  fe9 F, G;
+  fe9_cmov(F, v, u, neg);
+  fe9_cmov(G, u, v, neg);
+  fe9_mul<true>(r.X, E, F);
+  fe9_mul<false>(r.Y, G, H);
+  fe9_mul<false>(r.Z, u, v);
+  if (WithT) fe9_mul<true>(r.T, E, H);
+}
+
+CG_HD void ge9_to_p2(ge_p2& o, const ge9_p3& r) {
+  fe_from_fe9(o.X, r.X);
+  fe_from_fe9(o.Y, r.Y);
+  fe_from_fe9(o.Z, r.Z);
+}

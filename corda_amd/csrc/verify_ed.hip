@@ -188,7 +188,7 @@ __global__ void __launch_bounds__(64) k_ed_wide_fwd(uint32_t n_keys, const EdKey
   if (hdr[i].status != 0) return;
   EdWideSlot& ws = wed[wide_idx[i]];
   constexpr int CPG = ED_WIDE_GROUP / ED_WIDE_CHUNK;
-  ed_wide_group_pass<false>(nullptr, &ws.zpre[L.j][CPG * L.g], ws.bases[L.j], (int)L.g, c_ed.d2);
+  ed_wide_group_pass<false>((ge_niels*)nullptr, &ws.zpre[L.j][CPG * L.g], ws.bases[L.j], (int)L.g, c_ed.d2);
 }
 
 __global__ void __launch_bounds__(64) k_ed_wide_inv(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
@@ -291,6 +291,7 @@ __global__ void __launch_bounds__(64) k_ed_bwide_init(EdBWideTab* __restrict__ o
   constexpr uint32_t G = EdWideCfg::kBMult / 8;
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t u = (uint32_t)(g / G), grp = (uint32_t)(g % G);
+  if (g == 0) ge9_niels_identity_half(out->ident);
   if (u >= (uint32_t)EdWideCfg::kBDigits) return;
   ed_bwide_group(&out->t[u][8 * grp], bases[u], 0, (int)grp, c_ed.d2);
 }
@@ -521,29 +522,54 @@ __device__ __forceinline__ void ed_lds_niels(ge_niels& n, const uint8_t* wave_ld
   d[29] = *(const uint32_t*)(wave_lds + 64 * 116 + 4 * lane);
 }
 
-__device__ __forceinline__ const ge_niels* ed_op_src(const EdTab& TA, const EdBWideTab& TB, bool is_b, int row, int d) {
+// the radix-2^29 wide-table entries (fe9.h, 112 B): 7 x 16-B chunks, the same lane-linear image
+__device__ __forceinline__ void ed_glds_niels9(const ge9_niels* src, uint32_t wave_lds_off) {
+  const uint8_t* s = (const uint8_t*)src;
+#pragma unroll
+  for (int c = 0; c < 7; ++c)
+    __builtin_amdgcn_global_load_lds((cg_gbl_ptr)(s + 16 * c), ed_lds_at(wave_lds_off, 64 * 16 * c), 16, 0, 0);
+}
+__device__ __forceinline__ void ed_lds_niels9(ge9_niels& n, const uint8_t* wave_lds, uint32_t lane) {
+  uint32_t* d = (uint32_t*)&n;
+#pragma unroll
+  for (int c = 0; c < 7; ++c) {
+    const uint4 v = *(const uint4*)(wave_lds + 64 * 16 * c + 16 * lane);
+    d[4 * c] = v.x;
+    d[4 * c + 1] = v.y;
+    d[4 * c + 2] = v.z;
+    if (c < 6) d[4 * c + 3] = v.w;  // the pad dword stays unread
+  }
+}
+static_assert(64 * sizeof(ge9_niels) <= EdOps::kWaveBytes, "the LDS image holds either entry form");
+
+__device__ __forceinline__ const ge_niels* ed_op_src(const EdTab& TA, int row, int d) {
   const int a = d < 0 ? -d : d;
-  const int idx = a > 0 ? a - 1 : 0;
-  return is_b ? &TB.t[row][idx] : &TA.t[row][idx];
+  return &TA.t[row][a > 0 ? a - 1 : 0];
+}
+__device__ __forceinline__ const ge9_niels* ed_b_src(const EdBWideTab& TB, int row, int d) {
+  const int a = d < 0 ? -d : d;
+  return a > 0 ? &TB.t[row][a - 1] : &TB.ident;  // a zero digit adds the identity entry
 }
 
+// The 55 A additions in radix 2^25.5 (full-table entries), then the 12 B additions in radix 2^29
+// (fe9.h, the wide B table's entry form), one entry gathered into LDS one op ahead throughout.
 __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* __restrict__ dw, const EdTab& TA,
                                                     const EdBWideTab& TB, uint8_t* wave_lds, uint32_t lane) {
-  constexpr int N = EdOps::kOps;
+  constexpr int N = EdOps::kOps, NA = EdOps::kNa1 + EdOps::kNa0;
   const uint32_t wl = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(cg_lds_ptr)wave_lds);
   int widx, sh, row;
   bool is_b;
   // prologue: op 0's digit and entry, op 1's digit word
   ed_op_info(0, widx, sh, is_b, row);
   int d_cur = ed_op_digit(dw[widx], sh, is_b);
-  ed_glds_niels(ed_op_src(TA, TB, is_b, row, d_cur), wl);
+  ed_glds_niels(ed_op_src(TA, row, d_cur), wl);
   ed_op_info(1, widx, sh, is_b, row);
   uint32_t w_next = dw[widx];
   ge_p3 R;
   ge_p3_0(R);
   ge_p1p1 t;
   ge_p2 q;
-  for (int o = 0; o < N; ++o) {
+  for (int o = 0; o < NA; ++o) {
     if (o == EdOps::kOps1) {  // window 1 -> 0: W doublings while op o's entry is in flight
       for (int d = 0; d < ED_W - 1; ++d) {
         ge_p2_dbl(t, q);
@@ -556,30 +582,40 @@ __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* 
     ge_niels n;
     ed_lds_niels(n, wave_lds, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
-    const bool half = o >= EdOps::kNa1 + EdOps::kNa0;  // B ops: half-scaled wide-table entries
-    if (d_cur == 0) {
-      if (half) ge_niels_identity_half(n);
-      else ge_niels_identity(n);
-    }
+    if (d_cur == 0) ge_niels_identity(n);
     const bool neg = d_cur < 0;  // the sign goes through the addition, not the entry
+    ed_op_info(o + 1, widx, sh, is_b, row);
+    d_cur = ed_op_digit(w_next, sh, is_b);
+    if (is_b) ed_glds_niels9(ed_b_src(TB, row, d_cur), wl);
+    else ed_glds_niels(ed_op_src(TA, row, d_cur), wl);
+    ed_op_info(o + 2, widx, sh, is_b, row);
+    w_next = dw[widx];
+    ge_madd_signed(t, R, n, neg);
+    if (o + 1 == EdOps::kOps1) ge_p1p1_to_p2(q, t);
+    else ge_p1p1_to_p3(R, t);
+  }
+  ge9_p3 R9;
+  ge9_from_p3(R9, R);
+  for (int o = NA; o < N; ++o) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ge9_niels n;
+    ed_lds_niels9(n, wave_lds, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bool neg = d_cur < 0;
     if (o + 1 < N) {
       ed_op_info(o + 1, widx, sh, is_b, row);
       d_cur = ed_op_digit(w_next, sh, is_b);
-      ed_glds_niels(ed_op_src(TA, TB, is_b, row, d_cur), wl);
+      ed_glds_niels9(ed_b_src(TB, row, d_cur), wl);
       if (o + 2 < N) {
         ed_op_info(o + 2, widx, sh, is_b, row);
         w_next = dw[widx];
       }
-    }
-    if (half) ge_madd_half_signed(t, R, n, neg);
-    else ge_madd_signed(t, R, n, neg);
-    if (o + 1 == N || o + 1 == EdOps::kOps1) {
-      ge_p1p1_to_p2(q, t);
+      ge9_madd_half<true>(R9, R9, n, neg);
     } else {
-      ge_p1p1_to_p3(R, t);
+      ge9_madd_half<false>(R9, R9, n, neg);
     }
   }
-  out = q;
+  ge9_to_p2(out, R9);
 }
 
 // A/B on one box (gpurun_out/ab_sw1, profiles/r01/ed25519_v9): the pipelined ladder at 2
@@ -640,13 +676,14 @@ __device__ __forceinline__ int ed_wide_digit(uint32_t w, int sh, bool is_b) {
   return EdWideCfg::kBBits == 16 ? (int)(int16_t)(uint16_t)(w >> sh) : (int)w;
 }
 
-__device__ __forceinline__ const ge_niels* ed_wide_src(const EdWideTab& TA, const EdBWideTab& TB, bool is_b, int row,
-                                                       int d) {
+__device__ __forceinline__ const ge9_niels* ed_wide_src(const EdWideTab& TA, const EdBWideTab& TB, bool is_b, int row,
+                                                        int d) {
   const int a = d < 0 ? -d : d;
-  const int idx = a > 0 ? a - 1 : 0;
-  return is_b ? &TB.t[row][idx] : &TA.t[row][idx];
+  if (a == 0) return &TB.ident;  // a zero digit adds the identity entry (no select in the ladder)
+  return is_b ? &TB.t[row][a - 1] : &TA.t[row][a - 1];
 }
 
+// 44 signed mixed additions in the radix-2^29 arithmetic (fe9.h: ed_double_scalar_wide's form)
 __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint32_t* __restrict__ dw,
                                                          const EdWideTab& TA, const EdBWideTab& TB, uint8_t* wave_lds,
                                                          uint32_t lane) {
@@ -656,32 +693,33 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
   bool is_b;
   ed_wide_op(0, widx, sh, is_b, row);
   int d_cur = ed_wide_digit(dw[widx], sh, is_b);
-  ed_glds_niels(ed_wide_src(TA, TB, is_b, row, d_cur), wl);
+  ed_glds_niels9(ed_wide_src(TA, TB, is_b, row, d_cur), wl);
   ed_wide_op(1, widx, sh, is_b, row);
   uint32_t w_next = dw[widx];
-  ge_p3 R;
-  ge_p3_0(R);
-  ge_p1p1 t;
-  for (int o = 0; o < N; ++o) {
+  ge9_p3 R;
+  ge9_p3_0(R);
+  for (int o = 0; o + 1 < N; ++o) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // op o's entry and op o+1's digit word
-    ge_niels n;
-    ed_lds_niels(n, wave_lds, lane);
+    ge9_niels n;
+    ed_lds_niels9(n, wave_lds, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
-    if (d_cur == 0) ge_niels_identity_half(n);
     const bool neg = d_cur < 0;
-    if (o + 1 < N) {
-      ed_wide_op(o + 1, widx, sh, is_b, row);
-      d_cur = ed_wide_digit(w_next, sh, is_b);
-      ed_glds_niels(ed_wide_src(TA, TB, is_b, row, d_cur), wl);
-      if (o + 2 < N) {
-        ed_wide_op(o + 2, widx, sh, is_b, row);
-        w_next = dw[widx];
-      }
+    ed_wide_op(o + 1, widx, sh, is_b, row);
+    d_cur = ed_wide_digit(w_next, sh, is_b);
+    ed_glds_niels9(ed_wide_src(TA, TB, is_b, row, d_cur), wl);
+    if (o + 2 < N) {
+      ed_wide_op(o + 2, widx, sh, is_b, row);
+      w_next = dw[widx];
     }
-    ge_madd_half_signed(t, R, n, neg);
-    if (o + 1 < N) ge_p1p1_to_p3(R, t);
+    ge9_madd_half<true>(R, R, n, neg);
   }
-  ge_p1p1_to_p2(out, t);
+  {  // the last addition: projective output
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ge9_niels n;
+    ed_lds_niels9(n, wave_lds, lane);
+    ge9_madd_half<false>(R, R, n, d_cur < 0);
+  }
+  ge9_to_p2(out, R);
 }
 
 // A/B (profiles/r02/w4_rejected): forcing 4 waves/SIMD (128 VGPRs, 52 B/lane of scratch) cost 4% of
@@ -898,7 +936,7 @@ void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8
 void ed_launch_ladder_wide(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
                            const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
-  const unsigned grid = walk_grid(n_items, B, WALK_CAP(ED_LADDER_PF_WAVES));
+  const unsigned grid = walk_grid(n_items, B, WALK_CAP(4));  // fe9 ladder: 110 VGPRs, 4 waves/SIMD
   hipLaunchKernelGGL(k_ed_ladder_wide, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
                      (const uint32_t*)w.wide_idx, (const EdWideSlot*)w.wed, bwide(d_btab), d_status, iw.slots, iw.ed);
 }

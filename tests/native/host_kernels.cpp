@@ -6,8 +6,10 @@
 #include <string.h>
 
 #include "../../corda_amd/csrc/ed25519.h"
+#include "../../corda_amd/csrc/fe9.h"
 #ifdef FE_OP_COUNT
 uint64_t g_fe_nmul = 0, g_fe_nsq = 0;
+uint64_t g_fe9_nmul = 0;
 uint64_t g_m29_nmul[2][2] = {{0, 0}, {0, 0}};
 #endif
 
@@ -33,6 +35,27 @@ void t_fe_sq(const uint32_t* f, uint32_t* out) {
   memcpy(a.v, f, 40);
   fe_sq(c, a);
   memcpy(out, c.v, 40);
+}
+// radix-2^29 products (fe9.h): sgn selects fe9_mul<true> (signed limbs)
+void t_fe9_mul(int sgn, const uint32_t* f, const uint32_t* g, uint32_t* out) {
+  fe9 a, b, c;
+  memcpy(a.v, f, 36);
+  memcpy(b.v, g, 36);
+  if (sgn) fe9_mul<true>(c, a, b);
+  else fe9_mul<false>(c, a, b);
+  memcpy(out, c.v, 36);
+}
+void t_fe9_to_words(const uint32_t* f, uint32_t* out) {
+  fe9 a;
+  memcpy(a.v, f, 36);
+  fe9_to_words255(out, a);
+}
+void t_fe9_from_fe(const uint32_t* f, uint32_t* out) {
+  fe a;
+  fe9 b;
+  memcpy(a.v, f, 40);
+  fe9_from_fe(b, a);
+  memcpy(out, b.v, 36);
 }
 void t_fe_tobytes(const uint32_t* f, uint32_t* out) {
   fe a;
@@ -509,13 +532,14 @@ static int ed_verify_wb(const uint32_t* aw, const uint32_t* sw, const uint8_t* m
   tbw_touch(es);
   ge_p2 R;
 #ifdef FE_OP_COUNT
-  g_fe_nmul = g_fe_nsq = 0;
+  g_fe_nmul = g_fe_nsq = g_fe9_nmul = 0;
 #endif
   ed_double_scalar_fw<ED_W, ED_K, Signed>(R, eh, es, TA, *g_TBW, host_pick, host_pick);
 #ifdef FE_OP_COUNT
-  if (counts) {
+  if (counts) {  // [0..1] radix-2^25.5 products and squarings (A part), [2] radix-2^29 products (B part)
     counts[0] = g_fe_nmul;
     counts[1] = g_fe_nsq;
+    counts[2] = g_fe9_nmul;
   }
 #endif
   fe zi;
@@ -543,6 +567,7 @@ static ge_p3 g_TBW_base[EdWideCfg::kBDigits];  // 2^{16u} B
 static void tbw_init() {
   if (g_TBW) return;
   g_TBW = new EdBWideTab;
+  ge9_niels_identity_half(g_TBW->ident);
   g_TBW_built.assign(EdWideCfg::kBDigits * (EdWideCfg::kBMult / 8), false);
   ge_p3 B;
   fe x, y, two_inv, t;
@@ -593,9 +618,11 @@ extern "C" int t_ed_wide_row_cmp(uint32_t m) {
   }
   ed_small_mul(P, B, m, g_C.d2);
   static ge_niels a[EdWideCfg::kMult], b[EdWideCfg::kMult];
-  static fe pre[EdWideCfg::kMult], zc[EdWideCfg::kMult];
-  for (int g = 0; g < 4; ++g)  // any split; parked in the entries (the host policy) ...
-    ed_wide_row_build(a, EdParkRow{a + 32 * g, pre + 32 * g}, P, 32 * g, 32 * g + 32, g_C.d2);
+  static fe pre[EdWideCfg::kMult], zc[EdWideCfg::kMult], px[EdWideCfg::kMult], py[EdWideCfg::kMult],
+      pz[EdWideCfg::kMult];
+  for (int g = 0; g < 4; ++g)  // any split; parked in plain arrays (the host policy) ...
+    ed_wide_row_build(a, EdParkRow{px + 32 * g, py + 32 * g, pz + 32 * g, pre + 32 * g}, P, 32 * g, 32 * g + 32,
+                      g_C.d2);
   {  // ... or lane-interleaved (the device policy): the same entries
     static ge_niels a2[EdWideCfg::kMult];
     static uint32_t park[EdWideCfg::kMult * ED_PARK_DWORDS];
@@ -604,7 +631,7 @@ extern "C" int t_ed_wide_row_cmp(uint32_t m) {
     if (memcmp(a, a2, sizeof a) != 0) return -1;
   }
   constexpr int CPG = ED_WIDE_GROUP / ED_WIDE_CHUNK;
-  for (int g = 0; g < ED_WIDE_GROUPS; ++g) ed_wide_group_pass<false>(nullptr, &zc[CPG * g], P, g, g_C.d2);
+  for (int g = 0; g < ED_WIDE_GROUPS; ++g) ed_wide_group_pass<false>((ge_niels*)nullptr, &zc[CPG * g], P, g, g_C.d2);
   fe_invert_run<ED_WIDE_CHUNKS>(zc, zc + ED_WIDE_CHUNKS);
   for (int g = 0; g < ED_WIDE_GROUPS; ++g) ed_wide_group_pass<true>(&b[ED_WIDE_GROUP * g], &zc[CPG * g], P, g, g_C.d2);
   int bad = 0;
@@ -648,7 +675,8 @@ extern "C" int t_ed_verify_wide(const uint32_t* aw, const uint32_t* sw, const ui
       for (int g = 0; g < ED_WIDE_ROW_LANES; ++g)
       {
         const int e0 = g * (EdWideCfg::kMult / ED_WIDE_ROW_LANES), e1 = e0 + EdWideCfg::kMult / ED_WIDE_ROW_LANES;
-        ed_wide_row_build(TA->t[j], EdParkRow{TA->t[j] + e0, zpre[j] + e0}, P, e0, e1, g_C.d2);
+        static fe px[EdWideCfg::kMult], py[EdWideCfg::kMult], pz[EdWideCfg::kMult];
+        ed_wide_row_build(TA->t[j], EdParkRow{px, py, pz, zpre[j] + e0}, P, e0, e1, g_C.d2);
       }
     }
 #ifdef FE_OP_COUNT
@@ -687,10 +715,11 @@ extern "C" int t_ed_verify_wide(const uint32_t* aw, const uint32_t* sw, const ui
 #ifdef FE_OP_COUNT
   g_fe_nmul = g_fe_nsq = 0;
 #endif
-  ed_double_scalar_wide(R, eh, es, *TA, *g_TBW, host_pick, host_pick);
+  g_fe9_nmul = 0;
+  ed_double_scalar_wide(R, eh, es, *TA, *g_TBW);
 #ifdef FE_OP_COUNT
   if (counts) {
-    counts[0] = g_fe_nmul;
+    counts[0] = g_fe9_nmul;  // radix-2^29 products (fe9.h): the wide ladder has no fe products
     counts[1] = g_fe_nsq;
   }
 #endif

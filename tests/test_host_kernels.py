@@ -207,10 +207,11 @@ def test_executed_work_constants_match_lane_code():
     _, _, mul_f, sq_f, mul_i, sq_i = (int(x) for x in out[:6])
     import ctypes
     lib.t_ed_verify_wb.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64, ctypes.c_void_p]
-    lad = np.zeros(2, dtype=np.uint64)
+    lad = np.zeros(3, dtype=np.uint64)
     assert lib.t_ed_verify_wb(ptr(words(key)), ptr(words(sig)), ptr(m), len(msg), ptr(lad)) == 0
-    mul_v, sq_v = int(lad[0]), int(lad[1])
+    mul_v, sq_v, mul9 = int(lad[0]), int(lad[1]), int(lad[2])
     assert (mul_v, sq_v) == bench.ED_VERIFY_FE, (mul_v, sq_v)
+    assert mul9 == bench.ED_VERIFY_FE9, mul9
     assert (mul_f, sq_f) == bench.ED_FINISH_FE, (mul_f, sq_f)
     assert (mul_i, sq_i) == bench.ED_INVERT_FE, (mul_i, sq_i)
 
@@ -425,3 +426,60 @@ def test_ed_wide_row_build_matches_three_pass():
     lib.t_ed_wide_row_cmp.argtypes = [ctypes.c_uint32]
     for m in (1, 2, 3, 8, 255, 4096, 65537, 0x7fffffff):
         assert lib.t_ed_wide_row_cmp(m) == 0, m
+
+
+# ---------------------------------------------------------------- radix-2^29 products (fe9.h)
+R29 = [29 * i for i in range(9)]
+
+
+def _fe9_int(v, signed=False):
+    return sum((int(np.int32(x)) if signed else int(x)) << o for x, o in zip(np.asarray(v, np.uint32), R29))
+
+
+def _fe9_class(rng, cls):
+    """Random limbs of one operand class of fe9.h, biased to the class's extremes."""
+    M = 1 << 29
+    hi = {"T": M, "A2": 2 * M + (1 << 18), "V": 3 * M + (1 << 17)}
+    out = []
+    for i in range(9):
+        if cls == "S":
+            b = M + (1 << 17) - 1
+            x = rng.choice([b, -b, rng.randrange(-b, b + 1)])
+            out.append(x & 0xffffffff)
+            continue
+        top = hi[cls] - 1 if not (cls == "T" and i != 1) else M - 1
+        if cls == "T" and i == 1:
+            top = M + (1 << 17) - 1
+        lo = (1 << 28) if cls == "V" else 0
+        out.append(rng.choice([top, lo, rng.randrange(lo, top + 1)]))
+    return np.array(out, np.uint32)
+
+
+@pytest.mark.parametrize("ca,cb,sgn", [("T", "T", 0), ("A2", "T", 0), ("A2", "A2", 0), ("A2", "V", 0), ("V", "A2", 0),
+                                       ("S", "T", 1), ("S", "A2", 1), ("S", "V", 1), ("S", "S", 1), ("T", "T", 1)])
+def test_fe9_mul_operand_classes(ca, cb, sgn):
+    """Every product the wide ladder forms (fe9.h operand classes) is exact with tight output;
+    the host build asserts each 64-bit column (FE_BOUNDS_CHECK) on extreme and random limbs."""
+    lib = hostk.lib()
+    rng = random.Random(hash((ca, cb, sgn)) & 0xffff)
+    out = np.zeros(9, np.uint32)
+    for _ in range(400):
+        a, b = _fe9_class(rng, ca), _fe9_class(rng, cb)
+        lib.t_fe9_mul(sgn, ptr(a), ptr(b), ptr(out))
+        assert (_fe9_int(out) - _fe9_int(a, sgn) * _fe9_int(b, sgn)) % P == 0
+        assert all(int(x) < (1 << 29) for i, x in enumerate(out) if i != 1) and int(out[1]) < (1 << 29) + (1 << 17)
+
+
+def test_fe9_conversions():
+    lib = hostk.lib()
+    rng = random.Random(9)
+    w = np.zeros(8, np.uint32)
+    f9 = np.zeros(9, np.uint32)
+    for _ in range(300):
+        x = rng.choice([rng.randrange(P), P - 1, 0, 1, 2 ** 255 - 20])
+        lib.t_fe9_from_fe(ptr(hostk.int_to_limbs(x)), ptr(f9))
+        assert _fe9_int(f9) == x and all(int(v) < (1 << 29) for v in f9)
+        big = _fe9_class(rng, rng.choice(["T", "A2", "V"]))  # any non-negative limbs
+        lib.t_fe9_to_words(ptr(big), ptr(w))
+        y = sum(int(v) << (32 * i) for i, v in enumerate(w))
+        assert y < 2 ** 255 and (y - _fe9_int(big)) % P == 0

@@ -73,7 +73,8 @@ struct SpliceHdr {
   uint64_t ids;       // device address of the 32-byte ids
   uint64_t n_ids;
   uint64_t img_off;   // byte offset of the images in the workspace
-  uint64_t slot;      // bytes per image (16-aligned, >= the longest message + 16)
+  uint64_t slot;      // bytes per image: round16(longest prefix + 32 + suffix), zero-filled past the
+                      // image (SpliceLd's aligned 16-byte reads past img_len see zeros)
   uint64_t w512_off;  // byte offset of the TmplW512 records
 };
 #define SPLICE_HDR_BYTES 256u

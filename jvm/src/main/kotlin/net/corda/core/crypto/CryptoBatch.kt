@@ -20,6 +20,12 @@ object CryptoBatch {
     private external fun nativeOpenPool(devices: IntArray): Long
     private external fun nativeVerify(ctx: Long, keys: ByteBuffer, nKeys: Int, items: ByteBuffer, nItems: Long,
                                       arena: ByteBuffer, arenaLen: Long, mode: Int, status: ByteBuffer): Int
+    private external fun nativeClose(ctx: Long)
+    private external fun nativeVerifyTransactions(ctx: Long, txs: ByteBuffer, nTx: Long, comps: ByteBuffer, nComps: Long,
+                                                  keys: ByteBuffer, nKeys: Int, sigs: ByteBuffer, nSigs: Long,
+                                                  tmpls: ByteBuffer, nTmpls: Int, arena: ByteBuffer, arenaLen: Long,
+                                                  mode: Int, idsOut: ByteBuffer, txStatusOut: ByteBuffer,
+                                                  sigStatusOut: ByteBuffer): Int
     private external fun nativeVerifyTxSignatures(ctx: Long, pool: Long, keys: ByteBuffer, nKeys: Int, ids: ByteBuffer,
                                                   nIds: Long, sigs: ByteBuffer, nSigs: Long, tmpls: ByteBuffer,
                                                   nTmpls: Int, arena: ByteBuffer, arenaLen: Long, mode: Int,
@@ -29,7 +35,11 @@ object CryptoBatch {
     const val MODE_ISVALID = 1
     private const val KEY_SPKI = 1
 
-    private val ctx: Long by lazy { nativeOpen(0) }
+    private val ctxDelegate = lazy { nativeOpen(0) }
+    private val ctx: Long by ctxDelegate
+
+    /** Releases the device context (cg_close); a later call opens a new one only in a new process. */
+    fun close() { if (ctxDelegate.isInitialized()) nativeClose(ctx) }
     /** Set by a node that drives every GPU from one process: the tx-signature calls then shard over the pool. */
     @Volatile var pool: Long = 0
     fun usePool(devices: IntArray) { pool = nativeOpenPool(devices) }
@@ -75,17 +85,27 @@ object CryptoBatch {
         return ByteArray(items.size).also { status.get(it) }
     }
 
+    /** SignableData(id, metadata) = prefix || id || suffix: found by serialising with two ids that
+     *  differ in every byte (0^32 and 0xFF^32) and taking the first differing offset, then checking
+     *  that the bytes around the id agree (a prefix that happens to end in 0x00, or an earlier run of
+     *  zero bytes, cannot shift the split). Mirrors corda_amd/signable.py:template. */
+    fun signableTemplate(m: SignatureMetadata): Pair<ByteArray, ByteArray> {
+        val a = SignableData(SecureHash.zeroHash, m).serialize().bytes
+        val b = SignableData(SecureHash.SHA256(ByteArray(32) { 0xFF.toByte() }), m).serialize().bytes
+        check(a.size == b.size) { "SignableData serialisation depends on the id's value" }
+        val at = a.indices.first { a[it] != b[it] }
+        check(at + 32 <= a.size && (at until at + 32).all { a[it] == 0.toByte() && b[it] == 0xFF.toByte() } &&
+              (at + 32 until a.size).all { a[it] == b[it] }) { "id not found as 32 contiguous bytes" }
+        return a.copyOfRange(0, at) to a.copyOfRange(at + 32, a.size)
+    }
+
     /** Batch Crypto.doVerify(txId, TransactionSignature) (Crypto.kt:499-502) for every signature of
      *  every transaction, SignableData spliced on the device: one status byte per signature, in order. */
     fun verifyTxSignatures(txs: List<Pair<SecureHash, List<TransactionSignature>>>, mode: Int = MODE_DOVERIFY): ByteArray {
         val all = txs.flatMap { it.second }
         val metas = LinkedHashMap<SignatureMetadata, Int>()
         all.forEach { metas.getOrPut(it.signatureMetadata) { metas.size } }
-        val split = metas.keys.map { m ->                         // SignableData(0^32, m) around the id
-            val bytes = SignableData(SecureHash.zeroHash, m).serialize().bytes
-            val at = (0..bytes.size - 32).first { i -> (0 until 32).all { bytes[i + it] == 0.toByte() } }
-            bytes.copyOfRange(0, at) to bytes.copyOfRange(at + 32, bytes.size)
-        }
+        val split = metas.keys.map { signableTemplate(it) }
         val arena = direct(all.sumOf { it.bytes.size + 4 } + split.sumOf { it.first.size + it.second.size + 8 } +
                            all.map { it.by }.distinct().sumOf { it.encoded.size + 4 } + 16)
         val keys = Keys(all.map { it.by }, arena)
@@ -112,6 +132,29 @@ object CryptoBatch {
                                           mode, status)
         check(rc == 0) { "cg_verify_tx_signatures failed: $rc" }
         return ByteArray(all.size).also { status.get(it) }
+    }
+
+    /** cg_verify_batch over tables already in the C ABI's layout (the out-of-process verifier's batch
+     *  request body, VerifierBatchApi.kt): no re-encoding. One status byte per item. */
+    fun verifyPacked(keys: ByteBuffer, nKeys: Int, items: ByteBuffer, nItems: Int, arena: ByteBuffer, arenaLen: Long,
+                     mode: Int = MODE_DOVERIFY): ByteArray {
+        val status = direct(nItems)
+        val rc = nativeVerify(ctx, keys, nKeys, items, nItems.toLong(), arena, arenaLen, mode, status)
+        check(rc == 0) { "cg_verify_batch failed: $rc" }
+        return ByteArray(nItems).also { status.get(it) }
+    }
+
+    /** WireTransaction ids + every signature in one call (cg_verify_transactions, include/cordagpu.h):
+     *  the tables are the C ABI's own (cg_tx / cg_component / cg_txsig / cg_signable_tmpl, built by the
+     *  out-of-process verifier from the request body it already holds). Fills the 32-byte ids, one
+     *  status per transaction (Merkle) and one per signature. */
+    fun verifyTransactionsPacked(txs: ByteBuffer, nTx: Long, comps: ByteBuffer, nComps: Long, keys: ByteBuffer,
+                                 nKeys: Int, sigs: ByteBuffer, nSigs: Long, tmpls: ByteBuffer, nTmpls: Int,
+                                 arena: ByteBuffer, arenaLen: Long, idsOut: ByteBuffer, txStatusOut: ByteBuffer,
+                                 sigStatusOut: ByteBuffer, mode: Int = MODE_DOVERIFY) {
+        val rc = nativeVerifyTransactions(ctx, txs, nTx, comps, nComps, keys, nKeys, sigs, nSigs, tmpls, nTmpls, arena,
+                                          arenaLen, mode, idsOut, txStatusOut, sigStatusOut)
+        check(rc == 0) { "cg_verify_transactions failed: $rc" }
     }
 
     /** Re-raise what the serial Crypto.doVerify would have done for an item; a scheme the GPU does not

@@ -109,3 +109,32 @@ def test_worker_gpu_golden(engine):
             r = V.BatchSignatureResponse.from_bytes(w.handle(V.BatchSignatureRequest.from_batch(3, b, mode).to_bytes()))
             assert r.error is None and r.verification_id == 3
             assert np.array_equal(r.status, want)
+
+
+def test_wire_format_matches_kotlin_constants():
+    """jvm/.../VerifierBatchApi.kt (not compiled here: no JDK) encodes the same header as this
+    module: magic words, header sizes and the C ABI record sizes agree."""
+    import os
+    import re
+    from corda_amd import batch as B
+    from corda_amd import verifier as V
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    kt = open(os.path.join(root, "jvm/src/main/kotlin/net/corda/nodeapi/VerifierBatchApi.kt")).read()
+    const = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"const val (\w+) = (0x[0-9a-fA-F]+|\d+)", kt)}
+    const.update({m.group(1): int(m.group(2), 0) for m in re.finditer(r"private const val (\w+) = (0x[0-9a-fA-F]+|\d+)", kt)})
+    assert const["REQ_MAGIC"].to_bytes(4, "little") == V._REQ_MAGIC
+    assert const["RSP_MAGIC"].to_bytes(4, "little") == V._RSP_MAGIC
+    assert const["REQ_HEADER"] == V._REQ_HDR.size and const["RSP_HEADER"] == V._RSP_HDR.size
+    assert const["KEY_BYTES"] == B.KEY_DTYPE.itemsize and const["ITEM_BYTES"] == B.ITEM_DTYPE.itemsize
+
+
+def test_jni_exports_match_kotlin_externals():
+    """Every `external fun` of CryptoBatch.kt has its JNI export in cordagpu_jni.c and vice versa."""
+    import os
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    kt = open(os.path.join(root, "jvm/src/main/kotlin/net/corda/core/crypto/CryptoBatch.kt")).read()
+    c = open(os.path.join(root, "jvm/jni/cordagpu_jni.c")).read()
+    ext = set(re.findall(r"external fun (\w+)\(", kt))
+    exp = set(re.findall(r"Java_net_corda_core_crypto_CryptoBatch_(\w+)\(", c))
+    assert ext == exp and ext, (ext ^ exp)

@@ -88,6 +88,11 @@ struct cg_ctx {
   std::mutex mu;
   DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
   DevBuf wide;  // wide-table pools (keyws.h), sized by the largest call's item count
+  // wide slots this context may allocate: lowered when the device's free memory cannot hold the
+  // pool a call asks for (another process or context on the device), so the call runs
+  // with fewer hot keys on wide tables (full tables for the rest: slower, same verdicts) instead of
+  // failing with CG_ERR_NOMEM
+  uint32_t wide_max = 8192u;
   // transaction pipeline: verify items, spliced messages, templates; host-entry staging
   DevBuf txitems, msgs, tmpls, h_txs, h_comps, h_sigs, h_ids, h_txst;
   // tear-offs: leaf-hash workspace
@@ -133,10 +138,25 @@ uint64_t chunk_of(const cg_ctx* c, uint64_t n) {
 // before chunk k's back).
 size_t item_half_bytes(uint64_t ws_items) { return (cg::item_ws_bytes(ws_items) + 255) & ~(size_t)255; }
 hipError_t ensure_ws(cg_ctx* c, uint32_t n_keys, uint64_t ws_items, uint64_t call_items = 0) {
-  const size_t wide = cg::wide_bytes(n_keys, call_items);
+  size_t wide = cg::wide_bytes(n_keys, call_items, c->wide_max);
   const size_t items = item_half_bytes(ws_items) * (call_items > ws_items ? 2 : 1);
   if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= items && c->wide.cap >= wide)
     return hipSuccess;
+  if (wide > c->wide.cap) {  // cap the wide pool by the device's free memory (keeping 1 GiB spare)
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+      const size_t need_other = (c->keyprep.cap >= cg::keyprep_bytes(n_keys) ? 0 : cg::keyprep_bytes(n_keys)) +
+                                (c->itemws.cap >= items ? 0 : items);
+      const size_t avail = free_b + c->wide.cap;  // the current pool is freed before the new one
+      const size_t spare = (size_t)1 << 30;
+      if (wide + need_other + spare > avail) {
+        const size_t room = avail > need_other + spare ? avail - need_other - spare : 0;
+        const size_t per = cg::wide_slot_bytes();
+        c->wide_max = (uint32_t)std::min<size_t>(room / per, c->wide_max);
+        wide = cg::wide_bytes(n_keys, call_items, c->wide_max);
+      }
+    }
+  }
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess) e = c->keyprep.ensure(cg::keyprep_bytes(n_keys));
   if (e == hipSuccess) e = c->itemws.ensure(items);
@@ -150,8 +170,8 @@ cg::WidePool wide_for(cg_ctx* c, uint32_t n_keys, uint64_t n_items) {
     const char* v = getenv("CG_NO_WIDE_TABLES");
     return v && v[0] == '1';
   }();
-  if (off || c->wide.cap < cg::wide_bytes(n_keys, n_items)) return cg::WidePool{};
-  cg::WidePool p = cg::make_wide_pool(c->wide.p, n_keys, n_items);
+  if (off || c->wide.cap < cg::wide_bytes(n_keys, n_items, c->wide_max)) return cg::WidePool{};
+  cg::WidePool p = cg::make_wide_pool(c->wide.p, n_keys, n_items, c->wide_max);
   static const uint32_t min_ed = [] {  // CG_WIDE_MIN_USES_ED / _EC: override the thresholds (A/B runs)
     const char* v = getenv("CG_WIDE_MIN_USES_ED");
     return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;

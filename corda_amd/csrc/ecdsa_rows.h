@@ -12,6 +12,7 @@
 // Exception cases (R = +-T, R = infinity) are handled inside jac_madd, so adversarial
 // inputs stay exact; honest lanes never take those branches.
 #pragma once
+#include "ec9.h"
 #include "ecdsa.h"
 
 #define EC_W 6
@@ -380,6 +381,16 @@ CG_HD uint32_t ecdsa_x_check(const Jac& R, const u256w& r, const EcConsts& K) {
     if (m29_eq<C, 0>(t, R.X)) return 0;
   }
   return 1;
+}
+
+// the same check on a wide-ladder result in ec9.h's signed form
+template <int C>
+CG_HD uint32_t ecdsa_x_check9(const Jac& R, const u256w& r, const EcConsts& K) {
+  Jac q;
+  ec9_to_m29<C>(q.X, R.X);
+  ec9_to_m29<C>(q.Y, R.Y);
+  ec9_to_m29<C>(q.Z, R.Z);
+  return ecdsa_x_check<C>(q, r, K);
 }
 
 template <class Row>
@@ -887,7 +898,7 @@ CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u
       const int a = b < 0 ? -b : b;  // the top digit alone reaches 129..256: row 32
       if (a > EC_WIDE_MULT) ec_pick(x, y, TQ.t[EC_WIDE_DIGITS], a - EC_WIDE_MULT);
       else ec_pick(x, y, TQ.t[j], a);
-      jac_madd_w<C>(R, inf, x, y, b < 0, K);
+      jac_madd9<C>(R, inf, x, y, b < 0, K);
     }
   }
 #pragma unroll 1
@@ -896,10 +907,10 @@ CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u
     if (a != 0) {
       f29 x, y;
       ec_pick(x, y, TG.t[u], a < 0 ? -a : a);
-      jac_madd_w<C>(R, inf, x, y, a < 0, K);
+      jac_madd9<C>(R, inf, x, y, a < 0, K);
     }
   }
-  return ecdsa_x_check<C>(R, r, K);
+  return ecdsa_x_check9<C>(R, r, K);
 }
 
 // G wide row u, multiples 32 g + 1 .. 32 g + 32 (one lane of the per-context table build)

@@ -115,8 +115,9 @@ hipError_t upload_constants();
 size_t keyprep_bytes(uint32_t n_keys);
 // Wide-table pools for a call of n_items over n_keys (keyws.h: keys with many items get one table
 // row per radix-2^8 digit): bytes, and the pool view over `base` (caps 0 when nothing can be wide).
-size_t wide_bytes(uint32_t n_keys, uint64_t n_items);
-WidePool make_wide_pool(void* base, uint32_t n_keys, uint64_t n_items);
+size_t wide_bytes(uint32_t n_keys, uint64_t n_items, uint32_t max_slots = 8192u);
+size_t wide_slot_bytes();  // one Ed25519 + one ECDSA wide slot
+WidePool make_wide_pool(void* base, uint32_t n_keys, uint64_t n_items, uint32_t max_slots = 8192u);
 
 // Enqueue the whole verify pipeline for one batch on `stream`:
 //   key prep (one lane per key) -> per-scheme verify (one lane per item) -> status bytes.

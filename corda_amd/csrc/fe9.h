@@ -58,6 +58,24 @@ CG_HD uint32_t fe9_opaque(uint32_t v) {
   return v;
 }
 
+// a b + c as one MAC whose result the compiler may not re-associate (an empty asm pins it): product
+// scanning keeps the carry inside the column's MAC chain instead of a 64-bit add per column. (The
+// MAC itself as inline asm made the hazard recognizer put an s_nop after every one: 313 per addition.)
+CG_HD uint64_t fe9_mac_u(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t r = (uint64_t)a * b + c;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(r));
+#endif
+  return r;
+}
+CG_HD int64_t fe9_mac_i(uint32_t a, uint32_t b, int64_t c) {
+  int64_t r = (int64_t)(int32_t)a * (int32_t)b + c;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(r));
+#endif
+  return r;
+}
+
 CG_HD void fe9_0(fe9& h) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) h.v[i] = 0;
@@ -173,15 +191,26 @@ CG_HD void fe9_mul(fe9& out, const fe9& a, const fe9& b) {
   acc_t acc = Signed ? (acc_t)(-(int64_t)19 * ((int64_t)1 << 40)) : 0;
 #pragma unroll
   for (int m = 0; m < 9; ++m) {
+#ifndef FE9_SCAN_ASM  // 1: pinned MACs (fe9_mac_*): 1004 -> 993 VALU per addition, but 176 s_nop (rejected)
+#define FE9_SCAN_ASM 0
+#endif
 #pragma unroll
     for (int i = 0; i <= m; ++i) {
-      if (Signed) acc += (acc_t)(int64_t)(int32_t)a.v[i] * (int64_t)(int32_t)b.v[m - i];
-      else acc += (acc_t)((uint64_t)a.v[i] * b.v[m - i]);
+      if (FE9_SCAN_ASM && m > 0) {  // every MAC of the chain (an asm one among C adds is re-associated anyway);
+                                   // column 0 stays C: its constant addend then needs no VGPR copy
+        if (Signed) acc = (acc_t)fe9_mac_i(a.v[i], b.v[m - i], (int64_t)acc);
+        else acc = (acc_t)fe9_mac_u(a.v[i], b.v[m - i], (uint64_t)acc);
+      } else if (Signed) {
+        acc += (acc_t)(int64_t)(int32_t)a.v[i] * (int64_t)(int32_t)b.v[m - i];
+      } else {
+        acc += (acc_t)((uint64_t)a.v[i] * b.v[m - i]);
+      }
     }
-    if (m <= 7) acc += (acc_t)((uint64_t)(uint32_t)hc[m] * k1216);
+    if (m <= 7) acc = (acc_t)fe9_mac_u((uint32_t)hc[m], k1216, (uint64_t)acc);
     if (m >= 1) {
-      if (Signed) acc += (acc_t)((int64_t)(int32_t)(uint32_t)((uint64_t)hc[m - 1] >> 32) * (int64_t)(int32_t)k9728);
-      else acc += (acc_t)((uint64_t)(uint32_t)((uint64_t)hc[m - 1] >> 32) * k9728);
+      const uint32_t hi = (uint32_t)((uint64_t)hc[m - 1] >> 32);
+      if (Signed) acc = (acc_t)fe9_mac_i(hi, k9728, (int64_t)acc);
+      else acc = (acc_t)fe9_mac_u(hi, k9728, (uint64_t)acc);
     }
     d[m] = (uint32_t)acc & FE9_M;
     if (m < 8) {

@@ -264,10 +264,13 @@ struct EcWideSlot {
   };
 };
 // Slots for a call of n_items over n_keys: no more keys can reach KEY_WIDE_MIN_USES.
-static inline uint32_t wide_cap(uint32_t n_keys, uint64_t n_items, uint32_t min_uses = KEY_WIDE_MIN_USES) {
+// max_slots: the context's device-memory cap (cordagpu.cpp ensure_ws: ADVICE r3).
+static inline uint32_t wide_cap(uint32_t n_keys, uint64_t n_items, uint32_t max_slots = KEY_WIDE_MAX,
+                                uint32_t min_uses = KEY_WIDE_MIN_USES) {
   uint64_t c = n_items / min_uses;
   if (c > n_keys) c = n_keys;
   if (c > KEY_WIDE_MAX) c = KEY_WIDE_MAX;
+  if (c > max_slots) c = max_slots;
   return (uint32_t)c;
 }
 static inline size_t wide_pool_bytes(uint32_t cap) {

@@ -10,9 +10,12 @@
 //
 // Failure: a shard whose call fails with a device fault (CG_ERR_DEVICE) marks its slot unhealthy
 // and has its slice reset to CG_NOT_RUN; failed shards are then re-run on the slots that are still
-// healthy, round-robin, until every shard has run or no healthy slot is left. Argument, range and
-// capacity errors (CG_ERR_ARG / CG_ERR_RANGE / CG_ERR_NOMEM) say nothing about the device: they
-// end the call with that code and leave every slot as it was. An unhealthy slot is
+// healthy, round-robin, until every shard has run or no healthy slot is left. Argument and range
+// errors (CG_ERR_ARG / CG_ERR_RANGE) say nothing about the device: they end the call with that code
+// and leave every slot as it was. A capacity error (CG_ERR_NOMEM: that context could not
+// allocate, e.g. another process holds the device's memory) re-queues the shard on another live
+// slot without touching the slot's health; only a shard every live slot has refused stays
+// CG_NOT_RUN, and the call then returns CG_ERR_NOMEM after the other shards ran. An unhealthy slot is
 // re-probed at the start of every call (probe(slot): the context answers and no drill fault is
 // set) and rejoins the plan when it answers. The reference
 // gets this from Artemis redelivery of the verifier's request (VerifierTests.kt:73-99,
@@ -34,6 +37,7 @@ struct PoolShard {
   uint64_t first, count;
   uint32_t slot;
   int rc;
+  uint64_t refused;  // slots (bit s, s < 64) that answered CG_ERR_NOMEM for this shard
 };
 
 struct PoolReport {
@@ -64,7 +68,7 @@ int pool_run(std::vector<uint8_t>& healthy, uint64_t n_items, uint8_t* status, V
   const uint64_t k = live.size();
   for (uint64_t j = 0; j < k; ++j) {
     const uint64_t a = n_items * j / k, b = n_items * (j + 1) / k;
-    if (b > a) pending.push_back(PoolShard{a, b - a, 0, CG_OK});
+    if (b > a) pending.push_back(PoolShard{a, b - a, 0, CG_OK, 0});
   }
   if (n_items && k == 0) {
     r.not_run = n_items;
@@ -72,7 +76,7 @@ int pool_run(std::vector<uint8_t>& healthy, uint64_t n_items, uint8_t* status, V
     return CG_ERR_DEVICE;
   }
   r.shards = (uint32_t)pending.size();
-  bool first = true;
+  bool first = true, nomem = false;
   while (!pending.empty()) {
     refresh();
     if (live.empty()) {
@@ -80,22 +84,51 @@ int pool_run(std::vector<uint8_t>& healthy, uint64_t n_items, uint8_t* status, V
       if (rep) *rep = r;
       return CG_ERR_DEVICE;
     }
-    // one shard per healthy slot per pass (a slot's context serialises its calls anyway)
-    const size_t take = pending.size() < live.size() ? pending.size() : live.size();
-    std::vector<PoolShard> pass(pending.begin(), pending.begin() + take);
-    pending.erase(pending.begin(), pending.begin() + take);
-    for (size_t j = 0; j < take; ++j) pass[j].slot = live[j];
-    if (!first) r.reruns += (uint32_t)take;
+    // one shard per live slot per pass (a slot's context serialises its calls anyway), never on a
+    // slot that refused it for capacity; a shard every live slot has refused is given up
+    std::vector<PoolShard> pass, keep;
+    std::vector<uint8_t> used(healthy.size(), 0);
+    for (PoolShard& sh : pending) {
+      bool any = false;
+      int pick = -1;
+      for (uint32_t s : live) {
+        const bool refused = s < 64 && ((sh.refused >> s) & 1u);
+        if (refused) continue;
+        any = true;
+        if (!used[s]) {
+          pick = (int)s;
+          break;
+        }
+      }
+      if (!any) {
+        nomem = true;
+        r.not_run += sh.count;
+      } else if (pick < 0) {
+        keep.push_back(sh);
+      } else {
+        used[pick] = 1;
+        sh.slot = (uint32_t)pick;
+        pass.push_back(sh);
+      }
+    }
+    pending.swap(keep);
+    if (pass.empty()) continue;
+    if (!first) r.reruns += (uint32_t)pass.size();
     first = false;
     std::vector<std::thread> th;
-    th.reserve(take);
+    th.reserve(pass.size());
     for (PoolShard& sh : pass) th.emplace_back([&sh, &verify]() { sh.rc = verify(sh.slot, sh.first, sh.count); });
     for (std::thread& t : th) t.join();
     int hard = CG_OK;
     for (PoolShard& sh : pass) {
       if (sh.rc == CG_OK) continue;
       memset(status + sh.first, CG_NOT_RUN, sh.count);
-      if (sh.rc != CG_ERR_DEVICE) {  // the caller's input or capacity, not the device
+      if (sh.rc == CG_ERR_NOMEM && sh.slot < 64) {  // capacity: try another slot, the slot stays healthy
+        sh.refused |= 1ull << sh.slot;
+        pending.push_back(sh);
+        continue;
+      }
+      if (sh.rc != CG_ERR_DEVICE) {  // the caller's input, not the device
         if (hard == CG_OK) hard = sh.rc;
         r.not_run += sh.count;
         continue;
@@ -113,7 +146,7 @@ int pool_run(std::vector<uint8_t>& healthy, uint64_t n_items, uint8_t* status, V
     }
   }
   if (rep) *rep = r;
-  return CG_OK;
+  return nomem ? CG_ERR_NOMEM : CG_OK;
 }
 
 }  // namespace cg

@@ -143,9 +143,12 @@ hipError_t upload_constants() {
 }
 
 size_t keyprep_bytes(uint32_t n_keys) { return key_ws_bytes(n_keys); }
-size_t wide_bytes(uint32_t n_keys, uint64_t n_items) { return wide_pool_bytes(wide_cap(n_keys, n_items)); }
-WidePool make_wide_pool(void* base, uint32_t n_keys, uint64_t n_items) {
-  return wide_pool(base, wide_cap(n_keys, n_items));
+size_t wide_bytes(uint32_t n_keys, uint64_t n_items, uint32_t max_slots) {
+  return wide_pool_bytes(wide_cap(n_keys, n_items, max_slots));
+}
+size_t wide_slot_bytes() { return wide_pool_bytes(1); }
+WidePool make_wide_pool(void* base, uint32_t n_keys, uint64_t n_items, uint32_t max_slots) {
+  return wide_pool(base, wide_cap(n_keys, n_items, max_slots));
 }
 size_t item_ws_bytes(uint64_t n_items) { return item_ws_total(n_items); }
 size_t btab_bytes() { return const_tab_bytes(); }

@@ -420,9 +420,9 @@ __global__ void __launch_bounds__(256) k_ec_ladder_wide(const cg_item* __restric
         d_next = ec_wide_digit(dq, dg, o + 1);
         ec_glds_aff(ec_wide_src(TQ, *gw, o + 1, d_next), wl);
       }
-      if (d != 0) jac_madd_w<C>(R, inf, x, y, d < 0, K);
+      if (d != 0) jac_madd9<C>(R, inf, x, y, d < 0, K);  // signed-limb form (ec9.h)
     }
-    status[i] = (uint8_t)ecdsa_x_check<C>(R, w.r, K);
+    status[i] = (uint8_t)ecdsa_x_check9<C>(R, w.r, K);
   }
 }
 

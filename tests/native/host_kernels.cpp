@@ -917,6 +917,96 @@ static int madd_w_cmp(uint64_t seed, int n) {
   }
   return bad;
 }
+// jac_madd9 (ec9.h, signed limbs) against the exception-complete jac_madd over chains of n additions
+// of random multiples of G (a wide ladder's 44 and more), with Q = +-acc cases (the exact path);
+// every product's columns are asserted below 2^63 (FE_BOUNDS_CHECK). Returns mismatching chains.
+template <int C>
+static int madd9_cmp(uint64_t seed, int chains, int len) {
+  EcConsts K;
+  ec_consts_init<C>(K);
+  uint64_t s = seed;
+  auto rnd = [&]() {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    return s;
+  };
+  int bad = 0;
+  for (int t = 0; t < chains; ++t) {
+    Jac ref, got;
+    jac_set_inf<C>(ref, K);
+    got = ref;
+    bool inf = true;
+    for (int o = 0; o < len; ++o) {
+      f29 qx, qy;
+      const int kind = (int)(rnd() % 64);
+      bool neg = rnd() & 1;
+      if (o > 0 && kind == 0) {  // Q = +-R (doubling or infinity through the exact path)
+        f29 ax, ay;
+        jac_to_affine<C>(ax, ay, ref, K);
+        if (m29_iszero<C, 0>(ref.Z)) continue;
+        qx = ax;
+        qy = ay;
+      } else {
+        Jac q;
+        jac_small_mul_aff<C>(q, K.gx, K.gy, 1 + (uint32_t)(rnd() % 100000), K);
+        jac_to_affine<C>(qx, qy, q, K);
+      }
+      f29 y = qy;
+      if (neg) m29_neg<C, 0>(y, qy);
+      if (m29_iszero<C, 0>(ref.Z)) {  // jac_madd's infinity input: R = Q
+        ref.X = qx;
+        ref.Y = y;
+        ref.Z = K.one_p;
+      } else {
+        jac_madd<C>(ref, ref, qx, y, K);
+      }
+      jac_madd9<C>(got, inf, qx, qy, neg, K);
+    }
+    Jac g;
+    ec9_to_m29<C>(g.X, got.X);
+    ec9_to_m29<C>(g.Y, got.Y);
+    ec9_to_m29<C>(g.Z, got.Z);
+    const bool rinf = m29_iszero<C, 0>(ref.Z), ginf = inf || m29_iszero<C, 0>(g.Z);
+    if (rinf || ginf) {
+      bad += rinf != ginf;
+      continue;
+    }
+    f29 x1, y1, x2, y2;
+    jac_to_affine<C>(x1, y1, ref, K);
+    jac_to_affine<C>(x2, y2, g, K);
+    if (!(m29_eq<C, 0>(x1, x2) && m29_eq<C, 0>(y1, y2))) ++bad;
+  }
+  return bad;
+}
+extern "C" void t_ec9_to_m29(int curve, const uint32_t* in, uint32_t* out) {
+  f29 a, r;
+  memcpy(a.v, in, 36);
+  if (curve == 1) ec9_to_m29<CG_CURVE_R1>(r, a);
+  else ec9_to_m29<CG_CURVE_K1>(r, a);
+  memcpy(out, r.v, 36);
+}
+extern "C" void t_ec9_mul(int curve, int form, const uint32_t* a, const uint32_t* b, const uint32_t* c,
+                          const uint32_t* d, uint32_t* out) {
+  f29 A, B, Cc, D, R;
+  memcpy(A.v, a, 36);
+  memcpy(B.v, b, 36);
+  memcpy(Cc.v, c, 36);
+  memcpy(D.v, d, 36);
+  if (curve == 1) {
+    if (form == 0) ec9_mul<CG_CURVE_R1>(R, A, B);
+    else if (form == 1) ec9_mul_add<CG_CURVE_R1>(R, A, B, Cc);
+    else ec9_mul2<CG_CURVE_R1>(R, A, B, Cc, D);
+  } else {
+    if (form == 0) ec9_mul<CG_CURVE_K1>(R, A, B);
+    else if (form == 1) ec9_mul_add<CG_CURVE_K1>(R, A, B, Cc);
+    else ec9_mul2<CG_CURVE_K1>(R, A, B, Cc, D);
+  }
+  memcpy(out, R.v, 36);
+}
+extern "C" int t_ec_madd9_cmp(int curve, uint64_t seed, int chains, int len) {
+  return curve == 1 ? madd9_cmp<CG_CURVE_R1>(seed, chains, len) : madd9_cmp<CG_CURVE_K1>(seed, chains, len);
+}
 extern "C" int t_ec_madd_w_cmp(int curve, uint64_t seed, int n) {
   return curve == 1 ? madd_w_cmp<CG_CURVE_R1>(seed, n) : madd_w_cmp<CG_CURVE_K1>(seed, n);
 }

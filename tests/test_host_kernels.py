@@ -384,7 +384,10 @@ def test_executed_work_constants_wide():
                                            int(k["fmt"]), int(itm["sig_off"]), int(itm["sig_len"]),
                                            int(itm["msg_off"]), int(itm["msg_len"]), ptr(o)) == 0
             lad.append(int(o[0]))
-        assert max(lad) == bench.EC_WIDE_MUL[name] and np.mean(lad) > 0.97 * max(lad), (name, lad)
+        # the full schedule is the common count; a lane whose H passes ec9.h's zero filter (false
+        # positives ~2^-24 per addition) recomputes 4 products on the exact path
+        assert int(np.median(lad)) == bench.EC_WIDE_MUL[name] and max(lad) <= bench.EC_WIDE_MUL[name] + 8, (name, lad)
+        assert np.mean(lad) > 0.97 * bench.EC_WIDE_MUL[name], (name, lad)
 
 
 @pytest.mark.parametrize("curve", [0, 1])
@@ -483,3 +486,13 @@ def test_fe9_conversions():
         lib.t_fe9_to_words(ptr(big), ptr(w))
         y = sum(int(v) << (32 * i) for i, v in enumerate(w))
         assert y < 2 ** 255 and (y - _fe9_int(big)) % P == 0
+
+
+@pytest.mark.parametrize("curve", [0, 1])
+def test_ec_madd9_matches_madd(curve):
+    """The wide ladder's signed-limb addition (ec9.h: no carry chains, fused X3 and Y3) follows the
+    exception-complete jac_madd over 60-addition chains of random multiples of G, including Q = +-R
+    (doubling / infinity through the exact path), every product column asserted < 2^63."""
+    lib = hostk.lib()
+    lib.t_ec_madd9_cmp.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+    assert lib.t_ec_madd9_cmp(curve, 777 + curve, 60, 60) == 0

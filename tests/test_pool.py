@@ -116,16 +116,29 @@ def test_empty_batch(batch):
     assert rc == 0 and st.size == 0 and int(calls.sum()) == 0
 
 
-def test_capacity_error_does_not_poison_the_slot(batch):
-    """A non-device error (here CG_ERR_NOMEM) ends the call with that code and leaves every slot
-    healthy: one oversized batch cannot kill the pool."""
+def test_capacity_error_reruns_elsewhere_and_keeps_the_slot(batch):
+    """A slot that cannot allocate (CG_ERR_NOMEM: e.g. another process holds its device's memory)
+    hands its shard to another live slot and stays healthy: the call completes."""
     L = _lib()
     b, exp = batch
     rc, st, h, calls, rep = _run(L, b, 3, fail_arg=0b010)
-    assert rc == -3 and list(h) == [1, 1, 1] and int(rep[2]) == 0
-    assert int(rep[3]) > 0 and np.all(st[st != 255] == exp[st != 255])
+    assert rc == 0 and np.array_equal(st, exp)
+    assert list(h) == [1, 1, 1] and int(rep[2]) == 0 and int(rep[1]) == 1 and calls[1] == 1
     rc, st, h, calls, rep = _run(L, b, 3)
     assert rc == 0 and np.array_equal(st, exp)
+
+
+def test_capacity_error_on_every_slot_leaves_not_run(batch):
+    """Only a shard every live slot refused stays CG_NOT_RUN, and the call returns CG_ERR_NOMEM;
+    no slot is marked unhealthy for it (the device is fine)."""
+    L = _lib()
+    b, exp = batch
+    rc, st, h, calls, rep = _run(L, b, 3, fail_arg=0b111)
+    assert rc == -3 and list(h) == [1, 1, 1] and int(rep[2]) == 0
+    assert int(rep[3]) == b.n and np.all(st == 255) and list(calls) == [3, 3, 3]
+    # two slots refuse: everything runs on the third
+    rc, st, h, calls, rep = _run(L, b, 3, fail_arg=0b011)
+    assert rc == 0 and np.array_equal(st, exp) and list(h) == [1, 1, 1]
 
 
 def test_unhealthy_slot_rejoins_after_probe(batch):

@@ -107,6 +107,7 @@ struct cg_ctx {
   size_t pin_counts_cap = 0;
   std::vector<hipEvent_t> seg;
   hipEvent_t tev[4] = {};
+  std::vector<hipEvent_t> segt;  // CG_HOST_TRACE: timing events behind each chunk's copy
   // the end of the last call's device work, whatever stream it ran on: the next call waits for it
   // before touching the shared workspace (async calls on different streams)
   hipEvent_t done = nullptr;
@@ -595,6 +596,7 @@ void cg_close(cg_ctx* c) {
       hipStreamSynchronize(*cs);
       hipStreamDestroy(*cs);
     }
+  for (hipEvent_t e : c->segt) hipEventDestroy(e);
   if (c->pin_counts) hipHostFree(c->pin_counts);
   for (hipEvent_t e : c->seg) hipEventDestroy(e);
   for (int k = 0; k < 4; ++k)
@@ -1130,9 +1132,15 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     // ms, ~1.4% of the headline, profiles/r03/ab_der), a wide table costs about 230 items' work.
     const cg::WidePool thr = cg::make_wide_pool(nullptr, n_keys, n_sigs);  // the wide thresholds
     const uint64_t floor_hot = S >= CG_TXSIG_COUNT_SAMPLE ? (uint64_t)std::max(thr.min_ed, thr.min_ec) : 0u;
+    // The raised estimate only where it decides a wide table: below the wide threshold the plain
+    // S c decides row 0 against full tables (a wrong full table costs ~230 ns, a wrong row 0 ~7 ns
+    // per use; at 1 in 8 the raised estimate put every sampled key of the 2^20-distinct-key leg,
+    // ~12 uses each, in full mode: 22-row builds for ~1M keys, profiles/r04/kd)
     for (uint32_t k = 0; k < n_keys; ++k) {
       const uint64_t c = counts[k];
-      uint64_t e = c ? (uint64_t)S * (c + 3 * (uint64_t)std::ceil(std::sqrt((double)c)) + 1)
+      const uint64_t up = (uint64_t)S * (c + 3 * (uint64_t)std::ceil(std::sqrt((double)c)) + 1);
+      const uint64_t wmin = keys[k].scheme == CG_EDDSA_ED25519_SHA512 ? thr.min_ed : thr.min_ec;
+      uint64_t e = c ? (up >= wmin ? up : (uint64_t)S * c)
                      : (S < 8u ? S : 8u);  // unsampled: row-0 tables (below the 32-use threshold)
       if (c && e < floor_hot) e = floor_hot;
       counts[k] = e > 0xfffffff0ull ? 0xfffffff0u : (uint32_t)e;
@@ -1211,15 +1219,37 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   // chunk k: its slice of the signature table, the ids it references not yet resident (a caller that
   // lists each transaction's signatures together ships each id once, with its first chunk), then its
   // signature bytes, on copy stream cs; seg[k] marks the end
+  // CG_HOST_TRACE=1: per-chunk host timings to stderr (extent scan, each copy call's return)
+  static const bool htrace = [] {
+    const char* v = getenv("CG_HOST_TRACE");
+    return v && v[0] == '1';
+  }();
+  auto ms_since = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
   auto copy_chunk = [&](uint64_t k, hipStream_t cs) {
     Extent ek, ik;
+    const double h0 = htrace ? ms_since() : 0;
     chunk_extents(k, ek, ik);
+    const double h1 = htrace ? ms_since() : 0;
     const uint64_t first = bounds[k], cnt = bounds[k + 1] - bounds[k];
     hipError_t e = hipMemcpyAsync((cg_txsig*)c->h_sigs.p + first, sigs + first, sizeof(cg_txsig) * cnt,
                                   hipMemcpyHostToDevice, cs);
+    const double h2 = htrace ? ms_since() : 0;
     if (e == hipSuccess) e = copy_missing(have_ids, ik, ids, (uint8_t*)c->h_ids.p, 0, cs);
+    const double h3 = htrace ? ms_since() : 0;
     if (e == hipSuccess) e = copy_missing(have, ek, arena, dwin, win.lo, cs);
     if (e == hipSuccess) e = hipEventRecord(c->seg[k], cs);
+    if (e == hipSuccess && htrace) {
+      while (c->segt.size() <= k) {
+        hipEvent_t ev;
+        if (hipEventCreate(&ev) != hipSuccess) break;
+        c->segt.push_back(ev);
+      }
+      if (c->segt.size() > k) e = hipEventRecord(c->segt[k], cs);
+    }
+    if (htrace)
+      fprintf(stderr, "[cg host] chunk %llu at %.3f: scan %.3f sigs %.3f (%.1f MB) ids %.3f arena %.3f (%.1f MB) ms\n",
+              (unsigned long long)k, h0, h1 - h0, h2 - h1, sizeof(cg_txsig) * cnt / 1e6, h3 - h2, ms_since() - h3,
+              ek.empty() ? 0.0 : (ek.hi - ek.lo) / 1e6);
     return e;
   };
   // The key-use counts gate only the key tables; chunk 0's bytes gate everything else. With
@@ -1261,6 +1291,8 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   cg::KeyUses uses;
   uses.counts = (const uint32_t*)c->aux1.p;
   uses.n = n_sigs;
+  uses.host_keys = keys;
+  uses.host_counts = counts.data();
   const hipError_t le = launch_txsig(c, (const cg_key*)c->keys.p, n_keys, (const uint8_t*)c->h_ids.p, n_ids,
                                      (const cg_txsig*)c->h_sigs.p, n_sigs, tmpls, n_tmpls, dbase, arena_len, mode, ds,
                                      s, slot, uses, &before, &bounds);
@@ -1270,7 +1302,20 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   HIP_TRY(hipMemcpyAsync(status_out, ds, n_sigs, hipMemcpyDeviceToHost, s), "D2H status");
   HIP_TRY(hipEventRecord(c->tev[3], s), "hipEventRecord");
   HIP_TRY(order_out(c, s), "hipEventRecord");
+  const double h_enq = htrace ? ms_since() : 0;
   HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (htrace) {
+    fprintf(stderr, "[cg host] enqueued at %.3f, done at %.3f ms; copies landed (device ms after the call's first event):",
+            h_enq, ms_since());
+    for (uint64_t k = 0; k < nch && k < c->segt.size(); ++k) {
+      float t = 0;
+      hipEventElapsedTime(&t, c->tev[0], c->segt[k]);
+      fprintf(stderr, " %.3f", t);
+    }
+    float t = 0;
+    hipEventElapsedTime(&t, c->tev[0], c->tev[2]);
+    fprintf(stderr, "; verify done %.3f\n", t);
+  }
   if (stats) {
     float a = 0, b = 0, d = 0;
     hipEventElapsedTime(&a, c->tev[0], c->tev[1]);

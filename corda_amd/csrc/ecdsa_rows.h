@@ -16,9 +16,11 @@
 #include "ecdsa.h"
 
 #define EC_W 6
+#ifndef EC_WINDOWS  // windows per row; EC_ROWS = ceil(43 / EC_WINDOWS) (A/B builds: 11 and 4)
 #define EC_WINDOWS 4
+#endif
 #define EC_DIGITS 43
-#define EC_ROWS 11
+#define EC_ROWS ((EC_DIGITS + EC_WINDOWS - 1) / EC_WINDOWS)
 #define EC_MULT 32
 #define EC_PACKED 11
 
@@ -154,6 +156,66 @@ CG_HD void ec_multiples(EcAff* out, const Jac& first, const Jac& step, int cnt, 
 template <int C>
 CG_HD void ec_row_build(EcAff* row, const Jac& base, EcRowScratch& s, const EcConsts& K) {
   ec_multiples<C>(row, base, base, EC_MULT, s, K);
+}
+
+// Row builds for many keys at once (k_ec_keyprep_tab): ec_row_build with the walk's points and
+// running products parked lane-interleaved (dword d of field q of entry k at
+// base[(k * EC_ROW_PARK + 9 q + d) * lanes + lane]), so one store of a wave is 64 consecutive
+// dwords. The per-key EcRowScratch made every store and load of the two walks touch 64 cache
+// lines: the 2^20-distinct-key leg's row-0 builds took 52 / 28 ms per call (profiles/r04/kd).
+#define EC_ROW_PARK 36  // X, Y, Z and the running product: 4 x 9 limbs
+struct EcRowParkLanes {
+  uint32_t* base;
+  uint32_t lane, lanes;
+  CG_HDM void st(int k, int q, const f29& f) const {
+    uint32_t* p = base + (size_t)(k * EC_ROW_PARK + q * 9) * lanes + lane;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) p[(size_t)d * lanes] = f.v[d];
+  }
+  CG_HDM void ld(int k, int q, f29& f) const {
+    const uint32_t* p = base + (size_t)(k * EC_ROW_PARK + q * 9) * lanes + lane;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) f.v[d] = p[(size_t)d * lanes];
+  }
+};
+template <int C>
+CG_HD void ec_row_build_parked(EcAff* row, const Jac& base, const EcRowParkLanes& pk, const EcConsts& K) {
+  Jac acc = base;
+  f29 run = acc.Z;
+  pk.st(0, 0, acc.X);
+  pk.st(0, 1, acc.Y);
+  pk.st(0, 2, acc.Z);
+  pk.st(0, 3, run);
+#pragma unroll 1
+  for (int k = 1; k < EC_MULT; ++k) {
+    jac_add<C>(acc, acc, base, K);  // k = 1: acc == base goes through the doubling branch
+    m29_mul<C, 0>(run, run, acc.Z);
+    pk.st(k, 0, acc.X);
+    pk.st(k, 1, acc.Y);
+    pk.st(k, 2, acc.Z);
+    pk.st(k, 3, run);
+  }
+  f29 inv;
+  m29_inv<C, 0>(inv, run, K.one_p);
+#pragma unroll 1
+  for (int k = EC_MULT - 1; k >= 0; --k) {
+    f29 X, Y, zi, zi2, zi3;
+    pk.ld(k, 0, X);
+    pk.ld(k, 1, Y);
+    if (k > 0) {
+      f29 pr, Z;
+      pk.ld(k - 1, 3, pr);
+      pk.ld(k, 2, Z);
+      m29_mul<C, 0>(zi, inv, pr);
+      m29_mul<C, 0>(inv, inv, Z);
+    } else {
+      zi = inv;
+    }
+    m29_sq<C, 0>(zi2, zi);
+    m29_mul<C, 0>(zi3, zi2, zi);
+    m29_mul<C, 0>(row[k].x, X, zi2);
+    m29_mul<C, 0>(row[k].y, Y, zi3);
+  }
 }
 
 // The 11 row bases 2^{24j} P of an affine (Montgomery) point.

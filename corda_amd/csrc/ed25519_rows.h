@@ -17,7 +17,9 @@
 // 2 windows (22 rows x 32 multiples per key, 6 doublings per item), B in signed radix 2^10
 // over a constant table (26 rows x 512).
 #define ED_W 6
+#ifndef ED_K  // windows per row (A/B builds: 11 gives 4 rows and 60 doublings per item)
 #define ED_K 2
+#endif
 #ifndef ED_WB
 #define ED_WB 10
 #endif
@@ -742,6 +744,54 @@ CG_HD void ed_wide_row_build(Out* out, const Park& pk, const ge_p3& P, int e0, i
     Z = Zn;
     pr = prn;
 #endif
+  }
+}
+
+// Full / row-0 row of plain niels multiples 1..M of P (ed_row_build's entries) with the walk parked
+// in `pk` (EdParkLanes: lane-interleaved, so a wave's stores are coalesced; ed_row_build parks in
+// the row's own entries, 64 cache lines per store of a wave: the 2^20-distinct-key leg's row-0
+// builds took 108 ms per call, profiles/r04/kd). k_ed_keyprep_tab's form.
+template <int M, class Park>
+CG_HD void ed_row_build_parked(ge_niels* row, const ge_p3& P, const fe& d2, const Park& pk) {
+  ge_cached c;
+  ge_p3_to_cached(c, P, d2);
+  ge_p3 R = P;
+  fe run;
+  fe_copy(run, R.Z);
+  pk.put(0, R.X, R.Y, R.Z, run);
+#pragma unroll 1
+  for (int k = 1; k < M; ++k) {
+    ge_p1p1 t;
+    ge_add_cached(t, R, c);
+    ge_p1p1_to_p3(R, t);
+    fe_mul(run, run, R.Z);
+    pk.put(k, R.X, R.Y, R.Z, run);
+  }
+  fe inv;
+  fe_invert(inv, run);
+#pragma unroll 1
+  for (int k = M - 1; k >= 0; --k) {
+    fe X, Y, Z, zi;
+    pk.get(k, X, Y, Z);
+    if (k > 0) {
+      fe pr;
+      pk.get_run(k - 1, pr);
+      fe_mul(zi, inv, pr);
+      fe_mul(inv, inv, Z);
+    } else {
+      fe_copy(zi, inv);
+    }
+    fe x, y, xy;
+    ge_niels n;
+    fe_mul(x, X, zi);
+    fe_mul(y, Y, zi);
+    fe_add(n.ypx, y, x);
+    fe_carry(n.ypx);
+    fe_sub(n.ymx, y, x);
+    fe_carry(n.ymx);
+    fe_mul(xy, x, y);
+    fe_mul(n.xy2d, xy, d2);
+    row[k] = n;
   }
 }
 

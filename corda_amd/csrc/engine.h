@@ -84,6 +84,10 @@ struct PendingTabs {
   uint32_t n_keys = 0;
   void* keyprep = nullptr;
   WidePool wide;
+  // per side stream (0 r1, 1 k1, 2 Ed25519): whether any key of the family gets row-0 / full
+  // tables; false only when the host counts prove none does (KeyUses::host_counts), so the
+  // near-empty table launch does not queue behind the wide builds for a slot
+  bool need_full[3] = {true, true, true};
 };
 
 struct Fork {
@@ -138,6 +142,10 @@ struct KeyUses {
   const cg_txsig* sigs = nullptr;
   const uint32_t* counts = nullptr;
   uint64_t n = 0;  // signatures the counts cover (sizes the wide pools)
+  // optional host copies of the key table and of `counts` (the host-buffer tx-signature path): the
+  // host then knows, as k_key_classify will, which families need row-0 / full tables
+  const cg_key* host_keys = nullptr;
+  const uint32_t* host_counts = nullptr;
 };
 // With `d_items` (or `src`), each key's table is sized by the number of items that use it
 // (keyws.h); with neither (cg_prepare_keys_device), every key gets full tables.

@@ -139,10 +139,7 @@ __device__ __forceinline__ uint64_t item_msg_len(const cg_item& it, uint64_t are
 typedef EdRowsCfg<ED_W, ED_K> EdCfg;
 typedef EdRowTabW<ED_W, ED_K> EdTab;  // 22 x 32 affine niels = 84480 B
 // base slots per key, one stride for both schemes (Ed25519 rows >= ECDSA rows)
-#define KEY_BASES EdCfg::kRows
-static_assert(KEY_BASES >= EC_ROWS, "ECDSA row bases fit a key's base slots");
-static_assert(EdCfg::kRows * EdCfg::kMult * sizeof(fe) <= EC_ROWS * sizeof(EcRowScratch),
-              "Ed25519 row-build Z prefixes live in the key's ECDSA scratch");
+#define KEY_BASES (EdCfg::kRows > EC_ROWS ? EdCfg::kRows : EC_ROWS)
 typedef EdBCfg<ED_W, ED_K, ED_WB> EdBCfgT;
 typedef EdBTabW<ED_W, ED_K, ED_WB> EdBTab;  // 26 x 512 affine niels = 1.6 MB, constant
 
@@ -186,20 +183,34 @@ __device__ __forceinline__ int plan_class_of_curve(int curve) { return curve == 
 //   hdr      EdKeyHdr (status [+ Abyte])                       64 B
 //   tab      EdTab | EcRowTab                                  84 480 B
 //   bases    KEY_BASES = 22 x (ge_p3 | Jac)                    3 520 B
-//   ecs      11 x EcRowScratch (ECDSA batch-inversion scratch;  50 688 B
-//            an Ed25519 key's row-build Z prefixes)
+// and, per family, the full / row-0 builds' park (ed_row_build_parked / ec_row_build_parked): one
+// lane-interleaved region of min(n_keys x rows, TAB_PARK_LANES) lanes, the build kernels' grid
+// (each lane loops over the compacted (key, row) tasks), 5 120 B (Ed25519) / 4 608 B (ECDSA) a lane.
 static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+#define TAB_PARK_LANES 131072u  // 2 waves per SIMD on 1024 SIMDs
+static inline uint32_t tab_park_lanes(uint32_t n_keys, uint32_t rows) {
+  uint64_t l = (uint64_t)(n_keys ? n_keys : 1) * rows;
+  if (l > TAB_PARK_LANES) l = TAB_PARK_LANES;
+  return (uint32_t)((l + 63) & ~(uint64_t)63);
+}
+#define ED_ROW_PARK_BYTES ((size_t)EdCfg::kMult * ED_PARK_DWORDS * 4)
+#define EC_ROW_PARK_BYTES ((size_t)EC_MULT * EC_ROW_PARK * 4)
+#define ROW0_COUNT_AT 8  // row0_count = full_count + 8 (the 256-B count block)
 struct KeyWs {
   EdKeyHdr* hdr;
   TabSlot* tab;
   BaseSlot* bases;
-  EcRowScratch* ecs;
+  uint32_t* park_ed;     // full / row-0 build park, Ed25519 (park_lanes_ed lanes)
+  uint32_t* park_ec[2];  // [CG_CURVE_K1], [CG_CURVE_R1] (park_lanes_ec lanes each)
+  uint32_t park_lanes_ed, park_lanes_ec;
   uint32_t* uses;  // items per key in this batch, saturating at >= ED_DIRECT_MAX_USES
                    // (KEY_USES_ALL: unknown -> full tables)
   uint32_t* full;  // per scheme class c (PLAN_ED / PLAN_R1 / PLAN_K1): the keys that get full
                    // tables, full[c * n_keys + l] for l < full_count[c] (any order), so the
                    // chain / row kernels run dense lanes however few keys are hot
   uint32_t* full_count;
+  uint32_t* row0;        // per class c: every used key without wide tables (its row 0 is built),
+  uint32_t* row0_count;  // row0[c * n_keys + l] for l < row0_count[c] (= full_count + ROW0_COUNT_AT)
   uint8_t* seen;   // 1 if any item of the batch uses the key (exact; uses is sampled)
   uint32_t* wide_idx;    // per key: its slot in the scheme's wide pool, or KEY_NOT_WIDE
   uint32_t* wide;        // per class c: the keys with wide tables, wide[c * n_keys + l]
@@ -297,14 +308,23 @@ static inline KeyWs key_ws(void* base, uint32_t n_keys, const WidePool* wp = nul
   p += al256(n * sizeof(TabSlot));
   w.bases = (BaseSlot*)p;
   p += al256(n * KEY_BASES * sizeof(BaseSlot));
-  w.ecs = (EcRowScratch*)p;
-  p += n * EC_ROWS * sizeof(EcRowScratch);
+  w.park_lanes_ed = tab_park_lanes(n_keys, EdCfg::kRows);
+  w.park_lanes_ec = tab_park_lanes(n_keys, EC_ROWS);
+  w.park_ed = (uint32_t*)p;
+  p += al256(w.park_lanes_ed * ED_ROW_PARK_BYTES);
+  for (int c = 0; c < 2; ++c) {
+    w.park_ec[c] = (uint32_t*)p;
+    p += al256(w.park_lanes_ec * EC_ROW_PARK_BYTES);
+  }
   w.uses = (uint32_t*)p;
   p += al256(n * sizeof(uint32_t));
   w.full = (uint32_t*)p;
   p += al256(3 * n * sizeof(uint32_t));
   w.full_count = (uint32_t*)p;
+  w.row0_count = w.full_count + ROW0_COUNT_AT;
   p += 256;
+  w.row0 = (uint32_t*)p;
+  p += al256(3 * n * sizeof(uint32_t));
   w.seen = p;
   p += al256(n);
   w.wide_idx = (uint32_t*)p;
@@ -323,8 +343,10 @@ static inline KeyWs key_ws(void* base, uint32_t n_keys, const WidePool* wp = nul
 static inline size_t key_ws_bytes(uint32_t n_keys) {
   const size_t n = n_keys ? n_keys : 1;
   return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(TabSlot)) + al256(n * KEY_BASES * sizeof(BaseSlot)) +
-         n * EC_ROWS * sizeof(EcRowScratch) + al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256 +
-         al256(n) + al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256;
+         al256(tab_park_lanes(n_keys, EdCfg::kRows) * ED_ROW_PARK_BYTES) +
+         2 * al256(tab_park_lanes(n_keys, EC_ROWS) * EC_ROW_PARK_BYTES) + al256(n * sizeof(uint32_t)) +
+         al256(3 * n * sizeof(uint32_t)) + 256 + al256(3 * n * sizeof(uint32_t)) + al256(n) +
+         al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256;
 }
 
 // Per-item workspace slot (indexed by plan position, so the schemes never share one):

@@ -34,7 +34,7 @@ __global__ void __launch_bounds__(256) k_key_init(uint32_t n_keys, uint32_t all,
                                                   uint8_t* __restrict__ seen, uint32_t* __restrict__ full_count,
                                                   uint32_t* __restrict__ wide_idx, uint32_t* __restrict__ wide_count) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < PLAN_CLASSES) full_count[i] = 0;
+  if (i < PLAN_CLASSES) full_count[i] = full_count[ROW0_COUNT_AT + i] = 0;
   if (i < PLAN_CLASSES + 2) wide_count[i] = 0;
   if (i >= n_keys) return;
   uses[i] = all ? KEY_USES_ALL : 0u;
@@ -101,10 +101,11 @@ __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ 
                                                      uint32_t* __restrict__ uses, const uint8_t* __restrict__ seen,
                                                      uint32_t* __restrict__ full, uint32_t* __restrict__ full_count,
                                                      uint32_t* __restrict__ wide_idx, uint32_t* __restrict__ wide,
-                                                     uint32_t* __restrict__ wide_count, uint32_t cap_ed,
-                                                     uint32_t cap_ec, uint32_t min_ed, uint32_t min_ec) {
+                                                     uint32_t* __restrict__ wide_count, uint32_t* __restrict__ row0,
+                                                     uint32_t cap_ed, uint32_t cap_ec, uint32_t min_ed,
+                                                     uint32_t min_ec) {
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  int c = -1, cw = -1;
+  int c = -1, cw = -1, c0 = -1;  // full list, wide list, row-0 list
   uint32_t u = 0;
   if (i < n_keys) {  // the estimate, made exact where it matters: a used key counts >= 1
     u = uses[i];
@@ -132,8 +133,16 @@ __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ 
       }
     }
   }
+  if (i < n_keys && u >= 1 && cw < 0) {  // every used key without wide tables gets its row 0
+    const uint8_t s = keys[i].scheme;
+    c0 = s == CG_EDDSA_ED25519_SHA512 ? PLAN_ED
+       : s == CG_ECDSA_SECP256R1_SHA256 ? PLAN_R1
+       : s == CG_ECDSA_SECP256K1_SHA256 ? PLAN_K1
+                                        : -1;
+  }
   list_append(c, i, n_keys, full, full_count);
   list_append(cw, i, n_keys, wide, wide_count);
+  list_append(c0, i, n_keys, row0, full_count + ROW0_COUNT_AT);
 }
 
 hipError_t upload_constants() {
@@ -188,7 +197,7 @@ static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
   // then the full / row-0 tables (usually few keys: launched ahead of the wide builds, their
   // near-empty grids queued behind the challenge hashes, which hold every SIMD, and stalled the
   // wide builds behind them by ~1.8 ms per call: profiles/r02/sha_v2/timeline_step.txt)
-  ed_launch_keyprep_tabs(p.keys, p.n_keys, w, fork->side[2], true, false);
+  if (p.need_full[2]) ed_launch_keyprep_tabs(p.keys, p.n_keys, w, fork->side[2], true, false);
   if (e == hipSuccess) e = hipEventRecord(fork->ready[2], fork->side[2]);
   // the curves' wide builds right after their own row-base chains, beside the Ed25519 builds, so
   // that they are done before the first chunk's fronts (after the Ed25519 builds, they ran 5.8 ->
@@ -203,7 +212,8 @@ static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
     if (e == hipSuccess && !concurrent) e = hipStreamWaitEvent(fork->side[k], fork->ed_tabs, 0);
     if (e != hipSuccess) break;
     ec_launch_keyprep_tabs(k == 0 ? CG_CURVE_R1 : CG_CURVE_K1, p.keys, p.n_keys, w, fork->side[k], false, true);
-    ec_launch_keyprep_tabs(k == 0 ? CG_CURVE_R1 : CG_CURVE_K1, p.keys, p.n_keys, w, fork->side[k], true, false);
+    if (p.need_full[k])
+      ec_launch_keyprep_tabs(k == 0 ? CG_CURVE_R1 : CG_CURVE_K1, p.keys, p.n_keys, w, fork->side[k], true, false);
     e = hipEventRecord(fork->ready[k], fork->side[k]);
   }
   return e;
@@ -211,6 +221,27 @@ static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
 
 hipError_t launch_key_tables(const Fork* fork, hipStream_t stream) {
   return fork ? launch_pending_tabs(fork, stream) : hipSuccess;
+}
+
+// k_key_classify's outcome from the host counts: does any key of family f (0 r1, 1 k1, 2 Ed25519)
+// end in row-0 or full-table mode? Mirrors the kernel (a counted key has u >= 1; wide when u >=
+// max(ED_DIRECT_MAX_USES, the pool's minimum) and the pool's slots hold every such key).
+static void families_needing_full(const KeyUses& src, uint32_t n_keys, const KeyWs& w, bool need[3]) {
+  uint32_t hot[2] = {0, 0};  // keys asking for a wide slot, per pool (0 Ed25519, 1 ECDSA)
+  bool low[3] = {false, false, false};
+  for (uint32_t i = 0; i < n_keys; ++i) {
+    const uint32_t u = src.host_counts[i];
+    if (u == 0) continue;
+    const uint8_t s = src.host_keys[i].scheme;
+    const int f = s == CG_ECDSA_SECP256R1_SHA256 ? 0 : s == CG_ECDSA_SECP256K1_SHA256 ? 1 : s == CG_EDDSA_ED25519_SHA512 ? 2 : -1;
+    if (f < 0) continue;
+    const int pool = f == 2 ? 0 : 1;
+    const uint32_t cap = pool == 0 ? w.cap_ed : w.cap_ec;
+    if (u >= ED_DIRECT_MAX_USES && u >= (pool == 0 ? w.min_ed : w.min_ec) && u != KEY_USES_ALL && cap) ++hot[pool];
+    else low[f] = true;
+  }
+  const bool over[2] = {hot[0] > w.cap_ed, hot[1] > w.cap_ec};
+  for (int f = 0; f < 3; ++f) need[f] = low[f] || over[f == 2 ? 0 : 1];
 }
 
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
@@ -234,8 +265,8 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
     hipLaunchKernelGGL(k_key_uses_txsig, dim3((unsigned)((src->n + 255) / 256)), dim3(256), 0, stream, src->sigs,
                        src->n, n_keys, w.uses, w.seen);
   hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys, w.uses,
-                     (const uint8_t*)w.seen, w.full, w.full_count, w.wide_idx, w.wide, w.wide_count, w.cap_ed,
-                     w.cap_ec, w.min_ed, w.min_ec);
+                     (const uint8_t*)w.seen, w.full, w.full_count, w.wide_idx, w.wide, w.wide_count, w.row0,
+                     w.cap_ed, w.cap_ec, w.min_ed, w.min_ec);
   static const bool serial = [] {  // CG_SERIAL_KEYPREP=1: key prep on the caller's stream (A/B runs)
     const char* v = getenv("CG_SERIAL_KEYPREP");
     return v && v[0] == '1';
@@ -277,6 +308,13 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   fork->pending.n_keys = n_keys;
   fork->pending.keyprep = d_keyprep;
   fork->pending.wide = counted && wide ? *wide : WidePool{};
+  for (int f = 0; f < 3; ++f) fork->pending.need_full[f] = true;
+  static const bool skip_full = [] {  // CG_SKIP_EMPTY_TABS=0: always launch the row-0 / full builds (A/B)
+    const char* v = getenv("CG_SKIP_EMPTY_TABS");
+    return !(v && v[0] == '0');
+  }();
+  if (skip_full && !d_items && src && src->counts && src->host_counts && src->host_keys)
+    families_needing_full(*src, n_keys, w, fork->pending.need_full);
   if (!counted) e = launch_pending_tabs(fork, stream);
   if (e != hipSuccess) return e;
   // the only key work on the main stream: Abyte for k_ed_hash (no decode)

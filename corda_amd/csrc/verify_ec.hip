@@ -62,34 +62,36 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_chain(uint32_t n_keys, const 
   }
 }
 
-// Lanes g < n_keys: row 0 of key g (every key of this curve with items); then row-major
-// (row j >= 1, position l of the curve's full-table list): only hot keys' rows 1..10 run.
+// The 32 affine multiples of a row base (ec_row_build_parked), for the compacted tasks: row 0 of
+// every used key of this curve without wide tables, then rows 1..10 of its full-table keys; a grid
+// of `lanes` lanes looping over the tasks, each parked in its own column (as k_ed_keyprep_tab).
 template <int C>
-__global__ void __launch_bounds__(64) k_ec_keyprep_tab(const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                       const EdKeyHdr* __restrict__ hdr,
+__global__ void __launch_bounds__(64) k_ec_keyprep_tab(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                        const BaseSlot* __restrict__ bases,
-                                                       const uint32_t* __restrict__ uses,
+                                                       const uint32_t* __restrict__ row0,
                                                        const uint32_t* __restrict__ full,
                                                        const uint32_t* __restrict__ full_count,
-                                                       const uint32_t* __restrict__ wide_idx,
-                                                       TabSlot* __restrict__ tabs, EcRowScratch* __restrict__ scratch) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                       TabSlot* __restrict__ tabs, uint32_t* __restrict__ park,
+                                                       uint32_t lanes) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= lanes) return;
   const int c = plan_class_of_curve(C);
-  uint32_t i, j;
-  if (g < n_keys) {
-    i = (uint32_t)g;
-    j = 0;
-    // a wide key's items run only the wide ladder: no row 0
-    if (keys[i].scheme != ec_scheme<C>() || uses[i] == 0 || wide_idx[i] != KEY_NOT_WIDE) return;
-  } else {
-    const uint64_t h = g - n_keys;
-    j = 1 + (uint32_t)(h / n_keys);
-    const uint32_t l = (uint32_t)(h % n_keys);
-    if (j >= (uint32_t)EC_ROWS || l >= full_count[c]) return;
-    i = full[(size_t)c * n_keys + l];
+  const uint32_t n0 = full_count[ROW0_COUNT_AT + c], nf = full_count[c];
+  const uint64_t tasks = n0 + (uint64_t)nf * (EC_ROWS - 1);
+  const EcRowParkLanes pk{park, p, lanes};
+  for (uint64_t t = p; t < tasks; t += lanes) {
+    uint32_t i, j;
+    if (t < n0) {
+      i = row0[(size_t)c * n_keys + t];
+      j = 0;
+    } else {
+      const uint64_t h = t - n0;
+      j = 1 + (uint32_t)(h / nf);
+      i = full[(size_t)c * n_keys + h % nf];
+    }
+    if (hdr[i].status != 0) continue;
+    ec_row_build_parked<C>(tabs[i].ec.t[j], bases[(size_t)i * KEY_BASES + j].ec, pk, c_ec[C]);
   }
-  if (hdr[i].status != 0) return;
-  ec_row_build<C>(tabs[i].ec.t[j], bases[(size_t)i * KEY_BASES + j].ec, scratch[(size_t)i * EC_ROWS + j], c_ec[C]);
 }
 
 // Wide tables (ecdsa_rows.h): one lane per wide key of this curve, the 32 row bases 2^{8j} Q
@@ -478,11 +480,10 @@ template <int C>
 static void launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream, bool full,
                                 bool wide) {
   const uint32_t B = 64;
-  const uint64_t elanes = (uint64_t)n_keys * EC_ROWS;
   if (full)
-    hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3((unsigned)((elanes + B - 1) / B)), dim3(B), 0, stream, d_keys,
-                       n_keys, w.hdr, w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full,
-                       (const uint32_t*)w.full_count, (const uint32_t*)w.wide_idx, w.tab, w.ecs);
+    hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3(w.park_lanes_ec / B), dim3(B), 0, stream, n_keys, w.hdr, w.bases,
+                       (const uint32_t*)w.row0, (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.tab,
+                       w.park_ec[C], w.park_lanes_ec);
   if (wide && w.cap_ec) {
     const uint64_t gl = (uint64_t)w.cap_ec * EC_WIDE_ROWS * EC_WIDE_GROUPS, rl = (uint64_t)w.cap_ec * EC_WIDE_ROWS;
     const uint32_t* wl = (const uint32_t*)w.wide;

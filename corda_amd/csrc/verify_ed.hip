@@ -115,35 +115,39 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_chain(uint32_t n_keys, const 
   }
 }
 
-// the 32 affine multiples of a row base, one inversion per row (ed_row_build; Z prefixes in the
-// key's ECDSA scratch, unused by an Ed25519 key). Lanes g < n_keys: row 0 of key g (every key
-// with items); then row-major (row j >= 1, position l of the full-table list), so only hot keys'
-// rows 1..21 run, on dense lanes.
-__global__ void __launch_bounds__(64) k_ed_keyprep_tab(const cg_key* __restrict__ keys, uint32_t n_keys,
-                                                       const EdKeyHdr* __restrict__ hdr,
+// The 32 affine multiples of a row base, one inversion per row (ed_row_build_parked), for the
+// compacted tasks: row 0 of every used key without wide tables (row0 list), then rows 1..21 of the
+// full-table keys (full list). A grid of `lanes` lanes (keyws.h tab_park_lanes), each looping over
+// tasks lane, lane + lanes, ... with its walk parked in its own lane-interleaved column of `park`.
+#ifndef ED_TAB_WAVES  // waves per SIMD the row builds' registers must allow (255 VGPRs + 56 AGPRs left 1)
+#define ED_TAB_WAVES 2
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ED_TAB_WAVES)))
+k_ed_keyprep_tab(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                        const BaseSlot* __restrict__ bases,
-                                                       const uint32_t* __restrict__ uses,
+                                                       const uint32_t* __restrict__ row0,
                                                        const uint32_t* __restrict__ full,
                                                        const uint32_t* __restrict__ full_count,
-                                                       const uint32_t* __restrict__ wide_idx,
-                                                       TabSlot* __restrict__ tabs, EcRowScratch* __restrict__ ecs) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t i, j;
-  if (g < n_keys) {
-    i = (uint32_t)g;
-    j = 0;
-    // a wide key's items run only the wide ladder: no row 0
-    if (keys[i].scheme != CG_EDDSA_ED25519_SHA512 || uses[i] == 0 || wide_idx[i] != KEY_NOT_WIDE) return;
-  } else {
-    const uint64_t h = g - n_keys;
-    j = 1 + (uint32_t)(h / n_keys);
-    const uint32_t l = (uint32_t)(h % n_keys);
-    if (j >= (uint32_t)EdCfg::kRows || l >= full_count[PLAN_ED]) return;
-    i = full[(size_t)PLAN_ED * n_keys + l];
+                                                       TabSlot* __restrict__ tabs, uint32_t* __restrict__ park,
+                                                       uint32_t lanes) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= lanes) return;
+  const uint32_t n0 = full_count[ROW0_COUNT_AT + PLAN_ED], nf = full_count[PLAN_ED];
+  const uint64_t tasks = n0 + (uint64_t)nf * (EdCfg::kRows - 1);
+  const EdParkLanes pk{park, p, lanes};
+  for (uint64_t t = p; t < tasks; t += lanes) {
+    uint32_t i, j;
+    if (t < n0) {
+      i = row0[(size_t)PLAN_ED * n_keys + t];
+      j = 0;
+    } else {
+      const uint64_t h = t - n0;
+      j = 1 + (uint32_t)(h / nf);
+      i = full[(size_t)PLAN_ED * n_keys + h % nf];
+    }
+    if (hdr[i].status != 0) continue;
+    ed_row_build_parked<EdCfg::kMult>(tabs[i].ed.t[j], bases[(size_t)i * KEY_BASES + j].ed, c_ed.d2, pk);
   }
-  if (hdr[i].status != 0) return;
-  fe* zpre = (fe*)(ecs + (size_t)i * EC_ROWS) + (size_t)j * EdCfg::kMult;
-  ed_row_build<EdCfg::kMult>(tabs[i].ed.t[j], bases[(size_t)i * KEY_BASES + j].ed, c_ed.d2, zpre);
 }
 
 // Wide tables (ed25519_rows.h): one lane per wide key, the 32 row bases 2^{8j} (-A) (a chain of
@@ -466,7 +470,12 @@ struct EdOps {
   static constexpr int kOps = kNa1 + kNa0 + EdWideCfg::kBDigits;
   static constexpr uint32_t kWaveBytes = 64 * sizeof(ge_niels);
 };
+#ifndef ED_LADDER_PF  // -DED_LADDER_PF=0: the unpipelined full-table ladder (A/B; any ED_K)
+#define ED_LADDER_PF 1
+#endif
+#if ED_LADDER_PF
 static_assert(ED_K == 2, "the flat op sequence is written for 2 windows");
+#endif
 static_assert(sizeof(ge_niels) == 120, "LDS chunking assumes 120-B niels entries");
 
 // op o -> (digit word index in EdDigits, shift, B?, row)
@@ -553,6 +562,7 @@ __device__ __forceinline__ const ge9_niels* ed_b_src(const EdBWideTab& TB, int r
 
 // The 55 A additions in radix 2^25.5 (full-table entries), then the 12 B additions in radix 2^29
 // (fe9.h, the wide B table's entry form), one entry gathered into LDS one op ahead throughout.
+#if ED_LADDER_PF
 __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* __restrict__ dw, const EdTab& TA,
                                                     const EdBWideTab& TB, uint8_t* wave_lds, uint32_t lane) {
   constexpr int N = EdOps::kOps, NA = EdOps::kNa1 + EdOps::kNa0;
@@ -618,17 +628,16 @@ __device__ __forceinline__ void ed_double_scalar_pf(ge_p2& out, const uint32_t* 
   ge9_to_p2(out, R9);
 }
 
+#endif
 // A/B on one box (gpurun_out/ab_sw1, profiles/r01/ed25519_v9): the pipelined ladder at 2
 // waves/SIMD (216 VGPRs, no scratch) against k_ed_ladder<true> at 3 waves/SIMD (168 VGPRs,
 // digits and spills in scratch): item kernels 4.24 vs 4.28 ms per 2^20 items. The gain is
 // small because the ladder is VALU-issue-bound, not latency-bound.
 // -DED_LADDER_PF=0 builds the unpipelined ladder for A/B runs (tools/ab.sh).
-#ifndef ED_LADDER_PF
-#define ED_LADDER_PF 1
-#endif
 #ifndef ED_LADDER_PF_WAVES
 #define ED_LADDER_PF_WAVES 2
 #endif
+#if ED_LADDER_PF
 __global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_pf(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
     const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBWideTab* __restrict__ btab,
@@ -653,6 +662,7 @@ __global__ void __launch_bounds__(256, ED_LADDER_PF_WAVES) k_ed_ladder_pf(
     ((ge_p2*)slots)[p] = q;
   }
 }
+#endif
 // ---------------------------------------------------------------- wide-table ladder
 // ed_double_scalar_wide as a flat sequence of 54 signed mixed additions (32 rows of the key's
 // wide table, then the 22 radix-2^12 B rows), no doublings; each op's entry gathered into LDS
@@ -881,11 +891,10 @@ void ed_launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const uint8
 void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& w, hipStream_t stream, bool full,
                             bool wide) {
   const uint32_t B = 64;
-  const uint64_t lanes = (uint64_t)n_keys * EdCfg::kRows;
   if (full)
-    hipLaunchKernelGGL(k_ed_keyprep_tab, dim3((unsigned)((lanes + B - 1) / B)), dim3(B), 0, stream, d_keys, n_keys,
-                       w.hdr, w.bases, (const uint32_t*)w.uses, (const uint32_t*)w.full, (const uint32_t*)w.full_count,
-                       (const uint32_t*)w.wide_idx, w.tab, w.ecs);
+    hipLaunchKernelGGL(k_ed_keyprep_tab, dim3(w.park_lanes_ed / B), dim3(B), 0, stream, n_keys, w.hdr, w.bases,
+                       (const uint32_t*)w.row0, (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.tab,
+                       w.park_ed, w.park_lanes_ed);
   if (wide && w.cap_ed) {
     const uint64_t gl = (uint64_t)w.cap_ed * EdWideCfg::kRows * ED_WIDE_GROUPS, rl = (uint64_t)w.cap_ed * EdWideCfg::kRows;
     const uint32_t* wl = (const uint32_t*)w.wide;
@@ -922,10 +931,13 @@ void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8
                       const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
   const unsigned grid = walk_grid(n_items, B, WALK_CAP(full && ED_LADDER_PF ? ED_LADDER_PF_WAVES : ED_LADDER_WAVES_PER_SIMD));
-  if (full && ED_LADDER_PF)
+#if ED_LADDER_PF
+  if (full)
     hipLaunchKernelGGL(k_ed_ladder_pf, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
                        w.tab, bwide(d_btab), d_status, iw.slots, iw.ed);
-  else if (full)
+  else
+#endif
+  if (full)
     hipLaunchKernelGGL(k_ed_ladder<true>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
                        w.tab, bwide(d_btab), d_status, iw.slots, iw.ed);
   else

@@ -1,3 +1,4 @@
+#include <type_traits>
 #include <vector>
 // Host build of the device lane code (corda_amd/csrc/*.h) with FE_BOUNDS_CHECK on, so the
 // exact arithmetic the HIP kernels run is checked on the CPU against the oracle and every
@@ -1074,4 +1075,50 @@ extern "C" int t_sha_splice_cmp(uint64_t seed, int n) {
     if (memcmp(h1, h2, sizeof h1)) ++bad;
   }
   return bad;
+}
+
+// k_ed_keyprep_tab / k_ec_keyprep_tab (ed_row_build_parked / ec_row_build_parked, lane-interleaved
+// park of 3 lanes, this lane = 1) against ed_row_build / ec_row_build for the row base m B / m G:
+// the number of entries that differ (byte-identical: the same field operations in the same order).
+extern "C" int t_row_parked_cmp(int family, uint32_t m) {
+  if (family == 2) {
+    init();
+    ge_p3 B, P;
+    fe x, y, two_inv, t;
+    fe_sub(x, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+    fe_add(y, g_C.Btab[1].ypx, g_C.Btab[1].ymx);
+    fe_0(t);
+    t.v[0] = 2;
+    fe_invert(two_inv, t);
+    fe_mul(B.X, x, two_inv);
+    fe_mul(B.Y, y, two_inv);
+    fe_1(B.Z);
+    fe_mul(B.T, B.X, B.Y);
+    ed_small_mul(P, B, m, g_C.d2);
+    static ge_niels a[(EdRowsCfg<ED_W, ED_K>::kMult)], b[(EdRowsCfg<ED_W, ED_K>::kMult)];
+    static fe zpre[(EdRowsCfg<ED_W, ED_K>::kMult)];
+    static uint32_t park[3 * (EdRowsCfg<ED_W, ED_K>::kMult) * ED_PARK_DWORDS];
+    ed_row_build<(EdRowsCfg<ED_W, ED_K>::kMult)>(a, P, g_C.d2, zpre);
+    ed_row_build_parked<(EdRowsCfg<ED_W, ED_K>::kMult)>(b, P, g_C.d2, EdParkLanes{park, 1u, 3u});
+    int bad = 0;
+    for (int k = 0; k < (EdRowsCfg<ED_W, ED_K>::kMult); ++k) bad += memcmp(&a[k], &b[k], sizeof a[k]) != 0;
+    return bad;
+  }
+  auto cmp = [&](auto tag) {
+    constexpr int C = decltype(tag)::value;
+    kinit();
+    const EcConsts& K = g_K[C];
+    Jac P;
+    jac_small_mul_aff<C>(P, K.gx, K.gy, m, K);
+    static EcAff a[EC_MULT], b[EC_MULT];
+    static EcRowScratch s;
+    static uint32_t park[3 * EC_MULT * EC_ROW_PARK];
+    ec_row_build<C>(a, P, s, K);
+    ec_row_build_parked<C>(b, P, EcRowParkLanes{park, 1u, 3u}, K);
+    int bad = 0;
+    for (int k = 0; k < EC_MULT; ++k) bad += memcmp(&a[k], &b[k], sizeof a[k]) != 0;
+    return bad;
+  };
+  return family == CG_CURVE_R1 ? cmp(std::integral_constant<int, CG_CURVE_R1>())
+                               : cmp(std::integral_constant<int, CG_CURVE_K1>());
 }

@@ -189,3 +189,22 @@ def test_tx_signatures_ecdsa_template_lengths():
     with Engine(0) as eng:
         st = eng.verify_tx_signatures(tb)
     assert np.array_equal(st, ref), f"{np.count_nonzero(st != ref)} differ"
+
+
+def test_tx_signatures_mixed_table_modes(spool):
+    """One family hot (every key wide, so the host counts skip its row-0 / full table builds) and
+    the other two cold (row-0 tables for unsampled keys, wide for sampled ones), for each family in
+    turn, through one host-buffer call each: verdicts equal the oracle's on the same pool items."""
+    from corda_amd.engine import Engine
+    from tools.workload import wl
+    b, labels, schemes, ids, id_idx, ref = spool
+    rng = np.random.default_rng(44)
+    with Engine(0) as eng:
+        for hot in (4, 3, 2):  # Ed25519, secp256r1, secp256k1 (Corda scheme numbers)
+            h, c = np.nonzero(schemes == hot)[0], np.nonzero(schemes != hot)[0]
+            idx = np.concatenate([rng.choice(h, 1_500_000), rng.choice(c, 30_000)])
+            rng.shuffle(idx)
+            tb = wl.tx_sig_stream(b, schemes, idx, ids, id_idx, nthreads=16)
+            st = eng.verify_tx_signatures(tb)
+            bad = np.nonzero(st != ref[idx])[0]
+            assert bad.size == 0, f"hot scheme {hot}: {bad.size} verdicts differ, first at {bad[:5]}"

@@ -496,3 +496,15 @@ def test_ec_madd9_matches_madd(curve):
     lib = hostk.lib()
     lib.t_ec_madd9_cmp.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
     assert lib.t_ec_madd9_cmp(curve, 777 + curve, 60, 60) == 0
+
+
+@pytest.mark.parametrize("family", [0, 1, 2])  # secp256k1, secp256r1, Ed25519
+def test_row_build_parked_matches_row_build(family):
+    """k_ed_keyprep_tab / k_ec_keyprep_tab's row build (the walk parked lane-interleaved in a shared
+    column, keyws.h tab_park_lanes) writes byte-identical entries to the in-row scratch build, for
+    several row bases, every product's bound asserted."""
+    import ctypes
+    lib = hostk.lib()
+    lib.t_row_parked_cmp.argtypes = [ctypes.c_int, ctypes.c_uint32]
+    for m in (1, 2, 3, 7, 255, 65537, 0x7fffffff):
+        assert lib.t_row_parked_cmp(family, m) == 0, m

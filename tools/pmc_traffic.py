@@ -1,6 +1,6 @@
 """Per-launch HBM traffic and VALU issue of the item kernels from rocprofv3 passes
 (tools/profile_r02.sh: --kernel-trace --stats, then --pmc FETCH_SIZE, --pmc WRITE_SIZE and an SQ pass,
-each its own process), written to profiles/r03/pmc_traffic.json for bench.py's roofline.
+each its own process), written to profiles/r04/pmc_traffic.json (PMC_TRAFFIC_FILE) for bench.py's roofline.
 
 HBM bytes (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE tallies 128-B requests at 64 B,
 so a wide streaming read reports half its bytes: hbm = 2*FETCH_SIZE + WRITE_SIZE (KB * 1024). The
@@ -138,9 +138,10 @@ def main():
            "valu_issue": {n: k["valu"] for n, k in kern.items() if "valu" in k}}
     with open(os.path.join(dest, "pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
-    if os.environ.get("PMC_TRAFFIC_HEADLINE", "1") == "1":  # the file bench.py's roofline reads
-        os.makedirs(os.path.join(ROOT, "profiles", "r03"), exist_ok=True)
-        with open(os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"), "w") as f:
+    if os.environ.get("PMC_TRAFFIC_HEADLINE", "1") == "1":  # the file bench.py's roofline reads (TRAFFIC_FILE)
+        head = os.path.join(ROOT, os.environ.get("PMC_TRAFFIC_FILE", "profiles/r04/pmc_traffic.json"))
+        os.makedirs(os.path.dirname(head), exist_ok=True)
+        with open(head, "w") as f:
             json.dump(out, f, indent=1)
     print(json.dumps({n: (k.get("hbm_bytes_per_launch"), k.get("valu", {}).get("issue_frac"),
                           k.get("trace", {}).get("avg_ms")) for n, k in kern.items()}))

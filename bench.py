@@ -82,8 +82,9 @@ MAC32_EXEC_PER_ED25519 = ED_VERIFY_FE9 * MAC_PER_MUL9 + ((ED_VERIFY_FE[0] + ED_F
 # SIMD executes (per-item mean 1% lower).
 EC_LADDER_MUL = {"secp256r1": 741, "secp256k1": 723}
 EC_WIDE_MUL = {"secp256r1": 476, "secp256k1": 476}  # k_ec_ladder_wide: 32 + 12 mixed additions + x-check
-# table modes (corda_amd/csrc/keyws.h): full tables from 32 items per key, wide from 384
-KEY_FULL_MIN_USES, KEY_WIDE_MAX = 32, 8192
+# table modes (corda_amd/csrc/keyws.h): quarter tables from 3 items per key, full from 32, wide from
+# KEY_WIDE_MIN_USES (1536 Ed25519 / 512 ECDSA)
+KEY_QUARTER_MIN_USES, KEY_FULL_MIN_USES, KEY_WIDE_MAX = 3, 32, 8192  # keyws.h
 KEY_WIDE_MIN_USES = {4: int(os.environ.get("CG_WIDE_MIN_USES_ED", 1536)), 3: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512)),
                      2: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512))}
 EC_INV_K = 8  # items per k_ec_inv lane (corda_amd/csrc/ecdsa_rows.h)
@@ -740,15 +741,17 @@ def bench_device(eng, dev, stream, b, tb, st_ref, steps):
 
 
 def table_modes(b, schemes):
-    """Items per key-table mode (keyws.h thresholds on the exact use counts): row 0 (< 32 uses),
-    full (32 .. wide threshold), wide (>= 1536 Ed25519 / 512 ECDSA uses, up to the pool cap)."""
+    """Items per key-table mode (keyws.h thresholds on the exact use counts): row 0 (< 3 uses),
+    quarter (3 .. 31), full (32 .. wide threshold), wide (>= 1536 Ed25519 / 512 ECDSA uses, up to
+    the pool cap). The library decides on its own (sampled) counts, so this is the intended split."""
     uses = np.bincount(b.items["key_idx"], minlength=len(b.keys))
     thr = np.array([KEY_WIDE_MIN_USES.get(int(s), 1 << 30) for s in b.keys["scheme"]])
     ku = uses[b.items["key_idx"]]
     kt = thr[b.items["key_idx"]]
     out = {}
     for name, sel in (("ed25519", schemes == 4), ("secp256r1", schemes == 3), ("secp256k1", schemes == 2)):
-        out[name] = {"row0": int((sel & (ku < KEY_FULL_MIN_USES)).sum()),
+        out[name] = {"row0": int((sel & (ku < KEY_QUARTER_MIN_USES)).sum()),
+                     "quarter": int((sel & (ku >= KEY_QUARTER_MIN_USES) & (ku < KEY_FULL_MIN_USES)).sum()),
                      "full": int((sel & (ku >= KEY_FULL_MIN_USES) & (ku < kt)).sum()),
                      "wide": int((sel & (ku >= kt)).sum())}
     out["keys_used"] = int((uses > 0).sum())

@@ -103,6 +103,10 @@ struct cg_ctx {
   // the tx-signature host path's second copy stream (chunk 0's bytes while the key-use counts are
   // sampled) and a pinned buffer for those counts (a pinned copy does not queue behind a pageable one)
   hipStream_t copy2 = nullptr;
+  // the exact key-use count (many keys): per host thread a byte counter per key (a wrap to 0 logs
+  // the key in ovf: +256), kept across calls so a call does not page-fault 16 fresh arrays in
+  std::vector<std::vector<uint8_t>> cnt8;
+  std::vector<std::vector<uint32_t>> ovf;
   uint32_t* pin_counts = nullptr;
   size_t pin_counts_cap = 0;
   std::vector<hipEvent_t> seg;
@@ -1084,7 +1088,11 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
       const uint32_t x = v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
       return x && (x & (x - 1)) == 0 ? x : 0u;
     }();
-    const uint32_t S = S_env ? S_env : n_sigs >= 256ull * (n_keys ? n_keys : 1) ? CG_TXSIG_COUNT_SAMPLE : 8u;
+    // Round 4: 1 (exact counts) instead of 1 in 8 when keys are many. With the quarter mode from 3
+    // uses, an unsampled key (unused, or used a few times) could not be given a mode: row 0 for all
+    // of them left ~20% of the 2^20-distinct-key leg's keys (12 uses) on the Horner ladder, quarter
+    // tables for all of them built tables for the Zipf leg's ~900k unused keys (125 -> 108 M sigs/s)
+    const uint32_t S = S_env ? S_env : n_sigs >= 256ull * (n_keys ? n_keys : 1) ? CG_TXSIG_COUNT_SAMPLE : 1u;
     // CG_TXSIG_SAMPLE_BLOCK (A/B): consecutive records per sample. 8 reads an eighth of the table's
     // cache lines instead of all of them (every 8th 24-B record): the pass went 5.3 -> 2.8 ms on the
     // configs[4] shard, 218 -> 238 M sigs/s (profiles/r03/env_ec3); a key the block sampling
@@ -1094,15 +1102,50 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
       const uint32_t x = v ? (uint32_t)strtoul(v, nullptr, 10) : CG_TXSIG_SAMPLE_BLOCK;
       return x >= 1 && x <= 64 ? x : CG_TXSIG_SAMPLE_BLOCK;
     }();
-    const uint64_t ng = (n_sigs + (uint64_t)S * B - 1) / ((uint64_t)S * B);
+    if (S == 1) {  // exact: byte counters per thread (1 MB for 2^20 keys, cache-resident), wraps logged
+      c->cnt8.resize(nt);
+      c->ovf.resize(nt);
+      auto scan8 = [&](uint64_t t) {
+        std::vector<uint8_t>& c8 = c->cnt8[t];
+        if (c8.size() < n_keys) c8.resize(n_keys);
+        memset(c8.data(), 0, n_keys);
+        std::vector<uint32_t>& of = c->ovf[t];
+        of.clear();
+        uint8_t* cc = c8.data();
+        for (uint64_t i = n_sigs * t / nt; i < n_sigs * (t + 1) / nt; ++i) {
+          const uint32_t k = sigs[i].key_idx;
+          if (k < n_keys && ++cc[k] == 0) of.push_back(k);
+        }
+      };
+      std::vector<std::thread> th;
+      for (uint64_t t = 1; t < nt; ++t) th.emplace_back(scan8, t);
+      scan8(0);
+      for (auto& t : th) t.join();
+      th.clear();
+      auto sum = [&](uint64_t t) {
+        for (uint64_t k = n_keys * t / nt; k < n_keys * (t + 1) / nt; ++k) {
+          uint32_t v = 0;
+          for (uint64_t u = 0; u < nt; ++u) v += c->cnt8[u][k];
+          counts[k] = v;
+        }
+      };
+      for (uint64_t t = 1; t < nt; ++t) th.emplace_back(sum, t);
+      sum(0);
+      for (auto& t : th) t.join();
+      for (uint64_t t = 0; t < nt; ++t)
+        for (uint32_t k : c->ovf[t]) counts[k] += 256u;
+      return;
+    }
+    const uint64_t Bs = B;
+    const uint64_t ng = (n_sigs + (uint64_t)S * Bs - 1) / ((uint64_t)S * Bs);
     std::vector<std::vector<uint32_t>> pc(nt > 1 ? nt : 0, std::vector<uint32_t>(n_keys ? n_keys : 1, 0u));
     auto scan = [&](uint64_t t) {
       uint32_t* cnt = nt > 1 ? pc[t].data() : counts.data();
       for (uint64_t g = ng * t / nt; g < ng * (t + 1) / nt; ++g) {
         // B consecutive records per group of S B, the block at a hashed position (no aliasing with
         // a layout that cycles through the keys); B > 1 reads fewer cache lines per sample
-        const uint64_t i0 = (g * S + (((uint32_t)g * 0x9E3779B1u) >> 24) % S) * B;
-        for (uint64_t i = i0; i < i0 + B && i < n_sigs; ++i)
+        const uint64_t i0 = (g * S + (((uint32_t)g * 0x9E3779B1u) >> 24) % S) * Bs;
+        for (uint64_t i = i0; i < i0 + Bs && i < n_sigs; ++i)
           if (sigs[i].key_idx < n_keys) ++cnt[sigs[i].key_idx];
       }
     };

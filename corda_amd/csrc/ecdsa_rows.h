@@ -21,6 +21,12 @@
 #endif
 #define EC_DIGITS 43
 #define EC_ROWS ((EC_DIGITS + EC_WINDOWS - 1) / EC_WINDOWS)
+// quarter tables (keyws.h): EC_QWINDOWS windows per row, EC_QROWS rows (row j = 2^{66 j} Q), in
+// the first EC_QROWS rows of the key's EcRowTab
+#ifndef EC_QWINDOWS
+#define EC_QWINDOWS 11
+#endif
+#define EC_QROWS ((EC_DIGITS + EC_QWINDOWS - 1) / EC_QWINDOWS)
 #define EC_MULT 32
 #define EC_PACKED 11
 
@@ -30,6 +36,9 @@ struct EcAff {
 
 struct EcRowTab {
   EcAff t[EC_ROWS][EC_MULT];  // t[j][k-1] = k * 2^{24j} * P
+};
+struct EcRowTabQ {
+  EcAff t[EC_QROWS][EC_MULT];  // t[j][k-1] = k * 2^{66j} * P (the quarter rows, same layout)
 };
 
 // Signed radix-64 digits of a < 2^256, 4 per word as signed bytes. The top digit covers
@@ -886,22 +895,25 @@ CG_HD void ec_add_g_wide(Jac& R, bool& inf, const u256w& u1, const TabG& TG, con
 // Stage 3: R = u2 Q + u1 G (Q over the per-key radix-64 rows in EC_WINDOWS windows, then G over
 // the constant wide table: 43 + 12 mixed additions, 18 doublings; the round-1 radix-2^10 G table
 // spread 26 additions over the windows), then the x-check. Returns 0 VALID / 1 INVALID.
-template <int C, class TabG, class TabQ>
-CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG, const TabQ& TQ,
-                                  const EcConsts& K) {
+// NW windows over NR rows (NW NR >= 43): the full tables (EC_WINDOWS, EC_ROWS) or the quarter ones
+// (EC_QWINDOWS, EC_QROWS: (NW - 1) 6 = 60 doublings)
+template <int C, int NW, int NR, class TabG, class TabQ>
+CG_HD uint32_t ecdsa_ladder_check_w(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG, const TabQ& TQ,
+                                    const EcConsts& K) {
+  static_assert(NW * NR >= EC_DIGITS, "every digit has a row");
   uint32_t dq[EC_PACKED];
   ec_recode_w6(dq, u2);
   Jac R;
   jac_set_inf<C>(R, K);
   bool inf = true;  // R = infinity: doublings skipped, the next addition loads the point
-  for (int i = EC_WINDOWS - 1; i >= 0; --i) {
-    if (i != EC_WINDOWS - 1 && !inf) {
+  for (int i = NW - 1; i >= 0; --i) {
+    if (i != NW - 1 && !inf) {
 #pragma unroll 1
       for (int d = 0; d < EC_W; ++d) jac_dbl_w<C>(R, R);
     }
 #pragma unroll 1
-    for (int j = 0; j < EC_ROWS; ++j) {
-      const int t = EC_WINDOWS * j + i;
+    for (int j = 0; j < NR; ++j) {
+      const int t = NW * j + i;
       if (t >= EC_DIGITS) continue;
       const int b = ec_digit6(dq, t);
       if (b != 0) {
@@ -913,6 +925,11 @@ CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w&
   }
   ec_add_g_wide<C>(R, inf, u1, TG, K);
   return ecdsa_x_check<C>(R, r, K);
+}
+template <int C, class TabG, class TabQ>
+CG_HD uint32_t ecdsa_ladder_check(const u256w& u1, const u256w& u2, const u256w& r, const TabG& TG, const TabQ& TQ,
+                                  const EcConsts& K) {
+  return ecdsa_ladder_check_w<C, EC_WINDOWS, EC_ROWS>(u1, u2, r, TG, TQ, K);
 }
 
 // The same check for a key that has only row 0 of its table (few items in the batch,

@@ -138,8 +138,18 @@ __device__ __forceinline__ uint64_t item_msg_len(const cg_item& it, uint64_t are
 // Row tables (ed25519_rows.h) with signed radix-64 digits: 43 digits in 11 rows of 4 windows.
 typedef EdRowsCfg<ED_W, ED_K> EdCfg;
 typedef EdRowTabW<ED_W, ED_K> EdTab;  // 22 x 32 affine niels = 84480 B
+// The quarter tables (keys with KEY_QUARTER_MIN_USES .. ED_DIRECT_MAX_USES - 1 items): the same
+// radix-2^6 digits in ED_QK windows per row, so 4 rows (row j = multiples of 2^{66 j} (-A)) and
+// 60 doublings per item, stored in the first 4 rows of the key's EdTab (a key has one mode).
+#ifndef ED_QK
+#define ED_QK 11
+#endif
+typedef EdRowsCfg<ED_W, ED_QK> EdQCfg;
+typedef EdRowTabW<ED_W, ED_QK> EdQTab;
+static_assert(EdQCfg::kRows <= EdCfg::kRows && EdQCfg::kMult == EdCfg::kMult, "quarter rows fit the full table");
 // base slots per key, one stride for both schemes (Ed25519 rows >= ECDSA rows)
 #define KEY_BASES (EdCfg::kRows > EC_ROWS ? EdCfg::kRows : EC_ROWS)
+static_assert(EC_QROWS <= EC_ROWS, "ECDSA quarter rows fit the full table");
 typedef EdBCfg<ED_W, ED_K, ED_WB> EdBCfgT;
 typedef EdBTabW<ED_W, ED_K, ED_WB> EdBTab;  // 26 x 512 affine niels = 1.6 MB, constant
 
@@ -169,6 +179,12 @@ union BaseSlot {
 #define PLAN_CLASSES 3
 #define PLAN_FULL 4  // ranges[PLAN_FULL + c]: first item of class c whose key has full tables
 #define PLAN_WIDE 7  // ranges[PLAN_WIDE + c]: first item of class c whose key has wide tables
+#define PLAN_QUART 10  // ranges[PLAN_QUART + c]: first item of class c whose key has quarter tables
+// Table-mode order inside a class (the plan's 2 mode bits): row 0, quarter, full, wide.
+#define PLAN_MODE_ROW0 0u
+#define PLAN_MODE_QUART 1u
+#define PLAN_MODE_FULL 2u
+#define PLAN_MODE_WIDE 3u
 // Items whose clear data is longer than this sort after the short ones of their class and table
 // mode (plan_sort.hip), so a wave hashes either short or long messages, never both.
 #define ITEM_LONG_MIN 1024u
@@ -195,7 +211,8 @@ static inline uint32_t tab_park_lanes(uint32_t n_keys, uint32_t rows) {
 }
 #define ED_ROW_PARK_BYTES ((size_t)EdCfg::kMult * ED_PARK_DWORDS * 4)
 #define EC_ROW_PARK_BYTES ((size_t)EC_MULT * EC_ROW_PARK * 4)
-#define ROW0_COUNT_AT 8  // row0_count = full_count + 8 (the 256-B count block)
+#define ROW0_COUNT_AT 8    // row0_count = full_count + 8 (the 256-B count block)
+#define QUART_COUNT_AT 16  // quart_count = full_count + 16
 struct KeyWs {
   EdKeyHdr* hdr;
   TabSlot* tab;
@@ -211,6 +228,8 @@ struct KeyWs {
   uint32_t* full_count;
   uint32_t* row0;        // per class c: every used key without wide tables (its row 0 is built),
   uint32_t* row0_count;  // row0[c * n_keys + l] for l < row0_count[c] (= full_count + ROW0_COUNT_AT)
+  uint32_t* quart;       // per class c: the keys with quarter tables (rows 1..3 built after row 0)
+  uint32_t* quart_count;  // (= full_count + QUART_COUNT_AT)
   uint8_t* seen;   // 1 if any item of the batch uses the key (exact; uses is sampled)
   uint32_t* wide_idx;    // per key: its slot in the scheme's wide pool, or KEY_NOT_WIDE
   uint32_t* wide;        // per class c: the keys with wide tables, wide[c * n_keys + l]
@@ -227,8 +246,12 @@ struct KeyWs {
 // cg_prepare_keys_device cannot, and builds every key in full). The mode changes only speed,
 // never a verdict: both ladders compute the same point.
 //   0 uses                        decode only (Abyte, status), no rows
-//   1 .. ED_DIRECT_MAX_USES - 1   row 0 only (the 32 affine multiples of -A): the item runs the
+//   1 .. KEY_QUARTER_MIN_USES - 1 row 0 only (the 32 affine multiples of -A): the item runs the
 //                                 252-doubling Horner ladder (ed_double_scalar_row0)
+//   .. ED_DIRECT_MAX_USES - 1     quarter: 4 rows, 60 doublings per item (ed_double_scalar_fw over
+//                                 EdQTab; ECDSA: EC_QROWS rows, ecdsa_ladder_check_w). Round 4: the
+//                                 2^20-distinct-key leg (~12 uses a key) went 65 -> 90 M sigs/s
+//                                 with quarter rows instead of row 0 (profiles/r04/kd)
 //   more                          all 22 rows: 6 doublings per item (ed_double_scalar_wb)
 // Break-even (measured on MI355X, 2^20 Ed25519 items): a key's full tables cost ~230 ns of
 // GPU time, the row-0 ladder ~7 ns more per item than the full-table one -> ~32 items.
@@ -249,6 +272,9 @@ struct KeyWs {
 #define KEY_WIDE_MAX 8192u  // wide slots per pool at most (Ed25519 9.4 GB / ECDSA 6.3 GB)
 #define KEY_USES_ALL 0xffffffffu
 #define KEY_USES_SAMPLE 4u  // k_key_uses samples by the top 2 bits of a 32-bit hash: 1 in 4
+#ifndef KEY_QUARTER_MIN_USES
+#define KEY_QUARTER_MIN_USES 3u
+#endif
 #ifndef ED_DIRECT_MAX_USES
 #define ED_DIRECT_MAX_USES 32u
 #endif
@@ -323,7 +349,10 @@ static inline KeyWs key_ws(void* base, uint32_t n_keys, const WidePool* wp = nul
   w.full_count = (uint32_t*)p;
   w.row0_count = w.full_count + ROW0_COUNT_AT;
   p += 256;
+  w.quart_count = w.full_count + QUART_COUNT_AT;
   w.row0 = (uint32_t*)p;
+  p += al256(3 * n * sizeof(uint32_t));
+  w.quart = (uint32_t*)p;
   p += al256(3 * n * sizeof(uint32_t));
   w.seen = p;
   p += al256(n);
@@ -345,7 +374,7 @@ static inline size_t key_ws_bytes(uint32_t n_keys) {
   return al256(n * sizeof(EdKeyHdr)) + al256(n * sizeof(TabSlot)) + al256(n * KEY_BASES * sizeof(BaseSlot)) +
          al256(tab_park_lanes(n_keys, EdCfg::kRows) * ED_ROW_PARK_BYTES) +
          2 * al256(tab_park_lanes(n_keys, EC_ROWS) * EC_ROW_PARK_BYTES) + al256(n * sizeof(uint32_t)) +
-         al256(3 * n * sizeof(uint32_t)) + 256 + al256(3 * n * sizeof(uint32_t)) + al256(n) +
+         al256(3 * n * sizeof(uint32_t)) + 256 + 2 * al256(3 * n * sizeof(uint32_t)) + al256(n) +
          al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256;
 }
 

@@ -53,7 +53,11 @@ __global__ void __launch_bounds__(256) k_plan_keys(const cg_item* __restrict__ i
                                        : PLAN_CLASSES;
   }
   uint32_t mode = 0;
-  if (c < PLAN_CLASSES) mode = wide_idx[k] != KEY_NOT_WIDE ? 2u : uses[k] >= ED_DIRECT_MAX_USES ? 1u : 0u;
+  if (c < PLAN_CLASSES)
+    mode = wide_idx[k] != KEY_NOT_WIDE         ? PLAN_MODE_WIDE
+         : uses[k] >= ED_DIRECT_MAX_USES      ? PLAN_MODE_FULL
+         : uses[k] >= KEY_QUARTER_MIN_USES    ? PLAN_MODE_QUART
+                                              : PLAN_MODE_ROW0;
   const uint32_t lng = items[i].msg_len > ITEM_LONG_MIN ? 1u : 0u;
   skey[i] = (c << kb) |
             (c < PLAN_CLASSES ? (mode << (kb - 2)) | (lng << (kb - 3)) | (k & ((1u << (kb - 3)) - 1u)) : 0u);
@@ -64,19 +68,23 @@ __global__ void k_plan_ranges(const uint32_t* __restrict__ skey, uint64_t n_item
                               uint32_t* __restrict__ ranges) {
   // lanes 0..3: class starts ranges[c] (ranges[3] = end of the verified classes); lanes 4..6:
   // ranges[PLAN_FULL + c] = first full-table item of class c; lanes 7..9: ranges[PLAN_WIDE + c] =
-  // first wide-table item of class c (the mode bits, keyws.h)
+  // first wide-table item; lanes 10..12: ranges[PLAN_QUART + c] = first quarter-table item (the mode
+  // bits, keyws.h: row 0, quarter, full, wide)
   const uint32_t t = threadIdx.x;
-  if (t >= PLAN_WIDE + PLAN_CLASSES) return;
+  if (t >= PLAN_QUART + PLAN_CLASSES) return;
   uint32_t c, target;
   if (t <= PLAN_CLASSES) {
     c = t;
     target = c << kb;
   } else if (t < PLAN_WIDE) {
     c = t - PLAN_FULL;
-    target = (c << kb) | (1u << (kb - 2));
-  } else {
+    target = (c << kb) | (PLAN_MODE_FULL << (kb - 2));
+  } else if (t < PLAN_QUART) {
     c = t - PLAN_WIDE;
-    target = (c << kb) | (2u << (kb - 2));
+    target = (c << kb) | (PLAN_MODE_WIDE << (kb - 2));
+  } else {
+    c = t - PLAN_QUART;
+    target = (c << kb) | (PLAN_MODE_QUART << (kb - 2));
   }
   uint64_t lo = 0, hi = n_items;  // first position with key >= target
   while (lo < hi) {

@@ -34,7 +34,7 @@ __global__ void __launch_bounds__(256) k_key_init(uint32_t n_keys, uint32_t all,
                                                   uint8_t* __restrict__ seen, uint32_t* __restrict__ full_count,
                                                   uint32_t* __restrict__ wide_idx, uint32_t* __restrict__ wide_count) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < PLAN_CLASSES) full_count[i] = full_count[ROW0_COUNT_AT + i] = 0;
+  if (i < PLAN_CLASSES) full_count[i] = full_count[ROW0_COUNT_AT + i] = full_count[QUART_COUNT_AT + i] = 0;
   if (i < PLAN_CLASSES + 2) wide_count[i] = 0;
   if (i >= n_keys) return;
   uses[i] = all ? KEY_USES_ALL : 0u;
@@ -96,16 +96,17 @@ __device__ __forceinline__ void list_append(int c, uint32_t i, uint32_t n_keys, 
 
 // Table mode per key: wide tables for keys with >= min_ed / min_ec items while the family's
 // wide pool has slots (one atomic per wide key: they are few), else full tables from
-// ED_DIRECT_MAX_USES items; the wide and full keys compacted per scheme class. One wave per block.
+// ED_DIRECT_MAX_USES items, quarter tables from KEY_QUARTER_MIN_USES, else row 0; the keys of each
+// mode compacted per scheme class (row0 lists every used key without wide tables). One wave a block.
 __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ keys, uint32_t n_keys,
                                                      uint32_t* __restrict__ uses, const uint8_t* __restrict__ seen,
                                                      uint32_t* __restrict__ full, uint32_t* __restrict__ full_count,
                                                      uint32_t* __restrict__ wide_idx, uint32_t* __restrict__ wide,
                                                      uint32_t* __restrict__ wide_count, uint32_t* __restrict__ row0,
-                                                     uint32_t cap_ed, uint32_t cap_ec, uint32_t min_ed,
-                                                     uint32_t min_ec) {
+                                                     uint32_t* __restrict__ quart, uint32_t cap_ed, uint32_t cap_ec,
+                                                     uint32_t min_ed, uint32_t min_ec) {
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  int c = -1, cw = -1, c0 = -1;  // full list, wide list, row-0 list
+  int c = -1, cw = -1, c0 = -1, cq = -1;  // full list, wide list, row-0 list, quarter list
   uint32_t u = 0;
   if (i < n_keys) {  // the estimate, made exact where it matters: a used key counts >= 1
     u = uses[i];
@@ -139,10 +140,12 @@ __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ 
        : s == CG_ECDSA_SECP256R1_SHA256 ? PLAN_R1
        : s == CG_ECDSA_SECP256K1_SHA256 ? PLAN_K1
                                         : -1;
+    if (u >= KEY_QUARTER_MIN_USES && u < ED_DIRECT_MAX_USES) cq = c0;  // and its quarter rows 1..3
   }
   list_append(c, i, n_keys, full, full_count);
   list_append(cw, i, n_keys, wide, wide_count);
   list_append(c0, i, n_keys, row0, full_count + ROW0_COUNT_AT);
+  list_append(cq, i, n_keys, quart, full_count + QUART_COUNT_AT);
 }
 
 hipError_t upload_constants() {
@@ -266,7 +269,7 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
                        src->n, n_keys, w.uses, w.seen);
   hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys, w.uses,
                      (const uint8_t*)w.seen, w.full, w.full_count, w.wide_idx, w.wide, w.wide_count, w.row0,
-                     w.cap_ed, w.cap_ec, w.min_ed, w.min_ec);
+                     w.quart, w.cap_ed, w.cap_ec, w.min_ed, w.min_ec);
   static const bool serial = [] {  // CG_SERIAL_KEYPREP=1: key prep on the caller's stream (A/B runs)
     const char* v = getenv("CG_SERIAL_KEYPREP");
     return v && v[0] == '1';

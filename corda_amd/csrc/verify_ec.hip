@@ -44,50 +44,60 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_decode(const cg_key* __restri
   hdr[i] = h;
 }
 
-// one lane per full-table key of this curve (keyws.h: the compacted list)
+// one lane per full-table key of this curve (keyws.h: the compacted list), then one per quarter key
 template <int C>
 __global__ void __launch_bounds__(64) k_ec_keyprep_chain(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                          const uint32_t* __restrict__ full,
+                                                         const uint32_t* __restrict__ quart,
                                                          const uint32_t* __restrict__ full_count,
                                                          BaseSlot* __restrict__ bases) {
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   const int c = plan_class_of_curve(C);
-  if (l >= full_count[c]) return;
-  const uint32_t i = full[(size_t)c * n_keys + l];
+  const uint32_t nf = full_count[c], nq = full_count[QUART_COUNT_AT + c];
+  if (l >= nf + nq) return;
+  const bool q = l >= nf;
+  const uint32_t i = q ? quart[(size_t)c * n_keys + (l - nf)] : full[(size_t)c * n_keys + l];
   if (hdr[i].status != 0) return;
   Jac P = bases[(size_t)i * KEY_BASES].ec;
-  for (int j = 1; j < EC_ROWS; ++j) {
-    jac_dbl_n<C>(P, P, EC_W * EC_WINDOWS);
+  const int rows = q ? EC_QROWS : EC_ROWS, step = EC_W * (q ? EC_QWINDOWS : EC_WINDOWS);
+  for (int j = 1; j < rows; ++j) {
+    jac_dbl_n<C>(P, P, step);
     bases[(size_t)i * KEY_BASES + j].ec = P;
   }
 }
 
 // The 32 affine multiples of a row base (ec_row_build_parked), for the compacted tasks: row 0 of
-// every used key of this curve without wide tables, then rows 1..10 of its full-table keys; a grid
+// every used key of this curve without wide tables, rows 1..10 of its full-table keys, rows 1..3 of
+// its quarter keys; a grid
 // of `lanes` lanes looping over the tasks, each parked in its own column (as k_ed_keyprep_tab).
 template <int C>
 __global__ void __launch_bounds__(64) k_ec_keyprep_tab(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                        const BaseSlot* __restrict__ bases,
                                                        const uint32_t* __restrict__ row0,
                                                        const uint32_t* __restrict__ full,
+                                                       const uint32_t* __restrict__ quart,
                                                        const uint32_t* __restrict__ full_count,
                                                        TabSlot* __restrict__ tabs, uint32_t* __restrict__ park,
                                                        uint32_t lanes) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= lanes) return;
   const int c = plan_class_of_curve(C);
-  const uint32_t n0 = full_count[ROW0_COUNT_AT + c], nf = full_count[c];
-  const uint64_t tasks = n0 + (uint64_t)nf * (EC_ROWS - 1);
+  const uint32_t n0 = full_count[ROW0_COUNT_AT + c], nf = full_count[c], nq = full_count[QUART_COUNT_AT + c];
+  const uint64_t tf = n0 + (uint64_t)nf * (EC_ROWS - 1), tasks = tf + (uint64_t)nq * (EC_QROWS - 1);
   const EcRowParkLanes pk{park, p, lanes};
   for (uint64_t t = p; t < tasks; t += lanes) {
     uint32_t i, j;
     if (t < n0) {
       i = row0[(size_t)c * n_keys + t];
       j = 0;
-    } else {
+    } else if (t < tf) {
       const uint64_t h = t - n0;
       j = 1 + (uint32_t)(h / nf);
       i = full[(size_t)c * n_keys + h % nf];
+    } else {  // quarter rows 1..EC_QROWS - 1
+      const uint64_t h = t - tf;
+      j = 1 + (uint32_t)(h / nq);
+      i = quart[(size_t)c * n_keys + h % nq];
     }
     if (hdr[i].status != 0) continue;
     ec_row_build_parked<C>(tabs[i].ec.t[j], bases[(size_t)i * KEY_BASES + j].ec, pk, c_ec[C]);
@@ -302,26 +312,33 @@ __global__ void __launch_bounds__(256) k_ec_inv(const uint32_t* __restrict__ per
   }
 }
 
-// Two launches over the curve's range, one per table mode (the plan keeps the modes in separate
-// waves, so a lane of the other mode exits with its whole wave); separate kernels keep the
-// full-table ladder's register allocation (3 waves/SIMD) free of the row-0 variant's.
-template <int C, bool Full>
+// One launch over the curve's range per table mode (the plan keeps the modes in separate waves, so
+// a lane of another mode exits with its whole wave); separate kernels keep each ladder's register
+// allocation free of the others'. Mode: PLAN_MODE_ROW0 / PLAN_MODE_QUART / PLAN_MODE_FULL.
+template <int C, int Mode>
 __global__ void __launch_bounds__(256) k_ec_ladder(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
                                                    const uint32_t* __restrict__ ranges,
                                                    const TabSlot* __restrict__ tabs,
                                                    const EcGWideTab* __restrict__ gtab, uint8_t* __restrict__ status,
                                                    const EcItemWs* __restrict__ ws) {
   const int cls = plan_class_of_curve(C);  // the plan's mode split (plan_sort.hip)
-  const uint32_t beg = Full ? ranges[PLAN_FULL + cls] : ranges[cls];
-  const uint32_t end = Full ? ranges[PLAN_WIDE + cls] : ranges[PLAN_FULL + cls];
+  const uint32_t beg = Mode == PLAN_MODE_FULL    ? ranges[PLAN_FULL + cls]
+                     : Mode == PLAN_MODE_QUART ? ranges[PLAN_QUART + cls]
+                                               : ranges[cls];
+  const uint32_t end = Mode == PLAN_MODE_FULL    ? ranges[PLAN_WIDE + cls]
+                     : Mode == PLAN_MODE_QUART ? ranges[PLAN_FULL + cls]
+                                               : ranges[PLAN_QUART + cls];
   for (Walk wk = walk_units(end - beg); wk.u < wk.end; wk.u += wk.step) {
     const uint64_t p = beg + wk.u;
     const uint32_t i = perm[p];
     if (status[i] != EC_PENDING_BASE + C) continue;
     const uint32_t key = items[i].key_idx;
     const EcItemWs w = ws[p];
-    if (Full) {
+    if (Mode == PLAN_MODE_FULL) {
       status[i] = (uint8_t)ecdsa_ladder_check<C>(w.a, w.b, w.r, *gtab, tabs[key].ec, c_ec[C]);
+    } else if (Mode == PLAN_MODE_QUART) {  // the first rows of the table, 2^{66 j} Q (keyws.h)
+      status[i] = (uint8_t)ecdsa_ladder_check_w<C, EC_QWINDOWS, EC_QROWS>(
+          w.a, w.b, w.r, *gtab, *(const EcRowTabQ*)&tabs[key].ec, c_ec[C]);
     } else {  // a key with few items: row 0 only (keyws.h)
       status[i] = (uint8_t)ecdsa_ladder_check_row0<C>(w.a, w.b, w.r, *gtab, tabs[key].ec.t[0], c_ec[C]);
     }
@@ -466,7 +483,7 @@ static void launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const u
                      w.bases);
   if (decoded) hipEventRecord(decoded, stream);
   hipLaunchKernelGGL(k_ec_keyprep_chain<C>, g, dim3(B), 0, stream, n_keys, w.hdr, (const uint32_t*)w.full,
-                     (const uint32_t*)w.full_count, w.bases);
+                     (const uint32_t*)w.quart, (const uint32_t*)w.full_count, w.bases);
   if (w.cap_ec) {
     const uint32_t lds = chain_spread_lds();
     if (lds) hipFuncSetAttribute((const void*)k_ec_wide_chain<C>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -482,8 +499,8 @@ static void launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const Key
   const uint32_t B = 64;
   if (full)
     hipLaunchKernelGGL(k_ec_keyprep_tab<C>, dim3(w.park_lanes_ec / B), dim3(B), 0, stream, n_keys, w.hdr, w.bases,
-                       (const uint32_t*)w.row0, (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.tab,
-                       w.park_ec[C], w.park_lanes_ec);
+                       (const uint32_t*)w.row0, (const uint32_t*)w.full, (const uint32_t*)w.quart,
+                       (const uint32_t*)w.full_count, w.tab, w.park_ec[C], w.park_lanes_ec);
   if (wide && w.cap_ec) {
     const uint64_t gl = (uint64_t)w.cap_ec * EC_WIDE_ROWS * EC_WIDE_GROUPS, rl = (uint64_t)w.cap_ec * EC_WIDE_ROWS;
     const uint32_t* wl = (const uint32_t*)w.wide;
@@ -556,12 +573,23 @@ void ec_launch_front(int curve, const cg_item* d_items, uint64_t n_items, const 
     launch_front<CG_CURVE_K1>(d_items, n_items, d_arena, arena_len, mode, d_status, w, d_msgs, msgs_len, iw, stream);
 }
 
+template <int C, int Mode>
+static void launch_ladder_m(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                            const ItemWs& iw, const void* d_btab, hipStream_t stream) {
+  const uint32_t B = 256;
+  hipLaunchKernelGGL((k_ec_ladder<C, Mode>), dim3(walk_grid(n_items, B, WALK_CAP(2))), dim3(B), 0, stream, d_items,
+                     iw.perm, iw.ranges, w.tab, gwide(d_btab, C), d_status, (const EcItemWs*)iw.slots);
+}
+// full: the full-table ladder; else the row-0 then the quarter-table one (the side streams)
 template <int C, bool Full>
 static void launch_ladder_t(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
                             const ItemWs& iw, const void* d_btab, hipStream_t stream) {
-  const uint32_t B = 256;
-  hipLaunchKernelGGL((k_ec_ladder<C, Full>), dim3(walk_grid(n_items, B, WALK_CAP(2))), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
-                     w.tab, gwide(d_btab, C), d_status, (const EcItemWs*)iw.slots);
+  if (Full) {
+    launch_ladder_m<C, PLAN_MODE_FULL>(d_items, n_items, d_status, w, iw, d_btab, stream);
+  } else {
+    launch_ladder_m<C, PLAN_MODE_ROW0>(d_items, n_items, d_status, w, iw, d_btab, stream);
+    launch_ladder_m<C, PLAN_MODE_QUART>(d_items, n_items, d_status, w, iw, d_btab, stream);
+  }
 }
 
 void ec_launch_ladder(int curve, bool full, const cg_item* d_items, uint64_t n_items, uint8_t* d_status,

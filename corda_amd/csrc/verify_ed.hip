@@ -102,22 +102,27 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_decode(const cg_key* __restri
 // (a serial chain of 240 doublings)
 __global__ void __launch_bounds__(64) k_ed_keyprep_chain(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                          const uint32_t* __restrict__ full,
+                                                         const uint32_t* __restrict__ quart,
                                                          const uint32_t* __restrict__ full_count,
                                                          BaseSlot* __restrict__ bases) {
+  // lanes [0, nf): full-table keys (21 x 12 doublings); [nf, nf + nq): quarter keys (3 x 66)
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= full_count[PLAN_ED]) return;
-  const uint32_t i = full[(size_t)PLAN_ED * n_keys + l];
+  const uint32_t nf = full_count[PLAN_ED], nq = full_count[QUART_COUNT_AT + PLAN_ED];
+  if (l >= nf + nq) return;
+  const bool q = l >= nf;
+  const uint32_t i = q ? quart[(size_t)PLAN_ED * n_keys + (l - nf)] : full[(size_t)PLAN_ED * n_keys + l];
   if (hdr[i].status != 0) return;
   ge_p3 P = bases[(size_t)i * KEY_BASES].ed;
-  for (int j = 1; j < EdCfg::kRows; ++j) {
-    ed_dbl_n(P, P, ED_W * ED_K);
+  const int rows = q ? EdQCfg::kRows : EdCfg::kRows, step = q ? ED_W * ED_QK : ED_W * ED_K;
+  for (int j = 1; j < rows; ++j) {
+    ed_dbl_n(P, P, step);
     bases[(size_t)i * KEY_BASES + j].ed = P;
   }
 }
 
 // The 32 affine multiples of a row base, one inversion per row (ed_row_build_parked), for the
 // compacted tasks: row 0 of every used key without wide tables (row0 list), then rows 1..21 of the
-// full-table keys (full list). A grid of `lanes` lanes (keyws.h tab_park_lanes), each looping over
+// full-table keys (full list), then rows 1..3 of the quarter-table keys (quart list). A grid of `lanes` lanes (keyws.h tab_park_lanes), each looping over
 // tasks lane, lane + lanes, ... with its walk parked in its own lane-interleaved column of `park`.
 #ifndef ED_TAB_WAVES  // waves per SIMD the row builds' registers must allow (255 VGPRs + 56 AGPRs left 1)
 #define ED_TAB_WAVES 2
@@ -127,23 +132,29 @@ k_ed_keyprep_tab(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                        const BaseSlot* __restrict__ bases,
                                                        const uint32_t* __restrict__ row0,
                                                        const uint32_t* __restrict__ full,
+                                                       const uint32_t* __restrict__ quart,
                                                        const uint32_t* __restrict__ full_count,
                                                        TabSlot* __restrict__ tabs, uint32_t* __restrict__ park,
                                                        uint32_t lanes) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= lanes) return;
-  const uint32_t n0 = full_count[ROW0_COUNT_AT + PLAN_ED], nf = full_count[PLAN_ED];
-  const uint64_t tasks = n0 + (uint64_t)nf * (EdCfg::kRows - 1);
+  const uint32_t n0 = full_count[ROW0_COUNT_AT + PLAN_ED], nf = full_count[PLAN_ED],
+                 nq = full_count[QUART_COUNT_AT + PLAN_ED];
+  const uint64_t tf = n0 + (uint64_t)nf * (EdCfg::kRows - 1), tasks = tf + (uint64_t)nq * (EdQCfg::kRows - 1);
   const EdParkLanes pk{park, p, lanes};
   for (uint64_t t = p; t < tasks; t += lanes) {
     uint32_t i, j;
     if (t < n0) {
       i = row0[(size_t)PLAN_ED * n_keys + t];
       j = 0;
-    } else {
+    } else if (t < tf) {
       const uint64_t h = t - n0;
       j = 1 + (uint32_t)(h / nf);
       i = full[(size_t)PLAN_ED * n_keys + h % nf];
+    } else {  // quarter rows 1..3 (their bases 2^{66 j} (-A) from the chain)
+      const uint64_t h = t - tf;
+      j = 1 + (uint32_t)(h / nq);
+      i = quart[(size_t)PLAN_ED * n_keys + h % nq];
     }
     if (hdr[i].status != 0) continue;
     ed_row_build_parked<EdCfg::kMult>(tabs[i].ed.t[j], bases[(size_t)i * KEY_BASES + j].ed, c_ed.d2, pk);
@@ -764,16 +775,21 @@ __global__ void __launch_bounds__(256, ED_LADDER_WIDE_WAVES) k_ed_ladder_wide(
 // One lane per pending Ed25519 plan position: R' = h (-A) + S' B over the per-key rows and the
 // constant radix-2^10 B table (both in global memory; the B table stays L2-resident), left
 // projective in the item slot.
-// Two launches over the Ed25519 range, one per table mode (the plan keeps the modes in separate
-// waves); separate kernels keep the full-table ladder's registers free of the row-0 variant's.
-template <bool Full>
+// One launch over the Ed25519 range per table mode (the plan keeps the modes in separate waves);
+// separate kernels keep each ladder's registers free of the others'. Mode: PLAN_MODE_ROW0 /
+// PLAN_MODE_QUART / PLAN_MODE_FULL (keyws.h).
+template <int Mode>
 __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
     const EdKeyHdr* __restrict__ hdr, const TabSlot* __restrict__ tabs, const EdBWideTab* __restrict__ btab,
     uint8_t* __restrict__ status, void* __restrict__ slots, EdCols ec) {
-  // the plan's mode split: row-0 keys' items first, then full-table keys' (plan_sort.hip)
-  const uint32_t beg = Full ? ranges[PLAN_FULL + PLAN_ED] : ranges[PLAN_ED];
-  const uint32_t end = Full ? ranges[PLAN_WIDE + PLAN_ED] : ranges[PLAN_FULL + PLAN_ED];
+  // the plan's mode split: row-0 keys' items, quarter-table keys', full-table keys' (plan_sort.hip)
+  const uint32_t beg = Mode == PLAN_MODE_FULL    ? ranges[PLAN_FULL + PLAN_ED]
+                     : Mode == PLAN_MODE_QUART ? ranges[PLAN_QUART + PLAN_ED]
+                                               : ranges[PLAN_ED];
+  const uint32_t end = Mode == PLAN_MODE_FULL    ? ranges[PLAN_WIDE + PLAN_ED]
+                     : Mode == PLAN_MODE_QUART ? ranges[PLAN_FULL + PLAN_ED]
+                                               : ranges[PLAN_QUART + PLAN_ED];
   for (Walk w = walk_units(end - beg); w.u < w.end; w.u += w.step) {
     const uint64_t p = beg + w.u;
     const uint32_t key = ec.key[p];
@@ -785,8 +801,11 @@ __global__ void __launch_bounds__(256, ED_LADDER_WAVES_PER_SIMD) k_ed_ladder(
     if (!ec.pend[p]) continue;
     const EdDigits d = ((const EdDigits*)slots)[p];
     ge_p2 q;
-    if (Full) {
+    if (Mode == PLAN_MODE_FULL) {
       ed_double_scalar_fw<ED_W, ED_K>(q, d.eh, d.es, tabs[key].ed, *btab, PickGlobal(), PickGlobal());
+    } else if (Mode == PLAN_MODE_QUART) {  // the first rows of the table, 2^{66 j} (-A) (keyws.h)
+      ed_double_scalar_fw<ED_W, ED_QK>(q, d.eh, d.es, *(const EdQTab*)&tabs[key].ed, *btab, PickGlobal(),
+                                       PickGlobal());
     } else {  // a key with few items: row 0 only (keyws.h)
       ed_double_scalar_row0w<ED_W, ED_K>(q, d.eh, d.es, tabs[key].ed.t[0], *btab, PickGlobal(), PickGlobal());
     }
@@ -878,7 +897,7 @@ void ed_launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const uint8
   hipLaunchKernelGGL(k_ed_keyprep_decode, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, d_keys, n_keys, d_arena,
                      arena_len, w.hdr, w.bases);
   hipLaunchKernelGGL(k_ed_keyprep_chain, dim3((n_keys + B - 1) / B), dim3(B), 0, stream, n_keys, w.hdr,
-                     (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.bases);
+                     (const uint32_t*)w.full, (const uint32_t*)w.quart, (const uint32_t*)w.full_count, w.bases);
   if (w.cap_ed) {
     const uint32_t lds = chain_spread_lds();
     if (lds) hipFuncSetAttribute((const void*)k_ed_wide_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -893,8 +912,8 @@ void ed_launch_keyprep_tabs(const cg_key* d_keys, uint32_t n_keys, const KeyWs& 
   const uint32_t B = 64;
   if (full)
     hipLaunchKernelGGL(k_ed_keyprep_tab, dim3(w.park_lanes_ed / B), dim3(B), 0, stream, n_keys, w.hdr, w.bases,
-                       (const uint32_t*)w.row0, (const uint32_t*)w.full, (const uint32_t*)w.full_count, w.tab,
-                       w.park_ed, w.park_lanes_ed);
+                       (const uint32_t*)w.row0, (const uint32_t*)w.full, (const uint32_t*)w.quart,
+                       (const uint32_t*)w.full_count, w.tab, w.park_ed, w.park_lanes_ed);
   if (wide && w.cap_ed) {
     const uint64_t gl = (uint64_t)w.cap_ed * EdWideCfg::kRows * ED_WIDE_GROUPS, rl = (uint64_t)w.cap_ed * EdWideCfg::kRows;
     const uint32_t* wl = (const uint32_t*)w.wide;
@@ -931,18 +950,22 @@ void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8
                       const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
   const unsigned grid = walk_grid(n_items, B, WALK_CAP(full && ED_LADDER_PF ? ED_LADDER_PF_WAVES : ED_LADDER_WAVES_PER_SIMD));
+  // full: the full-table ladder; else the row-0 then the quarter-table one (the side streams)
 #if ED_LADDER_PF
   if (full)
     hipLaunchKernelGGL(k_ed_ladder_pf, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
                        w.tab, bwide(d_btab), d_status, iw.slots, iw.ed);
   else
 #endif
-  if (full)
-    hipLaunchKernelGGL(k_ed_ladder<true>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
-                       w.tab, bwide(d_btab), d_status, iw.slots, iw.ed);
-  else
-    hipLaunchKernelGGL(k_ed_ladder<false>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
+  if (full) {
+    hipLaunchKernelGGL(k_ed_ladder<PLAN_MODE_FULL>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
                        w.hdr, w.tab, bwide(d_btab), d_status, iw.slots, iw.ed);
+  } else {
+    hipLaunchKernelGGL(k_ed_ladder<PLAN_MODE_ROW0>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
+                       w.hdr, w.tab, bwide(d_btab), d_status, iw.slots, iw.ed);
+    hipLaunchKernelGGL(k_ed_ladder<PLAN_MODE_QUART>, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges,
+                       w.hdr, w.tab, bwide(d_btab), d_status, iw.slots, iw.ed);
+  }
 }
 
 void ed_launch_ladder_wide(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,

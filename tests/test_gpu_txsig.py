@@ -208,3 +208,41 @@ def test_tx_signatures_mixed_table_modes(spool):
             st = eng.verify_tx_signatures(tb)
             bad = np.nonzero(st != ref[idx])[0]
             assert bad.size == 0, f"hot scheme {hot}: {bad.size} verdicts differ, first at {bad[:5]}"
+
+
+def test_every_table_mode_in_one_call(spool):
+    """Keys drawn 1, 2, 3, 6, 12, 31, 40 and 1900 times in one call, so that every table mode
+    (keyws.h: row 0, quarter, full, wide) and the boundaries between them carry items of every
+    scheme: the host-buffer tx-signature path (fewer than 256 uses a key on average: the exact
+    host count), the device one and the message form all give the oracle's verdicts on the same
+    pool items."""
+    import torch
+    from corda_amd.engine import Engine
+    from tools.workload import wl
+    b, labels, schemes, ids, id_idx, ref = spool
+    rng = np.random.default_rng(77)
+    per_key = [1, 2, 3, 6, 12, 31, 40, 1900]
+    key_of = b.items["key_idx"]
+    order = np.argsort(key_of, kind="stable")
+    starts = np.searchsorted(key_of[order], np.arange(len(b.keys) + 1))
+    draws = []
+    for k in range(len(b.keys)):
+        mine = order[starts[k]:starts[k + 1]]
+        if mine.size:
+            draws.append(rng.choice(mine, per_key[k % len(per_key)]))
+    idx = np.concatenate(draws)
+    rng.shuffle(idx)
+    tb = wl.tx_sig_stream(b, schemes, idx, ids, id_idx, nthreads=16)
+    with Engine(0) as eng:
+        st = eng.verify_tx_signatures(tb)
+        assert np.array_equal(st, ref[idx]), f"host path: {np.count_nonzero(st != ref[idx])} differ"
+        dev = torch.device("cuda", 0)
+        up = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).to(dev)  # noqa: E731
+        kd, ijd, sgd, ad = up(tb.keys), up(tb.ids), up(tb.sigs), up(tb.arena)
+        sd = torch.full((tb.n,), 255, dtype=torch.uint8, device=dev)
+        eng.verify_tx_signatures_device(kd.data_ptr(), len(tb.keys), ijd.data_ptr(), tb.n_ids, sgd.data_ptr(), tb.n,
+                                        tb.tmpls, ad.data_ptr(), tb.arena.size, sd.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(sd.cpu().numpy(), ref[idx]), "device path"
+        from corda_amd.batch import Batch
+        assert np.array_equal(eng.verify(Batch(b.keys, b.items[idx], b.arena)), ref[idx]), "message form"

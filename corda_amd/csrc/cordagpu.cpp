@@ -112,6 +112,8 @@ struct cg_ctx {
   std::vector<hipEvent_t> seg;
   hipEvent_t tev[4] = {};
   std::vector<hipEvent_t> segt;  // CG_HOST_TRACE: timing events behind each chunk's copy
+  hipEvent_t backt[2] = {nullptr, nullptr};  // CG_HOST_TRACE: chunk 0's back enqueued / tables ready
+  bool htrace = false;
   // the end of the last call's device work, whatever stream it ran on: the next call waits for it
   // before touching the shared workspace (async calls on different streams)
   hipEvent_t done = nullptr;
@@ -251,6 +253,12 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   if (e == hipSuccess && prepare && after_tables)
     for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(s, c->fork.ready[k], 0);
   auto back = [&](uint64_t k) {
+    if (k == 0 && c->htrace && c->backt[0]) {  // chunk 0's front done; every table family built
+      hipEventRecord(c->backt[0], s);
+      hipStream_t t = c->copy2;  // idle by now: the marker waits there, nothing else does
+      for (int q = 0; q < 3; ++q) hipStreamWaitEvent(t, c->fork.ready[q], 0);
+      hipEventRecord(c->backt[1], t);
+    }
     return cg::launch_items_back(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, d_status + at(k),
                                  c->keyprep.p, ws(k), c->btab.p, s, &c->fork, &wp);
   };
@@ -601,6 +609,8 @@ void cg_close(cg_ctx* c) {
       hipStreamDestroy(*cs);
     }
   for (hipEvent_t e : c->segt) hipEventDestroy(e);
+  for (hipEvent_t e : c->backt)
+    if (e) hipEventDestroy(e);
   if (c->pin_counts) hipHostFree(c->pin_counts);
   for (hipEvent_t e : c->seg) hipEventDestroy(e);
   for (int k = 0; k < 4; ++k)
@@ -1268,6 +1278,9 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     return v && v[0] == '1';
   }();
   auto ms_since = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+  c->htrace = htrace;
+  for (int q = 0; q < 2 && htrace; ++q)
+    if (!c->backt[q]) HIP_TRY(hipEventCreate(&c->backt[q]), "hipEventCreate");
   auto copy_chunk = [&](uint64_t k, hipStream_t cs) {
     Extent ek, ik;
     const double h0 = htrace ? ms_since() : 0;
@@ -1355,9 +1368,11 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
       hipEventElapsedTime(&t, c->tev[0], c->segt[k]);
       fprintf(stderr, " %.3f", t);
     }
-    float t = 0;
+    float t = 0, f0 = 0, tb = 0;
     hipEventElapsedTime(&t, c->tev[0], c->tev[2]);
-    fprintf(stderr, "; verify done %.3f\n", t);
+    hipEventElapsedTime(&f0, c->tev[0], c->backt[0]);
+    hipEventElapsedTime(&tb, c->tev[0], c->backt[1]);
+    fprintf(stderr, "; chunk 0 front done %.3f, tables built %.3f, verify done %.3f\n", f0, tb, t);
   }
   if (stats) {
     float a = 0, b = 0, d = 0;

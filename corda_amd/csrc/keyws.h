@@ -153,6 +153,31 @@ static_assert(EC_QROWS <= EC_ROWS, "ECDSA quarter rows fit the full table");
 typedef EdBCfg<ED_W, ED_K, ED_WB> EdBCfgT;
 typedef EdBTabW<ED_W, ED_K, ED_WB> EdBTab;  // 26 x 512 affine niels = 1.6 MB, constant
 
+// Row-base chains are latency-bound single waves (a key's doublings are one dependent sequence);
+// beside the throughput-bound row builds they got a fraction of their SIMD's issue and ran ~4x
+// slower (profiles/r03/env_copyq). CG_CHAIN_PRIO (default 1): the chain waves raise their issue
+// priority, so a build wave on the same SIMD issues only in their stall cycles.
+#ifndef CG_CHAIN_PRIO
+#define CG_CHAIN_PRIO 1
+#endif
+__device__ __forceinline__ void chain_prio() {
+#if CG_CHAIN_PRIO
+  __builtin_amdgcn_s_setprio(3);
+#endif
+}
+
+// CG_FRONT_PRIO (A/B): the per-chunk front kernels (item build, plan, challenge hashes, ECDSA prep
+// and s^-1) raise their issue priority, so the first chunk's front is not slowed by the key-table
+// builds it shares the chip with (its ladders wait for both).
+#ifndef CG_FRONT_PRIO
+#define CG_FRONT_PRIO 0
+#endif
+__device__ __forceinline__ void front_prio() {
+#if CG_FRONT_PRIO
+  __builtin_amdgcn_s_setprio(CG_FRONT_PRIO);
+#endif
+}
+
 // Per-key header: status (0 = decoded) and, for Ed25519, the canonical Abyte i2p hashes.
 struct EdKeyHdr {
   uint32_t status;

@@ -41,6 +41,7 @@ __global__ void __launch_bounds__(256) k_plan_keys(const cg_item* __restrict__ i
                                                    const uint32_t* __restrict__ uses,
                                                    const uint32_t* __restrict__ wide_idx,
                                                    uint32_t* __restrict__ skey, uint32_t* __restrict__ sval) {
+  front_prio();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_items) return;
   const uint32_t k = items[i].key_idx;
@@ -66,6 +67,7 @@ __global__ void __launch_bounds__(256) k_plan_keys(const cg_item* __restrict__ i
 
 __global__ void k_plan_ranges(const uint32_t* __restrict__ skey, uint64_t n_items, uint32_t kb,
                               uint32_t* __restrict__ ranges) {
+  front_prio();
   // lanes 0..3: class starts ranges[c] (ranges[3] = end of the verified classes); lanes 4..6:
   // ranges[PLAN_FULL + c] = first full-table item of class c; lanes 7..9: ranges[PLAN_WIDE + c] =
   // first wide-table item; lanes 10..12: ranges[PLAN_QUART + c] = first quarter-table item (the mode

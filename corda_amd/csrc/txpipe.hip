@@ -26,6 +26,7 @@ __global__ void __launch_bounds__(256) k_txsig_items(const cg_txsig* __restrict_
                                                      const cg_signable_tmpl* __restrict__ tmpls, uint32_t n_tmpls,
                                                      const uint8_t* __restrict__ tx_status, uint64_t n_tx,
                                                      uint64_t arena_len, cg_item* __restrict__ items) {
+  front_prio();
   const uint64_t j = first + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= first + n_sigs) return;
   const cg_txsig s = sigs[j];

@@ -14,6 +14,7 @@ namespace cg {
 
 __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_items, const cg_key* __restrict__ keys,
                               uint32_t n_keys, uint8_t* __restrict__ status) {
+  front_prio();
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_items) return;
   const uint32_t ki = items[i].key_idx;
@@ -186,10 +187,13 @@ static hipError_t launch_pending_tabs(const Fork* fork, hipStream_t stream) {
   // every family's row builds after ALL the row-base chains: a chain is one lane per key (a few
   // dozen waves, latency-bound), and beside another family's row builds it ran 4x slower (r1: 5.6
   // instead of 1.3 ms, then its rows after it: profiles/r03/env_copyq timeline). CG_CHAINS_FIRST=0:
-  // each family's builds right after its own chains (A/B).
+  // each family's builds right after its own chains (A/B). Round 4: with the chains' raised issue
+  // priority (keyws.h chain_prio) the builds no longer slow them, and each family's builds start
+  // as soon as its own chains end: CG_CHAINS_FIRST=1 restores the wait for all (3 x 3 runs each:
+  // chunk 0's front done 0.5-0.8 ms earlier, ~+2% whole-node, profiles/r04/phase1)
   static const bool chains_first = [] {
     const char* v = getenv("CG_CHAINS_FIRST");
-    return !(v && v[0] == '0');
+    return v && v[0] == '1';
   }();
   for (int k = 0; k < 3 && e == hipSuccess && chains_first; ++k)
     for (int q = 0; q < 3 && e == hipSuccess; ++q)
@@ -356,13 +360,15 @@ hipError_t launch_items_front(const cg_key* d_keys, uint32_t n_keys, const cg_it
   if (e == hipSuccess && fork) e = launch_pending_tabs(fork, stream);  // the first front starts the table builds
   if (e != hipSuccess) return e;
   // fronts: Ed25519 challenges (need only Abyte), ECDSA prep + s^-1 per curve (need the decoded key).
-  // CG_EC_FRONT_SIDE=1: each curve's front on its side stream beside the challenge hashes (its
+  // CG_EC_FRONT_SIDE: each curve's front on its side stream beside the challenge hashes (its
   // s^-1 batches leave ~1 wave per SIMD: latency-bound alone), joined before that curve's ladders.
   // The side stream waits for everything enqueued on `stream` so far: this chunk's plan, and the
   // ladders of the chunk two back, which read the item workspace this front writes.
+  // Round 4 default (with CG_ED_FINISH_SIDE): 282 / 287 / 282 -> 299 / 298 / 302 M sigs/s over three
+  // interleaved runs (profiles/r04/side); =0 keeps them on `stream`.
   static const bool ec_side = [] {
     const char* v = getenv("CG_EC_FRONT_SIDE");
-    return v && v[0] == '1';
+    return !(v && v[0] == '0');
   }();
   if (fork && ec_side && fork->ec_front_go) {
     e = hipEventRecord(fork->ec_front_go, stream);
@@ -430,8 +436,25 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
   CG_TIME(fork, CG_STAGE_ED_LADDER, stream, ed_launch_ladder(true, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (w.cap_ed)
     CG_TIME(fork, CG_STAGE_ED_LADDER_WIDE, stream, ed_launch_ladder_wide(d_items, n_items, d_status, w, iw, d_btab, stream));
-  if (fork) hipStreamWaitEvent(stream, fork->row0[2], 0);
-  CG_TIME(fork, CG_STAGE_ED_FINISH, stream, ed_launch_finish(d_items, n_items, d_arena, arena_len, d_status, iw, stream));
+  // CG_ED_FINISH_SIDE: the finish (16 items per lane share an inversion: ~1.6 waves per SIMD,
+  // latency-bound) runs on side stream 2 after the row-0 ladders there, beside the ECDSA ladders on
+  // this stream; the stream joins on it at the end of the back
+  static const bool fin_side = [] {  // default on (CG_EC_FRONT_SIDE's note); =0: on `stream`
+    const char* v = getenv("CG_ED_FINISH_SIDE");
+    return !(v && v[0] == '0');
+  }();
+  if (fork && fin_side) {
+    e = hipEventRecord(fork->front, stream);  // the Ed25519 ladders on this stream are enqueued
+    if (e == hipSuccess) e = hipStreamWaitEvent(fork->side[2], fork->front, 0);
+    if (e != hipSuccess) return e;
+    CG_TIME(fork, CG_STAGE_ED_FINISH, fork->side[2],
+            ed_launch_finish(d_items, n_items, d_arena, arena_len, d_status, iw, fork->side[2]));
+    e = hipEventRecord(fork->row0[2], fork->side[2]);
+    if (e != hipSuccess) return e;
+  } else {
+    if (fork) hipStreamWaitEvent(stream, fork->row0[2], 0);
+    CG_TIME(fork, CG_STAGE_ED_FINISH, stream, ed_launch_finish(d_items, n_items, d_arena, arena_len, d_status, iw, stream));
+  }
   if (fork) hipStreamWaitEvent(stream, fork->ready[0], 0);
   if (fork && fork->pending.ec_front_side) hipStreamWaitEvent(stream, fork->ec_front_done[0], 0);
   CG_TIME(fork, CG_STAGE_R1_LADDER, stream,
@@ -449,6 +472,7 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
   if (fork) {
     hipStreamWaitEvent(stream, fork->row0[0], 0);
     hipStreamWaitEvent(stream, fork->row0[1], 0);
+    if (fin_side) hipStreamWaitEvent(stream, fork->row0[2], 0);
   }
   return hipGetLastError();
 }

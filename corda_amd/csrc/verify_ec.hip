@@ -51,6 +51,7 @@ __global__ void __launch_bounds__(64) k_ec_keyprep_chain(uint32_t n_keys, const 
                                                          const uint32_t* __restrict__ quart,
                                                          const uint32_t* __restrict__ full_count,
                                                          BaseSlot* __restrict__ bases) {
+  chain_prio();
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   const int c = plan_class_of_curve(C);
   const uint32_t nf = full_count[c], nq = full_count[QUART_COUNT_AT + c];
@@ -113,6 +114,7 @@ __global__ void __launch_bounds__(64) k_ec_wide_chain(uint32_t n_keys, const EdK
                                                       const uint32_t* __restrict__ wide_count,
                                                       const uint32_t* __restrict__ wide_idx,
                                                       const BaseSlot* __restrict__ bases, EcWideSlot* __restrict__ wec) {
+  chain_prio();
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   const int c = plan_class_of_curve(C);
   if (l >= wide_count[c]) return;
@@ -243,6 +245,7 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
                                                  const uint8_t* __restrict__ msgs, uint64_t msgs_len,
                                                  uint32_t mode, uint8_t* __restrict__ status,
                                                  EcItemWs* __restrict__ ws) {
+  front_prio();
   EC_RANGE(C);
   // each lane's signature staged in LDS (21 dwords from its 4-aligned start: up to EC_SIG_STAGED
   // bytes) with six 16-byte loads, then parsed byte by byte from there (ecdsa.h DerStaged)
@@ -302,6 +305,7 @@ __global__ void __launch_bounds__(256) k_ec_prep(const cg_item* __restrict__ ite
 template <int C>
 __global__ void __launch_bounds__(256) k_ec_inv(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
                                                 const uint8_t* __restrict__ status, EcItemWs* __restrict__ ws) {
+  front_prio();
   EC_RANGE(C);
   for (Walk wk = walk_units((end - beg + EC_INV_K - 1) / EC_INV_K); wk.u < wk.end; wk.u += wk.step) {
     const uint64_t base = beg + wk.u * EC_INV_K;

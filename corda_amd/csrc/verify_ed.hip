@@ -105,6 +105,7 @@ __global__ void __launch_bounds__(64) k_ed_keyprep_chain(uint32_t n_keys, const 
                                                          const uint32_t* __restrict__ quart,
                                                          const uint32_t* __restrict__ full_count,
                                                          BaseSlot* __restrict__ bases) {
+  chain_prio();
   // lanes [0, nf): full-table keys (21 x 12 doublings); [nf, nf + nq): quarter keys (3 x 66)
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nf = full_count[PLAN_ED], nq = full_count[QUART_COUNT_AT + PLAN_ED];
@@ -168,6 +169,7 @@ __global__ void __launch_bounds__(64) k_ed_wide_chain(uint32_t n_keys, const EdK
                                                       const uint32_t* __restrict__ wide_count,
                                                       const uint32_t* __restrict__ wide_idx,
                                                       const BaseSlot* __restrict__ bases, EdWideSlot* __restrict__ wed) {
+  chain_prio();
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= wide_count[PLAN_ED]) return;
   const uint32_t i = wide[(size_t)PLAN_ED * n_keys + l];
@@ -446,6 +448,7 @@ __global__ void __launch_bounds__(256, ED_HASH_WAVES_PER_SIMD) k_ed_hash(
     const EdKeyHdr* __restrict__ hdr, const uint8_t* __restrict__ arena, uint64_t arena_len,
     const uint8_t* __restrict__ msgs, uint64_t msgs_len, uint32_t mode, uint8_t* __restrict__ status,
     EdDigits* __restrict__ dig, EdCols ec) {
+  front_prio();
   const uint32_t beg = ranges[PLAN_ED], wbeg = ranges[PLAN_WIDE + PLAN_ED];
   for (Walk w = walk_units(ranges[PLAN_ED + 1] - beg); w.u < w.end; w.u += w.step)
     ed_hash_one<Fused>(beg + w.u, items, perm, hdr, arena, arena_len, msgs, msgs_len, mode, status, dig,

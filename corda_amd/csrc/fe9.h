@@ -191,6 +191,9 @@ CG_HD void fe9_mul(fe9& out, const fe9& a, const fe9& b) {
   acc_t acc = Signed ? (acc_t)(-(int64_t)19 * ((int64_t)1 << 40)) : 0;
 #pragma unroll
   for (int m = 0; m < 9; ++m) {
+#ifndef FE9_PIN_ACC  // round 4: 2326 -> 2217 VALU per two additions (v_lshl_add_u64 126 -> 22, plus
+#define FE9_PIN_ACC 1  // 333 s_nop the other waves fill), k_ed_ladder_wide 2.80 -> 2.68 ms (profiles/r04/pin)
+#endif
 #ifndef FE9_SCAN_ASM  // 1: pinned MACs (fe9_mac_*): 1004 -> 993 VALU per addition, but 176 s_nop (rejected)
 #define FE9_SCAN_ASM 0
 #endif
@@ -205,6 +208,11 @@ CG_HD void fe9_mul(fe9& out, const fe9& a, const fe9& b) {
       } else {
         acc += (acc_t)((uint64_t)a.v[i] * b.v[m - i]);
       }
+#if defined(__HIP_DEVICE_COMPILE__) && FE9_PIN_ACC
+      // the running column sum as an opaque value after every MAC: the carry-in then stays the
+      // first MAC's addend instead of being re-associated into a separate 64-bit add
+      asm volatile("" : "+v"(acc));
+#endif
     }
     if (m <= 7) acc = (acc_t)fe9_mac_u((uint32_t)hc[m], k1216, (uint64_t)acc);
     if (m >= 1) {

@@ -278,6 +278,8 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
     const char* v = getenv("CG_SERIAL_KEYPREP");
     return v && v[0] == '1';
   }();
+  if (fork)  // every mode's ladders unless this call's host counts prove otherwise (below)
+    for (int f = 0; f < 3; ++f) fork->pending.need_full[f] = true;
   if (!fork || serial) {
     if (fork) {  // the item stages still wait for these events
       fork->pending.on = false;
@@ -315,7 +317,6 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   fork->pending.n_keys = n_keys;
   fork->pending.keyprep = d_keyprep;
   fork->pending.wide = counted && wide ? *wide : WidePool{};
-  for (int f = 0; f < 3; ++f) fork->pending.need_full[f] = true;
   static const bool skip_full = [] {  // CG_SKIP_EMPTY_TABS=0: always launch the row-0 / full builds (A/B)
     const char* v = getenv("CG_SKIP_EMPTY_TABS");
     return !(v && v[0] == '0');
@@ -420,12 +421,17 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
     for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipStreamWaitEvent(fork->side[k], fork->front, 0);
     if (e != hipSuccess) return e;
   }
-  CG_TIME(fork, CG_STAGE_ED_LADDER_ROW0, fork ? fork->side[2] : stream,
-          ed_launch_ladder(false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[2] : stream));
-  CG_TIME(fork, CG_STAGE_R1_LADDER_ROW0, fork ? fork->side[0] : stream,
-          ec_launch_ladder(CG_CURVE_R1, false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[0] : stream));
-  CG_TIME(fork, CG_STAGE_K1_LADDER_ROW0, fork ? fork->side[1] : stream,
-          ec_launch_ladder(CG_CURVE_K1, false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[1] : stream));
+  // (a family whose host counts prove it has no row-0 / quarter key launches none: launch_keyprep)
+  const bool* nf = fork ? fork->pending.need_full : nullptr;
+  if (!nf || nf[2])
+    CG_TIME(fork, CG_STAGE_ED_LADDER_ROW0, fork ? fork->side[2] : stream,
+            ed_launch_ladder(false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[2] : stream));
+  if (!nf || nf[0])
+    CG_TIME(fork, CG_STAGE_R1_LADDER_ROW0, fork ? fork->side[0] : stream,
+            ec_launch_ladder(CG_CURVE_R1, false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[0] : stream));
+  if (!nf || nf[1])
+    CG_TIME(fork, CG_STAGE_K1_LADDER_ROW0, fork ? fork->side[1] : stream,
+            ec_launch_ladder(CG_CURVE_K1, false, d_items, n_items, d_status, w, iw, d_btab, fork ? fork->side[1] : stream));
   if (fork) {
     for (int k = 0; k < 3 && e == hipSuccess; ++k) e = hipEventRecord(fork->row0[k], fork->side[k]);
     if (e != hipSuccess) return e;

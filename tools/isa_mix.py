@@ -1,5 +1,5 @@
 """VALU instruction mix of a kernel's hottest loop from its gfx950 assembly, priced with the measured
-per-instruction chip rates (profiles/r01/ubench_int.json), to turn rocprof's SQ_INSTS_VALU count into
+per-instruction chip rates (profiles/r04/ubench/, round 1's in profiles/r01/ubench_int.json), to turn rocprof's SQ_INSTS_VALU count into
 an issue-time estimate that does not assume every wave64 VALU op costs the same (VERDICT r1:
 "replace the 4-cycle issue_frac with per-opcode costs").
 
@@ -18,9 +18,11 @@ import re
 import sys
 
 SIMD_NS = lambda rate: 64 * 1024 / rate * 1e9  # noqa: E731
-RATES = {"v_mad_u64_u32": 2.7944e13, "v_add_u32": 5.9314e13, "v_add_co_u32": 3.6235e13,
-         "v_addc_co_u32": 3.6825e13, "v_mul_lo_u32": 3.3284e13, "v_mul_hi_u32": 3.5311e13,
-         "v_lshl_add_u32": 3.7817e13, "v_alignbit_b32": 3.7380e13, "v_lshlrev_b64": 3.6791e13}
+# round 4 (profiles/r04/ubench/ubench_peak_summary.json: 16 chains, 8 waves per SIMD); addc and
+# mul_hi priced as their measured siblings
+RATES = {"v_mad_u64_u32": 3.6412e13, "v_add_u32": 5.3575e13, "v_add_co_u32": 3.7041e13,
+         "v_addc_co_u32": 3.7041e13, "v_mul_lo_u32": 3.4681e13, "v_mul_hi_u32": 3.4681e13,
+         "v_lshl_add_u32": 3.6414e13, "v_alignbit_b32": 3.3392e13, "v_lshlrev_b64": 3.6807e13}
 FAST_VOP = SIMD_NS(RATES["v_add_u32"])
 SLOW_VOP3 = SIMD_NS(RATES["v_lshl_add_u32"])
 

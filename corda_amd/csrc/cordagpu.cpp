@@ -1282,52 +1282,12 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   c->htrace = htrace;
   for (int q = 0; q < 2 && htrace; ++q)
     if (!c->backt[q]) HIP_TRY(hipEventCreate(&c->backt[q]), "hipEventCreate");
-  // Chunks 1.. get their extents from a background thread started once chunk 0 is copied: the
-  // scan (~0.75 ms on 16 threads for a 2.6M-signature chunk) then overlaps the previous chunk's copy
-  // instead of delaying this one's (the host loop scan + copy per chunk had become slower than the
-  // device's per-chunk work: 0.6-0.8 ms idle on the main stream between chunks, profiles/r04/headline)
-  struct ExtentsAhead {
-    std::vector<Extent> ext, idx;
-    std::vector<char> done;
-    std::mutex mu;
-    std::condition_variable cv;
-    std::thread th;
-    ~ExtentsAhead() {
-      if (th.joinable()) th.join();
-    }
-  } ahead;
-  ahead.ext.resize(nch);
-  ahead.idx.resize(nch);
-  ahead.done.assign(nch, 0);
-  static const bool scan_ahead = [] {  // CG_EXTENTS_AHEAD=0: scan each chunk just before its copy (A/B)
-    const char* v = getenv("CG_EXTENTS_AHEAD");
-    return !(v && v[0] == '0');
-  }();
-  auto start_ahead = [&] {
-    if (!scan_ahead || nch < 2) return;
-    ahead.th = std::thread([&] {
-      for (uint64_t k = 1; k < nch; ++k) {
-        Extent e, i;
-        chunk_extents(k, e, i);
-        std::lock_guard<std::mutex> g(ahead.mu);
-        ahead.ext[k] = e;
-        ahead.idx[k] = i;
-        ahead.done[k] = 1;
-        ahead.cv.notify_all();
-      }
-    });
-  };
   auto copy_chunk = [&](uint64_t k, hipStream_t cs) {
     Extent ek, ik;
     const double h0 = htrace ? ms_since() : 0;
-    if (k > 0 && ahead.th.joinable()) {
-      std::unique_lock<std::mutex> g(ahead.mu);
-      ahead.cv.wait(g, [&] { return ahead.done[k] != 0; });
-      ek = ahead.ext[k];
-      ik = ahead.idx[k];
-    } else {
-      chunk_extents(k, ek, ik);
-    }
+    // (scanning the later chunks' extents ahead in a background thread measured neutral to -1%:
+    // the copies' landing times did not move, profiles/r04/ahead)
+    chunk_extents(k, ek, ik);
     const double h1 = htrace ? ms_since() : 0;
     const uint64_t first = bounds[k], cnt = bounds[k + 1] - bounds[k];
     hipError_t e = hipMemcpyAsync((cg_txsig*)c->h_sigs.p + first, sigs + first, sizeof(cg_txsig) * cnt,
@@ -1381,7 +1341,6 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   hipError_t copy_err = hipSuccess;
   const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t, uint64_t) {
     hipError_t e = overlap && k == 0 ? hipSuccess : copy_chunk(k, c->copy);
-    if (k == 0) start_ahead();  // after chunk 0's own scan: the two would share the host threads
     if (e == hipSuccess) e = hipStreamWaitEvent(s, c->seg[k], 0);
     if (e == hipSuccess && k == 0) e = hipEventRecord(c->tev[1], s);
     if (e != hipSuccess) copy_err = e;

@@ -104,6 +104,11 @@ struct cg_ctx {
   // the tx-signature host path's second copy stream (chunk 0's bytes while the key-use counts are
   // sampled) and a pinned buffer for those counts (a pinned copy does not queue behind a pageable one)
   hipStream_t copy2 = nullptr;
+  // CG_FRONT_STREAM=1: the host tx-signature path runs each chunk's main-stream front (items, plan,
+  // challenge hashes) on fstream, so chunk k + 1's front overlaps chunk k's back; fev[2 k] / [2 k + 1]:
+  // chunk k's front / back done; fs_active: the stream the prepare hooks enqueue on during a call
+  hipStream_t fstream = nullptr, fs_active = nullptr;
+  std::vector<hipEvent_t> fev;
   // the exact key-use count (many keys): per host thread a byte counter per key (a wrap to 0 logs
   // the key in ovf: +256), kept across calls so a call does not page-fault 16 fresh arrays in
   std::vector<std::vector<uint8_t>> cnt8;
@@ -114,6 +119,8 @@ struct cg_ctx {
   hipEvent_t tev[4] = {};
   std::vector<hipEvent_t> segt;  // CG_HOST_TRACE: timing events behind each chunk's copy
   hipEvent_t backt[2] = {nullptr, nullptr};  // CG_HOST_TRACE: chunk 0's back enqueued / tables ready
+  std::vector<hipEvent_t> fbt;  // CG_HOST_TRACE: per chunk, the main stream reaching its front / its back's end
+  std::vector<double> fbh;      // host ms at which chunk k's front kernels were enqueued
   bool htrace = false;
   // the end of the last call's device work, whatever stream it ran on: the next call waits for it
   // before touching the shared workspace (async calls on different streams)
@@ -260,13 +267,47 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
       for (int q = 0; q < 3; ++q) hipStreamWaitEvent(t, c->fork.ready[q], 0);
       hipEventRecord(c->backt[1], t);
     }
-    return cg::launch_items_back(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, d_status + at(k),
-                                 c->keyprep.p, ws(k), c->btab.p, s, &c->fork, &wp);
+    c->fork.mark = c->htrace && 3 * k + 2 < c->fbt.size() ? c->fbt[3 * k + 2] : nullptr;  // before the joins
+    const hipError_t r = cg::launch_items_back(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len,
+                                               d_status + at(k), c->keyprep.p, ws(k), c->btab.p, s, &c->fork, &wp);
+    c->fork.mark = nullptr;
+    if (c->htrace && 3 * k + 1 < c->fbt.size()) hipEventRecord(c->fbt[3 * k + 1], s);  // back k ends
+    return r;
   };
   if (prepare_blocks) {
     // host copies in the prepare hook block the enqueuing thread: chunk k's back goes in before
     // chunk k + 1's copy, so the device runs chunk k's ladders during it (with chunk k + 1's front
     // first, chunk k's ladders waited for chunk k + 1's copy: profiles/r03/v5 timeline)
+    static const bool fstr = [] {
+      const char* v = getenv("CG_FRONT_STREAM");
+      return v && v[0] == '1';
+    }();
+    if (fstr && two && c->fstream) {
+      // front k on fstream after back k - 2 (the item workspace it reuses), back k after front k
+      while (e == hipSuccess && c->fev.size() < 2 * nch + 1) {
+        hipEvent_t ev;
+        e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e == hipSuccess) c->fev.push_back(ev);
+      }
+      const hipStream_t fs = c->fstream;
+      if (e == hipSuccess) e = hipEventRecord(c->fev[2 * nch], s);  // key prep, Abyte, tables forked
+      if (e == hipSuccess) e = hipStreamWaitEvent(fs, c->fev[2 * nch], 0);
+      c->fs_active = fs;
+      for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
+        if (k >= 2) e = hipStreamWaitEvent(fs, c->fev[2 * (k - 2) + 1], 0);
+        if (e == hipSuccess) e = (*prepare)(k, at(k), cnt(k));  // the hooks enqueue on fs_active
+        if (e == hipSuccess)
+          e = cg::launch_items_front(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, mode,
+                                     d_status + at(k), c->keyprep.p, ws(k), fs, d_msgs, msgs_len, &c->fork, &wp,
+                                     false);
+        if (e == hipSuccess) e = hipEventRecord(c->fev[2 * k], fs);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, c->fev[2 * k], 0);
+        if (e == hipSuccess) e = back(k);
+        if (e == hipSuccess) e = hipEventRecord(c->fev[2 * k + 1], s);
+      }
+      c->fs_active = nullptr;
+      return e;
+    }
     for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
       e = front(k);
       if (e == hipSuccess) e = back(k);
@@ -544,7 +585,7 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
                      prop.multiProcessorCount > 0;
     std::vector<uint32_t> mask(own ? (prop.multiProcessorCount + 31) / 32 : 0, 0u);
     for (int cu = 0; own && cu < prop.multiProcessorCount; ++cu) mask[cu / 32] |= 1u << (cu % 32);
-    for (hipStream_t* cs : {&c->copy, &c->copy2})
+    for (hipStream_t* cs : {&c->copy, &c->copy2, &c->fstream})
       if (e == hipSuccess)
         e = own ? hipExtStreamCreateWithCUMask(cs, (uint32_t)mask.size(), mask.data())
                 : hipStreamCreateWithFlags(cs, hipStreamNonBlocking);
@@ -604,12 +645,14 @@ void cg_close(cg_ctx* c) {
   if (c->fork.ec_front_go) hipEventDestroy(c->fork.ec_front_go);
   for (int k = 0; k < 2; ++k)
     if (c->fork.ec_front_done[k]) hipEventDestroy(c->fork.ec_front_done[k]);
-  for (hipStream_t* cs : {&c->copy, &c->copy2})
+  for (hipStream_t* cs : {&c->copy, &c->copy2, &c->fstream})
     if (*cs) {
       hipStreamSynchronize(*cs);
       hipStreamDestroy(*cs);
     }
   for (hipEvent_t e : c->segt) hipEventDestroy(e);
+  for (hipEvent_t e : c->fev) hipEventDestroy(e);
+  for (hipEvent_t e : c->fbt) hipEventDestroy(e);
   for (hipEvent_t e : c->backt)
     if (e) hipEventDestroy(e);
   if (c->pin_counts) hipHostFree(c->pin_counts);
@@ -1022,7 +1065,7 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
     hipError_t r = ready ? (*ready)(k, first, cnt) : hipSuccess;
     if (r == hipSuccess)
       r = cg::launch_tx_sig_range(d_sigs, first, cnt, dt, n_tmpls, nullptr, n_ids, d_ids, arena_len, slot,
-                                  (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s);
+                                  (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, c->fs_active ? c->fs_active : s);
     return r;
   };
   if (e == hipSuccess)
@@ -1282,6 +1325,12 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   c->htrace = htrace;
   for (int q = 0; q < 2 && htrace; ++q)
     if (!c->backt[q]) HIP_TRY(hipEventCreate(&c->backt[q]), "hipEventCreate");
+  while (htrace && c->fbt.size() < 3 * nch) {
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreate(&ev), "hipEventCreate");
+    c->fbt.push_back(ev);
+  }
+  if (htrace) c->fbh.assign(nch, 0.0);
   auto copy_chunk = [&](uint64_t k, hipStream_t cs) {
     Extent ek, ik;
     const double h0 = htrace ? ms_since() : 0;
@@ -1341,8 +1390,13 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   hipError_t copy_err = hipSuccess;
   const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t, uint64_t) {
     hipError_t e = overlap && k == 0 ? hipSuccess : copy_chunk(k, c->copy);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, c->seg[k], 0);
-    if (e == hipSuccess && k == 0) e = hipEventRecord(c->tev[1], s);
+    const hipStream_t fs = c->fs_active ? c->fs_active : s;  // the stream chunk k's front runs on
+    if (e == hipSuccess) e = hipStreamWaitEvent(fs, c->seg[k], 0);
+    if (e == hipSuccess && htrace && 3 * k < c->fbt.size()) {
+      c->fbh[k] = ms_since();
+      e = hipEventRecord(c->fbt[3 * k], fs);  // the front's stream reaches chunk k's front
+    }
+    if (e == hipSuccess && k == 0) e = hipEventRecord(c->tev[1], fs);
     if (e != hipSuccess) copy_err = e;
     return e;
   };
@@ -1376,6 +1430,14 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     hipEventElapsedTime(&f0, c->tev[0], c->backt[0]);
     hipEventElapsedTime(&tb, c->tev[0], c->backt[1]);
     fprintf(stderr, "; chunk 0 front done %.3f, tables built %.3f, verify done %.3f\n", f0, tb, t);
+    for (uint64_t k = 0; k < nch && 3 * k + 2 < c->fbt.size(); ++k) {
+      float fs = 0, be = 0, bj = 0;
+      hipEventElapsedTime(&fs, c->tev[0], c->fbt[3 * k]);
+      hipEventElapsedTime(&bj, c->tev[0], c->fbt[3 * k + 2]);
+      hipEventElapsedTime(&be, c->tev[0], c->fbt[3 * k + 1]);
+      fprintf(stderr, "[cg host] chunk %llu: front enqueued (host) %.3f, front reached (device) %.3f, back's "
+              "kernels done %.3f, joins done %.3f\n", (unsigned long long)k, c->fbh[k], fs, bj, be);
+    }
   }
   if (stats) {
     float a = 0, b = 0, d = 0;

@@ -747,6 +747,121 @@ CG_HD void ed_wide_row_build(Out* out, const Park& pk, const ge_p3& P, int e0, i
   }
 }
 
+// ed_wide_row_build in the radix-2^29 arithmetic (fe9.h), the form k_ed_wide_rows runs (round 4):
+// the walk R += P by the cached addition in fe9 (every product's operand classes: A = (Y1+X1)(y+x)
+// uu A2 x T, B = (Y1-X1)(y-x) ss S x T, C = T1 2dT uu T x T, D = Z1 2Z uu T x T; E = A - B (S),
+// H = A + B (A2), G = D + C (A2), F = D + 128p - C (V); X3 = E F ss S x V, Y3 = G H uu A2 x A2,
+// Z3 = G F uu A2 x V, T3 = E H ss S x A2), the cached P, 1/(2 Z) and 4d made tight once per lane
+// in radix 2^25.5, the entries' sums carried to tight limbs (fe9_carry). The same entries as
+// ed_wide_row_build, equal mod p (test_ed_wide_row_build9_matches).
+#define ED_PARK9_DWORDS 36  // X, Y, Z and the running product: 4 x 9 limbs
+struct EdPark9Lanes {
+  uint32_t* base;
+  uint32_t lane, lanes;
+  CG_HDM void st(int k, int q, const fe9& f) const {
+    uint32_t* p = base + (size_t)(k * ED_PARK9_DWORDS + q * 9) * lanes + lane;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) p[(size_t)d * lanes] = f.v[d];
+  }
+  CG_HDM void ld(int k, int q, fe9& f) const {
+    const uint32_t* p = base + (size_t)(k * ED_PARK9_DWORDS + q * 9) * lanes + lane;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) f.v[d] = p[(size_t)d * lanes];
+  }
+};
+template <class Park>
+CG_HD void ed_wide_row_build9(ge9_niels* out, const Park& pk, const ge_p3& P, int e0, int e1, const fe& d2) {
+  fe9 cYpX, cYmX, cZ2, cT2d, d4;
+  {  // the cached P and 4d, tight
+    fe t;
+    fe_add(t, P.Y, P.X);
+    fe_carry(t);
+    fe9_from_fe(cYpX, t);
+    fe_sub(t, P.Y, P.X);
+    fe_carry(t);
+    fe9_from_fe(cYmX, t);
+    fe_add(t, P.Z, P.Z);
+    fe_carry(t);
+    fe9_from_fe(cZ2, t);
+    fe_mul(t, P.T, d2);
+    fe9_from_fe(cT2d, t);
+    fe_add(t, d2, d2);
+    fe_carry(t);
+    fe9_from_fe(d4, t);
+  }
+  ge9_p3 R;
+  {
+    ge_p3 R0;
+    if (e0 == 0) R0 = P;
+    else ed_small_mul(R0, P, (uint32_t)e0 + 1u, d2);
+    ge9_from_p3(R, R0);
+  }
+  fe9 run = R.Z;
+#pragma unroll 1
+  for (int k = e0; k < e1; ++k) {
+    if (k > e0) {
+      fe9 a, b, A, B, C, D, E, H, G, F;
+      fe9_add(a, R.Y, R.X);
+      fe9_sub(b, R.Y, R.X);
+      fe9_mul<false>(A, a, cYpX);
+      fe9_mul<true>(B, b, cYmX);
+      fe9_mul<false>(C, R.T, cT2d);
+      fe9_mul<false>(D, R.Z, cZ2);
+      fe9_sub(E, A, B);
+      fe9_add(H, A, B);
+      fe9_add(G, D, C);
+      fe9_subk(F, D, C);
+      fe9_mul<true>(R.X, E, F);
+      fe9_mul<false>(R.Y, G, H);
+      fe9_mul<false>(R.Z, G, F);
+      fe9_mul<true>(R.T, E, H);
+      fe9_mul<false>(run, run, R.Z);
+    }
+    const int i = k - e0;
+    pk.st(i, 0, R.X);
+    pk.st(i, 1, R.Y);
+    pk.st(i, 2, R.Z);
+    pk.st(i, 3, run);
+  }
+  fe9 inv;
+  {  // 1 / (2 Z_e0 .. Z_e1-1): the half-scaled entries' 1/2, one inversion in radix 2^25.5
+    fe r, h, t;
+    fe_from_fe9(r, run);
+    fe_invert(t, r);
+    fe_half(h);
+    fe_mul(r, t, h);
+    fe9_from_fe(inv, r);
+  }
+#pragma unroll 1
+  for (int k = e1 - 1; k >= e0; --k) {
+    const int i = k - e0;
+    fe9 X, Y, zi;
+    pk.ld(i, 0, X);
+    pk.ld(i, 1, Y);
+    if (k > e0) {
+      fe9 pr, Z;
+      pk.ld(i - 1, 3, pr);
+      pk.ld(i, 2, Z);
+      fe9_mul<false>(zi, inv, pr);
+      fe9_mul<false>(inv, inv, Z);
+    } else {
+      zi = inv;
+    }
+    fe9 x, y, s, xy;
+    fe9_mul<false>(x, X, zi);
+    fe9_mul<false>(y, Y, zi);
+    ge9_niels n;
+    fe9_add(s, y, x);
+    fe9_carry(n.ypx, s);
+    fe9_subk(s, y, x);
+    fe9_carry(n.ymx, s);
+    fe9_mul<false>(xy, x, y);
+    fe9_mul<false>(n.xy2d, xy, d4);
+    n.pad = 0;
+    out[k] = n;
+  }
+}
+
 // Full / row-0 row of plain niels multiples 1..M of P (ed_row_build's entries) with the walk parked
 // in `pk` (EdParkLanes: lane-interleaved, so a wave's stores are coalesced; ed_row_build parks in
 // the row's own entries, 64 cache lines per store of a wave: the 2^20-distinct-key leg's row-0

@@ -99,6 +99,7 @@ struct Fork {
   // ECDSA fronts on side[k] (CG_EC_FRONT_SIDE): main's plan done / curve k's front done
   hipEvent_t ec_front_go = nullptr, ec_front_done[2] = {nullptr, nullptr};
   mutable PendingTabs pending;
+  hipEvent_t mark = nullptr;  // CG_HOST_TRACE: recorded on the main stream before a back's final joins
 };
 
 // Dynamic LDS reserved by each row-base chain workgroup (CG_CHAIN_SPREAD=1: more than half a CU's

@@ -111,6 +111,25 @@ CG_HD void fe9_subk(fe9& h, const fe9& f, const fe9& g) {
     h.v[i] = (f.v[i] + k) - g.v[i];
   }
 }
+// Non-negative limbs below 2^31 (classes A2, V) -> tight (class T): one carry pass, the bits of
+// weight >= 2^261 folded back as 1216 into limb 0 and its carry into limb 1
+CG_HD void fe9_carry(fe9& h, const fe9& f) {
+  uint32_t n[9];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    FE_ASSERT(f.v[i] < (1u << 31));
+    c += f.v[i];
+    n[i] = (uint32_t)c & FE9_M;
+    c >>= 29;
+  }
+  const uint64_t x0 = (uint64_t)n[0] + c * 1216u;
+  h.v[0] = (uint32_t)x0 & FE9_M;
+  h.v[1] = n[1] + (uint32_t)(x0 >> 29);
+  FE_ASSERT(h.v[1] < (1u << 29) + (1u << 17));
+#pragma unroll
+  for (int i = 2; i < 9; ++i) h.v[i] = n[i];
+}
 CG_HD void fe9_cmov(fe9& h, const fe9& a, const fe9& b, bool take_b) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) h.v[i] = take_b ? b.v[i] : a.v[i];

@@ -476,6 +476,7 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
     CG_TIME(fork, CG_STAGE_K1_LADDER_WIDE, stream,
             ec_launch_ladder_wide(CG_CURVE_K1, d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) {
+    if (fork->mark) hipEventRecord(fork->mark, stream);
     hipStreamWaitEvent(stream, fork->row0[0], 0);
     hipStreamWaitEvent(stream, fork->row0[1], 0);
     if (fin_side) hipStreamWaitEvent(stream, fork->row0[2], 0);

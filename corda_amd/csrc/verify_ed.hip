@@ -234,6 +234,9 @@ __global__ void __launch_bounds__(64) k_ed_wide_bwd(uint32_t n_keys, const EdKey
                            c_ed.d2);
 }
 
+#ifndef ED_WIDE_ROWS9  // 1: the row walk in radix 2^29 (ed_wide_row_build9), 0: radix 2^25.5 (A/B)
+#define ED_WIDE_ROWS9 1
+#endif
 #ifndef ED_WIDE_ROWS_WAVES  // waves per SIMD the register allocation must allow
 #define ED_WIDE_ROWS_WAVES 2  // 3 spills 125 VGPRs
 #endif
@@ -249,8 +252,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ED_WIDE
   if (hdr[i].status != 0) return;
   EdWideSlot& ws = wed[wide_idx[i]];
   constexpr int per = EdWideCfg::kMult / ED_WIDE_ROW_LANES;
-  const EdParkLanes pk{ws.park, L.j * ED_WIDE_ROW_LANES + L.g, (uint32_t)(EdWideCfg::kRows * ED_WIDE_ROW_LANES)};
-  ed_wide_row_build(ws.tab.t[L.j], pk, ws.bases[L.j], per * (int)L.g, per * (int)L.g + per, c_ed.d2);
+  const uint32_t lane = L.j * ED_WIDE_ROW_LANES + L.g, lanes = (uint32_t)(EdWideCfg::kRows * ED_WIDE_ROW_LANES);
+#if ED_WIDE_ROWS9
+  ed_wide_row_build9(ws.tab.t[L.j], EdPark9Lanes{ws.park, lane, lanes}, ws.bases[L.j], per * (int)L.g,
+                     per * (int)L.g + per, c_ed.d2);
+#else
+  ed_wide_row_build(ws.tab.t[L.j], EdParkLanes{ws.park, lane, lanes}, ws.bases[L.j], per * (int)L.g,
+                    per * (int)L.g + per, c_ed.d2);
+#endif
 }
 #ifndef CG_ED_WIDE_ROWS
 #define CG_ED_WIDE_ROWS 1

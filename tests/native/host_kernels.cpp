@@ -631,6 +631,26 @@ extern "C" int t_ed_wide_row_cmp(uint32_t m) {
       ed_wide_row_build(a2, EdParkLanes{park, (uint32_t)g, 4u}, P, 32 * g, 32 * g + 32, g_C.d2);
     if (memcmp(a, a2, sizeof a) != 0) return -1;
   }
+  {  // k_ed_wide_rows' radix-2^29 walk (ed_wide_row_build9, split in 2 lanes): equal mod p
+    static ge9_niels a9[EdWideCfg::kMult];
+    static uint32_t park9[EdWideCfg::kMult * ED_PARK9_DWORDS];
+    for (int g = 0; g < 2; ++g)
+      ed_wide_row_build9(a9, EdPark9Lanes{park9, (uint32_t)g, 2u}, P, 64 * g, 64 * g + 64, g_C.d2);
+    for (int k = 0; k < EdWideCfg::kMult; ++k) {
+      const fe* fa[3] = {&a[k].ypx, &a[k].ymx, &a[k].xy2d};
+      const fe9* f9[3] = {&a9[k].ypx, &a9[k].ymx, &a9[k].xy2d};
+      for (int q = 0; q < 3; ++q) {
+        uint32_t u[8], v[8];
+        fe t;
+        fe_from_fe9(t, *f9[q]);
+        fe_tobytes_words(u, *fa[q]);
+        fe_tobytes_words(v, t);
+        if (memcmp(u, v, 32) != 0) return -2;
+        for (int i = 0; i < 9; ++i)  // tight limbs (class T): the ladder's operand bound
+          if (f9[q]->v[i] >= (i == 1 ? (1u << 29) + (1u << 17) : (1u << 29))) return -3;
+      }
+    }
+  }
   constexpr int CPG = ED_WIDE_GROUP / ED_WIDE_CHUNK;
   for (int g = 0; g < ED_WIDE_GROUPS; ++g) ed_wide_group_pass<false>((ge_niels*)nullptr, &zc[CPG * g], P, g, g_C.d2);
   fe_invert_run<ED_WIDE_CHUNKS>(zc, zc + ED_WIDE_CHUNKS);

@@ -400,8 +400,12 @@ __device__ __forceinline__ const EcAff* ec_wide_src(const EcWideTab& TQ, const E
   return &TG.t[o - EC_WIDE_DIGITS][a > 0 ? a - 1 : 0];
 }
 
+#ifndef EC_LADDER_WIDE_WAVES  // waves per SIMD the wide ladders' registers must allow: 3 (168 VGPRs, 20 B of
+#define EC_LADDER_WIDE_WAVES 3  // scratch for r1) against the compiler's 172 at 2: r1 1.73 -> 1.67 ms (profiles/r04/ecw3)
+#endif
 template <int C>
-__global__ void __launch_bounds__(256) k_ec_ladder_wide(const cg_item* __restrict__ items,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_LADDER_WIDE_WAVES)))
+k_ec_ladder_wide(const cg_item* __restrict__ items,
                                                         const uint32_t* __restrict__ perm,
                                                         const uint32_t* __restrict__ ranges,
                                                         const uint32_t* __restrict__ wide_idx,
@@ -611,7 +615,8 @@ template <int C>
 static void launch_ladder_wide_t(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
                                  const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
-  hipLaunchKernelGGL((k_ec_ladder_wide<C>), dim3(walk_grid(n_items, B, WALK_CAP(2))), dim3(B), 0, stream, d_items,
+  hipLaunchKernelGGL((k_ec_ladder_wide<C>), dim3(walk_grid(n_items, B, WALK_CAP(EC_LADDER_WIDE_WAVES))), dim3(B), 0,
+                     stream, d_items,
                      iw.perm, iw.ranges, (const uint32_t*)w.wide_idx, (const EcWideSlot*)w.wec, gwide(d_btab, C),
                      d_status, (const EcItemWs*)iw.slots);
 }

@@ -305,9 +305,10 @@ int cg_verify_transactions(cg_ctx* ctx, const cg_tx* txs, uint64_t n_tx, const c
  * the ids it references that are not resident yet, and its signature bytes, just before the
  * chunk runs, overlapping the key-table builds and the previous chunk's kernels. stats: ms_h2d =
  * until the first chunk's bytes are resident, ms_verify = the rest, ms_key_prep = the host-side
- * planning before the first copy (a block sample of the signature table for the key-table modes:
- * 8 consecutive records per sampled group, 1 group in 32 when the keys average 256+ uses, else
- * 1 in 8; each sampled key's count estimated upward, an unsampled key counted as row-0). */
+ * planning before the first copy (the key-use counts that pick each key's table mode: when the
+ * keys average 256+ uses, a block sample of the signature table, 8 consecutive records per group,
+ * 1 group in 32, each sampled key's count estimated upward and an unsampled key counted as row-0;
+ * otherwise every record counted, exact). The counts change only speed, never a verdict. */
 int cg_verify_tx_signatures(cg_ctx* ctx, const cg_key* keys, uint32_t n_keys, const uint8_t* ids, uint64_t n_ids,
                             const cg_txsig* sigs, uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,
                             const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,

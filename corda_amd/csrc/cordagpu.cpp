@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -20,6 +21,7 @@
 
 #include "../../include/cordagpu.h"
 #include "engine.h"
+#include "host_pool.h"
 #include "pool.h"
 
 namespace {
@@ -113,6 +115,8 @@ struct cg_ctx {
   // the key in ovf: +256), kept across calls so a call does not page-fault 16 fresh arrays in
   std::vector<std::vector<uint8_t>> cnt8;
   std::vector<std::vector<uint32_t>> ovf;
+  // host threads for the tx-signature path's scans (host_pool.h), started on the first large call
+  std::unique_ptr<cg::HostPool> hpool;
   uint32_t* pin_counts = nullptr;
   size_t pin_counts_cap = 0;
   std::vector<hipEvent_t> seg;
@@ -1132,6 +1136,15 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   // scanned just before its copy, while the device works on the chunks before it.
   std::vector<uint32_t> counts(n_keys ? n_keys : 1, 0u);
   const uint64_t nt = n_sigs < (1u << 16) ? 1 : 16;
+  if (nt > 1 && !c->hpool) c->hpool.reset(new cg::HostPool((unsigned)nt - 1));
+  // fn(t) for t in [0, m): on the context's pool (spawning 16 threads per scan cost 0.35-0.5 ms a round)
+  auto par = [&](uint64_t m, const std::function<void(uint64_t)>& fn) {
+    if (m > 1 && c->hpool) {
+      c->hpool->run(m, fn);
+    } else {
+      for (uint64_t t = 0; t < m; ++t) fn(t);
+    }
+  };
   auto sample_counts = [&] {
     // 1 in S signatures counted (CG_TXSIG_SAMPLE, a power of two, overrides): S = 32 when keys average
     // at least 256 uses (every key far above the 32-use full-table threshold), else 8: at S = 32 an
@@ -1171,11 +1184,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
           if (k < n_keys && ++cc[k] == 0) of.push_back(k);
         }
       };
-      std::vector<std::thread> th;
-      for (uint64_t t = 1; t < nt; ++t) th.emplace_back(scan8, t);
-      scan8(0);
-      for (auto& t : th) t.join();
-      th.clear();
+      par(nt, scan8);
       auto sum = [&](uint64_t t) {
         for (uint64_t k = n_keys * t / nt; k < n_keys * (t + 1) / nt; ++k) {
           uint32_t v = 0;
@@ -1183,9 +1192,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
           counts[k] = v;
         }
       };
-      for (uint64_t t = 1; t < nt; ++t) th.emplace_back(sum, t);
-      sum(0);
-      for (auto& t : th) t.join();
+      par(nt, sum);
       for (uint64_t t = 0; t < nt; ++t)
         for (uint32_t k : c->ovf[t]) counts[k] += 256u;
       return;
@@ -1206,16 +1213,11 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     if (nt == 1) {
       scan(0);
     } else {
-      std::vector<std::thread> th;
-      for (uint64_t t = 0; t < nt; ++t) th.emplace_back(scan, t);
-      for (auto& t : th) t.join();
-      th.clear();
-      for (uint64_t t = 0; t < nt; ++t)  // sum the per-thread counts, key ranges in parallel
-        th.emplace_back([&, t] {
-          for (uint64_t k = n_keys * t / nt; k < n_keys * (t + 1) / nt; ++k)
-            for (uint64_t u = 0; u < nt; ++u) counts[k] += pc[u][k];
-        });
-      for (auto& t : th) t.join();
+      par(nt, scan);
+      par(nt, [&](uint64_t t) {  // sum the per-thread counts, key ranges in parallel
+        for (uint64_t k = n_keys * t / nt; k < n_keys * (t + 1) / nt; ++k)
+          for (uint64_t u = 0; u < nt; ++u) counts[k] += pc[u][k];
+      });
     }
     // c sampled uses -> S (c + 3 sqrt(c) + 1): about three standard deviations above the unbiased
     // S c, so a key whose true count clears a mode threshold is not sampled below it (two were not
@@ -1257,13 +1259,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
       pe[t] = a;
       pi[t] = b;
     };
-    if (m == 1) {
-      scan(0);
-    } else {
-      std::vector<std::thread> th;
-      for (uint64_t t = 0; t < m; ++t) th.emplace_back(scan, t);
-      for (auto& t : th) t.join();
-    }
+    par(m, scan);
     for (uint64_t t = 0; t < m; ++t) {
       ext.merge(pe[t]);
       idx.merge(pi[t]);

@@ -62,7 +62,7 @@ MAC32_PER_ED25519 = N_FE_ED25519 * 64
 ED_VERIFY_FE = (319, 24)   # k_ed_ladder_pf: 43 mixed additions + 6 doublings in radix 2^25.5 ...
 ED_VERIFY_FE9 = 83         # ... then the 12 B additions in radix 2^29 (fe9.h products)
 ED_WIDE_FE = (307, 0)      # k_ed_ladder_wide: 32 + 12 mixed additions, no doublings (keys with wide tables), all fe9
-ED_WIDE_BUILD_FE = (63399, 18016)  # one key's wide table: 248-doubling chain, then per row two lanes each walking 64 entries (the second from 65 P), one inversion each, the walk back (k_ed_wide_rows)
+ED_WIDE_BUILD_FE = (62279, 9120)  # one key's wide table: 248-doubling chain, then per row one lane walking its 128 entries, one inversion, the walk back (k_ed_wide_rows, ED_WIDE_ROW_LANES 1)
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
 ED_FINISH_K = 16

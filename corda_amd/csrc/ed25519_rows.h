@@ -910,9 +910,9 @@ CG_HD void ed_row_build_parked(ge_niels* row, const ge_p3& P, const fe& d2, cons
   }
 }
 
-#ifndef ED_WIDE_ROW_LANES  // lanes per row (as EC_WIDE_ROW_LANES)
-#define ED_WIDE_ROW_LANES 2
-#endif
+#ifndef ED_WIDE_ROW_LANES  // lanes per row (as EC_WIDE_ROW_LANES): 1 / 2 / 4 lanes, headline A/B in 3
+#define ED_WIDE_ROW_LANES 1  // rounds: 314.2 / 311.5 / 311.1 M sigs/s (profiles/r04/erl; one inversion per row,
+#endif                       // one round of 2 waves per SIMD for the 4 096 keys' 32 rows)
 static_assert(EdWideCfg::kMult % ED_WIDE_ROW_LANES == 0, "row split");
 
 // ---------------------------------------------------------------- full / row-0 tables + wide B

@@ -130,7 +130,14 @@ def parse(argv=None):
     ap.add_argument("--host-steps", type=int, default=3, help="message-form cg_verify_batch calls (0: off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU work of the baseline sample")
-    ap.add_argument("--threads", type=int, default=0, help="host threads (0: the CPU quota, at most 16)")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="host threads of this rank (0: the CPU quota / LOCAL_WORLD_SIZE, at most 16)")
+    ap.add_argument("--engine-threads", type=int, default=0,
+                    help="cg_config.host_threads of the headline context (0: this rank's share when ranks "
+                         "share the node, else the library's budget)")
+    ap.add_argument("--host-register", type=int, default=1,
+                    help="1: register the headline's host buffers once (cg_host_register: DMA straight from "
+                         "them, no CPU staging copy), as a JVM node registers its persistent direct buffers")
     ap.add_argument("--configs1-items", type=int, default=1 << 20, help="configs[1] Ed25519 secondary (0: off)")
     ap.add_argument("--ecdsa-items", type=int, default=1 << 20, help="configs[2] ECDSA 50/50 secondary (0: off)")
     ap.add_argument("--pipeline-txs", type=int, default=1 << 20, help="configs[3] transaction pipeline (0: off)")
@@ -175,10 +182,70 @@ def free_port():
     return p
 
 
+def _lib_mod():
+    from corda_amd import _lib
+    return _lib
+
+
+def kfd_gpus(sysfs="/sys/class/kfd/kfd/topology/nodes", env=None):
+    """GPUs this process may use, counted without any HIP / HSA call: the KFD topology nodes with a
+    gfx target (CPU nodes have gfx_target_version 0), cut down by ROCR_VISIBLE_DEVICES /
+    HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES the way the runtime applies them (a list of ordinals)."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        for node in sorted(os.listdir(sysfs), key=lambda x: int(x) if x.isdigit() else 1 << 30):
+            try:
+                with open(os.path.join(sysfs, node, "properties")) as f:
+                    props = dict(l.split(None, 1) for l in f if len(l.split(None, 1)) == 2)
+            except OSError:
+                continue
+            if int(props.get("gfx_target_version", "0").strip() or 0) != 0:
+                n += 1
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids))
+    return n
+
+
+def gpu_initialised(fd_dir="/proc/self/fd"):
+    """True once this process has opened /dev/kfd, i.e. the HSA runtime under HIP has initialised
+    (loading libamdhip64 with `import torch` does not open it; the first HIP call does). A process
+    that has initialised the GPU must not exec or fork a GPU world from its own image."""
+    try:
+        for fd in os.listdir(fd_dir):
+            try:
+                if os.readlink(os.path.join(fd_dir, fd)) == "/dev/kfd":
+                    return True
+            except OSError:
+                continue
+    except OSError:
+        return False
+    return False
+
+
+def rank_host_threads(req, env=None):
+    """Host threads of this rank: the process's CPU quota (host_threads) divided among the ranks on
+    the node (LOCAL_WORLD_SIZE under torchrun), at least 1; --threads wins when given."""
+    env = os.environ if env is None else env
+    if req > 0:
+        return req
+    ranks = max(1, int(env.get("LOCAL_WORLD_SIZE", "1") or 1))
+    return max(1, host_threads(0) // ranks)
+
+
 def spawn_world(nproc, argv):
-    """Start the N-rank world as a CHILD process (this process has not touched the GPU: counting
-    devices does not initialise it) and return its exit code; rank 0's stdout passes through."""
+    """Start the N-rank world as a CHILD process (this process has not touched the GPU: the device
+    count comes from sysfs, and gpu_initialised() is checked) and return its exit code; rank 0's
+    stdout passes through."""
     import subprocess
+    if gpu_initialised():
+        raise SystemExit("bench.py: the GPU runtime is already initialised in the launcher process; "
+                         "refusing to start the world from it")
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(spawn_cmd(nproc, argv, free_port()), env=env)
@@ -851,12 +918,13 @@ def main(argv=None):
     a = parse(argv)
     if a.pool_devices:
         return main_pool(a)
-    import torch
-    # decide the world before any GPU call (device_count does not initialise the GPU on this image)
-    visible = torch.cuda.device_count() if "WORLD_SIZE" not in os.environ else a.gpus
+    # decide the world before any GPU call, and before torch is imported: the device count comes
+    # from the KFD topology in sysfs (no HIP / HSA call), so the launcher never initialises the GPU
+    visible = kfd_gpus() if "WORLD_SIZE" not in os.environ else a.gpus
     how, world = launch_plan(a.gpus, os.environ, visible)
     if how == "spawn":
         sys.exit(spawn_world(world, argv))
+    import torch
     import torch.distributed as dist
 
     rank = int(os.environ.get("RANK", "0"))
@@ -866,7 +934,9 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    threads = host_threads(a.threads)
+    # this rank's share of the host: the CPU quota / the ranks on the node (the engine's scans and
+    # the workload generator both use it)
+    threads = rank_host_threads(a.threads)
 
     from corda_amd import shard
     from corda_amd.engine import Engine
@@ -884,11 +954,21 @@ def main(argv=None):
     tb = wl.tx_sig_stream(pool, pool_schemes, idx, ids, id_idx, nthreads=threads)
     labels, schemes = pool_labels[idx], pool_schemes[idx]
     gen_s = time.time() - t0
-    eng = Engine(local, chunk_items=a.chunk_items, stage_timing=True)
+    # the engine's host threads: --engine-threads, else this rank's share when ranks share the node,
+    # else 0 (the library's own budget: the CPU quota / the contexts in this process)
+    eng_threads = a.engine_threads or (threads if world > 1 else 0)
+    eng = Engine(local, chunk_items=a.chunk_items, stage_timing=True, host_threads=eng_threads)
     eng.reserve(len(batch.keys), batch.n)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
     holder = {}
+    # zero-copy ingestion: the caller's persistent buffers registered once, outside the timed region
+    # (a JVM node registers its direct-buffer arena once; cg_host_register, include/cordagpu.h)
+    registered = []
+    if a.host_register and hasattr(_lib_mod().lib(), "cg_host_register"):
+        for arr in (tb.arena, tb.sigs, tb.ids):
+            if _lib_mod().host_register(arr):
+                registered.append(arr)
 
     def step():
         # the whole node: host arena -> host verdicts, one cg_verify_tx_signatures call (synchronous)
@@ -958,6 +1038,8 @@ def main(argv=None):
                               "note": "ms_key_prep = host-side planning (the key-use sample pass), ms_h2d = until "
                                       "the first chunk's bytes are resident, ms_verify = the rest"}}
     extra["table_modes_items"] = table_modes(batch, schemes)
+    extra["host"] = {"threads": threads, "engine_host_threads": eng_threads or "library budget",
+                     "registered_bytes": int(sum(x.nbytes for x in registered))}
     cpu = None
     if rank == 0 and world == 1:
         if a.device_steps > 0:
@@ -1020,6 +1102,8 @@ def main(argv=None):
     if world > 1:
         dist.destroy_process_group()
     eng.close()
+    for arr in registered:
+        _lib_mod().host_unregister(arr)
     if failed:
         sys.exit(3)  # a wrong verdict voids the number
 

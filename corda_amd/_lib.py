@@ -30,8 +30,8 @@ class cg_stats(ctypes.Structure):
 
 class cg_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32), ("max_items", ctypes.c_uint64),
-                ("max_arena", ctypes.c_uint64), ("chunk_items", ctypes.c_uint64),
-                ("reserved", ctypes.c_uint64 * 3)]
+                ("max_arena", ctypes.c_uint64), ("chunk_items", ctypes.c_uint64), ("host_threads", ctypes.c_uint32),
+                ("reserved0", ctypes.c_uint32), ("reserved", ctypes.c_uint64 * 2)]
 
 
 class cg_pool_stats(ctypes.Structure):
@@ -96,6 +96,13 @@ def lib():
             if hasattr(L, "cg_stage_times"):
                 L.cg_stage_times.argtypes = [vp, vp, vp, u32]
                 L.cg_stage_times.restype = i32
+            if hasattr(L, "cg_host_register"):  # older builds (A/B variants) lack the registration
+                L.cg_host_register.argtypes = [vp, u64]
+                L.cg_host_register.restype = i32
+                L.cg_host_unregister.argtypes = [vp]
+                L.cg_host_unregister.restype = i32
+                L.cg_host_registered.argtypes = [vp, u64]
+                L.cg_host_registered.restype = i32
             pool = hasattr(L, "cg_pool_open")  # older builds (A/B variants) lack the pool
             if pool:
                 L.cg_pool_open.argtypes = [ctypes.POINTER(vp), vp, u32, ctypes.POINTER(cg_config)]
@@ -119,6 +126,19 @@ def lib():
                 getattr(L, name).restype = i32
             _lib = L
         return _lib
+
+
+def host_register(arr):
+    """cg_host_register over a numpy array's bytes (kept alive and unchanged by the caller until
+    host_unregister): the host entry points then copy out of it by DMA, without CPU staging."""
+    if arr is None or arr.size == 0:
+        return False
+    check(lib().cg_host_register(arr.ctypes.data, arr.nbytes), "cg_host_register")
+    return True
+
+
+def host_unregister(arr):
+    check(lib().cg_host_unregister(arr.ctypes.data), "cg_host_unregister")
 
 
 def last_error():

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cmath>
@@ -21,6 +22,7 @@
 
 #include "../../include/cordagpu.h"
 #include "engine.h"
+#include "host_budget.h"
 #include "host_pool.h"
 #include "pool.h"
 
@@ -115,8 +117,13 @@ struct cg_ctx {
   // the key in ovf: +256), kept across calls so a call does not page-fault 16 fresh arrays in
   std::vector<std::vector<uint8_t>> cnt8;
   std::vector<std::vector<uint32_t>> ovf;
-  // host threads for the tx-signature path's scans (host_pool.h), started on the first large call
+  // host threads for the host paths' scans (host_pool.h), started on the first large call and sized
+  // by the budget (host_budget.h: cg_config.host_threads, CG_HOST_THREADS, or the CPU quota divided
+  // by the contexts open in the process), re-sized when the budget changes
   std::unique_ptr<cg::HostPool> hpool;
+  uint32_t host_req = 0;   // cg_config.host_threads
+  uint32_t quota = 1;      // the process's CPUs at cg_open
+  bool counted = false;    // included in g_live_ctx
   uint32_t* pin_counts = nullptr;
   size_t pin_counts_cap = 0;
   std::vector<hipEvent_t> seg;
@@ -134,6 +141,27 @@ struct cg_ctx {
 };
 
 namespace {
+
+// contexts open in this process (the default host budget divides the CPU quota among them)
+std::atomic<unsigned> g_live_ctx{0};
+
+// The host threads a call of n items may use: 1 below 2^16 items, else the budget; the pool is
+// (re)made to match, so nt parts run on nt threads.
+unsigned host_threads_of(cg_ctx* c, uint64_t n) {
+  if (n < (1u << 16)) return 1;
+  const unsigned nt = cg::host_threads_for(c->host_req, cg::host_threads_env(), c->quota, g_live_ctx.load());
+  if (nt > 1 && (!c->hpool || c->hpool->threads() != nt)) c->hpool.reset(new cg::HostPool(nt - 1));
+  return nt;
+}
+
+// fn(t) for t in [0, m) on the context's pool (or inline)
+void host_par(cg_ctx* c, uint64_t m, const std::function<void(uint64_t)>& fn) {
+  if (m > 1 && c->hpool) {
+    c->hpool->run(m, fn);
+  } else {
+    for (uint64_t t = 0; t < m; ++t) fn(t);
+  }
+}
 
 hipError_t order_in(cg_ctx* c, hipStream_t s) { return c->done_rec ? hipStreamWaitEvent(s, c->done, 0) : hipSuccess; }
 hipError_t order_out(cg_ctx* c, hipStream_t s) {
@@ -349,32 +377,24 @@ struct HostPlan {
   Extent keys, win;             // key bytes; everything the call reads
 };
 
-void plan_host(const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items, uint64_t arena_len,
-               uint64_t per, HostPlan& P) {
+void plan_host(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,
+               uint64_t arena_len, uint64_t per, HostPlan& P) {
   for (uint32_t k = 0; k < n_keys; ++k) P.keys.add(keys[k].off, keys[k].len, arena_len);
   const uint64_t nch = (n_items + per - 1) / per;
   P.first.resize(nch + 1);
   for (uint64_t k = 0; k <= nch; ++k) P.first[k] = n_items * k / nch;
   P.ext.assign(nch, Extent());
-  // one host thread per chunk (at most 16): the scan reads 32 B per item
-  auto scan = [&](uint64_t k0, uint64_t k1) {
-    for (uint64_t k = k0; k < k1; ++k) {
-      Extent x;  // thread-local until the end (neighbouring chunks' slots share cache lines)
-      for (uint64_t i = P.first[k]; i < P.first[k + 1]; ++i) {
-        x.add(items[i].sig_off, items[i].sig_len, arena_len);
-        x.add(items[i].msg_off, items[i].msg_len, arena_len);
-      }
-      P.ext[k] = x;
+  // the chunks' scans on the context's host pool (the budget's threads): 32 B read per item
+  auto scan = [&](uint64_t k) {
+    Extent x;  // thread-local until the end (neighbouring chunks' slots share cache lines)
+    for (uint64_t i = P.first[k]; i < P.first[k + 1]; ++i) {
+      x.add(items[i].sig_off, items[i].sig_len, arena_len);
+      x.add(items[i].msg_off, items[i].msg_len, arena_len);
     }
+    P.ext[k] = x;
   };
-  const uint64_t nt = nch < 16 ? nch : 16;
-  if (n_items < (1u << 16) || nt < 2) {
-    scan(0, nch);
-  } else {
-    std::vector<std::thread> th;
-    for (uint64_t t = 0; t < nt; ++t) th.emplace_back(scan, nch * t / nt, nch * (t + 1) / nt);
-    for (auto& t : th) t.join();
-  }
+  host_threads_of(c, n_items);
+  host_par(c, nch, scan);
   P.win = P.keys;
   for (const Extent& e : P.ext) P.win.merge(e);
   if (P.win.empty()) P.win.lo = P.win.hi = 0;
@@ -419,7 +439,7 @@ int verify_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
   const uint64_t pipe = c->chunk < CG_PIPELINE_CHUNK_ITEMS ? c->chunk : CG_PIPELINE_CHUNK_ITEMS;
   HostPlan P;
-  plan_host(keys, n_keys, items, n_items, arena_len, pipe, P);
+  plan_host(c, keys, n_keys, items, n_items, arena_len, pipe, P);
   const uint64_t nch = P.ext.size();
   const uint64_t per_max = (n_items + nch - 1) / nch;
   HIP_TRY(c->keys.ensure(sizeof(cg_key) * (n_keys ? n_keys : 1)), "hipMalloc(keys)");
@@ -502,13 +522,55 @@ int cg_device_count(void) {
 
 const char* cg_last_error(void) { return g_err.c_str(); }
 
+// ---- host memory registration (include/cordagpu.h: zero-copy ingestion)
+namespace {
+struct HostRange {
+  uint64_t lo, hi;
+};
+std::mutex g_reg_mu;
+std::vector<HostRange> g_reg;  // registered ranges, disjoint
+}  // namespace
+
+int cg_host_register(const void* p, uint64_t len) {
+  if (!p || !len) return fail(CG_ERR_ARG, "cg_host_register: NULL pointer or empty range");
+  const uint64_t lo = (uint64_t)(uintptr_t)p, hi = lo + len;
+  if (hi < lo) return fail(CG_ERR_ARG, "cg_host_register: range wraps the address space");
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  for (const HostRange& r : g_reg)
+    if (lo < r.hi && r.lo < hi) return fail(CG_ERR_ARG, "cg_host_register: range overlaps a registered one");
+  // portable: every device's DMA engines may read the pages (a cg_pool's slots, one process per node)
+  HIP_TRY(hipHostRegister(const_cast<void*>(p), (size_t)len, hipHostRegisterPortable), "hipHostRegister");
+  g_reg.push_back({lo, hi});
+  return CG_OK;
+}
+
+int cg_host_unregister(const void* p) {
+  const uint64_t lo = (uint64_t)(uintptr_t)p;
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  for (size_t i = 0; i < g_reg.size(); ++i) {
+    if (g_reg[i].lo != lo) continue;
+    g_reg.erase(g_reg.begin() + (ptrdiff_t)i);
+    HIP_TRY(hipHostUnregister(const_cast<void*>(p)), "hipHostUnregister");
+    return CG_OK;
+  }
+  return fail(CG_ERR_ARG, "cg_host_unregister: pointer was not registered");
+}
+
+int cg_host_registered(const void* p, uint64_t len) {
+  const uint64_t lo = (uint64_t)(uintptr_t)p, hi = lo + len;
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  for (const HostRange& r : g_reg)
+    if (lo >= r.lo && hi <= r.hi && hi >= lo) return 1;
+  return 0;
+}
+
 static_assert(sizeof(cg_config) == 56, "cg_config is 56 bytes in ABI v2");
 static_assert(sizeof(cg_item) == 32 && sizeof(cg_key) == 16 && sizeof(cg_txsig) == 24, "ABI struct sizes");
 
 int cg_open(cg_ctx** out, const cg_config* cfg) {
   if (!out) return fail(CG_ERR_ARG, "cg_open: out is NULL");
   *out = nullptr;
-  if (cfg && (cfg->reserved[0] || cfg->reserved[1] || cfg->reserved[2]))
+  if (cfg && (cfg->reserved0 || cfg->reserved[0] || cfg->reserved[1]))
     return fail(CG_ERR_ARG, "cg_open: cg_config.reserved must be 0 (ABI v2: 56-byte cg_config)");
   if (cfg && (cfg->flags & ~CG_FLAG_STAGE_TIMING)) return fail(CG_ERR_ARG, "cg_open: unknown cg_config.flags bits");
   int dev = cfg ? cfg->device : 0;
@@ -522,6 +584,8 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     return fail(CG_ERR_DEVICE, "cg_open: kernels are built for gfx950, device is %s", prop.gcnArchName);
   cg_ctx* c = new cg_ctx();
   c->device = dev;
+  c->host_req = cfg ? cfg->host_threads : 0u;
+  c->quota = cg::cpu_quota();
   if (cfg && cfg->chunk_items) {
     c->chunk = cfg->chunk_items;
     c->chunk_set = true;
@@ -611,12 +675,15 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
     cg_close(c);
     return rc;
   }
+  c->counted = true;
+  ++g_live_ctx;
   *out = c;
   return CG_OK;
 }
 
 void cg_close(cg_ctx* c) {
   if (!c) return;
+  if (c->counted) --g_live_ctx;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   c->keyprep.release();
@@ -1135,16 +1202,10 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   // that each key an unsampled signature may use has its row-0 table. Each chunk's byte extents are
   // scanned just before its copy, while the device works on the chunks before it.
   std::vector<uint32_t> counts(n_keys ? n_keys : 1, 0u);
-  const uint64_t nt = n_sigs < (1u << 16) ? 1 : 16;
-  if (nt > 1 && !c->hpool) c->hpool.reset(new cg::HostPool((unsigned)nt - 1));
-  // fn(t) for t in [0, m): on the context's pool (spawning 16 threads per scan cost 0.35-0.5 ms a round)
-  auto par = [&](uint64_t m, const std::function<void(uint64_t)>& fn) {
-    if (m > 1 && c->hpool) {
-      c->hpool->run(m, fn);
-    } else {
-      for (uint64_t t = 0; t < m; ++t) fn(t);
-    }
-  };
+  // the budget's host threads (host_budget.h), on the context's pool (spawning 16 threads per scan
+  // cost 0.35-0.5 ms a round)
+  const uint64_t nt = host_threads_of(c, n_sigs);
+  auto par = [&](uint64_t m, const std::function<void(uint64_t)>& fn) { host_par(c, m, fn); };
   auto sample_counts = [&] {
     // 1 in S signatures counted (CG_TXSIG_SAMPLE, a power of two, overrides): S = 32 when keys average
     // at least 256 uses (every key far above the 32-use full-table threshold), else 8: at S = 32 an

@@ -18,9 +18,11 @@ def _p(a):
 
 
 class Engine:
-    def __init__(self, device=0, chunk_items=0, stage_timing=False):
+    def __init__(self, device=0, chunk_items=0, stage_timing=False, host_threads=0):
+        """host_threads: cg_config.host_threads (0: CG_HOST_THREADS, else the CPU quota divided by the
+        contexts open in this process; include/cordagpu.h)."""
         L = _lib.lib()
-        cfg = _lib.cg_config(device, _lib.FLAG_STAGE_TIMING if stage_timing else 0, 0, 0, chunk_items)
+        cfg = _lib.cg_config(device, _lib.FLAG_STAGE_TIMING if stage_timing else 0, 0, 0, chunk_items, host_threads)
         h = ctypes.c_void_p()
         _lib.check(L.cg_open(ctypes.byref(h), ctypes.byref(cfg)), f"cg_open(device={device})")
         self._h = h
@@ -211,9 +213,9 @@ class EnginePool:
     slots, re-runs a failed slot's shard elsewhere, and returns one status byte per item (items
     no slot could run stay NOT_RUN and raise ``EngineUnavailable`` unless ``allow_partial``)."""
 
-    def __init__(self, devices, chunk_items=0):
+    def __init__(self, devices, chunk_items=0, host_threads=0):
         L = _lib.lib()
-        cfg = _lib.cg_config(0, 0, 0, 0, chunk_items)
+        cfg = _lib.cg_config(0, 0, 0, 0, chunk_items, host_threads)
         devs = (ctypes.c_int32 * len(devices))(*devices)
         h = ctypes.c_void_p()
         _lib.check(L.cg_pool_open(ctypes.byref(h), devs, len(devices), ctypes.byref(cfg)), "cg_pool_open")

@@ -163,7 +163,12 @@ typedef struct cg_config {
   uint64_t max_items;    /* workspace sizing hint (0 = grow on demand) */
   uint64_t max_arena;    /* workspace sizing hint (0 = grow on demand) */
   uint64_t chunk_items;  /* items per verify chunk (0 = CG_DEFAULT_CHUNK_ITEMS) */
-  uint64_t reserved[3];  /* must be 0: cg_open rejects anything else with CG_ERR_ARG */
+  uint32_t host_threads; /* host threads of this context's scans (key-use counts, chunk extents).
+                            0 = CG_HOST_THREADS from the environment if set, else the process's CPU
+                            quota (cgroup cpu.max, affinity) divided by the contexts open in the
+                            process; at most 64. One process per GPU: pass quota / GPUs per node. */
+  uint32_t reserved0;    /* must be 0 */
+  uint64_t reserved[2];  /* must be 0: cg_open rejects anything else with CG_ERR_ARG */
 } cg_config;             /* 56 bytes (static_assert in cordagpu.cpp) */
 
 typedef struct cg_stats {
@@ -186,6 +191,19 @@ const char* cg_last_error(void); /* thread-local message for the last non-OK ret
 
 int cg_open(cg_ctx** out, const cg_config* cfg);
 void cg_close(cg_ctx* ctx);
+
+/* Host memory registration (zero-copy ingestion). A caller that keeps its buffers across calls (a
+ * JVM direct ByteBuffer arena, the out-of-process verifier's request buffers) registers them once:
+ * the pages are pinned (hipHostRegister, every device) and the host entry points' copies out of
+ * them go by DMA straight from those pages instead of through the runtime's CPU staging copy
+ * (pageable memory: the calling thread memcpys every byte into a pinned bounce buffer first).
+ * Process-wide; ranges may not overlap. The caller must unregister a range before it frees or
+ * reuses that memory for anything else. Returns CG_OK, CG_ERR_ARG (NULL, zero length, overlap,
+ * unknown pointer) or CG_ERR_DEVICE (the runtime refused). cg_host_registered: 1 if [p, p + len)
+ * lies inside one registered range, else 0. */
+int cg_host_register(const void* p, uint64_t len);
+int cg_host_unregister(const void* p);
+int cg_host_registered(const void* p, uint64_t len);
 
 /* Host buffers in, host status bytes out (what a JNI caller hands over). The key table, the key
  * bytes and the item table go first; then the items are verified in consecutive chunks of at most

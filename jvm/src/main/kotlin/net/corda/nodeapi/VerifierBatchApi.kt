@@ -29,15 +29,17 @@ object VerifierBatchApi {
     /** keys / items / arena are the cg_key / cg_item tables and the byte arena they index. */
     class BatchSignatureRequest(val verificationId: Long, val mode: Int, val nKeys: Int, val nItems: Int,
                                 val body: ByteBuffer, val responseAddress: SimpleString?) {
-        /** Direct-buffer slices of the body in the C ABI layout (for CryptoBatch.verifyPacked). */
-        fun keys(): ByteBuffer = slice(REQ_HEADER, nKeys * KEY_BYTES)
-        fun items(): ByteBuffer = slice(REQ_HEADER + nKeys * KEY_BYTES, nItems * ITEM_BYTES)
-        fun arena(): ByteBuffer = slice(REQ_HEADER + nKeys * KEY_BYTES + nItems * ITEM_BYTES, arenaLen().toInt())
+        /** Direct-buffer slices of the body in the C ABI layout (for CryptoBatch.verifyPacked). Offsets
+         *  and lengths in Long, each checked to fit the body (parse() has checked that they add up). */
+        fun keys(): ByteBuffer = slice(REQ_HEADER.toLong(), nKeys.toLong() * KEY_BYTES)
+        fun items(): ByteBuffer = slice(REQ_HEADER + nKeys.toLong() * KEY_BYTES, nItems.toLong() * ITEM_BYTES)
+        fun arena(): ByteBuffer = slice(REQ_HEADER + nKeys.toLong() * KEY_BYTES + nItems.toLong() * ITEM_BYTES, arenaLen())
         fun arenaLen(): Long = body.getLong(32)
 
-        private fun slice(off: Int, len: Int): ByteBuffer {
+        private fun slice(off: Long, len: Long): ByteBuffer {
+            if (off < 0 || len < 0 || off + len > body.limit()) throw MalformedMessage("slice outside the body")
             val d = body.duplicate()
-            d.position(off).limit(off + len)
+            d.position(Math.toIntExact(off)).limit(Math.toIntExact(off + len))
             return d.slice().order(ByteOrder.LITTLE_ENDIAN)
         }
 
@@ -70,13 +72,19 @@ object VerifierBatchApi {
                 val mode = body.getShort(6).toInt()
                 if (mode != 0 && mode != 1) throw MalformedMessage("unknown mode $mode")
                 val id = body.getLong(8)
-                val nKeys = body.getInt(16)
+                // the header's counts are unsigned (verifier.py <4sHHqIIQQ): n_keys u32, n_items and
+                // arena_len u64. A u64 with the top bit set reads as a negative Long here: rejected,
+                // as is any count whose table could not fit a body (a ByteBuffer holds < 2^31 bytes),
+                // so the sum below cannot wrap and every slice lies inside the body
+                val nKeys = body.getInt(16).toLong() and 0xffffffffL
                 val nItems = body.getLong(24)
                 val arenaLen = body.getLong(32)
-                if (nItems > Int.MAX_VALUE || nKeys < 0 ||
-                    body.limit().toLong() != REQ_HEADER + nKeys.toLong() * KEY_BYTES + nItems * ITEM_BYTES + arenaLen)
+                if (nItems < 0 || arenaLen < 0 || nKeys > Int.MAX_VALUE / KEY_BYTES ||
+                    nItems > Int.MAX_VALUE / ITEM_BYTES || arenaLen > Int.MAX_VALUE)
+                    throw MalformedMessage("a header count is out of range")
+                if (body.limit().toLong() != REQ_HEADER + nKeys * KEY_BYTES + nItems * ITEM_BYTES + arenaLen)
                     throw MalformedMessage("body length does not match the header")
-                return BatchSignatureRequest(id, mode, nKeys, nItems.toInt(), body, replyTo)
+                return BatchSignatureRequest(id, mode, nKeys.toInt(), nItems.toInt(), body, replyTo)
             }
         }
     }

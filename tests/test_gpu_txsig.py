@@ -56,6 +56,37 @@ def test_tx_signatures_host_and_device_vs_oracle(spool):
             assert np.array_equal(st_m, st[:20000])
 
 
+def test_registered_host_buffers_and_thread_budgets(spool):
+    """Zero-copy ingestion (cg_host_register) and the host thread budget change only how the bytes
+    reach the device: the verdicts equal the oracle's with the caller's arena / signature table / ids
+    registered, for host budgets of 1, 2 and 16 threads, and after unregistering (pageable again)."""
+    from corda_amd import _lib
+    from corda_amd.engine import Engine
+    from tools.workload import wl
+    b, labels, schemes, ids, id_idx, ref = spool
+    idx = np.random.default_rng(5).integers(0, b.n, 300_000)
+    tb = wl.tx_sig_stream(b, schemes, idx, ids, id_idx, nthreads=16)
+    L = _lib.lib()
+    arrs = (tb.arena, tb.sigs, tb.ids)
+    for a in arrs:
+        assert _lib.host_register(a)
+        assert L.cg_host_registered(a.ctypes.data, a.nbytes) == 1
+    # overlapping and unknown ranges are refused
+    assert L.cg_host_register(tb.arena.ctypes.data + 8, 16) != 0
+    assert L.cg_host_unregister(tb.arena.ctypes.data + 8) != 0
+    try:
+        for threads in (1, 2, 16):
+            with Engine(0, chunk_items=70_001 if threads == 2 else 0, host_threads=threads) as eng:
+                st = eng.verify_tx_signatures(tb)
+                assert np.array_equal(st, ref[idx]), f"registered, {threads} threads: {np.count_nonzero(st != ref[idx])} differ"
+    finally:
+        for a in arrs:
+            _lib.host_unregister(a)
+    assert L.cg_host_registered(tb.arena.ctypes.data, tb.arena.nbytes) == 0
+    with Engine(0) as eng:
+        assert np.array_equal(eng.verify_tx_signatures(tb), ref[idx]), "pageable after unregistering"
+
+
 def test_tx_signatures_edges():
     """Out-of-range id / template index -> NOT_RUN; templates of any length (odd, empty prefix or
     suffix); isValid mode; an empty call; signatures before the keys in the arena."""

@@ -52,6 +52,48 @@ def test_malformed_requests():
         V.BatchSignatureRequest.from_bytes(bytes(bad_mode))
 
 
+def _kotlin_long(x):
+    """x as a JVM Long (64-bit two's complement)."""
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >> 63 else x
+
+
+def test_crafted_header_counts_are_rejected():
+    """n_keys = 2^28, n_items = 1 and an arena_len that, read as a signed Long, cancels
+    2^32 of key bytes: the lengths then add up modulo 2^64. Both parsers must refuse it: the Python
+    one reads the counts unsigned and never wraps; VerifierBatchApi.parse (not compiled here)
+    rejects a negative n_items / arena_len and any count whose table cannot fit a ByteBuffer."""
+    import os
+    import re
+    import struct
+    b, _, _ = _batch(1)
+    real = V.BatchSignatureRequest.from_batch(5, b).to_bytes()
+    n_keys, n_items = 1 << 28, 1
+    body_len = len(real)
+    # arena_len chosen so that 40 + 16 n_keys + 32 n_items + arena_len == body_len modulo 2^64
+    arena_len = (body_len - 40 - 16 * n_keys - 32 * n_items) % (1 << 64)
+    crafted = bytearray(real)
+    struct.pack_into("<IIQQ", crafted, 16, n_keys, 0, n_items, arena_len)
+    assert _kotlin_long(40 + 16 * n_keys + 32 * n_items + _kotlin_long(arena_len)) == body_len  # the wrap
+    with pytest.raises(V.MalformedMessage):
+        V.BatchSignatureRequest.from_bytes(bytes(crafted))
+    for field, val in ((24, 1 << 63), (32, (1 << 64) - 1)):  # negative as a Long
+        bad = bytearray(real)
+        struct.pack_into("<Q", bad, field, val)
+        with pytest.raises(V.MalformedMessage):
+            V.BatchSignatureRequest.from_bytes(bytes(bad))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    kt = open(os.path.join(root, "jvm/src/main/kotlin/net/corda/nodeapi/VerifierBatchApi.kt")).read()
+    parse = kt[kt.index("fun parse("):kt.index("class BatchSignatureResponse")]
+    assert "and 0xffffffffL" in parse  # n_keys read unsigned
+    assert re.search(r"nItems < 0 \|\| arenaLen < 0", parse)
+    assert "Int.MAX_VALUE / KEY_BYTES" in parse and "Int.MAX_VALUE / ITEM_BYTES" in parse
+    # the Kotlin model of the same check: the crafted header fails the range test before the sum
+    nk, ni, al = n_keys, n_items, _kotlin_long(arena_len)
+    assert ni < 0 or al < 0 or nk > (2 ** 31 - 1) // 16 or ni > (2 ** 31 - 1) // 32 or al > 2 ** 31 - 1
+    assert "Math.toIntExact" in kt[kt.index("private fun slice("):]
+
+
 class _RecordingEngine:
     """Stand-in for corda_amd.engine.Engine in host-logic tests: answers NOT_RUN-free statuses
     derived from the item index, and fails on request."""

@@ -60,8 +60,8 @@ MAC32_PER_ED25519 = N_FE_ED25519 * 64
 # (tests/native/host_kernels.cpp; pinned by tests/test_host_kernels.py::test_executed_work_*).
 # Ed25519 (field multiplies, squarings) in the radix-2^25.5 representation (fe25519.h):
 ED_VERIFY_FE = (319, 24)   # k_ed_ladder_pf: 43 mixed additions + 6 doublings in radix 2^25.5 ...
-ED_VERIFY_FE9 = 83         # ... then the 12 B additions in radix 2^29 (fe9.h products)
-ED_WIDE_FE = (307, 0)      # k_ed_ladder_wide: 32 + 12 mixed additions, no doublings (keys with wide tables), all fe9
+ED_VERIFY_FE9 = 69         # ... then the 10 B additions (radix-2^26 table) in radix 2^29 (fe9.h products)
+ED_WIDE_FE = (287, 0)      # k_ed_ladder_wide: 32 + 10 signed entries, no doublings (keys with wide tables), all fe9; the first entry is one product (identity + q0)
 ED_WIDE_BUILD_FE = (62279, 9120)  # one key's wide table: 248-doubling chain, then per row one lane walking its 128 entries, one inversion, the walk back (k_ed_wide_rows, ED_WIDE_ROW_LANES 1)
 ED_FINISH_FE = (5, 0)      # k_ed_finish: prefix product, unwinding, encode
 ED_INVERT_FE = (11, 254)   # one fe_invert, shared by ED_FINISH_K items
@@ -80,8 +80,8 @@ MAC32_EXEC_PER_ED25519 = ED_VERIFY_FE9 * MAC_PER_MUL9 + ((ED_VERIFY_FE[0] + ED_F
 # The ladder figure is its full schedule (every digit non-zero): a lane whose digit is zero skips
 # its addition, but the wave issues it for the other 63 lanes, so the full schedule is what the
 # SIMD executes (per-item mean 1% lower).
-EC_LADDER_MUL = {"secp256r1": 741, "secp256k1": 723}
-EC_WIDE_MUL = {"secp256r1": 476, "secp256k1": 476}  # k_ec_ladder_wide: 32 + 12 mixed additions + x-check
+EC_LADDER_MUL = {"secp256r1": 719, "secp256k1": 701}
+EC_WIDE_MUL = {"secp256r1": 454, "secp256k1": 454}  # k_ec_ladder_wide: 33 + 10 mixed additions (G radix 2^26) + x-check
 # table modes (corda_amd/csrc/keyws.h): quarter tables from 3 items per key, full from 32, wide from
 # KEY_WIDE_MIN_USES (1536 Ed25519 / 512 ECDSA)
 KEY_QUARTER_MIN_USES, KEY_FULL_MIN_USES, KEY_WIDE_MAX = 3, 32, 8192  # keyws.h
@@ -135,9 +135,11 @@ def parse(argv=None):
     ap.add_argument("--engine-threads", type=int, default=0,
                     help="cg_config.host_threads of the headline context (0: this rank's share when ranks "
                          "share the node, else the library's budget)")
-    ap.add_argument("--host-register", type=int, default=1,
+    ap.add_argument("--host-register", type=int, default=0,
                     help="1: register the headline's host buffers once (cg_host_register: DMA straight from "
-                         "them, no CPU staging copy), as a JVM node registers its persistent direct buffers")
+                         "them, no CPU staging copy), as a JVM node registers its persistent direct buffers; "
+                         "2: the same after copying them into 2 MB transparent huge pages; 0: pageable "
+                         "(measured fastest on one GPU, DESIGN §5)")
     ap.add_argument("--configs1-items", type=int, default=1 << 20, help="configs[1] Ed25519 secondary (0: off)")
     ap.add_argument("--ecdsa-items", type=int, default=1 << 20, help="configs[2] ECDSA 50/50 secondary (0: off)")
     ap.add_argument("--pipeline-txs", type=int, default=1 << 20, help="configs[3] transaction pipeline (0: off)")
@@ -185,6 +187,34 @@ def free_port():
 def _lib_mod():
     from corda_amd import _lib
     return _lib
+
+
+def hugepage_copy(arr):
+    """A copy of `arr` in an anonymous mapping advised MADV_HUGEPAGE, 2 MB aligned (so the kernel can
+    back it with transparent huge pages); returns (view, mapping)."""
+    import mmap
+    huge = 2 << 20
+    size = (arr.nbytes + 2 * huge - 1) // huge * huge
+    m = mmap.mmap(-1, size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    if hasattr(mmap, "MADV_HUGEPAGE"):
+        m.madvise(mmap.MADV_HUGEPAGE)
+    base = np.frombuffer(m, dtype=np.uint8)
+    off = (-base.ctypes.data) % huge
+    view = base[off:off + arr.nbytes].view(arr.dtype).reshape(arr.shape)
+    view[...] = arr
+    return view, m
+
+
+def anon_huge_kb():
+    """AnonHugePages of this process (kB), from /proc/self/smaps_rollup (0 if unreadable)."""
+    try:
+        with open("/proc/self/smaps_rollup") as f:
+            for l in f:
+                if l.startswith("AnonHugePages:"):
+                    return int(l.split()[1])
+    except OSError:
+        pass
+    return 0
 
 
 def kfd_gpus(sysfs="/sys/class/kfd/kfd/topology/nodes", env=None):
@@ -964,8 +994,15 @@ def main(argv=None):
     holder = {}
     # zero-copy ingestion: the caller's persistent buffers registered once, outside the timed region
     # (a JVM node registers its direct-buffer arena once; cg_host_register, include/cordagpu.h)
-    registered = []
+    registered, huge_maps = [], []
     if a.host_register and hasattr(_lib_mod().lib(), "cg_host_register"):
+        if a.host_register == 2:  # the same bytes in 2 MB transparent huge pages first
+            from corda_amd import batch as _B
+            cp = {}
+            for name in ("arena", "sigs", "ids"):
+                cp[name], m = hugepage_copy(getattr(tb, name))
+                huge_maps.append(m)
+            tb = _B.TxSigBatch(tb.keys, cp["ids"], cp["sigs"], tb.tmpls, cp["arena"])
         for arr in (tb.arena, tb.sigs, tb.ids):
             if _lib_mod().host_register(arr):
                 registered.append(arr)
@@ -1039,7 +1076,8 @@ def main(argv=None):
                                       "the first chunk's bytes are resident, ms_verify = the rest"}}
     extra["table_modes_items"] = table_modes(batch, schemes)
     extra["host"] = {"threads": threads, "engine_host_threads": eng_threads or "library budget",
-                     "registered_bytes": int(sum(x.nbytes for x in registered))}
+                     "registered_bytes": int(sum(x.nbytes for x in registered)), "host_register": a.host_register,
+                     "anon_huge_pages_kB": anon_huge_kb()}
     cpu = None
     if rank == 0 and world == 1:
         if a.device_steps > 0:

@@ -91,7 +91,10 @@ struct cg_ctx {
   cg::Fork fork = {{nullptr, nullptr, nullptr}, nullptr, {nullptr, nullptr}, {nullptr, nullptr, nullptr}, nullptr,
                    {nullptr, nullptr, nullptr}, nullptr};
   std::mutex mu;
-  DevBuf keyprep, itemws, btab, keys, items, arena, status, aux0, aux1, aux2;
+  DevBuf keyprep, itemws, keys, items, arena, status, aux0, aux1, aux2;
+  // the constant fixed-base tables (B, both curves' G; 86 GB at radix 2^26), shared by every context
+  // of this process on the device (acquire_tables / release_tables)
+  void* btab = nullptr;
   DevBuf wide;  // wide-table pools (keyws.h), sized by the largest call's item count
   // wide slots this context may allocate: lowered when the device's free memory cannot hold the
   // pool a call asks for (another process or context on the device), so the call runs
@@ -144,6 +147,57 @@ namespace {
 
 // contexts open in this process (the default host budget divides the CPU quota among them)
 std::atomic<unsigned> g_live_ctx{0};
+
+// The constant fixed-base tables, one copy per device per process: read-only after the build, so
+// every context on the device (a cg_pool's slots, a test's second context) shares it instead of
+// holding its own 86 GB (keyws.h const_tab_bytes: Ed25519 B and both curves' G at radix 2^26).
+struct SharedTables {
+  int device;
+  void* p;
+  unsigned refs;
+};
+std::mutex g_tab_mu;
+std::vector<SharedTables> g_tabs;
+
+hipError_t acquire_tables(int device, hipStream_t s, void** out) {
+  std::lock_guard<std::mutex> g(g_tab_mu);
+  for (SharedTables& t : g_tabs)
+    if (t.device == device) {
+      ++t.refs;
+      *out = t.p;
+      return hipSuccess;
+    }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, cg::btab_bytes());
+  if (e != hipSuccess) return e;
+  {  // built once over a temporary scratch, freed afterwards
+    DevBuf scratch;
+    e = scratch.ensure(cg::btab_scratch_bytes());
+    if (e == hipSuccess) e = cg::init_btab(p, scratch.p, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    scratch.release();
+  }
+  if (e != hipSuccess) {
+    hipFree(p);
+    return e;
+  }
+  g_tabs.push_back({device, p, 1u});
+  *out = p;
+  return hipSuccess;
+}
+
+void release_tables(int device, void* p) {
+  std::lock_guard<std::mutex> g(g_tab_mu);
+  for (size_t i = 0; i < g_tabs.size(); ++i)
+    if (g_tabs[i].device == device && g_tabs[i].p == p) {
+      if (--g_tabs[i].refs == 0) {
+        hipSetDevice(device);
+        hipFree(p);
+        g_tabs.erase(g_tabs.begin() + (ptrdiff_t)i);
+      }
+      return;
+    }
+}
 
 // The host threads a call of n items may use: 1 below 2^16 items, else the budget; the pool is
 // (re)made to match, so nt parts run on nt threads.
@@ -301,7 +355,7 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
     }
     c->fork.mark = c->htrace && 3 * k + 2 < c->fbt.size() ? c->fbt[3 * k + 2] : nullptr;  // before the joins
     const hipError_t r = cg::launch_items_back(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len,
-                                               d_status + at(k), c->keyprep.p, ws(k), c->btab.p, s, &c->fork, &wp);
+                                               d_status + at(k), c->keyprep.p, ws(k), c->btab, s, &c->fork, &wp);
     c->fork.mark = nullptr;
     if (c->htrace && 3 * k + 1 < c->fbt.size()) hipEventRecord(c->fbt[3 * k + 1], s);  // back k ends
     return r;
@@ -480,7 +534,7 @@ int verify_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_
     if (k == 0) HIP_TRY(hipEventRecord(c->tev[1], s), "hipEventRecord");
     const uint64_t f = P.first[k], cnt = P.first[k + 1] - f;
     HIP_TRY(cg::launch_items(dk, n_keys, di + f, cnt, dbase, arena_len, mode, ds + f, c->keyprep.p, c->itemws.p,
-                             c->btab.p, s, nullptr, 0, &c->fork, &wp), "launch_items");
+                             c->btab, s, nullptr, 0, &c->fork, &wp), "launch_items");
   }
   HIP_TRY(hipEventRecord(c->tev[2], s), "hipEventRecord");
   HIP_TRY(hipMemcpyAsync(status_out, ds, n_items, hipMemcpyDeviceToHost, s), "D2H status");
@@ -661,14 +715,7 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&c->tev[k]);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
   if (e == hipSuccess) e = cg::upload_constants();
-  if (e == hipSuccess) e = c->btab.ensure(cg::btab_bytes());
-  if (e == hipSuccess) {  // the constant tables (6.6 GB, built once per context) over a temporary scratch
-    DevBuf scratch;
-    e = scratch.ensure(cg::btab_scratch_bytes());
-    if (e == hipSuccess) e = cg::init_btab(c->btab.p, scratch.p, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    scratch.release();
-  }
+  if (e == hipSuccess) e = acquire_tables(c->device, c->stream, &c->btab);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     const int rc = hip_fail(e, "side streams / upload_constants / base-point tables");
@@ -689,7 +736,8 @@ void cg_close(cg_ctx* c) {
   c->keyprep.release();
   c->itemws.release();
   c->wide.release();
-  c->btab.release();
+  if (c->btab) release_tables(c->device, c->btab);
+  c->btab = nullptr;
   c->keys.release();
   c->items.release();
   c->arena.release();
@@ -824,7 +872,7 @@ int cg_verify_items_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   for (uint64_t f = 0; f < n_items; f += per) {
     const uint64_t cnt = per < n_items - f ? per : n_items - f;
     HIP_TRY(cg::launch_items(d_keys, n_keys, d_items + f, cnt, d_arena, arena_len, mode, d_status + f, c->keyprep.p,
-                             c->itemws.p, c->btab.p, s, nullptr, 0, &c->fork),
+                             c->itemws.p, c->btab, s, nullptr, 0, &c->fork),
             "launch_items");
   }
   HIP_TRY(order_out(c, s), "hipEventRecord");

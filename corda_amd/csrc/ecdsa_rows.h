@@ -489,7 +489,7 @@ CG_HD void ec_pick(f29& x, f29& y, const Row* row, int a) {
 #define EC_WIDE_MULT 128
 #define EC_WIDE_PACKED 16  // int16 digits (the top one reaches 256)
 #ifndef EC_WIDE_GW
-#define EC_WIDE_GW 22
+#define EC_WIDE_GW 26
 #endif
 #define EC_WIDE_GDIGITS ((257 + EC_WIDE_GW - 1) / EC_WIDE_GW)  // radix 2^16: 17, the last the carry out of bit 255
 #define EC_WIDE_GMULT (1 << (EC_WIDE_GW - 1))

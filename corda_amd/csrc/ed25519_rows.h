@@ -440,7 +440,7 @@ CG_HD void ed_btab_wb_row(ge_niels* row, const ge_p3& B, int u, const fe& d2) {
 // prefetch hides the HBM gathers of the 3 GB table: ecdsa_rows.h has the A/B.)
 #define ED_WIDE_W 8
 #ifndef ED_WIDE_BW
-#define ED_WIDE_BW 22
+#define ED_WIDE_BW 26
 #endif
 struct EdWideCfg {
   static constexpr int kDigits = (253 + ED_WIDE_W - 1) / ED_WIDE_W;  // 32: h < 2^253 leaves the carry room
@@ -475,15 +475,22 @@ struct EdBWideTab {
 // runs.
 CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t* esb, const EdWideTab& TA,
                                  const EdBWideTab& TB) {
-  ge9_p3 R;
-  ge9_p3_0(R);
-  for (int o = 0; o < EdWideCfg::kOps; ++o) {
+  auto entry = [&](int o, bool& neg) -> ge9_niels {
     const bool is_b = o >= EdWideCfg::kRows;
     const int dg = is_b ? sc_digit_at<EdWideCfg::kBBits>(esb, o - EdWideCfg::kRows) : sc_digit_b(eh, o);
     const int dp = dg < 0 ? -dg : dg;
-    const ge9_niels n = dp == 0 ? TB.ident : is_b ? TB.t[o - EdWideCfg::kRows][dp - 1] : TA.t[o][dp - 1];
-    if (o + 1 < EdWideCfg::kOps) ge9_madd_half<true>(R, R, n, dg < 0);
-    else ge9_madd_half<false>(R, R, n, dg < 0);
+    neg = dg < 0;
+    return dp == 0 ? TB.ident : is_b ? TB.t[o - EdWideCfg::kRows][dp - 1] : TA.t[o][dp - 1];
+  };
+  ge9_p3 R;
+  bool n0;
+  const ge9_niels q0 = entry(0, n0);
+  ge9_from_niels_half(R, q0, n0);  // identity + q0: one product, not seven
+  for (int o = 1; o < EdWideCfg::kOps; ++o) {
+    bool neg;
+    const ge9_niels n = entry(o, neg);
+    if (o + 1 < EdWideCfg::kOps) ge9_madd_half<true>(R, R, n, neg);
+    else ge9_madd_half<false>(R, R, n, neg);
   }
   ge9_to_p2(out, R);
 }

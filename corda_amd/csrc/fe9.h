@@ -398,6 +398,21 @@ CG_HD void ge9_madd_half(ge9_p3& r, const ge9_p3& p, const ge9_niels& q, bool ne
   if (WithT) fe9_mul<true>(r.T, E, H);
 }
 
+// r = (-1)^neg q as an extended point (the first entry of a ladder, added to the identity): x =
+// (y+x)/2 - (y-x)/2 and y = (y+x)/2 + (y-x)/2 carried tight, Z = 1, T = x y. One product and two
+// carry passes instead of ge9_madd_half's seven products (-x swaps the two halves: -q).
+CG_HD void ge9_from_niels_half(ge9_p3& r, const ge9_niels& q, bool neg) {
+  fe9 sp, sm, t;
+  fe9_cmov(sp, q.ypx, q.ymx, neg);
+  fe9_cmov(sm, q.ymx, q.ypx, neg);
+  fe9_subk(t, sp, sm);  // class V
+  fe9_carry(r.X, t);
+  fe9_add(t, sp, sm);   // class A2
+  fe9_carry(r.Y, t);
+  fe9_1(r.Z);
+  fe9_mul<false>(r.T, r.X, r.Y);
+}
+
 CG_HD void ge9_to_p2(ge_p2& o, const ge9_p3& r) {
   fe_from_fe9(o.X, r.X);
   fe_from_fe9(o.Y, r.Y);

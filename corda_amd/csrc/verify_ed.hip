@@ -716,7 +716,8 @@ __device__ __forceinline__ const ge9_niels* ed_wide_src(const EdWideTab& TA, con
   return is_b ? &TB.t[row][a - 1] : &TA.t[row][a - 1];
 }
 
-// 44 signed mixed additions in the radix-2^29 arithmetic (fe9.h: ed_double_scalar_wide's form)
+// 42 signed mixed additions (32 key rows + 10 B rows at radix 2^26) in the radix-2^29 arithmetic
+// (fe9.h: ed_double_scalar_wide's form), the first entry folded into the second addition
 __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint32_t* __restrict__ dw,
                                                          const EdWideTab& TA, const EdBWideTab& TB, uint8_t* wave_lds,
                                                          uint32_t lane) {
@@ -730,13 +731,12 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
   ed_wide_op(1, widx, sh, is_b, row);
   uint32_t w_next = dw[widx];
   ge9_p3 R;
-  ge9_p3_0(R);
-  for (int o = 0; o + 1 < N; ++o) {
+  // op o's entry from LDS into n, then op o + 1's gather and op o + 2's digit word issued
+  auto next = [&](int o, ge9_niels& n, bool& neg) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // op o's entry and op o+1's digit word
-    ge9_niels n;
     ed_lds_niels9(n, wave_lds, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
-    const bool neg = d_cur < 0;
+    neg = d_cur < 0;
     ed_wide_op(o + 1, widx, sh, is_b, row);
     d_cur = ed_wide_digit(w_next, sh, is_b);
     ed_glds_niels9(ed_wide_src(TA, TB, is_b, row, d_cur), wl);
@@ -744,6 +744,17 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
       ed_wide_op(o + 2, widx, sh, is_b, row);
       w_next = dw[widx];
     }
+  };
+  {  // op 0: identity + q0 (fe9.h ge9_from_niels_half: one product instead of an addition's seven)
+    ge9_niels n;
+    bool neg;
+    next(0, n, neg);
+    ge9_from_niels_half(R, n, neg);
+  }
+  for (int o = 1; o + 1 < N; ++o) {
+    ge9_niels n;
+    bool neg;
+    next(o, n, neg);
     ge9_madd_half<true>(R, R, n, neg);
   }
   {  // the last addition: projective output

@@ -100,7 +100,7 @@ struct cg_ctx {
   // pool a call asks for (another process or context on the device), so the call runs
   // with fewer hot keys on wide tables (full tables for the rest: slower, same verdicts) instead of
   // failing with CG_ERR_NOMEM
-  uint32_t wide_max = 8192u;
+  uint32_t wide_max = cg::kKeyWideMax;
   // transaction pipeline: verify items, spliced messages, templates; host-entry staging
   DevBuf txitems, msgs, tmpls, h_txs, h_comps, h_sigs, h_ids, h_txst;
   // tear-offs: leaf-hash workspace
@@ -111,11 +111,6 @@ struct cg_ctx {
   // the tx-signature host path's second copy stream (chunk 0's bytes while the key-use counts are
   // sampled) and a pinned buffer for those counts (a pinned copy does not queue behind a pageable one)
   hipStream_t copy2 = nullptr;
-  // CG_FRONT_STREAM=1: the host tx-signature path runs each chunk's main-stream front (items, plan,
-  // challenge hashes) on fstream, so chunk k + 1's front overlaps chunk k's back; fev[2 k] / [2 k + 1]:
-  // chunk k's front / back done; fs_active: the stream the prepare hooks enqueue on during a call
-  hipStream_t fstream = nullptr, fs_active = nullptr;
-  std::vector<hipEvent_t> fev;
   // the exact key-use count (many keys): per host thread a byte counter per key (a wrap to 0 logs
   // the key in ovf: +256), kept across calls so a call does not page-fault 16 fresh arrays in
   std::vector<std::vector<uint8_t>> cnt8;
@@ -239,10 +234,18 @@ uint64_t chunk_of(const cg_ctx* c, uint64_t n) {
 // before chunk k's back).
 size_t item_half_bytes(uint64_t ws_items) { return (cg::item_ws_bytes(ws_items) + 255) & ~(size_t)255; }
 hipError_t ensure_ws(cg_ctx* c, uint32_t n_keys, uint64_t ws_items, uint64_t call_items = 0) {
-  size_t wide = cg::wide_bytes(n_keys, call_items, c->wide_max);
+  // the wide pool is sized for the full slot cap (KEY_WIDE_MAX) whenever the device can hold it: a
+  // cap lowered by an earlier call that met low free memory (another process on the device) is
+  // raised again here once the memory is back, instead of staying low for the
+  // context's life
+  const uint32_t kmax = cg::kKeyWideMax;
+  size_t wide = cg::wide_bytes(n_keys, call_items, kmax);
   const size_t items = item_half_bytes(ws_items) * (call_items > ws_items ? 2 : 1);
-  if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= items && c->wide.cap >= wide)
+  if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= items && c->wide.cap >= wide) {
+    c->wide_max = kmax;
     return hipSuccess;
+  }
+  uint32_t cap = kmax;
   if (wide > c->wide.cap) {  // cap the wide pool by the device's free memory (keeping 1 GiB spare)
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
@@ -252,12 +255,14 @@ hipError_t ensure_ws(cg_ctx* c, uint32_t n_keys, uint64_t ws_items, uint64_t cal
       const size_t spare = (size_t)1 << 30;
       if (wide + need_other + spare > avail) {
         const size_t room = avail > need_other + spare ? avail - need_other - spare : 0;
-        const size_t per = cg::wide_slot_bytes();
-        c->wide_max = (uint32_t)std::min<size_t>(room / per, c->wide_max);
-        wide = cg::wide_bytes(n_keys, call_items, c->wide_max);
+        cap = (uint32_t)std::min<size_t>(room / cg::wide_slot_bytes(), kmax);
+        wide = cg::wide_bytes(n_keys, call_items, cap);
       }
     }
   }
+  c->wide_max = cap;
+  if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= items && c->wide.cap >= wide)
+    return hipSuccess;  // still short of memory: the pool the context has is the largest that fits
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess) e = c->keyprep.ensure(cg::keyprep_bytes(n_keys));
   if (e == hipSuccess) e = c->itemws.ensure(items);
@@ -364,36 +369,8 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
     // host copies in the prepare hook block the enqueuing thread: chunk k's back goes in before
     // chunk k + 1's copy, so the device runs chunk k's ladders during it (with chunk k + 1's front
     // first, chunk k's ladders waited for chunk k + 1's copy: profiles/r03/v5 timeline)
-    static const bool fstr = [] {
-      const char* v = getenv("CG_FRONT_STREAM");
-      return v && v[0] == '1';
-    }();
-    if (fstr && two && c->fstream) {
-      // front k on fstream after back k - 2 (the item workspace it reuses), back k after front k
-      while (e == hipSuccess && c->fev.size() < 2 * nch + 1) {
-        hipEvent_t ev;
-        e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (e == hipSuccess) c->fev.push_back(ev);
-      }
-      const hipStream_t fs = c->fstream;
-      if (e == hipSuccess) e = hipEventRecord(c->fev[2 * nch], s);  // key prep, Abyte, tables forked
-      if (e == hipSuccess) e = hipStreamWaitEvent(fs, c->fev[2 * nch], 0);
-      c->fs_active = fs;
-      for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
-        if (k >= 2) e = hipStreamWaitEvent(fs, c->fev[2 * (k - 2) + 1], 0);
-        if (e == hipSuccess) e = (*prepare)(k, at(k), cnt(k));  // the hooks enqueue on fs_active
-        if (e == hipSuccess)
-          e = cg::launch_items_front(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, mode,
-                                     d_status + at(k), c->keyprep.p, ws(k), fs, d_msgs, msgs_len, &c->fork, &wp,
-                                     false);
-        if (e == hipSuccess) e = hipEventRecord(c->fev[2 * k], fs);
-        if (e == hipSuccess) e = hipStreamWaitEvent(s, c->fev[2 * k], 0);
-        if (e == hipSuccess) e = back(k);
-        if (e == hipSuccess) e = hipEventRecord(c->fev[2 * k + 1], s);
-      }
-      c->fs_active = nullptr;
-      return e;
-    }
+    // (a front stream of its own, chunk k + 1's front beside chunk k's back, measured neutral twice:
+    // +1% in round 4, 315.4 -> 314.1 M sigs/s with the host pool, profiles/r04/fstr; removed in round 5)
     for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
       e = front(k);
       if (e == hipSuccess) e = back(k);
@@ -707,7 +684,7 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
                      prop.multiProcessorCount > 0;
     std::vector<uint32_t> mask(own ? (prop.multiProcessorCount + 31) / 32 : 0, 0u);
     for (int cu = 0; own && cu < prop.multiProcessorCount; ++cu) mask[cu / 32] |= 1u << (cu % 32);
-    for (hipStream_t* cs : {&c->copy, &c->copy2, &c->fstream})
+    for (hipStream_t* cs : {&c->copy, &c->copy2})
       if (e == hipSuccess)
         e = own ? hipExtStreamCreateWithCUMask(cs, (uint32_t)mask.size(), mask.data())
                 : hipStreamCreateWithFlags(cs, hipStreamNonBlocking);
@@ -764,13 +741,12 @@ void cg_close(cg_ctx* c) {
   if (c->fork.ec_front_go) hipEventDestroy(c->fork.ec_front_go);
   for (int k = 0; k < 2; ++k)
     if (c->fork.ec_front_done[k]) hipEventDestroy(c->fork.ec_front_done[k]);
-  for (hipStream_t* cs : {&c->copy, &c->copy2, &c->fstream})
+  for (hipStream_t* cs : {&c->copy, &c->copy2})
     if (*cs) {
       hipStreamSynchronize(*cs);
       hipStreamDestroy(*cs);
     }
   for (hipEvent_t e : c->segt) hipEventDestroy(e);
-  for (hipEvent_t e : c->fev) hipEventDestroy(e);
   for (hipEvent_t e : c->fbt) hipEventDestroy(e);
   for (hipEvent_t e : c->backt)
     if (e) hipEventDestroy(e);
@@ -1184,7 +1160,7 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
     hipError_t r = ready ? (*ready)(k, first, cnt) : hipSuccess;
     if (r == hipSuccess)
       r = cg::launch_tx_sig_range(d_sigs, first, cnt, dt, n_tmpls, nullptr, n_ids, d_ids, arena_len, slot,
-                                  (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, c->fs_active ? c->fs_active : s);
+                                  (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s);
     return r;
   };
   if (e == hipSuccess)
@@ -1495,7 +1471,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   hipError_t copy_err = hipSuccess;
   const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t, uint64_t) {
     hipError_t e = overlap && k == 0 ? hipSuccess : copy_chunk(k, c->copy);
-    const hipStream_t fs = c->fs_active ? c->fs_active : s;  // the stream chunk k's front runs on
+    const hipStream_t fs = s;  // the stream chunk k's front runs on
     if (e == hipSuccess) e = hipStreamWaitEvent(fs, c->seg[k], 0);
     if (e == hipSuccess && htrace && 3 * k < c->fbt.size()) {
       c->fbh[k] = ms_since();

@@ -88,6 +88,7 @@ struct PendingTabs {
   // tables; false only when the host counts prove none does (KeyUses::host_counts), so the
   // near-empty table launch does not queue behind the wide builds for a slot
   bool need_full[3] = {true, true, true};
+  uint32_t skip_mask = 0;  // bit f: !need_full[f] (k_key_classify checks it, k_mode_guard enforces it)
 };
 
 struct Fork {
@@ -122,6 +123,7 @@ size_t keyprep_bytes(uint32_t n_keys);
 // row per radix-2^8 digit): bytes, and the pool view over `base` (caps 0 when nothing can be wide).
 size_t wide_bytes(uint32_t n_keys, uint64_t n_items, uint32_t max_slots = 8192u);
 size_t wide_slot_bytes();  // one Ed25519 + one ECDSA wide slot
+constexpr uint32_t kKeyWideMax = 8192u;  // keyws.h KEY_WIDE_MAX (static_assert in verify.hip)
 WidePool make_wide_pool(void* base, uint32_t n_keys, uint64_t n_items, uint32_t max_slots = 8192u);
 
 // Enqueue the whole verify pipeline for one batch on `stream`:

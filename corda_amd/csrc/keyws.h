@@ -238,6 +238,11 @@ static inline uint32_t tab_park_lanes(uint32_t n_keys, uint32_t rows) {
 #define EC_ROW_PARK_BYTES ((size_t)EC_MULT * EC_ROW_PARK * 4)
 #define ROW0_COUNT_AT 8    // row0_count = full_count + 8 (the 256-B count block)
 #define QUART_COUNT_AT 16  // quart_count = full_count + 16
+// full_count[SKIP_MISMATCH_AT], bit f (0 secp256r1, 1 secp256k1, 2 Ed25519): k_key_classify put a
+// key of family f in row-0 / quarter / full mode although the host's counts skipped that family's
+// row-0 / quarter / full builds and ladders (families_needing_full): k_mode_guard then reports its
+// items CG_NOT_RUN instead of verdicts from stale tables
+#define SKIP_MISMATCH_AT 24
 struct KeyWs {
   EdKeyHdr* hdr;
   TabSlot* tab;

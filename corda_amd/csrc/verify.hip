@@ -36,6 +36,7 @@ __global__ void __launch_bounds__(256) k_key_init(uint32_t n_keys, uint32_t all,
                                                   uint32_t* __restrict__ wide_idx, uint32_t* __restrict__ wide_count) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < PLAN_CLASSES) full_count[i] = full_count[ROW0_COUNT_AT + i] = full_count[QUART_COUNT_AT + i] = 0;
+  if (i == 0) full_count[SKIP_MISMATCH_AT] = 0;
   if (i < PLAN_CLASSES + 2) wide_count[i] = 0;
   if (i >= n_keys) return;
   uses[i] = all ? KEY_USES_ALL : 0u;
@@ -105,7 +106,7 @@ __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ 
                                                      uint32_t* __restrict__ wide_idx, uint32_t* __restrict__ wide,
                                                      uint32_t* __restrict__ wide_count, uint32_t* __restrict__ row0,
                                                      uint32_t* __restrict__ quart, uint32_t cap_ed, uint32_t cap_ec,
-                                                     uint32_t min_ed, uint32_t min_ec) {
+                                                     uint32_t min_ed, uint32_t min_ec, uint32_t skip_mask) {
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
   int c = -1, cw = -1, c0 = -1, cq = -1;  // full list, wide list, row-0 list, quarter list
   uint32_t u = 0;
@@ -143,10 +144,33 @@ __global__ void __launch_bounds__(64) k_key_classify(const cg_key* __restrict__ 
                                         : -1;
     if (u >= KEY_QUARTER_MIN_USES && u < ED_DIRECT_MAX_USES) cq = c0;  // and its quarter rows 1..3
   }
+  if (skip_mask && (c >= 0 || c0 >= 0)) {  // a mode whose builds / ladders the host skipped
+    const int cls = c >= 0 ? c : c0;
+    const uint32_t f = cls == PLAN_R1 ? 0u : cls == PLAN_K1 ? 1u : 2u;
+    if ((skip_mask >> f) & 1u) atomicOr(&full_count[SKIP_MISMATCH_AT], 1u << f);
+  }
   list_append(c, i, n_keys, full, full_count);
   list_append(cw, i, n_keys, wide, wide_count);
   list_append(c0, i, n_keys, row0, full_count + ROW0_COUNT_AT);
   list_append(cq, i, n_keys, quart, full_count + QUART_COUNT_AT);
+}
+
+// The items of family f's row-0 / quarter / full modes -> CG_NOT_RUN when k_key_classify flagged f
+// (SKIP_MISMATCH_AT): their ladders or tables were skipped on the host's word. A uniform early exit
+// otherwise (one load of the flag per wave).
+__global__ void __launch_bounds__(256) k_mode_guard(const uint32_t* __restrict__ ranges,
+                                                    const uint32_t* __restrict__ perm,
+                                                    const uint32_t* __restrict__ full_count, uint32_t skip_mask,
+                                                    uint8_t* __restrict__ status) {
+  const uint32_t bad = full_count[SKIP_MISMATCH_AT] & skip_mask;
+  if (!bad) return;
+  for (int f = 0; f < 3; ++f) {
+    if (!((bad >> f) & 1u)) continue;
+    const int cls = f == 0 ? PLAN_R1 : f == 1 ? PLAN_K1 : PLAN_ED;
+    const uint32_t beg = ranges[cls], end = ranges[PLAN_WIDE + cls];
+    for (uint32_t p = beg + blockIdx.x * blockDim.x + threadIdx.x; p < end; p += gridDim.x * blockDim.x)
+      status[perm[p]] = CG_NOT_RUN;
+  }
 }
 
 hipError_t upload_constants() {
@@ -160,6 +184,7 @@ size_t wide_bytes(uint32_t n_keys, uint64_t n_items, uint32_t max_slots) {
   return wide_pool_bytes(wide_cap(n_keys, n_items, max_slots));
 }
 size_t wide_slot_bytes() { return wide_pool_bytes(1); }
+static_assert(kKeyWideMax == KEY_WIDE_MAX, "engine.h mirrors keyws.h");
 WidePool make_wide_pool(void* base, uint32_t n_keys, uint64_t n_items, uint32_t max_slots) {
   return wide_pool(base, wide_cap(n_keys, n_items, max_slots));
 }
@@ -271,15 +296,36 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   else if (src && src->sigs && src->n)
     hipLaunchKernelGGL(k_key_uses_txsig, dim3((unsigned)((src->n + 255) / 256)), dim3(256), 0, stream, src->sigs,
                        src->n, n_keys, w.uses, w.seen);
-  hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys, w.uses,
-                     (const uint8_t*)w.seen, w.full, w.full_count, w.wide_idx, w.wide, w.wide_count, w.row0,
-                     w.quart, w.cap_ed, w.cap_ec, w.min_ed, w.min_ec);
   static const bool serial = [] {  // CG_SERIAL_KEYPREP=1: key prep on the caller's stream (A/B runs)
     const char* v = getenv("CG_SERIAL_KEYPREP");
     return v && v[0] == '1';
   }();
-  if (fork)  // every mode's ladders unless this call's host counts prove otherwise (below)
+  static const bool skip_full = [] {  // CG_SKIP_EMPTY_TABS=0: always launch the row-0 / full builds (A/B)
+    const char* v = getenv("CG_SKIP_EMPTY_TABS");
+    return !(v && v[0] == '0');
+  }();
+  // every mode's builds and ladders unless this call's host counts prove a family has no row-0 /
+  // quarter / full key; the classification checks that proof on the device (k_mode_guard)
+  uint32_t skip_mask = 0;
+  if (fork) {
     for (int f = 0; f < 3; ++f) fork->pending.need_full[f] = true;
+    if (skip_full && !serial && !d_items && src && src->counts && src->host_counts && src->host_keys)
+      families_needing_full(*src, n_keys, w, fork->pending.need_full);
+    // CG_TEST_SKIP_FAMILIES=<mask> (tests only): skip those families' row-0 / quarter / full work as
+    // if the host counts had proved it unneeded, so that the device check can be seen to catch it
+    static const uint32_t test_skip = [] {
+      const char* v = getenv("CG_TEST_SKIP_FAMILIES");
+      return v ? (uint32_t)strtoul(v, nullptr, 0) & 7u : 0u;
+    }();
+    for (int f = 0; f < 3; ++f) {
+      if ((test_skip >> f) & 1u) fork->pending.need_full[f] = false;
+      if (!fork->pending.need_full[f]) skip_mask |= 1u << f;
+    }
+    fork->pending.skip_mask = skip_mask;
+  }
+  hipLaunchKernelGGL(k_key_classify, dim3((n_keys + 63) / 64), dim3(64), 0, stream, d_keys, n_keys, w.uses,
+                     (const uint8_t*)w.seen, w.full, w.full_count, w.wide_idx, w.wide, w.wide_count, w.row0,
+                     w.quart, w.cap_ed, w.cap_ec, w.min_ed, w.min_ec, skip_mask);
   if (!fork || serial) {
     if (fork) {  // the item stages still wait for these events
       fork->pending.on = false;
@@ -317,12 +363,6 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
   fork->pending.n_keys = n_keys;
   fork->pending.keyprep = d_keyprep;
   fork->pending.wide = counted && wide ? *wide : WidePool{};
-  static const bool skip_full = [] {  // CG_SKIP_EMPTY_TABS=0: always launch the row-0 / full builds (A/B)
-    const char* v = getenv("CG_SKIP_EMPTY_TABS");
-    return !(v && v[0] == '0');
-  }();
-  if (skip_full && !d_items && src && src->counts && src->host_counts && src->host_keys)
-    families_needing_full(*src, n_keys, w, fork->pending.need_full);
   if (!counted) e = launch_pending_tabs(fork, stream);
   if (e != hipSuccess) return e;
   // the only key work on the main stream: Abyte for k_ed_hash (no decode)
@@ -480,6 +520,9 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
     hipStreamWaitEvent(stream, fork->row0[0], 0);
     hipStreamWaitEvent(stream, fork->row0[1], 0);
     if (fin_side) hipStreamWaitEvent(stream, fork->row0[2], 0);
+    if (fork->pending.skip_mask)  // after every ladder and the finish of this chunk
+      hipLaunchKernelGGL(k_mode_guard, dim3(64), dim3(256), 0, stream, (const uint32_t*)iw.ranges,
+                         (const uint32_t*)iw.perm, (const uint32_t*)w.full_count, fork->pending.skip_mask, d_status);
   }
   return hipGetLastError();
 }

@@ -9,7 +9,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "c", "liboracle.so")
+# CG_SANITIZE=address (tests/test_sanitizers.py): the -fsanitize=address,undefined build (make asan)
+_SAN = os.environ.get("CG_SANITIZE", "") == "address"
+_LIB_PATH = os.path.join(_HERE, "c", "liboracle_asan.so" if _SAN else "liboracle.so")
 _lib = None
 
 

@@ -8,23 +8,31 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 # CG_HOSTK_DEFS="-DFOO ...": extra defines for a variant's host build (its own .so)
 DEFS = os.environ.get("CG_HOSTK_DEFS", "").split()
-SO = os.path.join(HERE, "native", "libhostkernels%s.so" % ("_" + "_".join(d.lstrip("-D") for d in DEFS) if DEFS else ""))
+# CG_SANITIZE=address (tests/test_sanitizers.py): an -fsanitize=address,undefined build of its own
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"] \
+    if os.environ.get("CG_SANITIZE", "") == "address" else []
+SO = os.path.join(HERE, "native", "libhostkernels%s%s.so" % ("_" + "_".join(d.lstrip("-D") for d in DEFS) if DEFS else "",
+                                                            "_asan" if SAN else ""))
 P = 2 ** 255 - 19
 L = 2 ** 252 + 27742317777372353535851937790883648493
 OFFS = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
 
 
 def build():
+    build_so()
+    return ctypes.CDLL(SO)
+
+
+def build_so():
     src = os.path.join(HERE, "native", "host_kernels.cpp")
     if not os.path.exists(SO) or os.path.getmtime(SO) < max(
             os.path.getmtime(os.path.join(HERE, "..", "corda_amd", "csrc", f))
             for f in os.listdir(os.path.join(HERE, "..", "corda_amd", "csrc")) if f.endswith(".h")) or \
             os.path.getmtime(SO) < os.path.getmtime(src):
         tmp = f"{SO}.{os.getpid()}.tmp"  # build aside and rename: parallel test workers never load a partial .so
-        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-DFE_BOUNDS_CHECK", "-DFE_OP_COUNT", *DEFS, "-fPIC",
-                               "-shared", "-o", tmp, src])
+        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-DFE_BOUNDS_CHECK", "-DFE_OP_COUNT", *DEFS, *SAN,
+                               "-fPIC", "-shared", "-o", tmp, src])
         os.replace(tmp, SO)
-    return ctypes.CDLL(SO)
 
 
 _lib = None

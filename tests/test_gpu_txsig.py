@@ -277,3 +277,34 @@ def test_every_table_mode_in_one_call(spool):
         assert np.array_equal(sd.cpu().numpy(), ref[idx]), "device path"
         from corda_amd.batch import Batch
         assert np.array_equal(eng.verify(Batch(b.keys, b.items[idx], b.arena)), ref[idx]), "message form"
+
+
+def test_skipped_modes_are_reported_not_run():
+    """the host skips a family's row-0 / quarter / full builds and ladders when its counts
+    prove no key needs them (verify.hip families_needing_full). If the device classification ever
+    disagrees, the items of those modes must come back CG_NOT_RUN, never a verdict from stale
+    tables. CG_TEST_SKIP_FAMILIES forces the skip for every family (in a child process: the library
+    reads it once): every verdict equals the oracle's or is NOT_RUN, and the skipped modes' items
+    are NOT_RUN; without it, every verdict is the oracle's."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for mask, expect_skip in (("7", True), ("0", False)):
+        env = dict(os.environ, CG_TEST_SKIP_FAMILIES=mask)
+        r = subprocess.run([sys.executable, os.path.join(here, "mode_guard_probe.py")], env=env, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+        assert out["wide"]["n"] > 0 and out["wide"]["oracle"] == out["wide"]["n"], out
+        assert out["other"]["n"] > 0 and out["other"]["other"] == 0, out
+        if expect_skip:
+            # every item is the oracle's verdict or NOT_RUN, never a verdict from tables that were not
+            # built; the items of the skipped modes are NOT_RUN. (Keys the sampled host count puts on
+            # wide tables -- a sampled key in a hot call is raised to the wide threshold -- keep
+            # their verdicts: their work is not skipped.)
+            o = out["other"]
+            assert o["not_run"] > 0 and o["not_run"] + o["oracle"] == o["n"], out
+        else:
+            assert out["other"]["oracle"] == out["other"]["n"], out

@@ -10,14 +10,21 @@ import subprocess
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SO = os.path.join(HERE, "native", "libhostpooltest.so")
+# CG_SANITIZE=thread (tests/test_sanitizers.py): a -fsanitize=thread build of its own
+TSAN = os.environ.get("CG_SANITIZE", "") == "thread"
+SO = os.path.join(HERE, "native", "libhostpooltest%s.so" % ("_tsan" if TSAN else ""))
 
 
-def _lib():
+def build():
     src = os.path.join(HERE, "native", "host_pool_test.cpp")
     hdr = os.path.join(HERE, "..", "corda_amd", "csrc", "host_pool.h")
     if not os.path.exists(SO) or os.path.getmtime(SO) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
-        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-o", SO, src, "-lpthread"])
+        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", *(["-fsanitize=thread"] if TSAN else []), "-fPIC",
+                               "-shared", "-o", SO, src, "-lpthread"])
+
+
+def _lib():
+    build()
     L = ctypes.CDLL(SO)
     L.hp_check.argtypes = [ctypes.c_uint32] * 3
     L.hp_check.restype = ctypes.c_uint64

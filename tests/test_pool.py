@@ -13,18 +13,25 @@ import golden_io
 from oracle import c_oracle
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SO = os.path.join(HERE, "native", "libpooltest.so")
+# CG_SANITIZE=thread (tests/test_sanitizers.py): a -fsanitize=thread build of its own
+TSAN = os.environ.get("CG_SANITIZE", "") == "thread"
+SO = os.path.join(HERE, "native", "libpooltest%s.so" % ("_tsan" if TSAN else ""))
 ORACLE_DIR = os.path.join(HERE, "..", "oracle", "c")
 
 
-def _lib():
+def build():
     src = os.path.join(HERE, "native", "pool_test.cpp")
     hdr = os.path.join(HERE, "..", "corda_amd", "csrc", "pool.h")
     if not os.path.exists(SO) or os.path.getmtime(SO) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
         c_oracle.lib()  # builds oracle/c if needed
-        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-o", SO, src,
+        subprocess.check_call(["g++", "-O1", "-g", "-std=c++17", *(["-fsanitize=thread"] if TSAN else []), "-fPIC",
+                               "-shared", "-o", SO, src,
                                f"-L{ORACLE_DIR}", "-loracle", f"-Wl,-rpath,{os.path.abspath(ORACLE_DIR)}",
                                "-lpthread"])
+
+
+def _lib():
+    build()
     L = ctypes.CDLL(SO)
     vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
     L.pt_pool_verify.argtypes = [vp, u32, vp, u64, vp, u64, u32, vp, u32, vp, u32, u32, u32, u32, vp, vp]

@@ -268,7 +268,18 @@ struct KeyWs {
   struct EcWideSlot* wec;
   uint32_t cap_ed, cap_ec;
   uint32_t min_ed, min_ec;
+  // the counting plan (plan_sort.hip): per key its ticket in its (class, mode, short / long) group
+  // (2n), the per-chunk bucket counts and their exclusive scan by bucket rank (2n + 1 each, plus
+  // one scan partial per 16k-bucket tile), and 64 words of group counts [0, 32) / group bases [32, 64)
+  uint32_t* pl_tick;
+  uint32_t* pl_cnt;
+  uint32_t* pl_pos;
+  uint32_t* pl_tile;
+  uint32_t* pl_grp;
 };
+#define PL_TILE 16384u  // buckets per scan tile (1024 threads x 16)
+static inline size_t pl_buckets(uint32_t n_keys) { return 2 * (size_t)(n_keys ? n_keys : 1) + 1; }
+static inline size_t pl_tiles(uint32_t n_keys) { return (pl_buckets(n_keys) + PL_TILE - 1) / PL_TILE; }
 
 // How much table a key gets, from the number of items that use it in the batch (one-shot entry
 // points estimate it from a hashed 1-in-KEY_USES_SAMPLE sample of the items, plus an exact
@@ -391,6 +402,16 @@ static inline KeyWs key_ws(void* base, uint32_t n_keys, const WidePool* wp = nul
   w.wide = (uint32_t*)p;
   p += al256(3 * n * sizeof(uint32_t));
   w.wide_count = (uint32_t*)p;
+  p += 256;
+  w.pl_tick = (uint32_t*)p;
+  p += al256(2 * n * sizeof(uint32_t));
+  w.pl_cnt = (uint32_t*)p;
+  p += al256(pl_buckets(n_keys) * sizeof(uint32_t));
+  w.pl_pos = (uint32_t*)p;
+  p += al256(pl_buckets(n_keys) * sizeof(uint32_t));
+  w.pl_tile = (uint32_t*)p;
+  p += al256(pl_tiles(n_keys) * sizeof(uint32_t));
+  w.pl_grp = (uint32_t*)p;
   w.wed = wp ? (EdWideSlot*)wp->ed : nullptr;
   w.wec = wp ? (EcWideSlot*)wp->ec : nullptr;
   w.cap_ed = wp ? wp->cap_ed : 0;
@@ -405,7 +426,8 @@ static inline size_t key_ws_bytes(uint32_t n_keys) {
          al256(tab_park_lanes(n_keys, EdCfg::kRows) * ED_ROW_PARK_BYTES) +
          2 * al256(tab_park_lanes(n_keys, EC_ROWS) * EC_ROW_PARK_BYTES) + al256(n * sizeof(uint32_t)) +
          al256(3 * n * sizeof(uint32_t)) + 256 + 2 * al256(3 * n * sizeof(uint32_t)) + al256(n) +
-         al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256;
+         al256(n * sizeof(uint32_t)) + al256(3 * n * sizeof(uint32_t)) + 256 + al256(2 * n * sizeof(uint32_t)) +
+         2 * al256(pl_buckets(n_keys) * sizeof(uint32_t)) + al256(pl_tiles(n_keys) * sizeof(uint32_t)) + 256;
 }
 
 // Per-item workspace slot (indexed by plan position, so the schemes never share one):
@@ -468,7 +490,7 @@ static inline size_t item_ws_total(uint64_t n_items) {
          al256(8 * n * sizeof(uint32_t)) + al256(n * sizeof(uint32_t)) + al256(n);
 }
 hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d_keys, uint32_t n_keys,
-                       const uint32_t* d_uses, const uint32_t* d_wide_idx, const ItemWs& iw, hipStream_t stream);
+                       const KeyWs& w, const ItemWs& iw, hipStream_t stream);
 
 // Constant tables per context: [Ed25519 B rows (radix 2^10)][G rows k1][G rows r1]
 // [Ed25519 B wide rows (radix 2^12)][G wide rows k1][G wide rows r1][row scratch]

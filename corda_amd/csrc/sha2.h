@@ -79,11 +79,25 @@ CG_HD uint64_t cg_xor3_64(uint64_t a, uint64_t b, uint64_t c) {
   return ((uint64_t)cg_xor3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
          cg_xor3_32((uint32_t)a, (uint32_t)b, (uint32_t)c);
 }
-// (e & f) ^ (~e & g): one bitfield select per 32-bit half
-CG_HD uint64_t cg_ch64(uint64_t e, uint64_t f, uint64_t g) { return (e & f) | (~e & g); }
 #ifndef CG_SHA512_BITOP3
-#define CG_SHA512_BITOP3 2  // maj only: the 64-bit xor3 form priced 3% worse (more moves), maj 3% better
+// 2: Maj as bitop3 (priced 3% better, round 2); 4: Ch as bitop3 (round 5: k_ed_hash 5.5 -> 5.35 ms
+// per headline step, profiles/r05/hash); the 64-bit xor3 form (1) costs more moves than it saves
+#define CG_SHA512_BITOP3 6
 #endif
+// (e & f) ^ (~e & g): one bitfield select per 32-bit half. With CG_SHA512_BITOP3 & 4 an opaque
+// bitop3 (truth table 0xCA: e ? f : g) per half: the compiler otherwise splits the disjoint OR into
+// two terms it adds into T1 separately (v_and + v_bfi + two 64-bit adds per round)
+CG_HD uint64_t cg_ch64(uint64_t e, uint64_t f, uint64_t g) {
+#if (CG_SHA512_BITOP3 & 4) && defined(__HIP_DEVICE_COMPILE__)
+  // (the builtin returns a signed int: each half goes through uint32_t before widening)
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(e >> 32), (uint32_t)(f >> 32),
+                                                            (uint32_t)(g >> 32), 0xCA);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)e, (uint32_t)f, (uint32_t)g, 0xCA);
+  return ((uint64_t)hi << 32) | lo;
+#else
+  return (e & f) | (~e & g);
+#endif
+}
 CG_HD uint64_t cg_maj64(uint64_t a, uint64_t b, uint64_t c) {
 #if CG_SHA512_BITOP3 & 2
   return ((uint64_t)cg_maj32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |

@@ -383,7 +383,7 @@ hipError_t launch_items_plan(const cg_key* d_keys, uint32_t n_keys, const cg_ite
   // plan: items sorted by (scheme class, key) (plan_sort.hip)
   hipError_t e = hipSuccess;
   CG_TIME(fork, CG_STAGE_PLAN, stream,
-          e = launch_plan(d_items, n_items, d_keys, n_keys, (const uint32_t*)w.uses, (const uint32_t*)w.wide_idx, iw,
+          e = launch_plan(d_items, n_items, d_keys, n_keys, w, iw,
                           stream));
   return e;
 }

@@ -362,11 +362,12 @@ static_assert(sizeof(EdDigitsWide) == ITEM_SLOT, "digits must fill one item slot
 // One lane per Ed25519 plan position: item checks, h = SHA-512(R || Abyte || M) mod L,
 // S' = i2p's slide value of S mod L, both recoded to signed radix-64 digits. Needs only the
 // decoded keys (Abyte), so it runs while the key tables are still being built.
-// 3 waves/SIMD (168 VGPRs, 16 B of scratch) instead of 2 at 171 VGPRs: the hash shares the chip
-// with the key-table build, and the extra wave per SIMD raised the headline 208 -> 214 M sigs/s
-// (A/B, profiles/r01/ed25519_v12/ab_hash_waves)
+// 4 waves/SIMD (128 VGPRs, 52 B of scratch, no spill inside the SHA-512 round loops): the rounds
+// are a dependent chain per lane, and at 3 waves (144 VGPRs) the SIMDs issued ~55% of the time;
+// round 5: 5.55 -> 5.16 ms of k_ed_hash per headline step, with Ch as bitop3 5.0 ms (A/B, two
+// rounds, profiles/r05/hash). (Round 1 went 2 -> 3 waves: 208 -> 214 M sigs/s.)
 #ifndef ED_HASH_WAVES_PER_SIMD
-#define ED_HASH_WAVES_PER_SIMD 3
+#define ED_HASH_WAVES_PER_SIMD 4
 #endif
 #ifndef ED_HASH_MID_SCHEDULE
 #define ED_HASH_MID_SCHEDULE 1

@@ -1,13 +1,13 @@
 // The batch plan: item indices grouped by (scheme class, table mode, long bit, key).
 //
-// Round 5: a counting plan (CG_PLAN_COUNTING, default) instead of the radix sort. A bucket is a
+// Round 5 also built a counting plan (-DCG_PLAN_COUNTING=1) in place of the radix sort. A bucket is a
 // (key, long bit) pair; the buckets are ranked by (class, mode, long) group, a key's rank inside its
 // group being an atomic ticket (any order of keys serves: locality is per key). Per chunk: zero the
 // counts, count every item into its bucket (the atomic's return value is the item's place in its
-// bucket), scan the counts in rank order, scatter. Five to seven small launches instead of the
-// onesweep sort's ~15 (its histogram, look-back and memset kernels: ~0.26 ms per headline chunk in
-// steady state, ~0.9 ms for chunk 0 beside the table builds, profiles/r05 timelines). Items of one
-// key are adjacent but no longer in input order within the key (nothing depends on that order).
+// bucket), scan the counts in rank order, scatter: five to seven small launches instead of the
+// onesweep sort's ~15. Measured slower (plan 1.7-1.9 -> 2.5-2.7 ms per headline step, 2 x 2 runs,
+// profiles/r05/plan): the 2.5M device-scope atomics with return per chunk go to ~400 counter lines
+// shared by every XCD, where the onesweep passes count digits in LDS. Kept for A/B, off.
 //
 // Each scheme's kernels then walk one dense range of `perm` (no lane idles on another scheme's
 // item), and inside a range the items of one key are adjacent, so the 64 lanes of a wave
@@ -274,7 +274,7 @@ __global__ void k_plan_ranges_cnt(const uint32_t* __restrict__ grp, const uint32
 }
 
 #ifndef CG_PLAN_COUNTING
-#define CG_PLAN_COUNTING 1
+#define CG_PLAN_COUNTING 0
 #endif
 
 hipError_t launch_plan(const cg_item* d_items, uint64_t n_items, const cg_key* d_keys, uint32_t n_keys,

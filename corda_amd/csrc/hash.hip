@@ -205,13 +205,20 @@ __device__ __forceinline__ uint32_t tx_block_word(const uint32_t* W, int j, uint
 // instruction: round 2 moved ~4x the component bytes, profiles/r02/tx_v4), then every lane reads
 // its own 17 dwords back (stride 17: no bank conflicts).
 #define TX_LDS_DW 17
+#ifndef TX_LEAVES_RING
+#define TX_LEAVES_RING 1
+#endif
 __global__ void __launch_bounds__(256) k_tx_leaves(const cg_tx* __restrict__ txs, const cg_component* __restrict__ comps,
                                                    const uint32_t* __restrict__ perm,
                                                    const uint32_t* __restrict__ ranges,
                                                    const uint32_t* __restrict__ map,
                                                    const uint8_t* __restrict__ arena, uint64_t arena_len,
                                                    uint8_t* __restrict__ status, uint8_t* __restrict__ ws) {
+#if TX_LEAVES_RING
+  __shared__ uint32_t ring_lds[4][2 * 64 * TX_LDS_DW];
+#else
   __shared__ uint32_t stage[4][64 * TX_LDS_DW];
+#endif
   __shared__ uint64_t sbase[4][64];
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -256,6 +263,87 @@ __global__ void __launch_bounds__(256) k_tx_leaves(const cg_tx* __restrict__ txs
     const uint32_t x = (uint32_t)__shfl_xor((int)mbl, o, 64);
     mbl = x > mbl ? x : mbl;
   }
+#if TX_LEAVES_RING
+  // Round 5: each 64-B sector of a component is loaded once. The 68-B window
+  // of round 3 straddled two sectors for every block, and the next block loaded the second again:
+  // 2.3x the component bytes in L1 -> L2 requests, and with every XCD's waves streaming the L2
+  // missed 79% of them (2.0x in memory-side reads, profiles/r05/tx/pmc). Now a ring of two sectors
+  // per component in LDS: block b reads sectors b and b + 1 (dwords o .. o + 16 from the first, o =
+  // the component's dword offset in its sector); sector b + 2 is loaded into registers while block b
+  // compresses and written over sector b's slot afterwards. Lane l loads quarter l & 3 of the
+  // sector of component 16 k + (l >> 2) for k = 0..3: four 16-B loads a lane, one 64-B request per
+  // sector.
+  sbase[wid][lane] = live && inside ? (c.off & ~(uint64_t)63) : ~(uint64_t)0;
+  const uint32_t o = (uint32_t)(c.off & 63) >> 2;
+  const uint32_t sh8 = (uint32_t)(c.off & 3) * 8u;
+  uint32_t h[8];
+  sha256_init(h);
+  uint32_t* ring = ring_lds[wid];  // [slot][component][17 dwords: 16 + 1 pad, conflict-free reads]
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's sbase is written
+  __builtin_amdgcn_wave_barrier();
+  auto load_sector = [&](uint64_t sec, uint4 (&r)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t cc = 16u * k + (lane >> 2), q = lane & 3u;
+      const uint64_t base = sbase[wid][cc];
+      const uint64_t a = base + 64ull * sec + 16ull * q;
+      if (base == ~(uint64_t)0 || a >= lr) {
+        r[k] = make_uint4(0, 0, 0, 0);
+      } else if (a + 16 <= lr) {
+        r[k] = *(const uint4*)(arena + a);
+      } else {  // the arena's last partial chunk: dword by dword
+        uint32_t d[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d[i] = a + 4 * i + 4 <= lr ? *(const uint32_t*)(arena + a + 4 * i) : 0u;
+        r[k] = make_uint4(d[0], d[1], d[2], d[3]);
+      }
+    }
+  };
+  auto store_sector = [&](uint32_t slot, const uint4 (&r)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t cc = 16u * k + (lane >> 2), q = lane & 3u;
+      uint32_t* d = ring + slot * 64 * TX_LDS_DW + cc * TX_LDS_DW + 4 * q;
+      d[0] = r[k].x;
+      d[1] = r[k].y;
+      d[2] = r[k].z;
+      d[3] = r[k].w;
+    }
+  };
+  {
+    uint4 r0[4], r1[4];
+    load_sector(0, r0);
+    load_sector(1, r1);
+    store_sector(0, r0);
+    store_sector(1, r1);
+  }
+  for (uint32_t blk = 0; blk < mbl; ++blk) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this block's two sectors are in LDS
+    __builtin_amdgcn_wave_barrier();
+    uint32_t W[TX_LDS_DW];
+#pragma unroll
+    for (int d = 0; d < TX_LDS_DW; ++d) {
+      const uint32_t x = o + (uint32_t)d;  // dword of the two-sector window
+      W[d] = ring[((blk + (x >> 4)) & 1u) * 64 * TX_LDS_DW + lane * TX_LDS_DW + (x & 15u)];
+    }
+    uint4 nx[4];
+    const bool more = blk + 1 < mbl;  // sector blk + 2 feeds block blk + 1
+    if (more) load_sector(blk + 2, nx);
+    if (blk < nbl) {
+      uint32_t w[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = tx_block_word(W, j, sh8, blk, len, n, salt ? nullptr : nonce);
+      if (blk + 1 == nbl) {
+        w[14] = (uint32_t)((n * 8) >> 32);
+        w[15] = (uint32_t)(n * 8);
+      }
+      sha256_compress(h, w);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's window reads are done
+    __builtin_amdgcn_wave_barrier();
+    if (more) store_sector(blk & 1u, nx);  // sector blk + 2 over sector blk
+  }
+#else
   sbase[wid][lane] = live && inside ? (c.off & ~(uint64_t)3) : ~(uint64_t)0;
   const uint32_t sh8 = (uint32_t)(c.off & 3) * 8u;
   uint32_t h[8];
@@ -286,6 +374,7 @@ __global__ void __launch_bounds__(256) k_tx_leaves(const cg_tx* __restrict__ txs
       sha256_compress(h, w);
     }
   }
+#endif
   if (!live) return;
   if (!inside) {
 #pragma unroll

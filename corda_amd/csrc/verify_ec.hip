@@ -184,6 +184,9 @@ __global__ void __launch_bounds__(64) k_ec_wide_bwd(uint32_t n_keys, const EdKey
                               ws.bases[L.j < EC_WIDE_DIGITS ? L.j : EC_WIDE_DIGITS - 1], (int)L.j, (int)L.g, c_ec[C]);
 }
 
+#ifndef EC_WIDE_ROWS_PRIO_R1
+#define EC_WIDE_ROWS_PRIO_R1 0
+#endif
 // one lane per (wide key, row): the row's 128 affine multiples by co-Z additions, one launch
 // (ecdsa_rows.h ec_wide_row_build; replaces the three passes above unless CG_EC_WIDE_COZ=0)
 template <int C>
@@ -191,6 +194,9 @@ __global__ void __launch_bounds__(64) k_ec_wide_rows(uint32_t n_keys, const EdKe
                                                      const uint32_t* __restrict__ wide,
                                                      const uint32_t* __restrict__ wide_count,
                                                      const uint32_t* __restrict__ wide_idx, EcWideSlot* __restrict__ wec) {
+#if EC_WIDE_ROWS_PRIO_R1  // (A/B) secp256r1's rows (its first ladder comes before secp256k1's) above k1's
+  if (C == CG_CURVE_R1) __builtin_amdgcn_s_setprio(EC_WIDE_ROWS_PRIO_R1);
+#endif
   const EcWideLane L = ec_wide_lane(EC_WIDE_ROWS, EC_WIDE_ROW_LANES);
   EC_WIDE_KEY(C, L);
   constexpr int per = EC_WIDE_MULT / EC_WIDE_ROW_LANES;

@@ -183,6 +183,92 @@ __global__ void __launch_bounds__(64) k_ed_wide_chain(uint32_t n_keys, const EdK
   }
 }
 
+// The same chain with four lanes per key (ED_CHAIN_QUAD, default): the chain is one wave per SIMD
+// on an otherwise idle chip at the start of a call, so its time is the dependent instruction
+// stream of one lane (~9 cycles per instruction at one wave per SIMD, profiles/r04/ubench), not
+// the chip's issue rate. A doubling's four squarings (X^2, Y^2, Z^2, (X+Y)^2) and its P1P1 -> P2/P3
+// products (X T, Z Y, Z T, X Y) run one per lane of a quad; the quad then holds the point redundantly
+// again after one DPP broadcast per limb and result. Same operations, operand order and bounds as
+// ed_dbl_n (ge25519.h ge_p2_dbl, ge_p1p1_to_p2/p3), so every limb equals the one-lane chain's.
+#ifndef ED_CHAIN_QUAD
+#define ED_CHAIN_QUAD 0
+#endif
+template <int J>
+__device__ __forceinline__ void fe_quad_bcast(fe& o, const fe& a) {  // lane J of each quad -> all four
+#pragma unroll
+  for (int k = 0; k < 10; ++k) o.v[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.v[k], J * 0x55, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void fe_pick4(fe& o, const fe& a, const fe& b, const fe& c, const fe& d, uint32_t q) {
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {  // values, not lvalues: a select of addresses became a scratch array
+    const uint32_t av = a.v[k], bv = b.v[k], cv = c.v[k], dv = d.v[k];
+    const uint32_t lo = (q & 1u) ? bv : av, hi = (q & 1u) ? dv : cv;
+    o.v[k] = (q & 2u) ? hi : lo;
+  }
+}
+// 2^n P (n >= 1); every lane of the quad holds P and ends holding 2^n P
+__device__ __forceinline__ void ed_dbl_n_quad(ge_p3& R, const ge_p3& P, int n, uint32_t q) {
+  ge_p2 p;
+  ge_p3_to_p2(p, P);
+  for (int i = 0; i < n; ++i) {
+    fe xy, in, s;
+    fe_add(xy, p.X, p.Y);  // 2T
+    fe_pick4(in, p.X, p.Y, p.Z, xy, q);
+    fe_sq(s, in);
+    fe xx, yy, zz, aa;
+    fe_quad_bcast<0>(xx, s);
+    fe_quad_bcast<1>(yy, s);
+    fe_quad_bcast<2>(zz, s);
+    fe_quad_bcast<3>(aa, s);
+    ge_p1p1 t;  // ge_p2_dbl's outputs
+    fe_add(t.T, zz, zz);  // fe_sq2: 2 Z^2, tight after the carry
+    fe_carry(t.T);
+    fe_add(t.Y, yy, xx);
+    fe_sub(t.Z, yy, xx);
+    fe_sub4(t.X, aa, t.Y);
+    fe_sub4(t.T, t.T, t.Z);
+    fe_carry(t.T);
+    fe f, g, m;  // lane 0: X T, 1: Z Y, 2: Z T, 3: X Y (ge_p1p1_to_p3's operand order)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      f.v[k] = (q == 0 || q == 3) ? t.X.v[k] : t.Z.v[k];
+      g.v[k] = (q == 0 || q == 2) ? t.T.v[k] : t.Y.v[k];
+    }
+    fe_mul(m, f, g);
+    fe_quad_bcast<0>(p.X, m);
+    fe_quad_bcast<1>(p.Y, m);
+    fe_quad_bcast<2>(p.Z, m);
+    if (i + 1 == n) fe_quad_bcast<3>(R.T, m);
+  }
+  fe_copy(R.X, p.X);
+  fe_copy(R.Y, p.Y);
+  fe_copy(R.Z, p.Z);
+}
+__global__ void __launch_bounds__(64) k_ed_wide_chain4(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
+                                                       const uint32_t* __restrict__ wide,
+                                                       const uint32_t* __restrict__ wide_count,
+                                                       const uint32_t* __restrict__ wide_idx,
+                                                       const BaseSlot* __restrict__ bases, EdWideSlot* __restrict__ wed) {
+  chain_prio();
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t l = t >> 2, q = t & 3u;  // the quad's key and this lane's part (quad-uniform exits)
+  if (l >= wide_count[PLAN_ED]) return;
+  const uint32_t i = wide[(size_t)PLAN_ED * n_keys + l];
+  if (hdr[i].status != 0) return;
+  EdWideSlot& ws = wed[wide_idx[i]];
+  ge_p3 P = bases[(size_t)i * KEY_BASES].ed;
+  fe* const out = &ws.bases[0].X + q;  // lane q stores coordinate q (X, Y, Z, T) of each base
+  fe c;
+  fe_pick4(c, P.X, P.Y, P.Z, P.T, q);
+  *out = c;
+  for (int j = 1; j < EdWideCfg::kRows; ++j) {
+    ed_dbl_n_quad(P, P, ED_WIDE_W, q);
+    fe_pick4(c, P.X, P.Y, P.Z, P.T, q);
+    out[(size_t)j * 4] = c;
+  }
+}
+static_assert(sizeof(ge_p3) == 4 * sizeof(fe), "ge_p3 is four consecutive field elements");
+
 // The row tables in three passes (ed25519_rows.h "wide-table build"): chunk Z products per (wide
 // key, row, group of 32) lane, one batch inversion per (wide key, row) lane over the row's 64 chunk
 // products (kept in the slot's zpre[j][0..63], prefixes in zpre[j][64..127]), then the entries.
@@ -240,12 +326,18 @@ __global__ void __launch_bounds__(64) k_ed_wide_bwd(uint32_t n_keys, const EdKey
 #ifndef ED_WIDE_ROWS_WAVES  // waves per SIMD the register allocation must allow
 #define ED_WIDE_ROWS_WAVES 2  // 3 spills 125 VGPRs
 #endif
+#ifndef ED_WIDE_ROWS_PRIO
+#define ED_WIDE_ROWS_PRIO 2
+#endif
 // one lane per (wide key, row): the row's 128 multiples, one inversion, one launch
 // (ed25519_rows.h ed_wide_row_build; replaces the three passes above unless CG_ED_WIDE_ROWS=0)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ED_WIDE_ROWS_WAVES))) k_ed_wide_rows(uint32_t n_keys, const EdKeyHdr* __restrict__ hdr,
                                                      const uint32_t* __restrict__ wide,
                                                      const uint32_t* __restrict__ wide_count,
                                                      const uint32_t* __restrict__ wide_idx, EdWideSlot* __restrict__ wed) {
+#if ED_WIDE_ROWS_PRIO  // (A/B) issue priority over the ECDSA row builds sharing the SIMDs
+  __builtin_amdgcn_s_setprio(ED_WIDE_ROWS_PRIO);
+#endif
   const WideLane L = wide_lane(EdWideCfg::kRows, ED_WIDE_ROW_LANES);
   if (L.l >= wide_count[PLAN_ED]) return;
   const uint32_t i = wide[(size_t)PLAN_ED * n_keys + L.l];
@@ -924,8 +1016,14 @@ void ed_launch_keyprep_chains(const cg_key* d_keys, uint32_t n_keys, const uint8
                      (const uint32_t*)w.full, (const uint32_t*)w.quart, (const uint32_t*)w.full_count, w.bases);
   if (w.cap_ed) {
     const uint32_t lds = chain_spread_lds();
-    if (lds) hipFuncSetAttribute((const void*)k_ed_wide_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_ed_wide_chain, dim3((w.cap_ed + B - 1) / B), dim3(B), lds, stream, n_keys, w.hdr,
+    static const bool quad = [] {  // CG_ED_CHAIN_QUAD=0 (A/B): the one-lane chain
+      const char* v = getenv("CG_ED_CHAIN_QUAD");
+      return v ? v[0] != '0' : ED_CHAIN_QUAD != 0;
+    }();
+    const auto kern = quad ? k_ed_wide_chain4 : k_ed_wide_chain;
+    const uint64_t lanes = (uint64_t)w.cap_ed * (quad ? 4u : 1u);
+    if (lds) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((lanes + B - 1) / B)), dim3(B), lds, stream, n_keys, w.hdr,
                        (const uint32_t*)w.wide, (const uint32_t*)w.wide_count, (const uint32_t*)w.wide_idx,
                        (const BaseSlot*)w.bases, w.wed);
   }

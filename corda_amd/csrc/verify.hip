@@ -501,20 +501,29 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
     if (fork) hipStreamWaitEvent(stream, fork->row0[2], 0);
     CG_TIME(fork, CG_STAGE_ED_FINISH, stream, ed_launch_finish(d_items, n_items, d_arena, arena_len, d_status, iw, stream));
   }
-  if (fork) hipStreamWaitEvent(stream, fork->ready[0], 0);
-  if (fork && fork->pending.ec_front_side) hipStreamWaitEvent(stream, fork->ec_front_done[0], 0);
-  CG_TIME(fork, CG_STAGE_R1_LADDER, stream,
-          ec_launch_ladder(CG_CURVE_R1, true, d_items, n_items, d_status, w, iw, d_btab, stream));
-  if (w.cap_ec)
-    CG_TIME(fork, CG_STAGE_R1_LADDER_WIDE, stream,
-            ec_launch_ladder_wide(CG_CURVE_R1, d_items, n_items, d_status, w, iw, d_btab, stream));
-  if (fork) hipStreamWaitEvent(stream, fork->ready[1], 0);
-  if (fork && fork->pending.ec_front_side) hipStreamWaitEvent(stream, fork->ec_front_done[1], 0);
-  CG_TIME(fork, CG_STAGE_K1_LADDER, stream,
-          ec_launch_ladder(CG_CURVE_K1, true, d_items, n_items, d_status, w, iw, d_btab, stream));
-  if (w.cap_ec)
-    CG_TIME(fork, CG_STAGE_K1_LADDER_WIDE, stream,
-            ec_launch_ladder_wide(CG_CURVE_K1, d_items, n_items, d_status, w, iw, d_btab, stream));
+  // CG_EC_LADDER_SIDE (A/B, bit 0 secp256r1, bit 1 secp256k1): the curve's full-table and wide
+  // ladders on its side stream (after its front and its row-0 ladders there) instead of after the
+  // Ed25519 ladders on this stream, so the issue-bound ladders fill each other's tails
+  static const uint32_t ec_side = [] {
+    const char* v = getenv("CG_EC_LADDER_SIDE");
+    return v ? (uint32_t)strtoul(v, nullptr, 10) & 3u : 0u;
+  }();
+  for (int k = 0; k < 2; ++k) {
+    const int curve = k == 0 ? CG_CURVE_R1 : CG_CURVE_K1;
+    const bool side = fork && (ec_side >> k & 1u);
+    const hipStream_t s = side ? fork->side[k] : stream;
+    if (fork) hipStreamWaitEvent(s, fork->ready[k], 0);
+    if (fork && fork->pending.ec_front_side) hipStreamWaitEvent(s, fork->ec_front_done[k], 0);
+    CG_TIME(fork, k == 0 ? CG_STAGE_R1_LADDER : CG_STAGE_K1_LADDER, s,
+            ec_launch_ladder(curve, true, d_items, n_items, d_status, w, iw, d_btab, s));
+    if (w.cap_ec)
+      CG_TIME(fork, k == 0 ? CG_STAGE_R1_LADDER_WIDE : CG_STAGE_K1_LADDER_WIDE, s,
+              ec_launch_ladder_wide(curve, d_items, n_items, d_status, w, iw, d_btab, s));
+    if (side) {  // the join below waits for this stream's last ladder
+      e = hipEventRecord(fork->row0[k], s);
+      if (e != hipSuccess) return e;
+    }
+  }
   if (fork) {
     if (fork->mark) hipEventRecord(fork->mark, stream);
     hipStreamWaitEvent(stream, fork->row0[0], 0);

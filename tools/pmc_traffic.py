@@ -2,10 +2,13 @@
 (tools/profile_r02.sh: --kernel-trace --stats, then --pmc FETCH_SIZE, --pmc WRITE_SIZE and an SQ pass,
 each its own process), written to profiles/r04/pmc_traffic.json (PMC_TRAFFIC_FILE) for bench.py's roofline.
 
-HBM bytes (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE tallies 128-B requests at 64 B,
-so a wide streaming read reports half its bytes: hbm = 2*FETCH_SIZE + WRITE_SIZE (KB * 1024). The
-doubling is calibrated for streaming reads, not 16-B table gathers, so the figure is an upper
-estimate.
+HBM bytes (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE = TCC_EA0_RDREQ x 64 B, so a
+wide streaming read (128-B requests) reports half its bytes while a table gather (64-B requests)
+reports them exactly (profiles/r05/calib: fetch_calib's stream, 112-B-entry gathers and 16-B
+gathers against their known byte counts). Round 5: with the memory-side read-request trio pass
+(tcc/: TCC_EA0_RDREQ, TCC_EA0_RDREQ_32B, TCC_BUBBLE = 128-B requests) each request is priced at its
+own size, hbm = 128 BUBBLE + 64 (RDREQ - BUBBLE - RDREQ_32B) + 32 RDREQ_32B + WRITE_SIZE; without
+it, round 4's upper estimate 2 FETCH_SIZE + WRITE_SIZE.
 
 VALU issue: SQ_INSTS_VALU wave-instructions of the kernel priced per opcode (tools/isa_mix.py: the
 hottest loop's static instruction mix x the measured chip rate of each opcode,
@@ -90,12 +93,16 @@ def main():
                 "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64"]
     vpath = os.path.join(prof, "valu", "run_counter_collection.csv")
     valu = per_launch(vpath, sq_names) if os.path.exists(vpath) else {}
+    trio = ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_BUBBLE_sum"]
+    tpath = os.path.join(prof, "tcc", "run_counter_collection.csv")
+    tcc = per_launch(tpath, trio) if os.path.exists(tpath) else {}
     trace = trace_stats(os.path.join(prof, "trace", "run_kernel_stats.csv"))
     os.makedirs(dest, exist_ok=True)
     for src, dst in (("trace/run_kernel_stats.csv", "kernel_stats.csv"),
                      ("fetch/run_counter_collection.csv", "pmc_fetch_size.csv"),
                      ("write/run_counter_collection.csv", "pmc_write_size.csv"),
-                     ("valu/run_counter_collection.csv", "pmc_valu.csv")):
+                     ("valu/run_counter_collection.csv", "pmc_valu.csv"),
+                     ("tcc/run_counter_collection.csv", "pmc_tcc_trio.csv")):
         if os.path.exists(os.path.join(prof, src)):
             shutil.copy(os.path.join(prof, src), os.path.join(dest, dst))
     kern = {}
@@ -106,7 +113,14 @@ def main():
         if n in fetch and n in write:
             k["fetch_kb"] = round(fetch[n]["FETCH_SIZE"], 1)
             k["write_kb"] = round(write[n]["WRITE_SIZE"], 1)
-            k["hbm_bytes_per_launch"] = int(round((2 * fetch[n]["FETCH_SIZE"] + write[n]["WRITE_SIZE"]) * 1024))
+            k["hbm_bytes_2x_fetch"] = int(round((2 * fetch[n]["FETCH_SIZE"] + write[n]["WRITE_SIZE"]) * 1024))
+            k["hbm_bytes_per_launch"] = k["hbm_bytes_2x_fetch"]
+            if n in tcc:
+                t = tcc[n]
+                rd, r32, bub = t["TCC_EA0_RDREQ_sum"], t["TCC_EA0_RDREQ_32B_sum"], t["TCC_BUBBLE_sum"]
+                k["read_requests"] = {"rdreq": rd, "rdreq_32b": r32, "bubble_128b": bub}
+                k["read_bytes_trio"] = int(round(128 * bub + 64 * (rd - bub - r32) + 32 * r32))
+                k["hbm_bytes_per_launch"] = int(round(k["read_bytes_trio"] + write[n]["WRITE_SIZE"] * 1024))
         if n in valu:
             v = valu[n]
             clk = v["GRBM_GUI_ACTIVE"] / 8
@@ -131,15 +145,18 @@ def main():
            "source": f"{rel}/ (rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE; SQ pass; "
                      "separate processes, bench.py --steps 3 on the headline workload)",
            "launches_kept": f"first {first_n()} dispatches per kernel (the headline leg)" if first_n() else "all",
-           "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts 128-B requests at 64 B); upper "
-                         "estimate for table gathers",
+           "correction": ("hbm = 128 TCC_BUBBLE + 64 (TCC_EA0_RDREQ - BUBBLE - RDREQ_32B) + 32 RDREQ_32B + WRITE_SIZE "
+                          "(each memory-side read request at its size; gfx950 FETCH_SIZE = RDREQ x 64 B), calibrated on "
+                          "tools/microbench/fetch_calib" if tcc else
+                          "hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts 128-B requests at 64 B); upper "
+                          "estimate for table gathers"),
            "kernels": kern,
            "hbm_bytes_per_launch": {n: k["hbm_bytes_per_launch"] for n, k in kern.items() if "hbm_bytes_per_launch" in k},
            "valu_issue": {n: k["valu"] for n, k in kern.items() if "valu" in k}}
     with open(os.path.join(dest, "pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     if os.environ.get("PMC_TRAFFIC_HEADLINE", "1") == "1":  # the file bench.py's roofline reads (TRAFFIC_FILE)
-        head = os.path.join(ROOT, os.environ.get("PMC_TRAFFIC_FILE", "profiles/r04/pmc_traffic.json"))
+        head = os.path.join(ROOT, os.environ.get("PMC_TRAFFIC_FILE", "profiles/r05/pmc_traffic.json"))
         os.makedirs(os.path.dirname(head), exist_ok=True)
         with open(head, "w") as f:
             json.dump(out, f, indent=1)

@@ -4,11 +4,11 @@ each its own process), written to profiles/r04/pmc_traffic.json (PMC_TRAFFIC_FIL
 
 HBM bytes (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE = TCC_EA0_RDREQ x 64 B, so a
 wide streaming read (128-B requests) reports half its bytes while a table gather (64-B requests)
-reports them exactly (profiles/r05/calib: fetch_calib's stream, 112-B-entry gathers and 16-B
-gathers against their known byte counts). Round 5: with the memory-side read-request trio pass
-(tcc/: TCC_EA0_RDREQ, TCC_EA0_RDREQ_32B, TCC_BUBBLE = 128-B requests) each request is priced at its
-own size, hbm = 128 BUBBLE + 64 (RDREQ - BUBBLE - RDREQ_32B) + 32 RDREQ_32B + WRITE_SIZE; without
-it, round 4's upper estimate 2 FETCH_SIZE + WRITE_SIZE.
+may report them exactly or at half (profiles/r05/calib: fetch_calib's stream, 112-B-entry gathers
+and 16-B gathers against their known byte counts). Round 5: with the read-requests-by-size pass
+(tcc/: TCC_EA0_RDREQ_32B / _64B / _128B, and _DRAM) each request is priced at its own size,
+hbm = 32 RDREQ_32B + 64 RDREQ_64B + 128 RDREQ_128B + WRITE_SIZE (TCC_BUBBLE, documented as the
+128-B requests, reads 0 on gfx950); without it, round 4's upper estimate 2 FETCH_SIZE + WRITE_SIZE.
 
 VALU issue: SQ_INSTS_VALU wave-instructions of the kernel priced per opcode (tools/isa_mix.py: the
 hottest loop's static instruction mix x the measured chip rate of each opcode,
@@ -93,7 +93,7 @@ def main():
                 "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64"]
     vpath = os.path.join(prof, "valu", "run_counter_collection.csv")
     valu = per_launch(vpath, sq_names) if os.path.exists(vpath) else {}
-    trio = ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_BUBBLE_sum"]
+    trio = ["TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum", "TCC_EA0_RDREQ_DRAM_sum"]
     tpath = os.path.join(prof, "tcc", "run_counter_collection.csv")
     tcc = per_launch(tpath, trio) if os.path.exists(tpath) else {}
     trace = trace_stats(os.path.join(prof, "trace", "run_kernel_stats.csv"))
@@ -117,9 +117,9 @@ def main():
             k["hbm_bytes_per_launch"] = k["hbm_bytes_2x_fetch"]
             if n in tcc:
                 t = tcc[n]
-                rd, r32, bub = t["TCC_EA0_RDREQ_sum"], t["TCC_EA0_RDREQ_32B_sum"], t["TCC_BUBBLE_sum"]
-                k["read_requests"] = {"rdreq": rd, "rdreq_32b": r32, "bubble_128b": bub}
-                k["read_bytes_trio"] = int(round(128 * bub + 64 * (rd - bub - r32) + 32 * r32))
+                r32, r64, r128 = t["TCC_EA0_RDREQ_32B_sum"], t["TCC_EA0_RDREQ_64B_sum"], t["TCC_EA0_RDREQ_128B_sum"]
+                k["read_requests"] = {"32b": r32, "64b": r64, "128b": r128, "dram": t["TCC_EA0_RDREQ_DRAM_sum"]}
+                k["read_bytes_trio"] = int(round(32 * r32 + 64 * r64 + 128 * r128))
                 k["hbm_bytes_per_launch"] = int(round(k["read_bytes_trio"] + write[n]["WRITE_SIZE"] * 1024))
         if n in valu:
             v = valu[n]
@@ -145,9 +145,9 @@ def main():
            "source": f"{rel}/ (rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE; --pmc WRITE_SIZE; SQ pass; "
                      "separate processes, bench.py --steps 3 on the headline workload)",
            "launches_kept": f"first {first_n()} dispatches per kernel (the headline leg)" if first_n() else "all",
-           "correction": ("hbm = 128 TCC_BUBBLE + 64 (TCC_EA0_RDREQ - BUBBLE - RDREQ_32B) + 32 RDREQ_32B + WRITE_SIZE "
-                          "(each memory-side read request at its size; gfx950 FETCH_SIZE = RDREQ x 64 B), calibrated on "
-                          "tools/microbench/fetch_calib" if tcc else
+           "correction": ("hbm = 32 TCC_EA0_RDREQ_32B + 64 RDREQ_64B + 128 RDREQ_128B + WRITE_SIZE (each memory-side "
+                          "read request at its size; gfx950 FETCH_SIZE = RDREQ x 64 B), checked on "
+                          "tools/microbench/fetch_calib (profiles/r05/calib)" if tcc else
                           "hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts 128-B requests at 64 B); upper "
                           "estimate for table gathers"),
            "kernels": kern,

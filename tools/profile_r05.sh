@@ -3,13 +3,13 @@
 # counter passes never combine --pmc with tracing domains.
 # usage: bash tools/profile_r05.sh <tag> <what...>
 #   headline  configs[4] shard (bench.py --steps 3): kernel trace + stats, FETCH_SIZE, WRITE_SIZE,
-#             the memory-side read-request trio (TCC_EA0_RDREQ, TCC_EA0_RDREQ_32B, TCC_BUBBLE), SQ
+#             the memory-side read requests by size (TCC_EA0_RDREQ_32B / _64B / _128B, _DRAM), SQ
 #   tx        the configs[3] transaction pipeline with a small headline: the same passes
 #   calib     tools/microbench/fetch_calib (known byte counts) under the same trio
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; shift
-TRIO="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_BUBBLE_sum"
+TRIO="TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_DRAM_sum"
 SQ="SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
 passes() {  # <outdir> <command...>
   local OUT=$1; shift

@@ -1412,12 +1412,40 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     c->fbt.push_back(ev);
   }
   if (htrace) c->fbh.assign(nch, 0.0);
+  // CG_SCAN_AHEAD=1 (A/B): chunk k+1's extent scan runs on the pool from a helper thread while this
+  // thread stages chunk k's copies (round 4 measured scanning ahead neutral to -1%, the copies'
+  // landing times did not move, profiles/r04/ahead; round 5's trace shows the main stream waiting
+  // 0.33 ms for chunk 1's bytes)
+  static const bool scan_ahead = [] {
+    const char* v = getenv("CG_SCAN_AHEAD");
+    return v && v[0] == '1';
+  }();
+  std::thread ahead_thr;
+  uint64_t ahead_k = ~0ull;
+  Extent ahead_ek, ahead_ik;
+  struct JoinAhead {  // every exit path joins the helper before the extents it writes go away
+    std::thread& t;
+    ~JoinAhead() {
+      if (t.joinable()) t.join();
+    }
+  } join_ahead{ahead_thr};
   auto copy_chunk = [&](uint64_t k, hipStream_t cs) {
     Extent ek, ik;
     const double h0 = htrace ? ms_since() : 0;
-    // (scanning the later chunks' extents ahead in a background thread measured neutral to -1%:
-    // the copies' landing times did not move, profiles/r04/ahead)
-    chunk_extents(k, ek, ik);
+    if (ahead_k == k) {
+      ahead_thr.join();
+      ek = ahead_ek;
+      ik = ahead_ik;
+      ahead_k = ~0ull;
+    } else {
+      chunk_extents(k, ek, ik);
+    }
+    if (scan_ahead && k + 1 < nch) {
+      ahead_k = k + 1;
+      ahead_ek = Extent();
+      ahead_ik = Extent();
+      ahead_thr = std::thread([&, k] { chunk_extents(k + 1, ahead_ek, ahead_ik); });
+    }
     const double h1 = htrace ? ms_since() : 0;
     const uint64_t first = bounds[k], cnt = bounds[k + 1] - bounds[k];
     hipError_t e = hipMemcpyAsync((cg_txsig*)c->h_sigs.p + first, sigs + first, sizeof(cg_txsig) * cnt,

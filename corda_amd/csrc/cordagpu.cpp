@@ -92,7 +92,7 @@ struct cg_ctx {
                    {nullptr, nullptr, nullptr}, nullptr};
   std::mutex mu;
   DevBuf keyprep, itemws, keys, items, arena, status, aux0, aux1, aux2;
-  // the constant fixed-base tables (B, both curves' G; 86 GB at radix 2^26), shared by every context
+  // the constant fixed-base tables (B, both curves' G; 91 GB at radix 2^26), shared by every context
   // of this process on the device (acquire_tables / release_tables)
   void* btab = nullptr;
   DevBuf wide;  // wide-table pools (keyws.h), sized by the largest call's item count
@@ -145,7 +145,7 @@ std::atomic<unsigned> g_live_ctx{0};
 
 // The constant fixed-base tables, one copy per device per process: read-only after the build, so
 // every context on the device (a cg_pool's slots, a test's second context) shares it instead of
-// holding its own 86 GB (keyws.h const_tab_bytes: Ed25519 B and both curves' G at radix 2^26).
+// holding its own 91 GB (keyws.h const_tab_bytes: Ed25519 B and both curves' G at radix 2^26).
 struct SharedTables {
   int device;
   void* p;

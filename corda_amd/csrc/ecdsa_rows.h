@@ -134,8 +134,8 @@ struct EcRowScratch {
 };
 
 // cnt (<= EC_MULT) affine points first + k step, k = 0..cnt-1, with one batched inversion.
-template <int C>
-CG_HD void ec_multiples(EcAff* out, const Jac& first, const Jac& step, int cnt, EcRowScratch& s, const EcConsts& K) {
+template <int C, class Out>
+CG_HD void ec_multiples(Out* out, const Jac& first, const Jac& step, int cnt, EcRowScratch& s, const EcConsts& K) {
   Jac acc = first;
   s.p[0] = acc;
   s.pre[0] = acc.Z;
@@ -500,8 +500,23 @@ static_assert(EC_WIDE_GDIGITS * EC_WIDE_GW > 256, "G digits: room for the recodi
 struct EcWideTab {
   EcAff t[EC_WIDE_ROWS][EC_WIDE_MULT];  // t[j][k-1] = k 2^{8j} Q; t[32][k-1] = (128 + k) 2^{248} Q
 };
+// G entries: EC_GWIDE_ENTRY_BYTES 128 (A/B) pads each 72-B entry to one 128-B line (a random
+// gather then fetches one line instead of ~1.55, as the Ed25519 B entries, fe9.h GE9_NIELS_BYTES),
+// at 42.9 instead of 24.2 GB per curve. Measured slower: 336.3 -> 332.4 M sigs/s over 4 pairs
+// (profiles/r05/ecg128); the 72-B packing stays.
+#ifndef EC_GWIDE_ENTRY_BYTES
+#define EC_GWIDE_ENTRY_BYTES 72
+#endif
+#if EC_GWIDE_ENTRY_BYTES == 72
+typedef EcAff EcAffG;
+#else
+struct EcAffG : EcAff {
+  uint32_t pad[(EC_GWIDE_ENTRY_BYTES - 72) / 4];
+};
+static_assert(sizeof(EcAffG) == EC_GWIDE_ENTRY_BYTES, "padded G entry");
+#endif
 struct EcGWideTab {
-  EcAff t[EC_WIDE_GDIGITS][EC_WIDE_GMULT];  // t[u][k-1] = k 2^{EC_WIDE_GW u} G
+  EcAffG t[EC_WIDE_GDIGITS][EC_WIDE_GMULT];  // t[u][k-1] = k 2^{EC_WIDE_GW u} G
 };
 // Batch-inversion scratch of one wide row (the Jacobian X, Y wait in the output entries)
 struct EcWideScratch {
@@ -994,8 +1009,8 @@ CG_HD uint32_t ecdsa_ladder_check_wide(const u256w& u1, const u256w& u2, const u
 
 // G wide row u, multiples 32 g + 1 .. 32 g + 32 (one lane of the per-context table build)
 // (the group from the row's base P = 2^{EC_WIDE_GW u} G: the host tests build only the groups their digits touch)
-template <int C>
-CG_HD void ec_gwide_group_from(EcAff* out, const Jac& P, int g, EcRowScratch& s, const EcConsts& K) {
+template <int C, class Out>
+CG_HD void ec_gwide_group_from(Out* out, const Jac& P, int g, EcRowScratch& s, const EcConsts& K) {
   const uint32_t m = 32u * (uint32_t)g + 1u;
   Jac F = P;
   for (int b = 30 - __builtin_clz(m); b >= 0; --b) {
@@ -1005,8 +1020,8 @@ CG_HD void ec_gwide_group_from(EcAff* out, const Jac& P, int g, EcRowScratch& s,
   ec_multiples<C>(out, F, P, EC_MULT, s, K);
 }
 
-template <int C>
-CG_HD void ec_gwide_group(EcAff* out, int u, int g, EcRowScratch& s, const EcConsts& K) {
+template <int C, class Out>
+CG_HD void ec_gwide_group(Out* out, int u, int g, EcRowScratch& s, const EcConsts& K) {
   Jac P = {K.gx, K.gy, K.one_p};
   if (u > 0) jac_dbl_n<C>(P, P, EC_WIDE_GW * u);
   ec_gwide_group_from<C>(out, P, g, s, K);

@@ -864,7 +864,7 @@ CG_HD void ed_wide_row_build9(ge9_niels* out, const Park& pk, const ge_p3& P, in
     fe9_carry(n.ymx, s);
     fe9_mul<false>(xy, x, y);
     fe9_mul<false>(n.xy2d, xy, d4);
-    n.pad = 0;
+    for (uint32_t& w : n.pad) w = 0;
     out[k] = n;
   }
 }

@@ -327,19 +327,27 @@ CG_HD void fe_from_fe9(fe& h, const fe9& f) {
 struct ge9_p3 {
   fe9 X, Y, Z, T;
 };
-// A half-scaled wide-table entry ((y+x)/2, (y-x)/2, x y d), tight; padded to 112 B (7 x 16-B LDS
-// DMA chunks, 16-B aligned rows).
+// A half-scaled wide-table entry ((y+x)/2, (y-x)/2, x y d), tight: 108 B of limbs, gathered as
+// 7 x 16-B LDS DMA chunks. Padded to one 128-B line (round 5; GE9_NIELS_BYTES 112 = the round-4
+// packing): a random gather into the fixed-base table then fetches one line instead of 1.9 (every
+// HBM read request is a 128-B line on gfx950, profiles/r05/calib). The B table grows 37.6 -> 42.9 GB;
+// headline A/B 326.9 -> 332.5 M sigs/s over 4 pairs (Ed25519 ladder 13.06 -> 12.75 ms per step,
+// profiles/r05/n128).
+#ifndef GE9_NIELS_BYTES
+#define GE9_NIELS_BYTES 128
+#endif
 struct ge9_niels {
   fe9 ypx, ymx, xy2d;
-  uint32_t pad;
+  uint32_t pad[(GE9_NIELS_BYTES - 108) / 4];
 };
-static_assert(sizeof(ge9_niels) == 112, "ge9_niels layout");
+static_assert(sizeof(ge9_niels) == GE9_NIELS_BYTES && (GE9_NIELS_BYTES == 112 || GE9_NIELS_BYTES == 128),
+              "ge9_niels layout");
 
 CG_HD void ge9_niels_from(ge9_niels& o, const ge_niels& n) {
   fe9_from_fe(o.ypx, n.ypx);
   fe9_from_fe(o.ymx, n.ymx);
   fe9_from_fe(o.xy2d, n.xy2d);
-  o.pad = 0;
+  for (uint32_t& w : o.pad) w = 0;
 }
 // store overloads for the table builders (the host tests also build fe tables)
 CG_HD void ed_niels_store(ge_niels* dst, const ge_niels& n) { *dst = n; }

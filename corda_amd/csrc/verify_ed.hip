@@ -665,7 +665,7 @@ __device__ __forceinline__ void ed_lds_niels9(ge9_niels& n, const uint8_t* wave_
     if (c < 6) d[4 * c + 3] = v.w;  // the pad dword stays unread
   }
 }
-static_assert(64 * sizeof(ge9_niels) <= EdOps::kWaveBytes, "the LDS image holds either entry form");
+static_assert(64 * 7 * 16 <= EdOps::kWaveBytes, "the LDS image (7 chunks a lane) holds either entry form");
 
 __device__ __forceinline__ const ge_niels* ed_op_src(const EdTab& TA, int row, int d) {
   const int a = d < 0 ? -d : d;

@@ -556,5 +556,8 @@ void ec_launch_ladder(int curve, bool full, const cg_item* d_items, uint64_t n_i
                       const KeyWs& w, const ItemWs& iw, const void* d_btab, hipStream_t stream);
 void ec_launch_ladder_wide(int curve, const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
                            const ItemWs& iw, const void* d_btab, hipStream_t stream);
+// both curves' wide ladders in one launch (verify_ec.hip k_ec_ladder_wide2)
+void ec_launch_ladder_wide_merged(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                                  const ItemWs& iw, const void* d_btab, hipStream_t stream);
 
 }  // namespace cg

@@ -508,6 +508,13 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
     const char* v = getenv("CG_EC_LADDER_SIDE");
     return v ? (uint32_t)strtoul(v, nullptr, 10) & 3u : 0u;
   }();
+  // CG_EC_WIDE_MERGED=1 (A/B): the two curves' wide ladders as one launch after both full-table
+  // ladders (k_ec_ladder_wide2), timed as the r1 wide stage
+  static const bool ec_merged = [] {
+    const char* v = getenv("CG_EC_WIDE_MERGED");
+    return v && v[0] == '1';
+  }();
+  const bool merged = ec_merged && !ec_side && w.cap_ec;
   for (int k = 0; k < 2; ++k) {
     const int curve = k == 0 ? CG_CURVE_R1 : CG_CURVE_K1;
     const bool side = fork && (ec_side >> k & 1u);
@@ -516,7 +523,7 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
     if (fork && fork->pending.ec_front_side) hipStreamWaitEvent(s, fork->ec_front_done[k], 0);
     CG_TIME(fork, k == 0 ? CG_STAGE_R1_LADDER : CG_STAGE_K1_LADDER, s,
             ec_launch_ladder(curve, true, d_items, n_items, d_status, w, iw, d_btab, s));
-    if (w.cap_ec)
+    if (w.cap_ec && !merged)
       CG_TIME(fork, k == 0 ? CG_STAGE_R1_LADDER_WIDE : CG_STAGE_K1_LADDER_WIDE, s,
               ec_launch_ladder_wide(curve, d_items, n_items, d_status, w, iw, d_btab, s));
     if (side) {  // the join below waits for this stream's last ladder
@@ -524,6 +531,9 @@ hipError_t launch_items_back(const cg_key* d_keys, uint32_t n_keys, const cg_ite
       if (e != hipSuccess) return e;
     }
   }
+  if (merged)
+    CG_TIME(fork, CG_STAGE_R1_LADDER_WIDE, stream,
+            ec_launch_ladder_wide_merged(d_items, n_items, d_status, w, iw, d_btab, stream));
   if (fork) {
     if (fork->mark) hipEventRecord(fork->mark, stream);
     hipStreamWaitEvent(stream, fork->row0[0], 0);

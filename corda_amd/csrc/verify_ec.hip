@@ -409,6 +409,45 @@ __device__ __forceinline__ const EcAff* ec_wide_src(const EcWideTab& TQ, const E
 #ifndef EC_LADDER_WIDE_WAVES  // waves per SIMD the wide ladders' registers must allow: 3 (168 VGPRs, 20 B of
 #define EC_LADDER_WIDE_WAVES 3  // scratch for r1) against the compiler's 172 at 2: r1 1.73 -> 1.67 ms (profiles/r04/ecw3)
 #endif
+// One plan position of a wide-table ECDSA item: u1 G + u2 Q over the wide tables, then BC's x check.
+template <int C>
+__device__ __forceinline__ void ec_wide_item(uint64_t p, const cg_item* __restrict__ items,
+                                             const uint32_t* __restrict__ perm, const uint32_t* __restrict__ wide_idx,
+                                             const EcWideSlot* __restrict__ wec, const EcGWideTab* __restrict__ gw,
+                                             uint8_t* __restrict__ status, const EcItemWs* __restrict__ ws,
+                                             const uint8_t* wave_lds, uint32_t wl, uint32_t lane) {
+  const EcConsts& K = c_ec[C];
+  const uint32_t i = perm[p];
+  if (status[i] != EC_PENDING_BASE + C) return;
+  // every lane still here runs the same DMA sequence; lanes that left do not take part, and the
+  // LDS image is per lane, so no barrier is needed
+  const uint32_t key = items[i].key_idx;
+  const EcItemWs w = ws[p];
+  const EcWideTab& TQ = wec[wide_idx[key]].tab;
+  uint32_t dg[EC_WIDE_GPACKED], dq[EC_WIDE_PACKED];
+  ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS, false, EC_WIDE_GBITS>(dg, w.a);
+  ec_recode_wide<EC_WIDE_W, EC_WIDE_DIGITS, true>(dq, w.b);
+  Jac R;
+  jac_set_inf<C>(R, K);
+  bool inf = true;
+  int d_next = ec_wide_digit(dq, dg, 0);
+  ec_glds_aff(ec_wide_src(TQ, *gw, 0, d_next), wl);
+#pragma unroll 1
+  for (int o = 0; o < EC_WIDE_OPS; ++o) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // op o's entry
+    f29 x, y;
+    ec_lds_aff(x, y, wave_lds, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
+    const int d = d_next;
+    if (o + 1 < EC_WIDE_OPS) {
+      d_next = ec_wide_digit(dq, dg, o + 1);
+      ec_glds_aff(ec_wide_src(TQ, *gw, o + 1, d_next), wl);
+    }
+    if (d != 0) jac_madd9<C>(R, inf, x, y, d < 0, K);  // signed-limb form (ec9.h)
+  }
+  status[i] = (uint8_t)ecdsa_x_check9<C>(R, w.r, K);
+}
+
 template <int C>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_LADDER_WIDE_WAVES)))
 k_ec_ladder_wide(const cg_item* __restrict__ items,
@@ -424,38 +463,31 @@ k_ec_ladder_wide(const cg_item* __restrict__ items,
   uint8_t* wave_lds = stage + (threadIdx.x >> 6) * EC_WAVE_LDS;
   const uint32_t wl = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(ec_lds_ptr)wave_lds);
   const uint32_t lane = __lane_id();
-  const EcConsts& K = c_ec[C];
-  for (Walk wk = walk_units(end - beg); wk.u < wk.end; wk.u += wk.step) {
-    const uint64_t p = beg + wk.u;
-    const uint32_t i = perm[p];
-    if (status[i] != EC_PENDING_BASE + C) continue;
-    // every lane still here runs the same DMA sequence; lanes that left do not take part, and the
-    // LDS image is per lane, so no barrier is needed
-    const uint32_t key = items[i].key_idx;
-    const EcItemWs w = ws[p];
-    const EcWideTab& TQ = wec[wide_idx[key]].tab;
-    uint32_t dg[EC_WIDE_GPACKED], dq[EC_WIDE_PACKED];
-    ec_recode_wide<EC_WIDE_GW, EC_WIDE_GDIGITS, false, EC_WIDE_GBITS>(dg, w.a);
-    ec_recode_wide<EC_WIDE_W, EC_WIDE_DIGITS, true>(dq, w.b);
-    Jac R;
-    jac_set_inf<C>(R, K);
-    bool inf = true;
-    int d_next = ec_wide_digit(dq, dg, 0);
-    ec_glds_aff(ec_wide_src(TQ, *gw, 0, d_next), wl);
-#pragma unroll 1
-    for (int o = 0; o < EC_WIDE_OPS; ++o) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // op o's entry
-      f29 x, y;
-      ec_lds_aff(x, y, wave_lds, lane);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
-      const int d = d_next;
-      if (o + 1 < EC_WIDE_OPS) {
-        d_next = ec_wide_digit(dq, dg, o + 1);
-        ec_glds_aff(ec_wide_src(TQ, *gw, o + 1, d_next), wl);
-      }
-      if (d != 0) jac_madd9<C>(R, inf, x, y, d < 0, K);  // signed-limb form (ec9.h)
-    }
-    status[i] = (uint8_t)ecdsa_x_check9<C>(R, w.r, K);
+  for (Walk wk = walk_units(end - beg); wk.u < wk.end; wk.u += wk.step)
+    ec_wide_item<C>(beg + wk.u, items, perm, wide_idx, wec, gw, status, ws, wave_lds, wl, lane);
+}
+
+// CG_EC_WIDE_MERGED (A/B): both curves' wide items in one launch, the secp256r1 range then the
+// secp256k1 range walked as one (a curve's launch alone leaves a partial last round of waves: the
+// k1 range is ~1.2 rounds of the resident lanes); a wave's items are of one curve except at the seam.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_LADDER_WIDE_WAVES)))
+k_ec_ladder_wide2(const cg_item* __restrict__ items, const uint32_t* __restrict__ perm,
+                  const uint32_t* __restrict__ ranges, const uint32_t* __restrict__ wide_idx,
+                  const EcWideSlot* __restrict__ wec, const EcGWideTab* __restrict__ gw_r1,
+                  const EcGWideTab* __restrict__ gw_k1, uint8_t* __restrict__ status,
+                  const EcItemWs* __restrict__ ws) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4 * EC_WAVE_LDS];
+  const int c1 = plan_class_of_curve(CG_CURVE_R1), c0 = plan_class_of_curve(CG_CURVE_K1);
+  const uint32_t b1 = ranges[PLAN_WIDE + c1], n1 = ranges[c1 + 1] - b1;
+  const uint32_t b0 = ranges[PLAN_WIDE + c0], n0 = ranges[c0 + 1] - b0;
+  uint8_t* wave_lds = stage + (threadIdx.x >> 6) * EC_WAVE_LDS;
+  const uint32_t wl = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(ec_lds_ptr)wave_lds);
+  const uint32_t lane = __lane_id();
+  for (Walk wk = walk_units((uint64_t)n1 + n0); wk.u < wk.end; wk.u += wk.step) {
+    if (wk.u < n1)
+      ec_wide_item<CG_CURVE_R1>(b1 + wk.u, items, perm, wide_idx, wec, gw_r1, status, ws, wave_lds, wl, lane);
+    else
+      ec_wide_item<CG_CURVE_K1>(b0 + (wk.u - n1), items, perm, wide_idx, wec, gw_k1, status, ws, wave_lds, wl, lane);
   }
 }
 
@@ -631,6 +663,14 @@ void ec_launch_ladder_wide(int curve, const cg_item* d_items, uint64_t n_items, 
                            const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   if (curve == CG_CURVE_R1) launch_ladder_wide_t<CG_CURVE_R1>(d_items, n_items, d_status, w, iw, d_btab, stream);
   else launch_ladder_wide_t<CG_CURVE_K1>(d_items, n_items, d_status, w, iw, d_btab, stream);
+}
+
+void ec_launch_ladder_wide_merged(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
+                                  const ItemWs& iw, const void* d_btab, hipStream_t stream) {
+  const uint32_t B = 256;
+  hipLaunchKernelGGL(k_ec_ladder_wide2, dim3(walk_grid(n_items, B, WALK_CAP(EC_LADDER_WIDE_WAVES))), dim3(B), 0, stream,
+                     d_items, iw.perm, iw.ranges, (const uint32_t*)w.wide_idx, (const EcWideSlot*)w.wec,
+                     gwide(d_btab, CG_CURVE_R1), gwide(d_btab, CG_CURVE_K1), d_status, (const EcItemWs*)iw.slots);
 }
 
 }  // namespace cg

@@ -1,5 +1,6 @@
 // Internal interface between the C ABI host code (cordagpu.cpp) and the HIP kernels.
 #pragma once
+#include <functional>
 #include <stdlib.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -101,6 +102,9 @@ struct Fork {
   hipEvent_t ec_front_go = nullptr, ec_front_done[2] = {nullptr, nullptr};
   mutable PendingTabs pending;
   hipEvent_t mark = nullptr;  // CG_HOST_TRACE: recorded on the main stream before a back's final joins
+  // Host hook launch_items_front runs once between a chunk's plan and its hashes (the host path's
+  // CG_SPLIT_COPY: the chunk's signature bytes are copied there, after its plan is enqueued)
+  const std::function<hipError_t()>* mid_front = nullptr;
 };
 
 // Dynamic LDS reserved by each row-base chain workgroup (CG_CHAIN_SPREAD=1: more than half a CU's

@@ -399,6 +399,7 @@ hipError_t launch_items_front(const cg_key* d_keys, uint32_t n_keys, const cg_it
   if (!planned)
     e = launch_items_plan(d_keys, n_keys, d_items, n_items, d_status, d_keyprep, d_item_ws, stream, fork, wide);
   if (e == hipSuccess && fork) e = launch_pending_tabs(fork, stream);  // the first front starts the table builds
+  if (e == hipSuccess && fork && fork->mid_front) e = (*fork->mid_front)();  // (the hook clears itself)
   if (e != hipSuccess) return e;
   // fronts: Ed25519 challenges (need only Abyte), ECDSA prep + s^-1 per curve (need the decoded key).
   // CG_EC_FRONT_SIDE: each curve's front on its side stream beside the challenge hashes (its

@@ -133,6 +133,55 @@ struct EcRowScratch {
   f29 pre[EC_MULT];
 };
 
+// A G wide-table entry packed into 64 B (EC_GWIDE_PACK, A/B): x and y as canonical 256-bit values
+// (little-endian dwords), so a random gather is one 128-B line request instead of ~1.5 and the
+// table is 21.5 instead of 24.2 GB per curve; the ladder unpacks the 29-bit limbs (ec_unpack256).
+// Measured: ECDSA wide ladders 7.72 / 3.43 -> 7.79 / 3.46 ms per step (r1 / k1), headline within
+// noise (profiles/r05/ec_pack): the unpacking costs what the bytes saved; the 72-B entries stay.
+struct EcAffG64 {
+  uint32_t w[16];
+};
+CG_HD void ec_pack256(uint32_t* w, const f29& a) {  // a canonical (< 2^256)
+  uint64_t acc = 0;
+  int bits = 0, j = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    acc |= (uint64_t)a.v[i] << bits;
+    bits += 29;
+    if (bits >= 32) {
+      w[j++] = (uint32_t)acc;
+      acc >>= 32;
+      bits -= 32;
+    }
+  }
+  FE_ASSERT(j == 8 && acc == 0);
+}
+CG_HD void ec_unpack256(f29& a, const uint32_t* w) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int b = 29 * i, j = b >> 5, sh = b & 31;
+    const uint32_t lo = w[j], hi = j + 1 < 8 ? w[j + 1] : 0u;
+    a.v[i] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & M29_MASK;
+  }
+}
+template <int C>
+CG_HD void ec_put(EcAff& o, const f29& x, const f29& y) {
+  o.x = x;
+  o.y = y;
+}
+template <int C>
+CG_HD void ec_put(EcAffG64& o, const f29& x, const f29& y) {
+  f29 c;
+  m29_canon<C, 0>(c, x);
+  ec_pack256(o.w, c);
+  m29_canon<C, 0>(c, y);
+  ec_pack256(o.w + 8, c);
+}
+CG_HD void ec_pick(f29& x, f29& y, const EcAffG64* row, int a) {
+  ec_unpack256(x, row[a - 1].w);
+  ec_unpack256(y, row[a - 1].w + 8);
+}
+
 // cnt (<= EC_MULT) affine points first + k step, k = 0..cnt-1, with one batched inversion.
 template <int C, class Out>
 CG_HD void ec_multiples(Out* out, const Jac& first, const Jac& step, int cnt, EcRowScratch& s, const EcConsts& K) {
@@ -156,8 +205,10 @@ CG_HD void ec_multiples(Out* out, const Jac& first, const Jac& step, int cnt, Ec
     }
     m29_sq<C, 0>(zi2, zi);
     m29_mul<C, 0>(zi3, zi2, zi);
-    m29_mul<C, 0>(out[k].x, s.p[k].X, zi2);
-    m29_mul<C, 0>(out[k].y, s.p[k].Y, zi3);
+    f29 ox, oy;
+    m29_mul<C, 0>(ox, s.p[k].X, zi2);
+    m29_mul<C, 0>(oy, s.p[k].Y, zi3);
+    ec_put<C>(out[k], ox, oy);
   }
 }
 
@@ -507,7 +558,12 @@ struct EcWideTab {
 #ifndef EC_GWIDE_ENTRY_BYTES
 #define EC_GWIDE_ENTRY_BYTES 72
 #endif
-#if EC_GWIDE_ENTRY_BYTES == 72
+#ifndef EC_GWIDE_PACK
+#define EC_GWIDE_PACK 0
+#endif
+#if EC_GWIDE_PACK
+typedef EcAffG64 EcAffG;
+#elif EC_GWIDE_ENTRY_BYTES == 72
 typedef EcAff EcAffG;
 #else
 struct EcAffG : EcAff {

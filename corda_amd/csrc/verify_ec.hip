@@ -400,10 +400,39 @@ __device__ __forceinline__ void ec_lds_aff(f29& x, f29& y, const uint8_t* wave_l
 __device__ __forceinline__ int ec_wide_digit(const uint32_t* dq, const uint32_t* dg, int o) {
   return o < EC_WIDE_DIGITS ? ec_digit10(dq, o) : ec_digit_at<EC_WIDE_GBITS>(dg, o - EC_WIDE_DIGITS);
 }
-__device__ __forceinline__ const EcAff* ec_wide_src(const EcWideTab& TQ, const EcGWideTab& TG, int o, int d) {
+__device__ __forceinline__ const void* ec_wide_src(const EcWideTab& TQ, const EcGWideTab& TG, int o, int d) {
   const int a = d < 0 ? -d : d;
   if (o < EC_WIDE_DIGITS) return a > EC_WIDE_MULT ? &TQ.t[EC_WIDE_DIGITS][a - EC_WIDE_MULT - 1] : &TQ.t[o][a > 0 ? a - 1 : 0];
   return &TG.t[o - EC_WIDE_DIGITS][a > 0 ? a - 1 : 0];
+}
+// op o's entry into / out of the wave's LDS image: the 72-B affine form, or (EC_GWIDE_PACK, G rows)
+// the 64-B packed form, 4 x 16-B chunks unpacked to limbs
+__device__ __forceinline__ void ec_wide_gather(const void* src, int o, uint32_t wl) {
+  if (EC_GWIDE_PACK && o >= EC_WIDE_DIGITS) {
+    const uint8_t* s = (const uint8_t*)src;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      __builtin_amdgcn_global_load_lds((ec_gbl_ptr)(s + 16 * c), ec_lds_at(wl, 64 * 16 * c), 16, 0, 0);
+  } else {
+    ec_glds_aff((const EcAff*)src, wl);
+  }
+}
+__device__ __forceinline__ void ec_wide_read(f29& x, f29& y, int o, const uint8_t* wave_lds, uint32_t lane) {
+  if (EC_GWIDE_PACK && o >= EC_WIDE_DIGITS) {
+    uint32_t w[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint4 v = *(const uint4*)(wave_lds + 64 * 16 * c + 16 * lane);
+      w[4 * c] = v.x;
+      w[4 * c + 1] = v.y;
+      w[4 * c + 2] = v.z;
+      w[4 * c + 3] = v.w;
+    }
+    ec_unpack256(x, w);
+    ec_unpack256(y, w + 8);
+  } else {
+    ec_lds_aff(x, y, wave_lds, lane);
+  }
 }
 
 #ifndef EC_LADDER_WIDE_WAVES  // waves per SIMD the wide ladders' registers must allow: 3 (168 VGPRs, 20 B of
@@ -431,17 +460,17 @@ __device__ __forceinline__ void ec_wide_item(uint64_t p, const cg_item* __restri
   jac_set_inf<C>(R, K);
   bool inf = true;
   int d_next = ec_wide_digit(dq, dg, 0);
-  ec_glds_aff(ec_wide_src(TQ, *gw, 0, d_next), wl);
+  ec_wide_gather(ec_wide_src(TQ, *gw, 0, d_next), 0, wl);
 #pragma unroll 1
   for (int o = 0; o < EC_WIDE_OPS; ++o) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // op o's entry
     f29 x, y;
-    ec_lds_aff(x, y, wave_lds, lane);
+    ec_wide_read(x, y, o, wave_lds, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot read before the next DMA lands
     const int d = d_next;
     if (o + 1 < EC_WIDE_OPS) {
       d_next = ec_wide_digit(dq, dg, o + 1);
-      ec_glds_aff(ec_wide_src(TQ, *gw, o + 1, d_next), wl);
+      ec_wide_gather(ec_wide_src(TQ, *gw, o + 1, d_next), o + 1, wl);
     }
     if (d != 0) jac_madd9<C>(R, inf, x, y, d < 0, K);  // signed-limb form (ec9.h)
   }

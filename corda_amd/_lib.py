@@ -31,7 +31,12 @@ class cg_stats(ctypes.Structure):
 class cg_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32), ("max_items", ctypes.c_uint64),
                 ("max_arena", ctypes.c_uint64), ("chunk_items", ctypes.c_uint64), ("host_threads", ctypes.c_uint32),
-                ("reserved0", ctypes.c_uint32), ("reserved", ctypes.c_uint64 * 2)]
+                ("reserved0", ctypes.c_uint32), ("table_bytes_max", ctypes.c_uint64), ("reserved1", ctypes.c_uint64)]
+
+
+class cg_info(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("fixed_base_bits", ctypes.c_uint32), ("table_bytes", ctypes.c_uint64),
+                ("host_threads", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("chunk_items", ctypes.c_uint64)]
 
 
 class cg_pool_stats(ctypes.Structure):
@@ -120,6 +125,17 @@ def lib():
                 L.cg_pool_verify_tx_signatures.restype = i32
                 L.cg_pool_inject_fault.argtypes = [vp, u32, i32]
                 L.cg_pool_inject_fault.restype = i32
+                if hasattr(L, "cg_pool_verify_transactions"):
+                    L.cg_pool_verify_transactions.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp, u64, vp, u32, vp, u64,
+                                                              u32, vp, vp, vp, ctypes.POINTER(cg_pool_stats)]
+                    L.cg_pool_verify_transactions.restype = i32
+            if hasattr(L, "cg_context_info"):  # round 6: the fixed-base table budget
+                L.cg_context_info.argtypes = [vp, ctypes.POINTER(cg_info)]
+                L.cg_context_info.restype = i32
+                L.cg_table_bytes.argtypes = [u32]
+                L.cg_table_bytes.restype = u64
+                L.cg_table_choice.argtypes = [u64, u64]
+                L.cg_table_choice.restype = u32
             for name in ("cg_verify_filtered", "cg_verify_filtered_device", "cg_verify_transactions", "cg_verify_transactions_device", "cg_reserve", "cg_verify_batch", "cg_verify_batch_device", "cg_sha256_batch",
                          "cg_sha512_batch", "cg_sha256_batch_device", "cg_merkle_roots", "cg_tx_ids",
                          "cg_tx_ids_device"):

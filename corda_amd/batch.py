@@ -122,6 +122,10 @@ class Batch:
     def n(self):
         return len(self.items)
 
+    def subset(self, idx):
+        """The items ``idx`` over the same key table and arena (a re-queue of NOT_RUN items)."""
+        return Batch(self.keys, np.ascontiguousarray(self.items[idx]), self.arena)
+
 
 class BatchBuilder:
     def __init__(self):
@@ -206,6 +210,10 @@ class TxSigBatch:
     @property
     def n_ids(self):
         return self.ids.size // 32
+
+    def subset(self, idx):
+        """The signatures ``idx`` over the same keys, ids, templates and arena (a re-queue)."""
+        return TxSigBatch(self.keys, self.ids, np.ascontiguousarray(self.sigs[idx]), self.tmpls, self.arena)
 
 
 class TxSigBuilder(BatchBuilder):

@@ -25,6 +25,15 @@
 #include "host_budget.h"
 #include "host_pool.h"
 #include "pool.h"
+#include "table_budget.h"
+
+// the other builds of the radix-dependent kernels (Makefile VARIANTS; engine.h EngineVariant)
+namespace cg24 {
+const cgt::EngineVariant& variant();
+}
+namespace cg22 {
+const cgt::EngineVariant& variant();
+}
 
 namespace {
 
@@ -92,9 +101,12 @@ struct cg_ctx {
                    {nullptr, nullptr, nullptr}, nullptr};
   std::mutex mu;
   DevBuf keyprep, itemws, keys, items, arena, status, aux0, aux1, aux2;
-  // the constant fixed-base tables (B, both curves' G; 91 GB at radix 2^26), shared by every context
-  // of this process on the device (acquire_tables / release_tables)
+  // the constant fixed-base tables (B, both curves' G; 91 GB at radix 2^26, 25 GB at 2^24, 6.9 GB at
+  // 2^22), shared by every context of this process on the device (acquire_tables / release_tables),
+  // and the build of the radix-dependent kernels that reads them (table_budget.h picks it at cg_open)
   void* btab = nullptr;
+  const cgt::EngineVariant* eng = nullptr;
+  uint64_t tab_bytes = 0;
   DevBuf wide;  // wide-table pools (keyws.h), sized by the largest call's item count
   // wide slots this context may allocate: lowered when the device's free memory cannot hold the
   // pool a call asks for (another process or context on the device), so the call runs
@@ -144,42 +156,72 @@ namespace {
 // contexts open in this process (the default host budget divides the CPU quota among them)
 std::atomic<unsigned> g_live_ctx{0};
 
+// The builds of the radix-dependent kernels, largest tables first (table_budget.h).
+const cgt::EngineVariant* const kVariants[] = {&cg::variant(), &cg24::variant(), &cg22::variant()};
+constexpr int kNumVariants = 3;
+
+std::vector<cgb::TableSet> table_sets() {
+  std::vector<cgb::TableSet> v;
+  for (const cgt::EngineVariant* e : kVariants) v.push_back({e->fixed_base_bits, (uint64_t)e->btab_bytes()});
+  return v;
+}
+
 // The constant fixed-base tables, one copy per device per process: read-only after the build, so
 // every context on the device (a cg_pool's slots, a test's second context) shares it instead of
-// holding its own 91 GB (keyws.h const_tab_bytes: Ed25519 B and both curves' G at radix 2^26).
+// holding its own (keyws.h const_tab_bytes: Ed25519 B and both curves' G at the variant's radix).
 struct SharedTables {
   int device;
+  int variant;
   void* p;
   unsigned refs;
 };
 std::mutex g_tab_mu;
 std::vector<SharedTables> g_tabs;
 
-hipError_t acquire_tables(int device, hipStream_t s, void** out) {
+// Picks the tables for a context on `device` under `budget` (0: automatic) and builds or shares them:
+// *out = the tables, *variant = the kernel build that reads them. Automatic: when the device cannot
+// allocate the set the free memory suggested (another process took it meanwhile), the next smaller.
+hipError_t acquire_tables(int device, hipStream_t s, uint64_t budget, void** out, int* variant) {
   std::lock_guard<std::mutex> g(g_tab_mu);
+  const std::vector<cgb::TableSet> sets = table_sets();
+  int held = -1;
+  for (const SharedTables& t : g_tabs)
+    if (t.device == device && (held < 0 || t.variant < held)) held = t.variant;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+  const int pick = cgb::pick_tables(sets.data(), kNumVariants, budget, free_b, held);
+  if (pick < 0) return hipErrorInvalidValue;
   for (SharedTables& t : g_tabs)
-    if (t.device == device) {
+    if (t.device == device && t.variant == pick) {
       ++t.refs;
       *out = t.p;
+      *variant = pick;
       return hipSuccess;
     }
-  void* p = nullptr;
-  hipError_t e = hipMalloc(&p, cg::btab_bytes());
-  if (e != hipSuccess) return e;
-  {  // built once over a temporary scratch, freed afterwards
-    DevBuf scratch;
-    e = scratch.ensure(cg::btab_scratch_bytes());
-    if (e == hipSuccess) e = cg::init_btab(p, scratch.p, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    scratch.release();
+  hipError_t e = hipErrorOutOfMemory;
+  for (int v = pick; v < kNumVariants; ++v) {
+    if (budget && sets[v].bytes > budget) continue;
+    void* p = nullptr;
+    e = hipMalloc(&p, sets[v].bytes);
+    if (e == hipSuccess) {  // built once over a temporary scratch, freed afterwards
+      DevBuf scratch;
+      e = scratch.ensure(kVariants[v]->btab_scratch_bytes());
+      if (e == hipSuccess) e = kVariants[v]->upload_constants();
+      if (e == hipSuccess) e = kVariants[v]->init_btab(p, scratch.p, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      scratch.release();
+      if (e == hipSuccess) {
+        g_tabs.push_back({device, v, p, 1u});
+        *out = p;
+        *variant = v;
+        return hipSuccess;
+      }
+      hipFree(p);
+    }
+    (void)hipGetLastError();
+    if (e != hipErrorOutOfMemory || budget) break;  // only the automatic choice steps down
   }
-  if (e != hipSuccess) {
-    hipFree(p);
-    return e;
-  }
-  g_tabs.push_back({device, p, 1u});
-  *out = p;
-  return hipSuccess;
+  return e;
 }
 
 void release_tables(int device, void* p) {
@@ -200,7 +242,8 @@ void release_tables(int device, void* p) {
 unsigned host_threads_of(cg_ctx* c, uint64_t n) {
   if (n < (1u << 16)) return 1;
   const unsigned nt = cg::host_threads_for(c->host_req, cg::host_threads_env(), c->quota, g_live_ctx.load());
-  if (nt > 1 && (!c->hpool || c->hpool->threads() != nt)) c->hpool.reset(new cg::HostPool(nt - 1));
+  if (nt <= 1) c->hpool.reset();  // a budget of one runs inline (host_par), not on an older, larger pool
+  else if (!c->hpool || c->hpool->threads() != nt) c->hpool.reset(new cg::HostPool(nt - 1));
   return nt;
 }
 
@@ -233,16 +276,16 @@ uint64_t chunk_of(const cg_ctx* c, uint64_t n) {
 // of time avoids that).
 // A call of more than one chunk gets two item workspaces (launch_chunked runs chunk k + 1's front
 // before chunk k's back).
-size_t item_half_bytes(uint64_t ws_items) { return (cg::item_ws_bytes(ws_items) + 255) & ~(size_t)255; }
+size_t item_half_bytes(const cg_ctx* c, uint64_t ws_items) { return (c->eng->item_ws_bytes(ws_items) + 255) & ~(size_t)255; }
 hipError_t ensure_ws(cg_ctx* c, uint32_t n_keys, uint64_t ws_items, uint64_t call_items = 0) {
   // the wide pool is sized for the full slot cap (KEY_WIDE_MAX) whenever the device can hold it: a
   // cap lowered by an earlier call that met low free memory (another process on the device) is
   // raised again here once the memory is back, instead of staying low for the
   // context's life
   const uint32_t kmax = cg::kKeyWideMax;
-  size_t wide = cg::wide_bytes(n_keys, call_items, kmax);
-  const size_t items = item_half_bytes(ws_items) * (call_items > ws_items ? 2 : 1);
-  if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= items && c->wide.cap >= wide) {
+  size_t wide = c->eng->wide_bytes(n_keys, call_items, kmax);
+  const size_t items = item_half_bytes(c, ws_items) * (call_items > ws_items ? 2 : 1);
+  if (c->keyprep.cap >= c->eng->keyprep_bytes(n_keys) && c->itemws.cap >= items && c->wide.cap >= wide) {
     c->wide_max = kmax;
     return hipSuccess;
   }
@@ -250,22 +293,22 @@ hipError_t ensure_ws(cg_ctx* c, uint32_t n_keys, uint64_t ws_items, uint64_t cal
   if (wide > c->wide.cap) {  // cap the wide pool by the device's free memory (keeping 1 GiB spare)
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-      const size_t need_other = (c->keyprep.cap >= cg::keyprep_bytes(n_keys) ? 0 : cg::keyprep_bytes(n_keys)) +
+      const size_t need_other = (c->keyprep.cap >= c->eng->keyprep_bytes(n_keys) ? 0 : c->eng->keyprep_bytes(n_keys)) +
                                 (c->itemws.cap >= items ? 0 : items);
       const size_t avail = free_b + c->wide.cap;  // the current pool is freed before the new one
       const size_t spare = (size_t)1 << 30;
       if (wide + need_other + spare > avail) {
         const size_t room = avail > need_other + spare ? avail - need_other - spare : 0;
-        cap = (uint32_t)std::min<size_t>(room / cg::wide_slot_bytes(), kmax);
-        wide = cg::wide_bytes(n_keys, call_items, cap);
+        cap = (uint32_t)std::min<size_t>(room / c->eng->wide_slot_bytes(), kmax);
+        wide = c->eng->wide_bytes(n_keys, call_items, cap);
       }
     }
   }
   c->wide_max = cap;
-  if (c->keyprep.cap >= cg::keyprep_bytes(n_keys) && c->itemws.cap >= items && c->wide.cap >= wide)
+  if (c->keyprep.cap >= c->eng->keyprep_bytes(n_keys) && c->itemws.cap >= items && c->wide.cap >= wide)
     return hipSuccess;  // still short of memory: the pool the context has is the largest that fits
   hipError_t e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = c->keyprep.ensure(cg::keyprep_bytes(n_keys));
+  if (e == hipSuccess) e = c->keyprep.ensure(c->eng->keyprep_bytes(n_keys));
   if (e == hipSuccess) e = c->itemws.ensure(items);
   if (e == hipSuccess) e = c->wide.ensure_exact(wide);
   return e;
@@ -277,8 +320,8 @@ cg::WidePool wide_for(cg_ctx* c, uint32_t n_keys, uint64_t n_items) {
     const char* v = getenv("CG_NO_WIDE_TABLES");
     return v && v[0] == '1';
   }();
-  if (off || c->wide.cap < cg::wide_bytes(n_keys, n_items, c->wide_max)) return cg::WidePool{};
-  cg::WidePool p = cg::make_wide_pool(c->wide.p, n_keys, n_items, c->wide_max);
+  if (off || c->wide.cap < c->eng->wide_bytes(n_keys, n_items, c->wide_max)) return cg::WidePool{};
+  cg::WidePool p = c->eng->make_wide_pool(c->wide.p, n_keys, n_items, c->wide_max);
   static const uint32_t min_ed = [] {  // CG_WIDE_MIN_USES_ED / _EC: override the thresholds (A/B runs)
     const char* v = getenv("CG_WIDE_MIN_USES_ED");
     return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
@@ -305,7 +348,7 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   // any chunk is prepared (so they overlap the host copies).
   if (n_items == 0) return hipSuccess;
   const cg::WidePool wp = wide_for(c, n_keys, n_items);
-  hipError_t e = cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork,
+  hipError_t e = c->eng->launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork,
                                     uses ? nullptr : d_items, n_items, &wp, uses);
   // chunk k = items [at(k), at(k) + cnt(k)): the caller's bounds (bounds[0] = 0, bounds[nch] = n),
   // else equal chunks of chunk_of(c, n) items; `per` (the largest chunk) sizes the item workspaces
@@ -321,10 +364,10 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
     return bounds ? (*bounds)[k + 1] - (*bounds)[k] : (per < n_items - k * per ? per : n_items - k * per);
   };
   // chunk k's item workspace: half k % 2 when the buffer holds two (ensure_ws), else the one
-  const bool two = nch > 1 && c->itemws.cap >= 2 * item_half_bytes(per);
-  auto ws = [&](uint64_t k) { return (void*)((uint8_t*)c->itemws.p + (two ? (k & 1) * item_half_bytes(per) : 0)); };
+  const bool two = nch > 1 && c->itemws.cap >= 2 * item_half_bytes(c, per);
+  auto ws = [&](uint64_t k) { return (void*)((uint8_t*)c->itemws.p + (two ? (k & 1) * item_half_bytes(c, per) : 0)); };
   auto plan = [&](uint64_t k) {
-    return cg::launch_items_plan(d_keys, n_keys, d_items + at(k), cnt(k), d_status + at(k), c->keyprep.p, ws(k), s,
+    return c->eng->launch_items_plan(d_keys, n_keys, d_items + at(k), cnt(k), d_status + at(k), c->keyprep.p, ws(k), s,
                                  &c->fork, &wp);
   };
   const bool pre_plan = two && !prepare;
@@ -333,7 +376,7 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
       const hipError_t w = (*prepare)(k, at(k), cnt(k));
       if (w != hipSuccess) return w;
     }
-    return cg::launch_items_front(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, mode, d_status + at(k),
+    return c->eng->launch_items_front(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, mode, d_status + at(k),
                                   c->keyprep.p, ws(k), s, d_msgs, msgs_len, &c->fork, &wp, pre_plan && k < 2);
   };
   // chunk k + 1's front (plan, hashes, ECDSA prep) before chunk k's back (ladders): the first
@@ -342,7 +385,7 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   // with one, the builds start first: they overlap the preparation of the first chunk.
   if (e == hipSuccess && pre_plan) e = plan(0);
   if (e == hipSuccess && pre_plan) e = plan(1);
-  if (e == hipSuccess && prepare) e = cg::launch_key_tables(&c->fork, s);
+  if (e == hipSuccess && prepare) e = c->eng->launch_key_tables(&c->fork, s);
   // CG_FRONT_AFTER_TABLES=1 (A/B): the first chunk's front waits for every key table, instead of
   // sharing the chip with the builds (both run at about half speed together:
   // profiles/r03/env_chains timelines)
@@ -360,7 +403,7 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
       hipEventRecord(c->backt[1], t);
     }
     c->fork.mark = c->htrace && 3 * k + 2 < c->fbt.size() ? c->fbt[3 * k + 2] : nullptr;  // before the joins
-    const hipError_t r = cg::launch_items_back(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len,
+    const hipError_t r = c->eng->launch_items_back(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len,
                                                d_status + at(k), c->keyprep.p, ws(k), c->btab, s, &c->fork, &wp);
     c->fork.mark = nullptr;
     if (c->htrace && 3 * k + 1 < c->fbt.size()) hipEventRecord(c->fbt[3 * k + 1], s);  // back k ends
@@ -503,7 +546,7 @@ int verify_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_
   const cg_item* di = (const cg_item*)c->items.p;
   uint8_t* ds = (uint8_t*)c->status.p;
   const cg::WidePool wp = wide_for(c, n_keys, n_items);
-  HIP_TRY(cg::launch_keyprep(dk, n_keys, dbase, arena_len, c->keyprep.p, s, &c->fork, di, n_items, &wp),
+  HIP_TRY(c->eng->launch_keyprep(dk, n_keys, dbase, arena_len, c->keyprep.p, s, &c->fork, di, n_items, &wp, nullptr),
           "launch_keyprep");
   for (uint64_t k = 0; k < nch; ++k) {
     HIP_TRY(copy_missing(have, P.ext[k], arena, dwin, P.win.lo, c->copy), "H2D arena");
@@ -511,7 +554,7 @@ int verify_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const cg_
     HIP_TRY(hipStreamWaitEvent(s, c->seg[k], 0), "hipStreamWaitEvent");
     if (k == 0) HIP_TRY(hipEventRecord(c->tev[1], s), "hipEventRecord");
     const uint64_t f = P.first[k], cnt = P.first[k + 1] - f;
-    HIP_TRY(cg::launch_items(dk, n_keys, di + f, cnt, dbase, arena_len, mode, ds + f, c->keyprep.p, c->itemws.p,
+    HIP_TRY(c->eng->launch_items(dk, n_keys, di + f, cnt, dbase, arena_len, mode, ds + f, c->keyprep.p, c->itemws.p,
                              c->btab, s, nullptr, 0, &c->fork, &wp), "launch_items");
   }
   HIP_TRY(hipEventRecord(c->tev[2], s), "hipEventRecord");
@@ -602,8 +645,16 @@ static_assert(sizeof(cg_item) == 32 && sizeof(cg_key) == 16 && sizeof(cg_txsig) 
 int cg_open(cg_ctx** out, const cg_config* cfg) {
   if (!out) return fail(CG_ERR_ARG, "cg_open: out is NULL");
   *out = nullptr;
-  if (cfg && (cfg->reserved0 || cfg->reserved[0] || cfg->reserved[1]))
+  if (cfg && (cfg->reserved0 || cfg->reserved1))
     return fail(CG_ERR_ARG, "cg_open: cg_config.reserved must be 0 (ABI v2: 56-byte cg_config)");
+  const uint64_t tab_budget = cfg && cfg->table_bytes_max ? cfg->table_bytes_max
+                                                          : cgb::table_bytes_env(getenv("CG_TABLE_BYTES_MAX"));
+  if (tab_budget && tab_budget < table_sets().back().bytes) {
+    char m[160];
+    snprintf(m, sizeof m, "cg_open: table_bytes_max %llu is below the smallest fixed-base tables (%llu bytes, radix 2^%u)",
+             (unsigned long long)tab_budget, (unsigned long long)table_sets().back().bytes, table_sets().back().bits);
+    return fail(CG_ERR_ARG, "%s", m);
+  }
   if (cfg && (cfg->flags & ~CG_FLAG_STAGE_TIMING)) return fail(CG_ERR_ARG, "cg_open: unknown cg_config.flags bits");
   int dev = cfg ? cfg->device : 0;
   int n = 0;
@@ -692,11 +743,16 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   }
   for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&c->tev[k]);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
-  if (e == hipSuccess) e = cg::upload_constants();
-  if (e == hipSuccess) e = acquire_tables(c->device, c->stream, &c->btab);
+  int var = 0;
+  if (e == hipSuccess) e = acquire_tables(c->device, c->stream, tab_budget, &c->btab, &var);
+  if (e == hipSuccess) {
+    c->eng = kVariants[var];
+    c->tab_bytes = c->eng->btab_bytes();
+    e = c->eng->upload_constants();  // per device: a table set built for another device uploaded there
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
-    const int rc = hip_fail(e, "side streams / upload_constants / base-point tables");
+    const int rc = hip_fail(e, "side streams / upload_constants / fixed-base tables");
     cg_close(c);
     return rc;
   }
@@ -768,6 +824,29 @@ void cg_close(cg_ctx* c) {
   delete c;
 }
 
+uint64_t cg_table_bytes(uint32_t fixed_base_bits) {
+  for (const cgb::TableSet& t : table_sets())
+    if (t.bits == fixed_base_bits) return t.bytes;
+  return 0;
+}
+
+uint32_t cg_table_choice(uint64_t table_bytes_max, uint64_t device_free) {
+  const std::vector<cgb::TableSet> sets = table_sets();
+  const int k = cgb::pick_tables(sets.data(), (int)sets.size(), table_bytes_max, device_free, -1);
+  return k < 0 ? 0u : sets[k].bits;
+}
+
+int cg_context_info(const cg_ctx* c, cg_info* out) {
+  if (!c || !out) return fail(CG_ERR_ARG, "cg_context_info: NULL argument");
+  memset(out, 0, sizeof *out);
+  out->device = c->device;
+  out->fixed_base_bits = c->eng ? c->eng->fixed_base_bits : 0u;
+  out->table_bytes = c->tab_bytes;
+  out->host_threads = cg::host_threads_for(c->host_req, cg::host_threads_env(), c->quota, g_live_ctx.load());
+  out->chunk_items = c->chunk;
+  return CG_OK;
+}
+
 int cg_stage_times(cg_ctx* c, double* ms_out, uint32_t* launches_out, uint32_t n) {
   if (!c || (n && (!ms_out || !launches_out))) return fail(CG_ERR_ARG, "cg_stage_times: NULL argument");
   std::lock_guard<std::mutex> g(c->mu);
@@ -822,13 +901,15 @@ int cg_prepare_keys_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   if (n_keys && !d_keys) return fail(CG_ERR_ARG, "cg_prepare_keys_device: keys is NULL");
   std::lock_guard<std::mutex> g(c->mu);
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
-  if (c->keyprep.cap < cg::keyprep_bytes(n_keys)) {
+  if (c->keyprep.cap < c->eng->keyprep_bytes(n_keys)) {
     HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
-    HIP_TRY(c->keyprep.ensure(cg::keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
+    HIP_TRY(c->keyprep.ensure(c->eng->keyprep_bytes(n_keys)), "hipMalloc(keyprep)");
   }
   hipStream_t s = stream_of(c, hip_stream);
   HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
-  HIP_TRY(cg::launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork), "launch_keyprep");
+  HIP_TRY(c->eng->launch_keyprep(d_keys, n_keys, d_arena, arena_len, c->keyprep.p, s, &c->fork, nullptr, 0, nullptr,
+                                 nullptr),
+          "launch_keyprep");
   HIP_TRY(order_out(c, s), "hipEventRecord");
   return CG_OK;
 }
@@ -840,7 +921,7 @@ int cg_verify_items_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   if (n_items && (!d_items || !d_status)) return fail(CG_ERR_ARG, "cg_verify_items_device: NULL buffer");
   if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_verify_items_device: bad mode");
   std::lock_guard<std::mutex> g(c->mu);
-  if (c->keyprep.cap < cg::keyprep_bytes(n_keys))
+  if (c->keyprep.cap < c->eng->keyprep_bytes(n_keys))
     return fail(CG_ERR_ARG, "cg_verify_items_device: keys were not prepared (call cg_prepare_keys_device)");
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
   HIP_TRY(ensure_ws(c, n_keys, chunk_of(c, n_items)), "hipMalloc(item workspace)");
@@ -849,8 +930,8 @@ int cg_verify_items_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, con
   const uint64_t per = chunk_of(c, n_items);
   for (uint64_t f = 0; f < n_items; f += per) {
     const uint64_t cnt = per < n_items - f ? per : n_items - f;
-    HIP_TRY(cg::launch_items(d_keys, n_keys, d_items + f, cnt, d_arena, arena_len, mode, d_status + f, c->keyprep.p,
-                             c->itemws.p, c->btab, s, nullptr, 0, &c->fork),
+    HIP_TRY(c->eng->launch_items(d_keys, n_keys, d_items + f, cnt, d_arena, arena_len, mode, d_status + f, c->keyprep.p,
+                             c->itemws.p, c->btab, s, nullptr, 0, &c->fork, nullptr),
             "launch_items");
   }
   HIP_TRY(order_out(c, s), "hipEventRecord");
@@ -1063,6 +1144,12 @@ int cg_verify_transactions_device(cg_ctx* c, const cg_tx* d_txs, uint64_t n_tx, 
                                     d_arena, arena_len, mode, d_ids, d_tx_status, d_sig_status, s);
 }
 
+static int verify_transactions_host_locked(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_component* comps,
+                                           uint64_t n_comps, const cg_key* keys, uint32_t n_keys, const cg_txsig* sigs,
+                                           uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,
+                                           const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* ids_out,
+                                           uint8_t* tx_status_out, uint8_t* sig_status_out);
+
 int cg_verify_transactions(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_component* comps, uint64_t n_comps,
                            const cg_key* keys, uint32_t n_keys, const cg_txsig* sigs, uint64_t n_sigs,
                            const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
@@ -1079,6 +1166,17 @@ int cg_verify_transactions(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_
   for (uint64_t i = 0; i < n_sigs; ++i) sig_status_out[i] = CG_NOT_RUN;
   if (n_tx == 0 && n_sigs == 0) return CG_OK;
   std::lock_guard<std::mutex> g(c->mu);
+  return verify_transactions_host_locked(c, txs, n_tx, comps, n_comps, keys, n_keys, sigs, n_sigs, tmpls, n_tmpls,
+                                         arena, arena_len, mode, ids_out, tx_status_out, sig_status_out);
+}
+
+// cg_verify_transactions with the arguments checked and the ctx lock held (also a cg_pool slot's call)
+static int verify_transactions_host_locked(cg_ctx* c, const cg_tx* txs, uint64_t n_tx, const cg_component* comps,
+                                           uint64_t n_comps, const cg_key* keys, uint32_t n_keys, const cg_txsig* sigs,
+                                           uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,
+                                           const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* ids_out,
+                                           uint8_t* tx_status_out, uint8_t* sig_status_out) {
+  if (c->fault) return fail(CG_ERR_DEVICE, "cg_verify_transactions: device fault (injected by cg_pool_inject_fault)");
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
   hipStream_t s = c->stream;
   HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
@@ -1316,7 +1414,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     // In a hot call (1 in 32: keys average 256+ uses) every sampled key is counted up to the wide
     // threshold: a few keys left in full-table mode cost a serial full-table launch per chunk (0.18
     // ms, ~1.4% of the headline, profiles/r03/ab_der), a wide table costs about 230 items' work.
-    const cg::WidePool thr = cg::make_wide_pool(nullptr, n_keys, n_sigs);  // the wide thresholds
+    const cg::WidePool thr = c->eng->make_wide_pool(nullptr, n_keys, n_sigs, cg::kKeyWideMax);  // the wide thresholds
     const uint64_t floor_hot = S >= CG_TXSIG_COUNT_SAMPLE ? (uint64_t)std::max(thr.min_ed, thr.min_ec) : 0u;
     // The raised estimate only where it decides a wide table: below the wide threshold the plain
     // S c decides row 0 against full tables (a wrong full table costs ~230 ns, a wrong row 0 ~7 ns
@@ -1853,6 +1951,37 @@ int cg_pool_verify_tx_signatures(cg_pool* p, const cg_key* keys, uint32_t n_keys
                      return verify_txsig_host_locked(c, keys, n_keys, ids, n_ids, sigs + first, count, tmpls, n_tmpls,
                                                      arena, arena_len, mode, status_out + first, nullptr);
                    });
+}
+
+// The whole call on one live slot (a signature may reference any transaction's id, so the call is not
+// sharded): pool_run over a single unit, i.e. the first live slot, and on a device fault the next one.
+int cg_pool_verify_transactions(cg_pool* p, const cg_tx* txs, uint64_t n_tx, const cg_component* comps,
+                                uint64_t n_comps, const cg_key* keys, uint32_t n_keys, const cg_txsig* sigs,
+                                uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
+                                uint64_t arena_len, uint32_t mode, uint8_t* ids_out, uint8_t* tx_status_out,
+                                uint8_t* sig_status_out, cg_pool_stats* stats) {
+  if (!p) return fail(CG_ERR_ARG, "cg_pool_verify_transactions: pool is NULL");
+  if (p->ctx.empty()) return fail(CG_ERR_ARG, "cg_pool_verify_transactions: empty pool");
+  if (n_tx && (!txs || !ids_out || !tx_status_out)) return fail(CG_ERR_ARG, "cg_pool_verify_transactions: NULL tx buffer");
+  if (n_sigs && (!sigs || !sig_status_out)) return fail(CG_ERR_ARG, "cg_pool_verify_transactions: NULL sig buffer");
+  if (n_comps && !comps) return fail(CG_ERR_ARG, "cg_pool_verify_transactions: comps is NULL");
+  if (n_keys && !keys) return fail(CG_ERR_ARG, "cg_pool_verify_transactions: keys is NULL");
+  if (n_tmpls && !tmpls) return fail(CG_ERR_ARG, "cg_pool_verify_transactions: templates is NULL");
+  if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_pool_verify_transactions: arena is NULL");
+  if (mode > CG_MODE_ISVALID) return fail(CG_ERR_ARG, "cg_pool_verify_transactions: bad mode");
+  for (uint64_t i = 0; i < n_sigs; ++i) sig_status_out[i] = CG_NOT_RUN;
+  if (n_tx == 0 && n_sigs == 0) return CG_OK;
+  uint8_t unit = CG_NOT_RUN;
+  const int rc = pool_call(p, 1, &unit, stats, "cg_pool_verify_transactions", [&](cg_ctx* c, uint64_t, uint64_t) {
+    const int r = verify_transactions_host_locked(c, txs, n_tx, comps, n_comps, keys, n_keys, sigs, n_sigs, tmpls,
+                                                  n_tmpls, arena, arena_len, mode, ids_out, tx_status_out,
+                                                  sig_status_out);
+    if (r != CG_OK)
+      for (uint64_t i = 0; i < n_sigs; ++i) sig_status_out[i] = CG_NOT_RUN;
+    return r;
+  });
+  if (stats) stats->not_run = rc == CG_OK ? 0 : n_sigs;
+  return rc;
 }
 
 int cg_pool_verify_batch(cg_pool* p, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,

@@ -9,7 +9,12 @@
 
 #include "../../include/cordagpu.h"
 
-namespace cg {
+// Types shared by every build of the kernels. The radix-dependent translation units (verify.hip,
+// verify_ed.hip, verify_ec.hip, plan_sort.hip) are compiled once per fixed-base table radix, the extra
+// builds with `cg` renamed (Makefile VARIANTS: -Dcg=cg24 / -Dcg=cg22), so these types live in a
+// namespace the rename does not touch and the C ABI layer hands the same objects to any build.
+namespace cgt {
+
 
 struct DeviceConsts;  // opaque
 // The wide-table pools of a call (keyws.h EdWideSlot / EcWideSlot arrays; host-allocated), one per
@@ -118,6 +123,68 @@ inline uint32_t chain_spread_lds() {
   return b;
 }
 
+
+// Where the per-key use counts come from when there is no verify-item table yet: a cg_txsig table
+// in HBM (sampled on the device) or exact counts (n_keys u32 in HBM, made by the host).
+struct KeyUses {
+  const cg_txsig* sigs = nullptr;
+  const uint32_t* counts = nullptr;
+  uint64_t n = 0;  // signatures the counts cover (sizes the wide pools)
+  // optional host copies of the key table and of `counts` (the host-buffer tx-signature path): the
+  // host then knows, as k_key_classify will, which families need row-0 / full tables
+  const cg_key* host_keys = nullptr;
+  const uint32_t* host_counts = nullptr;
+};
+
+// One build of the radix-dependent kernels: the entry points cordagpu.cpp calls through a context's
+// variant (cg_config.table_bytes_max picks it at cg_open). Each build defines cg::variant() (renamed
+// cg24::variant() / cg22::variant() in the others).
+struct EngineVariant {
+  uint32_t fixed_base_bits;  // radix 2^bits of the constant B / G tables
+  hipError_t (*upload_constants)();
+  size_t (*keyprep_bytes)(uint32_t n_keys);
+  size_t (*wide_bytes)(uint32_t n_keys, uint64_t n_items, uint32_t max_slots);
+  size_t (*wide_slot_bytes)();
+  WidePool (*make_wide_pool)(void* base, uint32_t n_keys, uint64_t n_items, uint32_t max_slots);
+  size_t (*btab_bytes)();
+  size_t (*btab_scratch_bytes)();
+  hipError_t (*init_btab)(void* d_btab, void* d_scratch, hipStream_t stream);
+  size_t (*item_ws_bytes)(uint64_t n_items);
+  hipError_t (*launch_keyprep)(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
+                               void* d_keyprep, hipStream_t stream, const Fork* fork, const cg_item* d_items,
+                               uint64_t n_items, const WidePool* wide, const KeyUses* src);
+  hipError_t (*launch_key_tables)(const Fork* fork, hipStream_t stream);
+  hipError_t (*launch_items)(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                             const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
+                             const void* d_keyprep, void* d_item_ws, const void* d_btab, hipStream_t stream,
+                             const uint8_t* d_msgs, uint64_t msgs_len, const Fork* fork, const WidePool* wide);
+  hipError_t (*launch_items_plan)(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                                  uint8_t* d_status, const void* d_keyprep, void* d_item_ws, hipStream_t stream,
+                                  const Fork* fork, const WidePool* wide);
+  hipError_t (*launch_items_front)(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                                   const uint8_t* d_arena, uint64_t arena_len, uint32_t mode, uint8_t* d_status,
+                                   const void* d_keyprep, void* d_item_ws, hipStream_t stream, const uint8_t* d_msgs,
+                                   uint64_t msgs_len, const Fork* fork, const WidePool* wide, bool planned);
+  hipError_t (*launch_items_back)(const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items, uint64_t n_items,
+                                  const uint8_t* d_arena, uint64_t arena_len, uint8_t* d_status, const void* d_keyprep,
+                                  void* d_item_ws, const void* d_btab, hipStream_t stream, const Fork* fork,
+                                  const WidePool* wide);
+};
+
+}  // namespace cgt
+
+namespace cg {
+
+using cgt::EngineVariant;
+using cgt::Fork;
+using cgt::PendingTabs;
+using cgt::StageTimer;
+using cgt::WidePool;
+using cgt::chain_spread_lds;
+
+// this build's entry points (verify.hip)
+const EngineVariant& variant();
+
 // Upload the constant tables (curve constants, base-point tables) for the current device.
 hipError_t upload_constants();
 
@@ -143,17 +210,7 @@ size_t btab_scratch_bytes();  // temporary scratch of init_btab (free once it ha
 hipError_t init_btab(void* d_btab, void* d_scratch, hipStream_t stream);
 // Bytes of per-item workspace (projective Ed25519 results awaiting the batched inversion).
 size_t item_ws_bytes(uint64_t n_items);
-// Where the per-key use counts come from when there is no verify-item table yet: a cg_txsig table
-// in HBM (sampled on the device) or exact counts (n_keys u32 in HBM, made by the host).
-struct KeyUses {
-  const cg_txsig* sigs = nullptr;
-  const uint32_t* counts = nullptr;
-  uint64_t n = 0;  // signatures the counts cover (sizes the wide pools)
-  // optional host copies of the key table and of `counts` (the host-buffer tx-signature path): the
-  // host then knows, as k_key_classify will, which families need row-0 / full tables
-  const cg_key* host_keys = nullptr;
-  const uint32_t* host_counts = nullptr;
-};
+using cgt::KeyUses;
 // With `d_items` (or `src`), each key's table is sized by the number of items that use it
 // (keyws.h); with neither (cg_prepare_keys_device), every key gets full tables.
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,

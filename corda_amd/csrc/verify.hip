@@ -279,6 +279,10 @@ static void families_needing_full(const KeyUses& src, uint32_t n_keys, const Key
 hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_arena, uint64_t arena_len,
                           void* d_keyprep, hipStream_t stream, const Fork* fork, const cg_item* d_items,
                           uint64_t n_items, const WidePool* wide, const KeyUses* src) {
+  if (fork) {  // a call with no keys must not inherit the previous call's skip (k_mode_guard reads it)
+    fork->pending.skip_mask = 0;
+    for (int f = 0; f < 3; ++f) fork->pending.need_full[f] = true;
+  }
   if (n_keys == 0) return hipSuccess;
   const bool counted = d_items || src;  // tables sized by the call's key uses
   if (!d_items && src) n_items = src->n;
@@ -318,7 +322,8 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
       return v ? (uint32_t)strtoul(v, nullptr, 0) & 7u : 0u;
     }();
     for (int f = 0; f < 3; ++f) {
-      if ((test_skip >> f) & 1u) fork->pending.need_full[f] = false;
+      // serial key prep builds every table, so a test skip there would only mark good items NOT_RUN
+      if (!serial && ((test_skip >> f) & 1u)) fork->pending.need_full[f] = false;
       if (!fork->pending.need_full[f]) skip_mask |= 1u << f;
     }
     fork->pending.skip_mask = skip_mask;
@@ -567,6 +572,16 @@ hipError_t launch_verify(const cg_key* d_keys, uint32_t n_keys, const cg_item* d
   if (e != hipSuccess) return e;
   return launch_items(d_keys, n_keys, d_items, n_items, d_arena, arena_len, mode, d_status, d_keyprep, d_item_ws,
                       d_btab, stream, d_msgs, msgs_len, fork, wide);
+}
+
+// This build's entry points for the C ABI layer (engine.h EngineVariant; one per fixed-base radix).
+static_assert(ED_WIDE_BW == EC_WIDE_GW, "one fixed-base radix per build (Makefile VARIANTS)");
+const EngineVariant& variant() {
+  static const EngineVariant v = {(uint32_t)ED_WIDE_BW, upload_constants, keyprep_bytes, wide_bytes, wide_slot_bytes,
+                                  make_wide_pool, btab_bytes, btab_scratch_bytes, init_btab, item_ws_bytes,
+                                  launch_keyprep, launch_key_tables, launch_items, launch_items_plan,
+                                  launch_items_front, launch_items_back};
+  return v;
 }
 
 }  // namespace cg

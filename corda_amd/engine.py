@@ -18,16 +18,24 @@ def _p(a):
 
 
 class Engine:
-    def __init__(self, device=0, chunk_items=0, stage_timing=False, host_threads=0):
+    def __init__(self, device=0, chunk_items=0, stage_timing=False, host_threads=0, table_bytes_max=0):
         """host_threads: cg_config.host_threads (0: CG_HOST_THREADS, else the CPU quota divided by the
-        contexts open in this process; include/cordagpu.h)."""
+        contexts open in this process); table_bytes_max: HBM the constant fixed-base tables may take
+        (0: automatic; include/cordagpu.h, corda_amd/csrc/table_budget.h)."""
         L = _lib.lib()
-        cfg = _lib.cg_config(device, _lib.FLAG_STAGE_TIMING if stage_timing else 0, 0, 0, chunk_items, host_threads)
+        cfg = _lib.cg_config(device, _lib.FLAG_STAGE_TIMING if stage_timing else 0, 0, 0, chunk_items, host_threads,
+                             0, table_bytes_max)
         h = ctypes.c_void_p()
         _lib.check(L.cg_open(ctypes.byref(h), ctypes.byref(cfg)), f"cg_open(device={device})")
         self._h = h
         self.device = device
         self.last_stats = None
+
+    def info(self):
+        """cg_context_info: device, fixed_base_bits (26 / 24 / 22), table_bytes, host_threads, chunk_items."""
+        inf = _lib.cg_info()
+        _lib.check(_lib.lib().cg_context_info(self._h, ctypes.byref(inf)), "cg_context_info")
+        return {k: getattr(inf, k) for k, _ in _lib.cg_info._fields_ if k != "reserved"}
 
     def close(self):
         if self._h:
@@ -213,9 +221,9 @@ class EnginePool:
     slots, re-runs a failed slot's shard elsewhere, and returns one status byte per item (items
     no slot could run stay NOT_RUN and raise ``EngineUnavailable`` unless ``allow_partial``)."""
 
-    def __init__(self, devices, chunk_items=0, host_threads=0):
+    def __init__(self, devices, chunk_items=0, host_threads=0, table_bytes_max=0):
         L = _lib.lib()
-        cfg = _lib.cg_config(0, 0, 0, 0, chunk_items, host_threads)
+        cfg = _lib.cg_config(0, 0, 0, 0, chunk_items, host_threads, 0, table_bytes_max)
         devs = (ctypes.c_int32 * len(devices))(*devices)
         h = ctypes.c_void_p()
         _lib.check(L.cg_pool_open(ctypes.byref(h), devs, len(devices), ctypes.byref(cfg)), "cg_pool_open")
@@ -267,4 +275,36 @@ class EnginePool:
         self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_pool_stats._fields_ if k != "reserved"}
         if rc != 0 and not allow_partial:
             _lib.check(rc, "cg_pool_verify_tx_signatures")
+        return st
+
+    def verify_transactions(self, txs, comps, keys, sigs, tmpls, arena, mode=MODE_DOVERIFY, allow_partial=False):
+        """cg_pool_verify_transactions: the whole call on one healthy slot, the next one on a device
+        fault. Returns (ids [n_tx, 32], tx_status, sig_status) as Engine.verify_transactions."""
+        ids = np.zeros(32 * len(txs), dtype=np.uint8)
+        txst = np.zeros(len(txs), dtype=np.uint8)
+        sst = np.full(len(sigs), 255, dtype=np.uint8)
+        stats = _lib.cg_pool_stats()
+        rc = _lib.lib().cg_pool_verify_transactions(self._h, _p(txs), len(txs), _p(comps), len(comps), _p(keys),
+                                                    len(keys), _p(sigs), len(sigs), _p(tmpls), len(tmpls), _p(arena),
+                                                    arena.size, mode, _p(ids), _p(txst), _p(sst), ctypes.byref(stats))
+        self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_pool_stats._fields_ if k != "reserved"}
+        if rc != 0 and not allow_partial:
+            _lib.check(rc, "cg_pool_verify_transactions")
+        return ids.reshape(-1, 32), txst, sst
+
+    def verify_requeue(self, batch, mode=MODE_DOVERIFY, between=None):
+        """The JVM binding's re-queue (CryptoBatch.kt verifyBatch): on CG_ERR_DEVICE only the items left
+        NOT_RUN go to the pool once more, as a sub-batch over the same keys and arena; what still stays
+        NOT_RUN is returned as NOT_RUN (the binding hands those to Crypto.doVerify one by one).
+        ``between()`` runs before the re-queue (tests clear a drill fault there)."""
+        st = self.verify(batch, mode, allow_partial=True)
+        rc_first = self.last_stats
+        todo = np.flatnonzero(st == 255)
+        if todo.size:
+            if between:
+                between()
+            sub = batch.subset(todo)
+            st2 = self.verify(sub, mode, allow_partial=True)
+            st[todo] = st2
+        self.first_stats = rc_first
         return st

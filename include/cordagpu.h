@@ -168,8 +168,20 @@ typedef struct cg_config {
                             quota (cgroup cpu.max, affinity) divided by the contexts open in the
                             process; at most 64. One process per GPU: pass quota / GPUs per node. */
   uint32_t reserved0;    /* must be 0 */
-  uint64_t reserved[2];  /* must be 0: cg_open rejects anything else with CG_ERR_ARG */
+  uint64_t table_bytes_max; /* HBM the constant fixed-base tables (Ed25519 B, secp256r1 / secp256k1 G) may
+                            take. They are built once per device per process at radix 2^26 (~91 GB), 2^24
+                            (~25 GB) or 2^22 (~6.9 GB): fewer additions per item the larger (42 / 43 / 44),
+                            same verdicts. > 0: the largest set within this many bytes (below the smallest:
+                            CG_ERR_ARG). 0: CG_TABLE_BYTES_MAX from the environment if set (bytes, K/M/G
+                            suffix), else automatic: a set this process already holds on the device, else
+                            the largest that leaves CG_TABLE_HEADROOM of the device's free memory, else the
+                            smallest; if its allocation fails (another process took the memory first), the
+                            next smaller. cg_context_info reports the choice. */
+  uint64_t reserved1;    /* must be 0: cg_open rejects anything else with CG_ERR_ARG */
 } cg_config;             /* 56 bytes (static_assert in cordagpu.cpp) */
+
+/* Device memory the automatic table choice leaves free for the calls' workspaces (16 GiB). */
+#define CG_TABLE_HEADROOM (16ull << 30)
 
 typedef struct cg_stats {
   uint64_t n_items;
@@ -183,6 +195,16 @@ typedef struct cg_stats {
 
 typedef struct cg_ctx cg_ctx;
 
+/* What a context was opened with (cg_context_info). */
+typedef struct cg_info {
+  int32_t device;
+  uint32_t fixed_base_bits; /* radix 2^bits of the constant fixed-base tables this context reads: 26, 24 or 22 */
+  uint64_t table_bytes;     /* their HBM (shared by every context of the process on the device) */
+  uint32_t host_threads;    /* the host budget of this context's scans now (host_budget.h) */
+  uint32_t reserved;
+  uint64_t chunk_items;     /* items per verify chunk */
+} cg_info;                  /* 32 bytes */
+
 /* Library / device info. */
 int cg_abi_version(void);
 const char* cg_build_info(void);
@@ -191,6 +213,13 @@ const char* cg_last_error(void); /* thread-local message for the last non-OK ret
 
 int cg_open(cg_ctx** out, const cg_config* cfg);
 void cg_close(cg_ctx* ctx);
+int cg_context_info(const cg_ctx* ctx, cg_info* out);
+/* The constant tables' budget arithmetic, HIP-free (no device needed): the HBM of the set at radix
+ * 2^fixed_base_bits (0: no such build), and the radix cg_open would pick for a table_bytes_max on a
+ * device with device_free bytes free and no set built yet in the process (0: the budget is below
+ * every set, cg_open returns CG_ERR_ARG). */
+uint64_t cg_table_bytes(uint32_t fixed_base_bits);
+uint32_t cg_table_choice(uint64_t table_bytes_max, uint64_t device_free);
 
 /* Host memory registration (zero-copy ingestion). A caller that keeps its buffers across calls (a
  * JVM direct ByteBuffer arena, the out-of-process verifier's request buffers) registers them once:
@@ -421,6 +450,15 @@ int cg_pool_verify_tx_signatures(cg_pool* pool, const cg_key* keys, uint32_t n_k
                                  uint64_t n_ids, const cg_txsig* sigs, uint64_t n_sigs,
                                  const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
                                  uint64_t arena_len, uint32_t mode, uint8_t* status_out, cg_pool_stats* stats_opt);
+/* cg_verify_transactions on a pool. A signature may reference any transaction's id, so the call is not
+ * sharded: it runs whole on the first healthy slot and, if that slot's device fails (the slot is then
+ * marked unhealthy), on the next one. When no slot could run it, every sig status stays CG_NOT_RUN and
+ * the call returns CG_ERR_DEVICE (re-queue the request). stats_opt->not_run counts the signatures. */
+int cg_pool_verify_transactions(cg_pool* pool, const cg_tx* txs, uint64_t n_tx, const cg_component* comps,
+                                uint64_t n_comps, const cg_key* keys, uint32_t n_keys, const cg_txsig* sigs,
+                                uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
+                                uint64_t arena_len, uint32_t mode, uint8_t* ids_out, uint8_t* tx_status_out,
+                                uint8_t* sig_status_out, cg_pool_stats* stats_opt);
 /* Failure drill: make every later call on `slot` fail as a device fault would (fail = 1), or
  * clear it and mark the slot healthy again (fail = 0). For tests and operational drills. */
 int cg_pool_inject_fault(cg_pool* pool, uint32_t slot, int fail);

@@ -17,6 +17,9 @@ import java.security.PublicKey
 import java.security.SignatureException
 import java.util.concurrent.TimeUnit
 import java.util.concurrent.atomic.AtomicInteger
+import java.util.concurrent.locks.ReentrantReadWriteLock
+import kotlin.concurrent.read
+import kotlin.concurrent.write
 
 data class BatchItem(val publicKey: PublicKey, val signatureData: ByteArray, val clearData: ByteArray)
 
@@ -24,20 +27,25 @@ data class BatchItem(val publicKey: PublicKey, val signatureData: ByteArray, val
  * The engine's node.conf block (INTEGRATION.md §5), beside the reference's verifierType
  * (NodeConfiguration.kt:33,98-101):
  *
- *   gpuVerifier { devices = [0, 1, 2, 3, 4, 5, 6, 7], minBatch = 4096, chunkItems = 0, hostThreads = 0 }
+ *   gpuVerifier { devices = [0, 1, 2, 3, 4, 5, 6, 7], minBatch = 4096, chunkItems = 0, hostThreads = 0,
+ *                 tableBytesMax = 0 }
  *
- * devices: HIP ordinals this process drives (one: a cg_ctx; several: a cg_pool sharding every batch).
+ * devices: HIP ordinals this process drives (one: a cg_ctx; several: a cg_pool sharding every batch:
+ *   every entry point works with either, see CryptoBatch.withHandles).
  * minBatch: batches with fewer signatures than this never leave the JVM (Crypto.doVerify per
  *   signature, the reference's own serial path): a GPU call has a fixed cost of a few ms.
  * chunkItems: cg_config.chunk_items (0: the library's default).
  * hostThreads: cg_config.host_threads, host threads of this process's scans (0: the cgroup CPU quota
  *   divided by the contexts the process opens).
+ * tableBytesMax: cg_config.table_bytes_max, HBM per device for the constant fixed-base tables (0:
+ *   automatic: ~91 GB when the device has room, ~25 / ~6.9 GB when other processes share it; a node
+ *   that runs several verifier processes per GPU sets e.g. 26000000000).
  */
 data class GpuVerifierConfig(val devices: IntArray = intArrayOf(0), val minBatch: Int = 4096,
-                             val chunkItems: Long = 0, val hostThreads: Int = 0) {
+                             val chunkItems: Long = 0, val hostThreads: Int = 0, val tableBytesMax: Long = 0) {
     init {
         require(devices.isNotEmpty() && devices.all { it >= 0 }) { "gpuVerifier.devices: at least one ordinal >= 0" }
-        require(minBatch >= 0 && chunkItems >= 0 && hostThreads >= 0) { "gpuVerifier: negative setting" }
+        require(minBatch >= 0 && chunkItems >= 0 && hostThreads >= 0 && tableBytesMax >= 0) { "gpuVerifier: negative setting" }
     }
 
     companion object {
@@ -48,7 +56,8 @@ data class GpuVerifierConfig(val devices: IntArray = intArrayOf(0), val minBatch
                 devices = opt("devices", { g.getIntList(it).toIntArray() }, intArrayOf(0)),
                 minBatch = opt("minBatch", g::getInt, 4096),
                 chunkItems = opt("chunkItems", g::getLong, 0L),
-                hostThreads = opt("hostThreads", g::getInt, 0))
+                hostThreads = opt("hostThreads", g::getInt, 0),
+                tableBytesMax = opt("tableBytesMax", g::getLong, 0L))
         }
     }
 }
@@ -56,13 +65,13 @@ data class GpuVerifierConfig(val devices: IntArray = intArrayOf(0), val minBatch
 object CryptoBatch {
     init { System.loadLibrary("cordagpu_jni") }           // links libcordagpu.so
 
-    private external fun nativeOpen(device: Int, chunkItems: Long, hostThreads: Int): Long
-    private external fun nativeOpenPool(devices: IntArray, chunkItems: Long, hostThreads: Int): Long
+    private external fun nativeOpen(device: Int, chunkItems: Long, hostThreads: Int, tableBytesMax: Long): Long
+    private external fun nativeOpenPool(devices: IntArray, chunkItems: Long, hostThreads: Int, tableBytesMax: Long): Long
     private external fun nativeClose(ctx: Long, pool: Long)
-    private external fun nativeVerify(ctx: Long, keys: ByteBuffer, nKeys: Int, items: ByteBuffer, nItems: Long,
+    private external fun nativeVerify(ctx: Long, pool: Long, keys: ByteBuffer, nKeys: Int, items: ByteBuffer, nItems: Long,
                                       arena: ByteBuffer, arenaLen: Long, mode: Int, status: ByteBuffer,
                                       stats: ByteBuffer): Int
-    private external fun nativeVerifyTransactions(ctx: Long, txs: ByteBuffer, nTx: Long, comps: ByteBuffer, nComps: Long,
+    private external fun nativeVerifyTransactions(ctx: Long, pool: Long, txs: ByteBuffer, nTx: Long, comps: ByteBuffer, nComps: Long,
                                                   keys: ByteBuffer, nKeys: Int, sigs: ByteBuffer, nSigs: Long,
                                                   tmpls: ByteBuffer, nTmpls: Int, arena: ByteBuffer, arenaLen: Long,
                                                   mode: Int, idsOut: ByteBuffer, txStatusOut: ByteBuffer,
@@ -88,6 +97,9 @@ object CryptoBatch {
     const val CG_UNSUPPORTED = 4
     const val CG_EMPTY = 5
     const val CG_NOT_RUN = 255
+    // include/cordagpu.h return codes
+    private const val CG_OK = 0
+    private const val CG_ERR_DEVICE = -2
 
     // cg_item.sig_len / cg_txsig.sig_len are 16-bit. A longer JVM signature is packed as a short
     // surrogate with the verdict the JVM gives the real bytes (corda_amd/batch.py sig_field):
@@ -101,10 +113,12 @@ object CryptoBatch {
     private const val STATS_BYTES = 56
 
     @Volatile private var config = GpuVerifierConfig()
-    // the native handles: 0 = not open (or closed); every entry point checks under `lock`
-    private val lock = Any()
-    @Volatile private var ctx: Long = 0
-    @Volatile private var pool: Long = 0
+    // the native handles (exactly one non-zero while open: ctx for one device, pool for several). Every
+    // native call holds the read lock from reading them until it returns; open and close() take the
+    // write lock, so close() waits for the calls in flight and never frees a handle under one (ADVICE r5)
+    private val rw = ReentrantReadWriteLock()
+    private var ctx: Long = 0
+    private var pool: Long = 0
 
     // Metrics named like the reference's verifier service (OutOfProcessTransactionVerifierService.kt:35-46)
     private fun metric(name: String) = "CryptoBatch.$name"
@@ -121,26 +135,45 @@ object CryptoBatch {
         metrics = registry
     }
 
-    /** The open handles (ctx for a single device, pool for several), opening them on first use. */
-    private fun handles(): Pair<Long, Long> {
-        synchronized(lock) {
-            if (ctx == 0L && pool == 0L) {
-                val c = config
-                if (c.devices.size == 1) ctx = nativeOpen(c.devices[0], c.chunkItems, c.hostThreads)
-                else pool = nativeOpenPool(c.devices, c.chunkItems, c.hostThreads)
+    /** Runs one native call with the open handles (ctx, pool), opening them on first use, under the
+     *  read lock: close() cannot free them until the call has returned. Every entry point calls the
+     *  engine through here, whichever of ctx (one device) / pool (several) is open. */
+    private inline fun <T> withHandles(call: (Long, Long) -> T): T {
+        while (true) {
+            rw.read { if (ctx != 0L || pool != 0L) return call(ctx, pool) }
+            rw.write {
+                if (ctx == 0L && pool == 0L) {
+                    val c = config
+                    if (c.devices.size == 1) ctx = nativeOpen(c.devices[0], c.chunkItems, c.hostThreads, c.tableBytesMax)
+                    else pool = nativeOpenPool(c.devices, c.chunkItems, c.hostThreads, c.tableBytesMax)
+                }
             }
-            return ctx to pool
         }
     }
 
-    /** Releases the device context / pool (cg_close / cg_pool_close). A later call opens a new one;
-     *  a call racing with close() fails with IllegalStateException instead of using a freed handle. */
+    /** Releases the device context / pool (cg_close / cg_pool_close) once the calls in flight have
+     *  returned (write lock). A later call opens a new one. */
     fun close() {
-        synchronized(lock) {
+        rw.write {
             if (ctx != 0L || pool != 0L) nativeClose(ctx, pool)
             ctx = 0
             pool = 0
         }
+    }
+
+    /** The C ABI's failure contract (include/cordagpu.h): CG_ERR_DEVICE leaves exactly the items no
+     *  device could run as CG_NOT_RUN (a pool has already re-run a failed device's shard on the healthy
+     *  ones). Those items, and only those, go to the engine once more through `rerun` (given their
+     *  indices, it returns their new statuses); what is still NOT_RUN after that stays NOT_RUN, and
+     *  raiseForStatus verifies it with the JVM's own Crypto.doVerify. Any other non-zero code is the
+     *  caller's input, not the device: thrown. Never throws for the whole batch on a device fault. */
+    private fun requeueNotRun(rc: Int, what: String, status: ByteArray, rerun: ((IntArray) -> ByteArray)?) {
+        if (rc == CG_OK) return
+        check(rc == CG_ERR_DEVICE) { "$what failed: $rc" }
+        val todo = status.indices.filter { (status[it].toInt() and 0xff) == CG_NOT_RUN }.toIntArray()
+        if (todo.isEmpty() || rerun == null) return
+        val again = try { rerun(todo) } catch (e: IllegalStateException) { return }   // still no device: stay NOT_RUN
+        for ((k, i) in todo.withIndex()) status[i] = again[k]
     }
 
     private inline fun <T> timed(n: Int, body: () -> T): T {
@@ -161,6 +194,8 @@ object CryptoBatch {
         val ok = status.count { it.toInt() == CG_VALID }
         m.meter(metric("Verification.Success")).mark(ok.toLong())
         m.meter(metric("Verification.Failure")).mark((status.size - ok).toLong())
+        // a pool call fills no cg_stats (n_items stays 0): no device stage times to report (ADVICE r5)
+        if (stats.getLong(0) == 0L) return
         val names = arrayOf("Device.H2D", "Device.KeyPrep", "Device.Verify", "Device.D2H", "Device.Total")
         for ((i, n) in names.withIndex())
             m.timer(metric(n)).update((stats.getDouble(16 + 8 * i) * 1e6).toLong(), TimeUnit.NANOSECONDS)
@@ -234,8 +269,14 @@ object CryptoBatch {
         }
     }
 
-    /** Batch overload of Crypto.doVerify / isValid: one status byte per item (include/cordagpu.h). */
+    /** Batch overload of Crypto.doVerify / isValid: one status byte per item (include/cordagpu.h).
+     *  One device or several (the pool shards the items); on a device fault the items left NOT_RUN are
+     *  re-queued once (requeueNotRun), and any still NOT_RUN reach the caller as NOT_RUN. */
     fun verifyBatch(items: List<BatchItem>, mode: Int = MODE_DOVERIFY): ByteArray = timed(items.size) {
+        verifyItems(items, mode, requeue = true)
+    }
+
+    private fun verifyItems(items: List<BatchItem>, mode: Int, requeue: Boolean): ByteArray {
         val arena = direct(items.sumOf { minOf(it.signatureData.size, SIG_LEN_MAX) + it.clearData.size + 8 } +
                            items.map { it.publicKey }.distinct().sumOf { it.encoded.size + 4 } + 16)
         val keys = Keys(items.map { it.publicKey }, arena)
@@ -252,12 +293,15 @@ object CryptoBatch {
         }
         val status = direct(items.size)
         val stats = direct(STATS_BYTES)
-        val (c, _) = handles()
-        check(c != 0L) { "CryptoBatch: verifyBatch needs a single-device context (gpuVerifier.devices has several)" }
-        val rc = nativeVerify(c, keys.table, keys.index.size, rec, items.size.toLong(), arena,
-                              arena.position().toLong(), mode, status, stats)
-        check(rc == 0) { "cg_verify_batch failed: $rc" }
-        ByteArray(items.size).also { status.get(it); record(stats, it) }
+        val rc = withHandles { c, p ->
+            nativeVerify(c, p, keys.table, keys.index.size, rec, items.size.toLong(), arena, arena.position().toLong(),
+                         mode, status, stats)
+        }
+        val st = ByteArray(items.size).also { status.get(it) }
+        requeueNotRun(rc, "cg_verify_batch", st,
+                      if (requeue) { todo -> verifyItems(todo.map { items[it] }, mode, requeue = false) } else null)
+        record(stats, st)
+        return st
     }
 
     /** Crypto.doVerify for every item, throwing what the first failing item's serial call throws.
@@ -287,76 +331,101 @@ object CryptoBatch {
 
     /** Batch Crypto.doVerify(txId, TransactionSignature) (Crypto.kt:499-502) for every signature of
      *  every transaction, SignableData spliced on the device: one status byte per signature, in order.
-     *  With several devices configured the call shards over the pool (cg_pool_verify_tx_signatures). */
+     *  With several devices configured the call shards over the pool (cg_pool_verify_tx_signatures). On
+     *  a device fault only the signatures left NOT_RUN are re-queued (requeueNotRun). */
     fun verifyTxSignatures(txs: List<Pair<SecureHash, List<TransactionSignature>>>, mode: Int = MODE_DOVERIFY): ByteArray {
         val all = txs.flatMap { it.second }
-        return timed(all.size) {
-            val metas = LinkedHashMap<SignatureMetadata, Int>()
-            all.forEach { metas.getOrPut(it.signatureMetadata) { metas.size } }
-            val split = metas.keys.map { signableTemplate(it) }
-            val arena = direct(all.sumOf { minOf(it.bytes.size, SIG_LEN_MAX) + 4 } +
-                               split.sumOf { it.first.size + it.second.size + 8 } +
-                               all.map { it.by }.distinct().sumOf { it.encoded.size + 4 } + 16)
-            val keys = Keys(all.map { it.by }, arena)
-            val tmpls = direct(24 * split.size)
-            for ((pre, suf) in split) {
-                arena.align4(); val p = arena.position().toLong(); arena.put(pre)
-                arena.align4(); val s = arena.position().toLong(); arena.put(suf)
-                tmpls.putLong(p).putLong(s).putInt(pre.size).putInt(suf.size)
-            }
-            val ids = direct(32 * txs.size)
-            val sigs = direct(24 * all.size)
-            txs.forEachIndexed { t, (id, list) ->
-                ids.put(id.bytes)
-                for (sig in list) {
-                    val ki = keys.index[sig.by]!!
-                    val bytes = sigField(keys.schemes[ki], sig.bytes)
-                    arena.align4()
-                    val off = arena.position().toLong(); arena.put(bytes)
-                    sigs.putLong(off).putInt(t).putInt(ki).putShort(bytes.size.toShort())
-                        .putShort(metas[sig.signatureMetadata]!!.toShort()).putInt(0)
-                }
-            }
-            val status = direct(all.size)
-            val stats = direct(STATS_BYTES)
-            val (c, p) = handles()
-            val rc = nativeVerifyTxSignatures(c, p, keys.table, keys.index.size, ids, txs.size.toLong(), sigs,
-                                              all.size.toLong(), tmpls, split.size, arena, arena.position().toLong(),
-                                              mode, status, stats)
-            check(rc == 0) { "cg_verify_tx_signatures failed: $rc" }
-            ByteArray(all.size).also { status.get(it); record(stats, it) }
+        return timed(all.size) { verifySigs(txs, mode, requeue = true) }
+    }
+
+    private fun verifySigs(txs: List<Pair<SecureHash, List<TransactionSignature>>>, mode: Int, requeue: Boolean): ByteArray {
+        val all = txs.flatMap { it.second }
+        val metas = LinkedHashMap<SignatureMetadata, Int>()
+        all.forEach { metas.getOrPut(it.signatureMetadata) { metas.size } }
+        val split = metas.keys.map { signableTemplate(it) }
+        val arena = direct(all.sumOf { minOf(it.bytes.size, SIG_LEN_MAX) + 4 } +
+                           split.sumOf { it.first.size + it.second.size + 8 } +
+                           all.map { it.by }.distinct().sumOf { it.encoded.size + 4 } + 16)
+        val keys = Keys(all.map { it.by }, arena)
+        val tmpls = direct(24 * split.size)
+        for ((pre, suf) in split) {
+            arena.align4(); val p = arena.position().toLong(); arena.put(pre)
+            arena.align4(); val s = arena.position().toLong(); arena.put(suf)
+            tmpls.putLong(p).putLong(s).putInt(pre.size).putInt(suf.size)
         }
+        val ids = direct(32 * txs.size)
+        val sigs = direct(24 * all.size)
+        txs.forEachIndexed { t, (id, list) ->
+            ids.put(id.bytes)
+            for (sig in list) {
+                val ki = keys.index[sig.by]!!
+                val bytes = sigField(keys.schemes[ki], sig.bytes)
+                arena.align4()
+                val off = arena.position().toLong(); arena.put(bytes)
+                sigs.putLong(off).putInt(t).putInt(ki).putShort(bytes.size.toShort())
+                    .putShort(metas[sig.signatureMetadata]!!.toShort()).putInt(0)
+            }
+        }
+        val status = direct(all.size)
+        val stats = direct(STATS_BYTES)
+        val rc = withHandles { c, p ->
+            nativeVerifyTxSignatures(c, p, keys.table, keys.index.size, ids, txs.size.toLong(), sigs, all.size.toLong(),
+                                     tmpls, split.size, arena, arena.position().toLong(), mode, status, stats)
+        }
+        val st = ByteArray(all.size).also { status.get(it) }
+        // the re-queue: the NOT_RUN signatures, each as a one-signature transaction of its own id
+        val owner = txs.flatMap { (id, list) -> list.map { id to it } }
+        requeueNotRun(rc, "cg_verify_tx_signatures", st,
+                      if (requeue) { todo -> verifySigs(todo.map { owner[it].first to listOf(owner[it].second) }, mode, false) }
+                      else null)
+        record(stats, st)
+        return st
     }
 
     /** cg_verify_batch over tables already in the C ABI's layout (the out-of-process verifier's batch
-     *  request body, VerifierBatchApi.kt): no re-encoding. One status byte per item. */
+     *  request body, VerifierBatchApi.kt): no re-encoding. One status byte per item; one device or a
+     *  pool. On a device fault the NOT_RUN items' records are re-queued once as a table of their own
+     *  (same keys and arena); any still NOT_RUN go back to the node as NOT_RUN. */
     fun verifyPacked(keys: ByteBuffer, nKeys: Int, items: ByteBuffer, nItems: Int, arena: ByteBuffer, arenaLen: Long,
                      mode: Int = MODE_DOVERIFY): ByteArray = timed(nItems) {
         require(nKeys >= 0 && nItems >= 0 && arenaLen >= 0) { "negative table size" }
         require(keys.capacity().toLong() >= 16L * nKeys && items.capacity().toLong() >= 32L * nItems &&
                 arena.capacity().toLong() >= arenaLen) { "a table is shorter than its count" }
+        verifyPackedItems(keys, nKeys, items, nItems, arena, arenaLen, mode, requeue = true)
+    }
+
+    private fun verifyPackedItems(keys: ByteBuffer, nKeys: Int, items: ByteBuffer, nItems: Int, arena: ByteBuffer,
+                                  arenaLen: Long, mode: Int, requeue: Boolean): ByteArray {
         val status = direct(nItems)
         val stats = direct(STATS_BYTES)
-        val (c, _) = handles()
-        check(c != 0L) { "CryptoBatch: verifyPacked needs a single-device context" }
-        val rc = nativeVerify(c, keys, nKeys, items, nItems.toLong(), arena, arenaLen, mode, status, stats)
-        check(rc == 0) { "cg_verify_batch failed: $rc" }
-        ByteArray(nItems).also { status.get(it); record(stats, it) }
+        val rc = withHandles { c, p -> nativeVerify(c, p, keys, nKeys, items, nItems.toLong(), arena, arenaLen, mode, status, stats) }
+        val st = ByteArray(nItems).also { status.get(it) }
+        requeueNotRun(rc, "cg_verify_batch", st, if (!requeue) null else { todo ->
+            val sub = direct(32 * todo.size)
+            val rec = ByteArray(32)
+            for (i in todo) { items.duplicate().apply { position(32 * i) }.get(rec); sub.put(rec) }
+            verifyPackedItems(keys, nKeys, sub, todo.size, arena, arenaLen, mode, requeue = false)
+        })
+        record(stats, st)
+        return st
     }
 
     /** WireTransaction ids + every signature in one call (cg_verify_transactions, include/cordagpu.h):
      *  the tables are the C ABI's own (cg_tx / cg_component / cg_txsig / cg_signable_tmpl, built by the
      *  out-of-process verifier from the request body it already holds). Fills the 32-byte ids, one
-     *  status per transaction (Merkle) and one per signature. */
+     *  status per transaction (Merkle) and one per signature. With a pool the call runs whole on one
+     *  healthy device and fails over to the next (cg_pool_verify_transactions: a signature may reference
+     *  any transaction's id, so it is not sharded). When no device could run it the signatures stay
+     *  NOT_RUN and the ids are not computed: IllegalStateException, the request is redelivered whole. */
     fun verifyTransactionsPacked(txs: ByteBuffer, nTx: Long, comps: ByteBuffer, nComps: Long, keys: ByteBuffer,
                                  nKeys: Int, sigs: ByteBuffer, nSigs: Long, tmpls: ByteBuffer, nTmpls: Int,
                                  arena: ByteBuffer, arenaLen: Long, idsOut: ByteBuffer, txStatusOut: ByteBuffer,
                                  sigStatusOut: ByteBuffer, mode: Int = MODE_DOVERIFY) {
-        val (c, _) = handles()
-        check(c != 0L) { "CryptoBatch: verifyTransactionsPacked needs a single-device context" }
-        val rc = nativeVerifyTransactions(c, txs, nTx, comps, nComps, keys, nKeys, sigs, nSigs, tmpls, nTmpls, arena,
-                                          arenaLen, mode, idsOut, txStatusOut, sigStatusOut)
-        check(rc == 0) { "cg_verify_transactions failed: $rc" }
+        val rc = withHandles { c, p ->
+            nativeVerifyTransactions(c, p, txs, nTx, comps, nComps, keys, nKeys, sigs, nSigs, tmpls, nTmpls, arena,
+                                     arenaLen, mode, idsOut, txStatusOut, sigStatusOut)
+        }
+        check(rc == CG_OK) { "cg_verify_transactions failed: $rc (no device could run it: redeliver the request)" }
     }
 
     /** Pins a direct buffer the caller keeps across calls (cg_host_register); unregister before freeing it. */
@@ -374,7 +443,8 @@ object CryptoBatch {
      *    3 KEY_INVALID   the JVM decoder's own exception, else InvalidKeyException
      *    4 UNSUPPORTED   Crypto.doVerify on the host (RSA / SPHINCS / COMPOSITE)
      *    5 EMPTY         IllegalArgumentException (Crypto.kt:476-477)
-     *    other (NOT_RUN) IllegalStateException: the item was never verified, re-queue it */
+     *  255 NOT_RUN       no device ran it (after the re-queue): Crypto.doVerify on the host, as UNSUPPORTED
+     *    other           IllegalStateException (not a status the engine writes) */
     fun raiseForStatus(status: Byte, item: BatchItem) {
         val scheme = Crypto.findSignatureScheme(item.publicKey)
         when (status.toInt() and 0xff) {
@@ -387,9 +457,10 @@ object CryptoBatch {
                 throw InvalidKeyException("public key rejected by the batch engine: ${scheme.schemeCodeName}")
             }
             CG_UNSUPPORTED -> { Crypto.doVerify(item.publicKey, item.signatureData, item.clearData); return }
+            CG_NOT_RUN -> { Crypto.doVerify(item.publicKey, item.signatureData, item.clearData); return }
             CG_EMPTY -> throw IllegalArgumentException(if (item.signatureData.isEmpty()) "Signature data is empty!"
                                                       else "Clear data is empty, nothing to verify!")
-            else -> throw IllegalStateException("signature not verified: re-queue")   // CG_NOT_RUN
+            else -> throw IllegalStateException("unknown engine status $status")
         }
     }
 

@@ -135,6 +135,9 @@ def parse(argv=None):
     ap.add_argument("--engine-threads", type=int, default=0,
                     help="cg_config.host_threads of the headline context (0: this rank's share when ranks "
                          "share the node, else the library's budget)")
+    ap.add_argument("--txsig-table", type=int, default=12, choices=(12, 24),
+                    help="the headline's signature table: 12 = cg_verify_tx_signatures_packed (12-byte records over "
+                         "the dense signature stream, round 6), 24 = cg_verify_tx_signatures (24-byte cg_txsig)")
     ap.add_argument("--host-register", type=int, default=0,
                     help="1: register the headline's host buffers once (cg_host_register: DMA straight from "
                          "them, no CPU staging copy), as a JVM node registers its persistent direct buffers; "
@@ -872,11 +875,13 @@ def bench_key_dist(a, eng, dist, rank, threads, steps):
     gen = time.time() - t0
     from corda_amd.batch import Batch
     modes = table_modes(Batch(pool.keys, pool.items[idx], pool.arena), ps[idx])
-    eng.verify_tx_signatures(tb)
+    pb = tb.packed() if a.txsig_table == 12 else None
+    call = (lambda: eng.verify_tx_signatures_packed(pb)) if pb is not None else (lambda: eng.verify_tx_signatures(tb))
+    call()
     eng.stage_times()
     t = time.perf_counter()
     for _ in range(steps):
-        st = eng.verify_tx_signatures(tb)
+        st = call()
     el = (time.perf_counter() - t) / steps
     stg = eng.stage_times()
     ver = check_verdicts(st, expected_verdicts(pl[idx], ps[idx]))
@@ -922,12 +927,14 @@ def main_pool(a):
     idx = wl.tx_ordered_draws(pool.n, n, id_idx, seed=a.seed + 1)
     tb = wl.tx_sig_stream(pool, ps, idx, ids, id_idx, nthreads=threads)
     gen_s = time.time() - t0
+    pb = tb.packed() if a.txsig_table == 12 else None
     with EnginePool(devices, chunk_items=a.chunk_items) as ep:
+        call = (lambda: ep.verify_tx_signatures_packed(pb)) if pb is not None else (lambda: ep.verify_tx_signatures(tb))
         for _ in range(a.warmup):
-            st = ep.verify_tx_signatures(tb)
+            st = call()
         t = time.perf_counter()
         for _ in range(a.steps):
-            st = ep.verify_tx_signatures(tb)
+            st = call()
         el = (time.perf_counter() - t) / a.steps
         stats = dict(ep.last_stats)
     ver = check_verdicts(st, expected_verdicts(pl[idx], ps[idx]))
@@ -935,7 +942,8 @@ def main_pool(a):
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic (as the headline)",
             "config": {"workload": f"BASELINE configs[4], whole node from one process: {a.items} signatures per slot "
-                                   f"over slots {devices} through cg_pool_verify_tx_signatures",
+                                   f"over slots {devices} through cg_pool_verify_tx_signatures"
+                                   + ("_packed" if pb is not None else ""),
                        "items": n, "parallelism": f"cg_pool{len(devices)}"},
             "pool_stats": stats, "verdicts": ver, "gen_s": round(gen_s, 1)}
     print(json.dumps(line), flush=True)
@@ -995,6 +1003,8 @@ def main(argv=None):
     # zero-copy ingestion: the caller's persistent buffers registered once, outside the timed region
     # (a JVM node registers its direct-buffer arena once; cg_host_register, include/cordagpu.h)
     registered, huge_maps = [], []
+    # the 12-byte table: the generator's arena tail is already the dense stream (a view, no copy)
+    pb = tb.packed() if a.txsig_table == 12 else None
     if a.host_register and hasattr(_lib_mod().lib(), "cg_host_register"):
         if a.host_register == 2:  # the same bytes in 2 MB transparent huge pages first
             from corda_amd import batch as _B
@@ -1003,13 +1013,14 @@ def main(argv=None):
                 cp[name], m = hugepage_copy(getattr(tb, name))
                 huge_maps.append(m)
             tb = _B.TxSigBatch(tb.keys, cp["ids"], cp["sigs"], tb.tmpls, cp["arena"])
-        for arr in (tb.arena, tb.sigs, tb.ids):
+            pb = tb.packed() if a.txsig_table == 12 else None
+        for arr in ((tb.arena, pb.sigs, pb.ids) if pb is not None else (tb.arena, tb.sigs, tb.ids)):
             if _lib_mod().host_register(arr):
                 registered.append(arr)
 
     def step():
-        # the whole node: host arena -> host verdicts, one cg_verify_tx_signatures call (synchronous)
-        holder["st"] = eng.verify_tx_signatures(tb)
+        # the whole node: host arena -> host verdicts, one cg_verify_tx_signatures(_packed) call (synchronous)
+        holder["st"] = eng.verify_tx_signatures_packed(pb) if pb is not None else eng.verify_tx_signatures(tb)
         if world > 1:  # RCCL all-gather of the per-GPU verdict vectors
             holder["all"] = shard.gather_verdicts(torch.from_numpy(holder["st"]).to(dev), world * tb.n, world)
 
@@ -1064,7 +1075,7 @@ def main(argv=None):
                 if "valu_issue" in tr:
                     roof["valu_issue"] = tr["valu_issue"]
 
-    h2d_bytes = int(tb.arena.size + tb.sigs.nbytes + tb.ids.nbytes + tb.keys.nbytes)
+    h2d_bytes = pb.h2d_bytes if pb is not None else int(tb.arena.size + tb.sigs.nbytes + tb.ids.nbytes + tb.keys.nbytes)
     extra = {"stages": stage_summary(stages, a.steps), "ecdsa_ladders": ec_roof, "roofline_full": roof,
              "verdicts": ver, "gen_s": round(gen_s, 1),
              "headline_h2d": {"bytes_per_call": h2d_bytes, "bytes_per_sig": round(h2d_bytes / tb.n, 1),
@@ -1116,10 +1127,12 @@ def main(argv=None):
                     "SignatureMetadata(1, scheme)) with every Appendix A corruption class (tools/workload)",
             "config": {"workload": "BASELINE configs[4] per-GPU shard, whole node: notary-style mixed batch 70% "
                                    "Ed25519 / 20% secp256r1 / 10% secp256k1, host arena -> host verdicts, one "
-                                   "cg_verify_tx_signatures call per step (batch Crypto.doVerify(txId, sig))",
+                                   + ("cg_verify_tx_signatures_packed (12-byte signature table)" if pb is not None
+                                      else "cg_verify_tx_signatures") +
+                                   " call per step (batch Crypto.doVerify(txId, sig))",
                        "items_per_gpu": a.items, "unique_pool": a.pool,
                        "mix": [n_ed, n_r1, a.items - n_ed - n_r1], "keys": len(batch.keys),
-                       "sigs_per_tx": a.sigs_per_tx, "h2d_bytes_per_gpu": h2d_bytes,
+                       "sigs_per_tx": a.sigs_per_tx, "h2d_bytes_per_gpu": h2d_bytes, "txsig_table": a.txsig_table,
                        "parallelism": f"shard{world}" + ("+rccl_allgather(verdicts)" if world > 1 else "")},
         }
         summary = {"verdicts_checked": ver["checked_vs_labels"], "label_mismatches": ver["label_mismatches"],

@@ -129,6 +129,17 @@ def lib():
                     L.cg_pool_verify_transactions.argtypes = [vp, vp, u64, vp, u64, vp, u32, vp, u64, vp, u32, vp, u64,
                                                               u32, vp, vp, vp, ctypes.POINTER(cg_pool_stats)]
                     L.cg_pool_verify_transactions.restype = i32
+            if hasattr(L, "cg_verify_tx_signatures_packed"):  # round 6: the 12-byte signature table
+                L.cg_verify_tx_signatures_packed.argtypes = [vp, vp, u32, vp, u64, vp, u64, vp, u64, vp, u32, vp, u64,
+                                                             u32, vp, ctypes.POINTER(cg_stats)]
+                L.cg_verify_tx_signatures_packed.restype = i32
+                L.cg_verify_tx_signatures_packed_device.argtypes = [vp, vp, u32, vp, u64, vp, u64, u64, u64, vp, u32,
+                                                                    vp, u64, u32, vp, vp]
+                L.cg_verify_tx_signatures_packed_device.restype = i32
+                if pool:
+                    L.cg_pool_verify_tx_signatures_packed.argtypes = [vp, vp, u32, vp, u64, vp, u64, vp, u64, vp, u32,
+                                                                      vp, u64, u32, vp, ctypes.POINTER(cg_pool_stats)]
+                    L.cg_pool_verify_tx_signatures_packed.restype = i32
             if hasattr(L, "cg_context_info"):  # round 6: the fixed-base table budget
                 L.cg_context_info.argtypes = [vp, ctypes.POINTER(cg_info)]
                 L.cg_context_info.restype = i32

@@ -18,6 +18,10 @@ TX_DTYPE = np.dtype([("first", "<u8"), ("n", "<u4"), ("reserved", "<u4"), ("salt
 TXSIG_DTYPE = np.dtype([("sig_off", "<u8"), ("tx_idx", "<u4"), ("key_idx", "<u4"), ("sig_len", "<u2"),
                         ("tmpl", "<u2"), ("reserved", "<u4")])
 TMPL_DTYPE = np.dtype([("prefix_off", "<u8"), ("suffix_off", "<u8"), ("prefix_len", "<u4"), ("suffix_len", "<u4")])
+# cg_txsig_packed (round 6): the 12-byte table over a dense signature stream (each signature at the
+# 4-byte-aligned end of the one before it)
+TXSIG12_DTYPE = np.dtype([("tx_idx", "<u4"), ("key_idx", "<u4"), ("sig_len", "<u2"), ("tmpl", "<u2")])
+assert TXSIG12_DTYPE.itemsize == 12
 # tear-offs (cg_pmt_node / cg_filtered_leaf / cg_filtered_tx)
 PMT_NODE_DTYPE = np.dtype([("hash_off", "<u8"), ("kind", "<u4"), ("reserved", "<u4")])
 FLEAF_DTYPE = np.dtype([("off", "<u8"), ("nonce_off", "<u8"), ("len", "<u4"), ("flags", "<u4")])
@@ -214,6 +218,60 @@ class TxSigBatch:
     def subset(self, idx):
         """The signatures ``idx`` over the same keys, ids, templates and arena (a re-queue)."""
         return TxSigBatch(self.keys, self.ids, np.ascontiguousarray(self.sigs[idx]), self.tmpls, self.arena)
+
+    def packed(self):
+        """The same signatures as cg_verify_tx_signatures_packed input (PackedTxSigBatch): the 12-byte
+        table and the dense signature stream. When the arena already holds the signatures back to back
+        in table order, 4-byte aligned, after everything else (wl.tx_sig_stream, a JVM writer), the
+        stream is a view of that tail and the arena is cut before it; otherwise the bytes are gathered."""
+        n = len(self.sigs)
+        sig12 = np.zeros(n, TXSIG12_DTYPE)
+        for f in ("tx_idx", "key_idx", "sig_len", "tmpl"):
+            sig12[f] = self.sigs[f]
+        span = (self.sigs["sig_len"].astype(np.uint64) + np.uint64(3)) & ~np.uint64(3)
+        rel = np.zeros(n, np.uint64)
+        if n > 1:
+            np.cumsum(span[:-1], out=rel[1:])
+        total = int(rel[-1] + span[-1]) if n else 0
+        start = int(self.sigs["sig_off"][0]) if n else int(self.arena.size)
+        head_end = 0
+        for k in self.keys:
+            head_end = max(head_end, int(k["off"]) + int(k["len"]))
+        for t in self.tmpls:
+            head_end = max(head_end, int(t["prefix_off"]) + int(t["prefix_len"]), int(t["suffix_off"]) + int(t["suffix_len"]))
+        if n and np.array_equal(self.sigs["sig_off"], np.uint64(start) + rel) and head_end <= start \
+                and start + total <= self.arena.size:
+            stream = self.arena[start:start + total]
+            arena = self.arena[:start]
+        else:
+            stream = np.zeros(total, np.uint8)
+            src = self.sigs["sig_off"].astype(np.int64)
+            for j in range(n):
+                ln = int(self.sigs["sig_len"][j])
+                stream[int(rel[j]):int(rel[j]) + ln] = self.arena[src[j]:src[j] + ln]
+            arena = self.arena
+        return PackedTxSigBatch(self.keys, self.ids, sig12, stream, self.tmpls, arena)
+
+
+class PackedTxSigBatch:
+    """cg_verify_tx_signatures_packed input: ``sigs`` (TXSIG12_DTYPE), ``stream`` (uint8: signature i
+    at the 4-byte-aligned end of signature i-1), ``arena`` (key and template bytes)."""
+
+    def __init__(self, keys, ids, sigs, stream, tmpls, arena):
+        self.keys, self.sigs, self.stream, self.tmpls, self.arena = keys, sigs, stream, tmpls, arena
+        self.ids = np.ascontiguousarray(ids, dtype=np.uint8).reshape(-1)
+
+    @property
+    def n(self):
+        return len(self.sigs)
+
+    @property
+    def n_ids(self):
+        return self.ids.size // 32
+
+    @property
+    def h2d_bytes(self):
+        return int(self.arena.size + self.stream.size + self.sigs.nbytes + self.ids.nbytes + self.keys.nbytes)
 
 
 class TxSigBuilder(BatchBuilder):

@@ -115,6 +115,7 @@ struct cg_ctx {
   uint32_t wide_max = cg::kKeyWideMax;
   // transaction pipeline: verify items, spliced messages, templates; host-entry staging
   DevBuf txitems, msgs, tmpls, h_txs, h_comps, h_sigs, h_ids, h_txst;
+  DevBuf sig12ws;  // the 12-byte signature table's per-block stream offsets (launch_tx_sig12_range)
   // tear-offs: leaf-hash workspace
   DevBuf ftxws;
   // host-buffer verify: a copy stream and one event per pipeline chunk (H2D of chunk k+1 overlaps
@@ -640,7 +641,8 @@ int cg_host_registered(const void* p, uint64_t len) {
 }
 
 static_assert(sizeof(cg_config) == 56, "cg_config is 56 bytes in ABI v2");
-static_assert(sizeof(cg_item) == 32 && sizeof(cg_key) == 16 && sizeof(cg_txsig) == 24, "ABI struct sizes");
+static_assert(sizeof(cg_item) == 32 && sizeof(cg_key) == 16 && sizeof(cg_txsig) == 24 && sizeof(cg_txsig_packed) == 12,
+              "ABI struct sizes");
 
 int cg_open(cg_ctx** out, const cg_config* cfg) {
   if (!out) return fail(CG_ERR_ARG, "cg_open: out is NULL");
@@ -779,7 +781,8 @@ void cg_close(cg_ctx* c) {
   c->aux0.release();
   c->aux1.release();
   c->aux2.release();
-  for (DevBuf* b : {&c->txitems, &c->msgs, &c->tmpls, &c->h_txs, &c->h_comps, &c->h_sigs, &c->h_ids, &c->h_txst, &c->ftxws})
+  for (DevBuf* b : {&c->txitems, &c->msgs, &c->tmpls, &c->h_txs, &c->h_comps, &c->h_sigs, &c->h_ids, &c->h_txst,
+                    &c->ftxws, &c->sig12ws})
     b->release();
   for (int k = 0; k < 3; ++k) {
     if (c->fork.side[k]) {
@@ -1243,12 +1246,22 @@ static hipError_t ensure_txsig_ws(cg_ctx* c, uint64_t n_sigs, uint32_t n_tmpls, 
 // `uses` (sampled from the signature table on the device, or the host's exact counts), each chunk's
 // verify items and spliced SignableData made just before its front (after `ready`, which the host
 // form uses to land the chunk's signature table slice and bytes).
+// The 12-byte table (cg_txsig_packed): d_sigs is null and `p12` says where the signatures sit: the
+// stream at arena offset sig_region, chunk k's first signature at stream offset (*chunk_base)[k] (host
+// form: the host sums the lengths as it scans each chunk) or every block's offset precomputed in
+// d_bases (device form).
+struct Packed12 {
+  const cg_txsig_packed* d_sigs = nullptr;
+  uint64_t sig_region = 0, sig_bytes_len = 0;
+  const std::vector<uint64_t>* chunk_base = nullptr;
+  const uint64_t* d_bases = nullptr;
+};
 static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_ids, uint64_t n_ids,
                                const cg_txsig* d_sigs, uint64_t n_sigs, const cg_signable_tmpl* tmpls,
                                uint32_t n_tmpls, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,
                                uint8_t* d_status, hipStream_t s, uint64_t slot, const cg::KeyUses& uses,
                                const std::function<hipError_t(uint64_t, uint64_t, uint64_t)>* ready,
-                               const std::vector<uint64_t>* bounds = nullptr) {
+                               const std::vector<uint64_t>* bounds = nullptr, const Packed12* p12 = nullptr) {
   if (n_sigs == 0) return hipSuccess;
   hipError_t e = hipSuccess;
   const cg_signable_tmpl* dt = (const cg_signable_tmpl*)c->tmpls.p;
@@ -1258,7 +1271,11 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
   const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> prepare = [&](uint64_t k, uint64_t first,
                                                                                uint64_t cnt) {
     hipError_t r = ready ? (*ready)(k, first, cnt) : hipSuccess;
-    if (r == hipSuccess)
+    if (r == hipSuccess && p12)
+      r = cg::launch_tx_sig12_range(p12->d_sigs, first, cnt, p12->sig_region, p12->sig_bytes_len,
+                                    p12->chunk_base ? (*p12->chunk_base)[k] : 0, p12->d_bases, dt, n_tmpls, n_ids,
+                                    arena_len, (cg_item*)c->txitems.p, c->sig12ws.p, s);
+    else if (r == hipSuccess)
       r = cg::launch_tx_sig_range(d_sigs, first, cnt, dt, n_tmpls, nullptr, n_ids, d_ids, arena_len, slot,
                                   (cg_item*)c->txitems.p, (uint8_t*)c->msgs.p, s);
     return r;
@@ -1274,11 +1291,41 @@ static hipError_t launch_txsig(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys,
 // the template bytes, the ids and the signature table (everything the key tables and the plans
 // need), then the signature bytes chunk by chunk, each copy issued just before its chunk's front
 // so that the key-table builds and the previous chunk's kernels run during it.
+// The 12-byte form (cg_verify_tx_signatures_packed): sigs is null, sigs12 the table, the signatures
+// dense in sig_bytes. On the device they follow the caller's arena at sig_region (16-aligned), so the
+// kernels address every byte by an absolute arena offset as in the 24-byte form; a key or template
+// that lies outside [0, arena_len) is moved out of the extended arena too (never reads a signature).
 static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const uint8_t* ids,
                                     uint64_t n_ids, const cg_txsig* sigs, uint64_t n_sigs,
                                     const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
-                                    uint64_t arena_len, uint32_t mode, uint8_t* status_out, cg_stats* stats) {
+                                    uint64_t arena_len, uint32_t mode, uint8_t* status_out, cg_stats* stats,
+                                    const cg_txsig_packed* sigs12 = nullptr, const uint8_t* sig_bytes = nullptr,
+                                    uint64_t sig_bytes_len = 0) {
   const auto t0 = std::chrono::steady_clock::now();
+  const bool packed = sigs12 != nullptr;
+  const size_t rec_bytes = packed ? sizeof(cg_txsig_packed) : sizeof(cg_txsig);
+  const uint64_t caller_len = arena_len;
+  const uint64_t sig_region = packed ? ((arena_len + 15) & ~(uint64_t)15) : 0;
+  if (packed) arena_len = sig_region + sig_bytes_len;  // what the kernels see
+  std::vector<cg_key> keys_fix;
+  std::vector<cg_signable_tmpl> tmpls_fix;
+  if (packed) {  // out-of-arena keys / templates stay out of range in the extended arena
+    auto out = [&](uint64_t off, uint64_t len) { return off > caller_len || len > caller_len - off; };
+    for (uint32_t k = 0; k < n_keys; ++k)
+      if (out(keys[k].off, keys[k].len)) {
+        if (keys_fix.empty()) keys_fix.assign(keys, keys + n_keys);
+        keys_fix[k].off = UINT64_MAX;
+      }
+    for (uint32_t k = 0; k < n_tmpls; ++k)
+      if (out(tmpls[k].prefix_off, tmpls[k].prefix_len) || out(tmpls[k].suffix_off, tmpls[k].suffix_len)) {
+        if (tmpls_fix.empty()) tmpls_fix.assign(tmpls, tmpls + n_tmpls);
+        tmpls_fix[k].prefix_off = UINT64_MAX;
+      }
+    if (!keys_fix.empty()) keys = keys_fix.data();
+    if (!tmpls_fix.empty()) tmpls = tmpls_fix.data();
+  }
+  // a record's key index, either table (the count passes)
+  auto key_at = [&](uint64_t i) -> uint32_t { return packed ? sigs12[i].key_idx : sigs[i].key_idx; };
   if (c->fault) return fail(CG_ERR_DEVICE, "cg_verify_tx_signatures: device fault (injected by cg_pool_inject_fault)");
   HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
   // chunks: the device chunk, but at least CG_TXSIG_MIN_CHUNKS of them for a large call unless the
@@ -1316,10 +1363,10 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   const uint64_t nch = bounds.size() - 1;
   // arena extents: key bytes + template bytes (the header), then each chunk's signature bytes
   Extent head, win;
-  for (uint32_t k = 0; k < n_keys; ++k) head.add(keys[k].off, keys[k].len, arena_len);
+  for (uint32_t k = 0; k < n_keys; ++k) head.add(keys[k].off, keys[k].len, caller_len);
   for (uint32_t k = 0; k < n_tmpls; ++k) {
-    head.add(tmpls[k].prefix_off, tmpls[k].prefix_len, arena_len);
-    head.add(tmpls[k].suffix_off, tmpls[k].suffix_len, arena_len);
+    head.add(tmpls[k].prefix_off, tmpls[k].prefix_len, caller_len);
+    head.add(tmpls[k].suffix_off, tmpls[k].suffix_len, caller_len);
   }
   // Key-use counts for the table modes from a 1-in-CG_TXSIG_COUNT_SAMPLE sample of the signature
   // table (16 host threads; the modes change only speed, never a verdict), every key at least 1 so
@@ -1364,10 +1411,14 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
         std::vector<uint32_t>& of = c->ovf[t];
         of.clear();
         uint8_t* cc = c8.data();
-        for (uint64_t i = n_sigs * t / nt; i < n_sigs * (t + 1) / nt; ++i) {
-          const uint32_t k = sigs[i].key_idx;
-          if (k < n_keys && ++cc[k] == 0) of.push_back(k);
-        }
+        auto run = [&](const auto* tab) {
+          for (uint64_t i = n_sigs * t / nt; i < n_sigs * (t + 1) / nt; ++i) {
+            const uint32_t k = tab[i].key_idx;
+            if (k < n_keys && ++cc[k] == 0) of.push_back(k);
+          }
+        };
+        if (packed) run(sigs12);
+        else run(sigs);
       };
       par(nt, scan8);
       auto sum = [&](uint64_t t) {
@@ -1391,8 +1442,10 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
         // B consecutive records per group of S B, the block at a hashed position (no aliasing with
         // a layout that cycles through the keys); B > 1 reads fewer cache lines per sample
         const uint64_t i0 = (g * S + (((uint32_t)g * 0x9E3779B1u) >> 24) % S) * Bs;
-        for (uint64_t i = i0; i < i0 + Bs && i < n_sigs; ++i)
-          if (sigs[i].key_idx < n_keys) ++cnt[sigs[i].key_idx];
+        for (uint64_t i = i0; i < i0 + Bs && i < n_sigs; ++i) {
+          const uint32_t k = key_at(i);
+          if (k < n_keys) ++cnt[k];
+        }
       }
     };
     if (nt == 1) {
@@ -1430,32 +1483,51 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
       counts[k] = e > 0xfffffff0ull ? 0xfffffff0u : (uint32_t)e;
     }
   };
-  // chunk k's signature bytes and id bytes (exact: a threaded scan of its slice of the table)
-  auto chunk_extents = [&](uint64_t k, Extent& ext, Extent& idx) {
+  // chunk k's signature bytes and id bytes (exact: a threaded scan of its slice of the table). The
+  // 12-byte table: the chunk's stream bytes (the sum of round_up(sig_len, 4)) in `span`, its extent
+  // set once its stream offset is known (copy_table: the chunks before it summed)
+  auto chunk_extents = [&](uint64_t k, Extent& ext, Extent& idx, uint64_t& span) {
     const uint64_t f = bounds[k], e = bounds[k + 1];
     const uint64_t m = (e - f) < (1u << 16) ? 1 : nt;
     std::vector<Extent> pe(m), pi(m);
+    std::vector<uint64_t> ps(m, 0);
     auto scan = [&](uint64_t t) {
       Extent a, b;  // thread-local until the end (the vector slots share cache lines)
-      for (uint64_t i = f + (e - f) * t / m; i < f + (e - f) * (t + 1) / m; ++i) {
-        a.add(sigs[i].sig_off, sigs[i].sig_len, arena_len);
-        if (sigs[i].tx_idx < n_ids) b.add(32ull * sigs[i].tx_idx, 32, 32ull * n_ids);
+      uint64_t sp = 0;
+      const uint64_t i0 = f + (e - f) * t / m, i1 = f + (e - f) * (t + 1) / m;
+      if (packed) {
+        for (uint64_t i = i0; i < i1; ++i) {
+          sp += ((uint64_t)sigs12[i].sig_len + 3u) & ~(uint64_t)3;
+          if (sigs12[i].tx_idx < n_ids) b.add(32ull * sigs12[i].tx_idx, 32, 32ull * n_ids);
+        }
+      } else {
+        for (uint64_t i = i0; i < i1; ++i) {
+          a.add(sigs[i].sig_off, sigs[i].sig_len, arena_len);
+          if (sigs[i].tx_idx < n_ids) b.add(32ull * sigs[i].tx_idx, 32, 32ull * n_ids);
+        }
       }
       pe[t] = a;
       pi[t] = b;
+      ps[t] = sp;
     };
     par(m, scan);
+    span = 0;
     for (uint64_t t = 0; t < m; ++t) {
       ext.merge(pe[t]);
       idx.merge(pi[t]);
+      span += ps[t];
     }
   };
+  // the 12-byte table: chunk k's first signature at stream offset cbase[k] (cbase[k + 1] is set when
+  // chunk k's table slice is staged)
+  std::vector<uint64_t> cbase(nch + 1, 0);
   // the device arena mirrors [0, arena_len) (only referenced bytes are copied)
   win.lo = 0;
   win.hi = arena_len;
   const uint64_t slot = tmpl_slot(tmpls, n_tmpls);
   HIP_TRY(c->keys.ensure(sizeof(cg_key) * (n_keys ? n_keys : 1)), "hipMalloc(keys)");
-  HIP_TRY(c->h_sigs.ensure(sizeof(cg_txsig) * n_sigs), "hipMalloc(sigs)");
+  HIP_TRY(c->h_sigs.ensure(rec_bytes * n_sigs), "hipMalloc(sigs)");
+  if (packed) HIP_TRY(c->sig12ws.ensure(cg::tx_sig12_scratch_bytes(per)), "hipMalloc(signature offsets)");
   HIP_TRY(c->aux1.ensure(sizeof(uint32_t) * counts.size()), "hipMalloc(key use counts)");
   HIP_TRY(c->h_ids.ensure(32 * (n_ids ? n_ids : 1)), "hipMalloc(ids)");
   HIP_TRY(c->arena.ensure((win.hi - win.lo) + 16), "hipMalloc(arena window)");
@@ -1494,6 +1566,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     HIP_TRY(hipMemcpyAsync(c->keys.p, keys, sizeof(cg_key) * n_keys, hipMemcpyHostToDevice, c->copy), "H2D keys");
   HIP_TRY(copy_missing(have, head, arena, dwin, win.lo, c->copy), "H2D key / template bytes");
   std::vector<std::pair<uint64_t, uint64_t>> have_ids;  // id bytes already resident
+  std::vector<std::pair<uint64_t, uint64_t>> have_sig;  // the 12-byte form's stream bytes already resident
   // chunk k: its slice of the signature table, the ids it references not yet resident (a caller that
   // lists each transaction's signatures together ships each id once, with its first chunk), then its
   // signature bytes, on copy stream cs; seg[k] marks the end
@@ -1521,7 +1594,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     return v && v[0] == '1';
   }();
   std::thread ahead_thr;
-  uint64_t ahead_k = ~0ull;
+  uint64_t ahead_k = ~0ull, ahead_span = 0;
   Extent ahead_ek, ahead_ik;
   struct JoinAhead {  // every exit path joins the helper before the extents it writes go away
     std::thread& t;
@@ -1537,24 +1610,34 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     Extent& ek = ext_e[k];
     Extent& ik = ext_i[k];
     const double h0 = htrace ? ms_since() : 0;
+    uint64_t span = 0;
     if (ahead_k == k) {
       ahead_thr.join();
       ek = ahead_ek;
       ik = ahead_ik;
+      span = ahead_span;
       ahead_k = ~0ull;
     } else {
-      chunk_extents(k, ek, ik);
+      chunk_extents(k, ek, ik, span);
+    }
+    if (packed) {  // the chunk's stream bytes, clipped to the caller's buffer (past it: CG_NOT_RUN)
+      cbase[k + 1] = cbase[k] + span;
+      ek = Extent();
+      ek.add(cbase[k], span, sig_bytes_len);
     }
     if (scan_ahead && k + 1 < nch) {
       ahead_k = k + 1;
       ahead_ek = Extent();
       ahead_ik = Extent();
-      ahead_thr = std::thread([&, k] { chunk_extents(k + 1, ahead_ek, ahead_ik); });
+      ahead_thr = std::thread([&, k] { chunk_extents(k + 1, ahead_ek, ahead_ik, ahead_span); });
     }
     const double h1 = htrace ? ms_since() : 0;
     const uint64_t first = bounds[k], cnt = bounds[k + 1] - bounds[k];
-    const hipError_t e = hipMemcpyAsync((cg_txsig*)c->h_sigs.p + first, sigs + first, sizeof(cg_txsig) * cnt,
-                                        hipMemcpyHostToDevice, cs);
+    const hipError_t e =
+        packed ? hipMemcpyAsync((cg_txsig_packed*)c->h_sigs.p + first, sigs12 + first, rec_bytes * cnt,
+                                hipMemcpyHostToDevice, cs)
+               : hipMemcpyAsync((cg_txsig*)c->h_sigs.p + first, sigs + first, rec_bytes * cnt, hipMemcpyHostToDevice,
+                                cs);
     ht[3 * k] = h0;
     ht[3 * k + 1] = h1 - h0;
     ht[3 * k + 2] = htrace ? ms_since() - h1 : 0;
@@ -1565,7 +1648,8 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     const double h2 = htrace ? ms_since() : 0;
     hipError_t e = copy_missing(have_ids, ext_i[k], ids, (uint8_t*)c->h_ids.p, 0, cs);
     const double h3 = htrace ? ms_since() : 0;
-    if (e == hipSuccess) e = copy_missing(have, ek, arena, dwin, win.lo, cs);
+    if (e == hipSuccess && packed) e = copy_missing(have_sig, ek, sig_bytes, dwin + sig_region, 0, cs);
+    else if (e == hipSuccess) e = copy_missing(have, ek, arena, dwin, win.lo, cs);
     if (e == hipSuccess) e = hipEventRecord(c->seg[k], cs);
     if (e == hipSuccess && htrace) {
       while (c->segt.size() <= k) {
@@ -1578,7 +1662,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     if (htrace)
       fprintf(stderr, "[cg host] chunk %llu at %.3f: scan %.3f sigs %.3f (%.1f MB) ids %.3f arena %.3f (%.1f MB) ms\n",
               (unsigned long long)k, ht[3 * k], ht[3 * k + 1], ht[3 * k + 2],
-              sizeof(cg_txsig) * (bounds[k + 1] - bounds[k]) / 1e6, h3 - h2, ms_since() - h3,
+              rec_bytes * (bounds[k + 1] - bounds[k]) / 1e6, h3 - h2, ms_since() - h3,
               ek.empty() ? 0.0 : (ek.hi - ek.lo) / 1e6);
     return e;
   };
@@ -1679,9 +1763,16 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   uses.n = n_sigs;
   uses.host_keys = keys;
   uses.host_counts = counts.data();
+  Packed12 p12;
+  if (packed) {
+    p12.d_sigs = (const cg_txsig_packed*)c->h_sigs.p;
+    p12.sig_region = sig_region;
+    p12.sig_bytes_len = sig_bytes_len;
+    p12.chunk_base = &cbase;
+  }
   const hipError_t le = launch_txsig(c, (const cg_key*)c->keys.p, n_keys, (const uint8_t*)c->h_ids.p, n_ids,
-                                     (const cg_txsig*)c->h_sigs.p, n_sigs, tmpls, n_tmpls, dbase, arena_len, mode, ds,
-                                     s, slot, uses, &before, &bounds);
+                                     packed ? nullptr : (const cg_txsig*)c->h_sigs.p, n_sigs, tmpls, n_tmpls, dbase,
+                                     arena_len, mode, ds, s, slot, uses, &before, &bounds, packed ? &p12 : nullptr);
   if (le == hipSuccess && c->fork.mid_front) {  // the last front did not consume its hook
     const hipError_t me = mid();
     if (me != hipSuccess) copy_err = me;
@@ -1769,6 +1860,67 @@ int cg_verify_tx_signatures_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_k
           "launch_txsig");
   HIP_TRY(order_out(c, s), "hipEventRecord");
   return CG_OK;
+}
+
+int cg_verify_tx_signatures_packed_device(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_ids,
+                                          uint64_t n_ids, const cg_txsig_packed* d_sigs, uint64_t n_sigs,
+                                          uint64_t sig_bytes_off, uint64_t sig_bytes_len,
+                                          const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* d_arena,
+                                          uint64_t arena_len, uint32_t mode, uint8_t* d_status, void* hip_stream) {
+  const int a = txsig_args("cg_verify_tx_signatures_packed_device", c, n_keys, d_keys, n_ids, d_ids, n_sigs, d_sigs,
+                           d_status, n_tmpls, tmpls, mode);
+  if (a != CG_OK) return a;
+  if (sig_bytes_off > arena_len || sig_bytes_len > arena_len - sig_bytes_off)
+    return fail(CG_ERR_ARG, "cg_verify_tx_signatures_packed_device: the signature stream lies outside the arena");
+  if (n_sigs == 0) return CG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->fault) return fail(CG_ERR_DEVICE, "cg_verify_tx_signatures_packed_device: device fault (injected)");
+  HIP_TRY(hipSetDevice(c->device), "hipSetDevice");
+  const uint64_t slot = tmpl_slot(tmpls, n_tmpls);
+  // equal chunks rounded to the 256-record blocks whose stream offsets are computed once for the table
+  uint64_t per = chunk_of(c, n_sigs);
+  per = (per + 255) & ~(uint64_t)255;
+  std::vector<uint64_t> bounds;
+  for (uint64_t f = 0; f < n_sigs; f += per) bounds.push_back(f);
+  bounds.push_back(n_sigs);
+  HIP_TRY(ensure_txsig_ws(c, n_sigs, n_tmpls, slot), "hipMalloc(tx signature workspace)");
+  HIP_TRY(ensure_ws(c, n_keys, per, n_sigs), "hipMalloc(workspace)");
+  HIP_TRY(c->sig12ws.ensure(cg::tx_sig12_scratch_bytes(n_sigs)), "hipMalloc(signature offsets)");
+  hipStream_t s = stream_of(c, hip_stream);
+  HIP_TRY(order_in(c, s), "hipStreamWaitEvent");
+  HIP_TRY(cg::launch_tx_sig12_bases(d_sigs, 0, n_sigs, 0, (uint64_t*)c->sig12ws.p, s), "launch_tx_sig12_bases");
+  cg::KeyUses uses;
+  uses.sigs12 = d_sigs;
+  uses.n = n_sigs;
+  Packed12 p12;
+  p12.d_sigs = d_sigs;
+  p12.sig_region = sig_bytes_off;
+  p12.sig_bytes_len = sig_bytes_len;
+  p12.d_bases = (const uint64_t*)c->sig12ws.p;
+  HIP_TRY(launch_txsig(c, d_keys, n_keys, d_ids, n_ids, nullptr, n_sigs, tmpls, n_tmpls, d_arena, arena_len, mode,
+                       d_status, s, slot, uses, nullptr, &bounds, &p12),
+          "launch_txsig");
+  HIP_TRY(order_out(c, s), "hipEventRecord");
+  return CG_OK;
+}
+
+int cg_verify_tx_signatures_packed(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const uint8_t* ids, uint64_t n_ids,
+                                   const cg_txsig_packed* sigs, uint64_t n_sigs, const uint8_t* sig_bytes,
+                                   uint64_t sig_bytes_len, const cg_signable_tmpl* tmpls, uint32_t n_tmpls,
+                                   const uint8_t* arena, uint64_t arena_len, uint32_t mode, uint8_t* status_out,
+                                   cg_stats* stats) {
+  const int a = txsig_args("cg_verify_tx_signatures_packed", c, n_keys, keys, n_ids, ids, n_sigs, sigs, status_out,
+                           n_tmpls, tmpls, mode);
+  if (a != CG_OK) return a;
+  if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_verify_tx_signatures_packed: arena is NULL");
+  if (sig_bytes_len && !sig_bytes) return fail(CG_ERR_ARG, "cg_verify_tx_signatures_packed: sig_bytes is NULL");
+  if (n_sigs) memset(status_out, CG_NOT_RUN, n_sigs);
+  if (n_sigs == 0) return CG_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  const int rc = verify_txsig_host_locked(c, keys, n_keys, ids, n_ids, nullptr, n_sigs, tmpls, n_tmpls, arena,
+                                          arena_len, mode, status_out, stats, sigs, sig_bytes, sig_bytes_len);
+  if (rc != CG_OK) memset(status_out, CG_NOT_RUN, n_sigs);
+  return rc;
 }
 
 int cg_verify_tx_signatures(cg_ctx* c, const cg_key* keys, uint32_t n_keys, const uint8_t* ids, uint64_t n_ids,
@@ -1982,6 +2134,51 @@ int cg_pool_verify_transactions(cg_pool* p, const cg_tx* txs, uint64_t n_tx, con
   });
   if (stats) stats->not_run = rc == CG_OK ? 0 : n_sigs;
   return rc;
+}
+
+int cg_pool_verify_tx_signatures_packed(cg_pool* p, const cg_key* keys, uint32_t n_keys, const uint8_t* ids,
+                                        uint64_t n_ids, const cg_txsig_packed* sigs, uint64_t n_sigs,
+                                        const uint8_t* sig_bytes, uint64_t sig_bytes_len,
+                                        const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
+                                        uint64_t arena_len, uint32_t mode, uint8_t* status_out,
+                                        cg_pool_stats* stats) {
+  if (!p) return fail(CG_ERR_ARG, "cg_pool_verify_tx_signatures_packed: pool is NULL");
+  if (p->ctx.empty()) return fail(CG_ERR_ARG, "cg_pool_verify_tx_signatures_packed: empty pool");
+  const int a = txsig_args("cg_pool_verify_tx_signatures_packed", p->ctx[0], n_keys, keys, n_ids, ids, n_sigs, sigs,
+                           status_out, n_tmpls, tmpls, mode);
+  if (a != CG_OK) return a;
+  if (arena_len && !arena) return fail(CG_ERR_ARG, "cg_pool_verify_tx_signatures_packed: arena is NULL");
+  if (sig_bytes_len && !sig_bytes) return fail(CG_ERR_ARG, "cg_pool_verify_tx_signatures_packed: sig_bytes is NULL");
+  // a shard [first, first + count) starts at the stream offset of record `first`: the sum of the spans
+  // before it, in one threaded pass over the table (a prefix per 2^16-record block), looked up per shard
+  const uint64_t B = 1u << 16, nb = (n_sigs + B - 1) / B;
+  std::vector<uint64_t> blk(nb + 1, 0);
+  {
+    const unsigned nt = std::max(1u, std::min<unsigned>(16, (unsigned)nb));
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+      th.emplace_back([&, t] {
+        for (uint64_t b = nb * t / nt; b < nb * (t + 1) / nt; ++b) {
+          uint64_t sp = 0;
+          for (uint64_t i = b * B; i < std::min(n_sigs, (b + 1) * B); ++i) sp += ((uint64_t)sigs[i].sig_len + 3u) & ~(uint64_t)3;
+          blk[b + 1] = sp;
+        }
+      });
+    for (std::thread& x : th) x.join();
+    for (uint64_t b = 0; b < nb; ++b) blk[b + 1] += blk[b];
+  }
+  auto stream_at = [&](uint64_t i) {
+    uint64_t o = blk[i / B];
+    for (uint64_t j = (i / B) * B; j < i; ++j) o += ((uint64_t)sigs[j].sig_len + 3u) & ~(uint64_t)3;
+    return o;
+  };
+  return pool_call(p, n_sigs, status_out, stats, "cg_pool_verify_tx_signatures_packed",
+                   [&](cg_ctx* c, uint64_t first, uint64_t count) {
+                     const uint64_t o = std::min(stream_at(first), sig_bytes_len);
+                     return verify_txsig_host_locked(c, keys, n_keys, ids, n_ids, nullptr, count, tmpls, n_tmpls,
+                                                     arena, arena_len, mode, status_out + first, nullptr, sigs + first,
+                                                     sig_bytes + o, sig_bytes_len - o);
+                   });
 }
 
 int cg_pool_verify_batch(cg_pool* p, const cg_key* keys, uint32_t n_keys, const cg_item* items, uint64_t n_items,

@@ -128,6 +128,7 @@ inline uint32_t chain_spread_lds() {
 // in HBM (sampled on the device) or exact counts (n_keys u32 in HBM, made by the host).
 struct KeyUses {
   const cg_txsig* sigs = nullptr;
+  const cg_txsig_packed* sigs12 = nullptr;  // or the 12-byte table (cg_verify_tx_signatures_packed_device)
   const uint32_t* counts = nullptr;
   uint64_t n = 0;  // signatures the counts cover (sizes the wide pools)
   // optional host copies of the key table and of `counts` (the host-buffer tx-signature path): the
@@ -277,6 +278,23 @@ hipError_t launch_tx_sig_range(const cg_txsig* d_sigs, uint64_t first, uint64_t 
                                uint32_t n_tmpls, const uint8_t* d_tx_status, uint64_t n_tx, const uint8_t* d_ids,
                                uint64_t arena_len, uint64_t slot, cg_item* d_items, uint8_t* d_msgs,
                                hipStream_t stream);
+
+// The 12-byte signature table (cg_txsig_packed): records [first, first + n) become verify items like
+// launch_tx_sig_range's, each signature's offset recovered by a prefix scan of round_up(sig_len, 4):
+// per 256-record block sums, an exclusive scan of those, then each block's own scan in the item kernel.
+// Signature j sits at sig_region + (offset of j in the signature stream) in the arena; one that runs
+// past sig_bytes_len of the stream gets CG_NOT_RUN. Either
+// `d_bases` holds the stream offset of every 256-record block of the whole table (tx_sig12_bases over
+// [0, n_all); `first` must then be a multiple of 256), or the range's blocks are summed and scanned
+// here, starting at stream offset `base`, into d_scratch (tx_sig12_scratch_bytes(n) bytes).
+size_t tx_sig12_scratch_bytes(uint64_t n);
+hipError_t launch_tx_sig12_bases(const cg_txsig_packed* d_sigs, uint64_t first, uint64_t n, uint64_t base,
+                                 uint64_t* d_bases, hipStream_t stream);
+hipError_t launch_tx_sig12_range(const cg_txsig_packed* d_sigs, uint64_t first, uint64_t n, uint64_t sig_region,
+                                 uint64_t sig_bytes_len, uint64_t base, const uint64_t* d_bases,
+                                 const cg_signable_tmpl* d_tmpls,
+                                 uint32_t n_tmpls, uint64_t n_tx, uint64_t arena_len, cg_item* d_items,
+                                 void* d_scratch, hipStream_t stream);
 
 // Merkle roots over independent leaf lists.
 hipError_t launch_merkle_roots(const uint8_t* d_leaves, const uint64_t* d_first, const uint32_t* d_count,

@@ -59,7 +59,8 @@ __global__ void __launch_bounds__(256) k_key_uses(const cg_item* __restrict__ it
 
 // The same, from a cg_txsig table (cg_verify_tx_signatures_device: the key tables are sized before
 // any verify item exists, so the per-chunk item builds and splices can follow them).
-__global__ void __launch_bounds__(256) k_key_uses_txsig(const cg_txsig* __restrict__ sigs, uint64_t n,
+template <class Sig>
+__global__ void __launch_bounds__(256) k_key_uses_txsig(const Sig* __restrict__ sigs, uint64_t n,
                                                         uint32_t n_keys, uint32_t* __restrict__ uses,
                                                         uint8_t* __restrict__ seen) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -298,8 +299,11 @@ hipError_t launch_keyprep(const cg_key* d_keys, uint32_t n_keys, const uint8_t* 
     hipLaunchKernelGGL(k_key_counts, dim3((n_keys + 255) / 256), dim3(256), 0, stream, src->counts, n_keys, w.uses,
                        w.seen);
   else if (src && src->sigs && src->n)
-    hipLaunchKernelGGL(k_key_uses_txsig, dim3((unsigned)((src->n + 255) / 256)), dim3(256), 0, stream, src->sigs,
-                       src->n, n_keys, w.uses, w.seen);
+    hipLaunchKernelGGL(k_key_uses_txsig<cg_txsig>, dim3((unsigned)((src->n + 255) / 256)), dim3(256), 0, stream,
+                       src->sigs, src->n, n_keys, w.uses, w.seen);
+  else if (src && src->sigs12 && src->n)
+    hipLaunchKernelGGL(k_key_uses_txsig<cg_txsig_packed>, dim3((unsigned)((src->n + 255) / 256)), dim3(256), 0,
+                       stream, src->sigs12, src->n, n_keys, w.uses, w.seen);
   static const bool serial = [] {  // CG_SERIAL_KEYPREP=1: key prep on the caller's stream (A/B runs)
     const char* v = getenv("CG_SERIAL_KEYPREP");
     return v && v[0] == '1';

@@ -206,6 +206,29 @@ class Engine:
         self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_stats._fields_}
         return st
 
+    def verify_tx_signatures_packed(self, pb, mode=MODE_DOVERIFY):
+        """cg_verify_tx_signatures_packed: ``pb`` a batch.PackedTxSigBatch (the 12-byte table and the
+        dense signature stream). One status byte per signature; cg_stats in last_stats."""
+        st = np.full(pb.n, 255, dtype=np.uint8)
+        stats = _lib.cg_stats()
+        rc = _lib.lib().cg_verify_tx_signatures_packed(self._h, _p(pb.keys), len(pb.keys), _p(pb.ids), pb.n_ids,
+                                                       _p(pb.sigs), pb.n, _p(pb.stream), pb.stream.size, _p(pb.tmpls),
+                                                       len(pb.tmpls), _p(pb.arena), pb.arena.size, mode, _p(st),
+                                                       ctypes.byref(stats))
+        _lib.check(rc, "cg_verify_tx_signatures_packed")
+        self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_stats._fields_}
+        return st
+
+    def verify_tx_signatures_packed_device(self, d_keys, n_keys, d_ids, n_ids, d_sigs, n_sigs, sig_bytes_off,
+                                           sig_bytes_len, tmpls, d_arena, arena_len, d_status, mode=MODE_DOVERIFY,
+                                           stream=0):
+        """Asynchronous device form: the signature stream at d_arena[sig_bytes_off, + sig_bytes_len)."""
+        assert tmpls.dtype == TMPL_DTYPE
+        rc = _lib.lib().cg_verify_tx_signatures_packed_device(self._h, d_keys, n_keys, d_ids, n_ids, d_sigs, n_sigs,
+                                                              sig_bytes_off, sig_bytes_len, _p(tmpls), len(tmpls),
+                                                              d_arena, arena_len, mode, d_status, stream or None)
+        _lib.check(rc, "cg_verify_tx_signatures_packed_device")
+
     def verify_tx_signatures_device(self, d_keys, n_keys, d_ids, n_ids, d_sigs, n_sigs, tmpls, d_arena, arena_len,
                                     d_status, mode=MODE_DOVERIFY, stream=0):
         """Asynchronous device form; `tmpls` is a host TMPL_DTYPE array (template bytes in the arena)."""
@@ -275,6 +298,19 @@ class EnginePool:
         self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_pool_stats._fields_ if k != "reserved"}
         if rc != 0 and not allow_partial:
             _lib.check(rc, "cg_pool_verify_tx_signatures")
+        return st
+
+    def verify_tx_signatures_packed(self, pb, mode=MODE_DOVERIFY, allow_partial=False):
+        """cg_pool_verify_tx_signatures_packed: the 12-byte table sharded over the healthy slots."""
+        st = np.full(pb.n, 255, dtype=np.uint8)
+        stats = _lib.cg_pool_stats()
+        rc = _lib.lib().cg_pool_verify_tx_signatures_packed(self._h, _p(pb.keys), len(pb.keys), _p(pb.ids), pb.n_ids,
+                                                            _p(pb.sigs), pb.n, _p(pb.stream), pb.stream.size,
+                                                            _p(pb.tmpls), len(pb.tmpls), _p(pb.arena), pb.arena.size,
+                                                            mode, _p(st), ctypes.byref(stats))
+        self.last_stats = {k: getattr(stats, k) for k, _ in _lib.cg_pool_stats._fields_ if k != "reserved"}
+        if rc != 0 and not allow_partial:
+            _lib.check(rc, "cg_pool_verify_tx_signatures_packed")
         return st
 
     def verify_transactions(self, txs, comps, keys, sigs, tmpls, arena, mode=MODE_DOVERIFY, allow_partial=False):

@@ -366,6 +366,37 @@ int cg_verify_tx_signatures_device(cg_ctx* ctx, const cg_key* d_keys, uint32_t n
                                    const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* d_arena,
                                    uint64_t arena_len, uint32_t mode, uint8_t* d_status, void* hip_stream);
 
+/* ---- The same call with a 12-byte signature table (round 6, VERDICT r5 item 4: the 24-byte cg_txsig
+ * was 300 MB of the 1.21 GB a BASELINE configs[4] shard ships over PCIe per call). A signature's bytes
+ * are not addressed by an offset: the caller writes the signatures back to back in table order into
+ * their own buffer, each starting at a 4-byte boundary (what a JVM writer appending to a direct
+ * ByteBuffer does):
+ *   signature i = sig_bytes[o_i .. o_i + sig_len_i),  o_0 = 0,  o_{i+1} = o_i + round_up(sig_len_i, 4)
+ * The engine recovers the o_i with a prefix scan on the device. A signature whose bytes run past
+ * sig_bytes_len gets CG_NOT_RUN; every other rule (ids, templates, the 16-bit surrogate for longer
+ * JVM signatures, statuses, stats) is cg_verify_tx_signatures'. `arena` holds the key and template
+ * bytes only. */
+typedef struct cg_txsig_packed {
+  uint32_t tx_idx;     /* transaction whose id is signed (index into ids) */
+  uint32_t key_idx;    /* TransactionSignature.by, index into the cg_key table */
+  uint16_t sig_len;
+  uint16_t tmpl;       /* SignatureMetadata template index */
+} cg_txsig_packed;     /* 12 bytes */
+
+int cg_verify_tx_signatures_packed(cg_ctx* ctx, const cg_key* keys, uint32_t n_keys, const uint8_t* ids,
+                                   uint64_t n_ids, const cg_txsig_packed* sigs, uint64_t n_sigs,
+                                   const uint8_t* sig_bytes, uint64_t sig_bytes_len, const cg_signable_tmpl* tmpls,
+                                   uint32_t n_tmpls, const uint8_t* arena, uint64_t arena_len, uint32_t mode,
+                                   uint8_t* status_out, cg_stats* stats_opt);
+/* Device buffers in HBM except `tmpls`; asynchronous on hip_stream. The signature stream lies inside
+ * the arena: d_arena[sig_bytes_off .. sig_bytes_off + sig_bytes_len) (one HBM buffer holding the key
+ * and template bytes and the stream: nothing is copied). */
+int cg_verify_tx_signatures_packed_device(cg_ctx* ctx, const cg_key* d_keys, uint32_t n_keys, const uint8_t* d_ids,
+                                          uint64_t n_ids, const cg_txsig_packed* d_sigs, uint64_t n_sigs,
+                                          uint64_t sig_bytes_off, uint64_t sig_bytes_len,
+                                          const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* d_arena,
+                                          uint64_t arena_len, uint32_t mode, uint8_t* d_status, void* hip_stream);
+
 /* ---- Tear-offs: FilteredTransaction.verify / PartialMerkleTree.verify.
  * Replaces, for a batch of filtered transactions (the non-validating notary's input,
  * NonValidatingNotaryFlow.kt:22-27), the serial
@@ -459,6 +490,14 @@ int cg_pool_verify_transactions(cg_pool* pool, const cg_tx* txs, uint64_t n_tx, 
                                 uint64_t n_sigs, const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
                                 uint64_t arena_len, uint32_t mode, uint8_t* ids_out, uint8_t* tx_status_out,
                                 uint8_t* sig_status_out, cg_pool_stats* stats_opt);
+/* cg_verify_tx_signatures_packed sharded the same way (each shard's signature bytes start where the
+ * previous shard's end: the library sums the lengths at the shard bounds). */
+int cg_pool_verify_tx_signatures_packed(cg_pool* pool, const cg_key* keys, uint32_t n_keys, const uint8_t* ids,
+                                        uint64_t n_ids, const cg_txsig_packed* sigs, uint64_t n_sigs,
+                                        const uint8_t* sig_bytes, uint64_t sig_bytes_len,
+                                        const cg_signable_tmpl* tmpls, uint32_t n_tmpls, const uint8_t* arena,
+                                        uint64_t arena_len, uint32_t mode, uint8_t* status_out,
+                                        cg_pool_stats* stats_opt);
 /* Failure drill: make every later call on `slot` fail as a device fault would (fail = 1), or
  * clear it and mark the slot healthy again (fail = 0). For tests and operational drills. */
 int cg_pool_inject_fault(cg_pool* pool, uint32_t slot, int fail);

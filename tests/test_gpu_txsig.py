@@ -308,3 +308,109 @@ def test_skipped_modes_are_reported_not_run():
             assert o["not_run"] > 0 and o["not_run"] + o["oracle"] == o["n"], out
         else:
             assert out["other"]["oracle"] == out["other"]["n"], out
+
+
+# ---- round 6: the 12-byte signature table over a dense signature stream (cg_txsig_packed,
+# VERDICT r5 item 4). Every verdict equals the 24-byte form's on the same signatures.
+def test_packed_host_device_pool_vs_oracle(spool):
+    import torch
+    from corda_amd.engine import Engine, EnginePool
+    from tools.workload import wl
+    b, labels, schemes, ids, id_idx, ref = spool
+    idx = np.random.default_rng(61).integers(0, b.n, 150_000)
+    tb = wl.tx_sig_stream(b, schemes, idx, ids, id_idx, nthreads=16)
+    pb = tb.packed()
+    assert np.shares_memory(pb.stream, tb.arena)  # the generator's tail is already the dense stream
+    assert pb.h2d_bytes < tb.arena.size + tb.sigs.nbytes + tb.ids.nbytes + tb.keys.nbytes - 11 * tb.n
+    for chunk in (0, 40_001):
+        with Engine(0, chunk_items=chunk) as eng:
+            st = eng.verify_tx_signatures_packed(pb)
+            assert np.array_equal(st, ref[idx]), f"packed host (chunk {chunk}): {np.count_nonzero(st != ref[idx])}"
+            # device form: the stream inside the one HBM arena (tb.arena = head || stream)
+            dev = torch.device("cuda", 0)
+            up = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).to(dev)  # noqa: E731
+            kd, ijd, sgd, ad = up(pb.keys), up(pb.ids), up(pb.sigs), up(tb.arena)
+            sd = torch.full((pb.n,), 255, dtype=torch.uint8, device=dev)
+            eng.verify_tx_signatures_packed_device(kd.data_ptr(), len(pb.keys), ijd.data_ptr(), pb.n_ids,
+                                                   sgd.data_ptr(), pb.n, pb.arena.size, pb.stream.size, pb.tmpls,
+                                                   ad.data_ptr(), tb.arena.size, sd.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(sd.cpu().numpy(), ref[idx]), "packed device"
+    with EnginePool([0, 0], chunk_items=30000) as ep:
+        assert np.array_equal(ep.verify_tx_signatures_packed(pb), ref[idx])
+        assert ep.last_stats["shards"] == 2
+        ep.inject_fault(1)
+        assert np.array_equal(ep.verify_tx_signatures_packed(pb), ref[idx])
+        assert ep.last_stats["reruns"] == 1
+
+
+def test_packed_edges():
+    """The 24-byte form's edge cases through the 12-byte table: out-of-range id / template -> NOT_RUN,
+    odd template lengths, isValid mode, an empty call; plus the packed form's own: signature bytes
+    gathered from an interleaved arena, a stream cut short (the signatures past its end NOT_RUN, the
+    rest unchanged), a key outside the caller's arena (as in the 24-byte form), and a JVM signature
+    longer than 65 535 bytes through its surrogate."""
+    from corda_amd.batch import TxSigBuilder
+    from corda_amd.engine import Engine
+    import golden_io
+    items = [it for it in golden_io.load("ed25519.json") if it["expect"] in ("VALID", "INVALID")][:6]
+    ec = [it for it in golden_io.load("ecdsa.json") if it["expect"] in ("VALID", "INVALID")][:6]
+    rng = np.random.default_rng(18)
+    bld = TxSigBuilder()
+    tx = [bld.tx_id(rng.integers(0, 256, 32, dtype=np.uint8).tobytes()) for _ in range(3)]
+    tm = [bld.template(b"\x01\x02\x03", b""), bld.template(b"", b"\xfe" * 7), bld.template(b"p" * 233, b"s" * 5)]
+    for j in range(90):
+        if j % 3 == 2:  # ECDSA, DER of 70-72 bytes: the stream's spans are not all 64
+            it = ec[j % len(ec)]
+            k = bld.key(it["scheme"], it["key_fmt"], bytes.fromhex(it["key"]))
+            bld.add_signature(k, tx[j % 3], tm[j % 3], bytes.fromhex(ec[(j * 5) % len(ec)]["sig"]))
+        else:
+            k = bld.key(4, 0, bytes.fromhex(items[j % len(items)]["key"]))
+            bld.add_signature(k, tx[j % 3], tm[j % 3], bytes.fromhex(items[(j * 7) % len(items)]["sig"]))
+        if j == 40:  # a signature past the 16-bit length: packed as its surrogate
+            bld.add_signature(k, tx[0], tm[0], b"\x30" + bytes(70000))
+    tb = bld.build()
+    tb.sigs[5]["tx_idx"] = 99
+    tb.sigs[6]["tmpl"] = 40
+    pb = tb.packed()
+    assert not np.shares_memory(pb.stream, tb.arena)  # templates interleave: the bytes were gathered
+    with Engine(0) as eng:
+        for mode in (B.MODE_DOVERIFY, B.MODE_ISVALID):
+            want = eng.verify_tx_signatures(tb, mode)
+            assert np.array_equal(want, c_oracle.verify_batch(txsig_util.to_message_batch(tb), mode, 4))
+            st = eng.verify_tx_signatures_packed(pb, mode)
+            assert st[5] == B.NOT_RUN and st[6] == B.NOT_RUN
+            assert np.array_equal(st, want)
+        # the stream cut inside signature 70: it and every later one NOT_RUN, the rest as before
+        span = (pb.sigs["sig_len"].astype(np.int64) + 3) & ~3
+        o70 = int(span[:70].sum())
+        short = B.PackedTxSigBatch(pb.keys, pb.ids, pb.sigs, pb.stream[:o70 + 10], pb.tmpls, pb.arena)
+        st = eng.verify_tx_signatures_packed(short)
+        assert np.all(st[70:] == B.NOT_RUN) and np.array_equal(st[:70], want[:70])
+        # a key outside the caller's arena: the 24-byte form's verdicts for that key's signatures
+        keys = pb.keys.copy()
+        keys[1]["off"] = pb.arena.size + 8  # would land inside the stream on the device
+        st = eng.verify_tx_signatures_packed(B.PackedTxSigBatch(keys, pb.ids, pb.sigs, pb.stream, pb.tmpls, pb.arena))
+        keys24 = tb.keys.copy()
+        keys24[1]["off"] = tb.arena.size + 8
+        want_k = eng.verify_tx_signatures(B.TxSigBatch(keys24, tb.ids, tb.sigs, tb.tmpls, tb.arena))
+        assert np.array_equal(st, want_k)
+        assert np.any(st[pb.sigs["key_idx"] == 1] != want[pb.sigs["key_idx"] == 1])
+        empty = B.PackedTxSigBatch(pb.keys, pb.ids, pb.sigs[:0], pb.stream[:0], pb.tmpls, pb.arena)
+        assert eng.verify_tx_signatures_packed(empty).size == 0
+
+
+def test_packed_8m_one_call(spool):
+    """The configs[4]-shaped call (> 8M signatures, one call) through the 12-byte table: idempotence
+    against the oracle's pool verdicts, as test_tx_signatures_8m_one_call."""
+    from corda_amd.engine import Engine
+    from tools.workload import wl
+    b, labels, schemes, ids, id_idx, ref = spool
+    n = 8_400_000
+    idx = np.random.default_rng(22).integers(0, b.n, n)
+    pb = wl.tx_sig_stream(b, schemes, idx, ids, id_idx, nthreads=16).packed()
+    with Engine(0) as eng:
+        st = eng.verify_tx_signatures_packed(pb)
+    assert not np.any(st == B.NOT_RUN)
+    bad = np.nonzero(st != ref[idx])[0]
+    assert bad.size == 0, f"{bad.size} of {n} verdicts differ"

@@ -36,8 +36,12 @@ typedef int64_t ec9_acc;
 // signed 32 x 32 -> 64 term (v_mad_i64_i32 when accumulated)
 CG_HD ec9_acc ec9_t(uint32_t a, uint32_t b) { return (ec9_acc)((int64_t)(int32_t)a * (int64_t)(int32_t)b); }
 
-// opaque copies: in a ladder loop the compiler otherwise widens loop-carried limb differences to
-// 64 bits and multiplies 64 x 64 (fe9.h saw +40% VALU from it)
+// opaque copies (round 5: every product pinned copies of its operands, because in a ladder loop the
+// compiler had widened loop-carried limb differences to 64 bits, as fe9.h saw). Round 6: the copies
+// cost a v_mov per limb whenever the operand stayed live (~110 per addition) and hid a square's
+// symmetry from the compiler; the products read their operands directly (EC9_PIN_COPIES restores the
+// copies for A/B: 329.9 vs 334.8 M sigs/s over 3 pairs, profiles/r06/ec_acc) and the ISA shows no
+// 64 x 64 multiply (tools/microbench/ec9_probe.hip)
 CG_HD void ec9_pin(f29& o, const f29& a) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
@@ -46,6 +50,28 @@ CG_HD void ec9_pin(f29& o, const f29& a) {
     asm volatile("" : "+v"(o.v[i]));
 #endif
   }
+}
+
+// EC9_PIN_ACC (round 6, default 1): the running column sum made opaque after each term, so a
+// column's chain starts from the carry instead of being summed from 0 and joined by a separate 64-bit
+// add (fe9.h's FE9_PIN_ACC, adopted for the Ed25519 ladder in round 4); secp256k1's low columns then
+// run after the high ones as one chain with the fold terms first. Per addition 1790 -> 1661 (r1) /
+// 1786 -> 1657 (k1) static VALU (tools/microbench/ec9_probe.hip), ~1000 hazard s_nop 0 the other
+// waves fill; headline A/B over 3 pairs 334.8 -> 341.7 M sigs/s, r1 ladder 7.44 -> 7.14, k1 3.38 ->
+// 3.12 ms per step (profiles/r06/ec_acc). 0: the independent column sums (A/B).
+#ifndef EC9_PIN_ACC
+#define EC9_PIN_ACC 1
+#endif
+// EC9_SQR=1: squares as 45 MACs against a doubled copy (ec9_col); 0: as general products (A/B)
+#ifndef EC9_SQR
+#define EC9_SQR 1
+#endif
+CG_HD void ec9_opaque(ec9_acc& x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (EC9_PIN_ACC) asm volatile("" : "+v"(x));
+#else
+  (void)x;
+#endif
 }
 
 CG_HD void ec9_add(f29& r, const f29& a, const f29& b) {
@@ -61,11 +87,31 @@ CG_HD void ec9_neg(f29& r, const f29& a) {
   for (int i = 0; i < 9; ++i) r.v[i] = 0u - a.v[i];
 }
 
+// Column k's product terms (i + j = k, 0 <= i, j < 9) of a b (+ c d), added to acc. Sq: a b is a
+// square, b = 2a (the caller's doubled copy): each pair i < j once as a_i (2 a_j), plus a_i^2 on
+// the diagonal -- 45 MACs instead of 81 (|2 a_j| < 2^31 for every limb class of ec9.h).
+template <bool Two, bool Sq>
+CG_HD void ec9_col(ec9_acc& acc, int k, const f29& a, const f29& b, const f29& c, const f29& d) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int j = k - i;
+    if (j < 0 || j > 8) continue;
+    if (Sq && i > j) continue;
+    acc += Sq && i == j ? ec9_t(a.v[i], a.v[i]) : ec9_t(a.v[i], b.v[j]);
+    ec9_opaque(acc);
+    if (Two) {
+      acc += ec9_t(c.v[i], d.v[j]);
+      ec9_opaque(acc);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- secp256r1: Montgomery
-template <bool Two, bool Add>
+template <bool Two, bool Add, bool Sq = false>
 CG_HD void ec9_mul_r1(f29& out, const f29& a0, const f29& b0, const f29& c0, const f29& d0, const f29& e) {
   constexpr uint32_t P7 = m29_limb(1, 0, 1, 7), P8 = m29_limb(1, 0, 1, 8);
   const uint32_t k9 = m29_opaque(1u << 9), k18 = m29_opaque(1u << 18);  // MACs, not shift pairs
+#ifdef EC9_PIN_COPIES
   f29 a, b, c, d;
   ec9_pin(a, a0);
   ec9_pin(b, b0);
@@ -73,17 +119,14 @@ CG_HD void ec9_mul_r1(f29& out, const f29& a0, const f29& b0, const f29& c0, con
     ec9_pin(c, c0);
     ec9_pin(d, d0);
   }
+#else
+  const f29 &a = a0, &b = b0, &c = c0, &d = d0;
+#endif
   uint32_t q[9];
   ec9_acc acc = 0;
 #pragma unroll
   for (int k = 0; k < 17; ++k) {
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int j = k - i;
-      if (j < 0 || j > 8) continue;
-      acc += ec9_t(a.v[i], b.v[j]);
-      if (Two) acc += ec9_t(c.v[i], d.v[j]);
-    }
+    ec9_col<Two, Sq>(acc, k, a, b, c, d);
 #pragma unroll
     for (int i = 0; i < 9; ++i) {  // q p = q (2^96 - 1 + 2^192 + p7 2^203 + p8 2^232) (mont29.h)
       const int j = k - i;
@@ -92,6 +135,7 @@ CG_HD void ec9_mul_r1(f29& out, const f29& a0, const f29& b0, const f29& c0, con
       if (j == 6) acc += ec9_t(q[i], k18);
       if (j == 7) acc += ec9_t(q[i], P7);
       if (j == 8) acc += ec9_t(q[i], P8);
+      if (j == 3 || j >= 6) ec9_opaque(acc);
     }
     if (Add && k >= 9) acc += (ec9_acc)(int32_t)e.v[k - 9];
     EC9_CHK(acc);
@@ -105,9 +149,10 @@ CG_HD void ec9_mul_r1(f29& out, const f29& a0, const f29& b0, const f29& c0, con
 }
 
 // ---------------------------------------------------------------- secp256k1: plain form, folded
-template <bool Two, bool Add>
+template <bool Two, bool Add, bool Sq = false>
 CG_HD void ec9_mul_k1(f29& out, const f29& a0, const f29& b0, const f29& c0, const f29& d0, const f29& e) {
   const uint32_t k31264 = m29_opaque(31264u), k256 = m29_opaque(256u);
+#ifdef EC9_PIN_COPIES
   f29 a, b, c, d;
   ec9_pin(a, a0);
   ec9_pin(b, b0);
@@ -115,26 +160,23 @@ CG_HD void ec9_mul_k1(f29& out, const f29& a0, const f29& b0, const f29& c0, con
     ec9_pin(c, c0);
     ec9_pin(d, d0);
   }
+#else
+  const f29 &a = a0, &b = b0, &c = c0, &d = d0;
+#endif
+#if !EC9_PIN_ACC
   ec9_acc col[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
     ec9_acc s = Add ? (ec9_acc)(int32_t)e.v[k] : 0;
-#pragma unroll
-    for (int i = 0; i <= k; ++i) {
-      s += ec9_t(a.v[i], b.v[k - i]);
-      if (Two) s += ec9_t(c.v[i], d.v[k - i]);
-    }
+    ec9_col<Two, Sq>(s, k, a, b, c, d);
     col[k] = s;
   }
+#endif
   uint32_t H[8];
   ec9_acc acc = 0;
 #pragma unroll
   for (int k = 9; k < 17; ++k) {
-#pragma unroll
-    for (int i = k - 8; i < 9; ++i) {
-      acc += ec9_t(a.v[i], b.v[k - i]);
-      if (Two) acc += ec9_t(c.v[i], d.v[k - i]);
-    }
+    ec9_col<Two, Sq>(acc, k, a, b, c, d);
     EC9_CHK(acc);
     H[k - 9] = (uint32_t)acc & M29_MASK;
     acc >>= 29;
@@ -142,13 +184,31 @@ CG_HD void ec9_mul_k1(f29& out, const f29& a0, const f29& b0, const f29& c0, con
   FE_ASSERT(acc > -((ec9_acc)1 << 31) && acc < ((ec9_acc)1 << 31));
   const uint32_t H8 = (uint32_t)(int32_t)acc;
   // H_m 2^{29 m} 2^261 = H_m 31264 (column m) + H_m 2^8 (column m + 1)
+  uint32_t M[9];
+#if EC9_PIN_ACC
+  // the low columns after the high ones: one chain from the carry, the fold terms and e first
+  acc = 0;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    if (Add) acc += (ec9_acc)(int32_t)e.v[j];
+    acc += ec9_t(j < 8 ? H[j] : H8, k31264);
+    ec9_opaque(acc);
+    if (j >= 1) {
+      acc += ec9_t(H[j - 1], k256);
+      ec9_opaque(acc);
+    }
+    ec9_col<Two, Sq>(acc, j, a, b, c, d);
+    EC9_CHK(acc);
+    M[j] = (uint32_t)acc & M29_MASK;
+    acc >>= 29;
+  }
+#else
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
     col[m] += ec9_t(H[m], k31264);
     col[m + 1] += ec9_t(H[m], k256);
   }
   col[8] += ec9_t(H8, k31264);
-  uint32_t M[9];
   acc = 0;
 #pragma unroll
   for (int j = 0; j < 9; ++j) {
@@ -157,6 +217,7 @@ CG_HD void ec9_mul_k1(f29& out, const f29& a0, const f29& b0, const f29& c0, con
     M[j] = (uint32_t)acc & M29_MASK;
     acc >>= 29;
   }
+#endif
   // top (weight 2^261) = acc + H8 2^8, folded as (2^37 + 31264) at its 32-bit halves
   const ec9_acc top = acc + (ec9_acc)(int32_t)H8 * 256;
   FE_ASSERT(top > -((ec9_acc)1 << 40) && top < ((ec9_acc)1 << 40));
@@ -184,6 +245,32 @@ CG_HD void ec9_mul_add(f29& out, const f29& a, const f29& b, const f29& e) {
   M29_COUNT(C, 0);
   if (C == CG_CURVE_R1) ec9_mul_r1<false, true>(out, a, b, a, b, e);
   else ec9_mul_k1<false, true>(out, a, b, a, b, e);
+}
+// a^2 (+ e): the pairs i < j once against a doubled copy (ec9_col)
+template <int C, bool Add>
+CG_HD void ec9_sqr_impl(f29& out, const f29& a, const f29& e) {
+  M29_COUNT(C, 0);
+  f29 a2;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) a2.v[i] = a.v[i] << 1;
+  if (C == CG_CURVE_R1) ec9_mul_r1<false, Add, true>(out, a, a2, a, a, e);
+  else ec9_mul_k1<false, Add, true>(out, a, a2, a, a, e);
+}
+template <int C>
+CG_HD void ec9_sqr(f29& out, const f29& a) {
+#if EC9_SQR
+  ec9_sqr_impl<C, false>(out, a, a);
+#else
+  ec9_mul<C>(out, a, a);
+#endif
+}
+template <int C>
+CG_HD void ec9_sqr_add(f29& out, const f29& a, const f29& e) {
+#if EC9_SQR
+  ec9_sqr_impl<C, true>(out, a, e);
+#else
+  ec9_mul_add<C>(out, a, a, e);
+#endif
 }
 // a b + c d, one reduction
 template <int C>
@@ -272,7 +359,7 @@ CG_HD void jac_madd9(Jac& r, bool& inf, const f29& x2, const f29& y2, bool neg, 
     return;
   }
   f29 Z1Z1, U2, ys, S2, H;
-  ec9_mul<C>(Z1Z1, r.Z, r.Z);
+  ec9_sqr<C>(Z1Z1, r.Z);
   ec9_mul<C>(U2, x2, Z1Z1);
 #pragma unroll
   for (int i = 0; i < 9; ++i) ys.v[i] = neg ? 0u - y2.v[i] : y2.v[i];  // S2 = +-y2 Z1^3
@@ -292,13 +379,13 @@ CG_HD void jac_madd9(Jac& r, bool& inf, const f29& x2, const f29& y2, bool neg, 
 #endif
   f29 rr, HH, HHH, V, E, t, nY;
   ec9_sub(rr, S2, r.Y);
-  ec9_mul<C>(HH, H, H);
+  ec9_sqr<C>(HH, H);
   ec9_mul<C>(HHH, H, HH);
   ec9_mul<C>(V, r.X, HH);
 #pragma unroll
   for (int i = 0; i < 9; ++i) E.v[i] = 0u - HHH.v[i] - 2u * V.v[i];  // X3 = rr^2 - HHH - 2V
   Jac o;
-  ec9_mul_add<C>(o.X, rr, rr, E);
+  ec9_sqr_add<C>(o.X, rr, E);
   ec9_sub(t, V, o.X);
   ec9_neg(nY, r.Y);
   ec9_mul2<C>(o.Y, rr, t, nY, HHH);  // Y3 = rr (V - X3) - Y1 HHH

@@ -182,7 +182,10 @@ CG_HD void fe9_mul(fe9& out, const fe9& a, const fe9& b) {
   FE_ASSERT(acc >= 0 && T < (1ull << 35));
 #else
   typedef typename std::conditional<Signed, int64_t, uint64_t>::type acc_t;
-#if defined(__HIP_DEVICE_COMPILE__)
+#ifndef FE9_PIN_COPIES
+#define FE9_PIN_COPIES 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && FE9_PIN_COPIES
   // opaque 32-bit operands: in the ladder loop the compiler otherwise widened loop-carried
   // differences to 64 bits and emitted 64 x 64-bit multiplies (3 MACs + moves each)
   fe9 a_, b_;
@@ -251,7 +254,7 @@ CG_HD void fe9_mul(fe9& out, const fe9& a, const fe9& b) {
     }
   }
   const uint64_t T = (uint64_t)acc;
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && FE9_PIN_COPIES
 #undef a
 #undef b
 #endif

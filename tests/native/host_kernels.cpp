@@ -1017,11 +1017,15 @@ extern "C" void t_ec9_mul(int curve, int form, const uint32_t* a, const uint32_t
   if (curve == 1) {
     if (form == 0) ec9_mul<CG_CURVE_R1>(R, A, B);
     else if (form == 1) ec9_mul_add<CG_CURVE_R1>(R, A, B, Cc);
-    else ec9_mul2<CG_CURVE_R1>(R, A, B, Cc, D);
+    else if (form == 2) ec9_mul2<CG_CURVE_R1>(R, A, B, Cc, D);
+    else if (form == 3) ec9_sqr<CG_CURVE_R1>(R, A);
+    else ec9_sqr_add<CG_CURVE_R1>(R, A, Cc);
   } else {
     if (form == 0) ec9_mul<CG_CURVE_K1>(R, A, B);
     else if (form == 1) ec9_mul_add<CG_CURVE_K1>(R, A, B, Cc);
-    else ec9_mul2<CG_CURVE_K1>(R, A, B, Cc, D);
+    else if (form == 2) ec9_mul2<CG_CURVE_K1>(R, A, B, Cc, D);
+    else if (form == 3) ec9_sqr<CG_CURVE_K1>(R, A);
+    else ec9_sqr_add<CG_CURVE_K1>(R, A, Cc);
   }
   memcpy(out, R.v, 36);
 }

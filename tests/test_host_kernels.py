@@ -508,3 +508,54 @@ def test_row_build_parked_matches_row_build(family):
     lib.t_row_parked_cmp.argtypes = [ctypes.c_int, ctypes.c_uint32]
     for m in (1, 2, 3, 7, 255, 65537, 0x7fffffff):
         assert lib.t_row_parked_cmp(family, m) == 0, m
+
+
+@pytest.mark.parametrize("curve", [0, 1])
+def test_ec9_product_forms_vs_big_integers(curve):
+    """ec9.h's five product forms (a b, a b + e, a b + c d, and round 6's squares a^2 and a^2 + e over
+    a doubled copy) against Python integers, on the operand classes jac_madd9 feeds them: tight
+    values T (digits 0..7 in [0, 2^29), the rest in the top limb; up to 6p, digits all 2^29 - 1 at the
+    extreme), differences S = T - T limb by limb, and e = -T - 2T (X3's E); every column bound
+    asserted (FE_BOUNDS_CHECK). secp256r1 is Montgomery (R = 2^261: the product carries R^-1),
+    secp256k1 plain."""
+    lib = hostk.lib()
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    lib.t_ec9_mul.argtypes = [ctypes.c_int, ctypes.c_int, u32p, u32p, u32p, u32p, u32p]
+    p = 2 ** 256 - 2 ** 32 - 977 if curve == 0 else 2 ** 256 - 2 ** 224 + 2 ** 192 + 2 ** 96 - 1
+    rinv = pow(2 ** 261, -1, p) if curve == 1 else 1
+    rng = random.Random(90 + curve)
+    M = (1 << 29) - 1
+
+    def tight(v):
+        return [(v >> (29 * i)) & M for i in range(8)] + [v >> 232]
+
+    def t_val(kind):
+        if kind == "max":  # every digit 2^29 - 1, the top at the class bound
+            return tight(((6 * p) >> 232 << 232) | ((1 << 232) - 1))
+        return tight(rng.randrange(6 * p))
+
+    def operand(kind):
+        t = t_val(kind)
+        if rng.random() < 0.5:
+            return t
+        u = t_val("rand" if kind == "max" else kind)
+        return [x - y for x, y in zip(t if kind != "max" else [0] * 9, u if kind != "max" else t)]
+
+    def arr(v):
+        return (ctypes.c_uint32 * 9)(*[x & 0xFFFFFFFF for x in v])
+
+    def val(v):
+        return sum(x << (29 * i) for i, x in enumerate(v))
+
+    out = (ctypes.c_uint32 * 9)()
+    for it in range(60):
+        kind = "max" if it < 6 else "rand"
+        a, b, c, d = operand(kind), operand(kind), operand(kind), operand(kind)
+        h, w = t_val(kind), t_val(kind)
+        e = [-x - 2 * y for x, y in zip(h, w)]
+        A, B, C, D, E = val(a), val(b), val(c), val(d), val(e)
+        for form, want in ((0, A * B * rinv), (1, A * B * rinv + E), (2, (A * B + C * D) * rinv),
+                           (3, A * A * rinv), (4, A * A * rinv + E)):
+            lib.t_ec9_mul(curve, form, arr(a), arr(b), arr(e if form in (1, 4) else c), arr(d), out)
+            got = val([ctypes.c_int32(x).value for x in out])
+            assert (got - want) % p == 0, (curve, form, it)

@@ -124,10 +124,15 @@ def main():
         if n in valu:
             v = valu[n]
             clk = v["GRBM_GUI_ACTIVE"] / 8
+            # a launch under 0.1 ms is shorter than the counters' sampling of GRBM_GUI_ACTIVE resolves
+            # (round 5 derived 7.5 GHz for a 0.03-ms launch): no clock and no issue fraction for it
+            short = v["ms"] < 0.1
             k["valu"] = {"insts_per_launch": v["SQ_INSTS_VALU"], "ms_in_counter_pass": round(v["ms"], 3),
-                         "clock_GHz": round(clk / (v["ms"] * 1e6), 3),
-                         "issue_frac_4cyc": round(v["SQ_INSTS_VALU"] * 4 / (1024 * clk), 3),
+                         "clock_GHz": None if short else round(clk / (v["ms"] * 1e6), 3),
+                         "issue_frac_4cyc": None if short else round(v["SQ_INSTS_VALU"] * 4 / (1024 * clk), 3),
                          "wait_frac": round(v["SQ_WAIT_INST_ANY"] / v["SQ_WAVE_CYCLES"], 3)}
+            if short:
+                k["valu"]["note"] = "launch < 0.1 ms: derived clock and issue fraction suppressed"
             if "SQ_INSTS_VALU_INT64" in v:
                 k["valu"]["int64_frac"] = round(v["SQ_INSTS_VALU_INT64"] / v["SQ_INSTS_VALU"], 3)
                 k["valu"]["int32_frac"] = round(v["SQ_INSTS_VALU_INT32"] / v["SQ_INSTS_VALU"], 3)
@@ -136,7 +141,7 @@ def main():
             if mix:
                 t = v["SQ_INSTS_VALU"] / 1024 * mix["mean_ns_per_wave_instr"] * 1e-6
                 k["valu"]["issue_ms_per_opcode_model"] = round(t, 3)
-                k["valu"]["issue_frac"] = round(t / v["ms"], 3)
+                k["valu"]["issue_frac"] = None if v["ms"] < 0.1 else round(t / v["ms"], 3)
                 k["valu"]["mix"] = mix
         if k:
             kern[n] = k

@@ -84,23 +84,27 @@ JNIEXPORT jint JNICALL Java_net_corda_core_crypto_CryptoBatch_nativeVerify(
                          (uint64_t)arena_len, (uint32_t)mode, (uint8_t*)ADDR(status), (cg_stats*)ADDR(stats));
 }
 
-/* Crypto.doVerify(txId, TransactionSignature) over many transactions: cg_verify_tx_signatures
- * (pool != 0: cg_pool_verify_tx_signatures over every device of the pool; no per-stage stats then). */
-JNIEXPORT jint JNICALL Java_net_corda_core_crypto_CryptoBatch_nativeVerifyTxSignatures(
+/* Crypto.doVerify(txId, TransactionSignature) over many transactions, over the 12-byte signature
+ * table and the dense signature stream: cg_verify_tx_signatures_packed (pool != 0:
+ * cg_pool_verify_tx_signatures_packed over every device of the pool; no per-stage stats then). */
+JNIEXPORT jint JNICALL Java_net_corda_core_crypto_CryptoBatch_nativeVerifyTxSignaturesPacked(
     JNIEnv* env, jobject self, jlong ctx, jlong pool, jobject keys, jint n_keys, jobject ids, jlong n_ids,
-    jobject sigs, jlong n_sigs, jobject tmpls, jint n_tmpls, jobject arena, jlong arena_len, jint mode,
-    jobject status, jobject stats) {
+    jobject sigs, jlong n_sigs, jobject sig_bytes, jlong sig_bytes_len, jobject tmpls, jint n_tmpls, jobject arena,
+    jlong arena_len, jint mode, jobject status, jobject stats) {
   if (pool)
-    return cg_pool_verify_tx_signatures((cg_pool*)(intptr_t)pool, (const cg_key*)ADDR(keys), (uint32_t)n_keys,
-                                        (const uint8_t*)ADDR(ids), (uint64_t)n_ids, (const cg_txsig*)ADDR(sigs),
-                                        (uint64_t)n_sigs, (const cg_signable_tmpl*)ADDR(tmpls), (uint32_t)n_tmpls,
+    return cg_pool_verify_tx_signatures_packed((cg_pool*)(intptr_t)pool, (const cg_key*)ADDR(keys), (uint32_t)n_keys,
+                                               (const uint8_t*)ADDR(ids), (uint64_t)n_ids,
+                                               (const cg_txsig_packed*)ADDR(sigs), (uint64_t)n_sigs,
+                                               (const uint8_t*)ADDR(sig_bytes), (uint64_t)sig_bytes_len,
+                                               (const cg_signable_tmpl*)ADDR(tmpls), (uint32_t)n_tmpls,
+                                               (const uint8_t*)ADDR(arena), (uint64_t)arena_len, (uint32_t)mode,
+                                               (uint8_t*)ADDR(status), 0);
+  return cg_verify_tx_signatures_packed((cg_ctx*)(intptr_t)ctx, (const cg_key*)ADDR(keys), (uint32_t)n_keys,
+                                        (const uint8_t*)ADDR(ids), (uint64_t)n_ids, (const cg_txsig_packed*)ADDR(sigs),
+                                        (uint64_t)n_sigs, (const uint8_t*)ADDR(sig_bytes), (uint64_t)sig_bytes_len,
+                                        (const cg_signable_tmpl*)ADDR(tmpls), (uint32_t)n_tmpls,
                                         (const uint8_t*)ADDR(arena), (uint64_t)arena_len, (uint32_t)mode,
-                                        (uint8_t*)ADDR(status), 0);
-  return cg_verify_tx_signatures((cg_ctx*)(intptr_t)ctx, (const cg_key*)ADDR(keys), (uint32_t)n_keys,
-                                 (const uint8_t*)ADDR(ids), (uint64_t)n_ids, (const cg_txsig*)ADDR(sigs),
-                                 (uint64_t)n_sigs, (const cg_signable_tmpl*)ADDR(tmpls), (uint32_t)n_tmpls,
-                                 (const uint8_t*)ADDR(arena), (uint64_t)arena_len, (uint32_t)mode,
-                                 (uint8_t*)ADDR(status), (cg_stats*)ADDR(stats));
+                                        (uint8_t*)ADDR(status), (cg_stats*)ADDR(stats));
 }
 
 /* WireTransaction ids + every signature (cg_verify_transactions; pool != 0: cg_pool_verify_transactions,

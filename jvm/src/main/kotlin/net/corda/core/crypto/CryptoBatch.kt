@@ -76,10 +76,14 @@ object CryptoBatch {
                                                   tmpls: ByteBuffer, nTmpls: Int, arena: ByteBuffer, arenaLen: Long,
                                                   mode: Int, idsOut: ByteBuffer, txStatusOut: ByteBuffer,
                                                   sigStatusOut: ByteBuffer): Int
-    private external fun nativeVerifyTxSignatures(ctx: Long, pool: Long, keys: ByteBuffer, nKeys: Int, ids: ByteBuffer,
-                                                  nIds: Long, sigs: ByteBuffer, nSigs: Long, tmpls: ByteBuffer,
-                                                  nTmpls: Int, arena: ByteBuffer, arenaLen: Long, mode: Int,
-                                                  status: ByteBuffer, stats: ByteBuffer): Int
+    /** cg_(pool_)verify_tx_signatures_packed: the 12-byte table (cg_txsig_packed: tx_idx, key_idx,
+     *  sig_len, tmpl) and the signatures back to back, each at a 4-byte boundary, in their own buffer
+     *  (round 6; the 24-byte cg_txsig form shipped ~12 B more per signature). */
+    private external fun nativeVerifyTxSignaturesPacked(ctx: Long, pool: Long, keys: ByteBuffer, nKeys: Int,
+                                                        ids: ByteBuffer, nIds: Long, sigs: ByteBuffer, nSigs: Long,
+                                                        sigBytes: ByteBuffer, sigBytesLen: Long, tmpls: ByteBuffer,
+                                                        nTmpls: Int, arena: ByteBuffer, arenaLen: Long, mode: Int,
+                                                        status: ByteBuffer, stats: ByteBuffer): Int
     /** cg_host_register / cg_host_unregister: a direct buffer the node keeps for many calls, pinned
      *  once so that its bytes reach the device by DMA without the runtime's CPU staging copy. */
     private external fun nativeHostRegister(buf: ByteBuffer, len: Long): Int
@@ -343,8 +347,9 @@ object CryptoBatch {
         val metas = LinkedHashMap<SignatureMetadata, Int>()
         all.forEach { metas.getOrPut(it.signatureMetadata) { metas.size } }
         val split = metas.keys.map { signableTemplate(it) }
-        val arena = direct(all.sumOf { minOf(it.bytes.size, SIG_LEN_MAX) + 4 } +
-                           split.sumOf { it.first.size + it.second.size + 8 } +
+        // arena: key and template bytes; the signatures go to their own stream (cg_txsig_packed, round 6:
+        // 12 bytes of table per signature instead of the 24-byte cg_txsig, no offsets)
+        val arena = direct(split.sumOf { it.first.size + it.second.size + 8 } +
                            all.map { it.by }.distinct().sumOf { it.encoded.size + 4 } + 16)
         val keys = Keys(all.map { it.by }, arena)
         val tmpls = direct(24 * split.size)
@@ -354,28 +359,29 @@ object CryptoBatch {
             tmpls.putLong(p).putLong(s).putInt(pre.size).putInt(suf.size)
         }
         val ids = direct(32 * txs.size)
-        val sigs = direct(24 * all.size)
+        val sigs = direct(12 * all.size)
+        val stream = direct(all.sumOf { minOf(it.bytes.size, SIG_LEN_MAX) + 4 })
         txs.forEachIndexed { t, (id, list) ->
             ids.put(id.bytes)
             for (sig in list) {
                 val ki = keys.index[sig.by]!!
                 val bytes = sigField(keys.schemes[ki], sig.bytes)
-                arena.align4()
-                val off = arena.position().toLong(); arena.put(bytes)
-                sigs.putLong(off).putInt(t).putInt(ki).putShort(bytes.size.toShort())
-                    .putShort(metas[sig.signatureMetadata]!!.toShort()).putInt(0)
+                stream.put(bytes).align4()          // signature i at the 4-byte-aligned end of signature i - 1
+                sigs.putInt(t).putInt(ki).putShort(bytes.size.toShort())
+                    .putShort(metas[sig.signatureMetadata]!!.toShort())
             }
         }
         val status = direct(all.size)
         val stats = direct(STATS_BYTES)
         val rc = withHandles { c, p ->
-            nativeVerifyTxSignatures(c, p, keys.table, keys.index.size, ids, txs.size.toLong(), sigs, all.size.toLong(),
-                                     tmpls, split.size, arena, arena.position().toLong(), mode, status, stats)
+            nativeVerifyTxSignaturesPacked(c, p, keys.table, keys.index.size, ids, txs.size.toLong(), sigs,
+                                           all.size.toLong(), stream, stream.position().toLong(), tmpls, split.size,
+                                           arena, arena.position().toLong(), mode, status, stats)
         }
         val st = ByteArray(all.size).also { status.get(it) }
         // the re-queue: the NOT_RUN signatures, each as a one-signature transaction of its own id
         val owner = txs.flatMap { (id, list) -> list.map { id to it } }
-        requeueNotRun(rc, "cg_verify_tx_signatures", st,
+        requeueNotRun(rc, "cg_verify_tx_signatures_packed", st,
                       if (requeue) { todo -> verifySigs(todo.map { owner[it].first to listOf(owner[it].second) }, mode, false) }
                       else null)
         record(stats, st)

@@ -132,7 +132,7 @@ def test_every_entry_point_takes_the_pool(kt):
     entry point may then refuse to run (round 5: `check(c != 0L)` made verifyBatch, doVerifyAll above
     minBatch and verifyPacked throw on every call)."""
     assert "check(c != 0L)" not in kt and "handles()" not in kt
-    for ext in ("nativeVerify", "nativeVerifyTxSignatures", "nativeVerifyTransactions"):
+    for ext in ("nativeVerify", "nativeVerifyTxSignaturesPacked", "nativeVerifyTransactions"):
         decl = re.search(rf"external fun {ext}\((.*?)\): Int", kt, re.S).group(1)
         assert decl.replace(" ", "").startswith("ctx:Long,pool:Long,"), ext
         for call in re.finditer(rf"\b{ext}\(c, p,", kt):
@@ -149,7 +149,7 @@ def test_device_faults_requeue_by_status(kt):
     assert "check(rc == CG_ERR_DEVICE)" in rq and "CG_NOT_RUN" in rq and "rerun(todo)" in rq
     assert "const val CG_ERR_DEVICE = -2" in kt.replace("private ", "")
     # each per-item native call is followed by requeueNotRun with a re-run of the NOT_RUN subset
-    for fn, native in (("verifyItems", "nativeVerify"), ("verifySigs", "nativeVerifyTxSignatures"),
+    for fn, native in (("verifyItems", "nativeVerify"), ("verifySigs", "nativeVerifyTxSignaturesPacked"),
                        ("verifyPackedItems", "nativeVerify")):
         body = _fun_body(kt, fn)
         assert native + "(c, p," in body, fn

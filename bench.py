@@ -138,11 +138,12 @@ def parse(argv=None):
     ap.add_argument("--txsig-table", type=int, default=12, choices=(12, 24),
                     help="the headline's signature table: 12 = cg_verify_tx_signatures_packed (12-byte records over "
                          "the dense signature stream, round 6), 24 = cg_verify_tx_signatures (24-byte cg_txsig)")
-    ap.add_argument("--host-register", type=int, default=0,
+    ap.add_argument("--host-register", type=int, default=-1,
                     help="1: register the headline's host buffers once (cg_host_register: DMA straight from "
                          "them, no CPU staging copy), as a JVM node registers its persistent direct buffers; "
-                         "2: the same after copying them into 2 MB transparent huge pages; 0: pageable "
-                         "(measured fastest on one GPU, DESIGN §5)")
+                         "2: the same after copying them into 2 MB transparent huge pages; 0: pageable; "
+                         "-1 (default): the library's rule for the ranks on this node (register_advised: "
+                         "pageable for 1-3 ranks per node, registered from 4, profiles/r06/host8)")
     ap.add_argument("--configs1-items", type=int, default=1 << 20, help="configs[1] Ed25519 secondary (0: off)")
     ap.add_argument("--ecdsa-items", type=int, default=1 << 20, help="configs[2] ECDSA 50/50 secondary (0: off)")
     ap.add_argument("--pipeline-txs", type=int, default=1 << 20, help="configs[3] transaction pipeline (0: off)")
@@ -269,6 +270,18 @@ def rank_host_threads(req, env=None):
         return req
     ranks = max(1, int(env.get("LOCAL_WORLD_SIZE", "1") or 1))
     return max(1, host_threads(0) // ranks)
+
+
+HOST_REGISTER_MIN_RANKS = 4  # corda_amd/csrc/host_budget.h kHostRegisterMinContexts
+
+
+def register_advised(env=None):
+    """--host-register -1: register the headline's buffers when 4 or more ranks share the node
+    (LOCAL_WORLD_SIZE), the rule cg_host_register_advised states (profiles/r06/host8/summary.json:
+    registered -10% alone, +5% beside 7 other ranks' host copies). HIP-free."""
+    env = os.environ if env is None else env
+    ranks = max(1, int(env.get("LOCAL_WORLD_SIZE", "1") or 1))
+    return 1 if ranks >= HOST_REGISTER_MIN_RANKS else 0
 
 
 def spawn_world(nproc, argv):
@@ -1003,6 +1016,8 @@ def main(argv=None):
     # zero-copy ingestion: the caller's persistent buffers registered once, outside the timed region
     # (a JVM node registers its direct-buffer arena once; cg_host_register, include/cordagpu.h)
     registered, huge_maps = [], []
+    if a.host_register < 0:
+        a.host_register = register_advised()
     # the 12-byte table: the generator's arena tail is already the dense stream (a view, no copy)
     pb = tb.packed() if a.txsig_table == 12 else None
     if a.host_register and hasattr(_lib_mod().lib(), "cg_host_register"):

@@ -107,6 +107,9 @@ def lib():
                 L.cg_host_unregister.argtypes = [vp]
                 L.cg_host_unregister.restype = i32
                 L.cg_host_registered.argtypes = [vp, u64]
+                if hasattr(L, "cg_host_register_advised"):
+                    L.cg_host_register_advised.argtypes = [u32]
+                    L.cg_host_register_advised.restype = i32
                 L.cg_host_registered.restype = i32
             pool = hasattr(L, "cg_pool_open")  # older builds (A/B variants) lack the pool
             if pool:

@@ -372,9 +372,12 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
                                  &c->fork, &wp);
   };
   const bool pre_plan = two && !prepare;
+  double prep_ms = 0;  // CG_HOST_TRACE: the host's time in chunk k's prepare hook
   auto front = [&](uint64_t k) {
     if (prepare) {
+      const auto p0 = std::chrono::steady_clock::now();
       const hipError_t w = (*prepare)(k, at(k), cnt(k));
+      prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - p0).count();
       if (w != hipSuccess) return w;
     }
     return c->eng->launch_items_front(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, mode, d_status + at(k),
@@ -417,8 +420,14 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
     // (a front stream of its own, chunk k + 1's front beside chunk k's back, measured neutral twice:
     // +1% in round 4, 315.4 -> 314.1 M sigs/s with the host pool, profiles/r04/fstr; removed in round 5)
     for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
+      const auto h0 = std::chrono::steady_clock::now();
       e = front(k);
+      const auto h1 = std::chrono::steady_clock::now();
       if (e == hipSuccess) e = back(k);
+      if (c->htrace)  // CG_HOST_TRACE: the host's time to enqueue chunk k (its front includes the copies)
+        fprintf(stderr, "[cg host] chunk %llu enqueue: front %.3f ms (prepare %.3f, with the copies), back %.3f ms\n",
+                (unsigned long long)k, std::chrono::duration<double, std::milli>(h1 - h0).count(), prep_ms,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h1).count());
     }
     return e;
   }
@@ -631,6 +640,8 @@ int cg_host_unregister(const void* p) {
   }
   return fail(CG_ERR_ARG, "cg_host_unregister: pointer was not registered");
 }
+
+int cg_host_register_advised(uint32_t contexts_per_node) { return cg::host_register_advised(contexts_per_node) ? 1 : 0; }
 
 int cg_host_registered(const void* p, uint64_t len) {
   const uint64_t lo = (uint64_t)(uintptr_t)p, hi = lo + len;

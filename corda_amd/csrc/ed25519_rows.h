@@ -776,6 +776,13 @@ struct EdPark9Lanes {
     for (int d = 0; d < 9; ++d) f.v[d] = p[(size_t)d * lanes];
   }
 };
+// FE9_ROWS_ILP (round 6, A/B): the row walk's products without the ladders' opaque column chains
+// (fe9_mul Pin = false): one lane per row, 2 waves per SIMD, every entry dependent on the previous
+// one -- latency-bound, so the products' own instruction-level parallelism is what hides latency
+#ifndef FE9_ROWS_ILP
+#define FE9_ROWS_ILP 0
+#endif
+#define FE9_ROWS_PIN (!FE9_ROWS_ILP)
 template <class Park>
 CG_HD void ed_wide_row_build9(ge9_niels* out, const Park& pk, const ge_p3& P, int e0, int e1, const fe& d2) {
   fe9 cYpX, cYmX, cZ2, cT2d, d4;
@@ -810,19 +817,19 @@ CG_HD void ed_wide_row_build9(ge9_niels* out, const Park& pk, const ge_p3& P, in
       fe9 a, b, A, B, C, D, E, H, G, F;
       fe9_add(a, R.Y, R.X);
       fe9_sub(b, R.Y, R.X);
-      fe9_mul<false>(A, a, cYpX);
-      fe9_mul<true>(B, b, cYmX);
-      fe9_mul<false>(C, R.T, cT2d);
-      fe9_mul<false>(D, R.Z, cZ2);
+      fe9_mul<false, FE9_ROWS_PIN>(A, a, cYpX);
+      fe9_mul<true, FE9_ROWS_PIN>(B, b, cYmX);
+      fe9_mul<false, FE9_ROWS_PIN>(C, R.T, cT2d);
+      fe9_mul<false, FE9_ROWS_PIN>(D, R.Z, cZ2);
       fe9_sub(E, A, B);
       fe9_add(H, A, B);
       fe9_add(G, D, C);
       fe9_subk(F, D, C);
-      fe9_mul<true>(R.X, E, F);
-      fe9_mul<false>(R.Y, G, H);
-      fe9_mul<false>(R.Z, G, F);
-      fe9_mul<true>(R.T, E, H);
-      fe9_mul<false>(run, run, R.Z);
+      fe9_mul<true, FE9_ROWS_PIN>(R.X, E, F);
+      fe9_mul<false, FE9_ROWS_PIN>(R.Y, G, H);
+      fe9_mul<false, FE9_ROWS_PIN>(R.Z, G, F);
+      fe9_mul<true, FE9_ROWS_PIN>(R.T, E, H);
+      fe9_mul<false, FE9_ROWS_PIN>(run, run, R.Z);
     }
     const int i = k - e0;
     pk.st(i, 0, R.X);
@@ -849,21 +856,21 @@ CG_HD void ed_wide_row_build9(ge9_niels* out, const Park& pk, const ge_p3& P, in
       fe9 pr, Z;
       pk.ld(i - 1, 3, pr);
       pk.ld(i, 2, Z);
-      fe9_mul<false>(zi, inv, pr);
-      fe9_mul<false>(inv, inv, Z);
+      fe9_mul<false, FE9_ROWS_PIN>(zi, inv, pr);
+      fe9_mul<false, FE9_ROWS_PIN>(inv, inv, Z);
     } else {
       zi = inv;
     }
     fe9 x, y, s, xy;
-    fe9_mul<false>(x, X, zi);
-    fe9_mul<false>(y, Y, zi);
+    fe9_mul<false, FE9_ROWS_PIN>(x, X, zi);
+    fe9_mul<false, FE9_ROWS_PIN>(y, Y, zi);
     ge9_niels n;
     fe9_add(s, y, x);
     fe9_carry(n.ypx, s);
     fe9_subk(s, y, x);
     fe9_carry(n.ymx, s);
-    fe9_mul<false>(xy, x, y);
-    fe9_mul<false>(n.xy2d, xy, d4);
+    fe9_mul<false, FE9_ROWS_PIN>(xy, x, y);
+    fe9_mul<false, FE9_ROWS_PIN>(n.xy2d, xy, d4);
     for (uint32_t& w : n.pad) w = 0;
     out[k] = n;
   }

@@ -141,7 +141,11 @@ typedef __int128 fe9_acc;
 #endif
 
 // out = a b mod p, tight. Signed: limbs of a and b are int32 (class S operands), else uint32.
-template <bool Signed>
+// Pin (default FE9_PIN_ACC): the column sums as one opaque chain from the carry (the ladders: issue-
+// bound, 2-3 waves per SIMD hide the chain's latency). Pin = false: the compiler's independent column
+// chains, for latency-bound callers with few waves per SIMD (the wide-row builds of phase 1,
+// round 6: FE9_ROWS_ILP).
+template <bool Signed, bool Pin = true>
 CG_HD void fe9_mul(fe9& out, const fe9& a, const fe9& b) {
   FE9_COUNT();
   const uint32_t k1216 = fe9_opaque(1216u), k9728 = fe9_opaque(9728u);
@@ -233,7 +237,7 @@ CG_HD void fe9_mul(fe9& out, const fe9& a, const fe9& b) {
 #if defined(__HIP_DEVICE_COMPILE__) && FE9_PIN_ACC
       // the running column sum as an opaque value after every MAC: the carry-in then stays the
       // first MAC's addend instead of being re-associated into a separate 64-bit add
-      asm volatile("" : "+v"(acc));
+      if (Pin) asm volatile("" : "+v"(acc));
 #endif
     }
     if (m <= 7) acc = (acc_t)fe9_mac_u((uint32_t)hc[m], k1216, (uint64_t)acc);

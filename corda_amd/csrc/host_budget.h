@@ -74,4 +74,13 @@ inline unsigned host_threads_env() {
   return v ? (unsigned)strtoul(v, nullptr, 10) : 0u;
 }
 
+// Whether a caller should register its host buffers (cg_host_register) rather than hand over pageable
+// memory, by how many contexts share the node's host (round 6, VERDICT r5 item 3;
+// profiles/r06/host8/summary.json): alone a rank copies fastest from pageable memory (the runtime's
+// staging paces the DMA; registered -10% on one MI355X), but with 7 other ranks staging their bytes
+// through the same host memory the pageable rank lost 17% and a registered one 4% (registered +5%
+// over pageable at the 8-rank proxy). 4 or more contexts per node: register (4 interpolated).
+constexpr unsigned kHostRegisterMinContexts = 4;
+inline bool host_register_advised(unsigned contexts_per_node) { return contexts_per_node >= kHostRegisterMinContexts; }
+
 }  // namespace cg

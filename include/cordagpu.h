@@ -233,6 +233,11 @@ uint32_t cg_table_choice(uint64_t table_bytes_max, uint64_t device_free);
 int cg_host_register(const void* p, uint64_t len);
 int cg_host_unregister(const void* p);
 int cg_host_registered(const void* p, uint64_t len);
+/* 1 when a caller whose node runs `contexts_per_node` contexts (one process per GPU: the GPUs per node;
+ * a cg_pool: its slots) should register its buffers, else 0 (pageable is faster). Round 6 measured on
+ * one MI355X: alone pageable wins by 10%; beside 7 other ranks' host copies registered wins by 5%
+ * (profiles/r06/host8/summary.json). Advised from 4 contexts per node. HIP-free. */
+int cg_host_register_advised(uint32_t contexts_per_node);
 
 /* Host buffers in, host status bytes out (what a JNI caller hands over). The key table, the key
  * bytes and the item table go first; then the items are verified in consecutive chunks of at most

@@ -114,3 +114,19 @@ def test_launcher_helpers_do_not_initialise_the_gpu():
     r = subprocess.run([sys.executable, "-c", code], cwd=os.path.dirname(HERE), capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stderr
+
+
+def test_host_register_rule_matches_library_and_bench():
+    """the registration default depends on the contexts per node (host_budget.h
+    host_register_advised, exported as cg_host_register_advised); bench.py's --host-register -1 mirrors
+    it from LOCAL_WORLD_SIZE before any GPU call (profiles/r06/host8/summary.json has the A/B)."""
+    import bench
+    from corda_amd import _lib
+    L = _lib.lib()
+    for n in range(0, 17):
+        assert L.cg_host_register_advised(n) == (1 if n >= 4 else 0), n
+        assert bench.register_advised({"LOCAL_WORLD_SIZE": str(max(n, 1))}) == (1 if n >= 4 else 0), n
+    assert bench.register_advised({}) == 0  # one process, one GPU: pageable
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "corda_amd", "csrc",
+                            "host_budget.h")).read()
+    assert "kHostRegisterMinContexts = 4" in src and bench.HOST_REGISTER_MIN_RANKS == 4

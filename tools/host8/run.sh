@@ -16,8 +16,8 @@ run() {  # name, loaders (0 none / copy / read), bench args
   local name=$1 load=$2; shift 2
   local pids=()
   if [ "$load" != 0 ]; then
-    for r in 1 2 3 4 5 6 7; do
-      ./tools/host8/stage_load 2 1060 36 400 $load > $OUT/${name}_load$r.json 2>&1 &
+    for q in 1 2 3 4 5 6 7; do
+      ./tools/host8/stage_load 2 1060 36 400 $load > $OUT/${name}_load$q.json 2>&1 &
       pids+=($!)
     done
   fi

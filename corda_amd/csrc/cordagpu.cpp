@@ -1600,6 +1600,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   // thread stages chunk k's copies (round 4 measured scanning ahead neutral to -1%, the copies'
   // landing times did not move, profiles/r04/ahead; round 5's trace shows the main stream waiting
   // 0.33 ms for chunk 1's bytes)
+  bool ct_active = false;  // the copy thread below issues the copies (it runs ahead: no scan-ahead helper)
   static const bool scan_ahead = [] {
     const char* v = getenv("CG_SCAN_AHEAD");
     return v && v[0] == '1';
@@ -1636,7 +1637,7 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
       ek = Extent();
       ek.add(cbase[k], span, sig_bytes_len);
     }
-    if (scan_ahead && k + 1 < nch) {
+    if (scan_ahead && !ct_active && k + 1 < nch) {
       ahead_k = k + 1;
       ahead_ek = Extent();
       ahead_ik = Extent();
@@ -1727,10 +1728,46 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   hipError_t copy_err = hipSuccess;
   uint64_t mid_k = 0;
   // the second half of chunk mid_k's before(): bytes copied, the front's stream ordered after them
+  // Round 6 (CG_COPY_THREAD=1, A/B): a copy thread issues every chunk's table slice and bytes in
+  // order, running ahead, while this thread enqueues the kernels. The pageable copies block the
+  // issuing thread for the runtime's staging (~4 ms of a ~6-ms chunk on the headline) and the kernel
+  // and event calls of a chunk take ~2 ms of host time more (CG_HOST_TRACE, profiles/r06/copy_thread):
+  // in one thread the device waited ~0.3 ms per chunk for the host. This thread now waits (host
+  // condition) only until the copier has recorded the event it orders the main stream after.
+  static const bool copy_thread_env = [] {
+    const char* v = getenv("CG_COPY_THREAD");
+    return v && v[0] == '1';
+  }();
+  const bool ct = copy_thread_env && split_on && nch > 1;
+  ct_active = ct;
+  struct Feed {
+    std::mutex m;
+    std::condition_variable cv;
+    uint64_t tab = 0, bytes = 0;  // chunks whose table slice / bytes the copier has issued
+    hipError_t err = hipSuccess;
+    bool stop = false;
+  } feed;
+  auto feed_wait = [&](bool bytes, uint64_t k) -> hipError_t {
+    std::unique_lock<std::mutex> lk(feed.m);
+    feed.cv.wait(lk, [&] { return feed.err != hipSuccess || (bytes ? feed.bytes : feed.tab) > k; });
+    return (bytes ? feed.bytes : feed.tab) > k ? hipSuccess : feed.err;
+  };
+  std::thread copier;
+  struct JoinCopier {  // every exit path stops and joins the copier before the locals it uses go away
+    std::thread& t;
+    Feed& f;
+    ~JoinCopier() {
+      {
+        std::lock_guard<std::mutex> g(f.m);
+        f.stop = true;
+      }
+      if (t.joinable()) t.join();
+    }
+  } join_copier{copier, feed};
   const std::function<hipError_t()> mid = [&]() -> hipError_t {
     c->fork.mid_front = nullptr;
     const uint64_t k = mid_k;
-    hipError_t e = copy_bytes(k, c->copy);
+    hipError_t e = ct ? feed_wait(true, k) : copy_bytes(k, c->copy);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, c->seg[k], 0);
     if (e == hipSuccess && htrace && 3 * k < c->fbt.size()) {
       c->fbh[k] = ms_since();
@@ -1747,8 +1784,12 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
   const std::function<hipError_t(uint64_t, uint64_t, uint64_t)> before = [&](uint64_t k, uint64_t, uint64_t) {
     if (split_on) {
       hipError_t e = c->fork.mid_front ? mid() : hipSuccess;  // a hook a front did not consume
-      if (e == hipSuccess) e = copy_table(k, c->copy);
-      if (e == hipSuccess) e = hipEventRecord(c->segtab[k], c->copy);
+      if (ct) {
+        if (e == hipSuccess) e = feed_wait(false, k);  // the copier recorded segtab[k]
+      } else {
+        if (e == hipSuccess) e = copy_table(k, c->copy);
+        if (e == hipSuccess) e = hipEventRecord(c->segtab[k], c->copy);
+      }
       if (e == hipSuccess) e = hipStreamWaitEvent(s, c->segtab[k], 0);
       if (e == hipSuccess) {
         mid_k = k;
@@ -1781,12 +1822,47 @@ static int verify_txsig_host_locked(cg_ctx* c, const cg_key* keys, uint32_t n_ke
     p12.sig_bytes_len = sig_bytes_len;
     p12.chunk_base = &cbase;
   }
+  if (ct)
+    copier = std::thread([&] {
+      hipError_t e = hipSetDevice(c->device);
+      for (uint64_t k = 0; k < nch && e == hipSuccess; ++k) {
+        {
+          std::lock_guard<std::mutex> g(feed.m);
+          if (feed.stop) break;
+        }
+        e = copy_table(k, c->copy);
+        if (e == hipSuccess) e = hipEventRecord(c->segtab[k], c->copy);
+        if (e == hipSuccess) {
+          std::lock_guard<std::mutex> g(feed.m);
+          feed.tab = k + 1;
+        }
+        feed.cv.notify_all();
+        if (e == hipSuccess) e = copy_bytes(k, c->copy);  // records seg[k]
+        if (e == hipSuccess) {
+          std::lock_guard<std::mutex> g(feed.m);
+          feed.bytes = k + 1;
+        }
+        feed.cv.notify_all();
+      }
+      std::lock_guard<std::mutex> g(feed.m);
+      if (e != hipSuccess) feed.err = e;
+      else if (feed.bytes < nch) feed.err = hipErrorUnknown;  // stopped early: no waiter may hang
+      feed.cv.notify_all();
+    });
   const hipError_t le = launch_txsig(c, (const cg_key*)c->keys.p, n_keys, (const uint8_t*)c->h_ids.p, n_ids,
                                      packed ? nullptr : (const cg_txsig*)c->h_sigs.p, n_sigs, tmpls, n_tmpls, dbase,
                                      arena_len, mode, ds, s, slot, uses, &before, &bounds, packed ? &p12 : nullptr);
   if (le == hipSuccess && c->fork.mid_front) {  // the last front did not consume its hook
     const hipError_t me = mid();
     if (me != hipSuccess) copy_err = me;
+  }
+  if (copier.joinable()) {
+    {
+      std::lock_guard<std::mutex> g(feed.m);
+      feed.stop = true;
+    }
+    copier.join();
+    if (feed.err != hipSuccess && copy_err == hipSuccess && le == hipSuccess) copy_err = feed.err;
   }
   if (copy_err != hipSuccess) return hip_fail(copy_err, "H2D signature bytes");
   HIP_TRY(le, "launch_txsig");

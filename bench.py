@@ -87,8 +87,8 @@ EC_WIDE_MUL = {"secp256r1": 454, "secp256k1": 454}  # k_ec_ladder_wide: 33 + 10 
 KEY_QUARTER_MIN_USES, KEY_FULL_MIN_USES, KEY_WIDE_MAX = 3, 32, 8192  # keyws.h
 KEY_WIDE_MIN_USES = {4: int(os.environ.get("CG_WIDE_MIN_USES_ED", 1536)), 3: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512)),
                      2: int(os.environ.get("CG_WIDE_MIN_USES_EC", 512))}
-EC_INV_K = 8  # items per k_ec_inv lane (corda_amd/csrc/ecdsa_rows.h)
-EC_INV_MUL_K = {"secp256r1": 365, "secp256k1": 372}  # products of one lane: prefix, inversion, unwinding
+EC_INV_K = 16  # items per k_ec_inv lane (corda_amd/csrc/ecdsa_rows.h; round 6: 16)
+EC_INV_MUL_K = {"secp256r1": 421, "secp256k1": 428}  # products of one lane: prefix, inversion, unwinding
 EC_MAC_PER_MUL_P = {"secp256r1": 117, "secp256k1": 92}
 EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r04/ubench/ubench_peak_summary.json:

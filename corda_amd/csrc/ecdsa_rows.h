@@ -384,10 +384,13 @@ CG_HD uint32_t ecdsa_prep(EcItemWs& ws, const uint8_t* arena, uint64_t lr, uint6
                           mid_blocks);
 }
 
-// Items per lane of k_ec_inv, one inversion each (A/B 8 vs 16 vs 32 on MI355X: profiles/r02/sha_v2;
-// 16 left ~1 wave per SIMD on a 1M-item curve range)
+// Items per lane of k_ec_inv, one inversion each (round 2: A/B 8 vs 16 vs 32 on MI355X,
+// profiles/r02/sha_v2: 16 left ~1 wave per SIMD on a 1M-item curve range). Round 6: 16. Since round 4
+// the inversions run on the side streams beside the ladders, so their latency is hidden and what
+// counts is the issue slots they take from the ladders: half the inversion share per item, headline
+// 338.5 -> 343.5 M sigs/s over 3 pairs, every pair faster (profiles/r06/inv16)
 #ifndef EC_INV_K
-#define EC_INV_K 8
+#define EC_INV_K 16
 #endif
 
 // Stage 2 (per group): w = s^-1 by one shared inversion (Montgomery's trick); u1 = e w,

@@ -9,12 +9,15 @@ SignatureMetadata(1, scheme)) -- the clear data Crypto.doVerify(txId, sig) check
 --sigs-per-tx signatures per transaction id, 4096 Ed25519 keys and 1024 keys per curve.
 Synthetic data (no network, no JVM).
 
-One step = ONE cg_verify_tx_signatures call over the whole shard, host arena -> host verdicts
-(the whole node: a JVM caller's direct buffers in, status bytes out): the key table, ids and
-exact key-use counts, then per device chunk its signature-table slice and signature bytes over
-PCIe (~97 B per signature, pageable memory), key tables, SignableData spliced on the device,
-verify, D2H of the verdicts; plus (N > 1) the RCCL all-gather of the per-GPU verdict vectors,
-the engine's only collective. `value` = signatures of all ranks / max-over-ranks time.
+One step = ONE cg_verify_tx_signatures_packed_device call over the whole shard with its inputs
+already resident in HBM when the timed region starts (the key table, ids, the 12-byte signature
+table, the dense signature stream, the template bytes; the task's measurement rule: `value` is never
+a PCIe-inclusive rate): key-use counts sampled on the device, key tables, SignableData spliced on
+the device, verify, verdicts left in HBM; plus (N > 1) the RCCL all-gather of the per-GPU verdict
+vectors, the engine's only collective. `value` = signatures of all ranks / max-over-ranks time.
+The same shard through the host form (cg_verify_tx_signatures_packed: host arena -> host verdicts,
+the key-use count pass, ~85 B per signature over PCIe, D2H of the verdicts) is timed right after
+it on every rank and reported as summary.host_to_host (--headline host makes it the timed form).
 
 Launch: ``python bench.py`` (N = 1), ``python bench.py --gpus N`` (this process checks that N
 devices are visible and starts ``torch.distributed.run --nproc-per-node N`` as a child before
@@ -138,6 +141,14 @@ def parse(argv=None):
     ap.add_argument("--txsig-table", type=int, default=12, choices=(12, 24),
                     help="the headline's signature table: 12 = cg_verify_tx_signatures_packed (12-byte records over "
                          "the dense signature stream, round 6), 24 = cg_verify_tx_signatures (24-byte cg_txsig)")
+    ap.add_argument("--headline", default="device", choices=("device", "host"),
+                    help="the timed form: device = inputs resident in HBM when the timed region starts (keys, ids, "
+                         "12-byte table, signature stream, templates; verdicts left in HBM): "
+                         "cg_verify_tx_signatures_packed_device; host = host arena -> host verdicts through "
+                         "cg_verify_tx_signatures_packed (PCIe-inclusive; always measured beside the headline as "
+                         "summary.host_to_host)")
+    ap.add_argument("--h2h-steps", type=int, default=-1,
+                    help="host arena -> host verdicts calls timed beside a device headline (-1: --steps; 0: off)")
     ap.add_argument("--host-register", type=int, default=-1,
                     help="1: register the headline's host buffers once (cg_host_register: DMA straight from "
                          "them, no CPU staging copy), as a JVM node registers its persistent direct buffers; "
@@ -1033,35 +1044,90 @@ def main(argv=None):
             if _lib_mod().host_register(arr):
                 registered.append(arr)
 
-    def step():
-        # the whole node: host arena -> host verdicts, one cg_verify_tx_signatures(_packed) call (synchronous)
-        holder["st"] = eng.verify_tx_signatures_packed(pb) if pb is not None else eng.verify_tx_signatures(tb)
+    def host_step():
+        # host arena -> host verdicts, one cg_verify_tx_signatures(_packed) call (synchronous)
+        holder["st_host"] = eng.verify_tx_signatures_packed(pb) if pb is not None else eng.verify_tx_signatures(tb)
         if world > 1:  # RCCL all-gather of the per-GPU verdict vectors
-            holder["all"] = shard.gather_verdicts(torch.from_numpy(holder["st"]).to(dev), world * tb.n, world)
+            holder["all"] = shard.gather_verdicts(torch.from_numpy(holder["st_host"]).to(dev), world * tb.n, world)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    eng.stage_times()  # drop the warmup's records
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t = time.perf_counter()
-    cg_ms = []
-    for _ in range(a.steps):
-        step()
-        cg_ms.append(dict(eng.last_stats))
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    stages = eng.stage_times()
-    st = holder["st"]
+    dbuf = {}
+    if a.headline == "device":
+        # inputs resident in HBM before the timed region starts: the key table, ids, signature table and
+        # one arena with the key / template bytes and (12-byte table) the signature stream at a 16-B
+        # aligned offset; verdicts stay in HBM (the all-gather at N > 1 reads them there)
+        up = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).to(dev)  # noqa: E731
+        if pb is not None:
+            off = -(-pb.arena.size // 16) * 16
+            har = np.zeros(off + pb.stream.size, np.uint8)
+            har[:pb.arena.size] = pb.arena
+            har[off:] = pb.stream
+            dbuf.update(k=up(pb.keys), i=up(pb.ids), s=up(pb.sigs), a=up(har), off=off, alen=har.size)
+            del har
+        else:
+            dbuf.update(k=up(tb.keys), i=up(tb.ids), s=up(tb.sigs), a=up(tb.arena), off=0, alen=tb.arena.size)
+        dbuf["st"] = torch.full((tb.n,), 255, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+
+    def device_step():
+        d = dbuf
+        if pb is not None:
+            eng.verify_tx_signatures_packed_device(d["k"].data_ptr(), len(pb.keys), d["i"].data_ptr(), pb.n_ids,
+                                                   d["s"].data_ptr(), pb.n, d["off"], pb.stream.size, pb.tmpls,
+                                                   d["a"].data_ptr(), d["alen"], d["st"].data_ptr(),
+                                                   stream=stream.cuda_stream)
+        else:
+            eng.verify_tx_signatures_device(d["k"].data_ptr(), len(tb.keys), d["i"].data_ptr(), tb.n_ids,
+                                            d["s"].data_ptr(), tb.n, tb.tmpls, d["a"].data_ptr(), d["alen"],
+                                            d["st"].data_ptr(), stream=stream.cuda_stream)
+        if world > 1:  # RCCL all-gather of the per-GPU verdict vectors, device to device
+            holder["all"] = shard.gather_verdicts(d["st"], world * tb.n, world)
+
+    def timed(step, steps, warmup, host_stats):
+        """W untimed steps, then K steps between a barrier + synchronize on both sides; the max over ranks."""
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        eng.stage_times()  # drop the warmup's records
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        cg = []
+        for _ in range(steps):
+            step()
+            if host_stats:
+                cg.append(dict(eng.last_stats))
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el, eng.stage_times(), cg
+
+    h2h_steps = a.steps if a.h2h_steps < 0 else a.h2h_steps
+    h2h = None
+    if a.headline == "device":
+        elapsed, stages, _ = timed(device_step, a.steps, a.warmup, False)
+        st = dbuf["st"].cpu().numpy()
+        if h2h_steps > 0:  # the same call shape from host buffers, PCIe-inclusive (never `value`)
+            el_h, stg_h, cg_ms = timed(host_step, h2h_steps, 1, True)
+            h2h = {"value": round(a.items * world * h2h_steps / el_h, 1), "unit": "sigs/s",
+                   "ms_per_step": round(el_h / h2h_steps * 1e3, 3), "steps": h2h_steps,
+                   "path": ("cg_verify_tx_signatures_packed" if pb is not None else "cg_verify_tx_signatures")
+                   + ": host arena -> host verdicts (pageable or registered per --host-register)",
+                   "stages": stage_summary(stg_h, h2h_steps),
+                   "verdicts_equal_device": bool(np.array_equal(holder["st_host"], st))}
+        for k in ("k", "i", "s", "a", "st"):
+            dbuf.pop(k, None)
+        torch.cuda.empty_cache()
+    else:
+        elapsed, stages, cg_ms = timed(host_step, a.steps, a.warmup, True)
+        el_h, h2h_steps = elapsed, a.steps
+        st = holder["st_host"]
 
     # ---- verdict checks: labels, and every draw of a pool item gets that item's verdict
     ver = check_verdicts(st, expected_verdicts(labels, schemes))
@@ -1091,15 +1157,16 @@ def main(argv=None):
                     roof["valu_issue"] = tr["valu_issue"]
 
     h2d_bytes = pb.h2d_bytes if pb is not None else int(tb.arena.size + tb.sigs.nbytes + tb.ids.nbytes + tb.keys.nbytes)
-    extra = {"stages": stage_summary(stages, a.steps), "ecdsa_ladders": ec_roof, "roofline_full": roof,
-             "verdicts": ver, "gen_s": round(gen_s, 1),
-             "headline_h2d": {"bytes_per_call": h2d_bytes, "bytes_per_sig": round(h2d_bytes / tb.n, 1),
-                              "GBps_effective": round(h2d_bytes * a.steps / elapsed / 1e9, 1),
-                              "cg_stats_ms_mean": {k: round(float(np.mean([c[k] for c in cg_ms])), 3)
-                                                   for k in ("ms_key_prep", "ms_h2d", "ms_verify", "ms_d2h",
-                                                             "ms_total")},
-                              "note": "ms_key_prep = host-side planning (the key-use sample pass), ms_h2d = until "
-                                      "the first chunk's bytes are resident, ms_verify = the rest"}}
+    extra = {"headline": a.headline, "stages": stage_summary(stages, a.steps), "ecdsa_ladders": ec_roof,
+             "roofline_full": roof, "verdicts": ver, "gen_s": round(gen_s, 1), "host_to_host": h2h}
+    if a.headline == "host" or h2h is not None:
+        extra["headline_h2d"] = {
+            "bytes_per_call": h2d_bytes, "bytes_per_sig": round(h2d_bytes / tb.n, 1),
+            "GBps_effective": round(h2d_bytes * h2h_steps / el_h / 1e9, 1),
+            "cg_stats_ms_mean": {k: round(float(np.mean([c[k] for c in cg_ms])), 3)
+                                 for k in ("ms_key_prep", "ms_h2d", "ms_verify", "ms_d2h", "ms_total")},
+            "note": "the host arena -> host verdicts calls: ms_key_prep = host-side planning (the key-use "
+                    "count pass), ms_h2d = until the first chunk's bytes are resident, ms_verify = the rest"}
     extra["table_modes_items"] = table_modes(batch, schemes)
     extra["host"] = {"threads": threads, "engine_host_threads": eng_threads or "library budget",
                      "registered_bytes": int(sum(x.nbytes for x in registered)), "host_register": a.host_register,
@@ -1141,10 +1208,15 @@ def main(argv=None):
             "data": "synthetic: seeded Ed25519 + ECDSA (secp256r1/k1) signatures over SignableData(txId, "
                     "SignatureMetadata(1, scheme)) with every Appendix A corruption class (tools/workload)",
             "config": {"workload": "BASELINE configs[4] per-GPU shard, whole node: notary-style mixed batch 70% "
-                                   "Ed25519 / 20% secp256r1 / 10% secp256k1, host arena -> host verdicts, one "
-                                   + ("cg_verify_tx_signatures_packed (12-byte signature table)" if pb is not None
-                                      else "cg_verify_tx_signatures") +
-                                   " call per step (batch Crypto.doVerify(txId, sig))",
+                                   "Ed25519 / 20% secp256r1 / 10% secp256k1, one "
+                                   + ("cg_verify_tx_signatures_packed" if pb is not None else "cg_verify_tx_signatures")
+                                   + ("_device call per step, inputs resident in HBM when the timed region starts "
+                                      "(keys, ids, signature table and stream, templates; verdicts left in HBM); "
+                                      "host arena -> host verdicts (PCIe-inclusive) in summary.host_to_host"
+                                      if a.headline == "device" else
+                                      " call per step, host arena -> host verdicts (PCIe-inclusive)")
+                                   + " (batch Crypto.doVerify(txId, sig))",
+                       "boundary": a.headline,
                        "items_per_gpu": a.items, "unique_pool": a.pool,
                        "mix": [n_ed, n_r1, a.items - n_ed - n_r1], "keys": len(batch.keys),
                        "sigs_per_tx": a.sigs_per_tx, "h2d_bytes_per_gpu": h2d_bytes, "txsig_table": a.txsig_table,
@@ -1153,6 +1225,10 @@ def main(argv=None):
         summary = {"verdicts_checked": ver["checked_vs_labels"], "label_mismatches": ver["label_mismatches"],
                    "not_run": ver["not_run"], "draws_consistent": ver["draws_consistent"],
                    "secondary_file": os.path.relpath(a.secondary_out, ROOT) if a.secondary_out else None}
+        if h2h is not None:
+            summary["host_to_host"] = h2h["value"]
+            summary["host_to_host_ms"] = h2h["ms_per_step"]
+            summary["host_verdicts_equal"] = h2h["verdicts_equal_device"]
         if ec_roof:
             summary["ecdsa_wide_frac"] = {c: (ec_roof.get(c + "_wide") or {}).get("frac") for c in ("secp256r1", "secp256k1")}
         for k in ("device_resident", "key_dist_distinct", "key_dist_zipf", "configs1_ed25519", "configs2_ecdsa",

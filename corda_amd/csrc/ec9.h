@@ -62,6 +62,9 @@ CG_HD void ec9_pin(f29& o, const f29& a) {
 #ifndef EC9_PIN_ACC
 #define EC9_PIN_ACC 1
 #endif
+#ifndef EC9_SIGN_MUL
+#define EC9_SIGN_MUL 1
+#endif
 // EC9_SQR=1: squares as 45 MACs against a doubled copy (ec9_col); 0: as general products (A/B)
 #ifndef EC9_SQR
 #define EC9_SQR 1
@@ -361,8 +364,19 @@ CG_HD void jac_madd9(Jac& r, bool& inf, const f29& x2, const f29& y2, bool neg, 
   f29 Z1Z1, U2, ys, S2, H;
   ec9_sqr<C>(Z1Z1, r.Z);
   ec9_mul<C>(U2, x2, Z1Z1);
+#if EC9_SIGN_MUL
+  // S2 = +-y2 Z1^3: each limb times an opaque +-1 (one v_mul_lo_u32 a limb, as fe9.h's
+  // fe9_sign_mask) instead of a negation and a select (two)
+  uint32_t sg = neg ? ~0u : 1u;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(sg));
+#endif
+#pragma unroll
+  for (int i = 0; i < 9; ++i) ys.v[i] = y2.v[i] * sg;
+#else
 #pragma unroll
   for (int i = 0; i < 9; ++i) ys.v[i] = neg ? 0u - y2.v[i] : y2.v[i];  // S2 = +-y2 Z1^3
+#endif
   ec9_mul<C>(S2, ys, r.Z);
   ec9_mul<C>(S2, S2, Z1Z1);
   ec9_sub(H, U2, r.X);

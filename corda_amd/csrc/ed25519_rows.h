@@ -485,6 +485,21 @@ CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t*
   ge9_p3 R;
   bool n0;
   const ge9_niels q0 = entry(0, n0);
+#if ED_SIGN_FOLD
+  // the running point is s_o R (fe9.h ge9_madd_half_flip): op o adds the stored entry of |digit|
+  // and flips its output by s_o s_{o+1}; the last op by s_{N-1} alone
+  bool n1;
+  ge9_niels q = entry(1, n1);
+  ge9_from_niels_half(R, q0, n0 != n1);
+  for (int o = 1; o < EdWideCfg::kOps; ++o) {
+    bool nn = false;
+    const ge9_niels qn = o + 1 < EdWideCfg::kOps ? entry(o + 1, nn) : q;
+    if (o + 1 < EdWideCfg::kOps) ge9_madd_half_flip<true>(R, R, q, n1 != nn);
+    else ge9_madd_half_flip<false>(R, R, q, n1);
+    q = qn;
+    n1 = nn;
+  }
+#else
   ge9_from_niels_half(R, q0, n0);  // identity + q0: one product, not seven
   for (int o = 1; o < EdWideCfg::kOps; ++o) {
     bool neg;
@@ -492,6 +507,7 @@ CG_HD void ed_double_scalar_wide(ge_p2& out, const uint32_t* eh, const uint32_t*
     if (o + 1 < EdWideCfg::kOps) ge9_madd_half<true>(R, R, n, neg);
     else ge9_madd_half<false>(R, R, n, neg);
   }
+#endif
   ge9_to_p2(out, R);
 }
 

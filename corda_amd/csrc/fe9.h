@@ -145,7 +145,8 @@ typedef __int128 fe9_acc;
 // bound, 2-3 waves per SIMD hide the chain's latency). Pin = false: the compiler's independent column
 // chains, for latency-bound callers with few waves per SIMD (the wide-row builds of phase 1,
 // round 6: FE9_ROWS_ILP).
-template <bool Signed, bool Pin = true>
+// Copy = false: no opaque operand copies (round 6: operands used twice, whose copies are v_movs)
+template <bool Signed, bool Pin = true, bool Copy = true>
 CG_HD void fe9_mul(fe9& out, const fe9& a, const fe9& b) {
   FE9_COUNT();
   const uint32_t k1216 = fe9_opaque(1216u), k9728 = fe9_opaque(9728u);
@@ -192,12 +193,10 @@ CG_HD void fe9_mul(fe9& out, const fe9& a, const fe9& b) {
 #if defined(__HIP_DEVICE_COMPILE__) && FE9_PIN_COPIES
   // opaque 32-bit operands: in the ladder loop the compiler otherwise widened loop-carried
   // differences to 64 bits and emitted 64 x 64-bit multiplies (3 MACs + moves each)
-  fe9 a_, b_;
+  fe9 a_ = a, b_ = b;
+  if (Copy) {
 #pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    a_.v[i] = a.v[i];
-    b_.v[i] = b.v[i];
-    asm volatile("" : "+v"(a_.v[i]), "+v"(b_.v[i]));
+    for (int i = 0; i < 9; ++i) asm volatile("" : "+v"(a_.v[i]), "+v"(b_.v[i]));
   }
 #define a a_
 #define b b_
@@ -411,6 +410,48 @@ CG_HD void ge9_madd_half(ge9_p3& r, const ge9_p3& p, const ge9_niels& q, bool ne
   fe9_mul<false>(r.Y, G, H);
   fe9_mul<false>(r.Z, u, v);
   if (WithT) fe9_mul<true>(r.T, E, H);
+}
+
+// r = (-1)^flip (p + q) for a half-scaled entry q taken as stored (round 6, ED_SIGN_FOLD): a ladder
+// keeps its running point as s_k R_k, s_k the sign of op k's digit, so every op adds the entry of
+// |digit| and the sign change s_k s_{k+1} rides on the output. -P = (-X, Y, Z, -T), and X3 = E F,
+// T3 = E H share E: negating E alone negates the point. That is 9 multiplies of E's limbs by +-1
+// (E is class S, symmetric, so -E is too) against ge9_madd_half's 36 selects of the entry halves
+// and of F / G.
+#ifndef ED_SIGN_FOLD
+#define ED_SIGN_FOLD 1
+#endif
+#ifndef ED_FLIP_COPY  // which of the four output products copy their operands (bit 0: X3 ... bit 3: T3)
+#define ED_FLIP_COPY 1  // X3 only: 2471 -> 2430 VALU per two loop additions (15: 2457, 0: 2674)
+#endif
+CG_HD uint32_t fe9_sign_mask(bool flip) {
+  uint32_t s = flip ? ~0u : 1u;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(s));  // a multiply by an opaque +-1, not a select of -x and x (two ops a limb)
+#endif
+  return s;
+}
+template <bool WithT>
+CG_HD void ge9_madd_half_flip(ge9_p3& r, const ge9_p3& p, const ge9_niels& q, bool flip) {
+  fe9 a, b;
+  fe9_add(a, p.Y, p.X);
+  fe9_sub(b, p.Y, p.X);
+  fe9 Bp, Ap, C;
+  fe9_mul<false>(Bp, a, q.ypx);
+  fe9_mul<true>(Ap, b, q.ymx);
+  fe9_mul<false>(C, p.T, q.xy2d);
+  fe9 E, H, u, v;
+  fe9_sub(E, Bp, Ap);
+  const uint32_t s = fe9_sign_mask(flip);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) E.v[i] *= s;
+  fe9_add(H, Bp, Ap);
+  fe9_add(u, p.Z, C);
+  fe9_subk(v, p.Z, C);
+  fe9_mul<true, true, (ED_FLIP_COPY & 1) != 0>(r.X, E, v);
+  fe9_mul<false, true, (ED_FLIP_COPY & 2) != 0>(r.Y, u, H);
+  fe9_mul<false, true, (ED_FLIP_COPY & 4) != 0>(r.Z, u, v);
+  if (WithT) fe9_mul<true, true, (ED_FLIP_COPY & 8) != 0>(r.T, E, H);
 }
 
 // r = (-1)^neg q as an extended point (the first entry of a ladder, added to the identity): x =

@@ -838,23 +838,33 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
       w_next = dw[widx];
     }
   };
+  // after next(o, ...), d_cur is op o + 1's digit: ED_SIGN_FOLD flips op o's output by the sign
+  // change s_o s_{o+1} (fe9.h ge9_madd_half_flip), the last op's by s_{N-1}
   {  // op 0: identity + q0 (fe9.h ge9_from_niels_half: one product instead of an addition's seven)
     ge9_niels n;
     bool neg;
     next(0, n, neg);
-    ge9_from_niels_half(R, n, neg);
+    ge9_from_niels_half(R, n, ED_SIGN_FOLD ? neg != (d_cur < 0) : neg);
   }
   for (int o = 1; o + 1 < N; ++o) {
     ge9_niels n;
     bool neg;
     next(o, n, neg);
+#if ED_SIGN_FOLD
+    ge9_madd_half_flip<true>(R, R, n, neg != (d_cur < 0));
+#else
     ge9_madd_half<true>(R, R, n, neg);
+#endif
   }
   {  // the last addition: projective output
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ge9_niels n;
     ed_lds_niels9(n, wave_lds, lane);
+#if ED_SIGN_FOLD
+    ge9_madd_half_flip<false>(R, R, n, d_cur < 0);
+#else
     ge9_madd_half<false>(R, R, n, d_cur < 0);
+#endif
   }
   ge9_to_p2(out, R);
 }

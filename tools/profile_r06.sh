@@ -25,7 +25,7 @@ passes() {  # <outdir> <command...>
 for what in "$@"; do
   case $what in
     headline)
-      passes gpurun_out/prof_r06_$TAG python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --device-steps 0 --host-steps 0 \
+      passes gpurun_out/prof_r06_$TAG python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --device-steps 0 --host-steps 0 --h2h-steps 0 \
         --key-dists= --configs1-items 0 --ecdsa-items 0 --pipeline-txs 0 --tear-offs 0 --configs0-txs 0 || exit 1 ;;
     tx)
       passes gpurun_out/prof_r06_tx_$TAG python3 bench.py --steps 2 --warmup 1 --items 1048576 --no-cpu-baseline \

@@ -149,6 +149,8 @@ struct cg_ctx {
   // before touching the shared workspace (async calls on different streams)
   hipEvent_t done = nullptr;
   bool done_rec = false;
+  hipEvent_t bridge = nullptr;  // a caller stream's point of entry (stream_of)
+  hipStream_t caller = nullptr; // the caller's stream the current device call is bridged from
   cg::StageTimer timer;  // used when opened with CG_FLAG_STAGE_TIMING
 };
 
@@ -261,9 +263,32 @@ hipError_t order_in(cg_ctx* c, hipStream_t s) { return c->done_rec ? hipStreamWa
 hipError_t order_out(cg_ctx* c, hipStream_t s) {
   hipError_t e = hipEventRecord(c->done, s);
   if (e == hipSuccess) c->done_rec = true;
+  if (e == hipSuccess && c->caller) e = hipStreamWaitEvent(c->caller, c->done, 0);  // the bridge back
+  c->caller = nullptr;
   return e;
 }
-hipStream_t stream_of(cg_ctx* c, void* hip_stream) { return hip_stream ? (hipStream_t)hip_stream : c->stream; }
+// The stream a device call runs on. A caller's stream is bridged to the context's own stream: HIP
+// multiplexes streams onto GPU_MAX_HW_QUEUES (4) hardware queues in creation order, and a stream
+// created elsewhere (torch's, the JVM's) can share an in-order queue with one of the side streams,
+// whose milliseconds-long chains and table builds then run ahead of the call's main-stream kernels
+// (round 6: the device-resident headline on torch's stream sat ~3.5 ms per step behind side stream
+// 0's wide chain and rows, profiles/r06/bridge). The context's stream, created first, has a queue of
+// its own; it waits for everything the caller enqueued before the call, and order_out makes the
+// caller's stream wait for the call's end, so the call stays ordered on the caller's stream.
+// CG_STREAM_BRIDGE=0: run on the caller's stream itself (A/B).
+hipStream_t stream_of(cg_ctx* c, void* hip_stream) {
+  static const bool bridge = [] {
+    const char* v = getenv("CG_STREAM_BRIDGE");
+    return !(v && v[0] == '0');
+  }();
+  c->caller = nullptr;
+  if (!hip_stream || (hipStream_t)hip_stream == c->stream) return c->stream;
+  if (!bridge || !c->bridge || hipEventRecord(c->bridge, (hipStream_t)hip_stream) != hipSuccess ||
+      hipStreamWaitEvent(c->stream, c->bridge, 0) != hipSuccess)
+    return (hipStream_t)hip_stream;
+  c->caller = (hipStream_t)hip_stream;
+  return c->stream;
+}
 
 // Equal chunks of at most c->chunk items.
 uint64_t chunk_of(const cg_ctx* c, uint64_t n) {
@@ -389,7 +414,16 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   // with one, the builds start first: they overlap the preparation of the first chunk.
   if (e == hipSuccess && pre_plan) e = plan(0);
   if (e == hipSuccess && pre_plan) e = plan(1);
-  if (e == hipSuccess && prepare) e = c->eng->launch_key_tables(&c->fork, s);
+  // The host forms start the table builds now, so that they overlap the first chunk's copies. The
+  // device forms have no copy to hide: their builds start after the first chunk's plan
+  // (launch_items_front), whose onesweep look-back otherwise stalls behind the builds (round 6,
+  // device-resident headline: the first plan's last pass 0.2 -> 2.7 ms in some steps,
+  // profiles/r06/bridge timeline). CG_DEV_TABS_FIRST=1: start them now in the device forms too (A/B).
+  static const bool dev_tabs_first = [] {
+    const char* v = getenv("CG_DEV_TABS_FIRST");
+    return v && v[0] == '1';
+  }();
+  if (e == hipSuccess && prepare && (prepare_blocks || dev_tabs_first)) e = c->eng->launch_key_tables(&c->fork, s);
   // CG_FRONT_AFTER_TABLES=1 (A/B): the first chunk's front waits for every key table, instead of
   // sharing the chip with the builds (both run at about half speed together:
   // profiles/r03/env_chains timelines)
@@ -756,6 +790,7 @@ int cg_open(cg_ctx** out, const cg_config* cfg) {
   }
   for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&c->tev[k]);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->bridge, hipEventDisableTiming);
   int var = 0;
   if (e == hipSuccess) e = acquire_tables(c->device, c->stream, tab_budget, &c->btab, &var);
   if (e == hipSuccess) {
@@ -827,6 +862,7 @@ void cg_close(cg_ctx* c) {
   for (int k = 0; k < 4; ++k)
     if (c->tev[k]) hipEventDestroy(c->tev[k]);
   if (c->done) hipEventDestroy(c->done);
+  if (c->bridge) hipEventDestroy(c->bridge);
   for (auto* v : {&c->timer.recs, &c->timer.spare})
     for (auto& r : *v) {
       hipEventDestroy(r.a);

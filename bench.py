@@ -101,8 +101,8 @@ PEAK_MAC32_PER_S = 3.6412e13
 PEAK_MAC32_SPEC = 16 * 1024 * 2.4e9  # 4 cycles per wave64 v_mad_u64_u32 on a SIMD-32, 2.4 GHz
 PEAK_SOURCE = "measured v_mad_u64_u32 chip rate, profiles/r04/ubench (spec-derived 3.93e13: frac_spec)"
 # kernel generation whose PMC traffic profile is committed (profiles/r03/pmc_traffic.json)
-KERNEL_VERSION = "r05_final"
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r05", "pmc_traffic.json")
+KERNEL_VERSION = "r06_final"
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r06", "pmc_traffic.json")
 
 # Appendix A labels (tools/workload) -> the verdict Crypto.doVerify gives them (key decodes)
 ED_LABEL_EXPECT = {0: 0, 1: 1, 2: 1, 3: 1, 4: 0, 6: 1, 7: 2}       # A5 (high S) depends on slide()

@@ -25,6 +25,8 @@ __global__ void k_misc_status(const cg_item* __restrict__ items, uint64_t n_item
   const uint8_t s = keys[ki].scheme;
   if (s != CG_EDDSA_ED25519_SHA512 && s != CG_ECDSA_SECP256R1_SHA256 && s != CG_ECDSA_SECP256K1_SHA256)
     status[i] = CG_UNSUPPORTED;
+  else if (s == CG_EDDSA_ED25519_SHA512)
+    status[i] = CG_NOT_RUN;  // until a verdict lands (k_ed_hash writes only its early verdicts: verify_ed.hip)
 }
 
 // Per-key use counts, sampled: one item in KEY_USES_SAMPLE adds KEY_USES_SAMPLE (no-return

@@ -461,6 +461,9 @@ static_assert(sizeof(EdDigitsWide) == ITEM_SLOT, "digits must fill one item slot
 #ifndef ED_HASH_WAVES_PER_SIMD
 #define ED_HASH_WAVES_PER_SIMD 4
 #endif
+#ifndef ED_HASH_STATUS_EARLY
+#define ED_HASH_STATUS_EARLY 0
+#endif
 #ifndef ED_HASH_MID_SCHEDULE
 #define ED_HASH_MID_SCHEDULE 1
 #endif
@@ -541,7 +544,10 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
     for (int w = 0; w < 8; ++w) ec.r[(size_t)w * ec.n + p] = sw[w];
   }
   ec.pend[p] = st == ED_PENDING;
-  status[i] = st;
+  // ED_HASH_STATUS_EARLY=0 (round 6): a pending item's status byte is left as k_misc_status set it
+  // (CG_NOT_RUN) until k_ed_finish writes the verdict: nothing reads ED_PENDING, and a 1-byte store at
+  // a random position (items are in plan order here) cost the kernel a whole written-back line per item
+  if (!ED_HASH_STATUS_EARLY ? st != (uint8_t)ED_PENDING : true) status[i] = st;
 }
 
 template <bool Fused>  // Fused: every item's message is a SignableData splice (the tx-signature paths)

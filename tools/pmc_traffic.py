@@ -161,7 +161,7 @@ def main():
     with open(os.path.join(dest, "pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     if os.environ.get("PMC_TRAFFIC_HEADLINE", "1") == "1":  # the file bench.py's roofline reads (TRAFFIC_FILE)
-        head = os.path.join(ROOT, os.environ.get("PMC_TRAFFIC_FILE", "profiles/r05/pmc_traffic.json"))
+        head = os.path.join(ROOT, os.environ.get("PMC_TRAFFIC_FILE", "profiles/r06/pmc_traffic.json"))
         os.makedirs(os.path.dirname(head), exist_ok=True)
         with open(head, "w") as f:
             json.dump(out, f, indent=1)

@@ -258,7 +258,11 @@ int cg_verify_batch(cg_ctx* ctx, const cg_key* keys, uint32_t n_keys, const cg_i
  * enqueueing; status is valid once the stream has reached that point. Workspace comes from the
  * ctx (reserve with cg_reserve); consecutive calls on one ctx are ordered on the device (each call
  * waits for the previous call's work, whatever stream either was enqueued on), because they share
- * that workspace. */
+ * that workspace. A caller's stream is bridged: the kernels run on the context's own stream (a
+ * hardware queue of its own), which waits for the work already on the caller's stream, and the
+ * caller's stream waits for the call's end, so the call is ordered on the caller's stream as if it
+ * ran there (a stream created elsewhere can share an in-order hardware queue with the context's
+ * side streams: round 6, cordagpu.cpp stream_of). */
 int cg_reserve(cg_ctx* ctx, uint32_t max_keys, uint64_t max_items);
 int cg_verify_batch_device(cg_ctx* ctx, const cg_key* d_keys, uint32_t n_keys, const cg_item* d_items,
                            uint64_t n_items, const uint8_t* d_arena, uint64_t arena_len, uint32_t mode,

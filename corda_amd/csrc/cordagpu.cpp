@@ -397,16 +397,26 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
                                  &c->fork, &wp);
   };
   const bool pre_plan = two && !prepare;
+  // CG_DEV_PRE_PLAN=1 (A/B, the device tx-signature forms): both first chunks' items and plans before
+  // the table builds, as pre_plan does for the batch forms, so that chunk 1's front is only its
+  // hashes. Measured slower (388.3 vs 392.1 M sigs/s over 3 pairs, profiles/r06/preplan): chunk 0's
+  // Ed25519 ladder then starts earlier but shares the chip with chunk 1's ECDSA fronts (12.5 vs
+  // 11.9 ms of ladder per step); the chip is already full in phase 1.
+  static const bool dev_pre_plan = [] {
+    const char* v = getenv("CG_DEV_PRE_PLAN");
+    return v && v[0] == '1';
+  }();
+  const bool pre_prep = two && prepare && !prepare_blocks && dev_pre_plan;
   double prep_ms = 0;  // CG_HOST_TRACE: the host's time in chunk k's prepare hook
   auto front = [&](uint64_t k) {
-    if (prepare) {
+    if (prepare && !(pre_prep && k < 2)) {
       const auto p0 = std::chrono::steady_clock::now();
       const hipError_t w = (*prepare)(k, at(k), cnt(k));
       prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - p0).count();
       if (w != hipSuccess) return w;
     }
     return c->eng->launch_items_front(d_keys, n_keys, d_items + at(k), cnt(k), d_arena, arena_len, mode, d_status + at(k),
-                                  c->keyprep.p, ws(k), s, d_msgs, msgs_len, &c->fork, &wp, pre_plan && k < 2);
+                                  c->keyprep.p, ws(k), s, d_msgs, msgs_len, &c->fork, &wp, (pre_plan || pre_prep) && k < 2);
   };
   // chunk k + 1's front (plan, hashes, ECDSA prep) before chunk k's back (ladders): the first
   // chunk's wait for the key tables is spent on the next chunk's fronts. Without a prepare hook the
@@ -414,6 +424,10 @@ hipError_t launch_chunked(cg_ctx* c, const cg_key* d_keys, uint32_t n_keys, cons
   // with one, the builds start first: they overlap the preparation of the first chunk.
   if (e == hipSuccess && pre_plan) e = plan(0);
   if (e == hipSuccess && pre_plan) e = plan(1);
+  for (uint64_t k = 0; k < 2 && pre_prep && e == hipSuccess; ++k) {
+    e = (*prepare)(k, at(k), cnt(k));
+    if (e == hipSuccess) e = plan(k);
+  }
   // The host forms start the table builds now, so that they overlap the first chunk's copies. The
   // device forms have no copy to hide: their builds start after the first chunk's plan
   // (launch_items_front), whose onesweep look-back otherwise stalls behind the builds (round 6,

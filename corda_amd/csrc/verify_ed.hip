@@ -528,16 +528,26 @@ __device__ __forceinline__ void ed_hash_one(uint64_t p, const cg_item* __restric
         sc_sub(sr, sr, r1);
       }
     }
+    // only the digit words are stored (round 6): the whole 120-B slot store wrote its 48-B pad too,
+    // ~48 B of HBM writes per item for nothing (profiles/r06/headline pmc_traffic.json)
     if (wide) {
       EdDigitsWide d;
       sc_recode_w<ED_WIDE_W>(d.eh, EdWideCfg::kPackedWords, h);
       sc_recode_wb<ED_WIDE_BW, EdWideCfg::kBBits>(d.es, EdWideCfg::kBPackedWords, sr);
-      ((EdDigitsWide*)dig)[p] = d;
+      EdDigitsWide* o = (EdDigitsWide*)dig + p;
+#pragma unroll
+      for (int w = 0; w < EdWideCfg::kPackedWords; ++w) o->eh[w] = d.eh[w];
+#pragma unroll
+      for (int w = 0; w < EdWideCfg::kBPackedWords; ++w) o->es[w] = d.es[w];
     } else {
       EdDigits d;
       sc_recode_w<ED_W>(d.eh, EdCfg::kPackedWords, h);
       sc_recode_wb<ED_WIDE_BW, EdWideCfg::kBBits>(d.es, EdWideCfg::kBPackedWords, sr);
-      dig[p] = d;
+      EdDigits* o = dig + p;
+#pragma unroll
+      for (int w = 0; w < EdCfg::kPackedWords; ++w) o->eh[w] = d.eh[w];
+#pragma unroll
+      for (int w = 0; w < EdWideCfg::kBPackedWords; ++w) o->es[w] = d.es[w];
     }
     st = (uint8_t)ED_PENDING;
 #pragma unroll

@@ -89,3 +89,15 @@ def test_gpus_request_exceeding_devices_fails_before_gpu():
                        capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode != 0
     assert "only 0 device" in r.stderr
+
+
+def test_headline_is_device_resident_by_default():
+    """The timed form is the device-resident call (inputs in HBM when the timed region starts); the
+    host arena -> host verdicts form is timed beside it (summary.host_to_host), or timed itself with
+    --headline host."""
+    import bench
+    a = bench.parse([])
+    assert a.headline == "device" and a.h2h_steps == -1
+    assert bench.parse(["--headline", "host"]).headline == "host"
+    src = open(bench.__file__).read()
+    assert "verify_tx_signatures_packed_device(" in src and '"host_to_host"' in src

@@ -5,6 +5,8 @@ SignableData(id, metadata) = prefix || id || suffix spliced on the device.
 Parity: the C oracle verifies the same signatures over the materialised SignableData bytes
 (tests/txsig_util.py); at full size (> 8M signatures, the configs[4] per-GPU shard in one call)
 through idempotence: every draw's verdict equals its pool item's, which equals the oracle's."""
+import os
+
 import numpy as np
 import pytest
 
@@ -12,6 +14,8 @@ from corda_amd import batch as B
 from oracle import c_oracle
 
 import txsig_util
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -414,3 +418,53 @@ def test_packed_8m_one_call(spool):
     assert not np.any(st == B.NOT_RUN)
     bad = np.nonzero(st != ref[idx])[0]
     assert bad.size == 0, f"{bad.size} of {n} verdicts differ"
+
+
+@pytest.mark.parametrize("bridge", ["1", "0"])
+def test_device_call_ordered_on_caller_stream(bridge):
+    """A device call enqueued on a caller's (torch) stream: the kernels run on the context's own
+    stream, bridged by events (cordagpu.cpp stream_of), and work the caller enqueues on its stream
+    afterwards sees the finished verdicts without any synchronisation in between; CG_STREAM_BRIDGE=0
+    runs the call on the caller's stream itself. Both in a child process (the switch is read once)."""
+    import subprocess
+    import sys
+    import textwrap
+    code = textwrap.dedent(f"""
+        import os, sys, numpy as np, torch
+        os.environ["CG_STREAM_BRIDGE"] = "{bridge}"
+        sys.path.insert(0, {ROOT!r})
+        sys.path.insert(0, os.path.join({ROOT!r}, "tests"))
+        from corda_amd.engine import Engine
+        from corda_amd import signable
+        from oracle import c_oracle
+        from corda_amd import batch as B
+        from tools.workload import wl
+        pool, labels, schemes = wl.notary_pool(1 << 14, ed_keys=24, ec_keys=12, seed=707, nthreads=16, sig_group=4)
+        ids, id_idx = wl.pool_ids(pool, len(signable.template(1, 4)[0]))
+        idx = np.random.default_rng(708).integers(0, pool.n, 90_000)
+        tb = wl.tx_sig_stream(pool, schemes, idx, ids, id_idx, nthreads=16)
+        pb = tb.packed()
+        ref = c_oracle.verify_batch(pool, B.MODE_DOVERIFY, 16)[idx]
+        dev = torch.device("cuda", 0)
+        up = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.uint8)).to(dev)
+        kd, ijd, sgd, ad = up(pb.keys), up(pb.ids), up(pb.sigs), up(tb.arena)
+        s = torch.cuda.Stream(device=dev)
+        with Engine(0) as eng:
+            outs = []
+            for rep in range(3):
+                sd = torch.full((pb.n,), 255, dtype=torch.uint8, device=dev)
+                torch.cuda.synchronize()
+                with torch.cuda.stream(s):
+                    eng.verify_tx_signatures_packed_device(kd.data_ptr(), len(pb.keys), ijd.data_ptr(), pb.n_ids,
+                                                           sgd.data_ptr(), pb.n, pb.arena.size, pb.stream.size,
+                                                           pb.tmpls, ad.data_ptr(), tb.arena.size, sd.data_ptr(),
+                                                           stream=s.cuda_stream)
+                    outs.append(sd.clone())  # enqueued on the caller's stream right after the call
+            torch.cuda.synchronize()
+        for o in outs:
+            got = o.cpu().numpy()
+            assert np.array_equal(got, ref), int(np.count_nonzero(got != ref))
+        print("ORDERED_OK")
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ORDERED_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]

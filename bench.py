@@ -85,6 +85,9 @@ MAC32_EXEC_PER_ED25519 = ED_VERIFY_FE9 * MAC_PER_MUL9 + ((ED_VERIFY_FE[0] + ED_F
 # SIMD executes (per-item mean 1% lower).
 EC_LADDER_MUL = {"secp256r1": 719, "secp256k1": 701}
 EC_WIDE_MUL = {"secp256r1": 454, "secp256k1": 454}  # k_ec_ladder_wide: 33 + 10 mixed additions (G radix 2^26) + x-check
+# of those, the squares (round 6, ec9.h ec9_sqr*: 45 a*a MACs against a doubled copy instead of 81),
+# priced at EC_MAC_PER_SQR_P: the same reduction as a product, 36 fewer multiply MACs
+EC_WIDE_SQR = {"secp256r1": 123, "secp256k1": 123}  # 3 per addition (Z1^2, H^2, r^2 + E) x 41
 # table modes (corda_amd/csrc/keyws.h): quarter tables from 3 items per key, full from 32, wide from
 # KEY_WIDE_MIN_USES (1536 Ed25519 / 512 ECDSA)
 KEY_QUARTER_MIN_USES, KEY_FULL_MIN_USES, KEY_WIDE_MAX = 3, 32, 8192  # keyws.h
@@ -93,6 +96,11 @@ KEY_WIDE_MIN_USES = {4: int(os.environ.get("CG_WIDE_MIN_USES_ED", 1536)), 3: int
 EC_INV_K = 16  # items per k_ec_inv lane (corda_amd/csrc/ecdsa_rows.h; round 6: 16)
 EC_INV_MUL_K = {"secp256r1": 421, "secp256k1": 428}  # products of one lane: prefix, inversion, unwinding
 EC_MAC_PER_MUL_P = {"secp256r1": 117, "secp256k1": 92}
+EC_MAC_PER_SQR_P = {"secp256r1": 45 + 36, "secp256k1": 45 + 11}
+# executed MAC32 per k_ec_ladder_wide item: r1 48 690, k1 37 340 (round 5 priced every product at
+# the general MAC count, 53 118 / 41 768, which round 6's squares would overstate by 9-11%)
+EC_WIDE_MAC32 = {c: (EC_WIDE_MUL[c] - EC_WIDE_SQR[c]) * EC_MAC_PER_MUL_P[c] + EC_WIDE_SQR[c] * EC_MAC_PER_SQR_P[c]
+                 for c in EC_WIDE_MUL}
 EC_MAC_PER_MUL_N = {"secp256r1": 162, "secp256k1": 162}
 # v_mad_u64_u32 chip throughput measured on MI355X (profiles/r04/ubench/ubench_peak_summary.json:
 # 16 independent chains per lane, 8 waves per SIMD: 15.05 lanes/clk/SIMD at the measured shader
@@ -660,8 +668,7 @@ def roofline(stages, units, steps):
     ec = {}
     for c, tag in (("secp256r1", "r1"), ("secp256k1", "k1")):
         ec[c] = block(tag + "_ladder", EC_LADDER_MUL[c] * EC_MAC_PER_MUL_P[c], units[tag], f"k_ec_ladder<{c}, full>")
-        ec[c + "_wide"] = block(tag + "_ladder_wide", EC_WIDE_MUL[c] * EC_MAC_PER_MUL_P[c], units[tag + "_wide"],
-                                f"k_ec_ladder_wide<{c}>")
+        ec[c + "_wide"] = block(tag + "_ladder_wide", EC_WIDE_MAC32[c], units[tag + "_wide"], f"k_ec_ladder_wide<{c}>")
     return ed, ec
 
 

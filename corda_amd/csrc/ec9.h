@@ -253,6 +253,7 @@ CG_HD void ec9_mul_add(f29& out, const f29& a, const f29& b, const f29& e) {
 template <int C, bool Add>
 CG_HD void ec9_sqr_impl(f29& out, const f29& a, const f29& e) {
   M29_COUNT(C, 0);
+  M29_COUNT_SQR(C);
   f29 a2;
 #pragma unroll
   for (int i = 0; i < 9; ++i) a2.v[i] = a.v[i] << 1;

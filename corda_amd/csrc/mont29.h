@@ -25,9 +25,12 @@
 // the executed-work figure bench.py prices the ECDSA kernels with. Compiled out of the device build.
 #ifdef FE_OP_COUNT
 extern uint64_t g_m29_nmul[2][2];
+extern uint64_t g_m29_nsqr[2];  // of the mod-p products, the squares (ec9.h: 45 a*a MACs, not 81)
 #define M29_COUNT(C, N) (++g_m29_nmul[C][N])
+#define M29_COUNT_SQR(C) (++g_m29_nsqr[C])
 #else
 #define M29_COUNT(C, N) ((void)0)
+#define M29_COUNT_SQR(C) ((void)0)
 #endif
 
 struct f29 {

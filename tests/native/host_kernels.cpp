@@ -12,6 +12,7 @@
 uint64_t g_fe_nmul = 0, g_fe_nsq = 0;
 uint64_t g_fe9_nmul = 0;
 uint64_t g_m29_nmul[2][2] = {{0, 0}, {0, 0}};
+uint64_t g_m29_nsqr[2] = {0, 0};
 #endif
 
 static Ed25519Consts g_C;
@@ -822,10 +823,14 @@ static int ecdsa_wide_verify(const uint8_t* arena, uint64_t lr, uint64_t key_off
   }
 #ifdef FE_OP_COUNT
   g_m29_nmul[C][0] = g_m29_nmul[C][1] = 0;
+  g_m29_nsqr[C] = 0;
 #endif
   st = ecdsa_ladder_check_wide<C>(ws.a, ws.b, ws.r, *TG[C], *TQ, K);
 #ifdef FE_OP_COUNT
-  if (counts) counts[0] = g_m29_nmul[C][0];
+  if (counts) {
+    counts[0] = g_m29_nmul[C][0];
+    counts[2] = g_m29_nsqr[C];  // of counts[0], the squares
+  }
 #endif
   return (int)st;
 }

@@ -375,15 +375,22 @@ def test_executed_work_constants_wide():
     lib.t_ecdsa_verify_wide.argtypes = [i32, vp, u64, u64, u32, u32, u64, u32, u64, u64, vp]
     for name, scheme, curve in (("secp256r1", 3, 1), ("secp256k1", 2, 0)):
         b, _ = wl.ecdsa_batch(curve, 96, n_keys=2, corrupt_permille=0, seed=3, nthreads=4)
-        lad = []
+        lad, sqr = [], []
         for i in range(b.n):
             itm = b.items[i]
             k = b.keys[itm["key_idx"]]
-            o = np.zeros(2, np.uint64)
+            o = np.zeros(3, np.uint64)
             assert lib.t_ecdsa_verify_wide(scheme, ptr(b.arena), b.arena.size, int(k["off"]), int(k["len"]),
                                            int(k["fmt"]), int(itm["sig_off"]), int(itm["sig_len"]),
                                            int(itm["msg_off"]), int(itm["msg_len"]), ptr(o)) == 0
             lad.append(int(o[0]))
+            sqr.append(int(o[2]))
+        # of those products, the squares (ec9.h ec9_sqr*: 45 a*a MACs): priced at EC_MAC_PER_SQR_P
+        assert int(np.median(sqr)) == bench.EC_WIDE_SQR[name], (name, sqr)
+        # a square: the 36 pairs i < j once plus the 9 diagonal terms, then the product's reduction
+        assert bench.EC_MAC_PER_SQR_P[name] == 36 + 9 + (bench.EC_MAC_PER_MUL_P[name] - 81)
+        assert bench.EC_WIDE_MAC32[name] == ((bench.EC_WIDE_MUL[name] - bench.EC_WIDE_SQR[name]) * bench.EC_MAC_PER_MUL_P[name]
+                                             + bench.EC_WIDE_SQR[name] * bench.EC_MAC_PER_SQR_P[name])
         # the full schedule is the common count; a lane whose H passes ec9.h's zero filter (false
         # positives ~2^-24 per addition) recomputes 4 products on the exact path
         assert int(np.median(lad)) == bench.EC_WIDE_MUL[name] and max(lad) <= bench.EC_WIDE_MUL[name] + 8, (name, lad)

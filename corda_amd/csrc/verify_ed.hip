@@ -891,6 +891,9 @@ __device__ __forceinline__ void ed_double_scalar_wide_pf(ge_p2& out, const uint3
 #ifndef ED_LADDER_WIDE_WAVES
 #define ED_LADDER_WIDE_WAVES ED_LADDER_PF_WAVES
 #endif
+#ifndef ED_LADDER_WIDE_OCC  // the waves per SIMD the register use allows (the persistent grid's cap)
+#define ED_LADDER_WIDE_OCC 4
+#endif
 __global__ void __launch_bounds__(256, ED_LADDER_WIDE_WAVES) k_ed_ladder_wide(
     const cg_item* __restrict__ items, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ ranges,
     const EdKeyHdr* __restrict__ hdr, const uint32_t* __restrict__ wide_idx, const EdWideSlot* __restrict__ wed,
@@ -1119,7 +1122,7 @@ void ed_launch_ladder(bool full, const cg_item* d_items, uint64_t n_items, uint8
 void ed_launch_ladder_wide(const cg_item* d_items, uint64_t n_items, uint8_t* d_status, const KeyWs& w,
                            const ItemWs& iw, const void* d_btab, hipStream_t stream) {
   const uint32_t B = 256;
-  const unsigned grid = walk_grid(n_items, B, WALK_CAP(4));  // fe9 ladder: 110 VGPRs, 4 waves/SIMD
+  const unsigned grid = walk_grid(n_items, B, WALK_CAP(ED_LADDER_WIDE_OCC));  // fe9 ladder: 106 VGPRs, 4 waves/SIMD
   hipLaunchKernelGGL(k_ed_ladder_wide, dim3(grid), dim3(B), 0, stream, d_items, iw.perm, iw.ranges, w.hdr,
                      (const uint32_t*)w.wide_idx, (const EdWideSlot*)w.wed, bwide(d_btab), d_status, iw.slots, iw.ed);
 }

@@ -155,6 +155,10 @@ def parse(argv=None):
                          "cg_verify_tx_signatures_packed_device; host = host arena -> host verdicts through "
                          "cg_verify_tx_signatures_packed (PCIe-inclusive; always measured beside the headline as "
                          "summary.host_to_host)")
+    ap.add_argument("--contexts", type=int, default=1,
+                    help="device-form steps alternate over this many contexts on the GPU (each call on its "
+                         "context's own stream, so a call's key-table phase can overlap the previous call's "
+                         "ladders: several verifiers on one device); 1: one context, calls in order")
     ap.add_argument("--h2h-steps", type=int, default=-1,
                     help="host arena -> host verdicts calls timed beside a device headline (-1: --steps; 0: off)")
     ap.add_argument("--host-register", type=int, default=-1,
@@ -1028,6 +1032,12 @@ def main(argv=None):
     eng_threads = a.engine_threads or (threads if world > 1 else 0)
     eng = Engine(local, chunk_items=a.chunk_items, stage_timing=True, host_threads=eng_threads)
     eng.reserve(len(batch.keys), batch.n)
+    engs = [eng]
+    if a.headline == "device":
+        for _ in range(max(a.contexts, 1) - 1):
+            e2 = Engine(local, chunk_items=a.chunk_items, stage_timing=True, host_threads=eng_threads)
+            e2.reserve(len(batch.keys), batch.n)
+            engs.append(e2)
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
     holder = {}
@@ -1073,28 +1083,43 @@ def main(argv=None):
         else:
             dbuf.update(k=up(tb.keys), i=up(tb.ids), s=up(tb.sigs), a=up(tb.arena), off=0, alen=tb.arena.size)
         dbuf["st"] = torch.full((tb.n,), 255, dtype=torch.uint8, device=dev)
+        dbuf["sts"] = [dbuf["st"]] + [torch.full((tb.n,), 255, dtype=torch.uint8, device=dev) for _ in engs[1:]]
         torch.cuda.synchronize(dev)
 
     def device_step():
         d = dbuf
+        k = holder.get("k", 0)
+        holder["k"] = k + 1
+        e, st_k = engs[k % len(engs)], d["sts"][k % len(engs)]
+        # one context: on torch's stream (bridged to the context's); several: each on its own stream
+        sp = stream.cuda_stream if len(engs) == 1 else 0
         if pb is not None:
-            eng.verify_tx_signatures_packed_device(d["k"].data_ptr(), len(pb.keys), d["i"].data_ptr(), pb.n_ids,
-                                                   d["s"].data_ptr(), pb.n, d["off"], pb.stream.size, pb.tmpls,
-                                                   d["a"].data_ptr(), d["alen"], d["st"].data_ptr(),
-                                                   stream=stream.cuda_stream)
+            e.verify_tx_signatures_packed_device(d["k"].data_ptr(), len(pb.keys), d["i"].data_ptr(), pb.n_ids,
+                                                 d["s"].data_ptr(), pb.n, d["off"], pb.stream.size, pb.tmpls,
+                                                 d["a"].data_ptr(), d["alen"], st_k.data_ptr(), stream=sp)
         else:
-            eng.verify_tx_signatures_device(d["k"].data_ptr(), len(tb.keys), d["i"].data_ptr(), tb.n_ids,
-                                            d["s"].data_ptr(), tb.n, tb.tmpls, d["a"].data_ptr(), d["alen"],
-                                            d["st"].data_ptr(), stream=stream.cuda_stream)
+            e.verify_tx_signatures_device(d["k"].data_ptr(), len(tb.keys), d["i"].data_ptr(), tb.n_ids,
+                                          d["s"].data_ptr(), tb.n, tb.tmpls, d["a"].data_ptr(), d["alen"],
+                                          st_k.data_ptr(), stream=sp)
         if world > 1:  # RCCL all-gather of the per-GPU verdict vectors, device to device
-            holder["all"] = shard.gather_verdicts(d["st"], world * tb.n, world)
+            if len(engs) > 1:
+                torch.cuda.synchronize(dev)
+            holder["all"] = shard.gather_verdicts(st_k, world * tb.n, world)
+
+    def all_stage_times():
+        out = {}
+        for e in engs:
+            for name, (ms, n) in e.stage_times().items():
+                m0, n0 = out.get(name, (0.0, 0))
+                out[name] = (m0 + ms, n0 + n)
+        return out
 
     def timed(step, steps, warmup, host_stats):
         """W untimed steps, then K steps between a barrier + synchronize on both sides; the max over ranks."""
         for _ in range(warmup):
             step()
         torch.cuda.synchronize(dev)
-        eng.stage_times()  # drop the warmup's records
+        all_stage_times()  # drop the warmup's records
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -1113,13 +1138,16 @@ def main(argv=None):
             tt = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = float(tt.item())
-        return el, eng.stage_times(), cg
+        return el, all_stage_times(), cg
 
     h2h_steps = a.steps if a.h2h_steps < 0 else a.h2h_steps
     h2h = None
     if a.headline == "device":
         elapsed, stages, _ = timed(device_step, a.steps, a.warmup, False)
         st = dbuf["st"].cpu().numpy()
+        for other in dbuf["sts"][1:]:  # every context's last verdicts agree
+            if not np.array_equal(other.cpu().numpy(), st):
+                st = np.full_like(st, 255)
         if h2h_steps > 0:  # the same call shape from host buffers, PCIe-inclusive (never `value`)
             el_h, stg_h, cg_ms = timed(host_step, h2h_steps, 1, True)
             h2h = {"value": round(a.items * world * h2h_steps / el_h, 1), "unit": "sigs/s",
@@ -1128,8 +1156,10 @@ def main(argv=None):
                    + ": host arena -> host verdicts (pageable or registered per --host-register)",
                    "stages": stage_summary(stg_h, h2h_steps),
                    "verdicts_equal_device": bool(np.array_equal(holder["st_host"], st))}
-        for k in ("k", "i", "s", "a", "st"):
+        for k in ("k", "i", "s", "a", "st", "sts"):
             dbuf.pop(k, None)
+        for e in engs[1:]:
+            e.close()
         torch.cuda.empty_cache()
     else:
         elapsed, stages, cg_ms = timed(host_step, a.steps, a.warmup, True)
@@ -1223,7 +1253,7 @@ def main(argv=None):
                                       if a.headline == "device" else
                                       " call per step, host arena -> host verdicts (PCIe-inclusive)")
                                    + " (batch Crypto.doVerify(txId, sig))",
-                       "boundary": a.headline,
+                       "boundary": a.headline, "contexts": len(engs),
                        "items_per_gpu": a.items, "unique_pool": a.pool,
                        "mix": [n_ed, n_r1, a.items - n_ed - n_r1], "keys": len(batch.keys),
                        "sigs_per_tx": a.sigs_per_tx, "h2d_bytes_per_gpu": h2d_bytes, "txsig_table": a.txsig_table,

@@ -159,6 +159,9 @@ def parse(argv=None):
                     help="device-form steps alternate over this many contexts on the GPU (each call on its "
                          "context's own stream, so a call's key-table phase can overlap the previous call's "
                          "ladders: several verifiers on one device); 1: one context, calls in order")
+    ap.add_argument("--ctx2-steps", type=int, default=-1,
+                    help="with one headline context: the same device-form call timed again over two contexts on "
+                         "the GPU, reported as summary.two_contexts (-1: --steps; 0: off)")
     ap.add_argument("--h2h-steps", type=int, default=-1,
                     help="host arena -> host verdicts calls timed beside a device headline (-1: --steps; 0: off)")
     ap.add_argument("--host-register", type=int, default=-1,
@@ -1148,6 +1151,21 @@ def main(argv=None):
         for other in dbuf["sts"][1:]:  # every context's last verdicts agree
             if not np.array_equal(other.cpu().numpy(), st):
                 st = np.full_like(st, 255)
+        c2_steps = a.steps if a.ctx2_steps < 0 else a.ctx2_steps
+        if len(engs) == 1 and c2_steps > 0:
+            # two verifier contexts on the device, calls alternating (each on its own stream): a call's
+            # key-table phase runs beside the other call's ladders. Reported, not the headline: the
+            # overlap stretches every kernel's launch time, so the roofline would no longer be per kernel
+            e2 = Engine(local, chunk_items=a.chunk_items, stage_timing=True, host_threads=eng_threads)
+            e2.reserve(len(batch.keys), batch.n)
+            engs.append(e2)
+            dbuf["sts"].append(torch.full((tb.n,), 255, dtype=torch.uint8, device=dev))
+            holder["k"] = 0
+            el2, _, _ = timed(device_step, c2_steps, 2, False)
+            same = all(np.array_equal(x.cpu().numpy(), st) for x in dbuf["sts"])
+            holder["ctx2"] = {"value": round(a.items * world * c2_steps / el2, 1), "unit": "sigs/s",
+                              "ms_per_step": round(el2 / c2_steps * 1e3, 3), "steps": c2_steps,
+                              "verdicts_equal": bool(same)}
         if h2h_steps > 0:  # the same call shape from host buffers, PCIe-inclusive (never `value`)
             el_h, stg_h, cg_ms = timed(host_step, h2h_steps, 1, True)
             h2h = {"value": round(a.items * world * h2h_steps / el_h, 1), "unit": "sigs/s",
@@ -1195,7 +1213,8 @@ def main(argv=None):
 
     h2d_bytes = pb.h2d_bytes if pb is not None else int(tb.arena.size + tb.sigs.nbytes + tb.ids.nbytes + tb.keys.nbytes)
     extra = {"headline": a.headline, "stages": stage_summary(stages, a.steps), "ecdsa_ladders": ec_roof,
-             "roofline_full": roof, "verdicts": ver, "gen_s": round(gen_s, 1), "host_to_host": h2h}
+             "roofline_full": roof, "verdicts": ver, "gen_s": round(gen_s, 1), "host_to_host": h2h,
+             "two_contexts": holder.get("ctx2")}
     if a.headline == "host" or h2h is not None:
         extra["headline_h2d"] = {
             "bytes_per_call": h2d_bytes, "bytes_per_sig": round(h2d_bytes / tb.n, 1),
@@ -1253,7 +1272,7 @@ def main(argv=None):
                                       if a.headline == "device" else
                                       " call per step, host arena -> host verdicts (PCIe-inclusive)")
                                    + " (batch Crypto.doVerify(txId, sig))",
-                       "boundary": a.headline, "contexts": len(engs),
+                       "boundary": a.headline, "contexts": max(a.contexts, 1) if a.headline == "device" else 1,
                        "items_per_gpu": a.items, "unique_pool": a.pool,
                        "mix": [n_ed, n_r1, a.items - n_ed - n_r1], "keys": len(batch.keys),
                        "sigs_per_tx": a.sigs_per_tx, "h2d_bytes_per_gpu": h2d_bytes, "txsig_table": a.txsig_table,
@@ -1262,6 +1281,9 @@ def main(argv=None):
         summary = {"verdicts_checked": ver["checked_vs_labels"], "label_mismatches": ver["label_mismatches"],
                    "not_run": ver["not_run"], "draws_consistent": ver["draws_consistent"],
                    "secondary_file": os.path.relpath(a.secondary_out, ROOT) if a.secondary_out else None}
+        if holder.get("ctx2"):
+            summary["two_contexts"] = holder["ctx2"]["value"]
+            summary["two_contexts_equal"] = holder["ctx2"]["verdicts_equal"]
         if h2h is not None:
             summary["host_to_host"] = h2h["value"]
             summary["host_to_host_ms"] = h2h["ms_per_step"]

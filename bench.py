@@ -614,12 +614,12 @@ def stage_summary(times, steps_per_read):
 
 def headline_chunk(a, n):
     """Items per verify chunk of the headline call: cg_verify_tx_signatures splits a large host call
-    into at least 4 chunks unless the caller sets cg_config.chunk_items (cordagpu.cpp)."""
+    into at least 3 chunks (besides the first) unless the caller sets cg_config.chunk_items (cordagpu.cpp)."""
     chunk = eng_chunk(a)
     k = max(1, -(-n // chunk))
     per = -(-n // k)
-    if not a.chunk_items and n >= 4 * (1 << 20):
-        per = min(per, -(-n // 4))
+    if not a.chunk_items and n >= 3 * (1 << 20):
+        per = min(per, -(-n // 3))
     return per
 
 

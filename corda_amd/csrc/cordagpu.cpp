@@ -1275,7 +1275,10 @@ static int verify_transactions_host_locked(cg_ctx* c, const cg_tx* txs, uint64_t
 }
 
 // ---------------------------------------------------------------- signatures over known tx ids
-#define CG_TXSIG_MIN_CHUNKS 4u
+// the host tx-signature forms split a large call into at least this many chunks besides the smaller
+// first one (CG_TXSIG_FIRST_DIV): round 6 A/B on the configs[4] shard, 1/6 + 4 / 1/6 + 3 / 1/6 + 2
+// chunks = 345.4 / 351.3 / 334.7 M sigs/s over 3 rounds (profiles/r06/h2hchunks)
+#define CG_TXSIG_MIN_CHUNKS 3u
 #define CG_TXSIG_COUNT_SAMPLE 32u  // hot-key calls: 1 in 32 (blocks of 8 records): plan 3.0 -> 1.4-1.8 ms, 235 -> 237 / 247 M (profiles/r03/env_fd12)
 #define CG_TXSIG_SAMPLE_BLOCK 8u
 // The spliced-message slot of a template set: the longest prefix || id || suffix, 16-aligned.
